@@ -1,0 +1,209 @@
+"""Benchmark: training-step edges/sec on batches of 2394-fiber x 128-class
+complete bipartite graphs (BASELINE.json metric), plus the HBM roofline of the
+dominant kernel and the CPU oracle timed on the host.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--graphs G] [--blocks B]
+
+One process per GPU (torchrun for N > 1).  Each rank trains on its own G
+synthetic graphs (weak scaling); gradients are mean-all-reduced over RCCL once
+per step.  A step is the reference training step (train.py:133-141):
+zero_grad, GNN forward, loss_function (finaloutput=False), backward,
+all-reduce, Adam.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "pfs-neural-net_amd"), os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+NF, NC, FDIM = 2394, 128, 10
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--graphs", type=int, default=16, help="graphs per GPU")
+    ap.add_argument("--blocks", type=int, default=8, help="message-passing rounds")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    return ap.parse_args()
+
+
+def make_batch(G, rank, device):
+    """G synthetic graphs shaped like train.py's (train.py:88-104)."""
+    import pfsgnn
+    gen = torch.Generator().manual_seed(1234 + rank)
+    Ti = torch.randint(2, 13, (G * NC, 1), generator=gen).float()
+    Ni = torch.randint(1000, 100000, (G * NC, 1), generator=gen).float()
+    class_info = torch.cat([Ti, Ni], 1)
+    x_s = torch.arange(NF, dtype=torch.float).repeat(G).reshape(-1, 1)
+    e = torch.arange(G * NF * NC)
+    edge_index = torch.stack([e // NC, (e // (NF * NC)) * NC + e % NC])
+    x_e = 2.0 + 8.0 * torch.rand(G * NF * NC, FDIM, generator=gen)
+    x_u = torch.zeros(G, FDIM)
+    data = pfsgnn.BipartiteData(edge_index, x_s, class_info, x_e, x_u)
+    return data, class_info.to(device)
+
+
+# per-edge algorithmic HBM bytes of each main kernel
+def kernel_bytes_per_edge(F, first_block_excluded=False):
+    f = 4 * F
+    return {
+        "edge_mlp_fwd": 2 * f,   # read xe, write y
+        "source_fwd": f,         # read y
+        "target_fwd": f,         # read y
+        "target_bwd": f,         # read y
+        "source_bwd": 3 * f,     # read y, g_next; write g_tot
+        "edge_mlp_bwd": 4 * f,   # read g_tot, y, xe; write g_xe (blocks > 0)
+        "loss_fwd": f,
+        "loss_bwd": 2 * f,
+    }
+
+
+def cpu_baseline(blocks, seconds):
+    """The CPU oracle (oracle/, torch on the host cores) timed on a bounded sample
+    of the same workload: ONE 2394x128 graph, full training step incl. Adam."""
+    from harness import make_problem
+    from noise_ref import uniform_numpy
+    from oracle.ref_train import loss_function as oracle_loss
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    model, graph = make_problem(1, NF, NC, B=blocks, seed=0, dtype=torch.float32)
+    model.train()
+    opt = torch.optim.Adam(model.parameters(), lr=5e-4)
+    uni = torch.as_tensor(uniform_numpy(1, NF * NC))
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        opt.zero_grad()
+        out = model(graph)
+        loss, _ = oracle_loss(model, out.x_e, graph.x_t, 1, NF, NC, pclass=0.1, pfiber=0.1,
+                              sharpness=10.0, uniform=uni)
+        loss.backward()
+        opt.step()
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or steps >= 50:
+            break
+    return {"value": steps * NF * NC / el, "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} training step(s) of one {NF}x{NC} graph, {blocks} blocks, "
+                      f"oracle/ (torch CPU fp32, {threads} threads), {el:.1f}s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=device)
+
+    import pfsgnn
+    from pfsgnn import config, native
+    from pfsgnn.train import loss_function
+    from pfsgnn.distributed import allreduce_gradients, broadcast_parameters
+    config.device = device
+
+    G, B = args.graphs, args.blocks
+    torch.manual_seed(0)
+    gnn = pfsgnn.GNN(B=B, Fdim=FDIM, T=NC, F_s=1, F_t=2).to(device)
+    gnn.train()
+    broadcast_parameters(gnn)
+    opt = pfsgnn.FusedAdam(gnn.parameters(), lr=config.lr)
+    data, class_info = make_batch(G, rank, device)
+    E = G * NF * NC
+
+    def step(i):
+        gnn.zero_grad()
+        out = gnn(data)
+        loss, _ = loss_function(out, class_info, pclass=0.1, pfiber=0.1, sharpness=10.0, seed=i)
+        loss.backward()
+        allreduce_gradients(gnn)
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    native.timing_enable(True)
+    native.timing_reset()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    native.timing_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(loss).item(), "non-finite loss"
+
+    # ---- per-kernel times (HIP events on the launch stream, timed region only)
+    per_edge = kernel_bytes_per_edge(FDIM)
+    kt = {}
+    for k in native.KERNELS:
+        ms, n = native.timing_query(k)
+        if n:
+            kt[k] = (ms, n)
+    dom = max(kt, key=lambda k: kt[k][0])
+    ms, n = kt[dom]
+    launches_bytes = per_edge.get(dom, 4 * FDIM) * E
+    if dom == "edge_mlp_bwd":      # block 0 writes no input gradient
+        launches_bytes = (per_edge[dom] * (B - 1) + 3 * 4 * FDIM) * E / B
+    avg_s = ms / n / 1e3
+    achieved = launches_bytes / avg_s / 1e9
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "avg_launch_us": round(avg_s * 1e6, 1), "launches": n,
+                "bytes_per_launch": int(launches_bytes),
+                "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kt.items()}}
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(B, args.cpu_seconds)
+        value = world * E * args.steps / elapsed
+        line = {
+            "metric": "training-step edges/sec on 2394x128 bipartite batches; % HBM roofline",
+            "value": value, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"{G} complete bipartite {NF}x{NC} graphs per GPU, {B} "
+                                   f"message-passing blocks, Fdim {FDIM}; full training step "
+                                   f"(GNN fwd + train.py loss + bwd + Adam)",
+                       "fibers": NF, "classes": NC, "graphs_per_gpu": G, "global_graphs": G * world,
+                       "blocks": B, "fdim": FDIM, "edges_per_gpu_step": E,
+                       "parallelism": f"dp{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,205 @@
+/*
+ * pfsgnn.h -- C ABI of libpfsgnn.so, the MI355X (gfx950) bipartite
+ * message-passing engine that drops in behind the reference's
+ * EdgeModel / SModel / TModel / GlobalModel operator surface
+ * (joshua-lintropic/pfs-neural-net, src/gnn.py) and its training objective
+ * (src/train.py).
+ *
+ * Conventions
+ *   - every pointer is a DEVICE pointer (HBM) unless noted; float = fp32;
+ *   - node tensors are channel-major [C][N] (row stride N);
+ *   - edge tensors are channel-major [C][E] over the canonical fiber-major
+ *     order e = (g*NF + f)*NC + c of a batch of G complete bipartite graphs
+ *     with NF fibers (source nodes) and NC classes (target nodes) each;
+ *     NS = G*NF, NT = G*NC, E = G*NF*NC;
+ *   - weights are torch.nn.Linear matrices [out][in] with row stride `ldw`;
+ *     a column block is passed as (W + col0, ldw);
+ *   - (sc, sh) optional per-channel affine applied to an edge tensor on read
+ *     (lazy BatchNorm output); NULL means identity;
+ *   - gradient outputs named d* ACCUMULATE (+=); other outputs overwrite;
+ *   - `ws`/`ws_bytes` is caller-owned device scratch, at least
+ *     pfsgnn_workspace_bytes(G, NF, NC, F) bytes;
+ *   - `stream` is a hipStream_t; every call is asynchronous on it and
+ *     graph-capturable (no allocation, no synchronisation inside);
+ *   - return 0 on success, <0 on error (pfsgnn_last_error() has the text).
+ *
+ * Supported feature widths F (Fdim): 8, 10, 16.  NC <= 256.
+ */
+#ifndef PFSGNN_H
+#define PFSGNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* pfsgnn_version(void);
+const char* pfsgnn_last_error(void);
+size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F);
+
+/* Per-kernel HIP-event timing of the main edge/loss kernels (diagnostics for
+ * bench.py; off by default, must stay off while a stream is captured).
+ * Names: edge_mlp_fwd, source_fwd, target_fwd, target_bwd, source_bwd,
+ * edge_bn_sums, edge_mlp_bwd, loss_fwd, loss_bwd.  query() synchronises. */
+int pfsgnn_timing_enable(int on);
+int pfsgnn_timing_reset(void);
+int pfsgnn_timing_query(const char* name, double* total_ms, long long* count);
+
+/* ---------------------------------------------------------------- node ops
+ * The node-level Linear / LeakyReLU(0.1) / BatchNorm1d / RMSNorm pieces of
+ * MLP (gnn.py:65), SModel.node_mlp_2 (gnn.py:154), TModel.node_mlp_2
+ * (gnn.py:192), GlobalModel (gnn.py:223) and the encoders (gnn.py:297).   */
+
+/* Y[m][n] (+)= sum_k W[m][k] * act(X[k][n]) + bscale*b[m]; act = lrelu if act_in */
+int pfsgnn_lin(const float* W, int ldw, int M, int K, const float* X, int N,
+               const float* b, float bscale, int act_in, float* Y, int add, void* stream);
+/* out[k][n] (+)= (sum_m W[m][k] dY[m][n]) * (Z ? lrelu'(Z[k][n]) : 1) */
+int pfsgnn_lin_t(const float* W, int ldw, int M, int K, const float* dY, int N,
+                 const float* Z, float* out, int add, void* stream);
+/* dW[m][k] += sum_n dY[m][n] act(X[k][n]);  db[m] += dbscale * sum_n dY[m][n] */
+int pfsgnn_wgrad(const float* dY, int M, const float* X, int K, int N, int act_in,
+                 float* dW, int lddw, float* db, float dbscale,
+                 void* ws, size_t ws_bytes, void* stream);
+/* BatchNorm1d training forward over N rows (biased var for the output,
+ * unbiased for the running update; rm/rv may be NULL). */
+int pfsgnn_bn_fwd(const float* X, int C, int N, const float* gamma, const float* beta,
+                  float* rm, float* rv, float momentum, float eps,
+                  float* Y, float* mu, float* var, void* ws, size_t ws_bytes, void* stream);
+int pfsgnn_bn_bwd(const float* dY, const float* X, const float* mu, const float* var,
+                  const float* gamma, float eps, int C, int N,
+                  float* dX, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
+                  void* stream);
+/* out[c][g] = sum (or mean) over the n nodes of graph g of X[c][g*n + i] */
+int pfsgnn_graph_reduce(const float* X, int C, int G, int n, int mean, float* out, void* stream);
+/* out[c][g*n + i] += scale * src[c][g] */
+int pfsgnn_graph_bcast_add(float* out, int C, int G, int n, const float* src, float scale,
+                           void* stream);
+/* GlobalModel's RMSNorm, applied twice (gnn.py:223 + the Sequential child),
+ * over C features of G rows. y1 [C][G], r1/r2 [G] are saved for backward. */
+int pfsgnn_rms2_fwd(const float* X, int C, int G, const float* w, float eps,
+                    float* Y, float* y1, float* r1, float* r2, void* stream);
+int pfsgnn_rms2_bwd(const float* dY, const float* X, const float* w, const float* y1,
+                    const float* r1, const float* r2, int C, int G, float eps,
+                    float* dX, float* dw, void* ws, size_t ws_bytes, void* stream);
+/* EdgeModel's BatchNorm applied twice (gnn.py:101): from the batch moments
+ * (mu1, var1) of y give xe_new = sc*y + sh; updates running stats twice. */
+int pfsgnn_bn2_finalize(const float* mu1, const float* var1, const float* gamma,
+                        const float* beta, float* rm, float* rv, int C, long long n,
+                        float momentum, float eps, float* sc, float* sh, float* inv1,
+                        float* inv2, void* stream);
+/* its backward: g_y = alpha*g + gam0 + gam1*y from Sg = sum g, Sgx = sum g*xhat */
+int pfsgnn_bn2_bwd_coef(const float* Sg, const float* Sgx, const float* mu1, const float* var1,
+                        const float* gamma, int C, long long n, float eps, float* alpha,
+                        float* gam0, float* gam1, float* dgamma, float* dbeta, void* stream);
+/* SModel moment backward (gnn.py:140-153) -> per-fiber coefficients of
+ * g_m = C0 + d(C1 + d(C2 + d C3)), d = m - mean.  mom [4][C][NS] =
+ * (mean, c2, c3, c4); gst [4C][NS] = dL/d(mean, std, skew, kurt). */
+int pfsgnn_moment_coef(const float* mom, const float* gst, int C, int NS, int n,
+                       float* coef, void* stream);
+
+/* ---------------------------------------------------------------- edge ops */
+
+/* EdgeModel per-edge MLP (gnn.py:99-101 with the first Linear split):
+ * z1 = Ps[:,f] + Pt[:,c] + W1[:,2F:3F] x ; y = W2 lrelu(z1) + b2, where
+ * x = xsc*xe + xsh.  Also the batch moments mu/var (biased) of y. */
+int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe, const float* xsc,
+                        const float* xsh, const float* Ps, const float* Pt, const float* W1,
+                        const float* W2, const float* b2, float* y, float* mu, float* var,
+                        void* ws, size_t ws_bytes, void* stream);
+/* SModel per-edge message + per-fiber centred moments (gnn.py:136-151).
+ * mom [4][2F][NS]; hs [8F][NS] receives (mean, std, skew, kurt). */
+int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
+                      const float* sh, const float* Qt, const float* Ws1, const float* Ws2,
+                      const float* bs2, float* mom, float* hs, void* stream);
+/* TModel per-edge message, summed per class before its second Linear
+ * (gnn.py:188-190): hsum[:,c] = sum_f lrelu(Rs[:,f] + Wt1[:,F:2F] x). */
+int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
+                      const float* sh, const float* Rs, const float* Wt1, float* hsum,
+                      void* ws, size_t ws_bytes, void* stream);
+/* TModel edge backward: GzT[:,f] = sum_c g_z; dWt1[:,F:2F] += sum g_z x^T;
+ * optional gxe = Wt1[:,F:2F]^T g_z (standalone TModel only). */
+int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
+                      const float* sh, const float* Rs, const float* Wt1, const float* g_hsum,
+                      float* GzT, float* dWt1, float* gxe, void* ws, size_t ws_bytes,
+                      void* stream);
+/* SModel edge backward fused with TModel's per-edge input gradient, the
+ * downstream edge gradient and the edge BatchNorm's two gradient sums:
+ * g_tot = Ws1e^T g_zs + [Wt1e^T g_zt] + [g_next]; GzS per class;
+ * dWs1[:,F:2F], dWs2, dbs2 accumulated; Sg/Sgx = sums of g_tot, g_tot*xhat
+ * (xhat = (y-mu1)*inv1) when mu1 != NULL.  Rs/Wt1/g_hsum may be NULL. */
+int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
+                      const float* sh, const float* Qt, const float* Ws1, const float* Ws2,
+                      const float* bs2, const float* mean, const float* coef, const float* Rs,
+                      const float* Wt1, const float* g_hsum, const float* g_next,
+                      const float* mu1, const float* inv1, float* g_tot, float* GzS,
+                      float* dWs1, float* dWs2, float* dbs2, float* Sg, float* Sgx,
+                      void* ws, size_t ws_bytes, void* stream);
+/* Sg = sum g, Sgx = sum g*(y-mu1)*inv1 (standalone EdgeModel backward). */
+int pfsgnn_edge_bn_grad_sums(int G, int NF, int NC, int F, const float* g, const float* y,
+                             const float* mu1, const float* inv1, float* Sg, float* Sgx,
+                             void* ws, size_t ws_bytes, void* stream);
+/* EdgeModel per-edge MLP backward.  g_y = alpha*g_tot + gam0 + gam1*y;
+ * gxe (optional) = W1[:,2F:3F]^T g_z1; GzEs [4F][NS], GzEt [4F][NT] are
+ * the per-fiber / per-class sums of g_z1; dW1[:,2F:3F], dW2, db2 accumulated. */
+int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_tot, const float* alpha,
+                        const float* gam0, const float* gam1, const float* y, const float* xe,
+                        const float* xsc, const float* xsh, const float* Ps, const float* Pt,
+                        const float* W1, const float* W2, float* dW1, float* dW2, float* db2,
+                        float* gxe, float* GzEs, float* GzEt, void* ws, size_t ws_bytes,
+                        void* stream);
+
+/* ---------------------------------------------------------------- loss
+ * train.py:29-80: decoder_e (gnn.py:307) + softplus + softfloor (train.py:21)
+ * + scatters per class / fiber.  ci = class_info [>=2][NT] (row 0 = T_i,
+ * row 1 = N_i).  Noise uniforms come from a counter-based hash of
+ * (seed, edge).  tt (optional) = per-edge allocated time [E]. */
+int pfsgnn_loss_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
+                    const float* sh, const float* Wd1, const float* bd1, const float* Wd2,
+                    const float* bd2, const float* ci, float scale, float sharpness,
+                    float noiselevel, unsigned long long seed, float* n_prime,
+                    float* fiber_time, float* tmean, float* tvar, float* tt,
+                    void* ws, size_t ws_bytes, void* stream);
+int pfsgnn_loss_finalize(int G, int NF, int NC, const float* n_prime, const float* fiber_time,
+                         const float* tvar, const float* ci, float pclass, float pfiber,
+                         float total_time, float nfields, float wutils, float wvar,
+                         float* loss, float* utils, float* variance, float* Gn, float* Gf,
+                         float* Gv, void* stream);
+/* gscale: device scalar (upstream d loss), NULL = 1. gxe = d loss / d xe_final */
+int pfsgnn_loss_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
+                    const float* sh, const float* Wd1, const float* bd1, const float* Wd2,
+                    const float* bd2, const float* ci, float scale, float sharpness,
+                    float noiselevel, unsigned long long seed, const float* Gn,
+                    const float* Gf, const float* Gv, const float* tmean, const float* gscale,
+                    float* dWd1, float* dbd1, float* dWd2, float* dbd2, float* gxe,
+                    void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- layout
+ * The reference takes an arbitrary edge_index [2][E] (int64).  A complete
+ * bipartite batch in any edge order maps onto the canonical order by a
+ * permutation.  pfsgnn_layout_analyze validates edge_index (every
+ * (g, f, c) exactly once, src graph == tgt graph) and writes
+ * perm[canonical] = original edge id; status[0] = 1 if complete,
+ * status[1] = 1 if already canonical.  (status is device int32[2].) */
+int pfsgnn_layout_analyze(const int64_t* edge_index, long long E, int G, int NF, int NC,
+                          int32_t* perm, int32_t* status, void* ws, size_t ws_bytes,
+                          void* stream);
+/* row-major user edges [E][F] (original order) -> channel-major canonical [F][E] */
+int pfsgnn_edges_to_canonical(const float* src, long long E, int F, const int32_t* perm,
+                              float* dst, void* stream);
+/* channel-major canonical (sc*y+sh) -> row-major [E][F] original order (or,
+ * with rowmajor = 0, channel-major [F][E] in original order) */
+int pfsgnn_edges_from_canonical(const float* y, const float* sc, const float* sh, long long E,
+                                int F, const int32_t* perm, int rowmajor, float* dst,
+                                void* stream);
+
+/* ---------------------------------------------------------------- optimiser
+ * torch.optim.Adam (amsgrad=False, maximize=False) over one flat buffer. */
+int pfsgnn_adam(float* p, const float* g, float* m, float* v, long long n, int step, float lr,
+                float beta1, float beta2, float eps, float weight_decay, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PFSGNN_H */

@@ -1,0 +1,247 @@
+// pfsgnn_common.h -- shared device/host helpers for libpfsgnn (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include <string>
+
+#define PF_LEAKY 0.1f
+#define PF_BLOCK 256
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ errors
+namespace pf {
+void set_error(const std::string& msg);
+int fail(const char* where, const char* what);
+int check_launch(const char* where);
+// brackets one kernel launch with HIP events when pfsgnn_timing_enable(1)
+class Timer {
+ public:
+  Timer(const char* name, hipStream_t st);
+  void end();
+
+ private:
+  const char* name_;
+  hipStream_t st_;
+  hipEvent_t a_;
+};
+}  // namespace pf
+
+#define PF_REQUIRE(cond, where, what) \
+  do {                                \
+    if (!(cond)) return pf::fail(where, what); \
+  } while (0)
+
+// ------------------------------------------------------------ activations
+// torch.nn.LeakyReLU(0.1) and its backward (grad * (x > 0 ? 1 : slope)).
+__device__ __forceinline__ float lrelu(float x) { return x > 0.f ? x : PF_LEAKY * x; }
+__device__ __forceinline__ float dlrelu(float z) { return z > 0.f ? 1.f : PF_LEAKY; }
+
+// ------------------------------------------------------------ edge geometry
+// A block of 256 threads covers FPI = 256/SW fibers x SW lanes (SW = next
+// power of two >= NC; lanes c >= NC idle).  Thread t owns fiber slot t/SW and
+// class lane t%SW of every fiber tile it visits, so per-class sums stay in the
+// thread's registers and per-fiber sums are butterflies inside an aligned SW-lane
+// segment.  Block b works on graph b / BPG, fiber tiles [j*TPB, (j+1)*TPB).
+struct EdgeGeo {
+  int G, NF, NC, SW, FPI, TPG, BPG, TPB, nblocks;
+  long long E, NS, NT;
+};
+
+static inline EdgeGeo make_geo(int G, int NF, int NC) {
+  EdgeGeo g;
+  g.G = G; g.NF = NF; g.NC = NC;
+  g.SW = 1;
+  while (g.SW < NC) g.SW <<= 1;
+  g.FPI = PF_BLOCK / g.SW;
+  g.TPG = (NF + g.FPI - 1) / g.FPI;
+  int target = 1024;
+  int bpg = (target + G - 1) / G;
+  if (bpg > g.TPG) bpg = g.TPG;
+  if (bpg < 1) bpg = 1;
+  g.TPB = (g.TPG + bpg - 1) / bpg;
+  g.BPG = (g.TPG + g.TPB - 1) / g.TPB;
+  g.nblocks = G * g.BPG;
+  g.E = (long long)G * NF * NC;
+  g.NS = (long long)G * NF;
+  g.NT = (long long)G * NC;
+  return g;
+}
+
+// ------------------------------------------------------------ reductions
+// Sum NV values over the SW-lane segment of the calling thread; every lane
+// of the segment receives the sum.  Deterministic (fixed butterfly order).
+// `scratch` must hold 4*NV floats; SW is block-uniform.
+template <int NV>
+__device__ __forceinline__ void seg_sum(float (&v)[NV], int SW, float* scratch) {
+  const int w = SW < 64 ? SW : 64;
+  for (int o = w >> 1; o > 0; o >>= 1) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] += __shfl_xor(v[i], o);
+  }
+  if (SW > 64) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) scratch[wave * NV + i] = v[i];
+    }
+    __syncthreads();
+    const int wps = SW >> 6;
+    const int w0 = (wave / wps) * wps;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      float s = 0.f;
+      for (int k = 0; k < wps; ++k) s += scratch[(w0 + k) * NV + i];
+      v[i] = s;
+    }
+  }
+}
+
+// Sum NV values over the whole 256-thread block into out[0..NV) (LDS), valid
+// after the call for every thread.  `scratch` >= 4*NV floats.
+template <int NV>
+__device__ __forceinline__ void block_sum(float (&v)[NV], float* scratch) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    float x = v[i];
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    v[i] = x;
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) scratch[wave * NV + i] = v[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    v[i] = ((scratch[i] + scratch[NV + i]) + scratch[2 * NV + i]) + scratch[3 * NV + i];
+}
+
+// Reduce per-thread per-class accumulators acc[C] over the FPI fiber slots of
+// the block and write the block's partial [NC][C] to part.  `scratch` >= 256*C.
+template <int C>
+__device__ __forceinline__ void column_partial(const float (&acc)[C], int SW, int FPI, int NC,
+                                               float* scratch, float* part) {
+  const int t = threadIdx.x;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < C; ++i) scratch[t * C + i] = acc[i];
+  __syncthreads();
+  for (int idx = t; idx < NC * C; idx += PF_BLOCK) {
+    const int c = idx / C, i = idx - c * C;
+    float s = 0.f;
+    for (int sl = 0; sl < FPI; ++sl) s += scratch[(sl * SW + c) * C + i];
+    part[idx] = s;
+  }
+}
+
+// ------------------------------------------------------------ MFMA wgrad
+// Accumulates sum over a wave's 64 lanes (one edge each) of a (x) b, with
+// a in R^MA, b in R^NB, on v_mfma_f32_16x16x4_f32 (exact f32 products): the
+// edge index is the MFMA K dimension, staged through LDS rows [64][LDA] and
+// [64][LDB] (each lane writes its own row).  Lane l supplies A[i=l&15][k=l>>4]
+// = a_{edge 4s+(l>>4)}[16mt+i] and B[k][j=l&15] = b_{edge 4s+(l>>4)}[16nt+j].
+// Result D[16mt + 4*(l>>4) + r][16nt + (l&15)] = acc[mt][nt][r].
+template <int MA, int NB>
+struct WGrad {
+  static constexpr int MT = (MA + 15) / 16;
+  static constexpr int NT = (NB + 15) / 16;
+  static constexpr int LDA = MA | 1;  // odd: conflict-free row writes
+  static constexpr int LDB = NB | 1;
+  static constexpr int LDS_FLOATS = 64 * (LDA + LDB);  // per wave
+  floatx4 acc[MT][NT];
+
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < NT; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // wave-private LDS region; call stage() then (after a barrier) accum().
+  __device__ __forceinline__ void stage(float* region, const float* a, const float* b, int lane) {
+    float* A = region;
+    float* B = region + 64 * LDA;
+#pragma unroll
+    for (int i = 0; i < MA; ++i) A[lane * LDA + i] = a[i];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) B[lane * LDB + j] = b[j];
+  }
+
+  __device__ __forceinline__ void accum(const float* region, int lane) {
+    const float* A = region;
+    const float* B = region + 64 * LDA;
+    const int col = lane & 15;
+    const int kq = lane >> 4;
+#pragma unroll 4
+    for (int s = 0; s < 16; ++s) {
+      const int q = 4 * s + kq;
+      float av[MT], bv[NT];
+#pragma unroll
+      for (int a = 0; a < MT; ++a) {
+        const int i = 16 * a + col;
+        av[a] = (i < MA) ? A[q * LDA + i] : 0.f;
+      }
+#pragma unroll
+      for (int b = 0; b < NT; ++b) {
+        const int j = 16 * b + col;
+        bv[b] = (j < NB) ? B[q * LDB + j] : 0.f;
+      }
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+    }
+  }
+
+  // Sum the block's 4 waves and write the block partial [MA][NB] to part.
+  // `scratch` >= 4*MA*NB floats.
+  __device__ __forceinline__ void block_partial(float* scratch, float* part) {
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < NT; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = 16 * a + 4 * (lane >> 4) + r;
+          const int j = 16 * b + (lane & 15);
+          if (i < MA && j < NB) scratch[(wave * MA + i) * NB + j] = acc[a][b][r];
+        }
+    __syncthreads();
+    for (int idx = t; idx < MA * NB; idx += PF_BLOCK)
+      part[idx] = ((scratch[idx] + scratch[MA * NB + idx]) + scratch[2 * MA * NB + idx]) +
+                  scratch[3 * MA * NB + idx];
+  }
+};
+
+// ------------------------------------------------------------ noise
+// Counter-based uniform in [0,1) (24-bit), bit-identical to tests/noise_ref.py.
+__host__ __device__ __forceinline__ uint64_t pf_fmix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ float pf_uniform(uint64_t key, uint64_t e) {
+  const uint64_t z = pf_fmix64(key + (e + 1ull) * 0x9E3779B97F4A7C15ull);
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// ------------------------------------------------------------ reduce kernels
+// out[r*ldo + c] (+)= scale * sum_{b<nb} part[b*plen + r*ldp + c] -- finishes
+// every per-block partial deterministically (fixed block order).
+void launch_reduce_rows(const float* part, int nb, size_t plen, int ldp, int rows, int cols,
+                        float* out, int ldo, int add, float scale, hipStream_t st);
+// Column partials [G][BPG][NC][C] -> channel-major node tensor out[C][G*NC].
+void launch_reduce_columns(const float* part, int G, int BPG, int NC, int C, float* out,
+                           hipStream_t st);
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+static inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }

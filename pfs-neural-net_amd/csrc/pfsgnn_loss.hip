@@ -1,0 +1,501 @@
+// pfsgnn_loss.hip -- the training objective (train.py:21-80) fused over edges,
+// and the edge-layout helpers (canonical order <-> the caller's edge_index).
+#include "pfsgnn_common.h"
+#include "../../include/pfsgnn.h"
+
+#include <algorithm>
+#include <cmath>
+
+#define EDGE_PROLOGUE                                                  \
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;             \
+  const int bx = blockIdx.x;                                           \
+  const int gg = bx / geo.BPG, jj = bx - gg * geo.BPG;                 \
+  const int slot = t / geo.SW, cl = t - slot * geo.SW;                 \
+  const bool cvalid = cl < geo.NC;                                     \
+  const int tile0 = jj * geo.TPB;                                      \
+  const int tile1 = min(geo.TPG, tile0 + geo.TPB);                     \
+  const long long E = geo.E, NS = geo.NS, NT = geo.NT;                 \
+  const long long cn = (long long)gg * geo.NC + cl;                    \
+  (void)lane; (void)wave; (void)E; (void)NS; (void)NT; (void)cn;
+
+#define EDGE_TILE                                                      \
+  const int f = tile * geo.FPI + slot;                                 \
+  const bool fvalid = f < geo.NF;                                      \
+  const bool valid = cvalid && fvalid;                                 \
+  const long long n = (long long)gg * geo.NF + (fvalid ? f : 0);       \
+  const long long e = n * geo.NC + cl;                                 \
+  (void)e;
+
+struct SoftFloor {
+  float r, corr, two_pi, inv_pi;  // r = exp(-1/sharpness) (0 if sharpness == 0)
+};
+
+static SoftFloor make_softfloor(float sharpness) {
+  SoftFloor s;
+  const float pi = (float)M_PI;                           // x.new_tensor(np.pi)
+  s.r = sharpness == 0.f ? 0.f : expf(-1.0f / sharpness); // train.py:26
+  s.corr = atanf(s.r / (1.0f - s.r));
+  s.two_pi = 2.0f * pi;
+  s.inv_pi = 1.0f / pi;
+  return s;
+}
+
+// decoder_e + softplus*scale + softfloor + clamp (train.py:42-49, gnn.py:307-312)
+template <int F>
+struct EdgeLoss {
+  float zd[F], ad[F], pred, time, Ti, xx, th, graw, gal, tt;
+  __device__ __forceinline__ void run(const float (&x)[F], const float* __restrict__ Wd1,
+                                      const float* __restrict__ bd1, const float* __restrict__ Wd2,
+                                      const float* __restrict__ bd2, float scale, float Ti_,
+                                      float noise, const SoftFloor& sf) {
+    pred = bd2[0];
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      float s = bd1[j];
+#pragma unroll
+      for (int k = 0; k < F; ++k) s = fmaf(Wd1[j * F + k], x[k], s);
+      zd[j] = s;
+      ad[j] = lrelu(s);
+      pred = fmaf(Wd2[j], ad[j], pred);
+    }
+    const float sp = pred > 20.f ? pred : log1pf(expf(pred));  // F.softplus (threshold 20)
+    time = sp * scale;
+    Ti = Ti_;
+    xx = time / Ti + noise;
+    th = sf.two_pi * xx;
+    graw = xx + sf.inv_pi * (atanf(sf.r * sinf(th) / (1.0f - sf.r * cosf(th))) - sf.corr);
+    gal = graw < 0.f ? 0.f : graw;  // torch.maximum(0, g) (NaN propagates)
+    tt = gal * Ti;
+  }
+};
+
+template <int F>
+__global__ __launch_bounds__(256) void k_loss_fwd(EdgeGeo geo, const float* __restrict__ y,
+                                                  const float* __restrict__ sc,
+                                                  const float* __restrict__ sh,
+                                                  const float* __restrict__ Wd1,
+                                                  const float* __restrict__ bd1,
+                                                  const float* __restrict__ Wd2,
+                                                  const float* __restrict__ bd2,
+                                                  const float* __restrict__ ci, float scale,
+                                                  SoftFloor sf, float noiselevel, uint64_t key,
+                                                  float* __restrict__ fiber_time,
+                                                  float* __restrict__ tt_out,
+                                                  float* __restrict__ part) {
+  EDGE_PROLOGUE
+  __shared__ float lds[256 * 4];
+  float np = 0.f, wc = 0.f, wm = 0.f, wq = 0.f;
+  const float Ti = cvalid ? ci[cn] : 1.f;
+  for (int tile = tile0; tile < tile1; ++tile) {
+    EDGE_TILE
+    float x[F];
+#pragma unroll
+    for (int k = 0; k < F; ++k) {
+      const float v = valid ? y[(long long)k * E + e] : 0.f;
+      x[k] = sc ? fmaf(v, sc[k], sh[k]) : v;
+    }
+    const float noise = noiselevel * (pf_uniform(key, (uint64_t)e) - 0.5f);
+    EdgeLoss<F> L;
+    L.run(x, Wd1, bd1, Wd2, bd2, scale, Ti, noise, sf);
+    float ft[1] = {valid ? L.tt : 0.f};
+    if (valid) {
+      np += L.gal;
+      wc += 1.f;
+      const float d = L.tt - wm;
+      wm += d / wc;
+      wq = fmaf(d, L.tt - wm, wq);
+      if (tt_out) tt_out[e] = L.tt;
+    }
+    seg_sum<1>(ft, geo.SW, lds);
+    if (cl == 0 && fvalid) fiber_time[n] = ft[0];
+  }
+  __syncthreads();
+  lds[t * 4 + 0] = np;
+  lds[t * 4 + 1] = wc;
+  lds[t * 4 + 2] = wm;
+  lds[t * 4 + 3] = wq;
+  __syncthreads();
+  for (int c = t; c < geo.NC; c += 256) {
+    float P = 0.f, C0 = 0.f, M0 = 0.f, Q0 = 0.f;
+    for (int s = 0; s < geo.FPI; ++s) {
+      const float* q = lds + (s * geo.SW + c) * 4;
+      P += q[0];
+      const float cb = q[1], mb = q[2], qb = q[3];
+      const float tot = C0 + cb;
+      if (tot > 0.f) {
+        const float d = mb - M0;
+        M0 = M0 + d * (cb / tot);
+        Q0 = Q0 + qb + d * d * (C0 * cb / tot);
+      }
+      C0 = tot;
+    }
+    float* o = part + ((size_t)bx * geo.NC + c) * 4;
+    o[0] = P; o[1] = C0; o[2] = M0; o[3] = Q0;
+  }
+}
+
+__global__ void k_loss_class_reduce(const float* __restrict__ part, int G, int BPG, int NC,
+                                    int NF, float* __restrict__ n_prime, float* __restrict__ tmean,
+                                    float* __restrict__ tvar) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over G*NC
+  if (idx >= G * NC) return;
+  const int g = idx / NC, c = idx - g * NC;
+  double P = 0, C0 = 0, M0 = 0, Q0 = 0;
+  for (int b = 0; b < BPG; ++b) {
+    const float* q = part + (((size_t)g * BPG + b) * NC + c) * 4;
+    P += q[0];
+    const double cb = q[1], mb = q[2], qb = q[3];
+    const double tot = C0 + cb;
+    if (tot > 0) {
+      const double d = mb - M0;
+      M0 += d * (cb / tot);
+      Q0 += qb + d * d * (C0 * cb / tot);
+    }
+    C0 = tot;
+  }
+  n_prime[idx] = (float)P;
+  tmean[idx] = (float)M0;
+  tvar[idx] = NF > 1 ? (float)(Q0 / (double)(NF - 1)) : NAN;  // torch.var, correction=1
+}
+
+// one block per graph: train.py:53-71 and the per-node gradient coefficients
+__global__ __launch_bounds__(256) void k_loss_finalize(
+    int NF, int NC, int NT, const float* __restrict__ n_prime, const float* __restrict__ fiber_time,
+    const float* __restrict__ tvar, const float* __restrict__ ci, float pclass, float pfiber,
+    float total_time, float nfields, float wutils, float wvar, float* __restrict__ loss,
+    float* __restrict__ utils, float* __restrict__ variance, float* __restrict__ Gn,
+    float* __restrict__ Gf, float* __restrict__ Gv) {
+  const int g = blockIdx.x, t = threadIdx.x;
+  __shared__ float scratch[4 * 4];
+  __shared__ float smin[256];
+  // completeness min
+  float mn = INFINITY;
+  for (int c = t; c < NC; c += 256) {
+    const long long cn = (long long)g * NC + c;
+    const float Ni = ci[NT + cn] / nfields;
+    const float comp = n_prime[cn] / Ni;
+    mn = fminf(mn, comp);
+  }
+  smin[t] = mn;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (t < s) smin[t] = fminf(smin[t], smin[t + s]);
+    __syncthreads();
+  }
+  const float umin = smin[0];
+  float v[4] = {0.f, 0.f, 0.f, 0.f};  // ties, class penalty, fiber penalty, variance
+  for (int c = t; c < NC; c += 256) {
+    const long long cn = (long long)g * NC + c;
+    const float Ni = ci[NT + cn] / nfields;
+    const float comp = n_prime[cn] / Ni;
+    v[0] += comp == umin ? 1.f : 0.f;
+    const float over = fmaxf(n_prime[cn] - Ni, 0.f);
+    v[1] += over * over;
+    v[3] += tvar[cn];
+  }
+  for (int f = t; f < NF; f += 256) {
+    const long long n = (long long)g * NF + f;
+    const float ot = fiber_time[n] - total_time;
+    const float lk = lrelu(ot);
+    v[2] += lk * lk;
+    Gf[n] = pfiber * 2.f * lk * dlrelu(ot);
+  }
+  block_sum<4>(v, scratch);
+  const float ties = v[0];
+  for (int c = t; c < NC; c += 256) {
+    const long long cn = (long long)g * NC + c;
+    const float Ni = ci[NT + cn] / nfields;
+    const float comp = n_prime[cn] / Ni;
+    const float over = fmaxf(n_prime[cn] - Ni, 0.f);
+    Gn[cn] = (comp == umin ? -wutils / ties : 0.f) / Ni + 2.f * pclass * over;
+    Gv[cn] = -wvar * 2.f / (float)(NF - 1);
+  }
+  if (t == 0) {
+    utils[g] = umin;
+    variance[g] = v[3];
+    loss[g] = -wutils * umin + pfiber * v[2] + pclass * v[1] - wvar * v[3];
+  }
+}
+
+template <int F>
+__global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __restrict__ y,
+                                                  const float* __restrict__ sc,
+                                                  const float* __restrict__ sh,
+                                                  const float* __restrict__ Wd1,
+                                                  const float* __restrict__ bd1,
+                                                  const float* __restrict__ Wd2,
+                                                  const float* __restrict__ bd2,
+                                                  const float* __restrict__ ci, float scale,
+                                                  SoftFloor sf, float noiselevel, uint64_t key,
+                                                  const float* __restrict__ Gn,
+                                                  const float* __restrict__ Gf,
+                                                  const float* __restrict__ Gv,
+                                                  const float* __restrict__ tmean,
+                                                  const float* __restrict__ gscale,
+                                                  float* __restrict__ gxe,
+                                                  float* __restrict__ partW,
+                                                  float* __restrict__ partV) {
+  using WG = WGrad<F, F + 1>;  // g_zd (x) [x, 1] -> dWd1 | dbd1
+  EDGE_PROLOGUE
+  constexpr int LDS_N = (4 * WG::LDS_FLOATS > 4 * F * (F + 1)) ? 4 * WG::LDS_FLOATS
+                                                                : 4 * F * (F + 1);
+  __shared__ float lds[LDS_N + 4 * (F + 1)];
+  float* region = lds + wave * WG::LDS_FLOATS;
+  WG wg;
+  wg.zero();
+  float acc[F + 1];
+#pragma unroll
+  for (int j = 0; j <= F; ++j) acc[j] = 0.f;
+  const float gs = gscale ? gscale[0] : 1.f;
+  const float Ti = cvalid ? ci[cn] : 1.f;
+  const float Gn_c = cvalid ? Gn[cn] : 0.f, Gv_c = cvalid ? Gv[cn] : 0.f;
+  const float tm_c = cvalid ? tmean[cn] : 0.f;
+  for (int tile = tile0; tile < tile1; ++tile) {
+    EDGE_TILE
+    float x[F + 1];
+#pragma unroll
+    for (int k = 0; k < F; ++k) {
+      const float v = valid ? y[(long long)k * E + e] : 0.f;
+      x[k] = sc ? fmaf(v, sc[k], sh[k]) : v;
+    }
+    x[F] = 1.f;
+    const float noise = noiselevel * (pf_uniform(key, (uint64_t)e) - 0.5f);
+    EdgeLoss<F> L;
+    float xf[F];
+#pragma unroll
+    for (int k = 0; k < F; ++k) xf[k] = x[k];
+    L.run(xf, Wd1, bd1, Wd2, bd2, scale, Ti, noise, sf);
+    const float g_tt = Gf[n] + Gv_c * (L.tt - tm_c);
+    const float g_gal = Gn_c + Ti * g_tt;
+    const float mask = L.graw > 0.f ? 1.f : (L.graw == 0.f ? 0.5f : 0.f);
+    const float cth = cosf(L.th);
+    const float dsf = 1.f + 2.f * (sf.r * cth - sf.r * sf.r) / (1.f - 2.f * sf.r * cth + sf.r * sf.r);
+    const float g_time = g_gal * mask * dsf / Ti;
+    const float sig = L.pred > 20.f ? 1.f : 1.f / (1.f + expf(-L.pred));
+    const float g_pred = valid ? gs * g_time * scale * sig : 0.f;
+    float gz[F];
+#pragma unroll
+    for (int j = 0; j < F; ++j) {
+      acc[j] = fmaf(g_pred, L.ad[j], acc[j]);
+      gz[j] = Wd2[j] * g_pred * dlrelu(L.zd[j]);
+    }
+    acc[F] += g_pred;
+    if (valid) {
+#pragma unroll
+      for (int k = 0; k < F; ++k) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < F; ++j) s = fmaf(Wd1[j * F + k], gz[j], s);
+        gxe[(long long)k * E + e] = s;
+      }
+    }
+    wg.stage(region, gz, x, lane);
+    __syncthreads();
+    wg.accum(region, lane);
+    __syncthreads();
+  }
+  wg.block_partial(lds, partW + (size_t)bx * F * (F + 1));
+  block_sum<F + 1>(acc, lds + LDS_N);
+  if (t <= F) {
+    float val = 0.f;
+#pragma unroll
+    for (int i = 0; i <= F; ++i) val = (i == t) ? acc[i] : val;
+    partV[(size_t)bx * (F + 1) + t] = val;
+  }
+}
+
+// ------------------------------------------------------------ layout
+__global__ void k_layout_init(int32_t* status) {
+  if (threadIdx.x == 0) { status[0] = 1; status[1] = 1; }
+}
+
+__global__ void k_layout_scatter(const int64_t* __restrict__ ei, long long E, int G, int NF, int NC,
+                                 int32_t* __restrict__ perm, int32_t* __restrict__ cnt,
+                                 int32_t* __restrict__ status) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const long long NS = (long long)G * NF, NT = (long long)G * NC;
+  const long long s = ei[e], tg = ei[E + e];
+  if (s < 0 || s >= NS || tg < 0 || tg >= NT) { atomicAnd(&status[0], 0); atomicAnd(&status[1], 0); return; }
+  const long long g = s / NF, gt = tg / NC;
+  if (g != gt) { atomicAnd(&status[0], 0); atomicAnd(&status[1], 0); return; }
+  const long long k = s * NC + (tg - gt * NC);
+  atomicAdd(&cnt[k], 1);
+  perm[k] = (int32_t)e;
+  if (k != e) atomicAnd(&status[1], 0);
+}
+
+__global__ void k_layout_check(const int32_t* __restrict__ cnt, long long E,
+                               int32_t* __restrict__ status) {
+  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= E) return;
+  if (cnt[k] != 1) { atomicAnd(&status[0], 0); atomicAnd(&status[1], 0); }
+}
+
+__global__ void k_to_canonical(const float* __restrict__ src, long long E, int F,
+                               const int32_t* __restrict__ perm, float* __restrict__ dst) {
+  const long long ec = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ec >= E) return;
+  const long long es = perm ? perm[ec] : ec;
+  for (int k = 0; k < F; ++k) dst[(long long)k * E + ec] = src[es * F + k];
+}
+
+__global__ void k_from_canonical(const float* __restrict__ y, const float* __restrict__ sc,
+                                 const float* __restrict__ sh, long long E, int F,
+                                 const int32_t* __restrict__ perm, int rowmajor,
+                                 float* __restrict__ dst) {
+  const long long ec = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ec >= E) return;
+  const long long ed = perm ? perm[ec] : ec;
+  for (int k = 0; k < F; ++k) {
+    float v = y[(long long)k * E + ec];
+    if (sc) v = fmaf(v, sc[k], sh[k]);
+    if (rowmajor) dst[ed * F + k] = v;
+    else dst[(long long)k * E + ed] = v;
+  }
+}
+
+// ------------------------------------------------------------ host side
+namespace {
+struct Ws {
+  char* p;
+  size_t left;
+  float* take(size_t nfloats) {
+    const size_t b = align256(nfloats * sizeof(float));
+    if (b > left) return nullptr;
+    float* r = reinterpret_cast<float*>(p);
+    p += b;
+    left -= b;
+    return r;
+  }
+};
+int check_dims(const char* where, int G, int NF, int NC, int F) {
+  if (G <= 0 || NF <= 1 || NC <= 0) return pf::fail(where, "need G > 0, NF > 1, NC > 0");
+  if (NC > 256) return pf::fail(where, "NC > 256 is not supported by the dense edge kernels");
+  if (F != 8 && F != 10 && F != 16) return pf::fail(where, "unsupported Fdim (8, 10, 16)");
+  return 0;
+}
+#define DISPATCH_F(F, ...)                                   \
+  switch (F) {                                               \
+    case 8: { constexpr int FF = 8; __VA_ARGS__; } break;    \
+    case 10: { constexpr int FF = 10; __VA_ARGS__; } break;  \
+    case 16: { constexpr int FF = 16; __VA_ARGS__; } break;  \
+    default: return pf::fail("dispatch", "unsupported F");   \
+  }
+}  // namespace
+
+static uint64_t noise_key(unsigned long long seed) {
+  return pf_fmix64((uint64_t)seed ^ 0xD1B54A32D192ED03ull);
+}
+
+extern "C" int pfsgnn_loss_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
+                               const float* sh, const float* Wd1, const float* bd1,
+                               const float* Wd2, const float* bd2, const float* ci, float scale,
+                               float sharpness, float noiselevel, unsigned long long seed,
+                               float* n_prime, float* fiber_time, float* tmean, float* tvar,
+                               float* tt, void* ws, size_t ws_bytes, void* stream) {
+  if (int rc = check_dims("pfsgnn_loss_fwd", G, NF, NC, F)) return rc;
+  PF_REQUIRE(y && Wd1 && bd1 && Wd2 && bd2 && ci && n_prime && fiber_time && tmean && tvar,
+             "pfsgnn_loss_fwd", "null");
+  const EdgeGeo geo = make_geo(G, NF, NC);
+  Ws w{reinterpret_cast<char*>(ws), ws_bytes};
+  float* part = w.take((size_t)geo.nblocks * NC * 4);
+  PF_REQUIRE(part, "pfsgnn_loss_fwd", "workspace too small");
+  hipStream_t st = as_stream(stream);
+  const SoftFloor sf = make_softfloor(sharpness);
+  const uint64_t key = noise_key(seed);
+  { pf::Timer tm_("loss_fwd", st);
+  DISPATCH_F(F, hipLaunchKernelGGL(k_loss_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
+                                   sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sf, noiselevel, key,
+                                   fiber_time, tt, part));
+  tm_.end(); }
+  hipLaunchKernelGGL(k_loss_class_reduce, dim3((G * NC + 255) / 256), dim3(256), 0, st, part, G,
+                     geo.BPG, NC, NF, n_prime, tmean, tvar);
+  return pf::check_launch("pfsgnn_loss_fwd");
+}
+
+extern "C" int pfsgnn_loss_finalize(int G, int NF, int NC, const float* n_prime,
+                                    const float* fiber_time, const float* tvar, const float* ci,
+                                    float pclass, float pfiber, float total_time, float nfields,
+                                    float wutils, float wvar, float* loss, float* utils,
+                                    float* variance, float* Gn, float* Gf, float* Gv,
+                                    void* stream) {
+  PF_REQUIRE(G > 0 && NF > 1 && NC > 0, "pfsgnn_loss_finalize", "bad dims");
+  PF_REQUIRE(n_prime && fiber_time && tvar && ci && loss && utils && variance && Gn && Gf && Gv,
+             "pfsgnn_loss_finalize", "null");
+  hipLaunchKernelGGL(k_loss_finalize, dim3(G), dim3(256), 0, as_stream(stream), NF, NC, G * NC,
+                     n_prime, fiber_time, tvar, ci, pclass, pfiber, total_time, nfields, wutils,
+                     wvar, loss, utils, variance, Gn, Gf, Gv);
+  return pf::check_launch("pfsgnn_loss_finalize");
+}
+
+extern "C" int pfsgnn_loss_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
+                               const float* sh, const float* Wd1, const float* bd1,
+                               const float* Wd2, const float* bd2, const float* ci, float scale,
+                               float sharpness, float noiselevel, unsigned long long seed,
+                               const float* Gn, const float* Gf, const float* Gv,
+                               const float* tmean, const float* gscale, float* dWd1, float* dbd1,
+                               float* dWd2, float* dbd2, float* gxe, void* ws, size_t ws_bytes,
+                               void* stream) {
+  if (int rc = check_dims("pfsgnn_loss_bwd", G, NF, NC, F)) return rc;
+  PF_REQUIRE(y && Wd1 && bd1 && Wd2 && bd2 && ci && Gn && Gf && Gv && tmean && dWd1 && dbd1 &&
+                 dWd2 && dbd2 && gxe,
+             "pfsgnn_loss_bwd", "null");
+  const EdgeGeo geo = make_geo(G, NF, NC);
+  const size_t nb = geo.nblocks;
+  Ws w{reinterpret_cast<char*>(ws), ws_bytes};
+  float* pW = w.take(nb * F * (F + 1));
+  float* pV = w.take(nb * (F + 1));
+  PF_REQUIRE(pW && pV, "pfsgnn_loss_bwd", "workspace too small");
+  hipStream_t st = as_stream(stream);
+  const SoftFloor sf = make_softfloor(sharpness);
+  const uint64_t key = noise_key(seed);
+  { pf::Timer tm_("loss_bwd", st);
+  DISPATCH_F(F, hipLaunchKernelGGL(k_loss_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y, sc,
+                                   sh, Wd1, bd1, Wd2, bd2, ci, scale, sf, noiselevel, key, Gn, Gf,
+                                   Gv, tmean, gscale, gxe, pW, pV));
+  tm_.end(); }
+  launch_reduce_rows(pW, nb, (size_t)F * (F + 1), F + 1, F, F, dWd1, F, 1, 1.f, st);
+  launch_reduce_rows(pW + F, nb, (size_t)F * (F + 1), F + 1, F, 1, dbd1, 1, 1, 1.f, st);
+  launch_reduce_rows(pV, nb, (size_t)(F + 1), F, 1, F, dWd2, F, 1, 1.f, st);
+  launch_reduce_rows(pV + F, nb, (size_t)(F + 1), 1, 1, 1, dbd2, 1, 1, 1.f, st);
+  return pf::check_launch("pfsgnn_loss_bwd");
+}
+
+extern "C" int pfsgnn_layout_analyze(const int64_t* edge_index, long long E, int G, int NF, int NC,
+                                     int32_t* perm, int32_t* status, void* ws, size_t ws_bytes,
+                                     void* stream) {
+  PF_REQUIRE(edge_index && perm && status && E > 0, "pfsgnn_layout_analyze", "null/empty");
+  PF_REQUIRE(E == (long long)G * NF * NC, "pfsgnn_layout_analyze",
+             "E != G*NF*NC: not a complete bipartite batch");
+  PF_REQUIRE(E < (1ll << 31), "pfsgnn_layout_analyze", "E too large for int32 permutation");
+  PF_REQUIRE(ws && ws_bytes >= (size_t)E * sizeof(int32_t), "pfsgnn_layout_analyze",
+             "workspace too small");
+  hipStream_t st = as_stream(stream);
+  int32_t* cnt = reinterpret_cast<int32_t*>(ws);
+  if (hipMemsetAsync(cnt, 0, (size_t)E * sizeof(int32_t), st) != hipSuccess)
+    return pf::fail("pfsgnn_layout_analyze", "memset");
+  hipLaunchKernelGGL(k_layout_init, dim3(1), dim3(64), 0, st, status);
+  const unsigned nbk = (unsigned)((E + 255) / 256);
+  hipLaunchKernelGGL(k_layout_scatter, dim3(nbk), dim3(256), 0, st, edge_index, E, G, NF, NC, perm,
+                     cnt, status);
+  hipLaunchKernelGGL(k_layout_check, dim3(nbk), dim3(256), 0, st, cnt, E, status);
+  return pf::check_launch("pfsgnn_layout_analyze");
+}
+
+extern "C" int pfsgnn_edges_to_canonical(const float* src, long long E, int F, const int32_t* perm,
+                                         float* dst, void* stream) {
+  PF_REQUIRE(src && dst && E > 0 && F > 0, "pfsgnn_edges_to_canonical", "bad arguments");
+  hipLaunchKernelGGL(k_to_canonical, dim3((unsigned)((E + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), src, E, F, perm, dst);
+  return pf::check_launch("pfsgnn_edges_to_canonical");
+}
+
+extern "C" int pfsgnn_edges_from_canonical(const float* y, const float* sc, const float* sh,
+                                           long long E, int F, const int32_t* perm, int rowmajor,
+                                           float* dst, void* stream) {
+  PF_REQUIRE(y && dst && E > 0 && F > 0, "pfsgnn_edges_from_canonical", "bad arguments");
+  hipLaunchKernelGGL(k_from_canonical, dim3((unsigned)((E + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), y, sc, sh, E, F, perm, rowmajor, dst);
+  return pf::check_launch("pfsgnn_edges_from_canonical");
+}

@@ -1,0 +1,728 @@
+// pfsgnn_node.hip -- node-level ops (channel-major [C][N] tensors).
+//
+// These carry the per-node / per-graph parts of the reference modules:
+// the MLPs (gnn.py:65), BatchNorm1d over fibers / classes (gnn.py:154, 192),
+// the GlobalModel means + double RMSNorm (gnn.py:218-223) and the
+// per-graph broadcast of u (gnn.py:100/153/191).  Node tensors are small
+// (G*NF fibers, G*NC classes) and L2-resident; the hot path is the edge ops.
+#include "pfsgnn_common.h"
+#include "../../include/pfsgnn.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <cmath>
+#include <map>
+#include <vector>
+
+namespace pf {
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+int fail(const char* where, const char* what) {
+  g_err = std::string(where) + ": " + what;
+  return -1;
+}
+int check_launch(const char* where) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_err = std::string(where) + ": " + hipGetErrorString(e);
+    return -2;
+  }
+  return 0;
+}
+}  // namespace pf
+
+// ---------------------------------------------------------------- timing
+// Optional per-kernel HIP-event timing (off by default; never enabled while a
+// stream is being captured).  Each main edge kernel launch is bracketed by two
+// events on its own stream; pfsgnn_timing_query() resolves them.
+namespace pf {
+struct TimerRec {
+  hipEvent_t a, b;
+};
+static bool g_timing = false;
+static std::map<std::string, std::vector<TimerRec>> g_pending;
+static std::map<std::string, std::pair<double, long long>> g_done;
+static std::vector<hipEvent_t> g_pool;
+
+static hipEvent_t take_event() {
+  if (!g_pool.empty()) {
+    hipEvent_t e = g_pool.back();
+    g_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+Timer::Timer(const char* name, hipStream_t st) : name_(name), st_(st), a_(nullptr) {
+  if (!g_timing) return;
+  a_ = take_event();
+  if (a_) (void)hipEventRecord(a_, st_);
+}
+
+void Timer::end() {
+  if (!g_timing || !a_) return;
+  hipEvent_t b = take_event();
+  if (!b) return;
+  (void)hipEventRecord(b, st_);
+  g_pending[name_].push_back({a_, b});
+  a_ = nullptr;
+}
+
+static void resolve(const std::string& name) {
+  auto it = g_pending.find(name);
+  if (it == g_pending.end()) return;
+  for (auto& r : it->second) {
+    float ms = 0.f;
+    (void)hipEventSynchronize(r.b);
+    (void)hipEventElapsedTime(&ms, r.a, r.b);
+    auto& d = g_done[name];
+    d.first += ms;
+    d.second += 1;
+    g_pool.push_back(r.a);
+    g_pool.push_back(r.b);
+  }
+  it->second.clear();
+}
+}  // namespace pf
+
+extern "C" int pfsgnn_timing_enable(int on) {
+  pf::g_timing = on != 0;
+  return 0;
+}
+
+extern "C" int pfsgnn_timing_reset(void) {
+  for (auto& kv : pf::g_pending) pf::resolve(kv.first);
+  pf::g_done.clear();
+  return 0;
+}
+
+extern "C" int pfsgnn_timing_query(const char* name, double* total_ms, long long* count) {
+  pf::resolve(name);
+  auto it = pf::g_done.find(name);
+  *total_ms = it == pf::g_done.end() ? 0.0 : it->second.first;
+  *count = it == pf::g_done.end() ? 0 : it->second.second;
+  return 0;
+}
+
+extern "C" const char* pfsgnn_last_error(void) { return pf::g_err.c_str(); }
+extern "C" const char* pfsgnn_version(void) { return "pfsgnn 0.1 gfx950"; }
+
+// ---------------------------------------------------------------- reduce
+__global__ void k_reduce_rows(const float* __restrict__ part, int nb, size_t plen, int ldp,
+                              int rows, int cols, float* __restrict__ out, int ldo, int add,
+                              float scale) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * cols) return;
+  const int r = idx / cols, c = idx - r * cols;
+  const float* p = part + (size_t)r * ldp + c;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += p[(size_t)b * plen];
+  float* o = out + (size_t)r * ldo + c;
+  *o = add ? (*o + scale * s) : scale * s;
+}
+
+void launch_reduce_rows(const float* part, int nb, size_t plen, int ldp, int rows, int cols,
+                        float* out, int ldo, int add, float scale, hipStream_t st) {
+  const int len = rows * cols;
+  hipLaunchKernelGGL(k_reduce_rows, dim3((len + 255) / 256), dim3(256), 0, st, part, nb, plen, ldp,
+                     rows, cols, out, ldo, add, scale);
+}
+
+__global__ void k_reduce_columns(const float* __restrict__ part, int G, int BPG, int NC, int C,
+                                 float* __restrict__ out) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over G*NC*C
+  const int total = G * NC * C;
+  if (idx >= total) return;
+  const int g = idx / (NC * C);
+  const int rem = idx - g * NC * C;  // c*C + i
+  const int c = rem / C, i = rem - c * C;
+  float s = 0.f;
+  const float* p = part + (size_t)g * BPG * NC * C + rem;
+  for (int b = 0; b < BPG; ++b) s += p[(size_t)b * NC * C];
+  out[(size_t)i * G * NC + (size_t)g * NC + c] = s;
+}
+
+void launch_reduce_columns(const float* part, int G, int BPG, int NC, int C, float* out,
+                           hipStream_t st) {
+  const int total = G * NC * C;
+  hipLaunchKernelGGL(k_reduce_columns, dim3((total + 255) / 256), dim3(256), 0, st, part, G, BPG,
+                     NC, C, out);
+}
+
+// ---------------------------------------------------------------- lin
+// One thread per column n, 16 output rows per thread; weights are uniform
+// (scalar loads), the input column is streamed once per 16 rows.
+#define LIN_MB 16
+__global__ __launch_bounds__(256) void k_lin(const float* __restrict__ W, int ldw, int M, int K,
+                                             const float* __restrict__ X, int N,
+                                             const float* __restrict__ b, float bscale, int act_in,
+                                             float* __restrict__ Y, int add) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int m0 = blockIdx.y * LIN_MB;
+  if (n >= N) return;
+  float acc[LIN_MB];
+#pragma unroll
+  for (int i = 0; i < LIN_MB; ++i) acc[i] = 0.f;
+  for (int k = 0; k < K; ++k) {
+    float x = X[(size_t)k * N + n];
+    if (act_in) x = lrelu(x);
+#pragma unroll
+    for (int i = 0; i < LIN_MB; ++i)
+      if (m0 + i < M) acc[i] = fmaf(W[(size_t)(m0 + i) * ldw + k], x, acc[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < LIN_MB; ++i) {
+    const int m = m0 + i;
+    if (m < M) {
+      float v = acc[i];
+      if (b) v += bscale * b[m];
+      float* o = Y + (size_t)m * N + n;
+      *o = add ? (*o + v) : v;
+    }
+  }
+}
+
+extern "C" int pfsgnn_lin(const float* W, int ldw, int M, int K, const float* X, int N,
+                          const float* b, float bscale, int act_in, float* Y, int add,
+                          void* stream) {
+  PF_REQUIRE(W && X && Y && M > 0 && K > 0 && N > 0, "pfsgnn_lin", "bad arguments");
+  dim3 grid((N + 255) / 256, (M + LIN_MB - 1) / LIN_MB);
+  hipLaunchKernelGGL(k_lin, grid, dim3(256), 0, as_stream(stream), W, ldw, M, K, X, N, b, bscale,
+                     act_in, Y, add);
+  return pf::check_launch("pfsgnn_lin");
+}
+
+__global__ __launch_bounds__(256) void k_lin_t(const float* __restrict__ W, int ldw, int M, int K,
+                                               const float* __restrict__ dY, int N,
+                                               const float* __restrict__ Z,
+                                               float* __restrict__ out, int add) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k0 = blockIdx.y * LIN_MB;
+  if (n >= N) return;
+  float acc[LIN_MB];
+#pragma unroll
+  for (int i = 0; i < LIN_MB; ++i) acc[i] = 0.f;
+  for (int m = 0; m < M; ++m) {
+    const float g = dY[(size_t)m * N + n];
+#pragma unroll
+    for (int i = 0; i < LIN_MB; ++i)
+      if (k0 + i < K) acc[i] = fmaf(W[(size_t)m * ldw + k0 + i], g, acc[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < LIN_MB; ++i) {
+    const int k = k0 + i;
+    if (k < K) {
+      float v = acc[i];
+      if (Z) v *= dlrelu(Z[(size_t)k * N + n]);
+      float* o = out + (size_t)k * N + n;
+      *o = add ? (*o + v) : v;
+    }
+  }
+}
+
+extern "C" int pfsgnn_lin_t(const float* W, int ldw, int M, int K, const float* dY, int N,
+                            const float* Z, float* out, int add, void* stream) {
+  PF_REQUIRE(W && dY && out && M > 0 && K > 0 && N > 0, "pfsgnn_lin_t", "bad arguments");
+  dim3 grid((N + 255) / 256, (K + LIN_MB - 1) / LIN_MB);
+  hipLaunchKernelGGL(k_lin_t, grid, dim3(256), 0, as_stream(stream), W, ldw, M, K, dY, N, Z, out,
+                     add);
+  return pf::check_launch("pfsgnn_lin_t");
+}
+
+// ---------------------------------------------------------------- wgrad
+// dW[m][k] += sum_n dY[m][n] act(X[k][n]).  Output tiles of 16x16 on
+// v_mfma_f32_16x16x4_f32 with the node index as the MFMA K dimension; the
+// N range is split over blocks (per-block partials + deterministic reduce).
+__global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ dY, int M,
+                                               const float* __restrict__ X, int K, int N,
+                                               int act_in, int tilesK, int chunk,
+                                               float* __restrict__ part) {
+  const int tile = blockIdx.x;
+  const int tm = tile / tilesK, tk = tile - tm * tilesK;
+  const int split = blockIdx.y;
+  const int c0 = split * chunk;
+  const int c1 = min(N, c0 + chunk);
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int row = tm * 16 + (lane & 15);  // m for A operand
+  const int colk = tk * 16 + (lane & 15); // k for B operand
+  const int kq = lane >> 4;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  const bool rv = row < M, cv = colk < K;
+  const float* dyr = dY + (size_t)(rv ? row : 0) * N;
+  const float* xr = X + (size_t)(cv ? colk : 0) * N;
+  for (int base = c0 + 4 * wave; base < c1; base += 16) {
+    const int n = base + kq;
+    const bool nv = n < c1;
+    const float a = (rv && nv) ? dyr[n] : 0.f;
+    float b = (cv && nv) ? xr[n] : 0.f;
+    if (act_in) b = lrelu(b);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+  }
+  __shared__ float red[4][16][16];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wave][4 * (lane >> 4) + r][lane & 15] = acc[r];
+  __syncthreads();
+  // part layout [split][M][K]
+  const int i = t >> 4, j = t & 15;
+  const int m = tm * 16 + i, k = tk * 16 + j;
+  if (m < M && k < K) {
+    const float s = ((red[0][i][j] + red[1][i][j]) + red[2][i][j]) + red[3][i][j];
+    part[(size_t)split * M * K + (size_t)m * K + k] = s;
+  }
+}
+
+// db[m] += scale * sum_n dY[m][n]   (one block per row)
+__global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ dY, int N,
+                                                float* __restrict__ db, float scale) {
+  const int m = blockIdx.x;
+  float s = 0.f;
+  for (int n = threadIdx.x; n < N; n += 256) s += dY[(size_t)m * N + n];
+  __shared__ float scratch[4];
+  float v[1] = {s};
+  block_sum<1>(v, scratch);
+  if (threadIdx.x == 0) db[m] += scale * v[0];
+}
+
+static int wgrad_splits(int N) {
+  int s = (N + 2047) / 2048;
+  return std::max(1, std::min(s, 64));
+}
+
+extern "C" int pfsgnn_wgrad(const float* dY, int M, const float* X, int K, int N, int act_in,
+                            float* dW, int lddw, float* db, float dbscale, void* ws,
+                            size_t ws_bytes, void* stream) {
+  PF_REQUIRE(dY && X && dW && M > 0 && K > 0 && N > 0, "pfsgnn_wgrad", "bad arguments");
+  hipStream_t st = as_stream(stream);
+  const int splits = wgrad_splits(N);
+  const size_t need = (size_t)splits * M * K * sizeof(float);
+  PF_REQUIRE(ws && ws_bytes >= need, "pfsgnn_wgrad", "workspace too small");
+  const int chunk = (N + splits - 1) / splits;
+  const int tilesM = (M + 15) / 16, tilesK = (K + 15) / 16;
+  float* part = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(k_wgrad, dim3(tilesM * tilesK, splits), dim3(256), 0, st, dY, M, X, K, N,
+                     act_in, tilesK, chunk, part);
+  launch_reduce_rows(part, splits, (size_t)M * K, K, M, K, dW, lddw, 1, 1.f, st);
+  if (db) hipLaunchKernelGGL(k_rowsum, dim3(M), dim3(256), 0, st, dY, N, db, dbscale);
+  return pf::check_launch("pfsgnn_wgrad");
+}
+
+// ---------------------------------------------------------------- batchnorm
+// Per-channel Welford partials: grid (C, S); part[c][s] = (count, mean, M2).
+__global__ __launch_bounds__(256) void k_bn_stats(const float* __restrict__ X, int N, int S,
+                                                  float* __restrict__ part) {
+  const int c = blockIdx.x, s = blockIdx.y;
+  const int chunk = (N + S - 1) / S;
+  const int n0 = s * chunk, n1 = min(N, n0 + chunk);
+  float cnt = 0.f, mean = 0.f, m2 = 0.f;
+  for (int n = n0 + threadIdx.x; n < n1; n += 256) {
+    const float x = X[(size_t)c * N + n];
+    cnt += 1.f;
+    const float d = x - mean;
+    mean += d / cnt;
+    m2 += d * (x - mean);
+  }
+  // merge across the block (Chan), tree over lanes then waves
+  for (int o = 32; o > 0; o >>= 1) {
+    const float cb = __shfl_xor(cnt, o), mb = __shfl_xor(mean, o), qb = __shfl_xor(m2, o);
+    const float tot = cnt + cb;
+    if (tot > 0.f) {
+      const float d = mb - mean;
+      mean = mean + d * (cb / tot);
+      m2 = m2 + qb + d * d * (cnt * cb / tot);
+    }
+    cnt = tot;
+  }
+  __shared__ float sh[4][3];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) { sh[wave][0] = cnt; sh[wave][1] = mean; sh[wave][2] = m2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float C0 = sh[0][0], M0 = sh[0][1], Q0 = sh[0][2];
+    for (int w = 1; w < 4; ++w) {
+      const float cb = sh[w][0], mb = sh[w][1], qb = sh[w][2];
+      const float tot = C0 + cb;
+      if (tot > 0.f) {
+        const float d = mb - M0;
+        M0 = M0 + d * (cb / tot);
+        Q0 = Q0 + qb + d * d * (C0 * cb / tot);
+      }
+      C0 = tot;
+    }
+    float* p = part + ((size_t)c * S + s) * 3;
+    p[0] = C0; p[1] = M0; p[2] = Q0;
+  }
+}
+
+// merge S partials per channel (double), write mu/var, update running stats
+__global__ void k_bn_finalize(const float* __restrict__ part, int C, int S, long long N,
+                              float* __restrict__ mu, float* __restrict__ var,
+                              float* __restrict__ rm, float* __restrict__ rv, float momentum) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double cnt = 0, mean = 0, m2 = 0;
+  for (int s = 0; s < S; ++s) {
+    const float* p = part + ((size_t)c * S + s) * 3;
+    const double cb = p[0], mb = p[1], qb = p[2];
+    const double tot = cnt + cb;
+    if (tot > 0) {
+      const double d = mb - mean;
+      mean += d * (cb / tot);
+      m2 += qb + d * d * (cnt * cb / tot);
+    }
+    cnt = tot;
+  }
+  const double v = m2 / (double)N;
+  mu[c] = (float)mean;
+  var[c] = (float)v;
+  if (rm) {
+    const double unb = N > 1 ? m2 / (double)(N - 1) : v;
+    rm[c] = (float)((1.0 - momentum) * rm[c] + momentum * mean);
+    rv[c] = (float)((1.0 - momentum) * rv[c] + momentum * unb);
+  }
+}
+
+__global__ void k_bn_apply(const float* __restrict__ X, int C, int N, const float* __restrict__ mu,
+                           const float* __restrict__ var, const float* __restrict__ gamma,
+                           const float* __restrict__ beta, float eps, float* __restrict__ Y) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)C * N) return;
+  const int c = (int)(idx / N);
+  const float inv = 1.0f / sqrtf(var[c] + eps);
+  Y[idx] = (X[idx] - mu[c]) * inv * gamma[c] + beta[c];
+}
+
+static int bn_splits(int N) { return std::max(1, std::min(64, (N + 4095) / 4096)); }
+
+extern "C" int pfsgnn_bn_fwd(const float* X, int C, int N, const float* gamma, const float* beta,
+                             float* rm, float* rv, float momentum, float eps, float* Y, float* mu,
+                             float* var, void* ws, size_t ws_bytes, void* stream) {
+  PF_REQUIRE(X && Y && mu && var && gamma && beta && C > 0 && N > 1, "pfsgnn_bn_fwd",
+             "bad arguments (BatchNorm needs more than one value per channel)");
+  hipStream_t st = as_stream(stream);
+  const int S = bn_splits(N);
+  const size_t need = (size_t)C * S * 3 * sizeof(float);
+  PF_REQUIRE(ws && ws_bytes >= need, "pfsgnn_bn_fwd", "workspace too small");
+  float* pool = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(k_bn_stats, dim3(C, S), dim3(256), 0, st, X, N, S, pool);
+  hipLaunchKernelGGL(k_bn_finalize, dim3(1), dim3(64), 0, st, pool, C, S, (long long)N, mu, var,
+                     rm, rv, momentum);
+  const size_t tot = (size_t)C * N;
+  hipLaunchKernelGGL(k_bn_apply, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, X, C, N,
+                     mu, var, gamma, beta, eps, Y);
+  return pf::check_launch("pfsgnn_bn_fwd");
+}
+
+// backward sums per channel: Sg = sum dY, Sgx = sum dY*xhat (one block per channel)
+__global__ __launch_bounds__(256) void k_bn_bwd_sums(const float* __restrict__ dY,
+                                                     const float* __restrict__ X, int N,
+                                                     const float* __restrict__ mu,
+                                                     const float* __restrict__ var, float eps,
+                                                     float* __restrict__ sums) {
+  const int c = blockIdx.x;
+  const float m = mu[c], inv = 1.0f / sqrtf(var[c] + eps);
+  float v[2] = {0.f, 0.f};
+  for (int n = threadIdx.x; n < N; n += 256) {
+    const float g = dY[(size_t)c * N + n];
+    v[0] += g;
+    v[1] += g * (X[(size_t)c * N + n] - m) * inv;
+  }
+  __shared__ float scratch[8];
+  block_sum<2>(v, scratch);
+  if (threadIdx.x == 0) { sums[2 * c] = v[0]; sums[2 * c + 1] = v[1]; }
+}
+
+__global__ void k_bn_bwd_apply(const float* __restrict__ dY, const float* __restrict__ X, int C,
+                               int N, const float* __restrict__ mu, const float* __restrict__ var,
+                               const float* __restrict__ gamma, float eps,
+                               const float* __restrict__ sums, float* __restrict__ dX,
+                               float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < (size_t)C) {
+    dgamma[idx] += sums[2 * idx + 1];
+    dbeta[idx] += sums[2 * idx];
+  }
+  if (idx >= (size_t)C * N) return;
+  const int c = (int)(idx / N);
+  const float inv = 1.0f / sqrtf(var[c] + eps);
+  const float xh = (X[idx] - mu[c]) * inv;
+  dX[idx] = gamma[c] * inv * (dY[idx] - sums[2 * c] / N - xh * (sums[2 * c + 1] / N));
+}
+
+extern "C" int pfsgnn_bn_bwd(const float* dY, const float* X, const float* mu, const float* var,
+                             const float* gamma, float eps, int C, int N, float* dX, float* dgamma,
+                             float* dbeta, void* ws, size_t ws_bytes, void* stream) {
+  PF_REQUIRE(dY && X && dX && C > 0 && N > 0, "pfsgnn_bn_bwd", "bad arguments");
+  PF_REQUIRE(ws && ws_bytes >= (size_t)2 * C * sizeof(float), "pfsgnn_bn_bwd",
+             "workspace too small");
+  hipStream_t st = as_stream(stream);
+  float* sums = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(k_bn_bwd_sums, dim3(C), dim3(256), 0, st, dY, X, N, mu, var, eps, sums);
+  const size_t tot = (size_t)C * N;
+  hipLaunchKernelGGL(k_bn_bwd_apply, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, dY, X,
+                     C, N, mu, var, gamma, eps, sums, dX, dgamma, dbeta);
+  return pf::check_launch("pfsgnn_bn_bwd");
+}
+
+// ---------------------------------------------------------------- graph ops
+__global__ void k_graph_reduce(const float* __restrict__ X, int C, int G, int n, int mean,
+                               float* __restrict__ out) {
+  const int cg = blockIdx.x;  // c*G + g
+  const int c = cg / G, g = cg - c * G;
+  float v[1] = {0.f};
+  const float* p = X + (size_t)c * G * n + (size_t)g * n;
+  for (int i = threadIdx.x; i < n; i += 256) v[0] += p[i];
+  __shared__ float scratch[4];
+  block_sum<1>(v, scratch);
+  if (threadIdx.x == 0) out[(size_t)c * G + g] = mean ? v[0] / (float)n : v[0];
+}
+
+extern "C" int pfsgnn_graph_reduce(const float* X, int C, int G, int n, int mean, float* out,
+                                   void* stream) {
+  PF_REQUIRE(X && out && C > 0 && G > 0 && n > 0, "pfsgnn_graph_reduce", "bad arguments");
+  hipLaunchKernelGGL(k_graph_reduce, dim3(C * G), dim3(256), 0, as_stream(stream), X, C, G, n,
+                     mean, out);
+  return pf::check_launch("pfsgnn_graph_reduce");
+}
+
+__global__ void k_graph_bcast_add(float* __restrict__ out, int C, int G, int n,
+                                  const float* __restrict__ src, float scale) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t tot = (size_t)C * G * n;
+  if (idx >= tot) return;
+  const size_t c = idx / ((size_t)G * n);
+  const size_t g = (idx - c * G * n) / n;
+  out[idx] += scale * src[c * G + g];
+}
+
+extern "C" int pfsgnn_graph_bcast_add(float* out, int C, int G, int n, const float* src,
+                                      float scale, void* stream) {
+  PF_REQUIRE(out && src && C > 0 && G > 0 && n > 0, "pfsgnn_graph_bcast_add", "bad arguments");
+  const size_t tot = (size_t)C * G * n;
+  hipLaunchKernelGGL(k_graph_bcast_add, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), out, C, G, n, src, scale);
+  return pf::check_launch("pfsgnn_graph_bcast_add");
+}
+
+// ---------------------------------------------------------------- RMSNorm x2
+// y = x * rsqrt(mean_c x^2 + eps) * w, applied twice (thread per graph row).
+__global__ void k_rms2_fwd(const float* __restrict__ X, int C, int G, const float* __restrict__ w,
+                           float eps, float* __restrict__ Y, float* __restrict__ y1,
+                           float* __restrict__ r1, float* __restrict__ r2) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  float s = 0.f;
+  for (int c = 0; c < C; ++c) { const float x = X[(size_t)c * G + g]; s += x * x; }
+  const float a = rsqrtf(s / C + eps);
+  float s2 = 0.f;
+  for (int c = 0; c < C; ++c) {
+    const float v = X[(size_t)c * G + g] * a * w[c];
+    y1[(size_t)c * G + g] = v;
+    s2 += v * v;
+  }
+  const float b = rsqrtf(s2 / C + eps);
+  for (int c = 0; c < C; ++c) Y[(size_t)c * G + g] = y1[(size_t)c * G + g] * b * w[c];
+  r1[g] = a;
+  r2[g] = b;
+}
+
+extern "C" int pfsgnn_rms2_fwd(const float* X, int C, int G, const float* w, float eps, float* Y,
+                               float* y1, float* r1, float* r2, void* stream) {
+  PF_REQUIRE(X && w && Y && y1 && r1 && r2 && C > 0 && G > 0, "pfsgnn_rms2_fwd", "bad arguments");
+  hipLaunchKernelGGL(k_rms2_fwd, dim3((G + 63) / 64), dim3(64), 0, as_stream(stream), X, C, G, w,
+                     eps, Y, y1, r1, r2);
+  return pf::check_launch("pfsgnn_rms2_fwd");
+}
+
+// backward: one block, thread per graph row computes dX; dw reduced over rows
+__global__ void k_rms2_bwd(const float* __restrict__ dY, const float* __restrict__ X,
+                           const float* __restrict__ w, const float* __restrict__ y1,
+                           const float* __restrict__ r1, const float* __restrict__ r2, int C,
+                           int G, float* __restrict__ dX, float* __restrict__ dwpart) {
+  // dwpart [G][C] per-row contributions, summed by the host-side reduce
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  const float a = r1[g], b = r2[g];
+  // second application: y = y1 * b * w
+  float dot = 0.f;
+  for (int c = 0; c < C; ++c) {
+    const float dy = dY[(size_t)c * G + g];
+    const float x = y1[(size_t)c * G + g];
+    dwpart[(size_t)g * C + c] = dy * x * b;
+    dot += dy * w[c] * x;
+  }
+  // d1 = b*dxn - x*b^3*dot/C, dxn = dy*w ; then first application on X
+  float dot2 = 0.f;
+  for (int c = 0; c < C; ++c) {
+    const float dy = dY[(size_t)c * G + g];
+    const float x1 = y1[(size_t)c * G + g];
+    const float d1 = b * dy * w[c] - x1 * b * b * b * dot / C;
+    dX[(size_t)c * G + g] = d1;  // temp
+    const float x0 = X[(size_t)c * G + g];
+    dwpart[(size_t)g * C + c] += d1 * x0 * a;
+    dot2 += d1 * w[c] * x0;
+  }
+  for (int c = 0; c < C; ++c) {
+    const float d1 = dX[(size_t)c * G + g];
+    const float x0 = X[(size_t)c * G + g];
+    dX[(size_t)c * G + g] = a * d1 * w[c] - x0 * a * a * a * dot2 / C;
+  }
+}
+
+extern "C" int pfsgnn_rms2_bwd(const float* dY, const float* X, const float* w, const float* y1,
+                               const float* r1, const float* r2, int C, int G, float eps,
+                               float* dX, float* dw, void* ws, size_t ws_bytes, void* stream) {
+  (void)eps;
+  PF_REQUIRE(dY && X && w && dX && dw && C > 0 && G > 0, "pfsgnn_rms2_bwd", "bad arguments");
+  hipStream_t st = as_stream(stream);
+  const size_t need = (size_t)G * C * sizeof(float);
+  PF_REQUIRE(ws && ws_bytes >= need, "pfsgnn_rms2_bwd", "workspace too small");
+  float* part = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(k_rms2_bwd, dim3((G + 63) / 64), dim3(64), 0, st, dY, X, w, y1, r1, r2, C, G,
+                     dX, part);
+  launch_reduce_rows(part, G, (size_t)C, C, 1, C, dw, C, 1, 1.f, st);
+  return pf::check_launch("pfsgnn_rms2_bwd");
+}
+
+// ---------------------------------------------------------------- BN x2 (edges)
+__global__ void k_bn2_finalize(const float* __restrict__ mu1, const float* __restrict__ var1,
+                               const float* __restrict__ gamma, const float* __restrict__ beta,
+                               float* __restrict__ rm, float* __restrict__ rv, int C, long long n,
+                               float momentum, float eps, float* __restrict__ sc,
+                               float* __restrict__ sh, float* __restrict__ inv1o,
+                               float* __restrict__ inv2o) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  const float g = gamma[c], bt = beta[c], m = mu1[c], v = var1[c];
+  const float inv1 = 1.0f / sqrtf(v + eps);
+  const float rho = v * inv1 * inv1;
+  const float v2 = g * g * rho;
+  const float inv2 = 1.0f / sqrtf(v2 + eps);
+  const float s = g * g * inv1 * inv2;
+  sc[c] = s;
+  sh[c] = bt - m * s;
+  inv1o[c] = inv1;
+  inv2o[c] = inv2;
+  if (rm) {
+    const float f = n > 1 ? (float)((double)n / (double)(n - 1)) : 1.f;
+    float a = (1.f - momentum) * rm[c] + momentum * m;
+    float b = (1.f - momentum) * rv[c] + momentum * (v * f);
+    a = (1.f - momentum) * a + momentum * bt;
+    b = (1.f - momentum) * b + momentum * (v2 * f);
+    rm[c] = a;
+    rv[c] = b;
+  }
+}
+
+extern "C" int pfsgnn_bn2_finalize(const float* mu1, const float* var1, const float* gamma,
+                                   const float* beta, float* rm, float* rv, int C, long long n,
+                                   float momentum, float eps, float* sc, float* sh, float* inv1,
+                                   float* inv2, void* stream) {
+  PF_REQUIRE(mu1 && var1 && gamma && beta && sc && sh && inv1 && inv2 && C > 0 && C <= 64,
+             "pfsgnn_bn2_finalize", "bad arguments");
+  hipLaunchKernelGGL(k_bn2_finalize, dim3(1), dim3(64), 0, as_stream(stream), mu1, var1, gamma,
+                     beta, rm, rv, C, n, momentum, eps, sc, sh, inv1, inv2);
+  return pf::check_launch("pfsgnn_bn2_finalize");
+}
+
+__global__ void k_bn2_bwd_coef(const float* __restrict__ Sg, const float* __restrict__ Sgx,
+                               const float* __restrict__ mu1, const float* __restrict__ var1,
+                               const float* __restrict__ gamma, int C, long long n, float eps,
+                               float* __restrict__ alpha, float* __restrict__ gam0,
+                               float* __restrict__ gam1, float* __restrict__ dgamma,
+                               float* __restrict__ dbeta) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  const float g = gamma[c], v = var1[c];
+  const float inv1 = 1.0f / sqrtf(v + eps);
+  const float rho = v * inv1 * inv1;
+  const float inv2 = 1.0f / sqrtf(g * g * rho + eps);
+  const float k = g * inv2;
+  const float M = Sgx[c] / (float)n;
+  const float a = g * inv1 * k;
+  const float g1 = -a * M * (k * k + 1.f - k * k * rho) * inv1;
+  alpha[c] = a;
+  gam1[c] = g1;
+  gam0[c] = -a * Sg[c] / (float)n - g1 * mu1[c];
+  dgamma[c] += k * Sgx[c] * (2.f - k * k * rho);
+  dbeta[c] += Sg[c];
+}
+
+extern "C" int pfsgnn_bn2_bwd_coef(const float* Sg, const float* Sgx, const float* mu1,
+                                   const float* var1, const float* gamma, int C, long long n,
+                                   float eps, float* alpha, float* gam0, float* gam1,
+                                   float* dgamma, float* dbeta, void* stream) {
+  PF_REQUIRE(Sg && Sgx && mu1 && var1 && gamma && alpha && gam0 && gam1 && dgamma && dbeta &&
+                 C > 0 && C <= 64,
+             "pfsgnn_bn2_bwd_coef", "bad arguments");
+  hipLaunchKernelGGL(k_bn2_bwd_coef, dim3(1), dim3(64), 0, as_stream(stream), Sg, Sgx, mu1, var1,
+                     gamma, C, n, eps, alpha, gam0, gam1, dgamma, dbeta);
+  return pf::check_launch("pfsgnn_bn2_bwd_coef");
+}
+
+// ---------------------------------------------------------------- moments
+__global__ void k_moment_coef(const float* __restrict__ mom, const float* __restrict__ gst, int C,
+                              int NS, int n, float* __restrict__ coef) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // over C*NS
+  const size_t CN = (size_t)C * NS;
+  if (idx >= CN) return;
+  const float c2 = mom[CN + idx], c3 = mom[2 * CN + idx], c4 = mom[3 * CN + idx];
+  const float gmean = gst[idx], gstd = gst[CN + idx], gskew = gst[2 * CN + idx],
+              gkurt = gst[3 * CN + idx];
+  const float var = c2 > 0.f ? c2 : 0.01f * c2;
+  const float sd = sqrtf(var + 1e-6f);
+  const float sd2 = sd * sd, sd3 = sd2 * sd, sd4 = sd2 * sd2;
+  const float A3 = gskew / sd3;
+  const float A4 = gkurt / sd4;
+  const float gstd_tot = gstd - 3.f * gskew * c3 / sd4 - 4.f * gkurt * c4 / (sd4 * sd);
+  const float gvr = gstd_tot / (2.f * sd) * (c2 > 0.f ? 1.f : 0.01f);
+  const float invn = 1.0f / (float)n;
+  coef[idx] = (gmean - 3.f * c2 * A3 - 4.f * c3 * A4) * invn;
+  coef[CN + idx] = 2.f * gvr * invn;
+  coef[2 * CN + idx] = 3.f * A3 * invn;
+  coef[3 * CN + idx] = 4.f * A4 * invn;
+}
+
+extern "C" int pfsgnn_moment_coef(const float* mom, const float* gst, int C, int NS, int n,
+                                  float* coef, void* stream) {
+  PF_REQUIRE(mom && gst && coef && C > 0 && NS > 0 && n > 0, "pfsgnn_moment_coef",
+             "bad arguments");
+  const size_t tot = (size_t)C * NS;
+  hipLaunchKernelGGL(k_moment_coef, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), mom, gst, C, NS, n, coef);
+  return pf::check_launch("pfsgnn_moment_coef");
+}
+
+// ---------------------------------------------------------------- adam
+// torch.optim.Adam single-tensor semantics (torch/optim/adam.py
+// _single_tensor_adam, amsgrad=False): bias corrections on the host in double.
+__global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                       float* __restrict__ v, long long n, float neg_step, float beta1, float beta2,
+                       float bc2_sqrt, float eps, float wd) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float gi = g[i];
+  if (wd != 0.f) gi = gi + wd * p[i];
+  const float mo = m[i];
+  const float mi = mo + (1.f - beta1) * (gi - mo);        // exp_avg.lerp_(grad, 1-beta1)
+  const float vi = v[i] * beta2 + (1.f - beta2) * gi * gi; // mul_(beta2).addcmul_(g, g, 1-beta2)
+  m[i] = mi;
+  v[i] = vi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;          // (sqrt(v)/sqrt(bc2)).add_(eps)
+  p[i] = p[i] + neg_step * (mi / denom);                   // addcdiv_(m, denom, -lr/bc1)
+}
+
+extern "C" int pfsgnn_adam(float* p, const float* g, float* m, float* v, long long n, int step,
+                           float lr, float beta1, float beta2, float eps, float weight_decay,
+                           void* stream) {
+  PF_REQUIRE(p && g && m && v && n > 0 && step >= 1, "pfsgnn_adam", "bad arguments");
+  const double bc1 = 1.0 - std::pow((double)beta1, step);
+  const double bc2 = 1.0 - std::pow((double)beta2, step);
+  const float neg_step = (float)(-(double)lr / bc1);
+  const float bc2_sqrt = (float)std::sqrt(bc2);
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream),
+                     p, g, m, v, n, neg_step, beta1, beta2, bc2_sqrt, eps, weight_decay);
+  return pf::check_launch("pfsgnn_adam");
+}

@@ -1,0 +1,350 @@
+"""Fused training-step engine for the bipartite fiber/class GNN.
+
+This is the orchestration layer of the hot path.  It runs ``GNN.forward``
+(gnn.py:280-305) and its backward -- which the reference gets from autograd
+through ``torch.cat`` / ``torch_scatter`` / BatchNorm -- as a short, explicit
+sequence of ops on a backend.  In the product the backend is
+``native.HipBackend``: every op is a HIP kernel in ``libpfsgnn.so`` reached
+through the C ABI in ``include/pfsgnn.h``.  (The test suite hands the same
+engine a torch-CPU emulation of the op set to check every hand-derived
+backward formula against the autograd oracle; the product never does.)
+
+Layouts (DESIGN.md §Data layout): node tensors are channel-major ``[C, N]``;
+edge tensors are channel-major ``[C, E]`` over the canonical fiber-major edge
+order ``e = (g*NF + f)*NC + c`` of a batch of G complete bipartite graphs.
+Edge state is kept *lazily*: an EdgeModel output is its pre-norm value ``y``
+plus a per-channel affine ``(sc, sh)`` (xe_new = sc*y + sh) -- the triple
+``xe3 = (y, sc, sh)``; consumers apply the affine on the fly, so inside the
+stack the normalised edge tensor is never written to HBM.
+
+Algebra used to cut per-edge work (all exact in real arithmetic):
+* the first Linear of every per-edge MLP is split over its concatenated input
+  (gnn.py:100/136/188): node parts are computed once per node (``Ps``, ``Pt``,
+  ``Qt``, ``Rs``) and gathered; only the edge-feature part is per edge;
+* TModel's ``scatter(MLP(msg), tgt, 'sum')`` (gnn.py:190) equals
+  ``W2 @ scatter(lrelu(W1 msg + b1)) + NF*b2``: the second Linear runs after
+  the per-class sum;
+* the EdgeModel's BatchNorm runs twice (gnn.py:101 -- ``super().forward`` runs
+  the Sequential's ``norm`` child, then ``self.norm`` again; the reference
+  checkpoint's num_batches_tracked = 2 x epochs confirms it) and collapses to
+  one affine forward and one per-channel coefficient triple backward;
+* in backward, TModel's per-edge input gradient is recomputed inside the
+  SModel edge pass, which also adds the downstream edge gradient and takes the
+  edge BatchNorm's two gradient sums -- one pass instead of four.
+"""
+import torch
+
+
+class Dims:
+    """Batch geometry: G graphs of NF fibers x NC classes, feature width F."""
+
+    def __init__(self, G, NF, NC, F):
+        self.G, self.NF, self.NC, self.F = int(G), int(NF), int(NC), int(F)
+        self.E = self.G * self.NF * self.NC
+        self.NS = self.G * self.NF
+        self.NT = self.G * self.NC
+
+    def __repr__(self):
+        return f"Dims(G={self.G}, NF={self.NF}, NC={self.NC}, F={self.F}, E={self.E})"
+
+
+def param_names(B, normed=True):
+    """Parameter names in the reference's state_dict order (gnn.py:266-278)."""
+    names = []
+
+    def mlp(pre):
+        names.extend([pre + ".0.weight", pre + ".0.bias", pre + ".2.weight", pre + ".2.bias"])
+
+    mlp("encoder_s")
+    mlp("encoder_t")
+    for b in range(B):
+        p = f"mpb.{b}."
+        mlp(p + "edge_model")
+        if normed:
+            names.extend([p + "edge_model.norm.weight", p + "edge_model.norm.bias"])
+        for m in ("s_model", "t_model"):
+            mlp(p + m + ".node_mlp_1")
+            mlp(p + m + ".node_mlp_2")
+            if normed:
+                names.extend([p + m + ".norm.weight", p + m + ".norm.bias"])
+        mlp(p + "global_model")
+        if normed:
+            names.append(p + "global_model.norm.weight")
+    mlp("decoder_e")
+    mlp("decoder_s")
+    return names
+
+
+class Engine:
+    def __init__(self, backend, F, B=0, Fs=1, Ft=1, T=1, normed=True, bn_eps=1e-5,
+                 bn_momentum=0.1, rms_eps=None):
+        self.be = backend
+        self.F, self.B, self.Fs, self.Ft, self.T = F, B, Fs, Ft, T
+        self.normed = normed
+        self.bn_eps = bn_eps
+        self.bn_momentum = bn_momentum
+        self.rms_eps = rms_eps
+
+    # ================================================================= MLP
+    def mlp_fwd(self, P, pre, X):
+        """MLP (gnn.py:65): Linear -> LeakyReLU(0.1) -> Linear on [K, N]."""
+        be = self.be
+        W1, b1, W2, b2 = P[pre + "0.weight"], P[pre + "0.bias"], P[pre + "2.weight"], P[pre + "2.bias"]
+        Z = be.lin(W1, 0, W1.shape[1], X, b=b1)
+        Y = be.lin(W2, 0, W2.shape[1], Z, b=b2, act_in=True)
+        return Y, (X, Z)
+
+    def mlp_bwd(self, P, Gr, pre, dY, saved, want_dx=True):
+        be = self.be
+        X, Z = saved
+        W1, W2 = P[pre + "0.weight"], P[pre + "2.weight"]
+        be.wgrad(dY, Z, Gr[pre + "2.weight"], db=Gr[pre + "2.bias"], act_in=True)
+        dZ = be.lin_t(W2, 0, W2.shape[1], dY, z=Z)
+        be.wgrad(dZ, X, Gr[pre + "0.weight"], db=Gr[pre + "0.bias"])
+        return be.lin_t(W1, 0, W1.shape[1], dZ) if want_dx else None
+
+    def _bn(self, P, BN, key, X):
+        if not self.normed:
+            return X, None
+        Y, mu, var = self.be.bn_fwd(X, P[key + "weight"], P[key + "bias"],
+                                    BN.get(key + "running_mean"), BN.get(key + "running_var"),
+                                    self.bn_momentum, self.bn_eps)
+        return Y, (X, mu, var)
+
+    def _bn_bwd(self, P, Gr, key, dY, saved):
+        if saved is None:
+            return dY
+        X, mu, var = saved
+        return self.be.bn_bwd(dY, X, mu, var, P[key + "weight"], self.bn_eps,
+                              Gr[key + "weight"], Gr[key + "bias"])
+
+    def _rms_eps(self, t):
+        return self.rms_eps if self.rms_eps is not None else torch.finfo(t.dtype).eps
+
+    # ========================================================= model pieces
+    # --- EdgeModel (gnn.py:86-101)
+    def edge_fwd(self, P, BN, d, pre, xs, xt, xe3, u):
+        be, F = self.be, self.F
+        W1, b1 = P[pre + "0.weight"], P[pre + "0.bias"]
+        W2, b2 = P[pre + "2.weight"], P[pre + "2.bias"]
+        Ps = be.lin(W1, 0, F, xs)
+        Pt = be.lin(W1, F, F, xt, b=b1)
+        be.graph_bcast_add(Pt, be.lin(W1, 3 * F, F, u))
+        y, mu1, var1 = be.edge_mlp_fwd(d, xe3[0], xe3[1], xe3[2], Ps, Pt, W1, W2, b2)
+        if self.normed:
+            key = pre + "norm."
+            sc, sh, inv1, _ = be.bn2_finalize(mu1, var1, P[key + "weight"], P[key + "bias"],
+                                              BN.get(key + "running_mean"), BN.get(key + "running_var"),
+                                              d.E, self.bn_momentum, self.bn_eps)
+        else:
+            sc = sh = inv1 = None
+        return dict(xs=xs, xt=xt, xe3=xe3, u=u, Ps=Ps, Pt=Pt, y=y, mu1=mu1, var1=var1,
+                    sc=sc, sh=sh, inv1=inv1)
+
+    def edge_bwd(self, P, Gr, d, pre, st, g_tot, Sg, Sgx, want_gxe, g_xs, g_xt, g_u):
+        """g_tot: d loss / d xe_new (canonical [F, E]); Sg/Sgx its BatchNorm sums.
+        Adds the node-input gradients into g_xs / g_xt / g_u; returns d loss / d xe_in."""
+        be, F, G = self.be, self.F, d.G
+        if self.normed:
+            key = pre + "norm."
+            alpha, gam0, gam1 = be.bn2_bwd_coef(Sg, Sgx, st["mu1"], st["var1"], P[key + "weight"],
+                                                d.E, self.bn_eps, Gr[key + "weight"], Gr[key + "bias"])
+        else:
+            alpha, gam0, gam1 = be.ones(F), be.zeros(F), be.zeros(F)
+        W1, W2 = P[pre + "0.weight"], P[pre + "2.weight"]
+        xe, xsc, xsh = st["xe3"]
+        dW1 = Gr[pre + "0.weight"]
+        g_xe, GzEs, GzEt = be.edge_mlp_bwd(d, g_tot, alpha, gam0, gam1, st["y"], xe, xsc, xsh,
+                                           st["Ps"], st["Pt"], W1, W2, dW1, Gr[pre + "2.weight"],
+                                           Gr[pre + "2.bias"], want_gxe=want_gxe)
+        be.wgrad(GzEs, st["xs"], dW1, col0=0)
+        be.lin_t(W1, 0, F, GzEs, out=g_xs, add=True)
+        be.wgrad(GzEt, st["xt"], dW1, col0=F, db=Gr[pre + "0.bias"])
+        be.lin_t(W1, F, F, GzEt, out=g_xt, add=True)
+        GzEu = be.graph_reduce(GzEt, G)
+        be.wgrad(GzEu, st["u"], dW1, col0=3 * F)
+        be.lin_t(W1, 3 * F, F, GzEu, out=g_u, add=True)
+        return g_xe
+
+    # --- SModel (gnn.py:123-154)
+    def source_fwd(self, P, BN, d, pre, xs, xt, xe3, u):
+        be, F = self.be, self.F
+        Ws1, bs1 = P[pre + "node_mlp_1.0.weight"], P[pre + "node_mlp_1.0.bias"]
+        Ws2, bs2 = P[pre + "node_mlp_1.2.weight"], P[pre + "node_mlp_1.2.bias"]
+        Qt = be.lin(Ws1, 0, F, xt, b=bs1)
+        hS = be.empty(10 * F, d.NS)
+        hS[0:F].copy_(xs)
+        mom = be.source_fwd(d, xe3[0], xe3[1], xe3[2], Qt, Ws1, Ws2, bs2, hS[F:9 * F])
+        hS[9 * F:10 * F].zero_()
+        be.graph_bcast_add(hS[9 * F:10 * F], u)
+        ys, sS = self.mlp_fwd(P, pre + "node_mlp_2.", hS)
+        xs_new, bnS = self._bn(P, BN, pre + "norm.", ys)
+        return dict(xs=xs, xt=xt, xe3=xe3, u=u, Qt=Qt, mom=mom, sS=sS, bnS=bnS, xs_new=xs_new)
+
+    def source_node_bwd(self, P, Gr, d, pre, st, g_xs_new, g_xs, g_u):
+        """Node half of the SModel backward; returns the per-fiber moment coefficients."""
+        be, F, G = self.be, self.F, d.G
+        g_ys = self._bn_bwd(P, Gr, pre + "norm.", g_xs_new, st["bnS"])
+        g_hS = self.mlp_bwd(P, Gr, pre + "node_mlp_2.", g_ys, st["sS"])
+        g_xs += g_hS[0:F]
+        g_u += be.graph_reduce(g_hS[9 * F:10 * F], G)
+        return be.moment_coef(st["mom"], g_hS[F:9 * F], d.NC)
+
+    def source_edge_bwd(self, P, Gr, d, pre, st, coef, tpart, g_next, bnstat, g_xt):
+        be, F = self.be, self.F
+        Ws1, Ws2 = P[pre + "node_mlp_1.0.weight"], P[pre + "node_mlp_1.2.weight"]
+        y, sc, sh = st["xe3"]
+        g_tot, GzS, Sg, Sgx = be.source_bwd(
+            d, y, sc, sh, st["Qt"], Ws1, Ws2, P[pre + "node_mlp_1.2.bias"], st["mom"][0], coef,
+            tpart, g_next, bnstat, Gr[pre + "node_mlp_1.0.weight"], Gr[pre + "node_mlp_1.2.weight"],
+            Gr[pre + "node_mlp_1.2.bias"])
+        be.wgrad(GzS, st["xt"], Gr[pre + "node_mlp_1.0.weight"], col0=0,
+                 db=Gr[pre + "node_mlp_1.0.bias"])
+        be.lin_t(Ws1, 0, F, GzS, out=g_xt, add=True)
+        return g_tot, Sg, Sgx
+
+    # --- TModel (gnn.py:175-192)
+    def target_fwd(self, P, BN, d, pre, xs, xt, xe3, u):
+        be, F = self.be, self.F
+        Wt1, bt1 = P[pre + "node_mlp_1.0.weight"], P[pre + "node_mlp_1.0.bias"]
+        Wt2, bt2 = P[pre + "node_mlp_1.2.weight"], P[pre + "node_mlp_1.2.bias"]
+        Rs = be.lin(Wt1, 0, F, xs, b=bt1)
+        hsum = be.target_fwd(d, xe3[0], xe3[1], xe3[2], Rs, Wt1)
+        hT = be.empty(4 * F, d.NT)
+        hT[0:F].copy_(xt)
+        be.lin(Wt2, 0, 2 * F, hsum, b=bt2, bscale=float(d.NF), out=hT[F:3 * F])
+        hT[3 * F:4 * F].zero_()
+        be.graph_bcast_add(hT[3 * F:4 * F], u)
+        yt, sT = self.mlp_fwd(P, pre + "node_mlp_2.", hT)
+        xt_new, bnT = self._bn(P, BN, pre + "norm.", yt)
+        return dict(xs=xs, xt=xt, xe3=xe3, u=u, Rs=Rs, hsum=hsum, sT=sT, bnT=bnT, xt_new=xt_new)
+
+    def target_node_bwd(self, P, Gr, d, pre, st, g_xt_new, g_xt, g_u):
+        be, F, G = self.be, self.F, d.G
+        g_yt = self._bn_bwd(P, Gr, pre + "norm.", g_xt_new, st["bnT"])
+        g_hT = self.mlp_bwd(P, Gr, pre + "node_mlp_2.", g_yt, st["sT"])
+        g_xt += g_hT[0:F]
+        g_agg = g_hT[F:3 * F]
+        g_u += be.graph_reduce(g_hT[3 * F:4 * F], G)
+        Wt2 = P[pre + "node_mlp_1.2.weight"]
+        be.wgrad(g_agg, st["hsum"], Gr[pre + "node_mlp_1.2.weight"],
+                 db=Gr[pre + "node_mlp_1.2.bias"], dbscale=float(d.NF))
+        return be.lin_t(Wt2, 0, 2 * F, g_agg)
+
+    def target_edge_bwd(self, P, Gr, d, pre, st, g_hsum, want_gxe, g_xs):
+        be, F = self.be, self.F
+        Wt1 = P[pre + "node_mlp_1.0.weight"]
+        y, sc, sh = st["xe3"]
+        GzT, gxe = be.target_bwd(d, y, sc, sh, st["Rs"], Wt1, g_hsum,
+                                 Gr[pre + "node_mlp_1.0.weight"], want_gxe=want_gxe)
+        be.wgrad(GzT, st["xs"], Gr[pre + "node_mlp_1.0.weight"], col0=0,
+                 db=Gr[pre + "node_mlp_1.0.bias"])
+        be.lin_t(Wt1, 0, F, GzT, out=g_xs, add=True)
+        return gxe
+
+    # --- GlobalModel (gnn.py:208-223; its RMSNorm also runs twice)
+    def global_fwd(self, P, d, pre, xs, xt, u):
+        be, F, G = self.be, self.F, d.G
+        hU = be.empty(3 * F, G)
+        hU[0:F].copy_(u)
+        hU[F:2 * F].copy_(be.graph_reduce(xs, G, mean=True))
+        hU[2 * F:3 * F].copy_(be.graph_reduce(xt, G, mean=True))
+        v, sU = self.mlp_fwd(P, pre, hU)
+        if self.normed:
+            u_new, rms = be.rms2_fwd(v, P[pre + "norm.weight"], self._rms_eps(v))
+        else:
+            u_new, rms = v, None
+        return dict(sU=sU, v=v, rms=rms, u_new=u_new)
+
+    def global_bwd(self, P, Gr, d, pre, st, g_u_new, g_xs, g_xt, g_u):
+        be, F = self.be, self.F
+        if self.normed:
+            g_v = be.rms2_bwd(g_u_new, st["v"], P[pre + "norm.weight"], st["rms"],
+                              self._rms_eps(st["v"]), Gr[pre + "norm.weight"])
+        else:
+            g_v = g_u_new
+        g_hU = self.mlp_bwd(P, Gr, pre, g_v, st["sU"])
+        g_u += g_hU[0:F]
+        be.graph_bcast_add(g_xs, g_hU[F:2 * F], 1.0 / d.NF)
+        be.graph_bcast_add(g_xt, g_hU[2 * F:3 * F], 1.0 / d.NC)
+
+    # ============================================================ GNN path
+    def forward(self, P, BN, d, xs_in, xt_in, xe_in, u_in, training=True):
+        """GNN.forward (gnn.py:280-305).  xs_in [Fs, NS], xt_in [Ft, NT], xe_in [F, E],
+        u_in [F, G] (channel-major).  Returns a context with the outputs
+        (xs, xt, xe3, u) and everything backward needs."""
+        if not training:
+            raise NotImplementedError("eval-mode BatchNorm (running statistics) is not on the "
+                                      "training hot path; see DESIGN.md §Scope")
+        xs, s_enc = self.mlp_fwd(P, "encoder_s.", xs_in)
+        xt, t_enc = self.mlp_fwd(P, "encoder_t.", xt_in)
+        ctx = {"d": d, "enc": (s_enc, t_enc), "blocks": []}
+        xe3 = (xe_in, None, None)
+        u = u_in
+        for b in range(self.B):
+            p = f"mpb.{b}."
+            se = self.edge_fwd(P, BN, d, p + "edge_model.", xs, xt, xe3, u)
+            xe3n = (se["y"], se["sc"], se["sh"])
+            ss = self.source_fwd(P, BN, d, p + "s_model.", xs, xt, xe3n, u)
+            stt = self.target_fwd(P, BN, d, p + "t_model.", ss["xs_new"], xt, xe3n, u)
+            su = self.global_fwd(P, d, p + "global_model.", ss["xs_new"], stt["xt_new"], u)
+            ctx["blocks"].append((se, ss, stt, su))
+            xs, xt, xe3, u = ss["xs_new"], stt["xt_new"], xe3n, su["u_new"]
+        ctx["out"] = (xs, xt, xe3, u)
+        return ctx
+
+    def backward(self, P, Gr, ctx, g_xe_out=None, g_xs_out=None, g_xt_out=None, g_u_out=None):
+        """Accumulates parameter gradients into ``Gr`` (same keys as ``P``).
+        g_xe_out is [F, E] canonical, w.r.t. the final edge features."""
+        d, be, F = ctx["d"], self.be, self.F
+        g_xs, g_xt, g_xe, g_u = g_xs_out, g_xt_out, g_xe_out, g_u_out
+        for b in reversed(range(self.B)):
+            se, ss, stt, su = ctx["blocks"][b]
+            p = f"mpb.{b}."
+            g_xs_new = be.zeros(F, d.NS) if g_xs is None else g_xs.clone()
+            g_xt_new = be.zeros(F, d.NT) if g_xt is None else g_xt.clone()
+            g_xs_in, g_xt_in, g_u_in = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
+            if g_u is not None:
+                self.global_bwd(P, Gr, d, p + "global_model.", su, g_u, g_xs_new, g_xt_new, g_u_in)
+            g_hsum = self.target_node_bwd(P, Gr, d, p + "t_model.", stt, g_xt_new, g_xt_in, g_u_in)
+            self.target_edge_bwd(P, Gr, d, p + "t_model.", stt, g_hsum, False, g_xs_new)
+            coef = self.source_node_bwd(P, Gr, d, p + "s_model.", ss, g_xs_new, g_xs_in, g_u_in)
+            Wt1 = P[p + "t_model.node_mlp_1.0.weight"]
+            bnstat = (se["mu1"], se["inv1"]) if self.normed else None
+            g_tot, Sg, Sgx = self.source_edge_bwd(P, Gr, d, p + "s_model.", ss, coef,
+                                                  (stt["Rs"], Wt1, g_hsum), g_xe, bnstat, g_xt_in)
+            g_xe = self.edge_bwd(P, Gr, d, p + "edge_model.", se, g_tot, Sg, Sgx, b > 0,
+                                 g_xs_in, g_xt_in, g_u_in)
+            g_xs, g_xt, g_u = g_xs_in, g_xt_in, g_u_in
+        s_enc, t_enc = ctx["enc"]
+        self.mlp_bwd(P, Gr, "encoder_s.", g_xs, s_enc, want_dx=False)
+        self.mlp_bwd(P, Gr, "encoder_t.", g_xt, t_enc, want_dx=False)
+
+    # ================================================================ loss
+    def loss_forward(self, P, d, xe3, ci, sharpness, seed, pclass=0.1, pfiber=0.1, total_time=42.0,
+                     nfields=10, wutils=2000.0, wvar=1.0, noiselevel=0.3, want_time=False):
+        """train.py:29-80 on the final edge state ``xe3``.  ``ci`` = class_info
+        channel-major [>=2, NT] (row 0 = T_i hours per visit, row 1 = N_i)."""
+        be = self.be
+        y, sc, sh = xe3
+        scale = total_time / d.NC                     # TOTAL_TIME/NCLASSES, train.py:42
+        dec = [P["decoder_e.0.weight"], P["decoder_e.0.bias"], P["decoder_e.2.weight"], P["decoder_e.2.bias"]]
+        n_prime, fiber_time, tmean, tvar, tt = be.loss_fwd(d, y, sc, sh, *dec, ci, scale, sharpness,
+                                                          noiselevel, seed, want_time)
+        loss, utils, variance, Gn, Gf, Gv = be.loss_finalize(d, n_prime, fiber_time, tvar, ci, pclass,
+                                                             pfiber, total_time, nfields, wutils, wvar)
+        lctx = dict(d=d, xe3=xe3, ci=ci, scale=scale, sharpness=sharpness, noiselevel=noiselevel,
+                    seed=seed, tmean=tmean, Gn=Gn, Gf=Gf, Gv=Gv)
+        diag = dict(loss=loss, utils=utils, variance=variance, n_prime=n_prime,
+                    fiber_time=fiber_time, time=tt)
+        return loss.sum(), diag, lctx
+
+    def loss_backward(self, P, Gr, lctx, gscale=1.0):
+        be, d = self.be, lctx["d"]
+        y, sc, sh = lctx["xe3"]
+        dec = [P["decoder_e.0.weight"], P["decoder_e.0.bias"], P["decoder_e.2.weight"], P["decoder_e.2.bias"]]
+        return be.loss_bwd(d, y, sc, sh, *dec, lctx["ci"], lctx["scale"], lctx["sharpness"],
+                           lctx["noiselevel"], lctx["seed"], lctx["Gn"], lctx["Gf"], lctx["Gv"],
+                           lctx["tmean"], gscale,
+                           Gr["decoder_e.0.weight"], Gr["decoder_e.0.bias"],
+                           Gr["decoder_e.2.weight"], Gr["decoder_e.2.bias"])

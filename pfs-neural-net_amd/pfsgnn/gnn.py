@@ -1,0 +1,595 @@
+"""Drop-in operator surface of the reference ``src/gnn.py`` on the HIP engine.
+
+Same classes, constructor signatures, forward signatures and state_dict keys
+as the reference (``BipartiteData`` gnn.py:7, ``Loader`` :49, ``MLP`` :65,
+``EdgeModel`` :73, ``SModel`` :104, ``TModel`` :157, ``GlobalModel`` :195,
+``Block`` :226, ``GNN`` :261), so a reference checkpoint loads with
+``load_state_dict`` and a reference training script runs unchanged apart from
+the import.  Every forward and backward is computed by ``libpfsgnn.so``
+through ``pfsgnn.engine``; PyTorch only allocates, streams and runs autograd's
+bookkeeping.
+
+Edge layout: the kernels run on the canonical fiber-major order of a batch of
+complete bipartite graphs.  ``edge_index`` may list the edges in any order
+(``graphs/graph-0.pt`` does: each fiber's classes come out of an unstable
+argsort); it is validated on the device once (cached per tensor) and mapped
+with a permutation, so results are reported in the caller's edge order.
+Graphs that are not complete bipartite are rejected loudly.
+
+Batching: G graphs collated PyG-style (``Batch.from_data_list``, increments
+from ``BipartiteData.__inc__``) with ``x_u`` of shape [G, F]; ``u[g]`` is
+broadcast to the edges / nodes of graph g and the GlobalModel means are
+per graph.  With G == 1 this is exactly the reference.
+"""
+import torch
+
+from . import config
+from .engine import Dims, Engine
+from .native import HipBackend
+
+_BACKEND = None
+
+
+def backend():
+    global _BACKEND
+    if _BACKEND is None:
+        _BACKEND = HipBackend()
+    return _BACKEND
+
+
+# ====================================================================== data
+class BipartiteData:
+    """gnn.py:7-47 without torch_geometric: same attributes and __inc__."""
+
+    def __init__(self, edge_index=None, x_s=None, x_t=None, x_e=None, x_u=None):
+        dev = config.device
+        self.edge_index = edge_index.to(dev) if edge_index is not None else None
+        self.x_s = x_s.to(dev) if x_s is not None else None
+        self.x_t = x_t.to(dev) if x_t is not None else None
+        if x_t is not None:
+            self.num_nodes = len(self.x_t)
+        self.x_e = x_e.to(dev) if x_e is not None else None
+        self.x_u = x_u.to(dev) if x_u is not None else None
+
+    def __inc__(self, key, value, *args):
+        if key == "edge_index":
+            return torch.tensor([[self.x_s.size(0)], [self.x_t.size(0)]], device=self.edge_index.device)
+        return 0
+
+    @property
+    def num_graphs(self):
+        return 1 if self.x_u is None else int(self.x_u.size(0))
+
+    def to(self, device):
+        out = BipartiteData.__new__(BipartiteData)
+        for k, v in self.__dict__.items():
+            setattr(out, k, v.to(device) if isinstance(v, torch.Tensor) else v)
+        return out
+
+    def keys(self):
+        return [k for k in ("edge_index", "x_s", "x_t", "x_e", "x_u") if getattr(self, k) is not None]
+
+
+class Batch:
+    @staticmethod
+    def from_data_list(graphs):
+        """PyG-style collation (torch_geometric.data.Batch) using __inc__."""
+        ei, xs, xt, xe, xu = [], [], [], [], []
+        inc = None
+        for g in graphs:
+            e = g.edge_index if inc is None else g.edge_index + inc
+            ei.append(e)
+            step = g.__inc__("edge_index", g.edge_index)
+            inc = step if inc is None else inc + step
+            xs.append(g.x_s)
+            xt.append(g.x_t)
+            xe.append(g.x_e)
+            xu.append(g.x_u)
+        return BipartiteData(torch.cat(ei, 1), torch.cat(xs), torch.cat(xt), torch.cat(xe), torch.cat(xu))
+
+
+class Loader(torch.utils.data.Dataset):
+    """gnn.py:49-63."""
+
+    def __init__(self, graphs_list=None):
+        self.graphs_list = graphs_list
+
+    def __len__(self):
+        return len(self.graphs_list)
+
+    def __getitem__(self, idx):
+        return self.graphs_list[idx]
+
+
+# ==================================================================== layout
+_LAYOUT_CACHE = {}
+_EDGE_CACHE = {}
+
+
+def geometry(x_s, x_t, x_u, edge_index, F):
+    """(Dims, perm) for a batch; perm is None when edge_index is already canonical."""
+    G = 1 if x_u is None else int(x_u.size(0))
+    S, T = int(x_s.size(0)), int(x_t.size(0))
+    if S % G or T % G:
+        raise ValueError(f"x_s ({S}) / x_t ({T}) rows are not a multiple of the {G} graphs in x_u")
+    NF, NC = S // G, T // G
+    d = Dims(G, NF, NC, F)
+    E = int(edge_index.size(1))
+    key = (edge_index.data_ptr(), edge_index._version, E, G, NF, NC)
+    hit = _LAYOUT_CACHE.get(key)
+    if hit is None:
+        if E != d.E:
+            raise NotImplementedError(
+                f"edge_index has {E} edges; the HIP kernels need a batch of complete bipartite "
+                f"graphs (G*NF*NC = {d.E}).  General sparse bipartite graphs are a later row of "
+                "the scope (DESIGN.md §Scope)")
+        perm, complete, identity = backend().layout_analyze(edge_index, G, NF, NC)
+        if not complete:
+            raise NotImplementedError("edge_index is not a complete bipartite batch (some "
+                                      "(fiber, class) pair is missing, repeated, or crosses graphs)")
+        hit = None if identity else perm
+        if len(_LAYOUT_CACHE) > 32:
+            _LAYOUT_CACHE.clear()
+        _LAYOUT_CACHE[key] = hit
+    return d, hit
+
+
+def edges_in(x_e, perm, cache=False):
+    """User edge features [E, F] -> canonical channel-major [F, E]."""
+    if perm is None and x_e.dtype == torch.float32 and x_e.is_cuda and x_e.t().is_contiguous():
+        return x_e.t()
+    key = (x_e.data_ptr(), x_e._version, tuple(x_e.shape), None if perm is None else perm.data_ptr())
+    if cache and key in _EDGE_CACHE:
+        return _EDGE_CACHE[key]
+    out = backend().edges_to_canonical(x_e, perm)
+    if cache:
+        if len(_EDGE_CACHE) > 4:
+            _EDGE_CACHE.clear()
+        _EDGE_CACHE[key] = out
+    return out
+
+
+def edges_out(xe3, perm, d):
+    """Canonical (y, sc, sh) -> user edge tensor [E, F] in the caller's order."""
+    be = backend()
+    y, sc, sh = xe3
+    if perm is None:
+        return be.edge_apply(d, y, sc, sh).t()
+    return be.edges_from_canonical(y, sc, sh, perm, rowmajor=True)
+
+
+def grad_edges_in(g, perm):
+    """Gradient w.r.t. a user edge tensor [E, F] -> canonical [F, E]."""
+    if g is None:
+        return None
+    if perm is None and g.t().is_contiguous():
+        return g.t()
+    return backend().edges_to_canonical(g.contiguous(), perm)
+
+
+def grad_edges_out(gc, perm):
+    if gc is None:
+        return None
+    if perm is None:
+        return gc.t()
+    return backend().edges_from_canonical(gc, None, None, perm, rowmajor=True)
+
+
+def _cm(x):
+    """[N, C] user node tensor -> channel-major [C, N] fp32 on the device."""
+    return x.detach().to(device=config.device, dtype=torch.float32).t().contiguous()
+
+
+# ========================================================= parameter store
+class _ParamMixin:
+    """Hands the engine a module's parameters and gradient tensors by name."""
+
+    def _check_device(self):
+        for n, p in self.named_parameters():
+            if not (p.is_cuda and p.dtype == torch.float32):
+                raise RuntimeError(f"parameter {n} must be float32 on the HIP device "
+                                   f"(call .to('cuda')); got {p.dtype} on {p.device}")
+
+    def _flat_sync(self):
+        self._check_device()
+
+    def _flat_params(self):
+        return {n: p.detach() for n, p in self.named_parameters()}
+
+    def _flat_grads(self):
+        out = {}
+        for n, p in self.named_parameters():
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            out[n] = p.grad
+        return out
+
+    def _bn_buffers(self):
+        return {n: b for n, b in self.named_buffers() if "running" in n}
+
+    def _bump_batches(self, edge_keys=(), node_keys=()):
+        bufs = dict(self.named_buffers())
+        for k in edge_keys:
+            bufs[k + "num_batches_tracked"].add_(2)
+        for k in node_keys:
+            bufs[k + "num_batches_tracked"].add_(1)
+
+
+class _FlatMixin(_ParamMixin):
+    """Top-level modules keep all parameters (and grads) as views of one flat
+    fp32 buffer in the reference's state_dict order: the optimiser (FusedAdam)
+    and the data-parallel gradient all-reduce then see a single buffer."""
+
+    def _flat_sync(self):
+        params = list(self.named_parameters())
+        flat = getattr(self, "_pf_flat", None)
+        if flat is not None and len(params) == len(self._pf_off):
+            ok = True
+            for (name, p), (off, n) in zip(params, self._pf_off):
+                if p.data_ptr() != flat.data_ptr() + 4 * off or p.device != flat.device:
+                    ok = False
+                    break
+            if ok:
+                return
+        dev = config.device
+        offs, total = [], 0
+        for _, p in params:
+            offs.append((total, p.numel()))
+            total += (p.numel() + 3) // 4 * 4
+        flat = torch.zeros(total, dtype=torch.float32, device=dev)
+        gflat = torch.zeros(total, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for (name, p), (off, n) in zip(params, offs):
+                flat[off:off + n].copy_(p.detach().reshape(-1))
+                p.data = flat[off:off + n].view(p.shape)
+                p.grad = None
+        for mod in self.modules():                     # move BN buffers along
+            if isinstance(mod, torch.nn.BatchNorm1d):
+                mod.to(dev)
+        self._pf_flat, self._pf_gflat, self._pf_off = flat, gflat, offs
+
+    def _flat_grads(self):
+        """Attach every p.grad as a view of the flat grad buffer (zeroing the
+        slices of grads that were None, keeping the values of existing ones)."""
+        params = [p for _, p in self.named_parameters()]
+        gflat = self._pf_gflat
+        need = [(p, off, n) for p, (off, n) in zip(params, self._pf_off)
+                if p.grad is None or p.grad.data_ptr() != gflat.data_ptr() + 4 * off]
+        if need:
+            if len(need) == len(params) and all(p.grad is None for p, _, _ in need):
+                gflat.zero_()
+                for p, off, n in need:
+                    p.grad = gflat[off:off + n].view(p.shape)
+            else:
+                for p, off, n in need:
+                    sl = gflat[off:off + n]
+                    if p.grad is None:
+                        sl.zero_()
+                    else:
+                        sl.copy_(p.grad.reshape(-1))
+                    p.grad = sl.view(p.shape)
+        return {n: p.grad for n, p in self.named_parameters()}
+
+    def flat_parameters(self):
+        """(flat params, flat grads) -- the buffers FusedAdam / DDP operate on."""
+        self._flat_sync()
+        self._flat_grads()
+        return self._pf_flat, self._pf_gflat
+
+
+def _norm_or_identity(module, Fdim, normed, kind):
+    if normed:
+        module.norm = torch.nn.BatchNorm1d(Fdim) if kind == "bn" else torch.nn.RMSNorm(Fdim)
+    else:
+        module.norm = lambda x: x
+
+
+def _engine_for(F, normed, B=0):
+    return Engine(backend(), F=F, B=B, normed=normed)
+
+
+# =================================================================== models
+class _MLPFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, module):
+        eng = _engine_for(module[0].out_features, True)
+        P = module._flat_params()
+        X = _cm(x)
+        Y, saved = eng.mlp_fwd(P, "", X)
+        ctx.module, ctx.saved_pf = module, saved
+        return Y.t()
+
+    @staticmethod
+    def backward(ctx, gy):
+        module = ctx.module
+        eng = _engine_for(module[0].out_features, True)
+        P = module._flat_params()
+        Gr = module._flat_grads()
+        dx = eng.mlp_bwd(P, Gr, "", gy.t().contiguous(), ctx.saved_pf, want_dx=True)
+        return dx.t(), None, None
+
+
+class MLP(_ParamMixin, torch.nn.Sequential):
+    """gnn.py:65-71: Linear(D1, D2) -> LeakyReLU(0.1) -> Linear(D2, D3)."""
+
+    def __init__(self, D1, D2, D3):
+        super().__init__(torch.nn.Linear(D1, D2), torch.nn.LeakyReLU(0.1), torch.nn.Linear(D2, D3))
+
+    def forward(self, x):
+        self._flat_sync()
+        return _MLPFn.apply(x, self[0].weight, self)
+
+
+def _graph_of(x_s, x_t, u, edge_index, F):
+    d, perm = geometry(x_s, x_t, u, edge_index, F)
+    return d, perm
+
+
+class _EdgeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_s, x_t, edge_attr, u, anchor, module, edge_index):
+        F = module.Fdim
+        d, perm = _graph_of(x_s, x_t, u, edge_index, F)
+        eng = _engine_for(F, module.normed)
+        P, BN = module._flat_params(), module._bn_buffers()
+        st = eng.edge_fwd(P, BN, d, "", _cm(x_s), _cm(x_t), (edges_in(edge_attr, perm), None, None), _cm(u))
+        if module.normed:
+            module._bump_batches(edge_keys=("norm.",))
+        ctx.pf = (module, d, perm, st)
+        return edges_out((st["y"], st["sc"], st["sh"]), perm, d)
+
+    @staticmethod
+    def backward(ctx, g):
+        module, d, perm, st = ctx.pf
+        be, F = backend(), module.Fdim
+        eng = _engine_for(F, module.normed)
+        P, Gr = module._flat_params(), module._flat_grads()
+        gc = grad_edges_in(g, perm).contiguous()
+        Sg = Sgx = None
+        if module.normed:
+            Sg, Sgx = be.edge_bn_grad_sums(d, gc, st["y"], st["mu1"], st["inv1"])
+        g_xs, g_xt, g_u = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
+        g_xe = eng.edge_bwd(P, Gr, d, "", st, gc, Sg, Sgx, True, g_xs, g_xt, g_u)
+        return g_xs.t(), g_xt.t(), grad_edges_out(g_xe, perm), g_u.t(), None, None, None
+
+
+class EdgeModel(MLP):
+    """gnn.py:73-101 (its BatchNorm runs twice, as in the reference)."""
+
+    def __init__(self, Fdim=10, normed=True):
+        F_message = 4 * Fdim
+        super().__init__(F_message, F_message, Fdim)
+        self.Fdim, self.normed = Fdim, normed
+        _norm_or_identity(self, Fdim, normed, "bn")
+
+    def forward(self, x_s, x_t, edge_index, edge_attr, u):
+        self._flat_sync()
+        return _EdgeFn.apply(x_s, x_t, edge_attr, u, self[0].weight, self, edge_index)
+
+
+class _SourceFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_s, x_t, edge_attr, u, anchor, module, edge_index):
+        F = module.Fdim
+        d, perm = _graph_of(x_s, x_t, u, edge_index, F)
+        eng = _engine_for(F, module.normed)
+        P, BN = module._flat_params(), module._bn_buffers()
+        st = eng.source_fwd(P, BN, d, "", _cm(x_s), _cm(x_t), (edges_in(edge_attr, perm), None, None), _cm(u))
+        if module.normed:
+            module._bump_batches(node_keys=("norm.",))
+        ctx.pf = (module, d, perm, st)
+        return st["xs_new"].t()
+
+    @staticmethod
+    def backward(ctx, g):
+        module, d, perm, st = ctx.pf
+        be, F = backend(), module.Fdim
+        eng = _engine_for(F, module.normed)
+        P, Gr = module._flat_params(), module._flat_grads()
+        g_xs, g_xt, g_u = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
+        coef = eng.source_node_bwd(P, Gr, d, "", st, g.t().contiguous(), g_xs, g_u)
+        g_tot, _, _ = eng.source_edge_bwd(P, Gr, d, "", st, coef, None, None, None, g_xt)
+        return g_xs.t(), g_xt.t(), grad_edges_out(g_tot, perm), g_u.t(), None, None, None
+
+
+class SModel(_ParamMixin, torch.nn.Module):
+    """gnn.py:104-154."""
+
+    def __init__(self, Fdim=10, normed=True):
+        super().__init__()
+        F_message = 2 * Fdim
+        self.node_mlp_1 = MLP(F_message, F_message, F_message)
+        F_message2 = 4 * F_message + 2 * Fdim
+        self.node_mlp_2 = MLP(F_message2, F_message2, Fdim)
+        self.Fdim, self.normed = Fdim, normed
+        _norm_or_identity(self, Fdim, normed, "bn")
+
+    def forward(self, x_s, x_t, edge_index, edge_attr, u):
+        self._flat_sync()
+        return _SourceFn.apply(x_s, x_t, edge_attr, u, self.node_mlp_1[0].weight, self, edge_index)
+
+
+class _TargetFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_s, x_t, edge_attr, u, anchor, module, edge_index):
+        F = module.Fdim
+        d, perm = _graph_of(x_s, x_t, u, edge_index, F)
+        eng = _engine_for(F, module.normed)
+        P, BN = module._flat_params(), module._bn_buffers()
+        st = eng.target_fwd(P, BN, d, "", _cm(x_s), _cm(x_t), (edges_in(edge_attr, perm), None, None), _cm(u))
+        if module.normed:
+            module._bump_batches(node_keys=("norm.",))
+        ctx.pf = (module, d, perm, st)
+        return st["xt_new"].t()
+
+    @staticmethod
+    def backward(ctx, g):
+        module, d, perm, st = ctx.pf
+        be, F = backend(), module.Fdim
+        eng = _engine_for(F, module.normed)
+        P, Gr = module._flat_params(), module._flat_grads()
+        g_xs, g_xt, g_u = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
+        g_hsum = eng.target_node_bwd(P, Gr, d, "", st, g.t().contiguous(), g_xt, g_u)
+        gxe = eng.target_edge_bwd(P, Gr, d, "", st, g_hsum, True, g_xs)
+        return g_xs.t(), g_xt.t(), grad_edges_out(gxe, perm), g_u.t(), None, None, None
+
+
+class TModel(_ParamMixin, torch.nn.Module):
+    """gnn.py:157-192."""
+
+    def __init__(self, Fdim=10, normed=True):
+        super().__init__()
+        F_message = 2 * Fdim
+        self.node_mlp_1 = MLP(F_message, F_message, F_message)
+        F_message2 = 4 * Fdim
+        self.node_mlp_2 = MLP(F_message2, F_message2, Fdim)
+        self.Fdim, self.normed = Fdim, normed
+        _norm_or_identity(self, Fdim, normed, "bn")
+
+    def forward(self, x_s, x_t, edge_index, edge_attr, u):
+        self._flat_sync()
+        return _TargetFn.apply(x_s, x_t, edge_attr, u, self.node_mlp_1[0].weight, self, edge_index)
+
+
+class _GlobalFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_s, x_t, u, anchor, module):
+        F = module.Fdim
+        G = int(u.size(0))
+        d = Dims(G, x_s.size(0) // G, x_t.size(0) // G, F)
+        eng = _engine_for(F, module.normed)
+        P = module._flat_params()
+        st = eng.global_fwd(P, d, "", _cm(x_s), _cm(x_t), _cm(u))
+        ctx.pf = (module, d, st)
+        return st["u_new"].t()
+
+    @staticmethod
+    def backward(ctx, g):
+        module, d, st = ctx.pf
+        be, F = backend(), module.Fdim
+        eng = _engine_for(F, module.normed)
+        P, Gr = module._flat_params(), module._flat_grads()
+        g_xs, g_xt, g_u = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
+        eng.global_bwd(P, Gr, d, "", st, g.t().contiguous(), g_xs, g_xt, g_u)
+        return g_xs.t(), g_xt.t(), g_u.t(), None, None
+
+
+class GlobalModel(MLP):
+    """gnn.py:195-223 (its RMSNorm runs twice, as in the reference)."""
+
+    def __init__(self, Fdim=10, normed=True):
+        F_message = 3 * Fdim
+        super().__init__(F_message, F_message, Fdim)
+        self.Fdim, self.normed = Fdim, normed
+        _norm_or_identity(self, Fdim, normed, "rms")
+
+    def forward(self, x_s, x_t, edge_index, edge_attr, u):
+        self._flat_sync()
+        return _GlobalFn.apply(x_s, x_t, u, self[0].weight, self)
+
+
+class Block(torch.nn.Module):
+    """gnn.py:226-259: edge -> source -> target -> global."""
+
+    def __init__(self, Fdim=10, e_model=True, s_model=True, t_model=True, u_model=True, normed=True):
+        super().__init__()
+        if e_model:
+            self.edge_model = EdgeModel(Fdim, normed=normed)
+        if s_model:
+            self.s_model = SModel(Fdim, normed=normed)
+        if t_model:
+            self.t_model = TModel(Fdim, normed=normed)
+        if u_model:
+            self.global_model = GlobalModel(Fdim, normed=normed)
+
+    def forward(self, args):
+        edge_index, x_s, x_t, x_e, x_u = args
+        if hasattr(self, "edge_model"):
+            x_e = self.edge_model(x_s, x_t, edge_index, x_e, x_u)
+        if hasattr(self, "s_model"):
+            x_s = self.s_model(x_s, x_t, edge_index, x_e, x_u)
+        if hasattr(self, "t_model"):
+            x_t = self.t_model(x_s, x_t, edge_index, x_e, x_u)
+        if hasattr(self, "global_model"):
+            x_u = self.global_model(x_s, x_t, edge_index, x_e, x_u)
+        return edge_index, x_s, x_t, x_e, x_u
+
+
+# ====================================================================== GNN
+class _GNNFn(torch.autograd.Function):
+    """The whole GNN.forward as one fused engine call; its backward is the
+    engine's hand-fused block backward (engine.Engine.backward)."""
+
+    @staticmethod
+    def forward(ctx, anchor, model, d, perm, xs_in, xt_in, xe_in, u_in):
+        P, BN = model._flat_params(), model._bn_buffers()
+        ectx = model._engine().forward(P, BN, d, xs_in, xt_in, xe_in, u_in)
+        if model.normed:
+            model._bump_batches(
+                edge_keys=[f"mpb.{b}.edge_model.norm." for b in range(model.B)],
+                node_keys=[f"mpb.{b}.{m}.norm." for b in range(model.B) for m in ("s_model", "t_model")])
+        xs, xt, xe3, u = ectx["out"]
+        ctx.pf = (model, d, perm, ectx)
+        model._pf_last = xe3
+        x_e = edges_out(xe3, perm, d)
+        return xs.t(), xt.t(), x_e, u.t()
+
+    @staticmethod
+    def backward(ctx, g_xs, g_xt, g_xe, g_u):
+        model, d, perm, ectx = ctx.pf
+        P, Gr = model._flat_params(), model._flat_grads()
+        cm = (lambda g: None if g is None else g.t().contiguous())
+        model._engine().backward(P, Gr, ectx, grad_edges_in(g_xe, perm), cm(g_xs), cm(g_xt), cm(g_u))
+        return (None,) * 8
+
+
+class GNN(_FlatMixin, torch.nn.Module):
+    """gnn.py:261-326."""
+
+    def __init__(self, B=4, Fdim=16, T=12, F_s=1, F_t=1, normed=True):
+        super().__init__()
+        self.encoder_s = MLP(F_s, Fdim, Fdim)
+        self.encoder_t = MLP(F_t, Fdim, Fdim)
+        self.mpb = torch.nn.Sequential(*(Block(Fdim, normed=normed) for b in range(B)))
+        self.decoder_e = MLP(Fdim, Fdim, 1)
+        self.decoder_s = MLP(Fdim, Fdim, T)
+        self.B, self.Fdim, self.T, self.F_s, self.F_t, self.normed = B, Fdim, T, F_s, F_t, normed
+
+    def _engine(self):
+        return Engine(backend(), F=self.Fdim, B=self.B, Fs=self.F_s, Ft=self.F_t, T=self.T,
+                      normed=self.normed)
+
+    def forward(self, graph):
+        if not self.training:
+            raise NotImplementedError("GNN.forward in eval mode (BatchNorm running statistics) is "
+                                      "not implemented on the HIP path; the reference trains in "
+                                      "train mode (train.py:108)")
+        for t in (graph.x_s, graph.x_t, graph.x_e, graph.x_u):
+            if t is not None and t.requires_grad:
+                raise NotImplementedError("gradients w.r.t. the graph inputs are not computed")
+        self._flat_sync()
+        d, perm = geometry(graph.x_s, graph.x_t, graph.x_u, graph.edge_index, self.Fdim)
+        xe_in = edges_in(graph.x_e, perm, cache=True)
+        anchor = self.encoder_s[0].weight
+        xs, xt, xe, u = _GNNFn.apply(anchor, self, d, perm, _cm(graph.x_s), _cm(graph.x_t),
+                                     xe_in, _cm(graph.x_u))
+        out = BipartiteData.__new__(BipartiteData)
+        out.edge_index, out.x_s, out.x_t, out.x_e, out.x_u = graph.edge_index, xs, xt, xe, u
+        out.num_nodes = xt.size(0)
+        # lets train.loss_function fuse on the lazy final edge state (y, sc, sh)
+        out._pf = (self, d, perm, xe, self.__dict__.pop("_pf_last"))
+        return out
+
+    def edge_prediction(self, x_e, scale=1):
+        """gnn.py:307-312 (``round`` is the identity: ``self.train`` is a bound
+        method, always truthy, gnn.py:321)."""
+        pred = self.decoder_e(x_e)
+        return torch.nn.functional.softplus(pred) * scale
+
+    def node_prediction(self, x_s, scale=1):
+        """gnn.py:314-319."""
+        pred = self.decoder_s(x_s)
+        return torch.softmax(pred, dim=-1) * scale
+
+    def round(self, x):
+        return x

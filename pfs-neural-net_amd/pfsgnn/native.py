@@ -1,0 +1,451 @@
+"""ctypes binding of libpfsgnn.so (the C ABI in include/pfsgnn.h) as an op backend.
+
+This is the only compute backend of the product.  There is no fallback: if
+the shared library is missing, or the process has no MI355X visible, every
+entry point raises ``NativeUnavailable`` -- the hot path never silently runs
+in PyTorch or on the CPU.
+
+Tensors are passed as raw device pointers on torch's current HIP stream, so
+PyTorch is only the allocator / stream / collective plumbing here.
+"""
+import ctypes
+import os
+
+import torch
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpfsgnn.so")
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+_lib = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+LL = ctypes.c_longlong
+FL = ctypes.c_float
+SZ = ctypes.c_size_t
+ULL = ctypes.c_ulonglong
+
+_SIGS = {
+    "pfsgnn_version": ([], ctypes.c_char_p),
+    "pfsgnn_last_error": ([], ctypes.c_char_p),
+    "pfsgnn_workspace_bytes": ([I, I, I, I], SZ),
+    "pfsgnn_timing_enable": ([I], I),
+    "pfsgnn_timing_reset": ([], I),
+    "pfsgnn_timing_query": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                             ctypes.POINTER(ctypes.c_longlong)], I),
+    "pfsgnn_lin": ([P, I, I, I, P, I, P, FL, I, P, I, P], I),
+    "pfsgnn_lin_t": ([P, I, I, I, P, I, P, P, I, P], I),
+    "pfsgnn_wgrad": ([P, I, P, I, I, I, P, I, P, FL, P, SZ, P], I),
+    "pfsgnn_bn_fwd": ([P, I, I, P, P, P, P, FL, FL, P, P, P, P, SZ, P], I),
+    "pfsgnn_bn_bwd": ([P, P, P, P, P, FL, I, I, P, P, P, P, SZ, P], I),
+    "pfsgnn_graph_reduce": ([P, I, I, I, I, P, P], I),
+    "pfsgnn_graph_bcast_add": ([P, I, I, I, P, FL, P], I),
+    "pfsgnn_rms2_fwd": ([P, I, I, P, FL, P, P, P, P, P], I),
+    "pfsgnn_rms2_bwd": ([P, P, P, P, P, P, I, I, FL, P, P, P, SZ, P], I),
+    "pfsgnn_bn2_finalize": ([P, P, P, P, P, P, I, LL, FL, FL, P, P, P, P, P], I),
+    "pfsgnn_bn2_bwd_coef": ([P, P, P, P, P, I, LL, FL, P, P, P, P, P, P], I),
+    "pfsgnn_moment_coef": ([P, P, I, I, I, P, P], I),
+    "pfsgnn_edge_mlp_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_source_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P], I),
+    "pfsgnn_target_fwd": ([I, I, I, I, P, P, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_target_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_source_bwd": ([I, I, I, I] + [P] * 22 + [P, SZ, P], I),
+    "pfsgnn_edge_bn_grad_sums": ([I, I, I, I, P, P, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_edge_mlp_bwd": ([I, I, I, I] + [P] * 18 + [P, SZ, P], I),
+    "pfsgnn_loss_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, FL, FL, ULL, P, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_loss_finalize": ([I, I, I, P, P, P, P, FL, FL, FL, FL, FL, FL, P, P, P, P, P, P, P], I),
+    "pfsgnn_loss_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, FL, FL, ULL, P, P, P, P, P,
+                         P, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_layout_analyze": ([P, LL, I, I, I, P, P, P, SZ, P], I),
+    "pfsgnn_edges_to_canonical": ([P, LL, I, P, P, P], I),
+    "pfsgnn_edges_from_canonical": ([P, P, P, LL, I, P, I, P, P], I),
+    "pfsgnn_adam": ([P, P, P, P, LL, I, FL, FL, FL, FL, FL, P], I),
+}
+
+
+def lib():
+    """Load libpfsgnn.so (once).  Raises NativeUnavailable if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            raise NativeUnavailable(
+                f"{_LIB_PATH} not found: build it with `make -C pfs-neural-net_amd` "
+                "(or __graft_entry__.build()); there is no non-HIP fallback")
+        L = ctypes.CDLL(_LIB_PATH)
+        for name, (args, ret) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = ret
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS.keys())
+
+
+KERNELS = ["edge_mlp_fwd", "source_fwd", "target_fwd", "target_bwd", "source_bwd",
+           "edge_bn_sums", "edge_mlp_bwd", "loss_fwd", "loss_bwd"]
+
+
+def timing_enable(on=True):
+    lib().pfsgnn_timing_enable(1 if on else 0)
+
+
+def timing_reset():
+    lib().pfsgnn_timing_reset()
+
+
+def timing_query(name):
+    """(total milliseconds, launches) of a main kernel since the last reset."""
+    ms = ctypes.c_double(0.0)
+    n = ctypes.c_longlong(0)
+    lib().pfsgnn_timing_query(name.encode(), ctypes.byref(ms), ctypes.byref(n))
+    return ms.value, n.value
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _check(rc, name):
+    if rc != 0:
+        msg = lib().pfsgnn_last_error().decode()
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+
+
+def _call(name, *args):
+    _check(getattr(lib(), name)(*args), name)
+
+
+class HipBackend:
+    """The op set of pfsgnn.engine on libpfsgnn.so (fp32, channel-major)."""
+
+    name = "hip"
+
+    def __init__(self, device=None):
+        if not torch.cuda.is_available():
+            raise NativeUnavailable("no HIP device visible: the pfsgnn hot path runs only on "
+                                    "an MI355X (gfx950); there is no CPU fallback")
+        lib()
+        self.device = torch.device(device or "cuda")
+        self.dtype = torch.float32
+        self._ws = None
+        self._ws_key = None
+
+    # ------------------------------------------------------------ memory
+    def empty(self, *shape):
+        return torch.empty(*shape, dtype=torch.float32, device=self.device)
+
+    def zeros(self, *shape):
+        return torch.zeros(*shape, dtype=torch.float32, device=self.device)
+
+    def ones(self, *shape):
+        return torch.ones(*shape, dtype=torch.float32, device=self.device)
+
+    def workspace(self, d=None):
+        need = lib().pfsgnn_workspace_bytes(d.G, d.NF, d.NC, d.F) if d is not None else 0
+        need = max(need, 16 << 20)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def _wsargs(self, d=None):
+        ws = self.workspace(d)
+        return ws.data_ptr(), ws.numel()
+
+    @staticmethod
+    def _chk(*ts):
+        for t in ts:
+            if t is not None:
+                assert t.dtype == torch.float32 and t.is_cuda and t.is_contiguous(), \
+                    (t.dtype, t.device, t.shape, t.stride())
+
+    # ------------------------------------------------------------ node ops
+    def lin(self, W, col0, ncol, X, b=None, act_in=False, out=None, add=False, bscale=1.0):
+        M, ldw = W.shape
+        N = X.shape[1]
+        assert X.shape[0] == ncol
+        if out is None:
+            out = self.empty(M, N)
+            add = False
+        self._chk(W, X, b, out)
+        _call("pfsgnn_lin", W.data_ptr() + 4 * col0, ldw, M, ncol, X.data_ptr(), N, _ptr(b),
+              float(bscale), int(act_in), out.data_ptr(), int(add), _stream())
+        return out
+
+    def lin_t(self, W, col0, ncol, dY, z=None, out=None, add=False):
+        M, ldw = W.shape
+        N = dY.shape[1]
+        if out is None:
+            out = self.empty(ncol, N)
+            add = False
+        self._chk(W, dY, z, out)
+        _call("pfsgnn_lin_t", W.data_ptr() + 4 * col0, ldw, M, ncol, dY.data_ptr(), N, _ptr(z),
+              out.data_ptr(), int(add), _stream())
+        return out
+
+    def wgrad(self, dY, X, dW, col0=0, db=None, act_in=False, dbscale=1.0):
+        M, N = dY.shape
+        K = X.shape[0]
+        self._chk(dY, X, dW, db)
+        ws, wsb = self._wsargs(getattr(self, "_dims", None))
+        _call("pfsgnn_wgrad", dY.data_ptr(), M, X.data_ptr(), K, N, int(act_in),
+              dW.data_ptr() + 4 * col0, dW.shape[1], _ptr(db), float(dbscale), ws, wsb, _stream())
+
+    def bn_fwd(self, X, gamma, beta, rm, rv, momentum, eps):
+        C, N = X.shape
+        Y, mu, var = self.empty(C, N), self.empty(C), self.empty(C)
+        self._chk(X, gamma, beta, rm, rv)
+        ws, wsb = self._wsargs(getattr(self, "_dims", None))
+        _call("pfsgnn_bn_fwd", X.data_ptr(), C, N, gamma.data_ptr(), beta.data_ptr(), _ptr(rm),
+              _ptr(rv), float(momentum), float(eps), Y.data_ptr(), mu.data_ptr(), var.data_ptr(),
+              ws, wsb, _stream())
+        return Y, mu, var
+
+    def bn_bwd(self, dY, X, mu, var, gamma, eps, dgamma, dbeta):
+        C, N = X.shape
+        dX = self.empty(C, N)
+        dY = dY.contiguous()
+        self._chk(dY, X, mu, var, gamma, dgamma, dbeta)
+        ws, wsb = self._wsargs(getattr(self, "_dims", None))
+        _call("pfsgnn_bn_bwd", dY.data_ptr(), X.data_ptr(), mu.data_ptr(), var.data_ptr(),
+              gamma.data_ptr(), float(eps), C, N, dX.data_ptr(), dgamma.data_ptr(),
+              dbeta.data_ptr(), ws, wsb, _stream())
+        return dX
+
+    def graph_reduce(self, X, G, mean=False):
+        C, N = X.shape
+        out = self.empty(C, G)
+        self._chk(X)
+        _call("pfsgnn_graph_reduce", X.data_ptr(), C, G, N // G, int(mean), out.data_ptr(),
+              _stream())
+        return out
+
+    def graph_bcast_add(self, out, src, scale=1.0):
+        C, N = out.shape
+        G = src.shape[1]
+        src = src.contiguous()
+        self._chk(out, src)
+        _call("pfsgnn_graph_bcast_add", out.data_ptr(), C, G, N // G, src.data_ptr(),
+              float(scale), _stream())
+        return out
+
+    def rms2_fwd(self, X, w, eps):
+        C, G = X.shape
+        Y, y1, r1, r2 = self.empty(C, G), self.empty(C, G), self.empty(G), self.empty(G)
+        self._chk(X, w)
+        _call("pfsgnn_rms2_fwd", X.data_ptr(), C, G, w.data_ptr(), float(eps), Y.data_ptr(),
+              y1.data_ptr(), r1.data_ptr(), r2.data_ptr(), _stream())
+        return Y, (y1, r1, r2)
+
+    def rms2_bwd(self, dY, X, w, saved, eps, dw):
+        y1, r1, r2 = saved
+        C, G = X.shape
+        dX = self.empty(C, G)
+        dY = dY.contiguous()
+        self._chk(dY, X, w, dw)
+        ws, wsb = self._wsargs(getattr(self, "_dims", None))
+        _call("pfsgnn_rms2_bwd", dY.data_ptr(), X.data_ptr(), w.data_ptr(), y1.data_ptr(),
+              r1.data_ptr(), r2.data_ptr(), C, G, float(eps), dX.data_ptr(), dw.data_ptr(), ws,
+              wsb, _stream())
+        return dX
+
+    def bn2_finalize(self, mu1, var1, gamma, beta, rm, rv, n, momentum, eps):
+        C = mu1.shape[0]
+        sc, sh, inv1, inv2 = self.empty(C), self.empty(C), self.empty(C), self.empty(C)
+        _call("pfsgnn_bn2_finalize", mu1.data_ptr(), var1.data_ptr(), gamma.data_ptr(),
+              beta.data_ptr(), _ptr(rm), _ptr(rv), C, int(n), float(momentum), float(eps),
+              sc.data_ptr(), sh.data_ptr(), inv1.data_ptr(), inv2.data_ptr(), _stream())
+        return sc, sh, inv1, inv2
+
+    def bn2_bwd_coef(self, Sg, Sgx, mu1, var1, gamma, n, eps, dgamma, dbeta):
+        C = mu1.shape[0]
+        a, g0, g1 = self.empty(C), self.empty(C), self.empty(C)
+        _call("pfsgnn_bn2_bwd_coef", Sg.data_ptr(), Sgx.data_ptr(), mu1.data_ptr(),
+              var1.data_ptr(), gamma.data_ptr(), C, int(n), float(eps), a.data_ptr(),
+              g0.data_ptr(), g1.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), _stream())
+        return a, g0, g1
+
+    def moment_coef(self, mom, gst, n):
+        _, C, NS = mom.shape
+        coef = self.empty(4, C, NS)
+        gst = gst.contiguous()
+        self._chk(mom, gst)
+        _call("pfsgnn_moment_coef", mom.data_ptr(), gst.data_ptr(), C, NS, int(n), coef.data_ptr(),
+              _stream())
+        return coef
+
+    # ------------------------------------------------------------ edge ops
+    def _set_dims(self, d):
+        self._dims = d
+
+    def edge_mlp_fwd(self, d, xe, xsc, xsh, Ps, Pt, W1, W2, b2):
+        self._set_dims(d)
+        y, mu, var = self.empty(d.F, d.E), self.empty(d.F), self.empty(d.F)
+        self._chk(xe, Ps, Pt, W1, W2, b2)
+        ws, wsb = self._wsargs(d)
+        _call("pfsgnn_edge_mlp_fwd", d.G, d.NF, d.NC, d.F, xe.data_ptr(), _ptr(xsc), _ptr(xsh),
+              Ps.data_ptr(), Pt.data_ptr(), W1.data_ptr(), W2.data_ptr(), b2.data_ptr(),
+              y.data_ptr(), mu.data_ptr(), var.data_ptr(), ws, wsb, _stream())
+        return y, mu, var
+
+    def source_fwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, hs_out):
+        mom = self.empty(4, 2 * d.F, d.NS)
+        self._chk(y, Qt, Ws1, Ws2, bs2, hs_out)
+        _call("pfsgnn_source_fwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
+              Qt.data_ptr(), Ws1.data_ptr(), Ws2.data_ptr(), bs2.data_ptr(), mom.data_ptr(),
+              hs_out.data_ptr(), _stream())
+        return mom
+
+    def target_fwd(self, d, y, sc, sh, Rs, Wt1):
+        hsum = self.empty(2 * d.F, d.NT)
+        ws, wsb = self._wsargs(d)
+        _call("pfsgnn_target_fwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
+              Rs.data_ptr(), Wt1.data_ptr(), hsum.data_ptr(), ws, wsb, _stream())
+        return hsum
+
+    def target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False):
+        GzT = self.empty(2 * d.F, d.NS)
+        gxe = self.empty(d.F, d.E) if want_gxe else None
+        g_hsum = g_hsum.contiguous()
+        ws, wsb = self._wsargs(d)
+        _call("pfsgnn_target_bwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
+              Rs.data_ptr(), Wt1.data_ptr(), g_hsum.data_ptr(), GzT.data_ptr(), dWt1.data_ptr(),
+              _ptr(gxe), ws, wsb, _stream())
+        return GzT, gxe
+
+    def source_bwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next, bnstat,
+                   dWs1, dWs2, dbs2):
+        g_tot = self.empty(d.F, d.E)
+        GzS = self.empty(2 * d.F, d.NT)
+        Rs = Wt1 = g_hsum = None
+        if tpart is not None:
+            Rs, Wt1, g_hsum = tpart
+            g_hsum = g_hsum.contiguous()
+        mu1 = inv1 = Sg = Sgx = None
+        if bnstat is not None:
+            mu1, inv1 = bnstat
+            Sg, Sgx = self.empty(d.F), self.empty(d.F)
+        mean = mean.contiguous()
+        if g_next is not None:
+            g_next = g_next.contiguous()
+        ws, wsb = self._wsargs(d)
+        _call("pfsgnn_source_bwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
+              Qt.data_ptr(), Ws1.data_ptr(), Ws2.data_ptr(), bs2.data_ptr(), mean.data_ptr(),
+              coef.data_ptr(), _ptr(Rs), _ptr(Wt1), _ptr(g_hsum), _ptr(g_next), _ptr(mu1),
+              _ptr(inv1), g_tot.data_ptr(), GzS.data_ptr(), dWs1.data_ptr(), dWs2.data_ptr(),
+              dbs2.data_ptr(), _ptr(Sg), _ptr(Sgx), ws, wsb, _stream())
+        return g_tot, GzS, Sg, Sgx
+
+    def edge_bn_grad_sums(self, d, g, y, mu1, inv1):
+        Sg, Sgx = self.empty(d.F), self.empty(d.F)
+        ws, wsb = self._wsargs(d)
+        _call("pfsgnn_edge_bn_grad_sums", d.G, d.NF, d.NC, d.F, g.data_ptr(), y.data_ptr(),
+              mu1.data_ptr(), inv1.data_ptr(), Sg.data_ptr(), Sgx.data_ptr(), ws, wsb, _stream())
+        return Sg, Sgx
+
+    def edge_mlp_bwd(self, d, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1, W2,
+                     dW1, dW2, db2, want_gxe=True):
+        gxe = self.empty(d.F, d.E) if want_gxe else None
+        GzEs, GzEt = self.empty(4 * d.F, d.NS), self.empty(4 * d.F, d.NT)
+        ws, wsb = self._wsargs(d)
+        _call("pfsgnn_edge_mlp_bwd", d.G, d.NF, d.NC, d.F, g_tot.data_ptr(), alpha.data_ptr(),
+              gam0.data_ptr(), gam1.data_ptr(), y.data_ptr(), xe.data_ptr(), _ptr(xsc), _ptr(xsh),
+              Ps.data_ptr(), Pt.data_ptr(), W1.data_ptr(), W2.data_ptr(), dW1.data_ptr(),
+              dW2.data_ptr(), db2.data_ptr(), _ptr(gxe), GzEs.data_ptr(), GzEt.data_ptr(), ws, wsb,
+              _stream())
+        return gxe, GzEs, GzEt
+
+    def edge_apply(self, d, y, sc, sh):
+        out = self.empty(d.F, d.E)
+        _call("pfsgnn_edges_from_canonical", y.data_ptr(), _ptr(sc), _ptr(sh), d.E, d.F, None, 0,
+              out.data_ptr(), _stream())
+        return out
+
+    # ------------------------------------------------------------ loss
+    def loss_fwd(self, d, y, sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sharpness, noiselevel, seed,
+                 want_time=False):
+        n_prime, fiber_time = self.empty(d.NT), self.empty(d.NS)
+        tmean, tvar = self.empty(d.NT), self.empty(d.NT)
+        tt = self.empty(d.E) if want_time else None
+        ci = ci.contiguous()
+        ws, wsb = self._wsargs(d)
+        _call("pfsgnn_loss_fwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
+              Wd1.data_ptr(), bd1.data_ptr(), Wd2.data_ptr(), bd2.data_ptr(), ci.data_ptr(),
+              float(scale), float(sharpness), float(noiselevel), int(seed) & ((1 << 64) - 1),
+              n_prime.data_ptr(), fiber_time.data_ptr(), tmean.data_ptr(), tvar.data_ptr(),
+              _ptr(tt), ws, wsb, _stream())
+        return n_prime, fiber_time, tmean, tvar, tt
+
+    def loss_finalize(self, d, n_prime, fiber_time, tvar, ci, pclass, pfiber, total_time, nfields,
+                      wutils, wvar, gscale=1.0):
+        loss, utils, variance = self.empty(d.G), self.empty(d.G), self.empty(d.G)
+        Gn, Gf, Gv = self.empty(d.NT), self.empty(d.NS), self.empty(d.NT)
+        ci = ci.contiguous()
+        _call("pfsgnn_loss_finalize", d.G, d.NF, d.NC, n_prime.data_ptr(), fiber_time.data_ptr(),
+              tvar.data_ptr(), ci.data_ptr(), float(pclass), float(pfiber), float(total_time),
+              float(nfields), float(wutils), float(wvar), loss.data_ptr(), utils.data_ptr(),
+              variance.data_ptr(), Gn.data_ptr(), Gf.data_ptr(), Gv.data_ptr(), _stream())
+        return loss, utils, variance, Gn, Gf, Gv
+
+    def loss_bwd(self, d, y, sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sharpness, noiselevel, seed,
+                 Gn, Gf, Gv, tmean, gscale, dWd1, dbd1, dWd2, dbd2):
+        gxe = self.empty(d.F, d.E)
+        gs = None
+        if isinstance(gscale, torch.Tensor):
+            gs = gscale.reshape(1).to(torch.float32).contiguous()
+        elif gscale != 1.0:
+            gs = torch.full((1,), float(gscale), dtype=torch.float32, device=self.device)
+        ci = ci.contiguous()
+        ws, wsb = self._wsargs(d)
+        _call("pfsgnn_loss_bwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
+              Wd1.data_ptr(), bd1.data_ptr(), Wd2.data_ptr(), bd2.data_ptr(), ci.data_ptr(),
+              float(scale), float(sharpness), float(noiselevel), int(seed) & ((1 << 64) - 1),
+              Gn.data_ptr(), Gf.data_ptr(), Gv.data_ptr(), tmean.data_ptr(), _ptr(gs),
+              dWd1.data_ptr(), dbd1.data_ptr(), dWd2.data_ptr(), dbd2.data_ptr(), gxe.data_ptr(),
+              ws, wsb, _stream())
+        return gxe
+
+    # ------------------------------------------------------------ layout / optim
+    def layout_analyze(self, edge_index, G, NF, NC):
+        E = edge_index.shape[1]
+        ei = edge_index.to(device=self.device, dtype=torch.int64).contiguous()
+        perm = torch.empty(E, dtype=torch.int32, device=self.device)
+        status = torch.empty(2, dtype=torch.int32, device=self.device)
+        ws = torch.empty(max(4 * E, 256), dtype=torch.uint8, device=self.device)
+        _call("pfsgnn_layout_analyze", ei.data_ptr(), E, G, NF, NC, perm.data_ptr(),
+              status.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+        st = status.cpu().tolist()
+        return perm, bool(st[0]), bool(st[1])
+
+    def edges_to_canonical(self, x, perm=None):
+        E, F = x.shape
+        x = x.to(device=self.device, dtype=torch.float32).contiguous()
+        out = self.empty(F, E)
+        _call("pfsgnn_edges_to_canonical", x.data_ptr(), E, F, _ptr(perm), out.data_ptr(),
+              _stream())
+        return out
+
+    def edges_from_canonical(self, y, sc, sh, perm=None, rowmajor=True):
+        F, E = y.shape
+        out = self.empty(E, F) if rowmajor else self.empty(F, E)
+        _call("pfsgnn_edges_from_canonical", y.data_ptr(), _ptr(sc), _ptr(sh), E, F, _ptr(perm),
+              int(rowmajor), out.data_ptr(), _stream())
+        return out
+
+    def adam(self, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay):
+        self._chk(p, g, m, v)
+        _call("pfsgnn_adam", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
+              int(step), float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
+              _stream())

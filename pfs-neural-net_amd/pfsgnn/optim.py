@@ -1,0 +1,101 @@
+"""FusedAdam: ``torch.optim.Adam`` (train.py:111) as one HIP kernel launch.
+
+Same hyper-parameters, update rule (torch/optim/adam.py, amsgrad=False,
+maximize=False: exp_avg.lerp_, exp_avg_sq.mul_.addcmul_, bias-corrected
+denominator, addcdiv_) and state_dict format as ``torch.optim.Adam``, so a
+reference checkpoint's ``optim_state`` loads into it.  When the parameters
+are views of one flat buffer (``pfsgnn.GNN`` keeps them so) the whole step is
+a single ``pfsgnn_adam`` launch over that buffer.
+"""
+import torch
+
+from .gnn import backend
+
+
+def _flat_base(tensors):
+    """If `tensors` are views laid out in one storage (possibly with gaps),
+    return (base_1d_tensor, [offsets]) covering them; else None."""
+    if not tensors:
+        return None
+    st = tensors[0].untyped_storage()
+    if any(t.untyped_storage().data_ptr() != st.data_ptr() or not t.is_contiguous() for t in tensors):
+        return None
+    offs = [t.storage_offset() for t in tensors]
+    lo = min(offs)
+    hi = max(o + t.numel() for o, t in zip(offs, tensors))
+    base = torch.empty(0, dtype=tensors[0].dtype, device=tensors[0].device)
+    base.set_(st, lo, (hi - lo,), (1,))
+    return base, [o - lo for o in offs]
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
+                        maximize=False)
+        super().__init__(params, defaults)
+        self._flat = {}
+
+    def _group_flat(self, gi, group):
+        ps = group["params"]
+        pb = _flat_base([p.detach() for p in ps])
+        gb = _flat_base([p.grad for p in ps]) if all(p.grad is not None for p in ps) else None
+        if pb is None or gb is None or pb[1] != gb[1] or pb[0].numel() != gb[0].numel():
+            return None
+        cache = self._flat.get(gi)
+        if cache is None or cache[0].numel() != pb[0].numel():
+            m = torch.zeros_like(pb[0])
+            v = torch.zeros_like(pb[0])
+            for p, off in zip(ps, pb[1]):
+                st = self.state.get(p)
+                if st and "exp_avg" in st:
+                    m[off:off + p.numel()].copy_(st["exp_avg"].reshape(-1))
+                    v[off:off + p.numel()].copy_(st["exp_avg_sq"].reshape(-1))
+            step = 0
+            for p in ps:
+                st = self.state.get(p)
+                if st and "step" in st:
+                    step = int(st["step"])
+            for p, off in zip(ps, pb[1]):
+                self.state[p] = {"step": torch.tensor(float(step)),
+                                 "exp_avg": m[off:off + p.numel()].view(p.shape),
+                                 "exp_avg_sq": v[off:off + p.numel()].view(p.shape)}
+            cache = (m, v)
+            self._flat[gi] = cache
+        return pb[0], gb[0], cache[0], cache[1]
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        be = backend()
+        for gi, group in enumerate(self.param_groups):
+            beta1, beta2 = group["betas"]
+            flat = self._group_flat(gi, group)
+            if flat is not None:
+                p, g, m, v = flat
+                st0 = self.state[group["params"][0]]
+                step = int(st0["step"]) + 1
+                be.adam(p, g, m, v, step, group["lr"], beta1, beta2, group["eps"],
+                        group["weight_decay"])
+                for q in group["params"]:
+                    self.state[q]["step"].fill_(float(step))
+                continue
+            for q in group["params"]:
+                if q.grad is None:
+                    continue
+                st = self.state[q]
+                if "exp_avg" not in st:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(q)
+                    st["exp_avg_sq"] = torch.zeros_like(q)
+                step = int(st["step"]) + 1
+                st["step"].fill_(float(step))
+                be.adam(q.detach(), q.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], step,
+                        group["lr"], beta1, beta2, group["eps"], group["weight_decay"])
+        return loss
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._flat = {}   # re-flattened (copying the loaded moments) at the next step

@@ -1,0 +1,167 @@
+"""Drop-in for the reference ``src/train.py`` objective and training loop.
+
+``loss_function`` (train.py:29-80) runs fused over the edges in
+``libpfsgnn.so``: decoder_e (gnn.py:307) + softplus + ``softfloor``
+(train.py:21) + the per-class / per-fiber scatters + penalties, with the
+backward as one more fused pass that hands the last message-passing block
+its edge gradient.  The loss reads the GNN's lazy final edge state directly
+(``graph._pf``), so the normalised edge features are never re-read.
+
+softfloor's noise: the reference draws ``torch.rand_like`` (train.py:22);
+here the uniforms come from a counter-based hash of (seed, edge id) computed
+in-kernel (``pfsgnn_common.h: pf_uniform``), with the per-call seed drawn from
+torch's global CPU generator -- so ``torch.manual_seed`` governs it as it
+governs the reference, a step is reproducible, and no RNG state lives on the
+device.
+"""
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+
+from . import config
+from .engine import Dims
+from .gnn import GNN, BipartiteData, backend, grad_edges_out
+
+_SEED_SPACE = (1 << 62)
+
+
+def draw_seed():
+    return int(torch.randint(0, _SEED_SPACE, (1,)).item())
+
+
+def softfloor(x, sharpness=20, noiselevel=0.3):
+    """train.py:21-27 on an arbitrary tensor (utility; the training objective
+    uses the fused in-kernel version).  Elementwise torch on the device."""
+    noise = noiselevel * (torch.rand_like(x) - 0.5)
+    x = x + noise
+    sharpness = x.new_tensor(sharpness)
+    pi = x.new_tensor(np.pi)
+    r = torch.where(sharpness == 0, torch.tensor(0.0, device=x.device), torch.exp(-1 / sharpness))
+    return x + 1 / pi * (torch.arctan(r * torch.sin(2 * pi * x) / (1 - r * torch.cos(2 * pi * x)))
+                         - torch.arctan(r / (torch.ones_like(r) - r)))
+
+
+class _LossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_e, anchor, model, d, perm, xe3, ci, sharpness, seed, pclass, pfiber,
+                want_time):
+        eng = model._engine()
+        P = model._flat_params()
+        loss, diag, lctx = eng.loss_forward(P, d, xe3, ci, sharpness, seed, pclass=pclass,
+                                            pfiber=pfiber, total_time=float(config.TOTAL_TIME),
+                                            nfields=float(config.NFIELDS), wutils=config.wutils,
+                                            wvar=config.wvar, want_time=want_time)
+        ctx.pf = (model, d, perm, lctx)
+        outs = (diag["utils"], diag["n_prime"], diag["fiber_time"], diag["variance"])
+        ctx.mark_non_differentiable(*outs)
+        if diag["time"] is not None:
+            ctx.mark_non_differentiable(diag["time"])
+        return (loss,) + outs + ((diag["time"],) if diag["time"] is not None else ())
+
+    @staticmethod
+    def backward(ctx, g_loss, *unused):
+        model, d, perm, lctx = ctx.pf
+        eng = model._engine()
+        P, Gr = model._flat_params(), model._flat_grads()
+        gc = eng.loss_backward(P, Gr, lctx, gscale=g_loss)
+        return (grad_edges_out(gc, perm),) + (None,) * 11
+
+
+def _class_info_cm(class_info, d):
+    ci = class_info.to(device=config.device, dtype=torch.float32)
+    if ci.dim() != 2 or ci.size(0) != d.NT or ci.size(1) < 2:
+        raise ValueError(f"class_info must be [G*NC, >=2] = [{d.NT}, >=2]; got {tuple(ci.shape)}")
+    return ci[:, :2].t().contiguous()
+
+
+def loss_function(graph, class_info, pclass=0.1, pfiber=1.0, sharpness=0.5, finaloutput=False,
+                  *, gnn=None, seed=None):
+    """train.py:29-80.  ``graph`` is the output of ``GNN.forward``; ``class_info``
+    is [NC, 2] (T_i, N_i) per class -- [G*NC, 2] for a batch of G graphs, whose
+    loss is the sum of the per-graph losses.  The reference reads the model
+    from a global ``gnn`` (train.py:42); here it comes with the graph (or
+    ``gnn=``).  Edge order must be the fiber-major layout train.py builds
+    (train.py:94), on which train.py:40 and :67 rely."""
+    pf = getattr(graph, "_pf", None)
+    if pf is None or pf[3] is not graph.x_e:
+        raise NotImplementedError("loss_function needs the BipartiteData returned by "
+                                  "pfsgnn.GNN.forward (the fused loss reads its edge state)")
+    model, d, perm, x_e, xe3 = pf
+    if gnn is not None and gnn is not model:
+        raise ValueError("graph was produced by a different GNN than `gnn`")
+    if perm is not None:
+        raise NotImplementedError("train.py's objective indexes edges by position "
+                                  "(train.py:40, :67): it needs the fiber-major edge order")
+    ci = _class_info_cm(class_info, d)
+    if seed is None:
+        seed = draw_seed()
+    outs = _LossFn.apply(x_e, model.encoder_s[0].weight, model, d, perm, xe3, ci, float(sharpness),
+                         int(seed), float(pclass), float(pfiber), bool(finaloutput))
+    loss, utils_g, n_prime, fiber_time, variance = outs[:5]
+    if not finaloutput:
+        return loss, utils_g.sum() if d.G > 1 else utils_g[0]
+    time = outs[5]
+    Ni = ci[1] / config.NFIELDS
+    comp = (n_prime / Ni).detach().cpu().numpy()
+    fibers = fiber_time.detach().cpu().numpy()
+    utils = utils_g.sum() if d.G > 1 else utils_g[0]
+    var = variance.sum() if d.G > 1 else variance[0]
+    return loss, utils, comp, n_prime, fibers, time, var
+
+
+# ---------------------------------------------------------------- training
+def complete_graph(class_info, nfibers, fdim, lo=2.0, hi=10.0):
+    """train.py:88-104: fiber counter x_s, class_info x_t, fiber-major complete
+    edges, x_e ~ U[lo, hi), u = 0."""
+    class_info = torch.as_tensor(class_info, dtype=torch.float, device=config.device)
+    nclasses = class_info.shape[0]
+    x_s = torch.arange(nfibers, dtype=torch.float, device=config.device).reshape(-1, 1)
+    edge_index = torch.cartesian_prod(torch.arange(nfibers), torch.arange(nclasses)).to(config.device).T
+    x_e = lo + (hi - lo) * torch.rand(size=(nfibers * nclasses, fdim)).to(config.device)
+    x_u = torch.zeros(1, fdim).to(config.device)
+    return BipartiteData(edge_index=edge_index, x_s=x_s, x_t=class_info, x_e=x_e, x_u=x_u)
+
+
+def main(argv=None):
+    """train.py:82-165 (training + checkpointing; the plotting of train.py:168-305
+    is not part of the hot path and is skipped)."""
+    from .optim import FusedAdam
+    argv = sys.argv[1:] if argv is None else argv
+    idx = int(os.environ.get("SLURM_ARRAY_TASK_ID", 0))
+    ID = str(idx)
+    class_info = torch.tensor(np.loadtxt(config.datafile), dtype=torch.float, device=config.device)
+    NF, NC = config.NFIBERS, class_info.shape[0]
+    graph = complete_graph(class_info, NF, config.Fdim)
+    gnn = GNN(Fdim=config.Fdim, B=3, F_s=1, F_t=class_info.shape[1], T=NC).to(config.device)
+    gnn.train()
+    optimizer = FusedAdam(gnn.parameters(), lr=config.lr)
+    nepochs = config.nepochs
+    start_epoch = 0
+    if argv:
+        ck = torch.load(argv[0], map_location=config.device, weights_only=True)
+        gnn.load_state_dict(ck["model_state"])
+        optimizer.load_state_dict(ck["optim_state"])
+        start_epoch = ck["epoch"] + 1
+    best_utility = 0.0
+    for epoch in range(start_epoch, nepochs):
+        gnn.zero_grad()
+        graph_ = gnn(graph)
+        sharp = config.sharps[0] + (config.sharps[1] - config.sharps[0]) * epoch / nepochs
+        loss, utility, comp, _, fiber_time, time, variance = loss_function(
+            graph_, class_info, pclass=config.pclass, pfiber=config.pfiber, sharpness=sharp,
+            finaloutput=True)
+        loss.backward()
+        optimizer.step()
+        if float(utility) > best_utility and sharp > config.min_sharp:
+            best_utility = float(utility)
+            torch.save({"epoch": epoch, "model_state": gnn.state_dict(),
+                        "optim_state": optimizer.state_dict()}, config.checkpoint_path + ID + ".pth")
+    torch.save({"epoch": nepochs, "model_state": gnn.state_dict(),
+                "optim_state": optimizer.state_dict()}, config.checkpoint_path + ID + ".pth")
+
+
+if __name__ == "__main__":
+    main()

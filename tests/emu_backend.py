@@ -1,0 +1,400 @@
+"""Torch-CPU emulation of the pfsgnn op set (TEST INFRASTRUCTURE ONLY).
+
+The product engine (``pfsgnn/engine.py``) orchestrates a small set of ops that
+the HIP library (``libpfsgnn.so``) implements as kernels.  This module
+implements the *same* ops, with the same arguments and layouts, in plain
+torch so that the orchestration (and every hand-derived backward formula in
+it) can be checked against the autograd oracle on the CPU, in float64, with
+no GPU.  It is never imported by product code and is not a fallback: the
+product backend is chosen explicitly and only ``HipBackend`` exists there.
+
+Layouts (see DESIGN.md §Data layout):
+* node tensors are channel-major ``[C, N]``;
+* edge tensors are channel-major ``[C, E]`` in the canonical fiber-major
+  order ``e = (g*NF + f)*NC + c``;
+* weights are torch ``Linear`` matrices ``[out, in]``; an op that uses a
+  column block of a weight takes ``(W, col0, ncol)``.
+"""
+import math
+
+import torch
+
+SLOPE = 0.1
+
+
+def lrelu(x, s=SLOPE):
+    return torch.where(x > 0, x, x * s)
+
+
+def dlrelu(z, s=SLOPE):
+    return torch.where(z > 0, torch.ones_like(z), torch.full_like(z, s))
+
+
+class Dims:
+    def __init__(self, G, NF, NC, F):
+        self.G, self.NF, self.NC, self.F = G, NF, NC, F
+        self.E = G * NF * NC
+        self.NS = G * NF
+        self.NT = G * NC
+
+
+def _edge_index(d, device):
+    e = torch.arange(d.E, device=device)
+    fib = e // d.NC
+    cls = (e // (d.NF * d.NC)) * d.NC + e % d.NC
+    return fib, cls
+
+
+def _aff(x, sc, sh):
+    if sc is None:
+        return x
+    return x * sc[:, None] + sh[:, None]
+
+
+class EmuBackend:
+    name = "emu"
+
+    def __init__(self, dtype=torch.float64):
+        self.dtype = dtype
+        self.device = torch.device("cpu")
+
+    def empty(self, *shape):
+        return torch.empty(*shape, dtype=self.dtype)
+
+    def zeros(self, *shape):
+        return torch.zeros(*shape, dtype=self.dtype)
+
+    def ones(self, *shape):
+        return torch.ones(*shape, dtype=self.dtype)
+
+    # ------------------------------------------------------------ node ops
+    def lin(self, W, col0, ncol, X, b=None, act_in=False, out=None, add=False, bscale=1.0):
+        Xa = lrelu(X) if act_in else X
+        Y = W[:, col0:col0 + ncol] @ Xa
+        if b is not None:
+            Y = Y + bscale * b[:, None]
+        if out is None:
+            return Y
+        if add:
+            out += Y
+        else:
+            out.copy_(Y)
+        return out
+
+    def lin_t(self, W, col0, ncol, dY, z=None, out=None, add=False):
+        R = W[:, col0:col0 + ncol].t() @ dY
+        if z is not None:
+            R = R * dlrelu(z)
+        if out is None:
+            return R
+        if add:
+            out += R
+        else:
+            out.copy_(R)
+        return out
+
+    def wgrad(self, dY, X, dW, col0=0, db=None, act_in=False, dbscale=1.0):
+        Xa = lrelu(X) if act_in else X
+        dW[:, col0:col0 + X.shape[0]] += dY @ Xa.t()
+        if db is not None:
+            db += dbscale * dY.sum(1)
+
+    def bn_fwd(self, X, gamma, beta, rm, rv, momentum, eps):
+        n = X.shape[1]
+        mu = X.mean(1)
+        var = ((X - mu[:, None]) ** 2).mean(1)
+        Y = (X - mu[:, None]) / torch.sqrt(var[:, None] + eps) * gamma[:, None] + beta[:, None]
+        if rm is not None:
+            rm.mul_(1 - momentum).add_(momentum * mu.to(rm.dtype))
+            rv.mul_(1 - momentum).add_(momentum * (var * n / max(n - 1, 1)).to(rv.dtype))
+        return Y, mu, var
+
+    def bn_bwd(self, dY, X, mu, var, gamma, eps, dgamma, dbeta):
+        inv = 1.0 / torch.sqrt(var + eps)
+        xh = (X - mu[:, None]) * inv[:, None]
+        Sg = dY.sum(1)
+        Sgx = (dY * xh).sum(1)
+        n = X.shape[1]
+        dgamma += Sgx
+        dbeta += Sg
+        return (gamma * inv)[:, None] * (dY - Sg[:, None] / n - xh * (Sgx / n)[:, None])
+
+    def graph_reduce(self, X, G, mean=False):
+        C, N = X.shape
+        R = X.reshape(C, G, N // G).sum(2)
+        return R / (N // G) if mean else R
+
+    def graph_bcast_add(self, out, src, scale=1.0):
+        C, N = out.shape
+        G = src.shape[1]
+        out += (src * scale).repeat_interleave(N // G, dim=1)
+        return out
+
+    def rms2_fwd(self, X, w, eps):
+        def one(x):
+            r = torch.rsqrt((x * x).mean(0, keepdim=True) + eps)
+            return x * r * w[:, None], r
+        Y1, r1 = one(X)
+        Y2, r2 = one(Y1)
+        return Y2, (Y1, r1, r2)
+
+    def rms2_bwd(self, dY, X, w, saved, eps, dw):
+        Y1, r1, r2 = saved
+
+        def back(dy, x, r):
+            # y = x * r * w,  r = (mean(x^2)+eps)^-1/2
+            dw.add_((dy * x * r).sum(1))
+            dxn = dy * w[:, None]
+            C = x.shape[0]
+            return r * dxn - x * (r ** 3) * (dxn * x).sum(0, keepdim=True) / C
+
+        d1 = back(dY, Y1, r2)
+        return back(d1, X, r1)
+
+    def bn2_finalize(self, mu1, var1, gamma, beta, rm, rv, n, momentum, eps):
+        """EdgeModel's BatchNorm applied twice (gnn.py:101 -- ``super().forward``
+        already runs ``self.norm`` as the Sequential's last child).  The second
+        application sees mean == beta and var == gamma^2 var1/(var1+eps), so
+        xe_new = sc*y + sh.  Updates the running stats twice, as the reference's
+        two calls do (checkpoint: num_batches_tracked == 2 x epochs)."""
+        inv1 = 1.0 / torch.sqrt(var1 + eps)
+        rho = var1 * inv1 * inv1
+        var2 = gamma * gamma * rho
+        inv2 = 1.0 / torch.sqrt(var2 + eps)
+        sc = gamma * gamma * inv1 * inv2
+        sh = beta - mu1 * sc
+        if rm is not None:
+            f = n / max(n - 1, 1)
+            rm.mul_(1 - momentum).add_(momentum * mu1.to(rm.dtype))
+            rv.mul_(1 - momentum).add_(momentum * (var1 * f).to(rv.dtype))
+            rm.mul_(1 - momentum).add_(momentum * beta.to(rm.dtype))
+            rv.mul_(1 - momentum).add_(momentum * (var2 * f).to(rv.dtype))
+        return sc, sh, inv1, inv2
+
+    def bn2_bwd_coef(self, Sg, Sgx, mu1, var1, gamma, n, eps, dgamma, dbeta):
+        """Backward of the double BatchNorm as g_y = alpha*g + gam0 + gam1*y."""
+        inv1 = 1.0 / torch.sqrt(var1 + eps)
+        rho = var1 * inv1 * inv1
+        inv2 = 1.0 / torch.sqrt(gamma * gamma * rho + eps)
+        k = gamma * inv2
+        M = Sgx / n
+        alpha = gamma * inv1 * k
+        gam1 = -alpha * M * (k * k + 1 - k * k * rho) * inv1
+        gam0 = -alpha * Sg / n - gam1 * mu1
+        dgamma += k * Sgx * (2 - k * k * rho)
+        dbeta += Sg
+        return alpha, gam0, gam1
+
+    def moment_coef(self, mom, gst, n):
+        """SModel moment backward (gnn.py:140-153) as per-fiber coefficients of
+        g_m = C0 + d*(C1 + d*(C2 + d*C3)), d = m - mean.  gst = d(loss)/d
+        [mean; std; skew; kurt] ([8F, NS])."""
+        mean, c2, c3, c4 = mom
+        C = mean.shape[0]
+        gmean, gstd, gskew, gkurt = gst[0:C], gst[C:2 * C], gst[2 * C:3 * C], gst[3 * C:4 * C]
+        var = torch.where(c2 > 0, c2, 0.01 * c2)
+        std = torch.sqrt(var + 1e-6)
+        A3 = gskew / std ** 3
+        A4 = gkurt / std ** 4
+        gstd_tot = gstd - 3 * gskew * c3 / std ** 4 - 4 * gkurt * c4 / std ** 5
+        gvr = gstd_tot / (2 * std) * torch.where(c2 > 0, torch.ones_like(c2), torch.full_like(c2, 0.01))
+        return torch.stack([(gmean - 3 * c2 * A3 - 4 * c3 * A4) / n, 2 * gvr / n, 3 * A3 / n, 4 * A4 / n])
+
+    # ------------------------------------------------------------ edge ops
+    def edge_mlp_fwd(self, d, xe, xsc, xsh, Ps, Pt, W1, W2, b2):
+        fib, cls = _edge_index(d, xe.device)
+        F = d.F
+        x = _aff(xe, xsc, xsh)
+        z1 = Ps[:, fib] + Pt[:, cls] + W1[:, 2 * F:3 * F] @ x
+        y = W2 @ lrelu(z1) + b2[:, None]
+        mu = y.mean(1)
+        var = ((y - mu[:, None]) ** 2).mean(1)
+        return y, mu, var
+
+    def source_fwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, hs_out):
+        """Per-fiber centred moments of the SModel message (gnn.py:136-151).
+        Returns mom [4, 2F, NS] = (mean, c2, c3, c4); writes the MLP inputs
+        (mean, std, skew, kurt) into hs_out [8F, NS]."""
+        fib, cls = _edge_index(d, y.device)
+        F = d.F
+        x = _aff(y, sc, sh)
+        zs = Qt[:, cls] + Ws1[:, F:2 * F] @ x
+        m = Ws2 @ lrelu(zs) + bs2[:, None]
+        C = 2 * F
+        mm = m.reshape(C, d.NS, d.NC)
+        mean = mm.mean(2)
+        dd = mm - mean[:, :, None]
+        c2 = (dd ** 2).mean(2)
+        c3 = (dd ** 3).mean(2)
+        c4 = (dd ** 4).mean(2)
+        var = torch.where(c2 > 0, c2, 0.01 * c2)
+        std = torch.sqrt(var + 1e-6)
+        hs_out[0:C] = mean
+        hs_out[C:2 * C] = std
+        hs_out[2 * C:3 * C] = c3 / std ** 3
+        hs_out[3 * C:4 * C] = c4 / std ** 4
+        return torch.stack([mean, c2, c3, c4])
+
+    def target_fwd(self, d, y, sc, sh, Rs, Wt1):
+        fib, cls = _edge_index(d, y.device)
+        F = d.F
+        x = _aff(y, sc, sh)
+        zt = Rs[:, fib] + Wt1[:, F:2 * F] @ x
+        at = lrelu(zt)
+        C = 2 * F
+        return at.reshape(C, d.G, d.NF, d.NC).sum(2).reshape(C, d.NT)
+
+    def target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False):
+        fib, cls = _edge_index(d, y.device)
+        F = d.F
+        x = _aff(y, sc, sh)
+        zt = Rs[:, fib] + Wt1[:, F:2 * F] @ x
+        gz = g_hsum[:, cls] * dlrelu(zt)
+        GzT = gz.reshape(2 * F, d.NS, d.NC).sum(2)
+        dWt1[:, F:2 * F] += gz @ x.t()
+        gxe = Wt1[:, F:2 * F].t() @ gz if want_gxe else None
+        return GzT, gxe
+
+    def source_bwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next,
+                   bnstat, dWs1, dWs2, dbs2):
+        """Returns (g_tot [F,E], GzS [2F, NT], Sg, Sgx).  ``coef`` = [4, 2F, NS]
+        (C0..C3 of g_m = C0 + d*(C1 + d*(C2 + d*C3)), d = m - mean)."""
+        fib, cls = _edge_index(d, y.device)
+        F = d.F
+        x = _aff(y, sc, sh)
+        zs = Qt[:, cls] + Ws1[:, F:2 * F] @ x
+        a = lrelu(zs)
+        m = Ws2 @ a + bs2[:, None]
+        dd = m - mean[:, fib]
+        gm = coef[0][:, fib] + dd * (coef[1][:, fib] + dd * (coef[2][:, fib] + dd * coef[3][:, fib]))
+        dWs2 += gm @ a.t()
+        dbs2 += gm.sum(1)
+        gz = (Ws2.t() @ gm) * dlrelu(zs)
+        dWs1[:, F:2 * F] += gz @ x.t()
+        g = Ws1[:, F:2 * F].t() @ gz
+        GzS = gz.reshape(2 * F, d.G, d.NF, d.NC).sum(2).reshape(2 * F, d.NT)
+        if tpart is not None:
+            Rs, Wt1, g_hsum = tpart
+            zt = Rs[:, fib] + Wt1[:, F:2 * F] @ x
+            gzt = g_hsum[:, cls] * dlrelu(zt)
+            g = g + Wt1[:, F:2 * F].t() @ gzt
+        if g_next is not None:
+            g = g + g_next
+        Sg = Sgx = None
+        if bnstat is not None:
+            mu1, inv1 = bnstat
+            xh = (y - mu1[:, None]) * inv1[:, None]
+            Sg = g.sum(1)
+            Sgx = (g * xh).sum(1)
+        return g, GzS, Sg, Sgx
+
+    def edge_bn_grad_sums(self, d, g, y, mu1, inv1):
+        xh = (y - mu1[:, None]) * inv1[:, None]
+        return g.sum(1), (g * xh).sum(1)
+
+    def edge_mlp_bwd(self, d, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1, W2,
+                     dW1, dW2, db2, want_gxe=True):
+        fib, cls = _edge_index(d, y.device)
+        F = d.F
+        gy = alpha[:, None] * g_tot + gam0[:, None] + gam1[:, None] * y
+        x = _aff(xe, xsc, xsh)
+        z1 = Ps[:, fib] + Pt[:, cls] + W1[:, 2 * F:3 * F] @ x
+        a1 = lrelu(z1)
+        dW2 += gy @ a1.t()
+        db2 += gy.sum(1)
+        gz = (W2.t() @ gy) * dlrelu(z1)
+        dW1[:, 2 * F:3 * F] += gz @ x.t()
+        GzEs = gz.reshape(4 * F, d.NS, d.NC).sum(2)
+        GzEt = gz.reshape(4 * F, d.G, d.NF, d.NC).sum(2).reshape(4 * F, d.NT)
+        gxe = W1[:, 2 * F:3 * F].t() @ gz if want_gxe else None
+        return gxe, GzEs, GzEt
+
+    def edge_apply(self, d, y, sc, sh):
+        return _aff(y, sc, sh).clone()
+
+    # ------------------------------------------------------------ loss ops
+    def loss_fwd(self, d, y, sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sharpness, noiselevel, seed,
+                 want_time=False):
+        """train.py:42-49 per edge, reduced per class / fiber.  ``uni`` [E] are the
+        uniforms of softfloor's noise.  Returns n_prime [NT], fiber_time [NS],
+        tt_mean [NT], tt_var [NT] (unbiased over fibers), tt [E]."""
+        fib, cls = _edge_index(d, y.device)
+        uni = self.noise_uniform(seed, d.E)
+        x = _aff(y, sc, sh)
+        zd = Wd1 @ x + bd1[:, None]
+        pred = (Wd2 @ lrelu(zd) + bd2[:, None])[0]
+        time = torch.nn.functional.softplus(pred) * scale
+        Ti = ci[0][cls]
+        v = time / Ti + noiselevel * (uni - 0.5)
+        r = 0.0 if sharpness == 0 else math.exp(-1.0 / sharpness)
+        th = 2 * math.pi * v
+        gal = v + (torch.atan(r * torch.sin(th) / (1 - r * torch.cos(th))) - math.atan(r / (1 - r))) / math.pi
+        gal = torch.clamp(gal, min=0.0)
+        tt = gal * Ti
+        n_prime = gal.reshape(d.G, d.NF, d.NC).sum(1).reshape(d.NT)
+        fiber_time = tt.reshape(d.NS, d.NC).sum(1)
+        T3 = tt.reshape(d.G, d.NF, d.NC)
+        tmean = T3.mean(1)
+        tvar = ((T3 - tmean[:, None, :]) ** 2).sum(1) / (d.NF - 1)
+        return n_prime, fiber_time, tmean.reshape(d.NT), tvar.reshape(d.NT), (tt if want_time else None)
+
+    def loss_bwd(self, d, y, sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sharpness, noiselevel, seed,
+                 Gn, Gf, Gv, tmean, gscale, dWd1, dbd1, dWd2, dbd2):
+        fib, cls = _edge_index(d, y.device)
+        uni = self.noise_uniform(seed, d.E)
+        Gn, Gf, Gv = Gn * gscale, Gf * gscale, Gv * gscale
+        x = _aff(y, sc, sh)
+        zd = Wd1 @ x + bd1[:, None]
+        ad = lrelu(zd)
+        pred = (Wd2 @ ad + bd2[:, None])[0]
+        time = torch.nn.functional.softplus(pred) * scale
+        Ti = ci[0][cls]
+        v = time / Ti + noiselevel * (uni - 0.5)
+        r = 0.0 if sharpness == 0 else math.exp(-1.0 / sharpness)
+        th = 2 * math.pi * v
+        graw = v + (torch.atan(r * torch.sin(th) / (1 - r * torch.cos(th))) - math.atan(r / (1 - r))) / math.pi
+        gal = torch.clamp(graw, min=0.0)
+        tt = gal * Ti
+        g_tt = Gf[fib] + Gv[cls] * (tt - tmean[cls])
+        g_gal = Gn[cls] + Ti * g_tt
+        mask = torch.where(graw > 0, torch.ones_like(graw),
+                           torch.where(graw == 0, torch.full_like(graw, 0.5), torch.zeros_like(graw)))
+        dsf = 1 + 2 * (r * torch.cos(th) - r * r) / (1 - 2 * r * torch.cos(th) + r * r)
+        g_time = g_gal * mask * dsf / Ti
+        sig = torch.where(pred > 20, torch.ones_like(pred), torch.sigmoid(pred))
+        g_pred = g_time * scale * sig
+        dWd2 += (g_pred[None, :] @ ad.t())
+        dbd2 += g_pred.sum().reshape(1)
+        gz = (Wd2.t() @ g_pred[None, :]) * dlrelu(zd)
+        dWd1 += gz @ x.t()
+        dbd1 += gz.sum(1)
+        return Wd1.t() @ gz
+
+    def loss_finalize(self, d, n_prime, fiber_time, tvar, ci, pclass, pfiber, total_time,
+                      nfields, wutils, wvar, gscale=1.0):
+        """train.py:53-71 per graph.  Returns loss [G], utils [G], variance [G] and
+        the per-node gradient coefficients Gn [NT], Gf [NS], Gv [NT] of the loss
+        (scaled by ``gscale``)."""
+        G, NC, NF = d.G, d.NC, d.NF
+        Ni = (ci[1] / nfields).reshape(G, NC)
+        npr = n_prime.reshape(G, NC)
+        comp = npr / Ni
+        utils = comp.min(1).values
+        ties = (comp == utils[:, None]).to(comp.dtype)
+        share = ties / ties.sum(1, keepdim=True)
+        over = torch.relu(npr - Ni)
+        cpen = pclass * (over ** 2).sum(1)
+        ot = fiber_time.reshape(G, NF) - total_time
+        lk = lrelu(ot)
+        fpen = pfiber * (lk ** 2).sum(1)
+        variance = tvar.reshape(G, NC).sum(1)
+        loss = -wutils * utils + fpen + cpen - wvar * variance
+        Gn = gscale * (-wutils * share / Ni + 2 * pclass * over)
+        Gf = gscale * pfiber * 2 * lk * dlrelu(ot)
+        Gv = torch.full_like(tvar, gscale * (-wvar) * 2.0 / (NF - 1))
+        return loss, utils, variance, Gn.reshape(-1), Gf.reshape(-1), Gv
+
+    # ------------------------------------------------------------ misc
+    def noise_uniform(self, seed, E):
+        from noise_ref import uniform_numpy
+        return torch.as_tensor(uniform_numpy(seed, E), dtype=self.dtype)

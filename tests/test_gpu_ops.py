@@ -1,0 +1,249 @@
+"""Op-level parity: every HIP op of libpfsgnn.so vs the same op emulated in
+float64 torch on identical inputs (tests/emu_backend.py), at several batch
+geometries (NC below / at / above a wave, non-power-of-two NC, several graphs).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from emu_backend import EmuBackend, Dims as EDims  # noqa: E402
+
+GEOMS = [(1, 37, 12), (2, 50, 16), (1, 9, 128), (3, 21, 5), (2, 7, 200), (1, 33, 64)]
+
+
+@pytest.fixture(scope="module")
+def hb():
+    from pfsgnn.native import HipBackend
+    return HipBackend()
+
+
+def r(*shape, scale=1.0, off=0.0, gen=None):
+    return (torch.randn(*shape, generator=gen, dtype=torch.float64) * scale + off)
+
+
+def cuda(t):
+    return None if t is None else t.to(torch.float32).cuda().contiguous()
+
+
+def cpu(t):
+    return None if t is None else t.detach().double().cpu()
+
+
+def close(a, b, rtol=2e-4, atol=1e-5, name=""):
+    a, b = cpu(a), cpu(b)
+    scale = b.abs().max().item() if b.numel() else 1.0
+    err = (a - b).abs().max().item() if b.numel() else 0.0
+    assert err <= atol + rtol * max(scale, 1e-30), f"{name}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+def dims(G, NF, NC, F=10):
+    from pfsgnn.engine import Dims
+    return Dims(G, NF, NC, F), EDims(G, NF, NC, F)
+
+
+@pytest.mark.parametrize("G,NF,NC", GEOMS)
+def test_edge_ops(hb, G, NF, NC):
+    F = 10
+    gen = torch.Generator().manual_seed(G * 1000 + NF * 10 + NC)
+    emu = EmuBackend()
+    d, de = dims(G, NF, NC, F)
+    E, NS, NT = d.E, d.NS, d.NT
+    xe = r(F, E, scale=2, off=3, gen=gen)
+    xsc, xsh = r(F, gen=gen) * 0.5 + 1, r(F, gen=gen)
+    Ps, Pt = r(4 * F, NS, gen=gen), r(4 * F, NT, gen=gen)
+    W1, W2, b2 = r(4 * F, 4 * F, scale=0.3, gen=gen), r(F, 4 * F, scale=0.3, gen=gen), r(F, gen=gen)
+    # edge_mlp_fwd
+    y_h, mu_h, var_h = hb.edge_mlp_fwd(d, cuda(xe), cuda(xsc), cuda(xsh), cuda(Ps), cuda(Pt), cuda(W1), cuda(W2), cuda(b2))
+    y_e, mu_e, var_e = emu.edge_mlp_fwd(de, xe, xsc, xsh, Ps, Pt, W1, W2, b2)
+    close(y_h, y_e, name="y"); close(mu_h, mu_e, name="mu"); close(var_h, var_e, name="var")
+    y = y_e
+    sc, sh = r(F, gen=gen) * 0.3 + 1, r(F, gen=gen)
+    # source_fwd
+    Qt = r(2 * F, NT, gen=gen)
+    Ws1, Ws2, bs2 = r(2 * F, 2 * F, scale=0.3, gen=gen), r(2 * F, 2 * F, scale=0.3, gen=gen), r(2 * F, gen=gen)
+    hs_h = torch.zeros(8 * F, NS, device="cuda")
+    hs_e = torch.zeros(8 * F, NS, dtype=torch.float64)
+    mom_h = hb.source_fwd(d, cuda(y), cuda(sc), cuda(sh), cuda(Qt), cuda(Ws1), cuda(Ws2), cuda(bs2), hs_h)
+    mom_e = emu.source_fwd(de, y, sc, sh, Qt, Ws1, Ws2, bs2, hs_e)
+    for i, nm in enumerate(["mean", "c2", "c3", "c4"]):
+        close(mom_h[i], mom_e[i], rtol=1e-3, name=nm)
+    close(hs_h, hs_e, rtol=2e-3, atol=1e-3, name="hs")
+    # target_fwd / bwd
+    Rs, Wt1 = r(2 * F, NS, gen=gen), r(2 * F, 2 * F, scale=0.3, gen=gen)
+    close(hb.target_fwd(d, cuda(y), cuda(sc), cuda(sh), cuda(Rs), cuda(Wt1)),
+          emu.target_fwd(de, y, sc, sh, Rs, Wt1), name="hsum")
+    g_hsum = r(2 * F, NT, gen=gen)
+    dWt1_h = torch.zeros(2 * F, 2 * F, device="cuda")
+    dWt1_e = torch.zeros(2 * F, 2 * F, dtype=torch.float64)
+    GzT_h, gxe_h = hb.target_bwd(d, cuda(y), cuda(sc), cuda(sh), cuda(Rs), cuda(Wt1), cuda(g_hsum), dWt1_h, want_gxe=True)
+    GzT_e, gxe_e = emu.target_bwd(de, y, sc, sh, Rs, Wt1, g_hsum, dWt1_e, want_gxe=True)
+    close(GzT_h, GzT_e, name="GzT"); close(gxe_h, gxe_e, name="gxeT"); close(dWt1_h, dWt1_e, name="dWt1")
+    # source_bwd (with T part, g_next, BN sums)
+    mean = r(2 * F, NS, gen=gen)
+    coef = r(4, 2 * F, NS, gen=gen) * torch.tensor([1, 0.3, 0.1, 0.03], dtype=torch.float64)[:, None, None]
+    g_next = r(F, E, gen=gen)
+    mu1, inv1 = r(F, gen=gen), r(F, gen=gen).abs() + 0.5
+    grads_h = [torch.zeros(2 * F, 2 * F, device="cuda"), torch.zeros(2 * F, 2 * F, device="cuda"), torch.zeros(2 * F, device="cuda")]
+    grads_e = [torch.zeros(2 * F, 2 * F, dtype=torch.float64), torch.zeros(2 * F, 2 * F, dtype=torch.float64), torch.zeros(2 * F, dtype=torch.float64)]
+    out_h = hb.source_bwd(d, cuda(y), cuda(sc), cuda(sh), cuda(Qt), cuda(Ws1), cuda(Ws2), cuda(bs2), cuda(mean), cuda(coef),
+                          (cuda(Rs), cuda(Wt1), cuda(g_hsum)), cuda(g_next), (cuda(mu1), cuda(inv1)), *grads_h)
+    out_e = emu.source_bwd(de, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, (Rs, Wt1, g_hsum), g_next, (mu1, inv1), *grads_e)
+    for a, b, nm in zip(out_h, out_e, ["g_tot", "GzS", "Sg", "Sgx"]):
+        close(a, b, rtol=5e-4, name=nm)
+    for a, b, nm in zip(grads_h, grads_e, ["dWs1", "dWs2", "dbs2"]):
+        close(a, b, rtol=5e-4, name=nm)
+    # source_bwd without optional parts
+    out_h = hb.source_bwd(d, cuda(y), None, None, cuda(Qt), cuda(Ws1), cuda(Ws2), cuda(bs2), cuda(mean), cuda(coef),
+                          None, None, None, *[g.zero_() for g in grads_h])
+    out_e = emu.source_bwd(de, y, None, None, Qt, Ws1, Ws2, bs2, mean, coef, None, None, None, *[g.zero_() for g in grads_e])
+    close(out_h[0], out_e[0], rtol=5e-4, name="g_tot(bare)")
+    close(out_h[1], out_e[1], rtol=5e-4, name="GzS(bare)")
+    # edge bn sums
+    Sg_h, Sgx_h = hb.edge_bn_grad_sums(d, cuda(g_next), cuda(y), cuda(mu1), cuda(inv1))
+    Sg_e, Sgx_e = emu.edge_bn_grad_sums(de, g_next, y, mu1, inv1)
+    close(Sg_h, Sg_e, name="Sg"); close(Sgx_h, Sgx_e, name="Sgx")
+    # edge_mlp_bwd
+    alpha, gam0, gam1 = r(F, gen=gen), r(F, gen=gen) * 0.1, r(F, gen=gen) * 0.1
+    gh = [torch.zeros(4 * F, 4 * F, device="cuda"), torch.zeros(F, 4 * F, device="cuda"), torch.zeros(F, device="cuda")]
+    ge = [torch.zeros(4 * F, 4 * F, dtype=torch.float64), torch.zeros(F, 4 * F, dtype=torch.float64), torch.zeros(F, dtype=torch.float64)]
+    oh = hb.edge_mlp_bwd(d, cuda(g_next), cuda(alpha), cuda(gam0), cuda(gam1), cuda(y), cuda(xe), cuda(xsc), cuda(xsh),
+                         cuda(Ps), cuda(Pt), cuda(W1), cuda(W2), *gh, want_gxe=True)
+    oe = emu.edge_mlp_bwd(de, g_next, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1, W2, *ge, want_gxe=True)
+    for a, b, nm in zip(oh, oe, ["gxe", "GzEs", "GzEt"]):
+        close(a, b, rtol=5e-4, name=nm)
+    for a, b, nm in zip(gh, ge, ["dW1", "dW2", "db2"]):
+        close(a, b, rtol=5e-4, name=nm)
+
+
+@pytest.mark.parametrize("G,NF,NC", [(1, 37, 12), (2, 50, 16), (1, 9, 128)])
+def test_node_ops(hb, G, NF, NC):
+    gen = torch.Generator().manual_seed(7)
+    emu = EmuBackend()
+    N = G * NF
+    for (M, K) in [(10, 1), (40, 10), (100, 100), (10, 100), (3, 7)]:
+        W, X, b = r(M, K + 3, gen=gen), r(K, N, gen=gen), r(M, gen=gen)
+        close(hb.lin(cuda(W), 2, K, cuda(X), b=cuda(b), act_in=True, bscale=3.0),
+              emu.lin(W, 2, K, X, b=b, act_in=True, bscale=3.0), name=f"lin{M}x{K}")
+        dY, Z = r(M, N, gen=gen), r(K, N, gen=gen)
+        close(hb.lin_t(cuda(W), 2, K, cuda(dY), z=cuda(Z)), emu.lin_t(W, 2, K, dY, z=Z), name="lin_t")
+        dW_h, db_h = torch.zeros(M, K + 3, device="cuda"), torch.zeros(M, device="cuda")
+        dW_e, db_e = torch.zeros(M, K + 3, dtype=torch.float64), torch.zeros(M, dtype=torch.float64)
+        hb.wgrad(cuda(dY), cuda(X), dW_h, col0=2, db=db_h, act_in=True, dbscale=2.0)
+        emu.wgrad(dY, X, dW_e, col0=2, db=db_e, act_in=True, dbscale=2.0)
+        close(dW_h, dW_e, name="wgrad"); close(db_h, db_e, name="db")
+    C = 10
+    X = r(C, N, scale=3, off=5, gen=gen)
+    gamma, beta = r(C, gen=gen).abs() + 0.5, r(C, gen=gen)
+    rm_h, rv_h = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    rm_e, rv_e = torch.zeros(C, dtype=torch.float64), torch.ones(C, dtype=torch.float64)
+    Yh, muh, varh = hb.bn_fwd(cuda(X), cuda(gamma), cuda(beta), rm_h, rv_h, 0.1, 1e-5)
+    Ye, mue, vare = emu.bn_fwd(X, gamma, beta, rm_e, rv_e, 0.1, 1e-5)
+    close(Yh, Ye, name="bn"); close(rm_h, rm_e, name="rm"); close(rv_h, rv_e, name="rv")
+    dY = r(C, N, gen=gen)
+    dg_h, dbt_h = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    dg_e, dbt_e = torch.zeros(C, dtype=torch.float64), torch.zeros(C, dtype=torch.float64)
+    close(hb.bn_bwd(cuda(dY), cuda(X), muh, varh, cuda(gamma), 1e-5, dg_h, dbt_h),
+          emu.bn_bwd(dY, X, mue, vare, gamma, 1e-5, dg_e, dbt_e), rtol=1e-3, name="bn_bwd")
+    close(dg_h, dg_e, name="dgamma"); close(dbt_h, dbt_e, name="dbeta")
+    close(hb.graph_reduce(cuda(X), G, mean=True), emu.graph_reduce(X, G, mean=True), name="greduce")
+    src = r(C, G, gen=gen)
+    oh, oe = cuda(X), X.clone()
+    hb.graph_bcast_add(oh, cuda(src), 0.5)
+    emu.graph_bcast_add(oe, src, 0.5)
+    close(oh, oe, name="bcast")
+    U = r(C, G, gen=gen)
+    w = r(C, gen=gen).abs() + 0.5
+    eps = float(torch.finfo(torch.float32).eps)
+    Yh, sh_ = hb.rms2_fwd(cuda(U), cuda(w), eps)
+    Ye, se_ = emu.rms2_fwd(U, w, eps)
+    close(Yh, Ye, name="rms2")
+    dw_h, dw_e = torch.zeros(C, device="cuda"), torch.zeros(C, dtype=torch.float64)
+    dU = r(C, G, gen=gen)
+    close(hb.rms2_bwd(cuda(dU), cuda(U), cuda(w), sh_, eps, dw_h), emu.rms2_bwd(dU, U, w, se_, eps, dw_e),
+          rtol=1e-3, name="rms2_bwd")
+    close(dw_h, dw_e, rtol=1e-3, name="rms_dw")
+    mom = torch.stack([r(20, N, gen=gen), r(20, N, gen=gen).abs() + 0.1, r(20, N, gen=gen) * 0.1, r(20, N, gen=gen).abs()])
+    gst = r(80, N, gen=gen)
+    close(hb.moment_coef(cuda(mom), cuda(gst), NC), emu.moment_coef(mom, gst, NC), rtol=1e-3, name="coef")
+    mu1, var1 = r(C, gen=gen), r(C, gen=gen).abs() + 0.1
+    a = hb.bn2_finalize(cuda(mu1), cuda(var1), cuda(gamma), cuda(beta), None, None, 1000, 0.1, 1e-5)
+    b = emu.bn2_finalize(mu1, var1, gamma, beta, None, None, 1000, 0.1, 1e-5)
+    for x, yv in zip(a, b):
+        close(x, yv, name="bn2")
+    Sg, Sgx = r(C, gen=gen), r(C, gen=gen)
+    dgh, dbh = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+    dge, dbe = torch.zeros(C, dtype=torch.float64), torch.zeros(C, dtype=torch.float64)
+    a = hb.bn2_bwd_coef(cuda(Sg), cuda(Sgx), cuda(mu1), cuda(var1), cuda(gamma), 1000, 1e-5, dgh, dbh)
+    b = emu.bn2_bwd_coef(Sg, Sgx, mu1, var1, gamma, 1000, 1e-5, dge, dbe)
+    for x, yv in zip(list(a) + [dgh, dbh], list(b) + [dge, dbe]):
+        close(x, yv, name="bn2bwd")
+
+
+@pytest.mark.parametrize("G,NF,NC", [(1, 37, 12), (2, 50, 16), (1, 9, 128)])
+def test_loss_ops(hb, G, NF, NC):
+    F = 10
+    gen = torch.Generator().manual_seed(11)
+    emu = EmuBackend()
+    d, de = dims(G, NF, NC, F)
+    y = r(F, d.E, gen=gen)
+    sc, sh = r(F, gen=gen) * 0.3 + 1, r(F, gen=gen)
+    Wd1, bd1, Wd2, bd2 = r(F, F, scale=0.3, gen=gen), r(F, gen=gen), r(1, F, scale=0.5, gen=gen), r(1, gen=gen) + 1.0
+    Ti = torch.randint(2, 13, (d.NT,), generator=gen).double()
+    Ni = torch.randint(100, 2000, (d.NT,), generator=gen).double()
+    ci = torch.stack([Ti, Ni])
+    for sharp in [0.0, 12.0]:
+        args = (Wd1, bd1, Wd2, bd2, ci, 42.0 / NC, sharp, 0.3, 99)
+        oh = hb.loss_fwd(d, cuda(y), cuda(sc), cuda(sh), *[cuda(a) if isinstance(a, torch.Tensor) else a for a in args], want_time=True)
+        oe = emu.loss_fwd(de, y, sc, sh, *args, want_time=True)
+        for a, b, nm in zip(oh, oe, ["n_prime", "fiber_time", "tmean", "tvar", "tt"]):
+            close(a, b, rtol=1e-3, atol=1e-4, name=nm)
+        fh = hb.loss_finalize(d, oh[0], oh[1], oh[3], cuda(ci), 0.1, 0.1, 42.0, 10.0, 2000.0, 1.0)
+        fe = emu.loss_finalize(de, oe[0], oe[1], oe[3], ci, 0.1, 0.1, 42.0, 10.0, 2000.0, 1.0)
+        for a, b, nm in zip(fh, fe, ["loss", "utils", "variance", "Gn", "Gf", "Gv"]):
+            close(a, b, rtol=1e-3, atol=1e-4, name=nm)
+        gh = [torch.zeros(F, F, device="cuda"), torch.zeros(F, device="cuda"), torch.zeros(1, F, device="cuda"), torch.zeros(1, device="cuda")]
+        ge = [torch.zeros(F, F, dtype=torch.float64), torch.zeros(F, dtype=torch.float64), torch.zeros(1, F, dtype=torch.float64), torch.zeros(1, dtype=torch.float64)]
+        gxh = hb.loss_bwd(d, cuda(y), cuda(sc), cuda(sh), *[cuda(a) if isinstance(a, torch.Tensor) else a for a in args],
+                          fh[3], fh[4], fh[5], oh[2], 1.0, *gh)
+        gxe = emu.loss_bwd(de, y, sc, sh, *args, fe[3], fe[4], fe[5], oe[2], 1.0, *ge)
+        close(gxh, gxe, rtol=2e-3, atol=1e-4, name="loss gxe")
+        for a, b, nm in zip(gh, ge, ["dWd1", "dbd1", "dWd2", "dbd2"]):
+            close(a, b, rtol=2e-3, atol=1e-4, name=nm)
+
+
+def test_noise_bit_exact(hb):
+    """The in-kernel softfloor uniforms equal tests/noise_ref.py bit for bit."""
+    from noise_ref import uniform_numpy
+    F, G, NF, NC = 8, 1, 16, 16
+    d, _ = dims(G, NF, NC, F)
+    y = torch.zeros(F, d.E, device="cuda")
+    # decoder = 0 -> pred = bd2 = 0 -> time = log(2)*scale ; choose scale so time/T = 0
+    z = torch.zeros
+    Wd1, bd1, Wd2, bd2 = z(F, F, device="cuda"), z(F, device="cuda"), z(1, F, device="cuda"), torch.full((1,), -1e4, device="cuda")
+    ci = torch.stack([torch.ones(NC), torch.full((NC,), 1e9)]).cuda()
+    out = hb.loss_fwd(d, y, None, None, Wd1, bd1, Wd2, bd2, ci, 1.0, 0.0, 1.0, 4242, want_time=True)
+    tt = out[4].cpu().double()
+    u = torch.as_tensor(uniform_numpy(4242, d.E)).double()
+    expect = torch.clamp(u - 0.5, min=0.0)      # time = softplus(-1e4) ~ 0; sharpness 0 -> identity
+    assert torch.allclose(tt, expect, atol=1e-6)
+
+
+def test_adam_matches_torch(hb):
+    from pfsgnn.optim import FusedAdam
+    torch.manual_seed(0)
+    ps = [torch.randn(17, 5, device="cuda", requires_grad=True), torch.randn(33, device="cuda", requires_grad=True)]
+    qs = [p.detach().clone().requires_grad_() for p in ps]
+    o1 = FusedAdam(ps, lr=5e-4, weight_decay=0.01)
+    o2 = torch.optim.Adam(qs, lr=5e-4, weight_decay=0.01)
+    for it in range(5):
+        for p, q in zip(ps, qs):
+            g = torch.randn_like(p)
+            p.grad = g.clone()
+            q.grad = g.clone()
+        o1.step()
+        o2.step()
+    for p, q in zip(ps, qs):
+        assert torch.allclose(p, q, rtol=1e-6, atol=1e-7), (p - q).abs().max()

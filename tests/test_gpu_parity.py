@@ -1,0 +1,202 @@
+"""End-to-end parity of the HIP path against the CPU oracle (the restated reference).
+
+Tolerance (fp32 path vs the float64 oracle): for every compared tensor,
+    max|ours - oracle64| <= max(TOL_K * max|oracle32 - oracle64|, TOL_REL * max|oracle64|)
+i.e. within TOL_K times the error the reference's own fp32 arithmetic makes on the
+same inputs, or TOL_REL relative to the tensor's scale, whichever is larger.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from harness import make_problem, canonical_edges  # noqa: E402
+from noise_ref import uniform_numpy  # noqa: E402
+from oracle.ref_gnn import Graph as OGraph  # noqa: E402
+from oracle import ref_gnn  # noqa: E402
+from oracle.ref_train import loss_function as oracle_loss  # noqa: E402
+
+TOL_K = 16.0
+TOL_REL = 3e-5
+
+
+def check(name, ours, r64, r32):
+    ours = ours.detach().double().cpu()
+    r64 = r64.detach().double().cpu()
+    r32 = r32.detach().double().cpu()
+    scale = r64.abs().max().item() if r64.numel() else 0.0
+    ref_err = (r32 - r64).abs().max().item() if r64.numel() else 0.0
+    err = (ours - r64).abs().max().item() if r64.numel() else 0.0
+    bound = max(TOL_K * ref_err, TOL_REL * scale, 1e-6)
+    assert err <= bound, f"{name}: err {err:.3e} > bound {bound:.3e} (oracle32 err {ref_err:.3e}, scale {scale:.3e})"
+
+
+def oracle_step(model, graph, G, NF, NC, seed, sharp, dtype):
+    m = copy.deepcopy(model).to(dtype)
+    m.train()
+    g = OGraph(graph.edge_index, graph.x_s.to(dtype), graph.x_t.to(dtype), graph.x_e.to(dtype),
+               graph.x_u.to(dtype), graph.s_batch, graph.t_batch)
+    out = m(g)
+    uni = torch.as_tensor(uniform_numpy(seed, G * NF * NC), dtype=dtype)
+    loss, diag = oracle_loss(m, out.x_e, g.x_t, G, NF, NC, pclass=0.1, pfiber=0.1, sharpness=sharp, uniform=uni)
+    loss.backward()
+    return m, out, loss
+
+
+def ours_step(model, graph, G, NF, NC, B, seed, sharp):
+    import pfsgnn
+    from pfsgnn.train import loss_function
+    gnn = pfsgnn.GNN(B=B, Fdim=10, T=12, F_s=1, F_t=2).cuda()
+    gnn.load_state_dict({k: v.float() for k, v in model.state_dict().items()})
+    gnn.train()
+    data = pfsgnn.BipartiteData(graph.edge_index, graph.x_s.float(), graph.x_t.float(), graph.x_e.float(),
+                                graph.x_u.float())
+    gnn.zero_grad()
+    out = gnn(data)
+    loss, util = loss_function(out, graph.x_t.float().cuda(), pclass=0.1, pfiber=0.1, sharpness=sharp, seed=seed)
+    loss.backward()
+    torch.cuda.synchronize()
+    return gnn, out, loss
+
+
+@pytest.mark.parametrize("G,NF,NC,B,sharp", [(1, 40, 12, 2, 12.0), (2, 24, 16, 2, 5.0),
+                                              (1, 16, 128, 1, 20.0), (3, 10, 7, 3, 0.0)])
+def test_gnn_training_step_matches_oracle(G, NF, NC, B, sharp):
+    model, graph = make_problem(G, NF, NC, B=B, seed=G + NF + NC)
+    seed = 777 + NC
+    m64, o64, l64 = oracle_step(model, graph, G, NF, NC, seed, sharp, torch.float64)
+    m32, o32, l32 = oracle_step(model, graph, G, NF, NC, seed, sharp, torch.float32)
+    gnn, out, loss = ours_step(model, graph, G, NF, NC, B, seed, sharp)
+    check("loss", loss, l64, l32)
+    check("x_e", out.x_e, o64.x_e, o32.x_e)
+    check("x_s", out.x_s, o64.x_s, o32.x_s)
+    check("x_t", out.x_t, o64.x_t, o32.x_t)
+    check("x_u", out.x_u, o64.x_u, o32.x_u)
+    p64, p32 = dict(m64.named_parameters()), dict(m32.named_parameters())
+    for name, p in gnn.named_parameters():
+        r64 = p64[name].grad if p64[name].grad is not None else torch.zeros_like(p64[name])
+        r32 = p32[name].grad if p32[name].grad is not None else torch.zeros_like(p32[name])
+        check("grad " + name, p.grad, r64, r32)
+    b64, b32 = m64.state_dict(), m32.state_dict()
+    for k, v in gnn.state_dict().items():
+        if "running" in k or "num_batches" in k:
+            check(k, v.double(), b64[k].double(), b32[k].double())
+
+
+def _module_case(cls_o, cls_h, G, NF, NC, F=10, seed=0):
+    torch.manual_seed(seed)
+    mo = cls_o(F).double()
+    with torch.no_grad():
+        for n, p in mo.named_parameters():
+            if n.startswith("norm."):
+                p.copy_(0.5 + torch.rand_like(p))
+    mh = cls_h(F).cuda()
+    mh.load_state_dict({k: v.float() for k, v in mo.state_dict().items()})
+    ei = canonical_edges(G, NF, NC)
+    gen = torch.Generator().manual_seed(seed + 1)
+    xs = torch.randn(G * NF, F, generator=gen, dtype=torch.float64)
+    xt = torch.randn(G * NC, F, generator=gen, dtype=torch.float64)
+    xe = torch.randn(G * NF * NC, F, generator=gen, dtype=torch.float64) * 2 + 1
+    u = torch.randn(G, F, generator=gen, dtype=torch.float64)
+    return mo, mh, ei, xs, xt, xe, u
+
+
+@pytest.mark.parametrize("kind", ["edge", "source", "target", "global"])
+@pytest.mark.parametrize("G,NF,NC", [(1, 30, 12), (2, 20, 16), (1, 8, 128)])
+def test_standalone_models_match_oracle(kind, G, NF, NC):
+    import pfsgnn
+    pairs = {"edge": (ref_gnn.EdgeModel, pfsgnn.EdgeModel), "source": (ref_gnn.SModel, pfsgnn.SModel),
+             "target": (ref_gnn.TModel, pfsgnn.TModel), "global": (ref_gnn.GlobalModel, pfsgnn.GlobalModel)}
+    mo, mh, ei, xs, xt, xe, u = _module_case(*pairs[kind], G, NF, NC)
+    sb = torch.arange(G).repeat_interleave(NF) if G > 1 else None
+    tb = torch.arange(G).repeat_interleave(NC) if G > 1 else None
+    res = {}
+    for dt in (torch.float64, torch.float32):
+        m = copy.deepcopy(mo).to(dt)
+        ins = [t.detach().clone().to(dt).requires_grad_() for t in (xs, xt, xe, u)]
+        if kind == "edge":
+            out = m(ins[0], ins[1], ei, ins[2], ins[3], sb)
+        elif kind == "source":
+            out = m(ins[0], ins[1], ei, ins[2], ins[3], sb)
+        elif kind == "target":
+            out = m(ins[0], ins[1], ei, ins[2], ins[3], tb)
+        else:
+            out = m(ins[0], ins[1], ei, ins[2], ins[3], sb, tb)
+        gout = torch.linspace(-1, 1, out.numel(), dtype=dt).reshape(out.shape)
+        (out * gout).sum().backward()
+        res[dt] = (m, out, ins)
+    insh = [t.float().cuda().requires_grad_() for t in (xs, xt, xe, u)]
+    outh = mh(insh[0], insh[1], ei.cuda(), insh[2], insh[3])
+    gout = torch.linspace(-1, 1, outh.numel(), dtype=torch.float32, device="cuda").reshape(outh.shape)
+    (outh * gout).sum().backward()
+    m64, o64, i64 = res[torch.float64]
+    m32, o32, i32 = res[torch.float32]
+    check(kind + " out", outh, o64, o32)
+    for nm, a, b, c in zip(["x_s", "x_t", "x_e", "u"], insh, i64, i32):
+        if b.grad is None:
+            continue
+        ga = a.grad if a.grad is not None else torch.zeros_like(a)
+        check(f"{kind} d{nm}", ga, b.grad, c.grad)
+    p64, p32 = dict(m64.named_parameters()), dict(m32.named_parameters())
+    for n, p in mh.named_parameters():
+        check(f"{kind} grad {n}", p.grad, p64[n].grad, p32[n].grad)
+
+
+def test_graph0_permuted_edge_order():
+    """graphs/graph-0.pt's own edge_index (classes of each fiber in argsort order):
+    the HIP path must index edges exactly as given (bit-exact edge_index)."""
+    import os
+    import pfsgnn
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "graph0.npz"))
+    ei = torch.as_tensor(z["edge_index"].astype(np.int64))
+    E = ei.shape[1]
+    gen = torch.Generator().manual_seed(3)
+    x_t = torch.as_tensor(z["x_t"]).double()
+    # graph-0's x_s / x_e / u are all zeros (recorded in the fixture); use small random
+    # values so the check is not degenerate, plus one pass with the true zeros below.
+    for zeros in (False, True):
+        x_s = torch.zeros(2000, 10, dtype=torch.float64) if zeros else 0.1 * torch.randn(2000, 10, generator=gen, dtype=torch.float64)
+        x_e = torch.zeros(E, 10, dtype=torch.float64) if zeros else torch.randn(E, 10, generator=gen, dtype=torch.float64)
+        u = torch.zeros(1, 10, dtype=torch.float64)
+        torch.manual_seed(5)
+        mo = ref_gnn.GNN(B=3, Fdim=10, T=12, F_s=10, F_t=10).double()
+        w = torch.linspace(-1, 1, E * 10, dtype=torch.float64).reshape(E, 10)
+        res = {}
+        for dt in (torch.float64, torch.float32):
+            m = copy.deepcopy(mo).to(dt)
+            out = m(OGraph(ei, x_s.to(dt), x_t.to(dt), x_e.to(dt), u.to(dt)))
+            (out.x_e * w.to(dt)).sum().backward()
+            res[dt] = (m, out)
+        gnn = pfsgnn.GNN(B=3, Fdim=10, T=12, F_s=10, F_t=10).cuda()
+        gnn.load_state_dict({k: v.float() for k, v in mo.state_dict().items()})
+        outh = gnn(pfsgnn.BipartiteData(ei, x_s.float(), x_t.float(), x_e.float(), u.float()))
+        (outh.x_e * w.float().cuda()).sum().backward()
+        (m64, o64), (m32, o32) = res[torch.float64], res[torch.float32]
+        # all-zero x_s makes every fiber identical: the fiber BatchNorm sees zero variance
+        # and its output is rounding noise amplified by 1/sqrt(eps); compare edges only there
+        check("graph0 x_e", outh.x_e, o64.x_e, o32.x_e)
+        if not zeros:
+            p64, p32 = dict(m64.named_parameters()), dict(m32.named_parameters())
+            for n, p in gnn.named_parameters():
+                g64 = p64[n].grad if p64[n].grad is not None else torch.zeros_like(p64[n])
+                g32 = p32[n].grad if p32[n].grad is not None else torch.zeros_like(p32[n])
+                check("graph0 grad " + n, p.grad, g64, g32)
+
+
+def test_step_is_bitwise_deterministic():
+    import pfsgnn
+    from pfsgnn.train import loss_function
+    model, graph = make_problem(2, 300, 128, B=2, seed=1)
+    outs = []
+    for rep in range(2):
+        gnn = pfsgnn.GNN(B=2, Fdim=10, T=12, F_s=1, F_t=2).cuda()
+        gnn.load_state_dict({k: v.float() for k, v in model.state_dict().items()})
+        data = pfsgnn.BipartiteData(graph.edge_index, graph.x_s.float(), graph.x_t.float(), graph.x_e.float(), graph.x_u.float())
+        out = gnn(data)
+        loss, _ = loss_function(out, graph.x_t.float().cuda(), pclass=0.1, pfiber=0.1, sharpness=10.0, seed=5)
+        loss.backward()
+        outs.append(torch.cat([p.grad.reshape(-1) for p in gnn.parameters()]).cpu())
+    assert torch.equal(outs[0], outs[1])
