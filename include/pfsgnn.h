@@ -8,9 +8,10 @@
  * Conventions
  *   - every pointer is a DEVICE pointer (HBM) unless noted; float = fp32;
  *   - node tensors are channel-major [C][N] (row stride N);
- *   - edge tensors are channel-major [C][E] over the canonical fiber-major
- *     order e = (g*NF + f)*NC + c of a batch of G complete bipartite graphs
- *     with NF fibers (source nodes) and NC classes (target nodes) each;
+ *   - edge tensors are channel-major [C][E] over the canonical CLASS-major
+ *     order e = (g*NC + c)*NF + f of a batch of G complete bipartite graphs
+ *     with NF fibers (source nodes) and NC classes (target nodes) each (the
+ *     caller's edge order is mapped by pfsgnn_layout_analyze);
  *     NS = G*NF, NT = G*NC, E = G*NF*NC;
  *   - weights are torch.nn.Linear matrices [out][in] with row stride `ldw`;
  *     a column block is passed as (W + col0, ldw);
@@ -23,7 +24,7 @@
  *     graph-capturable (no allocation, no synchronisation inside);
  *   - return 0 on success, <0 on error (pfsgnn_last_error() has the text).
  *
- * Supported feature widths F (Fdim): 8, 10, 16.  NC <= 256.
+ * Supported feature widths F (Fdim): 8, 10, 16.
  */
 #ifndef PFSGNN_H
 #define PFSGNN_H
@@ -112,7 +113,8 @@ int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe, const flo
  * mom [4][2F][NS]; hs [8F][NS] receives (mean, std, skew, kurt). */
 int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                       const float* sh, const float* Qt, const float* Ws1, const float* Ws2,
-                      const float* bs2, float* mom, float* hs, void* stream);
+                      const float* bs2, float* mom, float* hs, void* ws, size_t ws_bytes,
+                      void* stream);
 /* TModel per-edge message, summed per class before its second Linear
  * (gnn.py:188-190): hsum[:,c] = sum_f lrelu(Rs[:,f] + Wt1[:,F:2F] x). */
 int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
@@ -176,23 +178,25 @@ int pfsgnn_loss_bwd(int G, int NF, int NC, int F, const float* y, const float* s
                     void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- layout
- * The reference takes an arbitrary edge_index [2][E] (int64).  A complete
- * bipartite batch in any edge order maps onto the canonical order by a
- * permutation.  pfsgnn_layout_analyze validates edge_index (every
- * (g, f, c) exactly once, src graph == tgt graph) and writes
- * perm[canonical] = original edge id; status[0] = 1 if complete,
- * status[1] = 1 if already canonical.  (status is device int32[2].) */
+ * The reference takes an arbitrary edge_index [2][E] (int64, gnn.py:7).  A
+ * complete bipartite batch in any edge order maps onto the canonical
+ * class-major order by a permutation.  pfsgnn_layout_analyze validates
+ * edge_index (every (g, f, c) exactly once, src graph == tgt graph) and
+ * writes perm[canonical] = caller's edge id; status (device int32[3]):
+ * [0] complete, [1] caller order is train.py's fiber-major (g*NF+f)*NC+c
+ * (train.py:94), [2] caller order is already canonical.
+ * Conversions take mode 0 (perm), 1 (fiber-major, arithmetic), 2 (identity). */
 int pfsgnn_layout_analyze(const int64_t* edge_index, long long E, int G, int NF, int NC,
                           int32_t* perm, int32_t* status, void* ws, size_t ws_bytes,
                           void* stream);
-/* row-major user edges [E][F] (original order) -> channel-major canonical [F][E] */
-int pfsgnn_edges_to_canonical(const float* src, long long E, int F, const int32_t* perm,
-                              float* dst, void* stream);
-/* channel-major canonical (sc*y+sh) -> row-major [E][F] original order (or,
- * with rowmajor = 0, channel-major [F][E] in original order) */
-int pfsgnn_edges_from_canonical(const float* y, const float* sc, const float* sh, long long E,
-                                int F, const int32_t* perm, int rowmajor, float* dst,
-                                void* stream);
+/* caller-order row-major edges [E][F] -> channel-major canonical [F][E] */
+int pfsgnn_edges_to_canonical(const float* src, int G, int NF, int NC, int F, int mode,
+                              const int32_t* perm, float* dst, void* stream);
+/* canonical (sc*y+sh) -> caller order, row-major [E][F] (rowmajor = 1) or
+ * channel-major [F][E] (rowmajor = 0) */
+int pfsgnn_edges_from_canonical(const float* y, const float* sc, const float* sh, int G, int NF,
+                                int NC, int F, int mode, const int32_t* perm, int rowmajor,
+                                float* dst, void* stream);
 
 /* ---------------------------------------------------------------- optimiser
  * torch.optim.Adam (amsgrad=False, maximize=False) over one flat buffer. */

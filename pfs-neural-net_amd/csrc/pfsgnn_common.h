@@ -40,66 +40,49 @@ __device__ __forceinline__ float lrelu(float x) { return x > 0.f ? x : PF_LEAKY 
 __device__ __forceinline__ float dlrelu(float z) { return z > 0.f ? 1.f : PF_LEAKY; }
 
 // ------------------------------------------------------------ edge geometry
-// A block of 256 threads covers FPI = 256/SW fibers x SW lanes (SW = next
-// power of two >= NC; lanes c >= NC idle).  Thread t owns fiber slot t/SW and
-// class lane t%SW of every fiber tile it visits, so per-class sums stay in the
-// thread's registers and per-fiber sums are butterflies inside an aligned SW-lane
-// segment.  Block b works on graph b / BPG, fiber tiles [j*TPB, (j+1)*TPB).
+// Canonical edge order is class-major, e = (g*NC + c)*NF + f.  A block of 4
+// waves owns 64 consecutive fibers (lane = fiber) of one graph -- fiber group
+// fg of NFG = ceil(NF/64) -- and a range of CPS classes (class split ks of KS);
+// wave w takes classes c0 + w, c0 + w + 4, ...  KS is chosen so that the grid
+// has ~512 blocks (2 per CU) when the batch is small.
 struct EdgeGeo {
-  int G, NF, NC, SW, FPI, TPG, BPG, TPB, nblocks;
+  int G, NF, NC, NFG, KS, CPS, nblocks;
   long long E, NS, NT;
 };
 
 static inline EdgeGeo make_geo(int G, int NF, int NC) {
   EdgeGeo g;
   g.G = G; g.NF = NF; g.NC = NC;
-  g.SW = 1;
-  while (g.SW < NC) g.SW <<= 1;
-  g.FPI = PF_BLOCK / g.SW;
-  g.TPG = (NF + g.FPI - 1) / g.FPI;
-  int target = 1024;
-  int bpg = (target + G - 1) / G;
-  if (bpg > g.TPG) bpg = g.TPG;
-  if (bpg < 1) bpg = 1;
-  g.TPB = (g.TPG + bpg - 1) / bpg;
-  g.BPG = (g.TPG + g.TPB - 1) / g.TPB;
-  g.nblocks = G * g.BPG;
+  g.NFG = (NF + 63) / 64;
+  const int groups = G * g.NFG;
+  const int target = 512;
+  int ks = (target + groups - 1) / groups;
+  const int maxks = (NC + 3) / 4;
+  if (ks > maxks) ks = maxks;
+  if (ks < 1) ks = 1;
+  g.CPS = (NC + ks - 1) / ks;
+  g.KS = (NC + g.CPS - 1) / g.CPS;
+  g.nblocks = groups * g.KS;
   g.E = (long long)G * NF * NC;
   g.NS = (long long)G * NF;
   g.NT = (long long)G * NC;
   return g;
 }
 
-// ------------------------------------------------------------ reductions
-// Sum NV values over the SW-lane segment of the calling thread; every lane
-// of the segment receives the sum.  Deterministic (fixed butterfly order).
-// `scratch` must hold 4*NV floats; SW is block-uniform.
-template <int NV>
-__device__ __forceinline__ void seg_sum(float (&v)[NV], int SW, float* scratch) {
-  const int w = SW < 64 ? SW : 64;
-  for (int o = w >> 1; o > 0; o >>= 1) {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) v[i] += __shfl_xor(v[i], o);
-  }
-  if (SW > 64) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    __syncthreads();
-    if (lane == 0) {
-#pragma unroll
-      for (int i = 0; i < NV; ++i) scratch[wave * NV + i] = v[i];
-    }
-    __syncthreads();
-    const int wps = SW >> 6;
-    const int w0 = (wave / wps) * wps;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      float s = 0.f;
-      for (int k = 0; k < wps; ++k) s += scratch[(w0 + k) * NV + i];
-      v[i] = s;
-    }
-  }
+// 64-lane sum via DPP row butterflies + 4 readlanes; every lane gets the total
+__device__ __forceinline__ float wave_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+  const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+  const float c = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+  const float d = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+  return (a + b) + (c + d);
 }
 
+// ------------------------------------------------------------ reductions
 // Sum NV values over the whole 256-thread block into out[0..NV) (LDS), valid
 // after the call for every thread.  `scratch` >= 4*NV floats.
 template <int NV>
@@ -120,24 +103,6 @@ __device__ __forceinline__ void block_sum(float (&v)[NV], float* scratch) {
 #pragma unroll
   for (int i = 0; i < NV; ++i)
     v[i] = ((scratch[i] + scratch[NV + i]) + scratch[2 * NV + i]) + scratch[3 * NV + i];
-}
-
-// Reduce per-thread per-class accumulators acc[C] over the FPI fiber slots of
-// the block and write the block's partial [NC][C] to part.  `scratch` >= 256*C.
-template <int C>
-__device__ __forceinline__ void column_partial(const float (&acc)[C], int SW, int FPI, int NC,
-                                               float* scratch, float* part) {
-  const int t = threadIdx.x;
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < C; ++i) scratch[t * C + i] = acc[i];
-  __syncthreads();
-  for (int idx = t; idx < NC * C; idx += PF_BLOCK) {
-    const int c = idx / C, i = idx - c * C;
-    float s = 0.f;
-    for (int sl = 0; sl < FPI; ++sl) s += scratch[(sl * SW + c) * C + i];
-    part[idx] = s;
-  }
 }
 
 // ------------------------------------------------------------ MFMA wgrad
@@ -239,7 +204,7 @@ __device__ __forceinline__ float pf_uniform(uint64_t key, uint64_t e) {
 // every per-block partial deterministically (fixed block order).
 void launch_reduce_rows(const float* part, int nb, size_t plen, int ldp, int rows, int cols,
                         float* out, int ldo, int add, float scale, hipStream_t st);
-// Column partials [G][BPG][NC][C] -> channel-major node tensor out[C][G*NC].
+// Column partials [G][NFG][NC][C] -> channel-major node tensor out[C][G*NC].
 void launch_reduce_columns(const float* part, int G, int BPG, int NC, int C, float* out,
                            hipStream_t st);
 

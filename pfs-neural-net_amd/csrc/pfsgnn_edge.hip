@@ -1,53 +1,96 @@
 // pfsgnn_edge.hip -- per-edge kernels of the bipartite message-passing block.
 //
-// Every kernel streams the channel-major edge tensors once (one coalesced
-// dword load per channel per edge), runs the small per-edge MLP in fp32 on
-// the VALU with the weights as wave-uniform (scalar) operands, and does all of
-// its reductions on chip:
-//   * per-fiber sums  -> butterflies inside the fiber's SW-lane segment
-//                        (reference: scatter(..., src, reduce='mean'), gnn.py:140-144);
-//   * per-class sums  -> per-thread registers across the fiber tiles a block
-//                        visits, then one block-level pass (gnn.py:190);
-//   * weight grads    -> sum over edges of an outer product, on
-//                        v_mfma_f32_16x16x4_f32 with the edge as the K index;
-//   * batch moments   -> per-thread Welford / sums, merged per block.
-// Per-block partials are finished by deterministic reduce kernels, so a
-// training step is bitwise reproducible.
+// Canonical edge order is CLASS-major: e = (g*NC + c)*NF + f (channel-major
+// [C][E] tensors).  A wave owns 64 consecutive fibers (lane = fiber) of one
+// graph and walks classes; a 256-thread block = 4 waves on the SAME 64 fibers,
+// each taking every 4th class of the block's class range.  Consequences:
+//   * every edge-tensor load/store is one coalesced 256-B wave access;
+//   * per-class node data (Pt, Qt, g_hsum, ...) is wave-uniform: scalar loads;
+//   * per-fiber node data is per lane: registers or one LDS row per block;
+//   * per-fiber sums over classes (SModel moments gnn.py:140-144, fiber-side
+//     gradient sums) are thread-local accumulations, merged over the 4 waves once;
+//   * per-class sums over fibers (TModel scatter-sum gnn.py:190, class-side
+//     gradient sums) are column sums of the 64 rows a wave already staged in
+//     LDS for its weight-gradient MFMAs;
+//   * weight gradients are sums over edges of outer products, accumulated on
+//     v_mfma_f32_16x16x4_f32 (exact fp32 products) with the edge as the K index.
+// Every cross-block result goes through per-block partials and a fixed-order
+// reduce, so a training step is bitwise reproducible.
 #include "pfsgnn_common.h"
 #include "../../include/pfsgnn.h"
 
 #include <algorithm>
 
-#define EDGE_PROLOGUE                                                  \
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;             \
-  const int bx = blockIdx.x;                                           \
-  const int gg = bx / geo.BPG, jj = bx - gg * geo.BPG;                 \
-  const int slot = t / geo.SW, cl = t - slot * geo.SW;                 \
-  const bool cvalid = cl < geo.NC;                                     \
-  const int tile0 = jj * geo.TPB;                                      \
-  const int tile1 = min(geo.TPG, tile0 + geo.TPB);                     \
-  const long long E = geo.E, NS = geo.NS, NT = geo.NT;                 \
-  const long long cn = (long long)gg * geo.NC + cl;                    \
-  (void)lane; (void)wave; (void)E; (void)NS; (void)NT; (void)cn;
+#define EDGE_PROLOGUE                                                       \
+  const int t = threadIdx.x, lane = t & 63;                                 \
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);                  \
+  const int bx = blockIdx.x;                                                \
+  const int ks = bx % geo.KS, grp = bx / geo.KS;                            \
+  const int fg = grp % geo.NFG, gg = grp / geo.NFG;                         \
+  const int f = fg * 64 + lane;                                             \
+  const bool fvalid = f < geo.NF;                                           \
+  const long long n = (long long)gg * geo.NF + (fvalid ? f : 0);            \
+  const long long nbase = (long long)gg * geo.NF + (long long)fg * 64;      \
+  const int nvalid = min(64, geo.NF - fg * 64);                             \
+  const int c0 = ks * geo.CPS, c1 = min(geo.NC, c0 + geo.CPS);              \
+  const long long E = geo.E, NS = geo.NS, NT = geo.NT;                      \
+  (void)E; (void)NS; (void)NT; (void)n; (void)nbase; (void)nvalid;
 
-#define EDGE_TILE                                                      \
-  const int f = tile * geo.FPI + slot;                                 \
-  const bool fvalid = f < geo.NF;                                      \
-  const bool valid = cvalid && fvalid;                                 \
-  const long long n = (long long)gg * geo.NF + (fvalid ? f : 0);       \
-  const long long e = n * geo.NC + cl;                                 \
-  (void)e;
+#define CLASS_LOOP_BEGIN                                                    \
+  for (int c = c0 + wave; c < c1; c += 4) {                                 \
+    const long long cn = (long long)gg * geo.NC + c;                        \
+    const long long e = cn * geo.NF + (fvalid ? f : 0);
+
+#define CLASS_LOOP_END }
+
+// wave-private LDS hand-off: lanes' writes visible to the wave's later reads
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
 
 template <int F>
-__device__ __forceinline__ void load_edge(float (&x)[F], const float* __restrict__ src,
-                                          const float* __restrict__ sc,
-                                          const float* __restrict__ sh, long long e, long long E,
-                                          bool valid) {
+__device__ __forceinline__ void load_x(float (&x)[F], const float* __restrict__ src,
+                                       const float* __restrict__ sc, const float* __restrict__ sh,
+                                       long long e, long long E, bool valid) {
 #pragma unroll
   for (int k = 0; k < F; ++k) {
     float v = valid ? src[(long long)k * E + e] : 0.f;
     if (sc) v = valid ? fmaf(v, sc[k], sh[k]) : 0.f;
     x[k] = v;
+  }
+}
+
+// Sum over the wave's 64 staged rows of column `lane` (lanes < C), rows of
+// stride LD in the wave's LDS region.
+template <int C, int LD>
+__device__ __forceinline__ float column_sum_rows(const float* rows, int lane) {
+  float s = 0.f;
+  if (lane < C) {
+#pragma unroll 8
+    for (int r = 0; r < 64; ++r) s += rows[r * LD + lane];
+  }
+  return s;
+}
+
+// Merge per-lane per-fiber accumulators acc[C] of the 4 waves (fixed order)
+// and store them for the block's fibers: dst[h*NS + nbase + l] (coalesced).
+// `scratch` >= 4*C*64 floats.
+template <int C>
+__device__ __forceinline__ void fiber_store(const float (&acc)[C], float* scratch, int wave,
+                                            int lane, long long nbase, int nvalid, long long NS,
+                                            float* __restrict__ dst) {
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < C; ++h) scratch[(wave * C + h) * 64 + lane] = acc[h];
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < C * 64; idx += PF_BLOCK) {
+    const int h = idx >> 6, l = idx & 63;
+    if (l < nvalid) {
+      const float s = ((scratch[h * 64 + l] + scratch[(C + h) * 64 + l]) +
+                       scratch[(2 * C + h) * 64 + l]) + scratch[(3 * C + h) * 64 + l];
+      dst[(long long)h * NS + nbase + l] = s;
+    }
   }
 }
 
@@ -65,22 +108,24 @@ __global__ __launch_bounds__(256) void k_edge_mlp_fwd(EdgeGeo geo, const float* 
                                                       float* __restrict__ part) {
   constexpr int H = 4 * F;
   EDGE_PROLOGUE
+  float ps[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) ps[h] = fvalid ? Ps[(long long)h * NS + n] : 0.f;
   float cnt = 0.f, mean[F], m2[F];
 #pragma unroll
   for (int k = 0; k < F; ++k) { mean[k] = 0.f; m2[k] = 0.f; }
-  for (int tile = tile0; tile < tile1; ++tile) {
-    EDGE_TILE
-    if (valid) {
-      float x[F];
-      load_edge<F>(x, xe, xsc, xsh, e, E, true);
-      float a[H];
+  CLASS_LOOP_BEGIN
+    float x[F];
+    load_x<F>(x, xe, xsc, xsh, e, E, fvalid);
+    float a[H];
 #pragma unroll
-      for (int h = 0; h < H; ++h) {
-        float z = Ps[(long long)h * NS + n] + Pt[(long long)h * NT + cn];
+    for (int h = 0; h < H; ++h) {
+      float z = ps[h] + Pt[(long long)h * NT + cn];
 #pragma unroll
-        for (int k = 0; k < F; ++k) z = fmaf(W1[h * H + 2 * F + k], x[k], z);
-        a[h] = lrelu(z);
-      }
+      for (int k = 0; k < F; ++k) z = fmaf(W1[h * H + 2 * F + k], x[k], z);
+      a[h] = lrelu(z);
+    }
+    if (fvalid) {
       cnt += 1.f;
       const float rc = 1.0f / cnt;
 #pragma unroll
@@ -94,7 +139,7 @@ __global__ __launch_bounds__(256) void k_edge_mlp_fwd(EdgeGeo geo, const float* 
         m2[o] = fmaf(d, s - mean[o], m2[o]);
       }
     }
-  }
+  CLASS_LOOP_END
   // Chan merge over the block: lanes (butterfly) then waves (LDS)
   for (int off = 32; off > 0; off >>= 1) {
     const float cb = __shfl_xor(cnt, off);
@@ -110,17 +155,17 @@ __global__ __launch_bounds__(256) void k_edge_mlp_fwd(EdgeGeo geo, const float* 
     }
     cnt = tot;
   }
-  __shared__ float sh[4][1 + 2 * F];
+  __shared__ float shm[4][1 + 2 * F];
   if (lane == 0) {
-    sh[wave][0] = cnt;
+    shm[wave][0] = cnt;
 #pragma unroll
-    for (int k = 0; k < F; ++k) { sh[wave][1 + k] = mean[k]; sh[wave][1 + F + k] = m2[k]; }
+    for (int k = 0; k < F; ++k) { shm[wave][1 + k] = mean[k]; shm[wave][1 + F + k] = m2[k]; }
   }
   __syncthreads();
   if (t < F) {
-    float C0 = sh[0][0], M0 = sh[0][1 + t], Q0 = sh[0][1 + F + t];
+    float C0 = shm[0][0], M0 = shm[0][1 + t], Q0 = shm[0][1 + F + t];
     for (int w = 1; w < 4; ++w) {
-      const float cb = sh[w][0], mb = sh[w][1 + t], qb = sh[w][1 + F + t];
+      const float cb = shm[w][0], mb = shm[w][1 + t], qb = shm[w][1 + F + t];
       const float tot = C0 + cb;
       if (tot > 0.f) {
         const float d = mb - M0;
@@ -136,28 +181,87 @@ __global__ __launch_bounds__(256) void k_edge_mlp_fwd(EdgeGeo geo, const float* 
   }
 }
 
-// merge per-block Welford partials (double) -> mu, biased var
-__global__ void k_moments_finalize(const float* __restrict__ part, int nb, int F, long long n,
-                                   float* __restrict__ mu, float* __restrict__ var) {
-  const int k = threadIdx.x;
-  if (k >= F) return;
-  double cnt = 0, mean = 0, m2 = 0;
-  for (int b = 0; b < nb; ++b) {
-    const float* p = part + (size_t)b * (1 + 2 * F);
-    const double cb = p[0], mb = p[1 + k], qb = p[1 + F + k];
-    const double tot = cnt + cb;
-    if (tot > 0) {
-      const double d = mb - mean;
-      mean += d * (cb / tot);
-      m2 += qb + d * d * (cnt * cb / tot);
-    }
-    cnt = tot;
+__device__ __forceinline__ void chan_merge(double& C0, double& M0, double& Q0, double cb,
+                                           double mb, double qb) {
+  const double tot = C0 + cb;
+  if (tot > 0) {
+    const double d = mb - M0;
+    M0 += d * (cb / tot);
+    Q0 += qb + d * d * (C0 * cb / tot);
   }
-  mu[k] = (float)mean;
-  var[k] = (float)(m2 / (double)n);
+  C0 = tot;
+}
+
+// merge per-block Welford partials -> mu, biased var (one wave per channel)
+__global__ __launch_bounds__(64) void k_moments_finalize(const float* __restrict__ part, int nb,
+                                                         int F, long long n,
+                                                         float* __restrict__ mu,
+                                                         float* __restrict__ var) {
+  const int k = blockIdx.x, lane = threadIdx.x;
+  double cnt = 0, mean = 0, m2 = 0;
+  for (int b = lane; b < nb; b += 64) {
+    const float* p = part + (size_t)b * (1 + 2 * F);
+    chan_merge(cnt, mean, m2, p[0], p[1 + k], p[1 + F + k]);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const double cb = __shfl_xor(cnt, o), mb = __shfl_xor(mean, o), qb = __shfl_xor(m2, o);
+    double c1 = cnt, m1 = mean, q1 = m2;
+    if (lane & o) { c1 = cb; m1 = mb; q1 = qb; }
+    const double c2 = (lane & o) ? cnt : cb, mm2 = (lane & o) ? mean : mb,
+                 qq2 = (lane & o) ? m2 : qb;
+    chan_merge(c1, m1, q1, c2, mm2, qq2);
+    cnt = c1; mean = m1; m2 = q1;
+  }
+  if (lane == 0) {
+    mu[k] = (float)mean;
+    var[k] = (float)(m2 / (double)n);
+  }
 }
 
 // ============================================================ SModel fwd
+// Per fiber, the centred moments of the message over its NC classes
+// (gnn.py:140-151) by Pebay's one-pass update: every lane (fiber) folds its
+// classes into (mean, M2, M3, M4); the 4 waves of a block and then the KS class
+// splits are merged with Pebay's pairwise formulas.  Stable like the
+// reference's two-pass (m - mean)^p, and one read of the edge state.
+template <int F>
+__device__ __forceinline__ void source_message(const float (&x)[F], long long cn, long long NT,
+                                               const float* __restrict__ Qt,
+                                               const float* __restrict__ Ws1,
+                                               const float* __restrict__ Ws2,
+                                               const float* __restrict__ bs2, float (&m)[2 * F]) {
+  constexpr int C = 2 * F;
+  float a[C];
+#pragma unroll
+  for (int h = 0; h < C; ++h) {
+    float z = Qt[(long long)h * NT + cn];
+#pragma unroll
+    for (int k = 0; k < F; ++k) z = fmaf(Ws1[h * C + F + k], x[k], z);
+    a[h] = lrelu(z);
+  }
+#pragma unroll
+  for (int o = 0; o < C; ++o) {
+    float s = bs2[o];
+#pragma unroll
+    for (int h = 0; h < C; ++h) s = fmaf(Ws2[o * C + h], a[h], s);
+    m[o] = s;
+  }
+}
+
+// (na, mean, M2, M3, M4) <- merge with (nb, ...)   [Pebay 2008, eq. 3.1 ff.]
+template <typename T>
+__device__ __forceinline__ void pebay_merge(T na, T& ma, T& M2a, T& M3a, T& M4a, T nb, T mb,
+                                            T M2b, T M3b, T M4b) {
+  const T n = na + nb;
+  const T d = mb - ma, d2 = d * d, nanb = na * nb;
+  const T in = T(1) / n, in2 = in * in;
+  M4a = M4a + M4b + d2 * d2 * nanb * (na * na - nanb + nb * nb) * in2 * in +
+        T(6) * d2 * (na * na * M2b + nb * nb * M2a) * in2 + T(4) * d * (na * M3b - nb * M3a) * in;
+  M3a = M3a + M3b + d2 * d * nanb * (na - nb) * in2 + T(3) * d * (na * M2b - nb * M2a) * in;
+  M2a = M2a + M2b + d2 * nanb * in;
+  ma = ma + d * nb * in;
+}
+
 template <int F>
 __global__ __launch_bounds__(256) void k_source_fwd(EdgeGeo geo, const float* __restrict__ y,
                                                     const float* __restrict__ sc,
@@ -166,64 +270,109 @@ __global__ __launch_bounds__(256) void k_source_fwd(EdgeGeo geo, const float* __
                                                     const float* __restrict__ Ws1,
                                                     const float* __restrict__ Ws2,
                                                     const float* __restrict__ bs2,
-                                                    float* __restrict__ mom,
-                                                    float* __restrict__ hs) {
+                                                    float* __restrict__ partS) {
   constexpr int C = 2 * F;
   EDGE_PROLOGUE
-  __shared__ float scratch[4 * 3 * C];
-  const float invn = 1.0f / (float)geo.NC;
-  for (int tile = tile0; tile < tile1; ++tile) {
-    EDGE_TILE
-    float x[F];
-    load_edge<F>(x, y, sc, sh, e, E, valid);
-    float a[C];
+  __shared__ float scratch[2 * 4 * C * 64];
+  float S[4 * C];  // mean | M2 | M3 | M4
 #pragma unroll
-    for (int h = 0; h < C; ++h) {
-      float z = valid ? Qt[(long long)h * NT + cn] : 0.f;
-#pragma unroll
-      for (int k = 0; k < F; ++k) z = fmaf(Ws1[h * C + F + k], x[k], z);
-      a[h] = lrelu(z);
-    }
-    float m[C], s1[C];
+  for (int i = 0; i < 4 * C; ++i) S[i] = 0.f;
+  float cnt = 0.f;
+  CLASS_LOOP_BEGIN
+    float x[F], m[C];
+    load_x<F>(x, y, sc, sh, e, E, fvalid);
+    source_message<F>(x, cn, NT, Qt, Ws1, Ws2, bs2, m);
+    const float nold = cnt;
+    cnt += 1.f;
+    const float inv = 1.f / cnt, a3 = cnt - 2.f, a4 = cnt * cnt - 3.f * cnt + 3.f;
 #pragma unroll
     for (int o = 0; o < C; ++o) {
-      float s = bs2[o];
-#pragma unroll
-      for (int h = 0; h < C; ++h) s = fmaf(Ws2[o * C + h], a[h], s);
-      m[o] = valid ? s : 0.f;
-      s1[o] = m[o];
+      const float delta = m[o] - S[o];
+      const float dn = delta * inv, dn2 = dn * dn, t1 = delta * dn * nold;
+      S[3 * C + o] = fmaf(t1 * dn2, a4, fmaf(6.f * dn2, S[C + o], fmaf(-4.f * dn, S[2 * C + o],
+                                                                      S[3 * C + o])));
+      S[2 * C + o] = fmaf(t1 * dn, a3, fmaf(-3.f * dn, S[C + o], S[2 * C + o]));
+      S[C + o] += t1;
+      S[o] += dn;
     }
-    seg_sum<C>(s1, geo.SW, scratch);
-    float p[3 * C];
+  CLASS_LOOP_END
+  // merge the 4 waves: (0,2), (1,3) then (0,1)
+  auto wave_count = [&](int w) {
+    const int first = c0 + w;
+    return first < c1 ? (float)((c1 - first + 3) >> 2) : 0.f;
+  };
+  if (wave >= 2) {
 #pragma unroll
-    for (int o = 0; o < C; ++o) {
-      const float mean = s1[o] * invn;
-      const float d = valid ? m[o] - mean : 0.f;
-      const float d2 = d * d;
-      p[o] = d2;
-      p[C + o] = d2 * d;
-      p[2 * C + o] = d2 * d2;
-    }
-    seg_sum<3 * C>(p, geo.SW, scratch);
-    if (cl == 0 && fvalid) {
-      const long long CN = (long long)C * NS;
+    for (int i = 0; i < 4 * C; ++i) scratch[((wave - 2) * 4 * C + i) * 64 + lane] = S[i];
+  }
+  __syncthreads();
+  if (wave < 2) {
+    const float nb = wave_count(wave + 2);
+    if (nb > 0.f) {
 #pragma unroll
       for (int o = 0; o < C; ++o) {
-        const float mean = s1[o] * invn;
-        const float c2 = p[o] * invn, c3 = p[C + o] * invn, c4 = p[2 * C + o] * invn;
-        mom[(long long)o * NS + n] = mean;
-        mom[CN + (long long)o * NS + n] = c2;
-        mom[2 * CN + (long long)o * NS + n] = c3;
-        mom[3 * CN + (long long)o * NS + n] = c4;
-        const float var = c2 > 0.f ? c2 : 0.01f * c2;        // F.leaky_relu (slope 0.01)
-        const float sd = sqrtf(var + 1e-6f);
-        hs[(long long)o * NS + n] = mean;
-        hs[(long long)(C + o) * NS + n] = sd;
-        hs[(long long)(2 * C + o) * NS + n] = c3 / (sd * sd * sd);
-        hs[(long long)(3 * C + o) * NS + n] = c4 / ((sd * sd) * (sd * sd));
+        const float* q = scratch + (size_t)wave * 4 * C * 64 + lane;
+        pebay_merge(cnt, S[o], S[C + o], S[2 * C + o], S[3 * C + o], nb, q[o * 64],
+                    q[(C + o) * 64], q[(2 * C + o) * 64], q[(3 * C + o) * 64]);
       }
+      cnt += nb;
     }
   }
+  __syncthreads();
+  if (wave == 1) {
+#pragma unroll
+    for (int i = 0; i < 4 * C; ++i) scratch[i * 64 + lane] = S[i];
+    scratch[4 * C * 64 + lane] = cnt;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const float nb = scratch[4 * C * 64 + lane];
+    if (nb > 0.f) {
+#pragma unroll
+      for (int o = 0; o < C; ++o)
+        pebay_merge(cnt, S[o], S[C + o], S[2 * C + o], S[3 * C + o], nb, scratch[o * 64 + lane],
+                    scratch[(C + o) * 64 + lane], scratch[(2 * C + o) * 64 + lane],
+                    scratch[(3 * C + o) * 64 + lane]);
+    }
+    if (lane < nvalid) {
+      float* dst = partS + (size_t)ks * 4 * C * NS + nbase + lane;
+#pragma unroll
+      for (int i = 0; i < 4 * C; ++i) dst[(size_t)i * NS] = S[i];
+    }
+  }
+}
+
+// merges the KS partial moments per fiber (double) -> mom (mean, c2, c3, c4), hs
+__global__ void k_source_finalize(const float* __restrict__ partS, int KS, int CPS, int C,
+                                  long long NS, int NC, float* __restrict__ mom,
+                                  float* __restrict__ hs) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // over C*NS
+  const long long CNS = (long long)C * NS;
+  if (idx >= CNS) return;
+  double na = 0, mean = 0, M2 = 0, M3 = 0, M4 = 0;
+  for (int k = 0; k < KS; ++k) {
+    const float* p = partS + (size_t)k * 4 * CNS + idx;
+    const double nb = (double)(min(NC, (k + 1) * CPS) - k * CPS);
+    if (nb <= 0) break;
+    if (na == 0) {
+      mean = p[0]; M2 = p[CNS]; M3 = p[2 * CNS]; M4 = p[3 * CNS];
+    } else {
+      pebay_merge<double>(na, mean, M2, M3, M4, nb, p[0], p[CNS], p[2 * CNS], p[3 * CNS]);
+    }
+    na += nb;
+  }
+  const double invn = 1.0 / (double)NC;
+  const float c2 = (float)(M2 * invn), c3 = (float)(M3 * invn), c4 = (float)(M4 * invn);
+  mom[idx] = (float)mean;
+  mom[CNS + idx] = c2;
+  mom[2 * CNS + idx] = c3;
+  mom[3 * CNS + idx] = c4;
+  const float var = c2 > 0.f ? c2 : 0.01f * c2;  // F.leaky_relu (slope 0.01), gnn.py:141
+  const float sd = sqrtf(var + 1e-6f);
+  hs[idx] = (float)mean;
+  hs[CNS + idx] = sd;
+  hs[2 * CNS + idx] = c3 / (sd * sd * sd);
+  hs[3 * CNS + idx] = c4 / ((sd * sd) * (sd * sd));
 }
 
 // ============================================================ TModel fwd
@@ -235,26 +384,28 @@ __global__ __launch_bounds__(256) void k_target_fwd(EdgeGeo geo, const float* __
                                                     const float* __restrict__ Wt1,
                                                     float* __restrict__ part) {
   constexpr int C = 2 * F;
+  constexpr int LD = C | 1;
   EDGE_PROLOGUE
-  __shared__ float scratch[256 * C];
-  float acc[C];
+  __shared__ float rows[4 * 64 * LD];
+  float* R = rows + wave * 64 * LD;
+  float rs[C];
 #pragma unroll
-  for (int h = 0; h < C; ++h) acc[h] = 0.f;
-  for (int tile = tile0; tile < tile1; ++tile) {
-    EDGE_TILE
-    if (valid) {
-      float x[F];
-      load_edge<F>(x, y, sc, sh, e, E, true);
+  for (int h = 0; h < C; ++h) rs[h] = fvalid ? Rs[(long long)h * NS + n] : 0.f;
+  CLASS_LOOP_BEGIN
+    float x[F];
+    load_x<F>(x, y, sc, sh, e, E, fvalid);
 #pragma unroll
-      for (int h = 0; h < C; ++h) {
-        float z = Rs[(long long)h * NS + n];
+    for (int h = 0; h < C; ++h) {
+      float z = rs[h];
 #pragma unroll
-        for (int k = 0; k < F; ++k) z = fmaf(Wt1[h * C + F + k], x[k], z);
-        acc[h] += lrelu(z);
-      }
+      for (int k = 0; k < F; ++k) z = fmaf(Wt1[h * C + F + k], x[k], z);
+      R[lane * LD + h] = fvalid ? lrelu(z) : 0.f;
     }
-  }
-  column_partial<C>(acc, geo.SW, geo.FPI, geo.NC, scratch, part + (size_t)bx * geo.NC * C);
+    wave_lds_sync();
+    const float s = column_sum_rows<C, LD>(R, lane);
+    if (lane < C) part[(((size_t)gg * geo.NFG + fg) * geo.NC + c) * C + lane] = s;
+    wave_lds_sync();
+  CLASS_LOOP_END
 }
 
 // ============================================================ TModel bwd
@@ -267,30 +418,34 @@ __global__ __launch_bounds__(256) void k_target_bwd(EdgeGeo geo, const float* __
                                                     const float* __restrict__ g_hsum,
                                                     float* __restrict__ GzT,
                                                     float* __restrict__ gxe,
-                                                    float* __restrict__ part) {
+                                                    float* __restrict__ partW) {
   constexpr int C = 2 * F;
   using WG = WGrad<C, F>;
   EDGE_PROLOGUE
-  constexpr int LDS_N = 4 * WG::LDS_FLOATS + 4 * C;
-  static_assert(LDS_N >= 4 * C * F, "lds");
+  constexpr int A0 = 4 * WG::LDS_FLOATS, A1 = 4 * C * 64, A2 = 4 * C * F;
+  constexpr int LDS_N = A0 > A1 ? (A0 > A2 ? A0 : A2) : (A1 > A2 ? A1 : A2);
   __shared__ float lds[LDS_N];
   float* region = lds + wave * WG::LDS_FLOATS;
-  float* scratch = lds + 4 * WG::LDS_FLOATS;
   WG wg;
   wg.zero();
-  for (int tile = tile0; tile < tile1; ++tile) {
-    EDGE_TILE
-    float x[F];
-    load_edge<F>(x, y, sc, sh, e, E, valid);
-    float gz[C];
+  float rs[C], acc[C];
+#pragma unroll
+  for (int h = 0; h < C; ++h) {
+    rs[h] = fvalid ? Rs[(long long)h * NS + n] : 0.f;
+    acc[h] = 0.f;
+  }
+  CLASS_LOOP_BEGIN
+    float x[F], gz[C];
+    load_x<F>(x, y, sc, sh, e, E, fvalid);
 #pragma unroll
     for (int h = 0; h < C; ++h) {
-      float z = valid ? Rs[(long long)h * NS + n] : 0.f;
+      float z = rs[h];
 #pragma unroll
       for (int k = 0; k < F; ++k) z = fmaf(Wt1[h * C + F + k], x[k], z);
-      gz[h] = valid ? g_hsum[(long long)h * NT + cn] * dlrelu(z) : 0.f;
+      gz[h] = fvalid ? g_hsum[(long long)h * NT + cn] * dlrelu(z) : 0.f;
+      acc[h] += gz[h];
     }
-    if (gxe && valid) {
+    if (gxe && fvalid) {
 #pragma unroll
       for (int k = 0; k < F; ++k) {
         float s = 0.f;
@@ -300,16 +455,12 @@ __global__ __launch_bounds__(256) void k_target_bwd(EdgeGeo geo, const float* __
       }
     }
     wg.stage(region, gz, x, lane);
-    __syncthreads();
+    wave_lds_sync();
     wg.accum(region, lane);
-    __syncthreads();
-    seg_sum<C>(gz, geo.SW, scratch);
-    if (cl == 0 && fvalid) {
-#pragma unroll
-      for (int h = 0; h < C; ++h) GzT[(long long)h * NS + n] = gz[h];
-    }
-  }
-  wg.block_partial(lds, part + (size_t)bx * C * F);
+    wave_lds_sync();
+  CLASS_LOOP_END
+  fiber_store<C>(acc, lds, wave, lane, nbase, nvalid, NS, GzT + (size_t)ks * C * NS);
+  wg.block_partial(lds, partW + (size_t)bx * C * F);
 }
 
 // ============================================================ SModel bwd (+T, +BN sums)
@@ -325,61 +476,70 @@ __global__ __launch_bounds__(256) void k_source_bwd(
     float* __restrict__ partBN) {
   constexpr int C = 2 * F;
   using WG2 = WGrad<C, C + 1>;  // g_m (x) [a, 1]  -> dWs2 | dbs2
-  using WG1 = WGrad<C, F>;      // g_zs (x) x      -> dWs1[:, F:2F]
+  using WG1 = WGrad<C, F>;      // g_zs (x) x      -> dWs1[:, F:2F] (+ per-class sums of g_zs)
   constexpr int STAGE = WG2::LDS_FLOATS > WG1::LDS_FLOATS ? WG2::LDS_FLOATS : WG1::LDS_FLOATS;
-  constexpr int LOOP_N = 4 * STAGE;
-  constexpr int TAIL_N0 = (4 * C * (C + 1) > 256 * C) ? 4 * C * (C + 1) : 256 * C;
-  constexpr int LDS_N = LOOP_N > TAIL_N0 ? LOOP_N : TAIL_N0;
+  constexpr int NFIB = 6 * C;   // per-fiber LDS rows: mean, C0..C3, Rs
+  constexpr int TAIL = 4 * C * (C + 1) > 4 * 2 * F ? 4 * C * (C + 1) : 4 * 2 * F;
+  constexpr int LOOP_N = 4 * STAGE + NFIB * 64;
+  constexpr int LDS_N = LOOP_N > TAIL ? LOOP_N : TAIL;
   EDGE_PROLOGUE
   __shared__ float lds[LDS_N];
   float* region = lds + wave * STAGE;
-  float* scratch = lds;
+  float* fib = lds + 4 * STAGE;
+  const long long CNS = (long long)C * NS;
+  for (int idx = threadIdx.x; idx < NFIB * 64; idx += PF_BLOCK) {
+    const int r = idx >> 6, l = idx & 63;
+    float v = 0.f;
+    if (l < nvalid) {
+      const long long nn = nbase + l;
+      if (r < C) v = mean[(long long)r * NS + nn];
+      else if (r < 5 * C) v = coef[(long long)((r - C) / C) * CNS + (long long)((r - C) % C) * NS + nn];
+      else if (Rs) v = Rs[(long long)(r - 5 * C) * NS + nn];
+    }
+    fib[idx] = v;
+  }
+  __syncthreads();
   WG2 wg2;
   WG1 wg1;
   wg2.zero();
   wg1.zero();
-  float colS[C];
-#pragma unroll
-  for (int h = 0; h < C; ++h) colS[h] = 0.f;
   float sg[F], sgx[F];
 #pragma unroll
   for (int k = 0; k < F; ++k) { sg[k] = 0.f; sgx[k] = 0.f; }
-  const long long CN = (long long)C * NS;
-  for (int tile = tile0; tile < tile1; ++tile) {
-    EDGE_TILE
+  CLASS_LOOP_BEGIN
     float yv[F], x[F];
 #pragma unroll
     for (int k = 0; k < F; ++k) {
-      yv[k] = valid ? y[(long long)k * E + e] : 0.f;
-      x[k] = valid ? (sc ? fmaf(yv[k], sc[k], sh[k]) : yv[k]) : 0.f;
+      yv[k] = fvalid ? y[(long long)k * E + e] : 0.f;
+      x[k] = fvalid ? (sc ? fmaf(yv[k], sc[k], sh[k]) : yv[k]) : 0.f;
     }
-    // forward recompute of the SModel message
-    float zs[C], a[C + 1];
+    float* A = region;
+    float* B = region + 64 * WG2::LDA;
+    float zs[C];
 #pragma unroll
     for (int h = 0; h < C; ++h) {
-      float z = valid ? Qt[(long long)h * NT + cn] : 0.f;
+      float z = Qt[(long long)h * NT + cn];
 #pragma unroll
       for (int k = 0; k < F; ++k) z = fmaf(Ws1[h * C + F + k], x[k], z);
       zs[h] = z;
-      a[h] = lrelu(z);
+      B[lane * WG2::LDB + h] = lrelu(z);
     }
-    a[C] = 1.f;
+    B[lane * WG2::LDB + C] = 1.f;
     float gm[C];
 #pragma unroll
     for (int o = 0; o < C; ++o) {
       float s = bs2[o];
 #pragma unroll
-      for (int h = 0; h < C; ++h) s = fmaf(Ws2[o * C + h], a[h], s);
-      const long long idx = (long long)o * NS + n;
-      const float d = s - mean[idx];
-      const float c0 = coef[idx], c1 = coef[CN + idx], c2 = coef[2 * CN + idx],
-                  c3 = coef[3 * CN + idx];
-      gm[o] = valid ? fmaf(d, fmaf(d, fmaf(d, c3, c2), c1), c0) : 0.f;
+      for (int h = 0; h < C; ++h) s = fmaf(Ws2[o * C + h], lrelu(zs[h]), s);
+      const float d = s - fib[o * 64 + lane];
+      const float q0 = fib[(C + o) * 64 + lane], q1 = fib[(2 * C + o) * 64 + lane],
+                  q2 = fib[(3 * C + o) * 64 + lane], q3 = fib[(4 * C + o) * 64 + lane];
+      gm[o] = fvalid ? fmaf(d, fmaf(d, fmaf(d, q3, q2), q1), q0) : 0.f;
+      A[lane * WG2::LDA + o] = gm[o];
     }
-    wg2.stage(region, gm, a, lane);
-    __syncthreads();
+    wave_lds_sync();
     wg2.accum(region, lane);
-    __syncthreads();
+    wave_lds_sync();
     float gz[C];
 #pragma unroll
     for (int h = 0; h < C; ++h) {
@@ -387,12 +547,7 @@ __global__ __launch_bounds__(256) void k_source_bwd(
 #pragma unroll
       for (int o = 0; o < C; ++o) s = fmaf(Ws2[o * C + h], gm[o], s);
       gz[h] = s * dlrelu(zs[h]);
-      colS[h] += gz[h];
     }
-    wg1.stage(region, gz, x, lane);
-    __syncthreads();
-    wg1.accum(region, lane);
-    __syncthreads();
     float g[F];
 #pragma unroll
     for (int k = 0; k < F; ++k) {
@@ -401,14 +556,14 @@ __global__ __launch_bounds__(256) void k_source_bwd(
       for (int h = 0; h < C; ++h) s = fmaf(Ws1[h * C + F + k], gz[h], s);
       g[k] = s;
     }
-    if (Rs) {  // TModel's per-edge input gradient, recomputed
+    if (Rs) {  // TModel's per-edge input gradient, recomputed (gnn.py:188-190)
       float gzt[C];
 #pragma unroll
       for (int h = 0; h < C; ++h) {
-        float z = valid ? Rs[(long long)h * NS + n] : 0.f;
+        float z = fib[(5 * C + h) * 64 + lane];
 #pragma unroll
         for (int k = 0; k < F; ++k) z = fmaf(Wt1[h * C + F + k], x[k], z);
-        gzt[h] = valid ? g_hsum[(long long)h * NT + cn] * dlrelu(z) : 0.f;
+        gzt[h] = fvalid ? g_hsum[(long long)h * NT + cn] * dlrelu(z) : 0.f;
       }
 #pragma unroll
       for (int k = 0; k < F; ++k) {
@@ -420,34 +575,39 @@ __global__ __launch_bounds__(256) void k_source_bwd(
     }
     if (g_next) {
 #pragma unroll
-      for (int k = 0; k < F; ++k) g[k] += valid ? g_next[(long long)k * E + e] : 0.f;
+      for (int k = 0; k < F; ++k) g[k] += fvalid ? g_next[(long long)k * E + e] : 0.f;
     }
-    if (valid) {
+    if (fvalid) {
 #pragma unroll
       for (int k = 0; k < F; ++k) g_tot[(long long)k * E + e] = g[k];
     }
     if (mu1) {
 #pragma unroll
       for (int k = 0; k < F; ++k) {
-        const float gk = valid ? g[k] : 0.f;
+        const float gk = fvalid ? g[k] : 0.f;
         sg[k] += gk;
         sgx[k] = fmaf(gk, (yv[k] - mu1[k]) * inv1[k], sgx[k]);
       }
     }
-  }
-  wg2.block_partial(scratch, partW2 + (size_t)bx * C * (C + 1));
-  wg1.block_partial(scratch, partW1 + (size_t)bx * C * F);
-  column_partial<C>(colS, geo.SW, geo.FPI, geo.NC, scratch, partCol + (size_t)bx * geo.NC * C);
+    wg1.stage(region, gz, x, lane);
+    wave_lds_sync();
+    wg1.accum(region, lane);
+    const float cs = column_sum_rows<C, WG1::LDA>(region, lane);   // per-class sum of g_zs
+    if (lane < C) partCol[(((size_t)gg * geo.NFG + fg) * geo.NC + c) * C + lane] = cs;
+    wave_lds_sync();
+  CLASS_LOOP_END
+  wg2.block_partial(lds, partW2 + (size_t)bx * C * (C + 1));
+  wg1.block_partial(lds, partW1 + (size_t)bx * C * F);
   if (mu1) {
     float v[2 * F];
 #pragma unroll
     for (int k = 0; k < F; ++k) { v[k] = sg[k]; v[F + k] = sgx[k]; }
-    block_sum<2 * F>(v, scratch);
-    if (t < 2 * F) {
+    block_sum<2 * F>(v, lds);
+    if (threadIdx.x < 2 * F) {
       float val = 0.f;
 #pragma unroll
-      for (int i = 0; i < 2 * F; ++i) val = (i == t) ? v[i] : val;
-      partBN[(size_t)bx * 2 * F + t] = val;
+      for (int i = 0; i < 2 * F; ++i) val = ((int)threadIdx.x == i) ? v[i] : val;
+      partBN[(size_t)bx * 2 * F + threadIdx.x] = val;
     }
   }
 }
@@ -464,9 +624,8 @@ __global__ __launch_bounds__(256) void k_edge_bn_sums(EdgeGeo geo, const float* 
   float v[2 * F];
 #pragma unroll
   for (int k = 0; k < 2 * F; ++k) v[k] = 0.f;
-  for (int tile = tile0; tile < tile1; ++tile) {
-    EDGE_TILE
-    if (valid) {
+  CLASS_LOOP_BEGIN
+    if (fvalid) {
 #pragma unroll
       for (int k = 0; k < F; ++k) {
         const float gk = g[(long long)k * E + e];
@@ -474,13 +633,13 @@ __global__ __launch_bounds__(256) void k_edge_bn_sums(EdgeGeo geo, const float* 
         v[F + k] = fmaf(gk, (y[(long long)k * E + e] - mu1[k]) * inv1[k], v[F + k]);
       }
     }
-  }
+  CLASS_LOOP_END
   block_sum<2 * F>(v, scratch);
-  if (t < 2 * F) {
+  if (threadIdx.x < 2 * F) {
     float val = 0.f;
 #pragma unroll
-    for (int i = 0; i < 2 * F; ++i) val = (i == t) ? v[i] : val;
-    partBN[(size_t)bx * 2 * F + t] = val;
+    for (int i = 0; i < 2 * F; ++i) val = ((int)threadIdx.x == i) ? v[i] : val;
+    partBN[(size_t)bx * 2 * F + threadIdx.x] = val;
   }
 }
 
@@ -495,46 +654,53 @@ __global__ __launch_bounds__(256) void k_edge_mlp_bwd(
     float* __restrict__ partW2, float* __restrict__ partW1, float* __restrict__ partCol) {
   constexpr int H = 4 * F;
   using WG2 = WGrad<F, H + 1>;  // g_y (x) [a1, 1] -> dW2 | db2
-  using WG1 = WGrad<H, F>;      // g_z1 (x) x      -> dW1[:, 2F:3F]
+  using WG1 = WGrad<H, F>;      // g_z1 (x) x      -> dW1[:, 2F:3F] (+ per-class sums of g_z1)
   constexpr int STAGE = WG2::LDS_FLOATS > WG1::LDS_FLOATS ? WG2::LDS_FLOATS : WG1::LDS_FLOATS;
-  constexpr int LOOP_N = 4 * STAGE + 4 * H;
-  constexpr int TAIL_N0 = (4 * H * (F + 1) > 256 * H) ? 4 * H * (F + 1) : 256 * H;
-  constexpr int LDS_N = LOOP_N > TAIL_N0 ? LOOP_N : TAIL_N0;
+  constexpr int LOOP_N = 4 * STAGE + H * 64;
+  constexpr int TAIL0 = 4 * H * 64 > 4 * H * (F + 1) ? 4 * H * 64 : 4 * H * (F + 1);
+  constexpr int LDS_N = LOOP_N > TAIL0 ? LOOP_N : TAIL0;
   EDGE_PROLOGUE
   __shared__ float lds[LDS_N];
   float* region = lds + wave * STAGE;
-  float* scratch = lds + 4 * STAGE;  // seg_sum scratch during the loop
+  float* psl = lds + 4 * STAGE;
+  for (int idx = threadIdx.x; idx < H * 64; idx += PF_BLOCK) {
+    const int h = idx >> 6, l = idx & 63;
+    psl[idx] = l < nvalid ? Ps[(long long)h * NS + nbase + l] : 0.f;
+  }
+  __syncthreads();
   WG2 wg2;
   WG1 wg1;
   wg2.zero();
   wg1.zero();
-  float colT[H];
+  float acc[H];
 #pragma unroll
-  for (int h = 0; h < H; ++h) colT[h] = 0.f;
-  for (int tile = tile0; tile < tile1; ++tile) {
-    EDGE_TILE
+  for (int h = 0; h < H; ++h) acc[h] = 0.f;
+  CLASS_LOOP_BEGIN
     float gy[F], x[F];
 #pragma unroll
     for (int k = 0; k < F; ++k) {
-      const float gt = valid ? g_tot[(long long)k * E + e] : 0.f;
-      const float yk = valid ? y[(long long)k * E + e] : 0.f;
-      gy[k] = valid ? fmaf(gam1[k], yk, fmaf(alpha[k], gt, gam0[k])) : 0.f;
+      const float gt = fvalid ? g_tot[(long long)k * E + e] : 0.f;
+      const float yk = fvalid ? y[(long long)k * E + e] : 0.f;
+      gy[k] = fvalid ? fmaf(gam1[k], yk, fmaf(alpha[k], gt, gam0[k])) : 0.f;
     }
-    load_edge<F>(x, xe, xsc, xsh, e, E, valid);
-    float z[H], a[H + 1];
+    load_x<F>(x, xe, xsc, xsh, e, E, fvalid);
+    float* A = region;
+    float* B = region + 64 * WG2::LDA;
+#pragma unroll
+    for (int k = 0; k < F; ++k) A[lane * WG2::LDA + k] = gy[k];
+    float z[H];
 #pragma unroll
     for (int h = 0; h < H; ++h) {
-      float s = valid ? Ps[(long long)h * NS + n] + Pt[(long long)h * NT + cn] : 0.f;
+      float s = psl[h * 64 + lane] + Pt[(long long)h * NT + cn];
 #pragma unroll
       for (int k = 0; k < F; ++k) s = fmaf(W1[h * H + 2 * F + k], x[k], s);
       z[h] = s;
-      a[h] = lrelu(s);
+      B[lane * WG2::LDB + h] = lrelu(s);
     }
-    a[H] = 1.f;
-    wg2.stage(region, gy, a, lane);
-    __syncthreads();
+    B[lane * WG2::LDB + H] = 1.f;
+    wave_lds_sync();
     wg2.accum(region, lane);
-    __syncthreads();
+    wave_lds_sync();
     float gz[H];
 #pragma unroll
     for (int h = 0; h < H; ++h) {
@@ -542,9 +708,9 @@ __global__ __launch_bounds__(256) void k_edge_mlp_bwd(
 #pragma unroll
       for (int o = 0; o < F; ++o) s = fmaf(W2[o * H + h], gy[o], s);
       gz[h] = s * dlrelu(z[h]);
-      colT[h] += gz[h];
+      acc[h] += gz[h];
     }
-    if (gxe && valid) {
+    if (gxe && fvalid) {
 #pragma unroll
       for (int k = 0; k < F; ++k) {
         float s = 0.f;
@@ -554,18 +720,25 @@ __global__ __launch_bounds__(256) void k_edge_mlp_bwd(
       }
     }
     wg1.stage(region, gz, x, lane);
-    __syncthreads();
+    wave_lds_sync();
     wg1.accum(region, lane);
-    __syncthreads();
-    seg_sum<H>(gz, geo.SW, scratch);
-    if (cl == 0 && fvalid) {
-#pragma unroll
-      for (int h = 0; h < H; ++h) GzEs[(long long)h * NS + n] = gz[h];
-    }
-  }
+    const float cs = column_sum_rows<H, WG1::LDA>(region, lane);   // per-class sum of g_z1
+    if (lane < H) partCol[(((size_t)gg * geo.NFG + fg) * geo.NC + c) * H + lane] = cs;
+    wave_lds_sync();
+  CLASS_LOOP_END
+  fiber_store<H>(acc, lds, wave, lane, nbase, nvalid, NS, GzEs + (size_t)ks * H * NS);
   wg2.block_partial(lds, partW2 + (size_t)bx * F * (H + 1));
   wg1.block_partial(lds, partW1 + (size_t)bx * H * F);
-  column_partial<H>(colT, geo.SW, geo.FPI, geo.NC, lds, partCol + (size_t)bx * geo.NC * H);
+}
+
+// sum KS per-fiber partials [KS][C][NS] -> out[C][NS]
+__global__ void k_reduce_fiber(const float* __restrict__ part, int KS, long long len,
+                               float* __restrict__ out) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= len) return;
+  float s = 0.f;
+  for (int k = 0; k < KS; ++k) s += part[(size_t)k * len + idx];
+  out[idx] = s;
 }
 
 // ============================================================ host side
@@ -586,9 +759,8 @@ struct Ws {
 
 int check_dims(const char* where, int G, int NF, int NC, int F) {
   if (G <= 0 || NF <= 0 || NC <= 0) return pf::fail(where, "G, NF, NC must be positive");
-  if (NC > 256) return pf::fail(where, "NC > 256 is not supported by the dense edge kernels");
   if (F != 8 && F != 10 && F != 16) return pf::fail(where, "unsupported Fdim (8, 10, 16)");
-  if ((long long)G * NF * NC * 16 >= (1ll << 31) * 16ll) return pf::fail(where, "too many edges");
+  if ((long long)G * NF * NC >= (1ll << 31)) return pf::fail(where, "too many edges");
   return 0;
 }
 
@@ -600,22 +772,36 @@ int check_dims(const char* where, int G, int NF, int NC, int F) {
     default: return pf::fail("dispatch", "unsupported F");   \
   }
 
+// per-fiber outputs go straight to `out` when KS == 1, else to a KS-deep
+// partial in the workspace that fiber_finish() reduces in fixed order
+float* fiber_dst(const EdgeGeo& geo, int C, float* out, Ws& w) {
+  return geo.KS == 1 ? out : w.take((size_t)geo.KS * C * geo.NS);
+}
+void fiber_finish(const EdgeGeo& geo, int C, const float* dst, float* out, hipStream_t st) {
+  if (geo.KS == 1) return;
+  const long long len = (long long)C * geo.NS;
+  hipLaunchKernelGGL(k_reduce_fiber, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, st, dst,
+                     geo.KS, len, out);
+}
+
 }  // namespace
 
 extern "C" size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F) {
   const EdgeGeo geo = make_geo(G, NF, NC);
-  const size_t nb = geo.nblocks;
+  const size_t nb = geo.nblocks, ks = geo.KS, NS = geo.NS;
   const size_t H = 4 * F, C = 2 * F;
+  const size_t colp = (size_t)G * geo.NFG * NC;
   size_t edge = 0;
-  edge = std::max(edge, nb * (1 + 2 * F));                                   // mlp fwd
-  edge = std::max(edge, nb * NC * C);                                        // target fwd
-  edge = std::max(edge, nb * C * F);                                         // target bwd
-  edge = std::max(edge, nb * (C * (C + 1) + C * F + NC * C + 2 * F) + 1024); // source bwd
-  edge = std::max(edge, nb * (F * (H + 1) + H * F + NC * H) + 1024);         // edge bwd
-  edge = std::max(edge, nb * (NC * 4 + F * (F + 1) + F + 1) + 1024);         // loss
-  size_t node = (size_t)64 * 128 * 128 + 4096;                               // wgrad splits
-  size_t lay = (size_t)geo.E + 1024;                                         // layout counts
-  return (std::max(std::max(edge, node), lay) + 64 * 8) * sizeof(float) + 8 * 256;
+  edge = std::max(edge, nb * (1 + 2 * F));                                          // mlp fwd
+  edge = std::max(edge, ks * 4 * C * NS + C * NS + 1024);                           // source fwd
+  edge = std::max(edge, colp * C + 1024);                                           // target fwd
+  edge = std::max(edge, nb * C * F + ks * C * NS + 1024);                           // target bwd
+  edge = std::max(edge, nb * (C * (C + 1) + C * F + 2 * F) + colp * C + 4096);      // source bwd
+  edge = std::max(edge, nb * (F * (H + 1) + H * F) + colp * H + ks * H * NS + 4096);  // edge bwd
+  edge = std::max(edge, colp * 4 + nb * (F * (F + 1) + F + 1) + 4096);             // loss
+  size_t node = (size_t)64 * 128 * 128 + 4096;                                      // wgrad splits
+  size_t lay = (size_t)geo.E + 1024;                                                // layout counts
+  return (std::max(std::max(edge, node), lay) + 64 * 16) * sizeof(float) + 16 * 256;
 }
 
 extern "C" int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe,
@@ -634,7 +820,7 @@ extern "C" int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe
   DISPATCH_F(F, hipLaunchKernelGGL(k_edge_mlp_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
                                    xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part));
   tm_.end(); }
-  hipLaunchKernelGGL(k_moments_finalize, dim3(1), dim3(64), 0, st, part, geo.nblocks, F, geo.E,
+  hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(64), 0, st, part, geo.nblocks, F, geo.E,
                      mu, var);
   return pf::check_launch("pfsgnn_edge_mlp_fwd");
 }
@@ -642,15 +828,22 @@ extern "C" int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe
 extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                                  const float* sh, const float* Qt, const float* Ws1,
                                  const float* Ws2, const float* bs2, float* mom, float* hs,
-                                 void* stream) {
+                                 void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_source_fwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(y && Qt && Ws1 && Ws2 && bs2 && mom && hs, "pfsgnn_source_fwd", "null");
   const EdgeGeo geo = make_geo(G, NF, NC);
+  const int C = 2 * F;
+  Ws w{reinterpret_cast<char*>(ws), ws_bytes};
+  float* partS = w.take((size_t)geo.KS * 4 * C * geo.NS);
+  PF_REQUIRE(partS, "pfsgnn_source_fwd", "workspace too small");
   hipStream_t st = as_stream(stream);
   { pf::Timer tm_("source_fwd", st);
   DISPATCH_F(F, hipLaunchKernelGGL(k_source_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
-                                   sc, sh, Qt, Ws1, Ws2, bs2, mom, hs));
+                                   sc, sh, Qt, Ws1, Ws2, bs2, partS));
   tm_.end(); }
+  const long long len = (long long)C * geo.NS;
+  hipLaunchKernelGGL(k_source_finalize, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, st,
+                     partS, geo.KS, geo.CPS, C, geo.NS, NC, mom, hs);
   return pf::check_launch("pfsgnn_source_fwd");
 }
 
@@ -661,14 +854,14 @@ extern "C" int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, c
   PF_REQUIRE(y && Rs && Wt1 && hsum, "pfsgnn_target_fwd", "null");
   const EdgeGeo geo = make_geo(G, NF, NC);
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
-  float* part = w.take((size_t)geo.nblocks * NC * 2 * F);
+  float* part = w.take((size_t)G * geo.NFG * NC * 2 * F);
   PF_REQUIRE(part, "pfsgnn_target_fwd", "workspace too small");
   hipStream_t st = as_stream(stream);
   { pf::Timer tm_("target_fwd", st);
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
                                    sc, sh, Rs, Wt1, part));
   tm_.end(); }
-  launch_reduce_columns(part, G, geo.BPG, NC, 2 * F, hsum, st);
+  launch_reduce_columns(part, G, geo.NFG, NC, 2 * F, hsum, st);
   return pf::check_launch("pfsgnn_target_fwd");
 }
 
@@ -682,12 +875,14 @@ extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, c
   const int C = 2 * F;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
   float* part = w.take((size_t)geo.nblocks * C * F);
-  PF_REQUIRE(part, "pfsgnn_target_bwd", "workspace too small");
+  float* gz = fiber_dst(geo, C, GzT, w);
+  PF_REQUIRE(part && gz, "pfsgnn_target_bwd", "workspace too small");
   hipStream_t st = as_stream(stream);
   { pf::Timer tm_("target_bwd", st);
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
-                                   sc, sh, Rs, Wt1, g_hsum, GzT, gxe, part));
+                                   sc, sh, Rs, Wt1, g_hsum, gz, gxe, part));
   tm_.end(); }
+  fiber_finish(geo, C, gz, GzT, st);
   launch_reduce_rows(part, geo.nblocks, (size_t)C * F, F, C, F, dWt1 + F, C, 1, 1.f, st);
   return pf::check_launch("pfsgnn_target_bwd");
 }
@@ -712,7 +907,7 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
   float* pW2 = w.take(nb * C * (C + 1));
   float* pW1 = w.take(nb * C * F);
-  float* pCol = w.take(nb * NC * C);
+  float* pCol = w.take((size_t)G * geo.NFG * NC * C);
   float* pBN = w.take(nb * 2 * F);
   PF_REQUIRE(pW2 && pW1 && pCol && pBN, "pfsgnn_source_bwd", "workspace too small");
   hipStream_t st = as_stream(stream);
@@ -724,7 +919,7 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
   launch_reduce_rows(pW2, nb, (size_t)C * (C + 1), C + 1, C, C, dWs2, C, 1, 1.f, st);
   launch_reduce_rows(pW2 + C, nb, (size_t)C * (C + 1), C + 1, C, 1, dbs2, 1, 1, 1.f, st);
   launch_reduce_rows(pW1, nb, (size_t)C * F, F, C, F, dWs1 + F, C, 1, 1.f, st);
-  launch_reduce_columns(pCol, G, geo.BPG, NC, C, GzS, st);
+  launch_reduce_columns(pCol, G, geo.NFG, NC, C, GzS, st);
   if (mu1) {
     launch_reduce_rows(pBN, nb, (size_t)2 * F, F, 1, F, Sg, F, 0, 1.f, st);
     launch_reduce_rows(pBN + F, nb, (size_t)2 * F, F, 1, F, Sgx, F, 0, 1.f, st);
@@ -769,17 +964,19 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
   float* pW2 = w.take(nb * F * (H + 1));
   float* pW1 = w.take(nb * H * F);
-  float* pCol = w.take(nb * NC * H);
-  PF_REQUIRE(pW2 && pW1 && pCol, "pfsgnn_edge_mlp_bwd", "workspace too small");
+  float* pCol = w.take((size_t)G * geo.NFG * NC * H);
+  float* gs = fiber_dst(geo, H, GzEs, w);
+  PF_REQUIRE(pW2 && pW1 && pCol && gs, "pfsgnn_edge_mlp_bwd", "workspace too small");
   hipStream_t st = as_stream(stream);
   { pf::Timer tm_("edge_mlp_bwd", st);
   DISPATCH_F(F, hipLaunchKernelGGL(k_edge_mlp_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
                                    g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1, W2, gxe,
-                                   GzEs, pW2, pW1, pCol));
+                                   gs, pW2, pW1, pCol));
   tm_.end(); }
+  fiber_finish(geo, H, gs, GzEs, st);
   launch_reduce_rows(pW2, nb, (size_t)F * (H + 1), H + 1, F, H, dW2, H, 1, 1.f, st);
   launch_reduce_rows(pW2 + H, nb, (size_t)F * (H + 1), H + 1, F, 1, db2, 1, 1, 1.f, st);
   launch_reduce_rows(pW1, nb, (size_t)H * F, F, H, F, dW1 + 2 * F, H, 1, 1.f, st);
-  launch_reduce_columns(pCol, G, geo.BPG, NC, H, GzEt, st);
+  launch_reduce_columns(pCol, G, geo.NFG, NC, H, GzEt, st);
   return pf::check_launch("pfsgnn_edge_mlp_bwd");
 }

@@ -6,25 +6,33 @@
 #include <algorithm>
 #include <cmath>
 
-#define EDGE_PROLOGUE                                                  \
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;             \
-  const int bx = blockIdx.x;                                           \
-  const int gg = bx / geo.BPG, jj = bx - gg * geo.BPG;                 \
-  const int slot = t / geo.SW, cl = t - slot * geo.SW;                 \
-  const bool cvalid = cl < geo.NC;                                     \
-  const int tile0 = jj * geo.TPB;                                      \
-  const int tile1 = min(geo.TPG, tile0 + geo.TPB);                     \
-  const long long E = geo.E, NS = geo.NS, NT = geo.NT;                 \
-  const long long cn = (long long)gg * geo.NC + cl;                    \
-  (void)lane; (void)wave; (void)E; (void)NS; (void)NT; (void)cn;
+#define EDGE_PROLOGUE                                                       \
+  const int t = threadIdx.x, lane = t & 63;                                 \
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);                  \
+  const int bx = blockIdx.x;                                                \
+  const int ks = bx % geo.KS, grp = bx / geo.KS;                            \
+  const int fg = grp % geo.NFG, gg = grp / geo.NFG;                         \
+  const int f = fg * 64 + lane;                                             \
+  const bool fvalid = f < geo.NF;                                           \
+  const long long n = (long long)gg * geo.NF + (fvalid ? f : 0);            \
+  const long long nbase = (long long)gg * geo.NF + (long long)fg * 64;      \
+  const int nvalid = min(64, geo.NF - fg * 64);                             \
+  const int c0 = ks * geo.CPS, c1 = min(geo.NC, c0 + geo.CPS);              \
+  const long long E = geo.E, NS = geo.NS, NT = geo.NT;                      \
+  (void)E; (void)NS; (void)NT; (void)n; (void)nbase; (void)nvalid; (void)t;
 
-#define EDGE_TILE                                                      \
-  const int f = tile * geo.FPI + slot;                                 \
-  const bool fvalid = f < geo.NF;                                      \
-  const bool valid = cvalid && fvalid;                                 \
-  const long long n = (long long)gg * geo.NF + (fvalid ? f : 0);       \
-  const long long e = n * geo.NC + cl;                                 \
-  (void)e;
+#define CLASS_LOOP_BEGIN                                                    \
+  for (int c = c0 + wave; c < c1; c += 4) {                                 \
+    const long long cn = (long long)gg * geo.NC + c;                        \
+    const long long e = cn * geo.NF + (fvalid ? f : 0);                     \
+    const long long eu = n * geo.NC + c; /* train.py's fiber-major position */
+
+#define CLASS_LOOP_END }
+
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
 
 struct SoftFloor {
   float r, corr, two_pi, inv_pi;  // r = exp(-1/sharpness) (0 if sharpness == 0)
@@ -83,66 +91,49 @@ __global__ __launch_bounds__(256) void k_loss_fwd(EdgeGeo geo, const float* __re
                                                   float* __restrict__ tt_out,
                                                   float* __restrict__ part) {
   EDGE_PROLOGUE
-  __shared__ float lds[256 * 4];
-  float np = 0.f, wc = 0.f, wm = 0.f, wq = 0.f;
-  const float Ti = cvalid ? ci[cn] : 1.f;
-  for (int tile = tile0; tile < tile1; ++tile) {
-    EDGE_TILE
+  __shared__ float scratch[4 * 64];
+  float ft = 0.f;
+  const float nw = (float)nvalid;
+  CLASS_LOOP_BEGIN
     float x[F];
 #pragma unroll
     for (int k = 0; k < F; ++k) {
-      const float v = valid ? y[(long long)k * E + e] : 0.f;
+      const float v = fvalid ? y[(long long)k * E + e] : 0.f;
       x[k] = sc ? fmaf(v, sc[k], sh[k]) : v;
     }
-    const float noise = noiselevel * (pf_uniform(key, (uint64_t)e) - 0.5f);
+    const float noise = noiselevel * (pf_uniform(key, (uint64_t)eu) - 0.5f);
     EdgeLoss<F> L;
-    L.run(x, Wd1, bd1, Wd2, bd2, scale, Ti, noise, sf);
-    float ft[1] = {valid ? L.tt : 0.f};
-    if (valid) {
-      np += L.gal;
-      wc += 1.f;
-      const float d = L.tt - wm;
-      wm += d / wc;
-      wq = fmaf(d, L.tt - wm, wq);
-      if (tt_out) tt_out[e] = L.tt;
+    L.run(x, Wd1, bd1, Wd2, bd2, scale, ci[cn], noise, sf);
+    const float tt = fvalid ? L.tt : 0.f;
+    ft += tt;
+    if (tt_out && fvalid) tt_out[eu] = L.tt;
+    const float np = wave_sum(fvalid ? L.gal : 0.f);
+    const float mw = wave_sum(tt) / nw;
+    const float dv = fvalid ? tt - mw : 0.f;
+    const float qw = wave_sum(dv * dv);
+    if (lane == 0) {
+      float* o = part + (((size_t)gg * geo.NFG + fg) * geo.NC + c) * 4;
+      o[0] = np; o[1] = nw; o[2] = mw; o[3] = qw;
     }
-    seg_sum<1>(ft, geo.SW, lds);
-    if (cl == 0 && fvalid) fiber_time[n] = ft[0];
-  }
+  CLASS_LOOP_END
+  // fiber time: merge the 4 waves, KS-partial per fiber
   __syncthreads();
-  lds[t * 4 + 0] = np;
-  lds[t * 4 + 1] = wc;
-  lds[t * 4 + 2] = wm;
-  lds[t * 4 + 3] = wq;
+  scratch[wave * 64 + lane] = ft;
   __syncthreads();
-  for (int c = t; c < geo.NC; c += 256) {
-    float P = 0.f, C0 = 0.f, M0 = 0.f, Q0 = 0.f;
-    for (int s = 0; s < geo.FPI; ++s) {
-      const float* q = lds + (s * geo.SW + c) * 4;
-      P += q[0];
-      const float cb = q[1], mb = q[2], qb = q[3];
-      const float tot = C0 + cb;
-      if (tot > 0.f) {
-        const float d = mb - M0;
-        M0 = M0 + d * (cb / tot);
-        Q0 = Q0 + qb + d * d * (C0 * cb / tot);
-      }
-      C0 = tot;
-    }
-    float* o = part + ((size_t)bx * geo.NC + c) * 4;
-    o[0] = P; o[1] = C0; o[2] = M0; o[3] = Q0;
-  }
+  if (t < 64 && t < nvalid)
+    fiber_time[(size_t)ks * NS + nbase + t] =
+        ((scratch[t] + scratch[64 + t]) + scratch[128 + t]) + scratch[192 + t];
 }
 
-__global__ void k_loss_class_reduce(const float* __restrict__ part, int G, int BPG, int NC,
+__global__ void k_loss_class_reduce(const float* __restrict__ part, int G, int NFG, int NC,
                                     int NF, float* __restrict__ n_prime, float* __restrict__ tmean,
                                     float* __restrict__ tvar) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over G*NC
   if (idx >= G * NC) return;
   const int g = idx / NC, c = idx - g * NC;
   double P = 0, C0 = 0, M0 = 0, Q0 = 0;
-  for (int b = 0; b < BPG; ++b) {
-    const float* q = part + (((size_t)g * BPG + b) * NC + c) * 4;
+  for (int b = 0; b < NFG; ++b) {
+    const float* q = part + (((size_t)g * NFG + b) * NC + c) * 4;
     P += q[0];
     const double cb = q[1], mb = q[2], qb = q[3];
     const double tot = C0 + cb;
@@ -247,32 +238,30 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
 #pragma unroll
   for (int j = 0; j <= F; ++j) acc[j] = 0.f;
   const float gs = gscale ? gscale[0] : 1.f;
-  const float Ti = cvalid ? ci[cn] : 1.f;
-  const float Gn_c = cvalid ? Gn[cn] : 0.f, Gv_c = cvalid ? Gv[cn] : 0.f;
-  const float tm_c = cvalid ? tmean[cn] : 0.f;
-  for (int tile = tile0; tile < tile1; ++tile) {
-    EDGE_TILE
+  const float Gf_f = fvalid ? Gf[n] : 0.f;
+  CLASS_LOOP_BEGIN
+    const float Ti = ci[cn], Gn_c = Gn[cn], Gv_c = Gv[cn], tm_c = tmean[cn];
     float x[F + 1];
 #pragma unroll
     for (int k = 0; k < F; ++k) {
-      const float v = valid ? y[(long long)k * E + e] : 0.f;
+      const float v = fvalid ? y[(long long)k * E + e] : 0.f;
       x[k] = sc ? fmaf(v, sc[k], sh[k]) : v;
     }
     x[F] = 1.f;
-    const float noise = noiselevel * (pf_uniform(key, (uint64_t)e) - 0.5f);
+    const float noise = noiselevel * (pf_uniform(key, (uint64_t)eu) - 0.5f);
     EdgeLoss<F> L;
     float xf[F];
 #pragma unroll
     for (int k = 0; k < F; ++k) xf[k] = x[k];
     L.run(xf, Wd1, bd1, Wd2, bd2, scale, Ti, noise, sf);
-    const float g_tt = Gf[n] + Gv_c * (L.tt - tm_c);
+    const float g_tt = Gf_f + Gv_c * (L.tt - tm_c);
     const float g_gal = Gn_c + Ti * g_tt;
     const float mask = L.graw > 0.f ? 1.f : (L.graw == 0.f ? 0.5f : 0.f);
     const float cth = cosf(L.th);
     const float dsf = 1.f + 2.f * (sf.r * cth - sf.r * sf.r) / (1.f - 2.f * sf.r * cth + sf.r * sf.r);
     const float g_time = g_gal * mask * dsf / Ti;
     const float sig = L.pred > 20.f ? 1.f : 1.f / (1.f + expf(-L.pred));
-    const float g_pred = valid ? gs * g_time * scale * sig : 0.f;
+    const float g_pred = fvalid ? gs * g_time * scale * sig : 0.f;
     float gz[F];
 #pragma unroll
     for (int j = 0; j < F; ++j) {
@@ -280,7 +269,7 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
       gz[j] = Wd2[j] * g_pred * dlrelu(L.zd[j]);
     }
     acc[F] += g_pred;
-    if (valid) {
+    if (fvalid) {
 #pragma unroll
       for (int k = 0; k < F; ++k) {
         float s = 0.f;
@@ -290,10 +279,10 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
       }
     }
     wg.stage(region, gz, x, lane);
-    __syncthreads();
+    wave_lds_sync();
     wg.accum(region, lane);
-    __syncthreads();
-  }
+    wave_lds_sync();
+  CLASS_LOOP_END
   wg.block_partial(lds, partW + (size_t)bx * F * (F + 1));
   block_sum<F + 1>(acc, lds + LDS_N);
   if (t <= F) {
@@ -305,8 +294,20 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
 }
 
 // ------------------------------------------------------------ layout
+// Canonical index k = (g*NC + c)*NF + f.  mode 0: user edge id = perm[k];
+// mode 1: user order is train.py's fiber-major (g*NF + f)*NC + c (graph.py /
+// cartesian_prod, train.py:94); mode 2: user order is already canonical.
+__device__ __forceinline__ long long user_index(long long k, int NF, int NC, int mode,
+                                                const int32_t* __restrict__ perm) {
+  if (mode == 2) return k;
+  if (mode == 0) return perm[k];
+  const long long gc = k / NF, f = k - gc * NF;
+  const long long g = gc / NC, c = gc - g * NC;
+  return (g * NF + f) * NC + c;
+}
+
 __global__ void k_layout_init(int32_t* status) {
-  if (threadIdx.x == 0) { status[0] = 1; status[1] = 1; }
+  if (threadIdx.x == 0) { status[0] = 1; status[1] = 1; status[2] = 1; }
 }
 
 __global__ void k_layout_scatter(const int64_t* __restrict__ ei, long long E, int G, int NF, int NC,
@@ -316,43 +317,61 @@ __global__ void k_layout_scatter(const int64_t* __restrict__ ei, long long E, in
   if (e >= E) return;
   const long long NS = (long long)G * NF, NT = (long long)G * NC;
   const long long s = ei[e], tg = ei[E + e];
-  if (s < 0 || s >= NS || tg < 0 || tg >= NT) { atomicAnd(&status[0], 0); atomicAnd(&status[1], 0); return; }
+  if (s < 0 || s >= NS || tg < 0 || tg >= NT) {
+    atomicAnd(&status[0], 0); atomicAnd(&status[1], 0); atomicAnd(&status[2], 0);
+    return;
+  }
   const long long g = s / NF, gt = tg / NC;
-  if (g != gt) { atomicAnd(&status[0], 0); atomicAnd(&status[1], 0); return; }
-  const long long k = s * NC + (tg - gt * NC);
+  if (g != gt) {
+    atomicAnd(&status[0], 0); atomicAnd(&status[1], 0); atomicAnd(&status[2], 0);
+    return;
+  }
+  const long long f = s - g * NF, c = tg - gt * NC;
+  const long long k = (g * NC + c) * NF + f;
   atomicAdd(&cnt[k], 1);
   perm[k] = (int32_t)e;
-  if (k != e) atomicAnd(&status[1], 0);
+  if (e != s * NC + c) atomicAnd(&status[1], 0);
+  if (e != k) atomicAnd(&status[2], 0);
 }
 
 __global__ void k_layout_check(const int32_t* __restrict__ cnt, long long E,
                                int32_t* __restrict__ status) {
   const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= E) return;
-  if (cnt[k] != 1) { atomicAnd(&status[0], 0); atomicAnd(&status[1], 0); }
+  if (cnt[k] != 1) { atomicAnd(&status[0], 0); atomicAnd(&status[1], 0); atomicAnd(&status[2], 0); }
 }
 
-__global__ void k_to_canonical(const float* __restrict__ src, long long E, int F,
-                               const int32_t* __restrict__ perm, float* __restrict__ dst) {
-  const long long ec = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ec >= E) return;
-  const long long es = perm ? perm[ec] : ec;
-  for (int k = 0; k < F; ++k) dst[(long long)k * E + ec] = src[es * F + k];
+__global__ void k_to_canonical(const float* __restrict__ src, long long E, int NF, int NC, int F,
+                               int mode, const int32_t* __restrict__ perm,
+                               float* __restrict__ dst) {
+  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= E) return;
+  const long long eu = user_index(k, NF, NC, mode, perm);
+  for (int j = 0; j < F; ++j) dst[(long long)j * E + k] = src[eu * F + j];
 }
 
 __global__ void k_from_canonical(const float* __restrict__ y, const float* __restrict__ sc,
-                                 const float* __restrict__ sh, long long E, int F,
-                                 const int32_t* __restrict__ perm, int rowmajor,
+                                 const float* __restrict__ sh, long long E, int NF, int NC, int F,
+                                 int mode, const int32_t* __restrict__ perm, int rowmajor,
                                  float* __restrict__ dst) {
-  const long long ec = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ec >= E) return;
-  const long long ed = perm ? perm[ec] : ec;
-  for (int k = 0; k < F; ++k) {
-    float v = y[(long long)k * E + ec];
-    if (sc) v = fmaf(v, sc[k], sh[k]);
-    if (rowmajor) dst[ed * F + k] = v;
-    else dst[(long long)k * E + ed] = v;
+  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= E) return;
+  const long long eu = user_index(k, NF, NC, mode, perm);
+  for (int j = 0; j < F; ++j) {
+    float v = y[(long long)j * E + k];
+    if (sc) v = fmaf(v, sc[j], sh[j]);
+    if (rowmajor) dst[eu * F + j] = v;
+    else dst[(long long)j * E + eu] = v;
   }
+}
+
+__global__ void k_fiber_partial_sum(const float* __restrict__ part, int KS, long long len,
+                                    float* __restrict__ out) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= len) return;
+  float s = 0.f;
+  for (int k = 0; k < KS; ++k) s += part[(size_t)k * len + idx];
+  out[idx] = s;
 }
 
 // ------------------------------------------------------------ host side
@@ -399,18 +418,22 @@ extern "C" int pfsgnn_loss_fwd(int G, int NF, int NC, int F, const float* y, con
              "pfsgnn_loss_fwd", "null");
   const EdgeGeo geo = make_geo(G, NF, NC);
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
-  float* part = w.take((size_t)geo.nblocks * NC * 4);
-  PF_REQUIRE(part, "pfsgnn_loss_fwd", "workspace too small");
+  float* part = w.take((size_t)G * geo.NFG * NC * 4);
+  float* ftp = geo.KS == 1 ? fiber_time : w.take((size_t)geo.KS * geo.NS);
+  PF_REQUIRE(part && ftp, "pfsgnn_loss_fwd", "workspace too small");
   hipStream_t st = as_stream(stream);
   const SoftFloor sf = make_softfloor(sharpness);
   const uint64_t key = noise_key(seed);
   { pf::Timer tm_("loss_fwd", st);
   DISPATCH_F(F, hipLaunchKernelGGL(k_loss_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
                                    sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sf, noiselevel, key,
-                                   fiber_time, tt, part));
+                                   ftp, tt, part));
   tm_.end(); }
+  if (geo.KS > 1)
+    hipLaunchKernelGGL(k_fiber_partial_sum, dim3((unsigned)((geo.NS + 255) / 256)), dim3(256), 0,
+                       st, ftp, geo.KS, geo.NS, fiber_time);
   hipLaunchKernelGGL(k_loss_class_reduce, dim3((G * NC + 255) / 256), dim3(256), 0, st, part, G,
-                     geo.BPG, NC, NF, n_prime, tmean, tvar);
+                     geo.NFG, NC, NF, n_prime, tmean, tvar);
   return pf::check_launch("pfsgnn_loss_fwd");
 }
 
@@ -483,19 +506,23 @@ extern "C" int pfsgnn_layout_analyze(const int64_t* edge_index, long long E, int
   return pf::check_launch("pfsgnn_layout_analyze");
 }
 
-extern "C" int pfsgnn_edges_to_canonical(const float* src, long long E, int F, const int32_t* perm,
-                                         float* dst, void* stream) {
-  PF_REQUIRE(src && dst && E > 0 && F > 0, "pfsgnn_edges_to_canonical", "bad arguments");
+extern "C" int pfsgnn_edges_to_canonical(const float* src, int G, int NF, int NC, int F, int mode,
+                                         const int32_t* perm, float* dst, void* stream) {
+  const long long E = (long long)G * NF * NC;
+  PF_REQUIRE(src && dst && E > 0 && F > 0 && mode >= 0 && mode <= 2 && (mode != 0 || perm),
+             "pfsgnn_edges_to_canonical", "bad arguments");
   hipLaunchKernelGGL(k_to_canonical, dim3((unsigned)((E + 255) / 256)), dim3(256), 0,
-                     as_stream(stream), src, E, F, perm, dst);
+                     as_stream(stream), src, E, NF, NC, F, mode, perm, dst);
   return pf::check_launch("pfsgnn_edges_to_canonical");
 }
 
-extern "C" int pfsgnn_edges_from_canonical(const float* y, const float* sc, const float* sh,
-                                           long long E, int F, const int32_t* perm, int rowmajor,
-                                           float* dst, void* stream) {
-  PF_REQUIRE(y && dst && E > 0 && F > 0, "pfsgnn_edges_from_canonical", "bad arguments");
+extern "C" int pfsgnn_edges_from_canonical(const float* y, const float* sc, const float* sh, int G,
+                                           int NF, int NC, int F, int mode, const int32_t* perm,
+                                           int rowmajor, float* dst, void* stream) {
+  const long long E = (long long)G * NF * NC;
+  PF_REQUIRE(y && dst && E > 0 && F > 0 && mode >= 0 && mode <= 2 && (mode != 0 || perm),
+             "pfsgnn_edges_from_canonical", "bad arguments");
   hipLaunchKernelGGL(k_from_canonical, dim3((unsigned)((E + 255) / 256)), dim3(256), 0,
-                     as_stream(stream), y, sc, sh, E, F, perm, rowmajor, dst);
+                     as_stream(stream), y, sc, sh, E, NF, NC, F, mode, perm, rowmajor, dst);
   return pf::check_launch("pfsgnn_edges_from_canonical");
 }

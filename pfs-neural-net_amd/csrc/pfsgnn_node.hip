@@ -111,23 +111,31 @@ extern "C" const char* pfsgnn_last_error(void) { return pf::g_err.c_str(); }
 extern "C" const char* pfsgnn_version(void) { return "pfsgnn 0.1 gfx950"; }
 
 // ---------------------------------------------------------------- reduce
-__global__ void k_reduce_rows(const float* __restrict__ part, int nb, size_t plen, int ldp,
-                              int rows, int cols, float* __restrict__ out, int ldo, int add,
-                              float scale) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+// One 64-lane wave per output element: lane l sums partials l, l+64, ... in
+// order, then a fixed butterfly -- deterministic, and every lane's loads are
+// independent (no serial chain over the blocks).
+__global__ __launch_bounds__(256) void k_reduce_rows(const float* __restrict__ part, int nb,
+                                                     size_t plen, int ldp, int rows, int cols,
+                                                     float* __restrict__ out, int ldo, int add,
+                                                     float scale) {
+  const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (idx >= rows * cols) return;
   const int r = idx / cols, c = idx - r * cols;
   const float* p = part + (size_t)r * ldp + c;
   float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += p[(size_t)b * plen];
-  float* o = out + (size_t)r * ldo + c;
-  *o = add ? (*o + scale * s) : scale * s;
+  for (int b = lane; b < nb; b += 64) s += p[(size_t)b * plen];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) {
+    float* o = out + (size_t)r * ldo + c;
+    *o = add ? (*o + scale * s) : scale * s;
+  }
 }
 
 void launch_reduce_rows(const float* part, int nb, size_t plen, int ldp, int rows, int cols,
                         float* out, int ldo, int add, float scale, hipStream_t st) {
   const int len = rows * cols;
-  hipLaunchKernelGGL(k_reduce_rows, dim3((len + 255) / 256), dim3(256), 0, st, part, nb, plen, ldp,
+  hipLaunchKernelGGL(k_reduce_rows, dim3((len + 3) / 4), dim3(256), 0, st, part, nb, plen, ldp,
                      rows, cols, out, ldo, add, scale);
 }
 

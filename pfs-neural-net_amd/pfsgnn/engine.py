@@ -301,18 +301,33 @@ class Engine:
         for b in reversed(range(self.B)):
             se, ss, stt, su = ctx["blocks"][b]
             p = f"mpb.{b}."
-            g_xs_new = be.zeros(F, d.NS) if g_xs is None else g_xs.clone()
-            g_xt_new = be.zeros(F, d.NT) if g_xt is None else g_xt.clone()
             g_xs_in, g_xt_in, g_u_in = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
-            if g_u is not None:
-                self.global_bwd(P, Gr, d, p + "global_model.", su, g_u, g_xs_new, g_xt_new, g_u_in)
-            g_hsum = self.target_node_bwd(P, Gr, d, p + "t_model.", stt, g_xt_new, g_xt_in, g_u_in)
-            self.target_edge_bwd(P, Gr, d, p + "t_model.", stt, g_hsum, False, g_xs_new)
-            coef = self.source_node_bwd(P, Gr, d, p + "s_model.", ss, g_xs_new, g_xs_in, g_u_in)
-            Wt1 = P[p + "t_model.node_mlp_1.0.weight"]
+            # gradients that are None are exactly zero: the models whose outputs
+            # feed nothing downstream (the last block's S/T/Global under the
+            # train.py objective) contribute nothing and are skipped
+            live_t = g_u is not None or g_xt is not None
+            live_s = live_t or g_xs is not None
             bnstat = (se["mu1"], se["inv1"]) if self.normed else None
-            g_tot, Sg, Sgx = self.source_edge_bwd(P, Gr, d, p + "s_model.", ss, coef,
-                                                  (stt["Rs"], Wt1, g_hsum), g_xe, bnstat, g_xt_in)
+            if live_s:
+                g_xs_new = be.zeros(F, d.NS) if g_xs is None else g_xs.clone()
+                g_xt_new = be.zeros(F, d.NT) if g_xt is None else g_xt.clone()
+                if g_u is not None:
+                    self.global_bwd(P, Gr, d, p + "global_model.", su, g_u, g_xs_new, g_xt_new,
+                                    g_u_in)
+                tpart = None
+                if live_t:
+                    g_hsum = self.target_node_bwd(P, Gr, d, p + "t_model.", stt, g_xt_new, g_xt_in,
+                                                  g_u_in)
+                    self.target_edge_bwd(P, Gr, d, p + "t_model.", stt, g_hsum, False, g_xs_new)
+                    tpart = (stt["Rs"], P[p + "t_model.node_mlp_1.0.weight"], g_hsum)
+                coef = self.source_node_bwd(P, Gr, d, p + "s_model.", ss, g_xs_new, g_xs_in, g_u_in)
+                g_tot, Sg, Sgx = self.source_edge_bwd(P, Gr, d, p + "s_model.", ss, coef, tpart,
+                                                      g_xe, bnstat, g_xt_in)
+            else:
+                g_tot = be.zeros(F, d.E) if g_xe is None else g_xe
+                Sg = Sgx = None
+                if self.normed:
+                    Sg, Sgx = be.edge_bn_grad_sums(d, g_tot, se["y"], *bnstat)
             g_xe = self.edge_bwd(P, Gr, d, p + "edge_model.", se, g_tot, Sg, Sgx, b > 0,
                                  g_xs_in, g_xt_in, g_u_in)
             g_xs, g_xt, g_u = g_xs_in, g_xt_in, g_u_in

@@ -9,11 +9,14 @@ the import.  Every forward and backward is computed by ``libpfsgnn.so``
 through ``pfsgnn.engine``; PyTorch only allocates, streams and runs autograd's
 bookkeeping.
 
-Edge layout: the kernels run on the canonical fiber-major order of a batch of
-complete bipartite graphs.  ``edge_index`` may list the edges in any order
-(``graphs/graph-0.pt`` does: each fiber's classes come out of an unstable
-argsort); it is validated on the device once (cached per tensor) and mapped
-with a permutation, so results are reported in the caller's edge order.
+Edge layout: the kernels run on the canonical class-major order
+``(g*NC + c)*NF + f`` of a batch of complete bipartite graphs (one wavefront
+lane per fiber, one class per wave iteration; DESIGN.md §Data layout).
+``edge_index`` may list the edges in any order; it is validated on the device
+once (cached per tensor).  train.py's fiber-major order ((g*NF + f)*NC + c,
+train.py:94) is mapped arithmetically; any other order (``graphs/graph-0.pt``:
+each fiber's classes come out of an unstable argsort) through a permutation.
+Results are always reported in the caller's edge order.
 Graphs that are not complete bipartite are rejected loudly.
 
 Batching: G graphs collated PyG-style (``Batch.from_data_list``, increments
@@ -106,8 +109,23 @@ _LAYOUT_CACHE = {}
 _EDGE_CACHE = {}
 
 
+class Layout:
+    """How the caller's edge order maps onto the canonical class-major order
+    (the ``mode`` argument of pfsgnn_edges_{to,from}_canonical)."""
+    PERM, FIBER_MAJOR, CANONICAL = 0, 1, 2
+
+    def __init__(self, G, NF, NC, mode, perm=None, fiber_major=False):
+        self.G, self.NF, self.NC, self.mode = G, NF, NC, mode
+        self.perm = perm if mode == Layout.PERM else None
+        self.fiber_major = fiber_major    # caller order == train.py's positional order
+
+    @property
+    def key(self):
+        return (self.mode, None if self.perm is None else self.perm.data_ptr())
+
+
 def geometry(x_s, x_t, x_u, edge_index, F):
-    """(Dims, perm) for a batch; perm is None when edge_index is already canonical."""
+    """(Dims, Layout) for a batch."""
     G = 1 if x_u is None else int(x_u.size(0))
     S, T = int(x_s.size(0)), int(x_t.size(0))
     if S % G or T % G:
@@ -123,25 +141,27 @@ def geometry(x_s, x_t, x_u, edge_index, F):
                 f"edge_index has {E} edges; the HIP kernels need a batch of complete bipartite "
                 f"graphs (G*NF*NC = {d.E}).  General sparse bipartite graphs are a later row of "
                 "the scope (DESIGN.md §Scope)")
-        perm, complete, identity = backend().layout_analyze(edge_index, G, NF, NC)
+        perm, complete, fm, identity = backend().layout_analyze(edge_index, G, NF, NC)
         if not complete:
             raise NotImplementedError("edge_index is not a complete bipartite batch (some "
                                       "(fiber, class) pair is missing, repeated, or crosses graphs)")
-        hit = None if identity else perm
+        mode = Layout.CANONICAL if identity else (Layout.FIBER_MAJOR if fm else Layout.PERM)
+        hit = Layout(G, NF, NC, mode, perm, fiber_major=fm)
         if len(_LAYOUT_CACHE) > 32:
             _LAYOUT_CACHE.clear()
         _LAYOUT_CACHE[key] = hit
     return d, hit
 
 
-def edges_in(x_e, perm, cache=False):
+def edges_in(x_e, lay, cache=False):
     """User edge features [E, F] -> canonical channel-major [F, E]."""
-    if perm is None and x_e.dtype == torch.float32 and x_e.is_cuda and x_e.t().is_contiguous():
+    if (lay.mode == Layout.CANONICAL and x_e.dtype == torch.float32 and x_e.is_cuda
+            and x_e.t().is_contiguous()):
         return x_e.t()
-    key = (x_e.data_ptr(), x_e._version, tuple(x_e.shape), None if perm is None else perm.data_ptr())
+    key = (x_e.data_ptr(), x_e._version, tuple(x_e.shape), lay.key)
     if cache and key in _EDGE_CACHE:
         return _EDGE_CACHE[key]
-    out = backend().edges_to_canonical(x_e, perm)
+    out = backend().edges_to_canonical(x_e, lay)
     if cache:
         if len(_EDGE_CACHE) > 4:
             _EDGE_CACHE.clear()
@@ -149,30 +169,36 @@ def edges_in(x_e, perm, cache=False):
     return out
 
 
-def edges_out(xe3, perm, d):
+def edges_out(xe3, lay, d):
     """Canonical (y, sc, sh) -> user edge tensor [E, F] in the caller's order."""
     be = backend()
     y, sc, sh = xe3
-    if perm is None:
+    if lay.mode == Layout.CANONICAL:
         return be.edge_apply(d, y, sc, sh).t()
-    return be.edges_from_canonical(y, sc, sh, perm, rowmajor=True)
+    return be.edges_from_canonical(y, sc, sh, lay, rowmajor=True)
 
 
-def grad_edges_in(g, perm):
+def is_zero_grad(g):
+    """The placeholder gradient of a fused consumer that handed its canonical
+    gradient over directly (``train._LossFn``): an expanded zero scalar."""
+    return g is not None and g.dim() == 2 and g.stride() == (0, 0)
+
+
+def grad_edges_in(g, lay):
     """Gradient w.r.t. a user edge tensor [E, F] -> canonical [F, E]."""
-    if g is None:
+    if g is None or is_zero_grad(g):
         return None
-    if perm is None and g.t().is_contiguous():
+    if lay.mode == Layout.CANONICAL and g.t().is_contiguous():
         return g.t()
-    return backend().edges_to_canonical(g.contiguous(), perm)
+    return backend().edges_to_canonical(g.contiguous(), lay)
 
 
-def grad_edges_out(gc, perm):
+def grad_edges_out(gc, lay):
     if gc is None:
         return None
-    if perm is None:
+    if lay.mode == Layout.CANONICAL:
         return gc.t()
-    return backend().edges_from_canonical(gc, None, None, perm, rowmajor=True)
+    return backend().edges_from_canonical(gc, None, None, lay, rowmajor=True)
 
 
 def _cm(x):
@@ -321,36 +347,37 @@ class MLP(_ParamMixin, torch.nn.Sequential):
 
 
 def _graph_of(x_s, x_t, u, edge_index, F):
-    d, perm = geometry(x_s, x_t, u, edge_index, F)
-    return d, perm
+    d, lay = geometry(x_s, x_t, u, edge_index, F)
+    return d, lay
 
 
 class _EdgeFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_s, x_t, edge_attr, u, anchor, module, edge_index):
         F = module.Fdim
-        d, perm = _graph_of(x_s, x_t, u, edge_index, F)
+        d, lay = _graph_of(x_s, x_t, u, edge_index, F)
         eng = _engine_for(F, module.normed)
         P, BN = module._flat_params(), module._bn_buffers()
-        st = eng.edge_fwd(P, BN, d, "", _cm(x_s), _cm(x_t), (edges_in(edge_attr, perm), None, None), _cm(u))
+        st = eng.edge_fwd(P, BN, d, "", _cm(x_s), _cm(x_t), (edges_in(edge_attr, lay), None, None), _cm(u))
         if module.normed:
             module._bump_batches(edge_keys=("norm.",))
-        ctx.pf = (module, d, perm, st)
-        return edges_out((st["y"], st["sc"], st["sh"]), perm, d)
+        ctx.pf = (module, d, lay, st)
+        return edges_out((st["y"], st["sc"], st["sh"]), lay, d)
 
     @staticmethod
     def backward(ctx, g):
-        module, d, perm, st = ctx.pf
+        module, d, lay, st = ctx.pf
         be, F = backend(), module.Fdim
         eng = _engine_for(F, module.normed)
         P, Gr = module._flat_params(), module._flat_grads()
-        gc = grad_edges_in(g, perm).contiguous()
+        gc = grad_edges_in(g, lay)
+        gc = be.zeros(F, d.E) if gc is None else gc.contiguous()
         Sg = Sgx = None
         if module.normed:
             Sg, Sgx = be.edge_bn_grad_sums(d, gc, st["y"], st["mu1"], st["inv1"])
         g_xs, g_xt, g_u = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
         g_xe = eng.edge_bwd(P, Gr, d, "", st, gc, Sg, Sgx, True, g_xs, g_xt, g_u)
-        return g_xs.t(), g_xt.t(), grad_edges_out(g_xe, perm), g_u.t(), None, None, None
+        return g_xs.t(), g_xt.t(), grad_edges_out(g_xe, lay), g_u.t(), None, None, None
 
 
 class EdgeModel(MLP):
@@ -371,25 +398,25 @@ class _SourceFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_s, x_t, edge_attr, u, anchor, module, edge_index):
         F = module.Fdim
-        d, perm = _graph_of(x_s, x_t, u, edge_index, F)
+        d, lay = _graph_of(x_s, x_t, u, edge_index, F)
         eng = _engine_for(F, module.normed)
         P, BN = module._flat_params(), module._bn_buffers()
-        st = eng.source_fwd(P, BN, d, "", _cm(x_s), _cm(x_t), (edges_in(edge_attr, perm), None, None), _cm(u))
+        st = eng.source_fwd(P, BN, d, "", _cm(x_s), _cm(x_t), (edges_in(edge_attr, lay), None, None), _cm(u))
         if module.normed:
             module._bump_batches(node_keys=("norm.",))
-        ctx.pf = (module, d, perm, st)
+        ctx.pf = (module, d, lay, st)
         return st["xs_new"].t()
 
     @staticmethod
     def backward(ctx, g):
-        module, d, perm, st = ctx.pf
+        module, d, lay, st = ctx.pf
         be, F = backend(), module.Fdim
         eng = _engine_for(F, module.normed)
         P, Gr = module._flat_params(), module._flat_grads()
         g_xs, g_xt, g_u = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
         coef = eng.source_node_bwd(P, Gr, d, "", st, g.t().contiguous(), g_xs, g_u)
         g_tot, _, _ = eng.source_edge_bwd(P, Gr, d, "", st, coef, None, None, None, g_xt)
-        return g_xs.t(), g_xt.t(), grad_edges_out(g_tot, perm), g_u.t(), None, None, None
+        return g_xs.t(), g_xt.t(), grad_edges_out(g_tot, lay), g_u.t(), None, None, None
 
 
 class SModel(_ParamMixin, torch.nn.Module):
@@ -413,25 +440,25 @@ class _TargetFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_s, x_t, edge_attr, u, anchor, module, edge_index):
         F = module.Fdim
-        d, perm = _graph_of(x_s, x_t, u, edge_index, F)
+        d, lay = _graph_of(x_s, x_t, u, edge_index, F)
         eng = _engine_for(F, module.normed)
         P, BN = module._flat_params(), module._bn_buffers()
-        st = eng.target_fwd(P, BN, d, "", _cm(x_s), _cm(x_t), (edges_in(edge_attr, perm), None, None), _cm(u))
+        st = eng.target_fwd(P, BN, d, "", _cm(x_s), _cm(x_t), (edges_in(edge_attr, lay), None, None), _cm(u))
         if module.normed:
             module._bump_batches(node_keys=("norm.",))
-        ctx.pf = (module, d, perm, st)
+        ctx.pf = (module, d, lay, st)
         return st["xt_new"].t()
 
     @staticmethod
     def backward(ctx, g):
-        module, d, perm, st = ctx.pf
+        module, d, lay, st = ctx.pf
         be, F = backend(), module.Fdim
         eng = _engine_for(F, module.normed)
         P, Gr = module._flat_params(), module._flat_grads()
         g_xs, g_xt, g_u = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
         g_hsum = eng.target_node_bwd(P, Gr, d, "", st, g.t().contiguous(), g_xt, g_u)
         gxe = eng.target_edge_bwd(P, Gr, d, "", st, g_hsum, True, g_xs)
-        return g_xs.t(), g_xt.t(), grad_edges_out(gxe, perm), g_u.t(), None, None, None
+        return g_xs.t(), g_xt.t(), grad_edges_out(gxe, lay), g_u.t(), None, None, None
 
 
 class TModel(_ParamMixin, torch.nn.Module):
@@ -521,7 +548,8 @@ class _GNNFn(torch.autograd.Function):
     engine's hand-fused block backward (engine.Engine.backward)."""
 
     @staticmethod
-    def forward(ctx, anchor, model, d, perm, xs_in, xt_in, xe_in, u_in):
+    def forward(ctx, anchor, model, d, lay, xs_in, xt_in, xe_in, u_in):
+        ctx.set_materialize_grads(False)      # unused outputs -> None -> dead work skipped
         P, BN = model._flat_params(), model._bn_buffers()
         ectx = model._engine().forward(P, BN, d, xs_in, xt_in, xe_in, u_in)
         if model.normed:
@@ -529,17 +557,23 @@ class _GNNFn(torch.autograd.Function):
                 edge_keys=[f"mpb.{b}.edge_model.norm." for b in range(model.B)],
                 node_keys=[f"mpb.{b}.{m}.norm." for b in range(model.B) for m in ("s_model", "t_model")])
         xs, xt, xe3, u = ectx["out"]
-        ctx.pf = (model, d, perm, ectx)
-        model._pf_last = xe3
-        x_e = edges_out(xe3, perm, d)
+        ctx.pf = (model, d, lay, ectx)
+        model._pf_last = (xe3, ectx)
+        x_e = edges_out(xe3, lay, d)
         return xs.t(), xt.t(), x_e, u.t()
 
     @staticmethod
     def backward(ctx, g_xs, g_xt, g_xe, g_u):
-        model, d, perm, ectx = ctx.pf
+        model, d, lay, ectx = ctx.pf
         P, Gr = model._flat_params(), model._flat_grads()
         cm = (lambda g: None if g is None else g.t().contiguous())
-        model._engine().backward(P, Gr, ectx, grad_edges_in(g_xe, perm), cm(g_xs), cm(g_xt), cm(g_u))
+        gc = grad_edges_in(g_xe, lay)
+        # a fused consumer of x_e (train._LossFn) hands its gradient over in the
+        # canonical order instead of round-tripping it through the caller's order
+        handed = ectx.pop("g_xe_canonical", None)
+        if handed is not None:
+            gc = handed if gc is None else gc + handed
+        model._engine().backward(P, Gr, ectx, gc, cm(g_xs), cm(g_xt), cm(g_u))
         return (None,) * 8
 
 
@@ -568,16 +602,17 @@ class GNN(_FlatMixin, torch.nn.Module):
             if t is not None and t.requires_grad:
                 raise NotImplementedError("gradients w.r.t. the graph inputs are not computed")
         self._flat_sync()
-        d, perm = geometry(graph.x_s, graph.x_t, graph.x_u, graph.edge_index, self.Fdim)
-        xe_in = edges_in(graph.x_e, perm, cache=True)
+        d, lay = geometry(graph.x_s, graph.x_t, graph.x_u, graph.edge_index, self.Fdim)
+        xe_in = edges_in(graph.x_e, lay, cache=True)
         anchor = self.encoder_s[0].weight
-        xs, xt, xe, u = _GNNFn.apply(anchor, self, d, perm, _cm(graph.x_s), _cm(graph.x_t),
+        xs, xt, xe, u = _GNNFn.apply(anchor, self, d, lay, _cm(graph.x_s), _cm(graph.x_t),
                                      xe_in, _cm(graph.x_u))
         out = BipartiteData.__new__(BipartiteData)
         out.edge_index, out.x_s, out.x_t, out.x_e, out.x_u = graph.edge_index, xs, xt, xe, u
         out.num_nodes = xt.size(0)
         # lets train.loss_function fuse on the lazy final edge state (y, sc, sh)
-        out._pf = (self, d, perm, xe, self.__dict__.pop("_pf_last"))
+        xe3, ectx = self.__dict__.pop("_pf_last")
+        out._pf = (self, d, lay, xe, xe3, ectx)
         return out
 
     def edge_prediction(self, x_e, scale=1):

@@ -50,7 +50,7 @@ _SIGS = {
     "pfsgnn_bn2_bwd_coef": ([P, P, P, P, P, I, LL, FL, P, P, P, P, P, P], I),
     "pfsgnn_moment_coef": ([P, P, I, I, I, P, P], I),
     "pfsgnn_edge_mlp_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
-    "pfsgnn_source_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P], I),
+    "pfsgnn_source_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_target_fwd": ([I, I, I, I, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_target_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_source_bwd": ([I, I, I, I] + [P] * 22 + [P, SZ, P], I),
@@ -61,8 +61,8 @@ _SIGS = {
     "pfsgnn_loss_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, FL, FL, ULL, P, P, P, P, P,
                          P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_layout_analyze": ([P, LL, I, I, I, P, P, P, SZ, P], I),
-    "pfsgnn_edges_to_canonical": ([P, LL, I, P, P, P], I),
-    "pfsgnn_edges_from_canonical": ([P, P, P, LL, I, P, I, P, P], I),
+    "pfsgnn_edges_to_canonical": ([P, I, I, I, I, I, P, P, P], I),
+    "pfsgnn_edges_from_canonical": ([P, P, P, I, I, I, I, I, P, I, P, P], I),
     "pfsgnn_adam": ([P, P, P, P, LL, I, FL, FL, FL, FL, FL, P], I),
 }
 
@@ -303,9 +303,10 @@ class HipBackend:
     def source_fwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, hs_out):
         mom = self.empty(4, 2 * d.F, d.NS)
         self._chk(y, Qt, Ws1, Ws2, bs2, hs_out)
+        ws, wsb = self._wsargs(d)
         _call("pfsgnn_source_fwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
               Qt.data_ptr(), Ws1.data_ptr(), Ws2.data_ptr(), bs2.data_ptr(), mom.data_ptr(),
-              hs_out.data_ptr(), _stream())
+              hs_out.data_ptr(), ws, wsb, _stream())
         return mom
 
     def target_fwd(self, d, y, sc, sh, Rs, Wt1):
@@ -369,8 +370,8 @@ class HipBackend:
 
     def edge_apply(self, d, y, sc, sh):
         out = self.empty(d.F, d.E)
-        _call("pfsgnn_edges_from_canonical", y.data_ptr(), _ptr(sc), _ptr(sh), d.E, d.F, None, 0,
-              out.data_ptr(), _stream())
+        _call("pfsgnn_edges_from_canonical", y.data_ptr(), _ptr(sc), _ptr(sh), d.G, d.NF, d.NC,
+              d.F, 2, None, 0, out.data_ptr(), _stream())
         return out
 
     # ------------------------------------------------------------ loss
@@ -419,29 +420,32 @@ class HipBackend:
 
     # ------------------------------------------------------------ layout / optim
     def layout_analyze(self, edge_index, G, NF, NC):
+        """-> (perm [E] int32, complete, caller order is fiber-major, caller order is canonical)."""
         E = edge_index.shape[1]
         ei = edge_index.to(device=self.device, dtype=torch.int64).contiguous()
         perm = torch.empty(E, dtype=torch.int32, device=self.device)
-        status = torch.empty(2, dtype=torch.int32, device=self.device)
+        status = torch.empty(3, dtype=torch.int32, device=self.device)
         ws = torch.empty(max(4 * E, 256), dtype=torch.uint8, device=self.device)
         _call("pfsgnn_layout_analyze", ei.data_ptr(), E, G, NF, NC, perm.data_ptr(),
               status.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
         st = status.cpu().tolist()
-        return perm, bool(st[0]), bool(st[1])
+        return perm, bool(st[0]), bool(st[1]), bool(st[2])
 
-    def edges_to_canonical(self, x, perm=None):
+    def edges_to_canonical(self, x, lay):
+        """Caller-order [E, F] -> canonical channel-major [F, E]; ``lay`` carries
+        (G, NF, NC, mode, perm) (pfsgnn.gnn.Layout)."""
         E, F = x.shape
         x = x.to(device=self.device, dtype=torch.float32).contiguous()
         out = self.empty(F, E)
-        _call("pfsgnn_edges_to_canonical", x.data_ptr(), E, F, _ptr(perm), out.data_ptr(),
-              _stream())
+        _call("pfsgnn_edges_to_canonical", x.data_ptr(), lay.G, lay.NF, lay.NC, F, lay.mode,
+              _ptr(lay.perm), out.data_ptr(), _stream())
         return out
 
-    def edges_from_canonical(self, y, sc, sh, perm=None, rowmajor=True):
+    def edges_from_canonical(self, y, sc, sh, lay, rowmajor=True):
         F, E = y.shape
         out = self.empty(E, F) if rowmajor else self.empty(F, E)
-        _call("pfsgnn_edges_from_canonical", y.data_ptr(), _ptr(sc), _ptr(sh), E, F, _ptr(perm),
-              int(rowmajor), out.data_ptr(), _stream())
+        _call("pfsgnn_edges_from_canonical", y.data_ptr(), _ptr(sc), _ptr(sh), lay.G, lay.NF,
+              lay.NC, F, lay.mode, _ptr(lay.perm), int(rowmajor), out.data_ptr(), _stream())
         return out
 
     def adam(self, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay):

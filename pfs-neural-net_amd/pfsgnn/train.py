@@ -23,7 +23,7 @@ import torch
 
 from . import config
 from .engine import Dims
-from .gnn import GNN, BipartiteData, backend, grad_edges_out
+from .gnn import GNN, BipartiteData, backend
 
 _SEED_SPACE = (1 << 62)
 
@@ -46,7 +46,7 @@ def softfloor(x, sharpness=20, noiselevel=0.3):
 
 class _LossFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x_e, anchor, model, d, perm, xe3, ci, sharpness, seed, pclass, pfiber,
+    def forward(ctx, x_e, anchor, model, d, ectx, xe3, ci, sharpness, seed, pclass, pfiber,
                 want_time):
         eng = model._engine()
         P = model._flat_params()
@@ -54,7 +54,7 @@ class _LossFn(torch.autograd.Function):
                                             pfiber=pfiber, total_time=float(config.TOTAL_TIME),
                                             nfields=float(config.NFIELDS), wutils=config.wutils,
                                             wvar=config.wvar, want_time=want_time)
-        ctx.pf = (model, d, perm, lctx)
+        ctx.pf = (model, d, ectx, lctx)
         outs = (diag["utils"], diag["n_prime"], diag["fiber_time"], diag["variance"])
         ctx.mark_non_differentiable(*outs)
         if diag["time"] is not None:
@@ -63,11 +63,15 @@ class _LossFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_loss, *unused):
-        model, d, perm, lctx = ctx.pf
+        model, d, ectx, lctx = ctx.pf
         eng = model._engine()
         P, Gr = model._flat_params(), model._flat_grads()
         gc = eng.loss_backward(P, Gr, lctx, gscale=g_loss)
-        return (grad_edges_out(gc, perm),) + (None,) * 11
+        # hand the canonical [F, E] gradient straight to the GNN's backward
+        # (gnn._GNNFn.backward); autograd sees a stride-0 zero placeholder
+        prev = ectx.get("g_xe_canonical")
+        ectx["g_xe_canonical"] = gc if prev is None else prev + gc
+        return (gc.new_zeros(()).expand(d.E, d.F),) + (None,) * 11
 
 
 def _class_info_cm(class_info, d):
@@ -89,16 +93,16 @@ def loss_function(graph, class_info, pclass=0.1, pfiber=1.0, sharpness=0.5, fina
     if pf is None or pf[3] is not graph.x_e:
         raise NotImplementedError("loss_function needs the BipartiteData returned by "
                                   "pfsgnn.GNN.forward (the fused loss reads its edge state)")
-    model, d, perm, x_e, xe3 = pf
+    model, d, lay, x_e, xe3, ectx = pf
     if gnn is not None and gnn is not model:
         raise ValueError("graph was produced by a different GNN than `gnn`")
-    if perm is not None:
+    if not lay.fiber_major:
         raise NotImplementedError("train.py's objective indexes edges by position "
                                   "(train.py:40, :67): it needs the fiber-major edge order")
     ci = _class_info_cm(class_info, d)
     if seed is None:
         seed = draw_seed()
-    outs = _LossFn.apply(x_e, model.encoder_s[0].weight, model, d, perm, xe3, ci, float(sharpness),
+    outs = _LossFn.apply(x_e, model.encoder_s[0].weight, model, d, ectx, xe3, ci, float(sharpness),
                          int(seed), float(pclass), float(pfiber), bool(finaloutput))
     loss, utils_g, n_prime, fiber_time, variance = outs[:5]
     if not finaloutput:

@@ -10,8 +10,10 @@ product backend is chosen explicitly and only ``HipBackend`` exists there.
 
 Layouts (see DESIGN.md §Data layout):
 * node tensors are channel-major ``[C, N]``;
-* edge tensors are channel-major ``[C, E]`` in the canonical fiber-major
-  order ``e = (g*NF + f)*NC + c``;
+* edge tensors are channel-major ``[C, E]`` in the canonical class-major
+  order ``e = (g*NC + c)*NF + f`` (train.py's own edge order -- fiber-major
+  ``(g*NF + f)*NC + c`` -- is only seen at the boundary: the softfloor noise
+  is drawn per fiber-major position and ``tt`` is returned in it);
 * weights are torch ``Linear`` matrices ``[out, in]``; an op that uses a
   column block of a weight takes ``(W, col0, ncol)``.
 """
@@ -40,9 +42,22 @@ class Dims:
 
 def _edge_index(d, device):
     e = torch.arange(d.E, device=device)
-    fib = e // d.NC
-    cls = (e // (d.NF * d.NC)) * d.NC + e % d.NC
+    cls = e // d.NF
+    fib = (cls // d.NC) * d.NF + e % d.NF
     return fib, cls
+
+
+def _user_index(d, device):
+    """train.py's fiber-major position of each canonical edge."""
+    fib, cls = _edge_index(d, device)
+    return fib * d.NC + cls % d.NC
+
+
+def _seg(x, idx, n):
+    """Segment sum of [C, E] (or [E]) over edge -> node index."""
+    if x.dim() == 1:
+        return torch.zeros(n, dtype=x.dtype, device=x.device).index_add_(0, idx, x)
+    return torch.zeros(x.shape[0], n, dtype=x.dtype, device=x.device).index_add_(1, idx, x)
 
 
 def _aff(x, sc, sh):
@@ -221,12 +236,11 @@ class EmuBackend:
         zs = Qt[:, cls] + Ws1[:, F:2 * F] @ x
         m = Ws2 @ lrelu(zs) + bs2[:, None]
         C = 2 * F
-        mm = m.reshape(C, d.NS, d.NC)
-        mean = mm.mean(2)
-        dd = mm - mean[:, :, None]
-        c2 = (dd ** 2).mean(2)
-        c3 = (dd ** 3).mean(2)
-        c4 = (dd ** 4).mean(2)
+        mean = _seg(m, fib, d.NS) / d.NC
+        dd = m - mean[:, fib]
+        c2 = _seg(dd ** 2, fib, d.NS) / d.NC
+        c3 = _seg(dd ** 3, fib, d.NS) / d.NC
+        c4 = _seg(dd ** 4, fib, d.NS) / d.NC
         var = torch.where(c2 > 0, c2, 0.01 * c2)
         std = torch.sqrt(var + 1e-6)
         hs_out[0:C] = mean
@@ -241,8 +255,7 @@ class EmuBackend:
         x = _aff(y, sc, sh)
         zt = Rs[:, fib] + Wt1[:, F:2 * F] @ x
         at = lrelu(zt)
-        C = 2 * F
-        return at.reshape(C, d.G, d.NF, d.NC).sum(2).reshape(C, d.NT)
+        return _seg(at, cls, d.NT)
 
     def target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False):
         fib, cls = _edge_index(d, y.device)
@@ -250,7 +263,7 @@ class EmuBackend:
         x = _aff(y, sc, sh)
         zt = Rs[:, fib] + Wt1[:, F:2 * F] @ x
         gz = g_hsum[:, cls] * dlrelu(zt)
-        GzT = gz.reshape(2 * F, d.NS, d.NC).sum(2)
+        GzT = _seg(gz, fib, d.NS)
         dWt1[:, F:2 * F] += gz @ x.t()
         gxe = Wt1[:, F:2 * F].t() @ gz if want_gxe else None
         return GzT, gxe
@@ -272,7 +285,7 @@ class EmuBackend:
         gz = (Ws2.t() @ gm) * dlrelu(zs)
         dWs1[:, F:2 * F] += gz @ x.t()
         g = Ws1[:, F:2 * F].t() @ gz
-        GzS = gz.reshape(2 * F, d.G, d.NF, d.NC).sum(2).reshape(2 * F, d.NT)
+        GzS = _seg(gz, cls, d.NT)
         if tpart is not None:
             Rs, Wt1, g_hsum = tpart
             zt = Rs[:, fib] + Wt1[:, F:2 * F] @ x
@@ -304,8 +317,8 @@ class EmuBackend:
         db2 += gy.sum(1)
         gz = (W2.t() @ gy) * dlrelu(z1)
         dW1[:, 2 * F:3 * F] += gz @ x.t()
-        GzEs = gz.reshape(4 * F, d.NS, d.NC).sum(2)
-        GzEt = gz.reshape(4 * F, d.G, d.NF, d.NC).sum(2).reshape(4 * F, d.NT)
+        GzEs = _seg(gz, fib, d.NS)
+        GzEt = _seg(gz, cls, d.NT)
         gxe = W1[:, 2 * F:3 * F].t() @ gz if want_gxe else None
         return gxe, GzEs, GzEt
 
@@ -319,7 +332,8 @@ class EmuBackend:
         uniforms of softfloor's noise.  Returns n_prime [NT], fiber_time [NS],
         tt_mean [NT], tt_var [NT] (unbiased over fibers), tt [E]."""
         fib, cls = _edge_index(d, y.device)
-        uni = self.noise_uniform(seed, d.E)
+        eu = _user_index(d, y.device)
+        uni = self.noise_uniform(seed, d.E)[eu]
         x = _aff(y, sc, sh)
         zd = Wd1 @ x + bd1[:, None]
         pred = (Wd2 @ lrelu(zd) + bd2[:, None])[0]
@@ -331,17 +345,20 @@ class EmuBackend:
         gal = v + (torch.atan(r * torch.sin(th) / (1 - r * torch.cos(th))) - math.atan(r / (1 - r))) / math.pi
         gal = torch.clamp(gal, min=0.0)
         tt = gal * Ti
-        n_prime = gal.reshape(d.G, d.NF, d.NC).sum(1).reshape(d.NT)
-        fiber_time = tt.reshape(d.NS, d.NC).sum(1)
-        T3 = tt.reshape(d.G, d.NF, d.NC)
-        tmean = T3.mean(1)
-        tvar = ((T3 - tmean[:, None, :]) ** 2).sum(1) / (d.NF - 1)
-        return n_prime, fiber_time, tmean.reshape(d.NT), tvar.reshape(d.NT), (tt if want_time else None)
+        n_prime = _seg(gal, cls, d.NT)
+        fiber_time = _seg(tt, fib, d.NS)
+        tmean = _seg(tt, cls, d.NT) / d.NF
+        tvar = _seg((tt - tmean[cls]) ** 2, cls, d.NT) / (d.NF - 1)
+        tt_user = None
+        if want_time:
+            tt_user = torch.empty_like(tt)
+            tt_user[eu] = tt
+        return n_prime, fiber_time, tmean, tvar, tt_user
 
     def loss_bwd(self, d, y, sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sharpness, noiselevel, seed,
                  Gn, Gf, Gv, tmean, gscale, dWd1, dbd1, dWd2, dbd2):
         fib, cls = _edge_index(d, y.device)
-        uni = self.noise_uniform(seed, d.E)
+        uni = self.noise_uniform(seed, d.E)[_user_index(d, y.device)]
         Gn, Gf, Gv = Gn * gscale, Gf * gscale, Gv * gscale
         x = _aff(y, sc, sh)
         zd = Wd1 @ x + bd1[:, None]

@@ -6,10 +6,24 @@ from oracle.ref_gnn import GNN as OracleGNN, Graph as OracleGraph
 
 
 def canonical_edges(G, NF, NC):
+    """train.py's fiber-major edge order (g*NF + f)*NC + c (train.py:94, batched)."""
     e = torch.arange(G * NF * NC)
     src = e // NC
     tgt = (e // (NF * NC)) * NC + e % NC
     return torch.stack([src, tgt])
+
+
+def to_canonical(x, G, NF, NC):
+    """Fiber-major [E, F] edge tensor -> the kernels' class-major channel-major [F, E]
+    (canonical e = (g*NC + c)*NF + f)."""
+    F = x.shape[1]
+    return x.reshape(G, NF, NC, F).permute(3, 0, 2, 1).reshape(F, -1).contiguous()
+
+
+def from_canonical(xc, G, NF, NC):
+    """Inverse of to_canonical."""
+    F = xc.shape[0]
+    return xc.reshape(F, G, NC, NF).permute(1, 3, 2, 0).reshape(-1, F).contiguous()
 
 
 def make_problem(G, NF, NC, F=10, B=2, Fs=1, Ft=2, T=12, seed=0, dtype=torch.float64, normed=True):

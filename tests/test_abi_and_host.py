@@ -1,0 +1,89 @@
+"""CPU tests: the C ABI library loads and exports every symbol include/pfsgnn.h
+declares (no compute calls -- there is no GPU here), the host-side layout /
+batching / parameter logic, and the fail-loudly behaviour without a GPU."""
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "pfs-neural-net_amd")
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "pfsgnn.h")).read()
+    return sorted(set(re.findall(r"\b(pfsgnn_\w+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    so = os.path.join(PKG, "pfsgnn", "libpfsgnn.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-C", PKG, "-j8"], check=True, capture_output=True)
+    from pfsgnn import native
+    return native.lib()
+
+
+def test_library_exports_every_header_symbol(lib):
+    from pfsgnn import native
+    funcs = header_functions()
+    assert len(funcs) >= 30
+    for f in funcs:
+        assert hasattr(lib, f), f"libpfsgnn.so does not export {f}"
+        assert f in native._SIGS, f"native.py binds no signature for {f}"
+    assert lib.pfsgnn_version().decode().startswith("pfsgnn")
+
+
+def test_library_is_gfx950_code_object(lib):
+    so = os.path.join(PKG, "pfsgnn", "libpfsgnn.so")
+    blob = open(so, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob or b"gfx950" in blob
+
+
+def test_workspace_query_is_host_only(lib):
+    b = lib.pfsgnn_workspace_bytes(16, 2394, 128, 10)
+    assert 1 << 20 < b < 1 << 31
+
+
+def test_no_gpu_fails_loudly():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import pfsgnn
+    with pytest.raises(pfsgnn.NativeUnavailable):
+        pfsgnn.HipBackend()
+
+
+def test_batch_collation_follows_inc(monkeypatch):
+    import pfsgnn
+    from pfsgnn import config
+    monkeypatch.setattr(config, "device", torch.device("cpu"))
+    gs = []
+    for NF, NC in [(3, 2), (3, 2)]:
+        e = torch.arange(NF * NC)
+        ei = torch.stack([e // NC, e % NC])
+        gs.append(pfsgnn.BipartiteData(ei, torch.zeros(NF, 1), torch.zeros(NC, 2), torch.zeros(NF * NC, 4),
+                                       torch.zeros(1, 4)))
+    b = pfsgnn.Batch.from_data_list(gs)
+    assert b.edge_index[:, 6].tolist() == [3, 2]      # shifted by (x_s rows, x_t rows)
+    assert b.num_graphs == 2 and b.x_s.shape == (6, 1) and b.x_t.shape == (4, 2)
+    from harness import canonical_edges
+    assert torch.equal(b.edge_index, canonical_edges(2, 3, 2))
+
+
+def test_engine_param_order_is_reference_order():
+    from pfsgnn.engine import param_names
+    from oracle.ref_gnn import GNN
+    for B in (1, 3):
+        for normed in (True, False):
+            m = GNN(B=B, Fdim=10, T=12, F_s=1, F_t=2, normed=normed)
+            assert [n for n, _ in m.named_parameters()] == param_names(B, normed)
+
+
+def test_noise_reference_is_uniform():
+    from noise_ref import uniform_numpy
+    u = uniform_numpy(7, 200000)
+    assert u.min() >= 0.0 and u.max() < 1.0
+    assert abs(u.mean() - 0.5) < 0.005 and abs(u.var() - 1 / 12) < 0.002
+    assert (uniform_numpy(7, 10) == u[:10]).all() and (uniform_numpy(8, 10) != u[:10]).any()

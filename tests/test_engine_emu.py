@@ -12,7 +12,7 @@ import pytest
 import torch
 
 from emu_backend import EmuBackend, Dims
-from harness import make_problem
+from harness import from_canonical, make_problem, to_canonical
 from noise_ref import uniform_numpy
 from oracle.ref_train import loss_function as oracle_loss
 from pfsgnn.engine import Engine, param_names
@@ -36,7 +36,7 @@ def run_pair(G, NF, NC, F=10, B=2, normed=True, sharp=12.0, seed=0):
     BN = {k: v.clone() for k, v in model.state_dict().items() if "running" in k}
     d = Dims(G, NF, NC, F)
     ctx = eng.forward(P, BN, d, graph.x_s.t().contiguous(), graph.x_t.t().contiguous(),
-                      graph.x_e.t().contiguous(), graph.x_u.t().contiguous())
+                      to_canonical(graph.x_e, G, NF, NC), graph.x_u.t().contiguous())
     loss_e, diag_e, lctx = eng.loss_forward(P, d, ctx["out"][2], graph.x_t.t().contiguous(), sharp,
                                            1234, pclass=0.1, pfiber=0.1)
     g_next = eng.loss_backward(P, Gr, lctx)
@@ -51,7 +51,7 @@ def test_engine_matches_oracle_fp64(G, NF, NC, B):
     xe = be.edge_apply(ctx["d"], *xe3)
     assert torch.allclose(xs.t(), out.x_s, rtol=1e-9, atol=1e-9)
     assert torch.allclose(xt.t(), out.x_t, rtol=1e-9, atol=1e-9)
-    assert torch.allclose(xe.t(), out.x_e, rtol=1e-9, atol=1e-9)
+    assert torch.allclose(from_canonical(xe, G, NF, NC), out.x_e, rtol=1e-9, atol=1e-9)
     assert torch.allclose(u.t(), out.x_u, rtol=1e-9, atol=1e-9)
     assert torch.allclose(loss_e, loss_o, rtol=1e-10, atol=1e-8)
     names = param_names(B)

@@ -247,3 +247,50 @@ def test_adam_matches_torch(hb):
         o2.step()
     for p, q in zip(ps, qs):
         assert torch.allclose(p, q, rtol=1e-6, atol=1e-7), (p - q).abs().max()
+
+
+@pytest.mark.parametrize("G,NF,NC", [(1, 37, 12), (3, 21, 5), (2, 7, 200)])
+def test_layout_modes(hb, G, NF, NC):
+    """layout_analyze classifies the caller's edge order and the three conversion
+    modes (permutation / fiber-major arithmetic / identity) agree with the
+    harness's explicit index maps, bit-exactly."""
+    from harness import canonical_edges, from_canonical, to_canonical
+    from pfsgnn.gnn import Layout
+    F = 10
+    E = G * NF * NC
+    gen = torch.Generator().manual_seed(NF + NC)
+    x = torch.randn(E, F, generator=gen)
+    ei_fm = canonical_edges(G, NF, NC)
+    xc_ref = to_canonical(x, G, NF, NC)
+    # fiber-major (train.py's order)
+    perm, complete, fm, ident = hb.layout_analyze(ei_fm.cuda(), G, NF, NC)
+    assert complete and fm and not ident
+    for lay in (Layout(G, NF, NC, Layout.FIBER_MAJOR), Layout(G, NF, NC, Layout.PERM, perm)):
+        xc = hb.edges_to_canonical(x.cuda(), lay)
+        assert torch.equal(xc.cpu(), xc_ref)
+        back = hb.edges_from_canonical(xc, None, None, lay, rowmajor=True)
+        assert torch.equal(back.cpu(), x)
+    # arbitrary order
+    p = torch.randperm(E, generator=gen)
+    perm, complete, fm, ident = hb.layout_analyze(ei_fm[:, p].contiguous().cuda(), G, NF, NC)
+    assert complete and not fm and not ident
+    lay = Layout(G, NF, NC, Layout.PERM, perm)
+    xc = hb.edges_to_canonical(x[p].contiguous().cuda(), lay)
+    assert torch.equal(xc.cpu(), xc_ref)
+    sc, sh = torch.rand(F, generator=gen) + 0.5, torch.randn(F, generator=gen)
+    out = hb.edges_from_canonical(xc, sc.cuda(), sh.cuda(), lay, rowmajor=True).cpu()
+    assert torch.allclose(out, (x * sc + sh)[p], rtol=1e-6, atol=1e-6)
+    # canonical (class-major) order
+    ei_cm = ei_fm.t().reshape(G, NF, NC, 2).permute(0, 2, 1, 3).reshape(E, 2).t().contiguous()
+    perm, complete, fm, ident = hb.layout_analyze(ei_cm.cuda(), G, NF, NC)
+    assert complete and ident
+    assert torch.equal(perm.cpu(), torch.arange(E, dtype=torch.int32))
+    # incomplete / duplicated / cross-graph
+    bad = ei_fm.clone()
+    bad[1, 0] = bad[1, 1]
+    assert not hb.layout_analyze(bad.cuda(), G, NF, NC)[1]
+    if G > 1:
+        bad = ei_fm.clone()
+        bad[1, 0] = NC * (G - 1)
+        assert not hb.layout_analyze(bad.cuda(), G, NF, NC)[1]
+    assert torch.equal(from_canonical(xc_ref, G, NF, NC), x)
