@@ -9,6 +9,18 @@
 #define PF_LEAKY 0.1f
 #define PF_BLOCK 256
 
+// Wave-uniform read-only table (weights, per-class node rows) seen through the
+// constant address space, behind an opaque copy the compiler may not hoist:
+// reads inside a loop become s_load (scalar-cache hits) next to their use,
+// instead of hundreds of loop-invariant values hoisted into more SGPRs than
+// exist and spilled to VGPR lanes.
+typedef const float __attribute__((address_space(4)))* pf_cptr;
+__device__ __forceinline__ pf_cptr pf_fresh(const float* p) {
+  pf_cptr q = (pf_cptr)p;
+  asm volatile("" : "+s"(q));
+  return q;
+}
+
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------ errors
@@ -50,12 +62,15 @@ struct EdgeGeo {
   long long E, NS, NT;
 };
 
-static inline EdgeGeo make_geo(int G, int NF, int NC) {
+// Blocks of 4 waves on 64 fibers; KS class splits bring the grid to about
+// `target` blocks (2048 = 8 blocks of 4 waves per CU on 256 CUs: enough
+// resident waves to hide the scalar-weight and HBM latencies).
+static constexpr int PF_TARGET_BLOCKS = 2048;
+static inline EdgeGeo make_geo(int G, int NF, int NC, int target = PF_TARGET_BLOCKS) {
   EdgeGeo g;
   g.G = G; g.NF = NF; g.NC = NC;
   g.NFG = (NF + 63) / 64;
   const int groups = G * g.NFG;
-  const int target = 512;
   int ks = (target + groups - 1) / groups;
   const int maxks = (NC + 3) / 4;
   if (ks > maxks) ks = maxks;

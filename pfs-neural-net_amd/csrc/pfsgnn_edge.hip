@@ -34,12 +34,15 @@
   const int nvalid = min(64, geo.NF - fg * 64);                             \
   const int c0 = ks * geo.CPS, c1 = min(geo.NC, c0 + geo.CPS);              \
   const long long E = geo.E, NS = geo.NS, NT = geo.NT;                      \
-  (void)E; (void)NS; (void)NT; (void)n; (void)nbase; (void)nvalid;
+  const uint32_t RB = (uint32_t)geo.E * 4u; /* edge-tensor row bytes */      \
+  (void)E; (void)NS; (void)NT; (void)n; (void)nbase; (void)nvalid; (void)RB;
 
 #define CLASS_LOOP_BEGIN                                                    \
   for (int c = c0 + wave; c < c1; c += 4) {                                 \
     const long long cn = (long long)gg * geo.NC + c;                        \
-    const long long e = cn * geo.NF + (fvalid ? f : 0);
+    const long long e = cn * geo.NF + (fvalid ? f : 0);                     \
+    const uint32_t eo = (uint32_t)e * 4u; /* byte offset in a row */        \
+    (void)eo;
 
 #define CLASS_LOOP_END }
 
@@ -49,16 +52,37 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// Edge-tensor element at byte offset `off` (< 2^32: check_dims bounds C*E*4):
+// base pointer in SGPRs + one 32-bit VGPR offset -> global_load saddr form.
+__device__ __forceinline__ float ldE(const float* p, uint32_t off) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(p) + off);
+}
+__device__ __forceinline__ void stE(float* p, uint32_t off, float v) {
+  *reinterpret_cast<float*>(reinterpret_cast<char*>(p) + off) = v;
+}
+
+__device__ __forceinline__ float ldEz(const float* p, uint32_t off, bool valid) {
+  const float v = ldE(p, off);
+  return valid ? v : 0.f;
+}
+
+// x = (sc*src + sh) of one edge; every lane loads (invalid lanes alias fiber 0
+// of the graph, always in bounds) and invalid lanes are zeroed after.
 template <int F>
 __device__ __forceinline__ void load_x(float (&x)[F], const float* __restrict__ src,
-                                       const float* __restrict__ sc, const float* __restrict__ sh,
-                                       long long e, long long E, bool valid) {
+                                       const float* __restrict__ sc,
+                                       const float* __restrict__ sh, uint32_t eo, uint32_t RB,
+                                       bool valid) {
+  float v[F];
 #pragma unroll
-  for (int k = 0; k < F; ++k) {
-    float v = valid ? src[(long long)k * E + e] : 0.f;
-    if (sc) v = valid ? fmaf(v, sc[k], sh[k]) : 0.f;
-    x[k] = v;
+  for (int k = 0; k < F; ++k) v[k] = ldE(src, eo + (uint32_t)k * RB);
+  if (sc) {
+    pf_cptr a = pf_fresh(sc), b = pf_fresh(sh);
+#pragma unroll
+    for (int k = 0; k < F; ++k) v[k] = fmaf(v[k], a[k], b[k]);
   }
+#pragma unroll
+  for (int k = 0; k < F; ++k) x[k] = valid ? v[k] : 0.f;
 }
 
 // Sum over the wave's 64 staged rows of column `lane` (lanes < C), rows of
@@ -100,44 +124,66 @@ __global__ __launch_bounds__(256) void k_edge_mlp_fwd(EdgeGeo geo, const float* 
                                                       const float* __restrict__ xsc,
                                                       const float* __restrict__ xsh,
                                                       const float* __restrict__ Ps,
-                                                      const float* __restrict__ Pt,
+                                                      const float* __restrict__ PtT,
                                                       const float* __restrict__ W1,
-                                                      const float* __restrict__ W2,
+                                                      const float* __restrict__ W2T,
                                                       const float* __restrict__ b2,
                                                       float* __restrict__ y,
                                                       float* __restrict__ part) {
   constexpr int H = 4 * F;
   EDGE_PROLOGUE
-  float ps[H];
-#pragma unroll
-  for (int h = 0; h < H; ++h) ps[h] = fvalid ? Ps[(long long)h * NS + n] : 0.f;
+  // the block's 64 fibers' Ps rows, [H/4][64] float4 (conflict-free per lane)
+  __shared__ float4 psl[H / 4 * 64];
+  for (int j = wave; j < H / 4; j += 4) {
+    float4 v;
+    v.x = Ps[(long long)(4 * j + 0) * NS + n];
+    v.y = Ps[(long long)(4 * j + 1) * NS + n];
+    v.z = Ps[(long long)(4 * j + 2) * NS + n];
+    v.w = Ps[(long long)(4 * j + 3) * NS + n];
+    psl[j * 64 + lane] = v;
+  }
+  __syncthreads();
   float cnt = 0.f, mean[F], m2[F];
 #pragma unroll
   for (int k = 0; k < F; ++k) { mean[k] = 0.f; m2[k] = 0.f; }
   CLASS_LOOP_BEGIN
+    pf_cptr W1f = pf_fresh(W1 + 2 * F);
+    pf_cptr W2c = pf_fresh(W2T);
+    pf_cptr b2f = pf_fresh(b2);
+    pf_cptr ptc = pf_fresh(PtT + cn * H);
     float x[F];
-    load_x<F>(x, xe, xsc, xsh, e, E, fvalid);
-    float a[H];
+    load_x<F>(x, xe, xsc, xsh, eo, RB, fvalid);
+    // hidden unit by hidden unit: z_h -> a_h -> accumulated straight into y
+    float yo[F];
 #pragma unroll
-    for (int h = 0; h < H; ++h) {
-      float z = ps[h] + Pt[(long long)h * NT + cn];
+    for (int o = 0; o < F; ++o) yo[o] = b2f[o];
 #pragma unroll
-      for (int k = 0; k < F; ++k) z = fmaf(W1[h * H + 2 * F + k], x[k], z);
-      a[h] = lrelu(z);
+    for (int j = 0; j < H / 4; ++j) {
+      const float4 p4 = psl[j * 64 + lane];
+      const float pv[4] = {p4.x, p4.y, p4.z, p4.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int h = 4 * j + u;
+        float z = pv[u] + ptc[h];
+#pragma unroll
+        for (int k = 0; k < F; ++k) z = fmaf(W1f[h * H + k], x[k], z);
+        const float a = lrelu(z);
+#pragma unroll
+        for (int o = 0; o < F; ++o) yo[o] = fmaf(W2c[h * F + o], a, yo[o]);
+      }
+    }
+    const float cv = fvalid ? 1.f : 0.f;
+    cnt += cv;
+    const float rc = fvalid ? 1.0f / cnt : 0.f;
+#pragma unroll
+    for (int o = 0; o < F; ++o) {
+      const float d = yo[o] - mean[o];
+      mean[o] = fmaf(d, rc, mean[o]);
+      m2[o] = fmaf(d * cv, yo[o] - mean[o], m2[o]);
     }
     if (fvalid) {
-      cnt += 1.f;
-      const float rc = 1.0f / cnt;
 #pragma unroll
-      for (int o = 0; o < F; ++o) {
-        float s = b2[o];
-#pragma unroll
-        for (int h = 0; h < H; ++h) s = fmaf(W2[o * H + h], a[h], s);
-        y[(long long)o * E + e] = s;
-        const float d = s - mean[o];
-        mean[o] = fmaf(d, rc, mean[o]);
-        m2[o] = fmaf(d, s - mean[o], m2[o]);
-      }
+      for (int o = 0; o < F; ++o) stE(y, eo + (uint32_t)o * RB, yo[o]);
     }
   CLASS_LOOP_END
   // Chan merge over the block: lanes (butterfly) then waves (LDS)
@@ -225,26 +271,25 @@ __global__ __launch_bounds__(64) void k_moments_finalize(const float* __restrict
 // splits are merged with Pebay's pairwise formulas.  Stable like the
 // reference's two-pass (m - mean)^p, and one read of the edge state.
 template <int F>
-__device__ __forceinline__ void source_message(const float (&x)[F], long long cn, long long NT,
-                                               const float* __restrict__ Qt,
-                                               const float* __restrict__ Ws1,
-                                               const float* __restrict__ Ws2,
-                                               const float* __restrict__ bs2, float (&m)[2 * F]) {
+__device__ __forceinline__ void source_message(const float (&x)[F], const float* QtT,
+                                               long long cn, const float* Ws1,
+                                               const float* Ws2T, const float* bs2,
+                                               float (&m)[2 * F]) {
   constexpr int C = 2 * F;
-  float a[C];
+  pf_cptr qtc = pf_fresh(QtT + cn * C);
+  pf_cptr W1f = pf_fresh(Ws1 + F);
+  pf_cptr W2c = pf_fresh(Ws2T);
+  pf_cptr b2f = pf_fresh(bs2);
+#pragma unroll
+  for (int o = 0; o < C; ++o) m[o] = b2f[o];
 #pragma unroll
   for (int h = 0; h < C; ++h) {
-    float z = Qt[(long long)h * NT + cn];
+    float z = qtc[h];
 #pragma unroll
-    for (int k = 0; k < F; ++k) z = fmaf(Ws1[h * C + F + k], x[k], z);
-    a[h] = lrelu(z);
-  }
+    for (int k = 0; k < F; ++k) z = fmaf(W1f[h * C + k], x[k], z);
+    const float a = lrelu(z);
 #pragma unroll
-  for (int o = 0; o < C; ++o) {
-    float s = bs2[o];
-#pragma unroll
-    for (int h = 0; h < C; ++h) s = fmaf(Ws2[o * C + h], a[h], s);
-    m[o] = s;
+    for (int o = 0; o < C; ++o) m[o] = fmaf(W2c[h * C + o], a, m[o]);
   }
 }
 
@@ -266,9 +311,9 @@ template <int F>
 __global__ __launch_bounds__(256) void k_source_fwd(EdgeGeo geo, const float* __restrict__ y,
                                                     const float* __restrict__ sc,
                                                     const float* __restrict__ sh,
-                                                    const float* __restrict__ Qt,
+                                                    const float* __restrict__ QtT,
                                                     const float* __restrict__ Ws1,
-                                                    const float* __restrict__ Ws2,
+                                                    const float* __restrict__ Ws2T,
                                                     const float* __restrict__ bs2,
                                                     float* __restrict__ partS) {
   constexpr int C = 2 * F;
@@ -280,8 +325,8 @@ __global__ __launch_bounds__(256) void k_source_fwd(EdgeGeo geo, const float* __
   float cnt = 0.f;
   CLASS_LOOP_BEGIN
     float x[F], m[C];
-    load_x<F>(x, y, sc, sh, e, E, fvalid);
-    source_message<F>(x, cn, NT, Qt, Ws1, Ws2, bs2, m);
+    load_x<F>(x, y, sc, sh, eo, RB, fvalid);
+    source_message<F>(x, QtT, cn, Ws1, Ws2T, bs2, m);
     const float nold = cnt;
     cnt += 1.f;
     const float inv = 1.f / cnt, a3 = cnt - 2.f, a4 = cnt * cnt - 3.f * cnt + 3.f;
@@ -392,13 +437,14 @@ __global__ __launch_bounds__(256) void k_target_fwd(EdgeGeo geo, const float* __
 #pragma unroll
   for (int h = 0; h < C; ++h) rs[h] = fvalid ? Rs[(long long)h * NS + n] : 0.f;
   CLASS_LOOP_BEGIN
+    pf_cptr W1f = pf_fresh(Wt1 + F);
     float x[F];
-    load_x<F>(x, y, sc, sh, e, E, fvalid);
+    load_x<F>(x, y, sc, sh, eo, RB, fvalid);
 #pragma unroll
     for (int h = 0; h < C; ++h) {
       float z = rs[h];
 #pragma unroll
-      for (int k = 0; k < F; ++k) z = fmaf(Wt1[h * C + F + k], x[k], z);
+      for (int k = 0; k < F; ++k) z = fmaf(W1f[h * C + k], x[k], z);
       R[lane * LD + h] = fvalid ? lrelu(z) : 0.f;
     }
     wave_lds_sync();
@@ -415,7 +461,7 @@ __global__ __launch_bounds__(256) void k_target_bwd(EdgeGeo geo, const float* __
                                                     const float* __restrict__ sh,
                                                     const float* __restrict__ Rs,
                                                     const float* __restrict__ Wt1,
-                                                    const float* __restrict__ g_hsum,
+                                                    const float* __restrict__ g_hsumT,
                                                     float* __restrict__ GzT,
                                                     float* __restrict__ gxe,
                                                     float* __restrict__ partW) {
@@ -435,23 +481,30 @@ __global__ __launch_bounds__(256) void k_target_bwd(EdgeGeo geo, const float* __
     acc[h] = 0.f;
   }
   CLASS_LOOP_BEGIN
+    pf_cptr W1f = pf_fresh(Wt1 + F);
+    pf_cptr ghc = pf_fresh(g_hsumT + cn * C);
     float x[F], gz[C];
-    load_x<F>(x, y, sc, sh, e, E, fvalid);
+    load_x<F>(x, y, sc, sh, eo, RB, fvalid);
 #pragma unroll
     for (int h = 0; h < C; ++h) {
       float z = rs[h];
 #pragma unroll
-      for (int k = 0; k < F; ++k) z = fmaf(Wt1[h * C + F + k], x[k], z);
-      gz[h] = fvalid ? g_hsum[(long long)h * NT + cn] * dlrelu(z) : 0.f;
+      for (int k = 0; k < F; ++k) z = fmaf(W1f[h * C + k], x[k], z);
+      gz[h] = fvalid ? ghc[h] * dlrelu(z) : 0.f;
       acc[h] += gz[h];
     }
-    if (gxe && fvalid) {
+    if (gxe) {
+      float gx[F];
 #pragma unroll
       for (int k = 0; k < F; ++k) {
         float s = 0.f;
 #pragma unroll
-        for (int h = 0; h < C; ++h) s = fmaf(Wt1[h * C + F + k], gz[h], s);
-        gxe[(long long)k * E + e] = s;
+        for (int h = 0; h < C; ++h) s = fmaf(W1f[h * C + k], gz[h], s);
+        gx[k] = s;
+      }
+      if (fvalid) {
+#pragma unroll
+        for (int k = 0; k < F; ++k) stE(gxe, eo + (uint32_t)k * RB, gx[k]);
       }
     }
     wg.stage(region, gz, x, lane);
@@ -467,10 +520,10 @@ __global__ __launch_bounds__(256) void k_target_bwd(EdgeGeo geo, const float* __
 template <int F>
 __global__ __launch_bounds__(256) void k_source_bwd(
     EdgeGeo geo, const float* __restrict__ y, const float* __restrict__ sc,
-    const float* __restrict__ sh, const float* __restrict__ Qt, const float* __restrict__ Ws1,
+    const float* __restrict__ sh, const float* __restrict__ QtT, const float* __restrict__ Ws1,
     const float* __restrict__ Ws2, const float* __restrict__ bs2, const float* __restrict__ mean,
     const float* __restrict__ coef, const float* __restrict__ Rs, const float* __restrict__ Wt1,
-    const float* __restrict__ g_hsum, const float* __restrict__ g_next,
+    const float* __restrict__ g_hsumT, const float* __restrict__ g_next,
     const float* __restrict__ mu1, const float* __restrict__ inv1, float* __restrict__ g_tot,
     float* __restrict__ partW2, float* __restrict__ partW1, float* __restrict__ partCol,
     float* __restrict__ partBN) {
@@ -507,20 +560,29 @@ __global__ __launch_bounds__(256) void k_source_bwd(
 #pragma unroll
   for (int k = 0; k < F; ++k) { sg[k] = 0.f; sgx[k] = 0.f; }
   CLASS_LOOP_BEGIN
+    pf_cptr W1f = pf_fresh(Ws1 + F);
+    pf_cptr W2f = pf_fresh(Ws2);
+    pf_cptr b2f = pf_fresh(bs2);
+    pf_cptr qtc = pf_fresh(QtT + cn * C);
     float yv[F], x[F];
 #pragma unroll
-    for (int k = 0; k < F; ++k) {
-      yv[k] = fvalid ? y[(long long)k * E + e] : 0.f;
-      x[k] = fvalid ? (sc ? fmaf(yv[k], sc[k], sh[k]) : yv[k]) : 0.f;
+    for (int k = 0; k < F; ++k) yv[k] = ldEz(y, eo + (uint32_t)k * RB, fvalid);
+    if (sc) {
+      pf_cptr scf = pf_fresh(sc), shf = pf_fresh(sh);
+#pragma unroll
+      for (int k = 0; k < F; ++k) x[k] = fvalid ? fmaf(yv[k], scf[k], shf[k]) : 0.f;
+    } else {
+#pragma unroll
+      for (int k = 0; k < F; ++k) x[k] = yv[k];
     }
     float* A = region;
     float* B = region + 64 * WG2::LDA;
     float zs[C];
 #pragma unroll
     for (int h = 0; h < C; ++h) {
-      float z = Qt[(long long)h * NT + cn];
+      float z = qtc[h];
 #pragma unroll
-      for (int k = 0; k < F; ++k) z = fmaf(Ws1[h * C + F + k], x[k], z);
+      for (int k = 0; k < F; ++k) z = fmaf(W1f[h * C + k], x[k], z);
       zs[h] = z;
       B[lane * WG2::LDB + h] = lrelu(z);
     }
@@ -528,9 +590,9 @@ __global__ __launch_bounds__(256) void k_source_bwd(
     float gm[C];
 #pragma unroll
     for (int o = 0; o < C; ++o) {
-      float s = bs2[o];
+      float s = b2f[o];
 #pragma unroll
-      for (int h = 0; h < C; ++h) s = fmaf(Ws2[o * C + h], lrelu(zs[h]), s);
+      for (int h = 0; h < C; ++h) s = fmaf(W2f[o * C + h], lrelu(zs[h]), s);
       const float d = s - fib[o * 64 + lane];
       const float q0 = fib[(C + o) * 64 + lane], q1 = fib[(2 * C + o) * 64 + lane],
                   q2 = fib[(3 * C + o) * 64 + lane], q3 = fib[(4 * C + o) * 64 + lane];
@@ -540,53 +602,59 @@ __global__ __launch_bounds__(256) void k_source_bwd(
     wave_lds_sync();
     wg2.accum(region, lane);
     wave_lds_sync();
+    pf_cptr W2g = pf_fresh(Ws2);
     float gz[C];
 #pragma unroll
     for (int h = 0; h < C; ++h) {
       float s = 0.f;
 #pragma unroll
-      for (int o = 0; o < C; ++o) s = fmaf(Ws2[o * C + h], gm[o], s);
+      for (int o = 0; o < C; ++o) s = fmaf(W2g[o * C + h], gm[o], s);
       gz[h] = s * dlrelu(zs[h]);
     }
+    pf_cptr W1g = pf_fresh(Ws1 + F);
     float g[F];
 #pragma unroll
     for (int k = 0; k < F; ++k) {
       float s = 0.f;
 #pragma unroll
-      for (int h = 0; h < C; ++h) s = fmaf(Ws1[h * C + F + k], gz[h], s);
+      for (int h = 0; h < C; ++h) s = fmaf(W1g[h * C + k], gz[h], s);
       g[k] = s;
     }
     if (Rs) {  // TModel's per-edge input gradient, recomputed (gnn.py:188-190)
+      pf_cptr Wtf = pf_fresh(Wt1 + F);
+      pf_cptr ghc = pf_fresh(g_hsumT + cn * C);
       float gzt[C];
 #pragma unroll
       for (int h = 0; h < C; ++h) {
         float z = fib[(5 * C + h) * 64 + lane];
 #pragma unroll
-        for (int k = 0; k < F; ++k) z = fmaf(Wt1[h * C + F + k], x[k], z);
-        gzt[h] = fvalid ? g_hsum[(long long)h * NT + cn] * dlrelu(z) : 0.f;
+        for (int k = 0; k < F; ++k) z = fmaf(Wtf[h * C + k], x[k], z);
+        gzt[h] = fvalid ? ghc[h] * dlrelu(z) : 0.f;
       }
+      pf_cptr Wtg = pf_fresh(Wt1 + F);
 #pragma unroll
       for (int k = 0; k < F; ++k) {
         float s = g[k];
 #pragma unroll
-        for (int h = 0; h < C; ++h) s = fmaf(Wt1[h * C + F + k], gzt[h], s);
+        for (int h = 0; h < C; ++h) s = fmaf(Wtg[h * C + k], gzt[h], s);
         g[k] = s;
       }
     }
     if (g_next) {
 #pragma unroll
-      for (int k = 0; k < F; ++k) g[k] += fvalid ? g_next[(long long)k * E + e] : 0.f;
+      for (int k = 0; k < F; ++k) g[k] += ldEz(g_next, eo + (uint32_t)k * RB, fvalid);
     }
     if (fvalid) {
 #pragma unroll
-      for (int k = 0; k < F; ++k) g_tot[(long long)k * E + e] = g[k];
+      for (int k = 0; k < F; ++k) stE(g_tot, eo + (uint32_t)k * RB, g[k]);
     }
     if (mu1) {
+      pf_cptr m1 = pf_fresh(mu1), i1 = pf_fresh(inv1);
 #pragma unroll
       for (int k = 0; k < F; ++k) {
         const float gk = fvalid ? g[k] : 0.f;
         sg[k] += gk;
-        sgx[k] = fmaf(gk, (yv[k] - mu1[k]) * inv1[k], sgx[k]);
+        sgx[k] = fmaf(gk, (yv[k] - m1[k]) * i1[k], sgx[k]);
       }
     }
     wg1.stage(region, gz, x, lane);
@@ -625,13 +693,13 @@ __global__ __launch_bounds__(256) void k_edge_bn_sums(EdgeGeo geo, const float* 
 #pragma unroll
   for (int k = 0; k < 2 * F; ++k) v[k] = 0.f;
   CLASS_LOOP_BEGIN
-    if (fvalid) {
+    pf_cptr m1 = pf_fresh(mu1), i1 = pf_fresh(inv1);
 #pragma unroll
-      for (int k = 0; k < F; ++k) {
-        const float gk = g[(long long)k * E + e];
-        v[k] += gk;
-        v[F + k] = fmaf(gk, (y[(long long)k * E + e] - mu1[k]) * inv1[k], v[F + k]);
-      }
+    for (int k = 0; k < F; ++k) {
+      const float gk = ldEz(g, eo + (uint32_t)k * RB, fvalid);
+      const float yk = ldE(y, eo + (uint32_t)k * RB);
+      v[k] += gk;
+      v[F + k] = fmaf(gk, (yk - m1[k]) * i1[k], v[F + k]);
     }
   CLASS_LOOP_END
   block_sum<2 * F>(v, scratch);
@@ -649,7 +717,7 @@ __global__ __launch_bounds__(256) void k_edge_mlp_bwd(
     EdgeGeo geo, const float* __restrict__ g_tot, const float* __restrict__ alpha,
     const float* __restrict__ gam0, const float* __restrict__ gam1, const float* __restrict__ y,
     const float* __restrict__ xe, const float* __restrict__ xsc, const float* __restrict__ xsh,
-    const float* __restrict__ Ps, const float* __restrict__ Pt, const float* __restrict__ W1,
+    const float* __restrict__ Ps, const float* __restrict__ PtT, const float* __restrict__ W1,
     const float* __restrict__ W2, float* __restrict__ gxe, float* __restrict__ GzEs,
     float* __restrict__ partW2, float* __restrict__ partW1, float* __restrict__ partCol) {
   constexpr int H = 4 * F;
@@ -677,23 +745,28 @@ __global__ __launch_bounds__(256) void k_edge_mlp_bwd(
   for (int h = 0; h < H; ++h) acc[h] = 0.f;
   CLASS_LOOP_BEGIN
     float gy[F], x[F];
+    {
+      pf_cptr al = pf_fresh(alpha), g0 = pf_fresh(gam0), g1 = pf_fresh(gam1);
 #pragma unroll
-    for (int k = 0; k < F; ++k) {
-      const float gt = fvalid ? g_tot[(long long)k * E + e] : 0.f;
-      const float yk = fvalid ? y[(long long)k * E + e] : 0.f;
-      gy[k] = fvalid ? fmaf(gam1[k], yk, fmaf(alpha[k], gt, gam0[k])) : 0.f;
+      for (int k = 0; k < F; ++k) {
+        const float gt = ldE(g_tot, eo + (uint32_t)k * RB);
+        const float yk = ldE(y, eo + (uint32_t)k * RB);
+        gy[k] = fvalid ? fmaf(g1[k], yk, fmaf(al[k], gt, g0[k])) : 0.f;
+      }
     }
-    load_x<F>(x, xe, xsc, xsh, e, E, fvalid);
+    load_x<F>(x, xe, xsc, xsh, eo, RB, fvalid);
     float* A = region;
     float* B = region + 64 * WG2::LDA;
 #pragma unroll
     for (int k = 0; k < F; ++k) A[lane * WG2::LDA + k] = gy[k];
+    pf_cptr W1f = pf_fresh(W1 + 2 * F);
+    pf_cptr ptc = pf_fresh(PtT + cn * H);
     float z[H];
 #pragma unroll
     for (int h = 0; h < H; ++h) {
-      float s = psl[h * 64 + lane] + Pt[(long long)h * NT + cn];
+      float s = psl[h * 64 + lane] + ptc[h];
 #pragma unroll
-      for (int k = 0; k < F; ++k) s = fmaf(W1[h * H + 2 * F + k], x[k], s);
+      for (int k = 0; k < F; ++k) s = fmaf(W1f[h * H + k], x[k], s);
       z[h] = s;
       B[lane * WG2::LDB + h] = lrelu(s);
     }
@@ -701,22 +774,29 @@ __global__ __launch_bounds__(256) void k_edge_mlp_bwd(
     wave_lds_sync();
     wg2.accum(region, lane);
     wave_lds_sync();
+    pf_cptr W2g = pf_fresh(W2);
     float gz[H];
 #pragma unroll
     for (int h = 0; h < H; ++h) {
       float s = 0.f;
 #pragma unroll
-      for (int o = 0; o < F; ++o) s = fmaf(W2[o * H + h], gy[o], s);
+      for (int o = 0; o < F; ++o) s = fmaf(W2g[o * H + h], gy[o], s);
       gz[h] = s * dlrelu(z[h]);
       acc[h] += gz[h];
     }
-    if (gxe && fvalid) {
+    if (gxe) {
+      pf_cptr W1g = pf_fresh(W1 + 2 * F);
+      float gx[F];
 #pragma unroll
       for (int k = 0; k < F; ++k) {
         float s = 0.f;
 #pragma unroll
-        for (int h = 0; h < H; ++h) s = fmaf(W1[h * H + 2 * F + k], gz[h], s);
-        gxe[(long long)k * E + e] = s;
+        for (int h = 0; h < H; ++h) s = fmaf(W1g[h * H + k], gz[h], s);
+        gx[k] = s;
+      }
+      if (fvalid) {
+#pragma unroll
+        for (int k = 0; k < F; ++k) stE(gxe, eo + (uint32_t)k * RB, gx[k]);
       }
     }
     wg1.stage(region, gz, x, lane);
@@ -741,6 +821,16 @@ __global__ void k_reduce_fiber(const float* __restrict__ part, int KS, long long
   out[idx] = s;
 }
 
+// per-class node table [C][NT] -> class-major rows [NT][C] (scalar-loadable)
+__global__ void k_class_rows(const float* __restrict__ src, int C, long long NT,
+                             float* __restrict__ dst) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // over NT*C
+  if (idx >= NT * C) return;
+  const long long cn = idx / C;
+  const int h = (int)(idx - cn * C);
+  dst[idx] = src[(long long)h * NT + cn];
+}
+
 // ============================================================ host side
 namespace {
 
@@ -760,8 +850,25 @@ struct Ws {
 int check_dims(const char* where, int G, int NF, int NC, int F) {
   if (G <= 0 || NF <= 0 || NC <= 0) return pf::fail(where, "G, NF, NC must be positive");
   if (F != 8 && F != 10 && F != 16) return pf::fail(where, "unsupported Fdim (8, 10, 16)");
-  if ((long long)G * NF * NC >= (1ll << 31)) return pf::fail(where, "too many edges");
+  // edge tensors are addressed with 32-bit byte offsets (ldE/stE)
+  if ((long long)G * NF * NC * F * 4 >= (1ll << 32))
+    return pf::fail(where, "edge tensor exceeds 4 GiB (split the batch)");
   return 0;
+}
+
+// transposed copy [R][N] -> [N][R] in the workspace
+const float* transposed(const float* src, int R, long long N, Ws& w, hipStream_t st) {
+  if (!src) return nullptr;
+  float* dst = w.take((size_t)N * R);
+  if (!dst) return nullptr;
+  const long long len = N * R;
+  hipLaunchKernelGGL(k_class_rows, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, st, src, R,
+                     N, dst);
+  return dst;
+}
+// class-major copy of a per-class node table [C][NT]
+const float* class_rows(const float* src, int C, const EdgeGeo& geo, Ws& w, hipStream_t st) {
+  return transposed(src, C, geo.NT, w, st);
 }
 
 #define DISPATCH_F(F, ...)                                   \
@@ -798,7 +905,8 @@ extern "C" size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F) {
   edge = std::max(edge, nb * C * F + ks * C * NS + 1024);                           // target bwd
   edge = std::max(edge, nb * (C * (C + 1) + C * F + 2 * F) + colp * C + 4096);      // source bwd
   edge = std::max(edge, nb * (F * (H + 1) + H * F) + colp * H + ks * H * NS + 4096);  // edge bwd
-  edge = std::max(edge, colp * 4 + nb * (F * (F + 1) + F + 1) + 4096);             // loss
+  edge = std::max(edge, colp * 4 + ks * NS + nb * (F * (F + 1) + F + 1) + 4096);   // loss
+  edge += (size_t)geo.NT * (H + 2 * C) + 4 * H * H + 8 * 256;  // class_rows / transposed
   size_t node = (size_t)64 * 128 * 128 + 4096;                                      // wgrad splits
   size_t lay = (size_t)geo.E + 1024;                                                // layout counts
   return (std::max(std::max(edge, node), lay) + 64 * 16) * sizeof(float) + 16 * 256;
@@ -813,12 +921,14 @@ extern "C" int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe
   PF_REQUIRE(xe && Ps && Pt && W1 && W2 && b2 && y && mu && var, "pfsgnn_edge_mlp_fwd", "null");
   const EdgeGeo geo = make_geo(G, NF, NC);
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
-  float* part = w.take((size_t)geo.nblocks * (1 + 2 * F));
-  PF_REQUIRE(part, "pfsgnn_edge_mlp_fwd", "workspace too small");
   hipStream_t st = as_stream(stream);
+  float* part = w.take((size_t)geo.nblocks * (1 + 2 * F));
+  const float* PtT = class_rows(Pt, 4 * F, geo, w, st);
+  const float* W2T = transposed(W2, F, 4 * F, w, st);
+  PF_REQUIRE(part && PtT && W2T, "pfsgnn_edge_mlp_fwd", "workspace too small");
   { pf::Timer tm_("edge_mlp_fwd", st);
   DISPATCH_F(F, hipLaunchKernelGGL(k_edge_mlp_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
-                                   xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part));
+                                   xe, xsc, xsh, Ps, PtT, W1, W2T, b2, y, part));
   tm_.end(); }
   hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(64), 0, st, part, geo.nblocks, F, geo.E,
                      mu, var);
@@ -834,12 +944,14 @@ extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, c
   const EdgeGeo geo = make_geo(G, NF, NC);
   const int C = 2 * F;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
-  float* partS = w.take((size_t)geo.KS * 4 * C * geo.NS);
-  PF_REQUIRE(partS, "pfsgnn_source_fwd", "workspace too small");
   hipStream_t st = as_stream(stream);
+  float* partS = w.take((size_t)geo.KS * 4 * C * geo.NS);
+  const float* QtT = class_rows(Qt, C, geo, w, st);
+  const float* Ws2T = transposed(Ws2, C, C, w, st);
+  PF_REQUIRE(partS && QtT && Ws2T, "pfsgnn_source_fwd", "workspace too small");
   { pf::Timer tm_("source_fwd", st);
   DISPATCH_F(F, hipLaunchKernelGGL(k_source_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
-                                   sc, sh, Qt, Ws1, Ws2, bs2, partS));
+                                   sc, sh, QtT, Ws1, Ws2T, bs2, partS));
   tm_.end(); }
   const long long len = (long long)C * geo.NS;
   hipLaunchKernelGGL(k_source_finalize, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, st,
@@ -874,13 +986,14 @@ extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, c
   const EdgeGeo geo = make_geo(G, NF, NC);
   const int C = 2 * F;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
+  hipStream_t st = as_stream(stream);
   float* part = w.take((size_t)geo.nblocks * C * F);
   float* gz = fiber_dst(geo, C, GzT, w);
-  PF_REQUIRE(part && gz, "pfsgnn_target_bwd", "workspace too small");
-  hipStream_t st = as_stream(stream);
+  const float* ghT = class_rows(g_hsum, C, geo, w, st);
+  PF_REQUIRE(part && gz && ghT, "pfsgnn_target_bwd", "workspace too small");
   { pf::Timer tm_("target_bwd", st);
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
-                                   sc, sh, Rs, Wt1, g_hsum, gz, gxe, part));
+                                   sc, sh, Rs, Wt1, ghT, gz, gxe, part));
   tm_.end(); }
   fiber_finish(geo, C, gz, GzT, st);
   launch_reduce_rows(part, geo.nblocks, (size_t)C * F, F, C, F, dWt1 + F, C, 1, 1.f, st);
@@ -909,11 +1022,14 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
   float* pW1 = w.take(nb * C * F);
   float* pCol = w.take((size_t)G * geo.NFG * NC * C);
   float* pBN = w.take(nb * 2 * F);
-  PF_REQUIRE(pW2 && pW1 && pCol && pBN, "pfsgnn_source_bwd", "workspace too small");
   hipStream_t st = as_stream(stream);
+  const float* QtT = class_rows(Qt, C, geo, w, st);
+  const float* ghT = class_rows(g_hsum, C, geo, w, st);
+  PF_REQUIRE(pW2 && pW1 && pCol && pBN && QtT && (ghT || !g_hsum), "pfsgnn_source_bwd",
+             "workspace too small");
   { pf::Timer tm_("source_bwd", st);
   DISPATCH_F(F, hipLaunchKernelGGL(k_source_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
-                                   sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, g_hsum, g_next,
+                                   sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT, g_next,
                                    mu1, inv1, g_tot, pW2, pW1, pCol, pBN));
   tm_.end(); }
   launch_reduce_rows(pW2, nb, (size_t)C * (C + 1), C + 1, C, C, dWs2, C, 1, 1.f, st);
@@ -966,11 +1082,12 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
   float* pW1 = w.take(nb * H * F);
   float* pCol = w.take((size_t)G * geo.NFG * NC * H);
   float* gs = fiber_dst(geo, H, GzEs, w);
-  PF_REQUIRE(pW2 && pW1 && pCol && gs, "pfsgnn_edge_mlp_bwd", "workspace too small");
   hipStream_t st = as_stream(stream);
+  const float* PtT = class_rows(Pt, H, geo, w, st);
+  PF_REQUIRE(pW2 && pW1 && pCol && gs && PtT, "pfsgnn_edge_mlp_bwd", "workspace too small");
   { pf::Timer tm_("edge_mlp_bwd", st);
   DISPATCH_F(F, hipLaunchKernelGGL(k_edge_mlp_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
-                                   g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1, W2, gxe,
+                                   g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, PtT, W1, W2, gxe,
                                    gs, pW2, pW1, pCol));
   tm_.end(); }
   fiber_finish(geo, H, gs, GzEs, st);
