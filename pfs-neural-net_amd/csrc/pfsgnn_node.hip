@@ -161,30 +161,53 @@ void launch_reduce_columns(const float* part, int G, int BPG, int NC, int C, flo
 }
 
 // ---------------------------------------------------------------- lin
-// One thread per column n, 16 output rows per thread; weights are uniform
-// (scalar loads), the input column is streamed once per 16 rows.
+// One thread per column n, LIN_MB output rows per thread.  The K loop runs in
+// chunks of 8: the 8 input values of the column are loaded together (8 loads
+// in flight per thread instead of one dependent load per k), the weights are
+// wave-uniform rows read with s_load.
 #define LIN_MB 16
+#define LIN_KC 8
 __global__ __launch_bounds__(256) void k_lin(const float* __restrict__ W, int ldw, int M, int K,
                                              const float* __restrict__ X, int N,
                                              const float* __restrict__ b, float bscale, int act_in,
                                              float* __restrict__ Y, int add) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   const int m0 = blockIdx.y * LIN_MB;
-  if (n >= N) return;
+  const int nc = n < N ? n : N - 1;
+  const int mrows = min(LIN_MB, M - m0);
   float acc[LIN_MB];
 #pragma unroll
   for (int i = 0; i < LIN_MB; ++i) acc[i] = 0.f;
-  for (int k = 0; k < K; ++k) {
-    float x = X[(size_t)k * N + n];
+  int k = 0;
+  for (; k + LIN_KC <= K; k += LIN_KC) {
+    float xv[LIN_KC];
+#pragma unroll
+    for (int j = 0; j < LIN_KC; ++j) xv[j] = X[(size_t)(k + j) * N + nc];
+    if (act_in) {
+#pragma unroll
+      for (int j = 0; j < LIN_KC; ++j) xv[j] = lrelu(xv[j]);
+    }
+#pragma unroll
+    for (int i = 0; i < LIN_MB; ++i) {
+      if (i < mrows) {
+        pf_cptr w = pf_fresh(W + (size_t)(m0 + i) * ldw + k);
+#pragma unroll
+        for (int j = 0; j < LIN_KC; ++j) acc[i] = fmaf(w[j], xv[j], acc[i]);
+      }
+    }
+  }
+  for (; k < K; ++k) {
+    float x = X[(size_t)k * N + nc];
     if (act_in) x = lrelu(x);
 #pragma unroll
     for (int i = 0; i < LIN_MB; ++i)
-      if (m0 + i < M) acc[i] = fmaf(W[(size_t)(m0 + i) * ldw + k], x, acc[i]);
+      if (i < mrows) acc[i] = fmaf(W[(size_t)(m0 + i) * ldw + k], x, acc[i]);
   }
+  if (n >= N) return;
 #pragma unroll
   for (int i = 0; i < LIN_MB; ++i) {
-    const int m = m0 + i;
-    if (m < M) {
+    if (i < mrows) {
+      const int m = m0 + i;
       float v = acc[i];
       if (b) v += bscale * b[m];
       float* o = Y + (size_t)m * N + n;
@@ -209,20 +232,35 @@ __global__ __launch_bounds__(256) void k_lin_t(const float* __restrict__ W, int 
                                                float* __restrict__ out, int add) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   const int k0 = blockIdx.y * LIN_MB;
-  if (n >= N) return;
+  const int nc = n < N ? n : N - 1;
+  const int kcols = min(LIN_MB, K - k0);
   float acc[LIN_MB];
 #pragma unroll
   for (int i = 0; i < LIN_MB; ++i) acc[i] = 0.f;
-  for (int m = 0; m < M; ++m) {
-    const float g = dY[(size_t)m * N + n];
+  int m = 0;
+  for (; m + LIN_KC <= M; m += LIN_KC) {
+    float g[LIN_KC];
+#pragma unroll
+    for (int j = 0; j < LIN_KC; ++j) g[j] = dY[(size_t)(m + j) * N + nc];
+#pragma unroll
+    for (int j = 0; j < LIN_KC; ++j) {
+      pf_cptr w = pf_fresh(W + (size_t)(m + j) * ldw + k0);
+#pragma unroll
+      for (int i = 0; i < LIN_MB; ++i)
+        if (i < kcols) acc[i] = fmaf(w[i], g[j], acc[i]);
+    }
+  }
+  for (; m < M; ++m) {
+    const float g = dY[(size_t)m * N + nc];
 #pragma unroll
     for (int i = 0; i < LIN_MB; ++i)
-      if (k0 + i < K) acc[i] = fmaf(W[(size_t)m * ldw + k0 + i], g, acc[i]);
+      if (i < kcols) acc[i] = fmaf(W[(size_t)m * ldw + k0 + i], g, acc[i]);
   }
+  if (n >= N) return;
 #pragma unroll
   for (int i = 0; i < LIN_MB; ++i) {
-    const int k = k0 + i;
-    if (k < K) {
+    if (i < kcols) {
+      const int k = k0 + i;
       float v = acc[i];
       if (Z) v *= dlrelu(Z[(size_t)k * N + n]);
       float* o = out + (size_t)k * N + n;
@@ -241,12 +279,15 @@ extern "C" int pfsgnn_lin_t(const float* W, int ldw, int M, int K, const float* 
 }
 
 // ---------------------------------------------------------------- wgrad
-// dW[m][k] += sum_n dY[m][n] act(X[k][n]).  Output tiles of 16x16 on
-// v_mfma_f32_16x16x4_f32 with the node index as the MFMA K dimension; the
-// N range is split over blocks (per-block partials + deterministic reduce).
+// dW[m][k] += sum_n dY[m][n] act(X[k][n]) and (optionally) db[m] += s*sum_n dY[m][n]
+// as one more column k = K of ones.  Output tiles of 16x16 on
+// v_mfma_f32_16x16x4_f32 with the node index as the MFMA K dimension; the N
+// range is split over blocks (per-block partials + deterministic reduce).  A
+// wave walks its chunk 4 MFMAs at a time with all 8 loads issued first.
+#define WG_CHUNK 512
 __global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ dY, int M,
-                                               const float* __restrict__ X, int K, int N,
-                                               int act_in, int tilesK, int chunk,
+                                               const float* __restrict__ X, int K, int K1,
+                                               int N, int act_in, int tilesK, int chunk,
                                                float* __restrict__ part) {
   const int tile = blockIdx.x;
   const int tm = tile / tilesK, tk = tile - tm * tilesK;
@@ -258,45 +299,51 @@ __global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ dY, int
   const int colk = tk * 16 + (lane & 15); // k for B operand
   const int kq = lane >> 4;
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-  const bool rv = row < M, cv = colk < K;
+  const bool rv = row < M, cv = colk < K, ones = colk == K && K1 > K;
   const float* dyr = dY + (size_t)(rv ? row : 0) * N;
   const float* xr = X + (size_t)(cv ? colk : 0) * N;
-  for (int base = c0 + 4 * wave; base < c1; base += 16) {
-    const int n = base + kq;
+  // per MFMA step the 4 waves x 4 lane groups cover 16 consecutive n; the
+  // loop bounds are wave-uniform (MFMA needs every lane)
+  int wb = c0 + 4 * wave;
+  for (; wb + 63 < c1; wb += 64) {
+    float a[4], bb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = dyr[wb + kq + 16 * u];
+      bb[u] = xr[wb + kq + 16 * u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float bv = act_in ? lrelu(bb[u]) : bb[u];
+      bv = cv ? bv : (ones ? 1.f : 0.f);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(rv ? a[u] : 0.f, bv, acc, 0, 0, 0);
+    }
+  }
+  for (; wb < c1; wb += 16) {
+    const int n = wb + kq;
     const bool nv = n < c1;
     const float a = (rv && nv) ? dyr[n] : 0.f;
-    float b = (cv && nv) ? xr[n] : 0.f;
-    if (act_in) b = lrelu(b);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+    float bv = (cv && nv) ? xr[n] : 0.f;
+    if (act_in) bv = lrelu(bv);
+    if (ones) bv = nv ? 1.f : 0.f;
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc, 0, 0, 0);
   }
   __shared__ float red[4][16][16];
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[wave][4 * (lane >> 4) + r][lane & 15] = acc[r];
   __syncthreads();
-  // part layout [split][M][K]
+  // part layout [split][M][K1]
   const int i = t >> 4, j = t & 15;
   const int m = tm * 16 + i, k = tk * 16 + j;
-  if (m < M && k < K) {
+  if (m < M && k < K1) {
     const float s = ((red[0][i][j] + red[1][i][j]) + red[2][i][j]) + red[3][i][j];
-    part[(size_t)split * M * K + (size_t)m * K + k] = s;
+    part[(size_t)split * M * K1 + (size_t)m * K1 + k] = s;
   }
 }
 
-// db[m] += scale * sum_n dY[m][n]   (one block per row)
-__global__ __launch_bounds__(256) void k_rowsum(const float* __restrict__ dY, int N,
-                                                float* __restrict__ db, float scale) {
-  const int m = blockIdx.x;
-  float s = 0.f;
-  for (int n = threadIdx.x; n < N; n += 256) s += dY[(size_t)m * N + n];
-  __shared__ float scratch[4];
-  float v[1] = {s};
-  block_sum<1>(v, scratch);
-  if (threadIdx.x == 0) db[m] += scale * v[0];
-}
-
 static int wgrad_splits(int N) {
-  int s = (N + 2047) / 2048;
-  return std::max(1, std::min(s, 64));
+  int s = (N + WG_CHUNK - 1) / WG_CHUNK;
+  return std::max(1, std::min(s, 128));
 }
 
 extern "C" int pfsgnn_wgrad(const float* dY, int M, const float* X, int K, int N, int act_in,
@@ -305,15 +352,16 @@ extern "C" int pfsgnn_wgrad(const float* dY, int M, const float* X, int K, int N
   PF_REQUIRE(dY && X && dW && M > 0 && K > 0 && N > 0, "pfsgnn_wgrad", "bad arguments");
   hipStream_t st = as_stream(stream);
   const int splits = wgrad_splits(N);
-  const size_t need = (size_t)splits * M * K * sizeof(float);
+  const int K1 = K + (db ? 1 : 0);
+  const size_t need = (size_t)splits * M * K1 * sizeof(float);
   PF_REQUIRE(ws && ws_bytes >= need, "pfsgnn_wgrad", "workspace too small");
   const int chunk = (N + splits - 1) / splits;
-  const int tilesM = (M + 15) / 16, tilesK = (K + 15) / 16;
+  const int tilesM = (M + 15) / 16, tilesK = (K1 + 15) / 16;
   float* part = reinterpret_cast<float*>(ws);
-  hipLaunchKernelGGL(k_wgrad, dim3(tilesM * tilesK, splits), dim3(256), 0, st, dY, M, X, K, N,
+  hipLaunchKernelGGL(k_wgrad, dim3(tilesM * tilesK, splits), dim3(256), 0, st, dY, M, X, K, K1, N,
                      act_in, tilesK, chunk, part);
-  launch_reduce_rows(part, splits, (size_t)M * K, K, M, K, dW, lddw, 1, 1.f, st);
-  if (db) hipLaunchKernelGGL(k_rowsum, dim3(M), dim3(256), 0, st, dY, N, db, dbscale);
+  launch_reduce_rows(part, splits, (size_t)M * K1, K1, M, K, dW, lddw, 1, 1.f, st);
+  if (db) launch_reduce_rows(part + K, splits, (size_t)M * K1, K1, M, 1, db, 1, 1, dbscale, st);
   return pf::check_launch("pfsgnn_wgrad");
 }
 
