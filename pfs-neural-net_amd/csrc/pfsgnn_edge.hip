@@ -46,6 +46,59 @@
 
 #define CLASS_LOOP_END }
 
+// Software prefetch of the per-edge rows of the NEXT class while the current
+// one is computed: a wave issues its F-float loads one iteration ahead, so the
+// HBM latency is hidden behind a whole iteration of compute instead of being
+// waited out at the top of every iteration.  Arrays with a null source are
+// skipped (wave-uniform).
+template <int F, int NA>
+struct EdgeStream {
+  struct Buf { float v[NA][F]; };
+  const float* src[NA];
+  Buf b;
+  __device__ __forceinline__ void load(uint32_t eo, uint32_t RB) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+      if (src[a]) {
+#pragma unroll
+        for (int k = 0; k < F; ++k)
+          b.v[a][k] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(src[a]) +
+                                                      eo + (uint32_t)k * RB);
+      }
+    }
+  }
+};
+
+#define EO_OF(cc) \
+  ((uint32_t)((((long long)gg * geo.NC + (cc)) * geo.NF + (fvalid ? f : 0)) * 4))
+
+#define CLASS_LOOP_PF_BEGIN(S)                                              \
+  if (c0 + wave < c1) S.load(EO_OF(c0 + wave), RB);                         \
+  for (int c = c0 + wave; c < c1; c += 4) {                                 \
+    const long long cn = (long long)gg * geo.NC + c;                        \
+    const long long e = cn * geo.NF + (fvalid ? f : 0);                     \
+    const uint32_t eo = (uint32_t)e * 4u;                                   \
+    (void)eo;                                                               \
+    const auto cur = S.b;                                                   \
+    if (c + 4 < c1) S.load(EO_OF(c + 4), RB);
+
+// x = valid ? sc*v + sh : 0 from a prefetched raw row
+template <int F>
+__device__ __forceinline__ void affine_x(float (&x)[F], const float (&v)[F],
+                                         const float* __restrict__ sc,
+                                         const float* __restrict__ sh, bool valid) {
+  float t[F];
+#pragma unroll
+  for (int k = 0; k < F; ++k) t[k] = v[k];
+  if (sc) {
+    pf_cptr a = pf_fresh(sc), b = pf_fresh(sh);
+#pragma unroll
+    for (int k = 0; k < F; ++k) t[k] = fmaf(t[k], a[k], b[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < F; ++k) x[k] = valid ? t[k] : 0.f;
+}
+
 // wave-private LDS hand-off: lanes' writes visible to the wave's later reads
 __device__ __forceinline__ void wave_lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -146,13 +199,14 @@ __global__ __launch_bounds__(256) void k_edge_mlp_fwd(EdgeGeo geo, const float* 
   float cnt = 0.f, mean[F], m2[F];
 #pragma unroll
   for (int k = 0; k < F; ++k) { mean[k] = 0.f; m2[k] = 0.f; }
-  CLASS_LOOP_BEGIN
+  EdgeStream<F, 1> es{{xe}, {}};
+  CLASS_LOOP_PF_BEGIN(es)
     pf_cptr W1f = pf_fresh(W1 + 2 * F);
     pf_cptr W2c = pf_fresh(W2T);
     pf_cptr b2f = pf_fresh(b2);
     pf_cptr ptc = pf_fresh(PtT + cn * H);
     float x[F];
-    load_x<F>(x, xe, xsc, xsh, eo, RB, fvalid);
+    affine_x<F>(x, cur.v[0], xsc, xsh, fvalid);
     // hidden unit by hidden unit: z_h -> a_h -> accumulated straight into y
     float yo[F];
 #pragma unroll
@@ -323,9 +377,10 @@ __global__ __launch_bounds__(256) void k_source_fwd(EdgeGeo geo, const float* __
 #pragma unroll
   for (int i = 0; i < 4 * C; ++i) S[i] = 0.f;
   float cnt = 0.f;
-  CLASS_LOOP_BEGIN
+  EdgeStream<F, 1> es{{y}, {}};
+  CLASS_LOOP_PF_BEGIN(es)
     float x[F], m[C];
-    load_x<F>(x, y, sc, sh, eo, RB, fvalid);
+    affine_x<F>(x, cur.v[0], sc, sh, fvalid);
     source_message<F>(x, QtT, cn, Ws1, Ws2T, bs2, m);
     const float nold = cnt;
     cnt += 1.f;
@@ -436,10 +491,11 @@ __global__ __launch_bounds__(256) void k_target_fwd(EdgeGeo geo, const float* __
   float rs[C];
 #pragma unroll
   for (int h = 0; h < C; ++h) rs[h] = fvalid ? Rs[(long long)h * NS + n] : 0.f;
-  CLASS_LOOP_BEGIN
+  EdgeStream<F, 1> es{{y}, {}};
+  CLASS_LOOP_PF_BEGIN(es)
     pf_cptr W1f = pf_fresh(Wt1 + F);
     float x[F];
-    load_x<F>(x, y, sc, sh, eo, RB, fvalid);
+    affine_x<F>(x, cur.v[0], sc, sh, fvalid);
 #pragma unroll
     for (int h = 0; h < C; ++h) {
       float z = rs[h];
@@ -480,11 +536,12 @@ __global__ __launch_bounds__(256) void k_target_bwd(EdgeGeo geo, const float* __
     rs[h] = fvalid ? Rs[(long long)h * NS + n] : 0.f;
     acc[h] = 0.f;
   }
-  CLASS_LOOP_BEGIN
+  EdgeStream<F, 1> es{{y}, {}};
+  CLASS_LOOP_PF_BEGIN(es)
     pf_cptr W1f = pf_fresh(Wt1 + F);
     pf_cptr ghc = pf_fresh(g_hsumT + cn * C);
     float x[F], gz[C];
-    load_x<F>(x, y, sc, sh, eo, RB, fvalid);
+    affine_x<F>(x, cur.v[0], sc, sh, fvalid);
 #pragma unroll
     for (int h = 0; h < C; ++h) {
       float z = rs[h];
@@ -559,14 +616,15 @@ __global__ __launch_bounds__(256) void k_source_bwd(
   float sg[F], sgx[F];
 #pragma unroll
   for (int k = 0; k < F; ++k) { sg[k] = 0.f; sgx[k] = 0.f; }
-  CLASS_LOOP_BEGIN
+  EdgeStream<F, 2> es{{y, g_next}, {}};
+  CLASS_LOOP_PF_BEGIN(es)
     pf_cptr W1f = pf_fresh(Ws1 + F);
     pf_cptr W2f = pf_fresh(Ws2);
     pf_cptr b2f = pf_fresh(bs2);
     pf_cptr qtc = pf_fresh(QtT + cn * C);
     float yv[F], x[F];
 #pragma unroll
-    for (int k = 0; k < F; ++k) yv[k] = ldEz(y, eo + (uint32_t)k * RB, fvalid);
+    for (int k = 0; k < F; ++k) yv[k] = fvalid ? cur.v[0][k] : 0.f;
     if (sc) {
       pf_cptr scf = pf_fresh(sc), shf = pf_fresh(sh);
 #pragma unroll
@@ -642,7 +700,7 @@ __global__ __launch_bounds__(256) void k_source_bwd(
     }
     if (g_next) {
 #pragma unroll
-      for (int k = 0; k < F; ++k) g[k] += ldEz(g_next, eo + (uint32_t)k * RB, fvalid);
+      for (int k = 0; k < F; ++k) g[k] += fvalid ? cur.v[1][k] : 0.f;
     }
     if (fvalid) {
 #pragma unroll
@@ -712,103 +770,221 @@ __global__ __launch_bounds__(256) void k_edge_bn_sums(EdgeGeo geo, const float* 
 }
 
 // ============================================================ EdgeModel bwd
+// Per class (one wave = 64 fibers): g_y = alpha*g + gam0 + gam1*y; the hidden
+// layer is walked in tiles of 16 units.  Pass 1 recomputes z1 -> a1 into a
+// [64][17] LDS tile and accumulates dW2|db2 += g_y (x) [a1, 1] on
+// v_mfma_f32_16x16x4_f32 (edge = K).  Pass 2 forms g_z1 tile by tile into the
+// same LDS tile: dW1[:,2F:3F] += g_z1 (x) x on MFMA, per-class sums of g_z1
+// (class-side gradient) from the tile, per-fiber sums in registers, and the
+// edge-input gradient g_xe = W1[:,2F:3F]^T g_z1.  Only x rows, g_y rows and
+// one tile live in LDS (10 KB per wave), so 3 blocks fit a CU.
+// LDS tiles are COLUMN-major, [column][LTC] with the 64 edges of the wave
+// contiguous (+4 pad): a lane writes one float per column (conflict-free) and
+// an MFMA operand lane (col, kq) reads its 16 K-steps as 4 ds_read_b128,
+// K-step st <-> edge kq*16 + st (any fixed edge<->K map works for A and B).
+#define LTC 68
+__device__ __forceinline__ void tile_k16(const float* T, int col, int kq, float (&v)[16]) {
+  const float4* p = reinterpret_cast<const float4*>(T + col * LTC + kq * 16);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float4 q = p[j];
+    v[4 * j] = q.x; v[4 * j + 1] = q.y; v[4 * j + 2] = q.z; v[4 * j + 3] = q.w;
+  }
+}
+// column (lane & 15) of a 64-row tile, summed; the 4 row quarters combined in
+// a fixed (commutative) order so every lane of the column holds the same sum
+__device__ __forceinline__ float tile_colsum(const float* T, int lane) {
+  float v[16];
+  tile_k16(T, lane & 15, lane >> 4, v);
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s += v[r];
+  s += __shfl_xor(s, 16);
+  s += __shfl_xor(s, 32);
+  return s;
+}
+
 template <int F>
 __global__ __launch_bounds__(256) void k_edge_mlp_bwd(
     EdgeGeo geo, const float* __restrict__ g_tot, const float* __restrict__ alpha,
     const float* __restrict__ gam0, const float* __restrict__ gam1, const float* __restrict__ y,
     const float* __restrict__ xe, const float* __restrict__ xsc, const float* __restrict__ xsh,
     const float* __restrict__ Ps, const float* __restrict__ PtT, const float* __restrict__ W1,
-    const float* __restrict__ W2, float* __restrict__ gxe, float* __restrict__ GzEs,
+    const float* __restrict__ W2T, float* __restrict__ gxe, float* __restrict__ GzEs,
     float* __restrict__ partW2, float* __restrict__ partW1, float* __restrict__ partCol) {
   constexpr int H = 4 * F;
-  using WG2 = WGrad<F, H + 1>;  // g_y (x) [a1, 1] -> dW2 | db2
-  using WG1 = WGrad<H, F>;      // g_z1 (x) x      -> dW1[:, 2F:3F] (+ per-class sums of g_z1)
-  constexpr int STAGE = WG2::LDS_FLOATS > WG1::LDS_FLOATS ? WG2::LDS_FLOATS : WG1::LDS_FLOATS;
-  constexpr int LOOP_N = 4 * STAGE + H * 64;
-  constexpr int TAIL0 = 4 * H * 64 > 4 * H * (F + 1) ? 4 * H * 64 : 4 * H * (F + 1);
-  constexpr int LDS_N = LOOP_N > TAIL0 ? LOOP_N : TAIL0;
+  constexpr int NT2 = (H + 1 + 15) / 16;  // tiles of [a1, 1]
+  constexpr int NT1 = (H + 15) / 16;      // tiles of g_z1
+  constexpr int WAVE_F = LTC * (16 + 2 * F);
+  constexpr int EPI_F = 4 * 16 * 64 > 4 * H * (F + 1) ? 4 * 16 * 64 : 4 * H * (F + 1);
+  constexpr int LDS_F = 4 * WAVE_F > EPI_F ? 4 * WAVE_F : EPI_F;
   EDGE_PROLOGUE
-  __shared__ float lds[LDS_N];
-  float* region = lds + wave * STAGE;
-  float* psl = lds + 4 * STAGE;
-  for (int idx = threadIdx.x; idx < H * 64; idx += PF_BLOCK) {
-    const int h = idx >> 6, l = idx & 63;
-    psl[idx] = l < nvalid ? Ps[(long long)h * NS + nbase + l] : 0.f;
+  __shared__ float4 psl[H / 4 * 64];
+  __shared__ float lds[LDS_F];
+  float* T = lds + wave * WAVE_F;  // [16][LTC] tile
+  float* Xr = T + 16 * LTC;         // [F][LTC] x rows
+  float* Gr = Xr + F * LTC;         // [F][LTC] g_y rows
+  for (int j = wave; j < H / 4; j += 4) {
+    float4 v;
+    v.x = Ps[(long long)(4 * j + 0) * NS + n];
+    v.y = Ps[(long long)(4 * j + 1) * NS + n];
+    v.z = Ps[(long long)(4 * j + 2) * NS + n];
+    v.w = Ps[(long long)(4 * j + 3) * NS + n];
+    psl[j * 64 + lane] = v;
   }
   __syncthreads();
-  WG2 wg2;
-  WG1 wg1;
-  wg2.zero();
-  wg1.zero();
-  float acc[H];
+  const int col = lane & 15, kq = lane >> 4;
+  floatx4 acc2[NT2], acc1[NT1];
 #pragma unroll
-  for (int h = 0; h < H; ++h) acc[h] = 0.f;
-  CLASS_LOOP_BEGIN
+  for (int i = 0; i < NT2; ++i) acc2[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < NT1; ++i) acc1[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float accF[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) accF[h] = 0.f;
+  EdgeStream<F, 3> es{{g_tot, y, xe}, {}};
+  CLASS_LOOP_PF_BEGIN(es)
     float gy[F], x[F];
     {
       pf_cptr al = pf_fresh(alpha), g0 = pf_fresh(gam0), g1 = pf_fresh(gam1);
 #pragma unroll
-      for (int k = 0; k < F; ++k) {
-        const float gt = ldE(g_tot, eo + (uint32_t)k * RB);
-        const float yk = ldE(y, eo + (uint32_t)k * RB);
-        gy[k] = fvalid ? fmaf(g1[k], yk, fmaf(al[k], gt, g0[k])) : 0.f;
+      for (int k = 0; k < F; ++k)
+        gy[k] = fvalid ? fmaf(g1[k], cur.v[1][k], fmaf(al[k], cur.v[0][k], g0[k])) : 0.f;
+    }
+    affine_x<F>(x, cur.v[2], xsc, xsh, fvalid);
+#pragma unroll
+    for (int k = 0; k < F; ++k) {
+      Xr[k * LTC + lane] = x[k];
+      Gr[k * LTC + lane] = gy[k];
+    }
+    // ---- pass 1: a1 tiles, dW2 | db2
+    uint32_t pos[(H + 31) / 32];
+#pragma unroll
+    for (int i = 0; i < (H + 31) / 32; ++i) pos[i] = 0u;
+    {
+      pf_cptr W1f = pf_fresh(W1 + 2 * F);
+      pf_cptr ptc = pf_fresh(PtT + cn * H);
+#pragma unroll
+      for (int tt = 0; tt < NT2; ++tt) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int h = 16 * tt + u;
+          float v;
+          if (h < H) {
+            const float4 p4 = psl[(h >> 2) * 64 + lane];
+            const float pv = (h & 3) == 0 ? p4.x : (h & 3) == 1 ? p4.y : (h & 3) == 2 ? p4.z : p4.w;
+            float z = pv + ptc[h];
+#pragma unroll
+            for (int k = 0; k < F; ++k) z = fmaf(W1f[h * H + k], x[k], z);
+            pos[h >> 5] |= (z > 0.f ? 1u : 0u) << (h & 31);
+            v = lrelu(z);
+          } else {
+            v = h == H ? 1.f : 0.f;   // ones column -> db2
+          }
+          T[u * LTC + lane] = v;
+        }
+        wave_lds_sync();
+        float av[16], bv[16];
+        tile_k16(Gr, col < F ? col : 0, kq, av);
+        tile_k16(T, col, kq, bv);
+#pragma unroll
+        for (int st = 0; st < 16; ++st)
+          acc2[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(col < F ? av[st] : 0.f, bv[st],
+                                                          acc2[tt], 0, 0, 0);
+        wave_lds_sync();
       }
     }
-    load_x<F>(x, xe, xsc, xsh, eo, RB, fvalid);
-    float* A = region;
-    float* B = region + 64 * WG2::LDA;
+    // ---- pass 2: g_z1 tiles, dW1, class sums, fiber sums, g_xe
+    float gx[F];
 #pragma unroll
-    for (int k = 0; k < F; ++k) A[lane * WG2::LDA + k] = gy[k];
-    pf_cptr W1f = pf_fresh(W1 + 2 * F);
-    pf_cptr ptc = pf_fresh(PtT + cn * H);
-    float z[H];
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      float s = psl[h * 64 + lane] + ptc[h];
-#pragma unroll
-      for (int k = 0; k < F; ++k) s = fmaf(W1f[h * H + k], x[k], s);
-      z[h] = s;
-      B[lane * WG2::LDB + h] = lrelu(s);
-    }
-    B[lane * WG2::LDB + H] = 1.f;
-    wave_lds_sync();
-    wg2.accum(region, lane);
-    wave_lds_sync();
-    pf_cptr W2g = pf_fresh(W2);
-    float gz[H];
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      float s = 0.f;
-#pragma unroll
-      for (int o = 0; o < F; ++o) s = fmaf(W2g[o * H + h], gy[o], s);
-      gz[h] = s * dlrelu(z[h]);
-      acc[h] += gz[h];
-    }
-    if (gxe) {
+    for (int k = 0; k < F; ++k) gx[k] = 0.f;
+    {
+      pf_cptr W2c = pf_fresh(W2T);
       pf_cptr W1g = pf_fresh(W1 + 2 * F);
-      float gx[F];
 #pragma unroll
-      for (int k = 0; k < F; ++k) {
-        float s = 0.f;
+      for (int tt = 0; tt < NT1; ++tt) {
 #pragma unroll
-        for (int h = 0; h < H; ++h) s = fmaf(W1g[h * H + k], gz[h], s);
-        gx[k] = s;
-      }
-      if (fvalid) {
+        for (int u = 0; u < 16; ++u) {
+          const int h = 16 * tt + u;
+          float g = 0.f;
+          if (h < H) {
+            float s = 0.f;
 #pragma unroll
-        for (int k = 0; k < F; ++k) stE(gxe, eo + (uint32_t)k * RB, gx[k]);
+            for (int o = 0; o < F; ++o) s = fmaf(W2c[h * F + o], gy[o], s);
+            g = ((pos[h >> 5] >> (h & 31)) & 1u) ? s : PF_LEAKY * s;
+            accF[h] += g;
+            if (gxe) {
+#pragma unroll
+              for (int k = 0; k < F; ++k) gx[k] = fmaf(W1g[h * H + k], g, gx[k]);
+            }
+          }
+          T[u * LTC + lane] = g;
+        }
+        wave_lds_sync();
+        float av[16], bv[16];
+        tile_k16(T, col, kq, av);
+        tile_k16(Xr, col < F ? col : 0, kq, bv);
+#pragma unroll
+        for (int st = 0; st < 16; ++st)
+          acc1[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[st], col < F ? bv[st] : 0.f,
+                                                          acc1[tt], 0, 0, 0);
+        const float cs = tile_colsum(T, lane);
+        if (lane < 16 && 16 * tt + lane < H)
+          partCol[(((size_t)gg * geo.NFG + fg) * geo.NC + c) * H + 16 * tt + lane] = cs;
+        wave_lds_sync();
       }
     }
-    wg1.stage(region, gz, x, lane);
-    wave_lds_sync();
-    wg1.accum(region, lane);
-    const float cs = column_sum_rows<H, WG1::LDA>(region, lane);   // per-class sum of g_z1
-    if (lane < H) partCol[(((size_t)gg * geo.NFG + fg) * geo.NC + c) * H + lane] = cs;
-    wave_lds_sync();
+    if (gxe && fvalid) {
+#pragma unroll
+      for (int k = 0; k < F; ++k) stE(gxe, eo + (uint32_t)k * RB, gx[k]);
+    }
   CLASS_LOOP_END
-  fiber_store<H>(acc, lds, wave, lane, nbase, nvalid, NS, GzEs + (size_t)ks * H * NS);
-  wg2.block_partial(lds, partW2 + (size_t)bx * F * (H + 1));
-  wg1.block_partial(lds, partW1 + (size_t)bx * H * F);
+  // ---- per-fiber sums over the block's classes (16 channels per round)
+  __syncthreads();
+#pragma unroll
+  for (int h0 = 0; h0 < H; h0 += 16) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (h0 + u < H) lds[(wave * 16 + u) * 64 + lane] = accF[h0 + u];
+    __syncthreads();
+    for (int idx = t; idx < 16 * 64; idx += PF_BLOCK) {
+      const int u = idx >> 6, l = idx & 63;
+      if (h0 + u < H && l < nvalid)
+        GzEs[(size_t)ks * H * NS + (long long)(h0 + u) * NS + nbase + l] =
+            ((lds[u * 64 + l] + lds[(16 + u) * 64 + l]) + lds[(32 + u) * 64 + l]) +
+            lds[(48 + u) * 64 + l];
+    }
+    __syncthreads();
+  }
+  // ---- block partials of dW2|db2 [F][H+1] and dW1 [H][F]
+  {
+    float* sc2 = lds;  // [4][F][H+1]
+#pragma unroll
+    for (int tt = 0; tt < NT2; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = 4 * kq + r, h = 16 * tt + col;
+        if (o < F && h <= H) sc2[(wave * F + o) * (H + 1) + h] = acc2[tt][r];
+      }
+    __syncthreads();
+    for (int idx = t; idx < F * (H + 1); idx += PF_BLOCK)
+      partW2[(size_t)bx * F * (H + 1) + idx] =
+          ((sc2[idx] + sc2[F * (H + 1) + idx]) + sc2[2 * F * (H + 1) + idx]) +
+          sc2[3 * F * (H + 1) + idx];
+    __syncthreads();
+    float* sc1 = lds;  // [4][H][F]
+#pragma unroll
+    for (int tt = 0; tt < NT1; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int h = 16 * tt + 4 * kq + r, k = col;
+        if (h < H && k < F) sc1[(wave * H + h) * F + k] = acc1[tt][r];
+      }
+    __syncthreads();
+    for (int idx = t; idx < H * F; idx += PF_BLOCK)
+      partW1[(size_t)bx * H * F + idx] =
+          ((sc1[idx] + sc1[H * F + idx]) + sc1[2 * H * F + idx]) + sc1[3 * H * F + idx];
+  }
 }
 
 // sum KS per-fiber partials [KS][C][NS] -> out[C][NS]
@@ -1084,10 +1260,11 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
   float* gs = fiber_dst(geo, H, GzEs, w);
   hipStream_t st = as_stream(stream);
   const float* PtT = class_rows(Pt, H, geo, w, st);
-  PF_REQUIRE(pW2 && pW1 && pCol && gs && PtT, "pfsgnn_edge_mlp_bwd", "workspace too small");
+  const float* W2T = transposed(W2, F, H, w, st);
+  PF_REQUIRE(pW2 && pW1 && pCol && gs && PtT && W2T, "pfsgnn_edge_mlp_bwd", "workspace too small");
   { pf::Timer tm_("edge_mlp_bwd", st);
   DISPATCH_F(F, hipLaunchKernelGGL(k_edge_mlp_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
-                                   g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, PtT, W1, W2, gxe,
+                                   g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, PtT, W1, W2T, gxe,
                                    gs, pW2, pW1, pCol));
   tm_.end(); }
   fiber_finish(geo, H, gs, GzEs, st);
