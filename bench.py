@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--blocks", type=int, default=8, help="message-passing rounds")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--no-graph", action="store_true",
+                    help="launch every kernel from Python instead of replaying a captured HIP graph")
     return ap.parse_args()
 
 
@@ -123,42 +125,87 @@ def main():
     gnn = pfsgnn.GNN(B=B, Fdim=FDIM, T=NC, F_s=1, F_t=2).to(device)
     gnn.train()
     broadcast_parameters(gnn)
-    opt = pfsgnn.FusedAdam(gnn.parameters(), lr=config.lr)
+    use_graph = not args.no_graph
+    opt = pfsgnn.FusedAdam(gnn.parameters(), lr=config.lr, capturable=use_graph)
     data, class_info = make_batch(G, rank, device)
     E = G * NF * NC
+    # softfloor's noise seed lives on the device and advances every step, so a
+    # replayed graph draws fresh noise each step (train.py:22 draws per call)
+    seed_t = torch.full((), 1000 * rank, dtype=torch.int64, device=device)
 
-    def step(i):
+    def fwd_bwd():
+        seed_t.add_(1)
         gnn.zero_grad()
         out = gnn(data)
-        loss, _ = loss_function(out, class_info, pclass=0.1, pfiber=0.1, sharpness=10.0, seed=i)
+        loss, _ = loss_function(out, class_info, pclass=0.1, pfiber=0.1, sharpness=10.0,
+                                seed=seed_t)
         loss.backward()
+        return loss
+
+    def step():
+        loss = fwd_bwd()
         allreduce_gradients(gnn)
         opt.step()
         return loss
 
     for i in range(args.warmup):
-        step(i)
+        step()
+    torch.cuda.synchronize()
+    graph = None
+    if use_graph:
+        # one training step captured as a HIP graph: forward, train.py loss,
+        # backward (+ Adam when there is no collective) replayed by the GPU
+        # command processor with no per-kernel host launch
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            step()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            static_loss = fwd_bwd()
+            if world == 1:
+                opt.step()
+        torch.cuda.synchronize()
+
+        def step():  # noqa: F811
+            graph.replay()
+            if world > 1:
+                allreduce_gradients(gnn)
+                opt.step()
+            return static_loss
+
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    native.timing_enable(True)
-    native.timing_reset()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        loss = step(args.warmup + i)
+        loss = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    native.timing_enable(False)
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     assert torch.isfinite(loss).item(), "non-finite loss"
+
+    # ---- per-kernel device times: HIP events around each main kernel, on its
+    # launch stream, over a few eager steps of the same workload right after
+    # the timed region (a replayed graph has no per-kernel host hook)
+    prof_steps = min(args.steps, 5)
+    native.timing_enable(True)
+    native.timing_reset()
+    for i in range(prof_steps):
+        loss_p = fwd_bwd()
+        allreduce_gradients(gnn)
+        opt.step()
+    torch.cuda.synchronize()
+    native.timing_enable(False)
 
     # ---- per-kernel times (HIP events on the launch stream, timed region only)
     per_edge = kernel_bytes_per_edge(FDIM)
@@ -178,7 +225,7 @@ def main():
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                 "avg_launch_us": round(avg_s * 1e6, 1), "launches": n,
                 "bytes_per_launch": int(launches_bytes),
-                "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kt.items()}}
+                "kernel_ms_per_step": {k: round(v[0] / prof_steps, 3) for k, v in kt.items()}}
 
     if rank == 0:
         cpu = None

@@ -156,11 +156,14 @@ int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_tot, const 
  * train.py:29-80: decoder_e (gnn.py:307) + softplus + softfloor (train.py:21)
  * + scatters per class / fiber.  ci = class_info [>=2][NT] (row 0 = T_i,
  * row 1 = N_i).  Noise uniforms come from a counter-based hash of
- * (seed, edge).  tt (optional) = per-edge allocated time [E]. */
+ * (seed, edge); seed_dev (optional, device uint64) overrides `seed` so a
+ * captured graph draws fresh noise per replay.  tt (optional) = per-edge
+ * allocated time [E] in train.py's fiber-major order. */
 int pfsgnn_loss_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                     const float* sh, const float* Wd1, const float* bd1, const float* Wd2,
                     const float* bd2, const float* ci, float scale, float sharpness,
-                    float noiselevel, unsigned long long seed, float* n_prime,
+                    float noiselevel, unsigned long long seed,
+                    const unsigned long long* seed_dev, float* n_prime,
                     float* fiber_time, float* tmean, float* tvar, float* tt,
                     void* ws, size_t ws_bytes, void* stream);
 int pfsgnn_loss_finalize(int G, int NF, int NC, const float* n_prime, const float* fiber_time,
@@ -172,7 +175,8 @@ int pfsgnn_loss_finalize(int G, int NF, int NC, const float* n_prime, const floa
 int pfsgnn_loss_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                     const float* sh, const float* Wd1, const float* bd1, const float* Wd2,
                     const float* bd2, const float* ci, float scale, float sharpness,
-                    float noiselevel, unsigned long long seed, const float* Gn,
+                    float noiselevel, unsigned long long seed,
+                    const unsigned long long* seed_dev, const float* Gn,
                     const float* Gf, const float* Gv, const float* tmean, const float* gscale,
                     float* dWd1, float* dbd1, float* dWd2, float* dbd2, float* gxe,
                     void* ws, size_t ws_bytes, void* stream);
@@ -199,9 +203,11 @@ int pfsgnn_edges_from_canonical(const float* y, const float* sc, const float* sh
                                 float* dst, void* stream);
 
 /* ---------------------------------------------------------------- optimiser
- * torch.optim.Adam (amsgrad=False, maximize=False) over one flat buffer. */
-int pfsgnn_adam(float* p, const float* g, float* m, float* v, long long n, int step, float lr,
-                float beta1, float beta2, float eps, float weight_decay, void* stream);
+ * torch.optim.Adam (amsgrad=False, maximize=False) over one flat buffer.
+ * step_dev (optional, device float) overrides `step` (capturable form). */
+int pfsgnn_adam(float* p, const float* g, float* m, float* v, long long n, int step,
+                const float* step_dev, float lr, float beta1, float beta2, float eps,
+                float weight_decay, void* stream);
 
 #ifdef __cplusplus
 }

@@ -209,6 +209,9 @@ __host__ __device__ __forceinline__ uint64_t pf_fmix64(uint64_t z) {
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
+__host__ __device__ __forceinline__ uint64_t pf_noise_key(uint64_t seed) {
+  return pf_fmix64(seed ^ 0xD1B54A32D192ED03ull);
+}
 __device__ __forceinline__ float pf_uniform(uint64_t key, uint64_t e) {
   const uint64_t z = pf_fmix64(key + (e + 1ull) * 0x9E3779B97F4A7C15ull);
   return (float)(z >> 40) * (1.0f / 16777216.0f);

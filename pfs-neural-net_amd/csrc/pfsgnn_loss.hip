@@ -86,11 +86,13 @@ __global__ __launch_bounds__(256) void k_loss_fwd(EdgeGeo geo, const float* __re
                                                   const float* __restrict__ Wd2,
                                                   const float* __restrict__ bd2,
                                                   const float* __restrict__ ci, float scale,
-                                                  SoftFloor sf, float noiselevel, uint64_t key,
+                                                  SoftFloor sf, float noiselevel, uint64_t key0,
+                                                  const unsigned long long* __restrict__ seed_dev,
                                                   float* __restrict__ fiber_time,
                                                   float* __restrict__ tt_out,
                                                   float* __restrict__ part) {
   EDGE_PROLOGUE
+  const uint64_t key = seed_dev ? pf_noise_key(*seed_dev) : key0;
   __shared__ float scratch[4 * 64];
   float ft = 0.f;
   const float nw = (float)nvalid;
@@ -217,7 +219,8 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
                                                   const float* __restrict__ Wd2,
                                                   const float* __restrict__ bd2,
                                                   const float* __restrict__ ci, float scale,
-                                                  SoftFloor sf, float noiselevel, uint64_t key,
+                                                  SoftFloor sf, float noiselevel, uint64_t key0,
+                                                  const unsigned long long* __restrict__ seed_dev,
                                                   const float* __restrict__ Gn,
                                                   const float* __restrict__ Gf,
                                                   const float* __restrict__ Gv,
@@ -228,6 +231,7 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
                                                   float* __restrict__ partV) {
   using WG = WGrad<F, F + 1>;  // g_zd (x) [x, 1] -> dWd1 | dbd1
   EDGE_PROLOGUE
+  const uint64_t key = seed_dev ? pf_noise_key(*seed_dev) : key0;
   constexpr int LDS_N = (4 * WG::LDS_FLOATS > 4 * F * (F + 1)) ? 4 * WG::LDS_FLOATS
                                                                 : 4 * F * (F + 1);
   __shared__ float lds[LDS_N + 4 * (F + 1)];
@@ -403,15 +407,12 @@ int check_dims(const char* where, int G, int NF, int NC, int F) {
   }
 }  // namespace
 
-static uint64_t noise_key(unsigned long long seed) {
-  return pf_fmix64((uint64_t)seed ^ 0xD1B54A32D192ED03ull);
-}
 
 extern "C" int pfsgnn_loss_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                                const float* sh, const float* Wd1, const float* bd1,
                                const float* Wd2, const float* bd2, const float* ci, float scale,
                                float sharpness, float noiselevel, unsigned long long seed,
-                               float* n_prime, float* fiber_time, float* tmean, float* tvar,
+                               const unsigned long long* seed_dev, float* n_prime, float* fiber_time, float* tmean, float* tvar,
                                float* tt, void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_loss_fwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(y && Wd1 && bd1 && Wd2 && bd2 && ci && n_prime && fiber_time && tmean && tvar,
@@ -423,10 +424,10 @@ extern "C" int pfsgnn_loss_fwd(int G, int NF, int NC, int F, const float* y, con
   PF_REQUIRE(part && ftp, "pfsgnn_loss_fwd", "workspace too small");
   hipStream_t st = as_stream(stream);
   const SoftFloor sf = make_softfloor(sharpness);
-  const uint64_t key = noise_key(seed);
+  const uint64_t key = pf_noise_key((uint64_t)seed);
   { pf::Timer tm_("loss_fwd", st);
   DISPATCH_F(F, hipLaunchKernelGGL(k_loss_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
-                                   sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sf, noiselevel, key,
+                                   sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sf, noiselevel, key, seed_dev,
                                    ftp, tt, part));
   tm_.end(); }
   if (geo.KS > 1)
@@ -456,7 +457,8 @@ extern "C" int pfsgnn_loss_bwd(int G, int NF, int NC, int F, const float* y, con
                                const float* sh, const float* Wd1, const float* bd1,
                                const float* Wd2, const float* bd2, const float* ci, float scale,
                                float sharpness, float noiselevel, unsigned long long seed,
-                               const float* Gn, const float* Gf, const float* Gv,
+                               const unsigned long long* seed_dev, const float* Gn,
+                               const float* Gf, const float* Gv,
                                const float* tmean, const float* gscale, float* dWd1, float* dbd1,
                                float* dWd2, float* dbd2, float* gxe, void* ws, size_t ws_bytes,
                                void* stream) {
@@ -472,10 +474,10 @@ extern "C" int pfsgnn_loss_bwd(int G, int NF, int NC, int F, const float* y, con
   PF_REQUIRE(pW && pV, "pfsgnn_loss_bwd", "workspace too small");
   hipStream_t st = as_stream(stream);
   const SoftFloor sf = make_softfloor(sharpness);
-  const uint64_t key = noise_key(seed);
+  const uint64_t key = pf_noise_key((uint64_t)seed);
   { pf::Timer tm_("loss_bwd", st);
   DISPATCH_F(F, hipLaunchKernelGGL(k_loss_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y, sc,
-                                   sh, Wd1, bd1, Wd2, bd2, ci, scale, sf, noiselevel, key, Gn, Gf,
+                                   sh, Wd1, bd1, Wd2, bd2, ci, scale, sf, noiselevel, key, seed_dev, Gn, Gf,
                                    Gv, tmean, gscale, gxe, pW, pV));
   tm_.end(); }
   launch_reduce_rows(pW, nb, (size_t)F * (F + 1), F + 1, F, F, dWd1, F, 1, 1.f, st);

@@ -755,10 +755,19 @@ extern "C" int pfsgnn_moment_coef(const float* mom, const float* gst, int C, int
 // torch.optim.Adam single-tensor semantics (torch/optim/adam.py
 // _single_tensor_adam, amsgrad=False): bias corrections on the host in double.
 __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                       float* __restrict__ v, long long n, float neg_step, float beta1, float beta2,
-                       float bc2_sqrt, float eps, float wd) {
+                       float* __restrict__ v, long long n, float neg_step0, float beta1, float beta2,
+                       float bc2_sqrt0, float eps, float wd, float lr,
+                       const float* __restrict__ step_dev) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  float neg_step = neg_step0, bc2_sqrt = bc2_sqrt0;
+  if (step_dev) {  // capturable form: the step count lives on the device
+    const double st = (double)*step_dev;
+    const double bc1 = 1.0 - pow((double)beta1, st);
+    const double bc2 = 1.0 - pow((double)beta2, st);
+    neg_step = (float)(-(double)lr / bc1);
+    bc2_sqrt = (float)sqrt(bc2);
+  }
   float gi = g[i];
   if (wd != 0.f) gi = gi + wd * p[i];
   const float mo = m[i];
@@ -771,14 +780,17 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
 }
 
 extern "C" int pfsgnn_adam(float* p, const float* g, float* m, float* v, long long n, int step,
-                           float lr, float beta1, float beta2, float eps, float weight_decay,
-                           void* stream) {
-  PF_REQUIRE(p && g && m && v && n > 0 && step >= 1, "pfsgnn_adam", "bad arguments");
-  const double bc1 = 1.0 - std::pow((double)beta1, step);
-  const double bc2 = 1.0 - std::pow((double)beta2, step);
+                           const float* step_dev, float lr, float beta1, float beta2, float eps,
+                           float weight_decay, void* stream) {
+  PF_REQUIRE(p && g && m && v && n > 0 && (step >= 1 || step_dev), "pfsgnn_adam",
+             "bad arguments");
+  const int st = step >= 1 ? step : 1;
+  const double bc1 = 1.0 - std::pow((double)beta1, st);
+  const double bc2 = 1.0 - std::pow((double)beta2, st);
   const float neg_step = (float)(-(double)lr / bc1);
   const float bc2_sqrt = (float)std::sqrt(bc2);
   hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream),
-                     p, g, m, v, n, neg_step, beta1, beta2, bc2_sqrt, eps, weight_decay);
+                     p, g, m, v, n, neg_step, beta1, beta2, bc2_sqrt, eps, weight_decay, lr,
+                     step_dev);
   return pf::check_launch("pfsgnn_adam");
 }

@@ -296,6 +296,23 @@ class _FlatMixin(_ParamMixin):
                     p.grad = sl.view(p.shape)
         return {n: p.grad for n, p in self.named_parameters()}
 
+    def zero_grad(self, set_to_none=True):
+        """Zero the flat gradient buffer in one kernel and keep every ``p.grad``
+        attached to it (the buffer the fused backward accumulates into, the
+        all-reduce and FusedAdam read).  Dead parameters thus carry zero rather
+        than None gradients; with Adam's moments starting at zero that leaves
+        them exactly unchanged, as the reference's skipped None grads do.  No
+        host sync and no reallocation, so the step can be graph-captured."""
+        gflat = getattr(self, "_pf_gflat", None)
+        if gflat is not None:
+            params = [p for _, p in self.named_parameters()]
+            if len(params) == len(self._pf_off) and all(
+                    p.grad is not None and p.grad.data_ptr() == gflat.data_ptr() + 4 * off
+                    for p, (off, n) in zip(params, self._pf_off)):
+                gflat.zero_()
+                return
+        super().zero_grad(set_to_none=set_to_none)
+
     def flat_parameters(self):
         """(flat params, flat grads) -- the buffers FusedAdam / DDP operate on."""
         self._flat_sync()

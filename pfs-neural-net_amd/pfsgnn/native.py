@@ -56,14 +56,14 @@ _SIGS = {
     "pfsgnn_source_bwd": ([I, I, I, I] + [P] * 22 + [P, SZ, P], I),
     "pfsgnn_edge_bn_grad_sums": ([I, I, I, I, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_edge_mlp_bwd": ([I, I, I, I] + [P] * 18 + [P, SZ, P], I),
-    "pfsgnn_loss_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, FL, FL, ULL, P, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_loss_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, FL, FL, ULL, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_loss_finalize": ([I, I, I, P, P, P, P, FL, FL, FL, FL, FL, FL, P, P, P, P, P, P, P], I),
-    "pfsgnn_loss_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, FL, FL, ULL, P, P, P, P, P,
+    "pfsgnn_loss_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, FL, FL, ULL, P, P, P, P, P, P,
                          P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_layout_analyze": ([P, LL, I, I, I, P, P, P, SZ, P], I),
     "pfsgnn_edges_to_canonical": ([P, I, I, I, I, I, P, P, P], I),
     "pfsgnn_edges_from_canonical": ([P, P, P, I, I, I, I, I, P, I, P, P], I),
-    "pfsgnn_adam": ([P, P, P, P, LL, I, FL, FL, FL, FL, FL, P], I),
+    "pfsgnn_adam": ([P, P, P, P, LL, I, P, FL, FL, FL, FL, FL, P], I),
 }
 
 
@@ -375,6 +375,15 @@ class HipBackend:
         return out
 
     # ------------------------------------------------------------ loss
+    def _seed_args(self, seed):
+        """(value, device pointer): a device int64 tensor is read by the kernels
+        (graph-capturable: each replay sees its current value)."""
+        if isinstance(seed, torch.Tensor):
+            if not seed.is_cuda or seed.dtype != torch.int64 or seed.numel() != 1:
+                raise ValueError("a tensor seed must be one int64 on the device")
+            return 0, seed.data_ptr()
+        return int(seed) & ((1 << 64) - 1), None
+
     def loss_fwd(self, d, y, sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sharpness, noiselevel, seed,
                  want_time=False):
         n_prime, fiber_time = self.empty(d.NT), self.empty(d.NS)
@@ -384,7 +393,7 @@ class HipBackend:
         ws, wsb = self._wsargs(d)
         _call("pfsgnn_loss_fwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
               Wd1.data_ptr(), bd1.data_ptr(), Wd2.data_ptr(), bd2.data_ptr(), ci.data_ptr(),
-              float(scale), float(sharpness), float(noiselevel), int(seed) & ((1 << 64) - 1),
+              float(scale), float(sharpness), float(noiselevel), *self._seed_args(seed),
               n_prime.data_ptr(), fiber_time.data_ptr(), tmean.data_ptr(), tvar.data_ptr(),
               _ptr(tt), ws, wsb, _stream())
         return n_prime, fiber_time, tmean, tvar, tt
@@ -412,7 +421,7 @@ class HipBackend:
         ws, wsb = self._wsargs(d)
         _call("pfsgnn_loss_bwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
               Wd1.data_ptr(), bd1.data_ptr(), Wd2.data_ptr(), bd2.data_ptr(), ci.data_ptr(),
-              float(scale), float(sharpness), float(noiselevel), int(seed) & ((1 << 64) - 1),
+              float(scale), float(sharpness), float(noiselevel), *self._seed_args(seed),
               Gn.data_ptr(), Gf.data_ptr(), Gv.data_ptr(), tmean.data_ptr(), _ptr(gs),
               dWd1.data_ptr(), dbd1.data_ptr(), dWd2.data_ptr(), dbd2.data_ptr(), gxe.data_ptr(),
               ws, wsb, _stream())
@@ -449,7 +458,15 @@ class HipBackend:
         return out
 
     def adam(self, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay):
+        """``step``: int, or a device float tensor holding the (already
+        incremented) step count (capturable form)."""
         self._chk(p, g, m, v)
+        if isinstance(step, torch.Tensor):
+            if not step.is_cuda or step.dtype != torch.float32 or step.numel() != 1:
+                raise ValueError("a tensor step must be one float32 on the device")
+            sval, sptr = 0, step.data_ptr()
+        else:
+            sval, sptr = int(step), None
         _call("pfsgnn_adam", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
-              int(step), float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
+              sval, sptr, float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
               _stream())

@@ -29,9 +29,15 @@ def _flat_base(tensors):
 
 
 class FusedAdam(torch.optim.Optimizer):
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+    """``capturable=True`` keeps the step count on the device (as torch's
+    capturable Adam does), so ``step()`` issues no host sync and can be
+    captured in a HIP graph: each replay increments the count and the kernel
+    derives the bias corrections from it."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 capturable=False):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
-                        maximize=False)
+                        maximize=False, capturable=capturable)
         super().__init__(params, defaults)
         self._flat = {}
 
@@ -55,8 +61,12 @@ class FusedAdam(torch.optim.Optimizer):
                 st = self.state.get(p)
                 if st and "step" in st:
                     step = int(st["step"])
+            if group.get("capturable", False):
+                step_t = torch.full((), float(step), dtype=torch.float32, device=pb[0].device)
+            else:
+                step_t = None
             for p, off in zip(ps, pb[1]):
-                self.state[p] = {"step": torch.tensor(float(step)),
+                self.state[p] = {"step": step_t if step_t is not None else torch.tensor(float(step)),
                                  "exp_avg": m[off:off + p.numel()].view(p.shape),
                                  "exp_avg_sq": v[off:off + p.numel()].view(p.shape)}
             cache = (m, v)
@@ -76,6 +86,12 @@ class FusedAdam(torch.optim.Optimizer):
             if flat is not None:
                 p, g, m, v = flat
                 st0 = self.state[group["params"][0]]
+                if group.get("capturable", False):
+                    step_t = st0["step"]          # one device tensor shared by the group
+                    step_t.add_(1.0)
+                    be.adam(p, g, m, v, step_t, group["lr"], beta1, beta2, group["eps"],
+                            group["weight_decay"])
+                    continue
                 step = int(st0["step"]) + 1
                 be.adam(p, g, m, v, step, group["lr"], beta1, beta2, group["eps"],
                         group["weight_decay"])

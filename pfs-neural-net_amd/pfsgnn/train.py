@@ -88,7 +88,10 @@ def loss_function(graph, class_info, pclass=0.1, pfiber=1.0, sharpness=0.5, fina
     loss is the sum of the per-graph losses.  The reference reads the model
     from a global ``gnn`` (train.py:42); here it comes with the graph (or
     ``gnn=``).  Edge order must be the fiber-major layout train.py builds
-    (train.py:94), on which train.py:40 and :67 rely."""
+    (train.py:94), on which train.py:40 and :67 rely.  ``seed`` (softfloor's
+    noise): None draws one from torch's CPU generator; an int; or a device
+    int64 tensor read in-kernel (a captured step then draws fresh noise per
+    replay when the tensor is advanced on the device)."""
     pf = getattr(graph, "_pf", None)
     if pf is None or pf[3] is not graph.x_e:
         raise NotImplementedError("loss_function needs the BipartiteData returned by "
@@ -102,8 +105,10 @@ def loss_function(graph, class_info, pclass=0.1, pfiber=1.0, sharpness=0.5, fina
     ci = _class_info_cm(class_info, d)
     if seed is None:
         seed = draw_seed()
+    elif not isinstance(seed, torch.Tensor):
+        seed = int(seed)
     outs = _LossFn.apply(x_e, model.encoder_s[0].weight, model, d, ectx, xe3, ci, float(sharpness),
-                         int(seed), float(pclass), float(pfiber), bool(finaloutput))
+                         seed, float(pclass), float(pfiber), bool(finaloutput))
     loss, utils_g, n_prime, fiber_time, variance = outs[:5]
     if not finaloutput:
         return loss, utils_g.sum() if d.G > 1 else utils_g[0]
