@@ -1083,7 +1083,7 @@ extern "C" size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F) {
   edge = std::max(edge, nb * (F * (H + 1) + H * F) + colp * H + ks * H * NS + 4096);  // edge bwd
   edge = std::max(edge, colp * 4 + ks * NS + nb * (F * (F + 1) + F + 1) + 4096);   // loss
   edge += (size_t)geo.NT * (H + 2 * C) + 4 * H * H + 8 * 256;  // class_rows / transposed
-  size_t node = (size_t)128 * 161 * 161 + 4096;                                     // wgrad splits
+  size_t node = (size_t)512 * 161 * 161 + 4096;                                     // wgrad splits
   size_t lay = (size_t)geo.E + 1024;                                                // layout counts
   return (std::max(std::max(edge, node), lay) + 64 * 16) * sizeof(float) + 16 * 256;
 }

@@ -114,28 +114,44 @@ extern "C" const char* pfsgnn_version(void) { return "pfsgnn 0.1 gfx950"; }
 // One 64-lane wave per output element: lane l sums partials l, l+64, ... in
 // order, then a fixed butterfly -- deterministic, and every lane's loads are
 // independent (no serial chain over the blocks).
+// out[r][c] (+)= scale * sum_b part[b*plen + r*ldp + c].  A block owns 16
+// consecutive outputs x 16 partial lanes: thread (o, pl) sums partials
+// b = pl, pl+16, ... with 4 independent accumulators (4 loads in flight), the
+// 16 lanes are then combined in a fixed order -- deterministic for a given nb.
 __global__ __launch_bounds__(256) void k_reduce_rows(const float* __restrict__ part, int nb,
                                                      size_t plen, int ldp, int rows, int cols,
                                                      float* __restrict__ out, int ldo, int add,
                                                      float scale) {
-  const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (idx >= rows * cols) return;
-  const int r = idx / cols, c = idx - r * cols;
+  const int t = threadIdx.x, o = t & 15, pl = t >> 4;
+  const int idx = blockIdx.x * 16 + o;
+  const bool v = idx < rows * cols;
+  const int r = v ? idx / cols : 0, c = v ? idx - r * cols : 0;
   const float* p = part + (size_t)r * ldp + c;
-  float s = 0.f;
-  for (int b = lane; b < nb; b += 64) s += p[(size_t)b * plen];
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if (lane == 0) {
-    float* o = out + (size_t)r * ldo + c;
-    *o = add ? (*o + scale * s) : scale * s;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int b = pl;
+  for (; b + 48 < nb; b += 64) {
+    s0 += p[(size_t)b * plen];
+    s1 += p[(size_t)(b + 16) * plen];
+    s2 += p[(size_t)(b + 32) * plen];
+    s3 += p[(size_t)(b + 48) * plen];
+  }
+  for (; b < nb; b += 16) s0 += p[(size_t)b * plen];
+  __shared__ float sh[16][17];
+  sh[pl][o] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (t < 16 && v) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += sh[i][t];
+    float* op = out + (size_t)r * ldo + c;
+    *op = add ? (*op + scale * s) : scale * s;
   }
 }
 
 void launch_reduce_rows(const float* part, int nb, size_t plen, int ldp, int rows, int cols,
                         float* out, int ldo, int add, float scale, hipStream_t st) {
   const int len = rows * cols;
-  hipLaunchKernelGGL(k_reduce_rows, dim3((len + 3) / 4), dim3(256), 0, st, part, nb, plen, ldp,
+  hipLaunchKernelGGL(k_reduce_rows, dim3((len + 15) / 16), dim3(256), 0, st, part, nb, plen, ldp,
                      rows, cols, out, ldo, add, scale);
 }
 
@@ -160,208 +176,229 @@ void launch_reduce_columns(const float* part, int G, int BPG, int NC, int C, flo
                      NC, C, out);
 }
 
-// ---------------------------------------------------------------- lin
-// One thread per column n, LIN_MB output rows per thread.  The K loop runs in
-// chunks of 8: the 8 input values of the column are loaded together (8 loads
-// in flight per thread instead of one dependent load per k), the weights are
-// wave-uniform rows read with s_load.
-#define LIN_MB 16
-#define LIN_KC 8
-__global__ __launch_bounds__(256) void k_lin(const float* __restrict__ W, int ldw, int M, int K,
-                                             const float* __restrict__ X, int N,
-                                             const float* __restrict__ b, float bscale, int act_in,
-                                             float* __restrict__ Y, int add) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  const int m0 = blockIdx.y * LIN_MB;
-  const int nc = n < N ? n : N - 1;
-  const int mrows = min(LIN_MB, M - m0);
-  float acc[LIN_MB];
+// ---------------------------------------------------------------- lin / lin_t
+// Y[Mo][N] (+)= op(W)[Mo][Ki] . act(X)[Ki][N] (+ bscale*b) (* lrelu'(Z)) on
+// v_mfma_f32_16x16x4_f32: a wave owns 16 node columns and every output row
+// (MT tiles of 16), the node column is the MFMA N index, the input channel
+// the K index.  op(W) is staged per block in LDS in K-chunks of 32 (rows =
+// output channel) -- W for lin, W^T for lin_t; the 8 X loads of a chunk are
+// issued together.
+#define GK 32
+template <int MT>
+__global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ W, int ldw, int trans,
+                                              int Mo, int Ki, const float* __restrict__ X, int N,
+                                              const float* __restrict__ b, float bscale,
+                                              int act_in, const float* __restrict__ Z,
+                                              float* __restrict__ Y, int add) {
+  __shared__ float Ws[MT * 16][GK + 1];
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63, col = lane & 15, kq = lane >> 4;
+  const int n = blockIdx.x * 64 + wave * 16 + col;
+  const bool nv = n < N;
+  const int nc = nv ? n : N - 1;
+  floatx4 acc[MT];
 #pragma unroll
-  for (int i = 0; i < LIN_MB; ++i) acc[i] = 0.f;
-  int k = 0;
-  for (; k + LIN_KC <= K; k += LIN_KC) {
-    float xv[LIN_KC];
+  for (int i = 0; i < MT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int kc = 0; kc < Ki; kc += GK) {
+    const int kn = min(GK, Ki - kc);
+    __syncthreads();
+    for (int idx = t; idx < MT * 16 * GK; idx += 256) {
+      const int m = idx / GK, kk = idx - m * GK;
+      float v = 0.f;
+      if (m < Mo && kk < kn)
+        v = trans ? W[(size_t)(kc + kk) * ldw + m] : W[(size_t)m * ldw + kc + kk];
+      Ws[m][kk] = v;
+    }
+    __syncthreads();
+    float bv[GK / 4];
 #pragma unroll
-    for (int j = 0; j < LIN_KC; ++j) xv[j] = X[(size_t)(k + j) * N + nc];
-    if (act_in) {
-#pragma unroll
-      for (int j = 0; j < LIN_KC; ++j) xv[j] = lrelu(xv[j]);
+    for (int s = 0; s < GK / 4; ++s) {
+      const int kk = 4 * s + kq;
+      float v = 0.f;
+      if (kk < kn) v = X[(size_t)(kc + kk) * N + nc];
+      bv[s] = act_in ? lrelu(v) : v;
     }
 #pragma unroll
-    for (int i = 0; i < LIN_MB; ++i) {
-      if (i < mrows) {
-        pf_cptr w = pf_fresh(W + (size_t)(m0 + i) * ldw + k);
+    for (int s = 0; s < GK / 4; ++s) {
+      if (4 * s < kn) {
 #pragma unroll
-        for (int j = 0; j < LIN_KC; ++j) acc[i] = fmaf(w[j], xv[j], acc[i]);
+        for (int mt = 0; mt < MT; ++mt)
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ws[16 * mt + col][4 * s + kq], bv[s],
+                                                         acc[mt], 0, 0, 0);
       }
     }
   }
-  for (; k < K; ++k) {
-    float x = X[(size_t)k * N + nc];
-    if (act_in) x = lrelu(x);
+  if (!nv) return;
 #pragma unroll
-    for (int i = 0; i < LIN_MB; ++i)
-      if (i < mrows) acc[i] = fmaf(W[(size_t)(m0 + i) * ldw + k], x, acc[i]);
-  }
-  if (n >= N) return;
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-  for (int i = 0; i < LIN_MB; ++i) {
-    if (i < mrows) {
-      const int m = m0 + i;
-      float v = acc[i];
-      if (b) v += bscale * b[m];
-      float* o = Y + (size_t)m * N + n;
-      *o = add ? (*o + v) : v;
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * mt + 4 * kq + r;
+      if (row < Mo) {
+        float v = acc[mt][r];
+        if (b) v += bscale * b[row];
+        if (Z) v *= dlrelu(Z[(size_t)row * N + n]);
+        float* o = Y + (size_t)row * N + n;
+        *o = add ? (*o + v) : v;
+      }
     }
+}
+
+static int launch_gemm(const float* W, int ldw, int trans, int Mo, int Ki, const float* X, int N,
+                       const float* b, float bscale, int act_in, const float* Z, float* Y, int add,
+                       hipStream_t st, const char* where) {
+  const int MT = (Mo + 15) / 16;
+  dim3 grid((N + 63) / 64);
+#define PF_GEMM(T) \
+  case T: hipLaunchKernelGGL(k_gemm<T>, grid, dim3(256), 0, st, W, ldw, trans, Mo, Ki, X, N, b, \
+                             bscale, act_in, Z, Y, add); break;
+  switch (MT) {
+    PF_GEMM(1) PF_GEMM(2) PF_GEMM(3) PF_GEMM(4) PF_GEMM(5) PF_GEMM(6) PF_GEMM(7) PF_GEMM(8)
+    PF_GEMM(9) PF_GEMM(10) PF_GEMM(11)
+    default: return pf::fail(where, "output width > 176 not supported");
   }
+#undef PF_GEMM
+  return pf::check_launch(where);
 }
 
 extern "C" int pfsgnn_lin(const float* W, int ldw, int M, int K, const float* X, int N,
                           const float* b, float bscale, int act_in, float* Y, int add,
                           void* stream) {
   PF_REQUIRE(W && X && Y && M > 0 && K > 0 && N > 0, "pfsgnn_lin", "bad arguments");
-  dim3 grid((N + 255) / 256, (M + LIN_MB - 1) / LIN_MB);
-  hipLaunchKernelGGL(k_lin, grid, dim3(256), 0, as_stream(stream), W, ldw, M, K, X, N, b, bscale,
-                     act_in, Y, add);
-  return pf::check_launch("pfsgnn_lin");
-}
-
-__global__ __launch_bounds__(256) void k_lin_t(const float* __restrict__ W, int ldw, int M, int K,
-                                               const float* __restrict__ dY, int N,
-                                               const float* __restrict__ Z,
-                                               float* __restrict__ out, int add) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  const int k0 = blockIdx.y * LIN_MB;
-  const int nc = n < N ? n : N - 1;
-  const int kcols = min(LIN_MB, K - k0);
-  float acc[LIN_MB];
-#pragma unroll
-  for (int i = 0; i < LIN_MB; ++i) acc[i] = 0.f;
-  int m = 0;
-  for (; m + LIN_KC <= M; m += LIN_KC) {
-    float g[LIN_KC];
-#pragma unroll
-    for (int j = 0; j < LIN_KC; ++j) g[j] = dY[(size_t)(m + j) * N + nc];
-#pragma unroll
-    for (int j = 0; j < LIN_KC; ++j) {
-      pf_cptr w = pf_fresh(W + (size_t)(m + j) * ldw + k0);
-#pragma unroll
-      for (int i = 0; i < LIN_MB; ++i)
-        if (i < kcols) acc[i] = fmaf(w[i], g[j], acc[i]);
-    }
-  }
-  for (; m < M; ++m) {
-    const float g = dY[(size_t)m * N + nc];
-#pragma unroll
-    for (int i = 0; i < LIN_MB; ++i)
-      if (i < kcols) acc[i] = fmaf(W[(size_t)m * ldw + k0 + i], g, acc[i]);
-  }
-  if (n >= N) return;
-#pragma unroll
-  for (int i = 0; i < LIN_MB; ++i) {
-    if (i < kcols) {
-      const int k = k0 + i;
-      float v = acc[i];
-      if (Z) v *= dlrelu(Z[(size_t)k * N + n]);
-      float* o = out + (size_t)k * N + n;
-      *o = add ? (*o + v) : v;
-    }
-  }
+  return launch_gemm(W, ldw, 0, M, K, X, N, b, bscale, act_in, nullptr, Y, add,
+                     as_stream(stream), "pfsgnn_lin");
 }
 
 extern "C" int pfsgnn_lin_t(const float* W, int ldw, int M, int K, const float* dY, int N,
                             const float* Z, float* out, int add, void* stream) {
   PF_REQUIRE(W && dY && out && M > 0 && K > 0 && N > 0, "pfsgnn_lin_t", "bad arguments");
-  dim3 grid((N + 255) / 256, (K + LIN_MB - 1) / LIN_MB);
-  hipLaunchKernelGGL(k_lin_t, grid, dim3(256), 0, as_stream(stream), W, ldw, M, K, dY, N, Z, out,
-                     add);
-  return pf::check_launch("pfsgnn_lin_t");
+  // out[K][N] = W^T[K][M] . dY[M][N]
+  return launch_gemm(W, ldw, 1, K, M, dY, N, nullptr, 1.f, 0, Z, out, add, as_stream(stream),
+                     "pfsgnn_lin_t");
 }
 
 // ---------------------------------------------------------------- wgrad
 // dW[m][k] += sum_n dY[m][n] act(X[k][n]) and (optionally) db[m] += s*sum_n dY[m][n]
-// as one more column k = K of ones.  Output tiles of 16x16 on
-// v_mfma_f32_16x16x4_f32 with the node index as the MFMA K dimension; the N
-// range is split over blocks (per-block partials + deterministic reduce).  A
-// wave walks its chunk 4 MFMAs at a time with all 8 loads issued first.
-#define WG_CHUNK 512
-__global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ dY, int M,
+// as one more column k = K of ones.  A block owns a node range; it stages 64
+// nodes at a time in LDS, transposed ([n][m], [n][k]: one coalesced read of
+// dY and X per block), and its 4 waves own output tiles wave, wave+4, ... of
+// the [M][K1] result, accumulated on v_mfma_f32_16x16x4_f32 with the node as
+// the K index.  Per-block partials + a fixed-order reduce (deterministic).
+#define WG_WAVES 8
+// wave w owns output tiles w, w + 8, ... (TMAX slots) of the MT x KT grid
+template <int TMAX>
+__global__ __launch_bounds__(512) void k_wgrad(const float* __restrict__ dY, int M,
                                                const float* __restrict__ X, int K, int K1,
-                                               int N, int act_in, int tilesK, int chunk,
+                                               int N, int act_in, int chunk,
                                                float* __restrict__ part) {
-  const int tile = blockIdx.x;
-  const int tm = tile / tilesK, tk = tile - tm * tilesK;
-  const int split = blockIdx.y;
-  const int c0 = split * chunk;
-  const int c1 = min(N, c0 + chunk);
-  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  const int row = tm * 16 + (lane & 15);  // m for A operand
-  const int colk = tk * 16 + (lane & 15); // k for B operand
-  const int kq = lane >> 4;
-  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-  const bool rv = row < M, cv = colk < K, ones = colk == K && K1 > K;
-  const float* dyr = dY + (size_t)(rv ? row : 0) * N;
-  const float* xr = X + (size_t)(cv ? colk : 0) * N;
-  // per MFMA step the 4 waves x 4 lane groups cover 16 consecutive n; the
-  // loop bounds are wave-uniform (MFMA needs every lane)
-  int wb = c0 + 4 * wave;
-  for (; wb + 63 < c1; wb += 64) {
-    float a[4], bb[4];
+  extern __shared__ float sm[];
+  const int LM = M | 1, LK = K1 | 1;
+  float* Sd = sm;
+  float* Sx = sm + 64 * LM;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63, col = lane & 15, kq = lane >> 4;
+  const int KT = (K1 + 15) / 16, NTILE = ((M + 15) / 16) * KT;
+  const int n0 = blockIdx.x * chunk, n1 = min(N, n0 + chunk);
+  floatx4 acc[TMAX];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      a[u] = dyr[wb + kq + 16 * u];
-      bb[u] = xr[wb + kq + 16 * u];
+  for (int j = 0; j < TMAX; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int c = n0; c < n1; c += 64) {
+    __syncthreads();
+    for (int idx = t; idx < M * 64; idx += 64 * WG_WAVES) {
+      const int m = idx >> 6, nn = idx & 63;
+      Sd[nn * LM + m] = (c + nn < n1) ? dY[(size_t)m * N + c + nn] : 0.f;
     }
+    for (int idx = t; idx < K1 * 64; idx += 64 * WG_WAVES) {
+      const int k = idx >> 6, nn = idx & 63;
+      float v = 0.f;
+      if (c + nn < n1) {
+        if (k < K) {
+          v = X[(size_t)k * N + c + nn];
+          if (act_in) v = lrelu(v);
+        } else {
+          v = 1.f;
+        }
+      }
+      Sx[nn * LK + k] = v;
+    }
+    __syncthreads();
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      float bv = act_in ? lrelu(bb[u]) : bb[u];
-      bv = cv ? bv : (ones ? 1.f : 0.f);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(rv ? a[u] : 0.f, bv, acc, 0, 0, 0);
+    for (int j = 0; j < TMAX; ++j) {
+      const int tile = wave + WG_WAVES * j;
+      if (tile < NTILE) {
+        const int mt = tile / KT, kt = tile - mt * KT;
+        const int m = 16 * mt + col, k = 16 * kt + col;
+        const float* pa = Sd + (m < M ? m : 0);
+        const float* pb = Sx + (k < K1 ? k : 0);
+        const bool ma = m < M, mb = k < K1;
+#pragma unroll 4
+        for (int st = 0; st < 16; ++st) {
+          const int q = 4 * st + kq;
+          const float av = ma ? pa[q * LM] : 0.f;
+          const float bv = mb ? pb[q * LK] : 0.f;
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j], 0, 0, 0);
+        }
+      }
     }
   }
-  for (; wb < c1; wb += 16) {
-    const int n = wb + kq;
-    const bool nv = n < c1;
-    const float a = (rv && nv) ? dyr[n] : 0.f;
-    float bv = (cv && nv) ? xr[n] : 0.f;
-    if (act_in) bv = lrelu(bv);
-    if (ones) bv = nv ? 1.f : 0.f;
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc, 0, 0, 0);
-  }
-  __shared__ float red[4][16][16];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) red[wave][4 * (lane >> 4) + r][lane & 15] = acc[r];
-  __syncthreads();
-  // part layout [split][M][K1]
-  const int i = t >> 4, j = t & 15;
-  const int m = tm * 16 + i, k = tk * 16 + j;
-  if (m < M && k < K1) {
-    const float s = ((red[0][i][j] + red[1][i][j]) + red[2][i][j]) + red[3][i][j];
-    part[(size_t)split * M * K1 + (size_t)m * K1 + k] = s;
+  for (int j = 0; j < TMAX; ++j) {
+    const int tile = wave + WG_WAVES * j;
+    if (tile < NTILE) {
+      const int mt = tile / KT, kt = tile - mt * KT;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * mt + 4 * kq + r, k = 16 * kt + col;
+        if (m < M && k < K1)
+          part[(size_t)blockIdx.x * M * K1 + (size_t)m * K1 + k] = acc[j][r];
+      }
+    }
   }
 }
 
-static int wgrad_splits(int N) {
-  int s = (N + WG_CHUNK - 1) / WG_CHUNK;
-  return std::max(1, std::min(s, 128));
+static int wgrad_blocks(int N) {
+  int s = (N + 127) / 128;
+  return std::max(1, std::min(s, 512));
 }
 
 extern "C" int pfsgnn_wgrad(const float* dY, int M, const float* X, int K, int N, int act_in,
                             float* dW, int lddw, float* db, float dbscale, void* ws,
                             size_t ws_bytes, void* stream) {
   PF_REQUIRE(dY && X && dW && M > 0 && K > 0 && N > 0, "pfsgnn_wgrad", "bad arguments");
+  PF_REQUIRE(M <= 256 && K <= 256, "pfsgnn_wgrad", "M, K too large");
   hipStream_t st = as_stream(stream);
-  const int splits = wgrad_splits(N);
+  const int nbk = wgrad_blocks(N);
   const int K1 = K + (db ? 1 : 0);
-  const size_t need = (size_t)splits * M * K1 * sizeof(float);
+  const size_t need = (size_t)nbk * M * K1 * sizeof(float);
   PF_REQUIRE(ws && ws_bytes >= need, "pfsgnn_wgrad", "workspace too small");
-  const int chunk = (N + splits - 1) / splits;
-  const int tilesM = (M + 15) / 16, tilesK = (K1 + 15) / 16;
+  const int chunk = ((N + nbk - 1) / nbk + 63) / 64 * 64;
+  const int nblk = (N + chunk - 1) / chunk;
   float* part = reinterpret_cast<float*>(ws);
-  hipLaunchKernelGGL(k_wgrad, dim3(tilesM * tilesK, splits), dim3(256), 0, st, dY, M, X, K, K1, N,
-                     act_in, tilesK, chunk, part);
-  launch_reduce_rows(part, splits, (size_t)M * K1, K1, M, K, dW, lddw, 1, 1.f, st);
-  if (db) launch_reduce_rows(part + K, splits, (size_t)M * K1, K1, M, 1, db, 1, 1, dbscale, st);
+  const size_t lds = (size_t)64 * ((M | 1) + (K1 | 1)) * sizeof(float);
+  const int ntile = ((M + 15) / 16) * ((K1 + 15) / 16);
+  static bool attr_set = false;
+  if (!attr_set) {  // Fdim 16 stages up to ~83 KB of the CU's 160 KB LDS
+    const void* fns[4] = {reinterpret_cast<const void*>(&k_wgrad<1>),
+                          reinterpret_cast<const void*>(&k_wgrad<2>),
+                          reinterpret_cast<const void*>(&k_wgrad<8>),
+                          reinterpret_cast<const void*>(&k_wgrad<16>)};
+    for (const void* f : fns)
+      if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+          hipSuccess)
+        return pf::fail("pfsgnn_wgrad", "hipFuncSetAttribute");
+    attr_set = true;
+  }
+  const dim3 grid(nblk), blk(64 * WG_WAVES);
+  if (ntile <= WG_WAVES)
+    hipLaunchKernelGGL(k_wgrad<1>, grid, blk, lds, st, dY, M, X, K, K1, N, act_in, chunk, part);
+  else if (ntile <= 2 * WG_WAVES)
+    hipLaunchKernelGGL(k_wgrad<2>, grid, blk, lds, st, dY, M, X, K, K1, N, act_in, chunk, part);
+  else if (ntile <= 8 * WG_WAVES)
+    hipLaunchKernelGGL(k_wgrad<8>, grid, blk, lds, st, dY, M, X, K, K1, N, act_in, chunk, part);
+  else if (ntile <= 16 * WG_WAVES)
+    hipLaunchKernelGGL(k_wgrad<16>, grid, blk, lds, st, dY, M, X, K, K1, N, act_in, chunk, part);
+  else
+    return pf::fail("pfsgnn_wgrad", "too many output tiles");
+  launch_reduce_rows(part, nblk, (size_t)M * K1, K1, M, K, dW, lddw, 1, 1.f, st);
+  if (db) launch_reduce_rows(part + K, nblk, (size_t)M * K1, K1, M, 1, db, 1, 1, dbscale, st);
   return pf::check_launch("pfsgnn_wgrad");
 }
 
