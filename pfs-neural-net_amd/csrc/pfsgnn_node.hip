@@ -148,31 +148,87 @@ __global__ __launch_bounds__(256) void k_reduce_rows(const float* __restrict__ p
   }
 }
 
+// Stage 1 of a long reduction, in place: segment s of SEG partials is summed
+// (fixed order) into the segment's first partial row.  Every block reads and
+// writes only its own (segment, 16 outputs) cells.
+#define RED_SEG 128
+__global__ __launch_bounds__(256) void k_reduce_seg(float* __restrict__ part, int nb, size_t plen,
+                                                    int ldp, int rows, int cols) {
+  const int t = threadIdx.x, o = t & 15, pl = t >> 4;
+  const int idx = blockIdx.x * 16 + o;
+  const bool v = idx < rows * cols;
+  const int r = v ? idx / cols : 0, c = v ? idx - r * cols : 0;
+  const int b0 = blockIdx.y * RED_SEG, b1 = min(nb, b0 + RED_SEG);
+  float* p = part + (size_t)r * ldp + c;
+  float s0 = 0.f, s1 = 0.f;
+  int b = b0 + pl;
+  for (; b + 16 < b1; b += 32) {
+    s0 += p[(size_t)b * plen];
+    s1 += p[(size_t)(b + 16) * plen];
+  }
+  if (b < b1) s0 += p[(size_t)b * plen];
+  __shared__ float sh[16][17];
+  sh[pl][o] = s0 + s1;
+  __syncthreads();
+  if (t < 16 && v) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += sh[i][t];
+    p[(size_t)b0 * plen] = s;
+  }
+}
+
 void launch_reduce_rows(const float* part, int nb, size_t plen, int ldp, int rows, int cols,
                         float* out, int ldo, int add, float scale, hipStream_t st) {
   const int len = rows * cols;
+  if (nb > 2 * RED_SEG) {  // long: segment sums first (more loads in flight), in place
+    const int S = (nb + RED_SEG - 1) / RED_SEG;
+    hipLaunchKernelGGL(k_reduce_seg, dim3((len + 15) / 16, S), dim3(256), 0, st,
+                       const_cast<float*>(part), nb, plen, ldp, rows, cols);
+    nb = S;
+    plen *= RED_SEG;
+  }
   hipLaunchKernelGGL(k_reduce_rows, dim3((len + 15) / 16), dim3(256), 0, st, part, nb, plen, ldp,
                      rows, cols, out, ldo, add, scale);
 }
 
-__global__ void k_reduce_columns(const float* __restrict__ part, int G, int BPG, int NC, int C,
-                                 float* __restrict__ out) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over G*NC*C
+// per-class sums over the BPG fiber groups of a graph: out[i][g*NC + c] =
+// sum_b part[((g*BPG + b)*NC + c)*C + i]; 16 outputs x 16 partial lanes per
+// block, fixed-order combine (deterministic)
+__global__ __launch_bounds__(256) void k_reduce_columns(const float* __restrict__ part, int G,
+                                                        int BPG, int NC, int C,
+                                                        float* __restrict__ out) {
+  const int t = threadIdx.x, o = t & 15, pl = t >> 4;
+  const int idx = blockIdx.x * 16 + o;  // over G*NC*C, i fastest
   const int total = G * NC * C;
-  if (idx >= total) return;
-  const int g = idx / (NC * C);
-  const int rem = idx - g * NC * C;  // c*C + i
-  const int c = rem / C, i = rem - c * C;
-  float s = 0.f;
+  const bool v = idx < total;
+  const int ii = v ? idx : 0;
+  const int g = ii / (NC * C);
+  const int rem = ii - g * NC * C;
   const float* p = part + (size_t)g * BPG * NC * C + rem;
-  for (int b = 0; b < BPG; ++b) s += p[(size_t)b * NC * C];
-  out[(size_t)i * G * NC + (size_t)g * NC + c] = s;
+  float s0 = 0.f, s1 = 0.f;
+  int b = pl;
+  for (; b + 16 < BPG; b += 32) {
+    s0 += p[(size_t)b * NC * C];
+    s1 += p[(size_t)(b + 16) * NC * C];
+  }
+  if (b < BPG) s0 += p[(size_t)b * NC * C];
+  __shared__ float sh[16][17];
+  sh[pl][o] = s0 + s1;
+  __syncthreads();
+  if (t < 16 && v) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += sh[k][t];
+    const int c = rem / C, i = rem - c * C;
+    out[(size_t)i * G * NC + (size_t)g * NC + c] = s;
+  }
 }
 
 void launch_reduce_columns(const float* part, int G, int BPG, int NC, int C, float* out,
                            hipStream_t st) {
   const int total = G * NC * C;
-  hipLaunchKernelGGL(k_reduce_columns, dim3((total + 255) / 256), dim3(256), 0, st, part, G, BPG,
+  hipLaunchKernelGGL(k_reduce_columns, dim3((total + 15) / 16), dim3(256), 0, st, part, G, BPG,
                      NC, C, out);
 }
 
