@@ -74,6 +74,24 @@ def kernel_bytes_per_edge(F, first_block_excluded=False):
     }
 
 
+def pmc_traffic(kernel, E, F):
+    """HBM bytes per launch of `kernel` from the latest committed PMC pass
+    (profiles/<round>_traffic.json, made by tools/prof_pmc.sh +
+    tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE passes, FETCH
+    calibrated on k_edge_bn_sums), or None.  rocprofv3 cannot run inside the
+    process it profiles, so bench.py reads the pass rather than measuring it."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        key = f"k_{kernel}<{F}>"
+        if d.get("E") == E and d.get("F") == F and key in d.get("kernels", {}):
+            return d["kernels"][key]["traffic_bytes"], os.path.basename(path)
+    return None
+
+
 def cpu_baseline(blocks, seconds):
     """The CPU oracle (oracle/, torch on the host cores) timed on a bounded sample
     of the same workload: ONE 2394x128 graph, full training step incl. Adam."""
@@ -221,8 +239,11 @@ def main():
         launches_bytes = (per_edge[dom] * (B - 1) + 3 * 4 * FDIM) * E / B
     avg_s = ms / n / 1e3
     achieved = launches_bytes / avg_s / 1e9
+    tr = pmc_traffic(dom, E, FDIM)
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None if tr is None else int(tr[0]),
+                "traffic_source": None if tr is None else f"profiles/{tr[1]} (PMC bytes per launch)",
                 "avg_launch_us": round(avg_s * 1e6, 1), "launches": n,
                 "bytes_per_launch": int(launches_bytes),
                 "kernel_ms_per_step": {k: round(v[0] / prof_steps, 3) for k, v in kt.items()}}
