@@ -220,6 +220,18 @@ __device__ __forceinline__ float pf_uniform(uint64_t key, uint64_t e) {
 // ------------------------------------------------------------ reduce kernels
 // out[r*ldo + c] (+)= scale * sum_{b<nb} part[b*plen + r*ldp + c] -- finishes
 // every per-block partial deterministically (fixed block order).
+// One pending partial reduction; up to PF_MAX_RED of them share one launch.
+struct RedDesc {
+  const float* part;
+  int nb;
+  size_t plen;
+  int ldp, rows, cols;
+  float* out;
+  int ldo, add;
+  float scale;
+};
+#define PF_MAX_RED 4
+void launch_reduce_multi(const RedDesc* d, int n, hipStream_t st);
 void launch_reduce_rows(const float* part, int nb, size_t plen, int ldp, int rows, int cols,
                         float* out, int ldo, int add, float scale, hipStream_t st);
 // Column partials [G][NFG][NC][C] -> channel-major node tensor out[C][G*NC].

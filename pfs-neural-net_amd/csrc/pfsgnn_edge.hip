@@ -1208,14 +1208,15 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
                                    sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT, g_next,
                                    mu1, inv1, g_tot, pW2, pW1, pCol, pBN));
   tm_.end(); }
-  launch_reduce_rows(pW2, nb, (size_t)C * (C + 1), C + 1, C, C, dWs2, C, 1, 1.f, st);
-  launch_reduce_rows(pW2 + C, nb, (size_t)C * (C + 1), C + 1, C, 1, dbs2, 1, 1, 1.f, st);
-  launch_reduce_rows(pW1, nb, (size_t)C * F, F, C, F, dWs1 + F, C, 1, 1.f, st);
-  launch_reduce_columns(pCol, G, geo.NFG, NC, C, GzS, st);
-  if (mu1) {
-    launch_reduce_rows(pBN, nb, (size_t)2 * F, F, 1, F, Sg, F, 0, 1.f, st);
-    launch_reduce_rows(pBN + F, nb, (size_t)2 * F, F, 1, F, Sgx, F, 0, 1.f, st);
+  {
+    RedDesc rd[5] = {{pW2, (int)nb, (size_t)C * (C + 1), C + 1, C, C, dWs2, C, 1, 1.f},
+                     {pW2 + C, (int)nb, (size_t)C * (C + 1), C + 1, C, 1, dbs2, 1, 1, 1.f},
+                     {pW1, (int)nb, (size_t)C * F, F, C, F, dWs1 + F, C, 1, 1.f},
+                     {pBN, (int)nb, (size_t)2 * F, F, 1, F, Sg, F, 0, 1.f},
+                     {pBN + F, (int)nb, (size_t)2 * F, F, 1, F, Sgx, F, 0, 1.f}};
+    launch_reduce_multi(rd, mu1 ? 5 : 3, st);
   }
+  launch_reduce_columns(pCol, G, geo.NFG, NC, C, GzS, st);
   return pf::check_launch("pfsgnn_source_bwd");
 }
 
@@ -1234,8 +1235,11 @@ extern "C" int pfsgnn_edge_bn_grad_sums(int G, int NF, int NC, int F, const floa
   DISPATCH_F(F, hipLaunchKernelGGL(k_edge_bn_sums<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, g,
                                    y, mu1, inv1, pBN));
   tm_.end(); }
-  launch_reduce_rows(pBN, geo.nblocks, (size_t)2 * F, F, 1, F, Sg, F, 0, 1.f, st);
-  launch_reduce_rows(pBN + F, geo.nblocks, (size_t)2 * F, F, 1, F, Sgx, F, 0, 1.f, st);
+  {
+    RedDesc rd[2] = {{pBN, geo.nblocks, (size_t)2 * F, F, 1, F, Sg, F, 0, 1.f},
+                     {pBN + F, geo.nblocks, (size_t)2 * F, F, 1, F, Sgx, F, 0, 1.f}};
+    launch_reduce_multi(rd, 2, st);
+  }
   return pf::check_launch("pfsgnn_edge_bn_grad_sums");
 }
 
@@ -1268,9 +1272,12 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
                                    gs, pW2, pW1, pCol));
   tm_.end(); }
   fiber_finish(geo, H, gs, GzEs, st);
-  launch_reduce_rows(pW2, nb, (size_t)F * (H + 1), H + 1, F, H, dW2, H, 1, 1.f, st);
-  launch_reduce_rows(pW2 + H, nb, (size_t)F * (H + 1), H + 1, F, 1, db2, 1, 1, 1.f, st);
-  launch_reduce_rows(pW1, nb, (size_t)H * F, F, H, F, dW1 + 2 * F, H, 1, 1.f, st);
+  {
+    RedDesc rd[3] = {{pW2, (int)nb, (size_t)F * (H + 1), H + 1, F, H, dW2, H, 1, 1.f},
+                     {pW2 + H, (int)nb, (size_t)F * (H + 1), H + 1, F, 1, db2, 1, 1, 1.f},
+                     {pW1, (int)nb, (size_t)H * F, F, H, F, dW1 + 2 * F, H, 1, 1.f}};
+    launch_reduce_multi(rd, 3, st);
+  }
   launch_reduce_columns(pCol, G, geo.NFG, NC, H, GzEt, st);
   return pf::check_launch("pfsgnn_edge_mlp_bwd");
 }

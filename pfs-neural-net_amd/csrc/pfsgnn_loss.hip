@@ -480,10 +480,13 @@ extern "C" int pfsgnn_loss_bwd(int G, int NF, int NC, int F, const float* y, con
                                    sh, Wd1, bd1, Wd2, bd2, ci, scale, sf, noiselevel, key, seed_dev, Gn, Gf,
                                    Gv, tmean, gscale, gxe, pW, pV));
   tm_.end(); }
-  launch_reduce_rows(pW, nb, (size_t)F * (F + 1), F + 1, F, F, dWd1, F, 1, 1.f, st);
-  launch_reduce_rows(pW + F, nb, (size_t)F * (F + 1), F + 1, F, 1, dbd1, 1, 1, 1.f, st);
-  launch_reduce_rows(pV, nb, (size_t)(F + 1), F, 1, F, dWd2, F, 1, 1.f, st);
-  launch_reduce_rows(pV + F, nb, (size_t)(F + 1), 1, 1, 1, dbd2, 1, 1, 1.f, st);
+  {
+    RedDesc rd[4] = {{pW, (int)nb, (size_t)F * (F + 1), F + 1, F, F, dWd1, F, 1, 1.f},
+                     {pW + F, (int)nb, (size_t)F * (F + 1), F + 1, F, 1, dbd1, 1, 1, 1.f},
+                     {pV, (int)nb, (size_t)(F + 1), F, 1, F, dWd2, F, 1, 1.f},
+                     {pV + F, (int)nb, (size_t)(F + 1), 1, 1, 1, dbd2, 1, 1, 1.f}};
+    launch_reduce_multi(rd, 4, st);
+  }
   return pf::check_launch("pfsgnn_loss_bwd");
 }
 

@@ -114,28 +114,36 @@ extern "C" const char* pfsgnn_version(void) { return "pfsgnn 0.1 gfx950"; }
 // One 64-lane wave per output element: lane l sums partials l, l+64, ... in
 // order, then a fixed butterfly -- deterministic, and every lane's loads are
 // independent (no serial chain over the blocks).
-// out[r][c] (+)= scale * sum_b part[b*plen + r*ldp + c].  A block owns 16
-// consecutive outputs x 16 partial lanes: thread (o, pl) sums partials
-// b = pl, pl+16, ... with 4 independent accumulators (4 loads in flight), the
-// 16 lanes are then combined in a fixed order -- deterministic for a given nb.
-__global__ __launch_bounds__(256) void k_reduce_rows(const float* __restrict__ part, int nb,
-                                                     size_t plen, int ldp, int rows, int cols,
-                                                     float* __restrict__ out, int ldo, int add,
-                                                     float scale) {
+// Partial reductions out[r][c] (+)= scale * sum_b part[b*plen + r*ldp + c],
+// up to PF_MAX_RED independent ones per launch (blockIdx.z picks one).  A block
+// owns 16 consecutive outputs x 16 partial lanes: thread (o, pl) sums partials
+// b = pl, pl+16, ... with 4 independent accumulators (4 loads in flight); the
+// 16 lanes are combined in a fixed order -- deterministic for a given nb.
+// Long lists (nb > 256) first take an in-place stage: segment s of RED_SEG
+// partials is summed into the segment's first row (each block touches only its
+// own cells; the descriptors of one launch never share cells).
+#define RED_SEG 128
+struct RedPack {
+  RedDesc d[PF_MAX_RED];
+};
+
+__global__ __launch_bounds__(256) void k_reduce_rows(RedPack pk) {
+  const RedDesc& D = pk.d[blockIdx.z];
   const int t = threadIdx.x, o = t & 15, pl = t >> 4;
   const int idx = blockIdx.x * 16 + o;
-  const bool v = idx < rows * cols;
-  const int r = v ? idx / cols : 0, c = v ? idx - r * cols : 0;
-  const float* p = part + (size_t)r * ldp + c;
+  if (blockIdx.x * 16 >= D.rows * D.cols) return;
+  const bool v = idx < D.rows * D.cols;
+  const int r = v ? idx / D.cols : 0, c = v ? idx - r * D.cols : 0;
+  const float* p = D.part + (size_t)r * D.ldp + c;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   int b = pl;
-  for (; b + 48 < nb; b += 64) {
-    s0 += p[(size_t)b * plen];
-    s1 += p[(size_t)(b + 16) * plen];
-    s2 += p[(size_t)(b + 32) * plen];
-    s3 += p[(size_t)(b + 48) * plen];
+  for (; b + 48 < D.nb; b += 64) {
+    s0 += p[(size_t)b * D.plen];
+    s1 += p[(size_t)(b + 16) * D.plen];
+    s2 += p[(size_t)(b + 32) * D.plen];
+    s3 += p[(size_t)(b + 48) * D.plen];
   }
-  for (; b < nb; b += 16) s0 += p[(size_t)b * plen];
+  for (; b < D.nb; b += 16) s0 += p[(size_t)b * D.plen];
   __shared__ float sh[16][17];
   sh[pl][o] = (s0 + s1) + (s2 + s3);
   __syncthreads();
@@ -143,30 +151,28 @@ __global__ __launch_bounds__(256) void k_reduce_rows(const float* __restrict__ p
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) s += sh[i][t];
-    float* op = out + (size_t)r * ldo + c;
-    *op = add ? (*op + scale * s) : scale * s;
+    float* op = D.out + (size_t)r * D.ldo + c;
+    *op = D.add ? (*op + D.scale * s) : D.scale * s;
   }
 }
 
-// Stage 1 of a long reduction, in place: segment s of SEG partials is summed
-// (fixed order) into the segment's first partial row.  Every block reads and
-// writes only its own (segment, 16 outputs) cells.
-#define RED_SEG 128
-__global__ __launch_bounds__(256) void k_reduce_seg(float* __restrict__ part, int nb, size_t plen,
-                                                    int ldp, int rows, int cols) {
+__global__ __launch_bounds__(256) void k_reduce_seg(RedPack pk) {
+  const RedDesc& D = pk.d[blockIdx.z];
   const int t = threadIdx.x, o = t & 15, pl = t >> 4;
   const int idx = blockIdx.x * 16 + o;
-  const bool v = idx < rows * cols;
-  const int r = v ? idx / cols : 0, c = v ? idx - r * cols : 0;
-  const int b0 = blockIdx.y * RED_SEG, b1 = min(nb, b0 + RED_SEG);
-  float* p = part + (size_t)r * ldp + c;
+  const int b0 = blockIdx.y * RED_SEG;
+  if (blockIdx.x * 16 >= D.rows * D.cols || b0 >= D.nb || D.nb <= 2 * RED_SEG) return;
+  const bool v = idx < D.rows * D.cols;
+  const int r = v ? idx / D.cols : 0, c = v ? idx - r * D.cols : 0;
+  const int b1 = min(D.nb, b0 + RED_SEG);
+  float* p = const_cast<float*>(D.part) + (size_t)r * D.ldp + c;
   float s0 = 0.f, s1 = 0.f;
   int b = b0 + pl;
   for (; b + 16 < b1; b += 32) {
-    s0 += p[(size_t)b * plen];
-    s1 += p[(size_t)(b + 16) * plen];
+    s0 += p[(size_t)b * D.plen];
+    s1 += p[(size_t)(b + 16) * D.plen];
   }
-  if (b < b1) s0 += p[(size_t)b * plen];
+  if (b < b1) s0 += p[(size_t)b * D.plen];
   __shared__ float sh[16][17];
   sh[pl][o] = s0 + s1;
   __syncthreads();
@@ -174,22 +180,40 @@ __global__ __launch_bounds__(256) void k_reduce_seg(float* __restrict__ part, in
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) s += sh[i][t];
-    p[(size_t)b0 * plen] = s;
+    p[(size_t)b0 * D.plen] = s;
+  }
+}
+
+void launch_reduce_multi(const RedDesc* d, int n, hipStream_t st) {
+  for (int i0 = 0; i0 < n; i0 += PF_MAX_RED) {
+    const int m = std::min(PF_MAX_RED, n - i0);
+    RedPack pk{};
+    int gx = 1, gy = 1;
+    bool seg = false;
+    for (int i = 0; i < m; ++i) {
+      pk.d[i] = d[i0 + i];
+      gx = std::max(gx, (pk.d[i].rows * pk.d[i].cols + 15) / 16);
+      if (pk.d[i].nb > 2 * RED_SEG) {
+        seg = true;
+        gy = std::max(gy, (pk.d[i].nb + RED_SEG - 1) / RED_SEG);
+      }
+    }
+    if (seg) {
+      hipLaunchKernelGGL(k_reduce_seg, dim3(gx, gy, m), dim3(256), 0, st, pk);
+      for (int i = 0; i < m; ++i)
+        if (pk.d[i].nb > 2 * RED_SEG) {
+          pk.d[i].nb = (pk.d[i].nb + RED_SEG - 1) / RED_SEG;
+          pk.d[i].plen *= RED_SEG;
+        }
+    }
+    hipLaunchKernelGGL(k_reduce_rows, dim3(gx, 1, m), dim3(256), 0, st, pk);
   }
 }
 
 void launch_reduce_rows(const float* part, int nb, size_t plen, int ldp, int rows, int cols,
                         float* out, int ldo, int add, float scale, hipStream_t st) {
-  const int len = rows * cols;
-  if (nb > 2 * RED_SEG) {  // long: segment sums first (more loads in flight), in place
-    const int S = (nb + RED_SEG - 1) / RED_SEG;
-    hipLaunchKernelGGL(k_reduce_seg, dim3((len + 15) / 16, S), dim3(256), 0, st,
-                       const_cast<float*>(part), nb, plen, ldp, rows, cols);
-    nb = S;
-    plen *= RED_SEG;
-  }
-  hipLaunchKernelGGL(k_reduce_rows, dim3((len + 15) / 16), dim3(256), 0, st, part, nb, plen, ldp,
-                     rows, cols, out, ldo, add, scale);
+  RedDesc d{part, nb, plen, ldp, rows, cols, out, ldo, add, scale};
+  launch_reduce_multi(&d, 1, st);
 }
 
 // per-class sums over the BPG fiber groups of a graph: out[i][g*NC + c] =
@@ -453,8 +477,11 @@ extern "C" int pfsgnn_wgrad(const float* dY, int M, const float* X, int K, int N
     hipLaunchKernelGGL(k_wgrad<16>, grid, blk, lds, st, dY, M, X, K, K1, N, act_in, chunk, part);
   else
     return pf::fail("pfsgnn_wgrad", "too many output tiles");
-  launch_reduce_rows(part, nblk, (size_t)M * K1, K1, M, K, dW, lddw, 1, 1.f, st);
-  if (db) launch_reduce_rows(part + K, nblk, (size_t)M * K1, K1, M, 1, db, 1, 1, dbscale, st);
+  {
+    RedDesc rd[2] = {{part, nblk, (size_t)M * K1, K1, M, K, dW, lddw, 1, 1.f},
+                     {part + K, nblk, (size_t)M * K1, K1, M, 1, db, 1, 1, dbscale}};
+    launch_reduce_multi(rd, db ? 2 : 1, st);
+  }
   return pf::check_launch("pfsgnn_wgrad");
 }
 
