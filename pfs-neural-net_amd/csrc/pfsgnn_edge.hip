@@ -804,6 +804,24 @@ __device__ __forceinline__ float tile_colsum(const float* T, int lane) {
   return s;
 }
 
+// acc += A^T B over the wave's 64 edges from two column tiles (valid columns
+// col < na / col < nb; others read as 0), one float4 (4 K-steps) at a time
+__device__ __forceinline__ floatx4 tile_mfma(const float* A, int na, const float* B, int nb,
+                                             int col, int kq, floatx4 acc) {
+  const float4* pa = reinterpret_cast<const float4*>(A + (col < na ? col : 0) * LTC + kq * 16);
+  const float4* pb = reinterpret_cast<const float4*>(B + (col < nb ? col : 0) * LTC + kq * 16);
+  const bool ma = col < na, mb = col < nb;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 a = pa[q], b = pb[q];
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ma ? a.x : 0.f, mb ? b.x : 0.f, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ma ? a.y : 0.f, mb ? b.y : 0.f, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ma ? a.z : 0.f, mb ? b.z : 0.f, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ma ? a.w : 0.f, mb ? b.w : 0.f, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
 template <int F>
 __global__ __launch_bounds__(256) void k_edge_mlp_bwd(
     EdgeGeo geo, const float* __restrict__ g_tot, const float* __restrict__ alpha,
@@ -866,31 +884,42 @@ __global__ __launch_bounds__(256) void k_edge_mlp_bwd(
       pf_cptr ptc = pf_fresh(PtT + cn * H);
 #pragma unroll
       for (int tt = 0; tt < NT2; ++tt) {
+        // the tile's 16 values are computed before any of them is written: the
+        // scalar weight loads of a group are batched and waited for once, not
+        // interleaved with LDS writes (SMEM and LDS share lgkmcnt)
+        float tv[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int h = 16 * tt + u;
-          float v;
-          if (h < H) {
-            const float4 p4 = psl[(h >> 2) * 64 + lane];
-            const float pv = (h & 3) == 0 ? p4.x : (h & 3) == 1 ? p4.y : (h & 3) == 2 ? p4.z : p4.w;
-            float z = pv + ptc[h];
+        for (int u0 = 0; u0 < 16; u0 += 4) {
+          float wr[4][F], pt4[4];
 #pragma unroll
-            for (int k = 0; k < F; ++k) z = fmaf(W1f[h * H + k], x[k], z);
-            pos[h >> 5] |= (z > 0.f ? 1u : 0u) << (h & 31);
-            v = lrelu(z);
-          } else {
-            v = h == H ? 1.f : 0.f;   // ones column -> db2
+          for (int u = 0; u < 4; ++u) {
+            const int h = 16 * tt + u0 + u;
+            if (h < H) {
+              pt4[u] = ptc[h];
+#pragma unroll
+              for (int k = 0; k < F; ++k) wr[u][k] = W1f[h * H + k];
+            }
           }
-          T[u * LTC + lane] = v;
-        }
-        wave_lds_sync();
-        float av[16], bv[16];
-        tile_k16(Gr, col < F ? col : 0, kq, av);
-        tile_k16(T, col, kq, bv);
 #pragma unroll
-        for (int st = 0; st < 16; ++st)
-          acc2[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(col < F ? av[st] : 0.f, bv[st],
-                                                          acc2[tt], 0, 0, 0);
+          for (int u = 0; u < 4; ++u) {
+            const int h = 16 * tt + u0 + u;
+            if (h < H) {
+              const float4 p4 = psl[(h >> 2) * 64 + lane];
+              const float pv = (h & 3) == 0 ? p4.x : (h & 3) == 1 ? p4.y : (h & 3) == 2 ? p4.z : p4.w;
+              float z = pv + pt4[u];
+#pragma unroll
+              for (int k = 0; k < F; ++k) z = fmaf(wr[u][k], x[k], z);
+              pos[h >> 5] |= (z > 0.f ? 1u : 0u) << (h & 31);
+              tv[u0 + u] = lrelu(z);
+            } else {
+              tv[u0 + u] = h == H ? 1.f : 0.f;   // ones column -> db2
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) T[u * LTC + lane] = tv[u];
+        wave_lds_sync();
+        acc2[tt] = tile_mfma(Gr, F, T, 16, col, kq, acc2[tt]);
         wave_lds_sync();
       }
     }
@@ -903,31 +932,44 @@ __global__ __launch_bounds__(256) void k_edge_mlp_bwd(
       pf_cptr W1g = pf_fresh(W1 + 2 * F);
 #pragma unroll
       for (int tt = 0; tt < NT1; ++tt) {
+        float tv[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int h = 16 * tt + u;
-          float g = 0.f;
-          if (h < H) {
-            float s = 0.f;
+        for (int u0 = 0; u0 < 16; u0 += 2) {
+          float w2[2][F], w1[2][F];
 #pragma unroll
-            for (int o = 0; o < F; ++o) s = fmaf(W2c[h * F + o], gy[o], s);
-            g = ((pos[h >> 5] >> (h & 31)) & 1u) ? s : PF_LEAKY * s;
-            accF[h] += g;
-            if (gxe) {
+          for (int u = 0; u < 2; ++u) {
+            const int h = 16 * tt + u0 + u;
+            if (h < H) {
 #pragma unroll
-              for (int k = 0; k < F; ++k) gx[k] = fmaf(W1g[h * H + k], g, gx[k]);
+              for (int o = 0; o < F; ++o) w2[u][o] = W2c[h * F + o];
+              if (gxe) {
+#pragma unroll
+                for (int k = 0; k < F; ++k) w1[u][k] = W1g[h * H + k];
+              }
             }
           }
-          T[u * LTC + lane] = g;
-        }
-        wave_lds_sync();
-        float av[16], bv[16];
-        tile_k16(T, col, kq, av);
-        tile_k16(Xr, col < F ? col : 0, kq, bv);
 #pragma unroll
-        for (int st = 0; st < 16; ++st)
-          acc1[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[st], col < F ? bv[st] : 0.f,
-                                                          acc1[tt], 0, 0, 0);
+          for (int u = 0; u < 2; ++u) {
+            const int h = 16 * tt + u0 + u;
+            float g = 0.f;
+            if (h < H) {
+              float s = 0.f;
+#pragma unroll
+              for (int o = 0; o < F; ++o) s = fmaf(w2[u][o], gy[o], s);
+              g = ((pos[h >> 5] >> (h & 31)) & 1u) ? s : PF_LEAKY * s;
+              accF[h] += g;
+              if (gxe) {
+#pragma unroll
+                for (int k = 0; k < F; ++k) gx[k] = fmaf(w1[u][k], g, gx[k]);
+              }
+            }
+            tv[u0 + u] = g;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) T[u * LTC + lane] = tv[u];
+        wave_lds_sync();
+        acc1[tt] = tile_mfma(T, 16, Xr, F, col, kq, acc1[tt]);
         const float cs = tile_colsum(T, lane);
         if (lane < 16 && 16 * tt + lane < H)
           partCol[(((size_t)gg * geo.NFG + fg) * geo.NC + c) * H + 16 * tt + lane] = cs;

@@ -369,6 +369,43 @@ __global__ void k_from_canonical(const float* __restrict__ y, const float* __res
   }
 }
 
+// Fiber-major row-major output (train.py's order) through an LDS tile: a block
+// takes 64 fibers x 16 classes of one graph, reads the canonical rows
+// coalesced along the fibers, and writes each fiber's 16 classes x F values as
+// one contiguous run (dst row (g*NF + f)*NC + c).
+#define FC_CT 16
+template <int F>
+__global__ __launch_bounds__(256) void k_from_canonical_fm(const float* __restrict__ y,
+                                                           const float* __restrict__ sc,
+                                                           const float* __restrict__ sh, int G,
+                                                           int NF, int NC,
+                                                           float* __restrict__ dst) {
+  __shared__ float tile[64 * FC_CT * F + 64];
+  const int t = threadIdx.x;
+  const int nfg = (NF + 63) / 64, ncg = (NC + FC_CT - 1) / FC_CT;
+  const int b = blockIdx.x;
+  const int cg = b % ncg, fg = (b / ncg) % nfg, g = b / (ncg * nfg);
+  const int f0 = fg * 64, cb = cg * FC_CT;
+  const int nf = min(64, NF - f0), nc = min(FC_CT, NC - cb);
+  const long long E = (long long)G * NF * NC;
+  // tile[(fl * FC_CT + cl) * F + j]  (fiber-major, then class, then feature)
+  for (int idx = t; idx < F * FC_CT * 64; idx += 256) {
+    const int fl = idx & 63, rest = idx >> 6;
+    const int cl = rest % FC_CT, j = rest / FC_CT;
+    if (fl < nf && cl < nc) {
+      float v = y[(long long)j * E + ((long long)g * NC + cb + cl) * NF + f0 + fl];
+      if (sc) v = fmaf(v, sc[j], sh[j]);
+      tile[(fl * FC_CT + cl) * F + j] = v;
+    }
+  }
+  __syncthreads();
+  const int run = nc * F;  // contiguous floats per fiber
+  for (int idx = t; idx < nf * run; idx += 256) {
+    const int fl = idx / run, r = idx - fl * run;
+    dst[(((long long)g * NF + f0 + fl) * NC + cb) * F + r] = tile[fl * FC_CT * F + r];
+  }
+}
+
 __global__ void k_fiber_partial_sum(const float* __restrict__ part, int KS, long long len,
                                     float* __restrict__ out) {
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -527,6 +564,18 @@ extern "C" int pfsgnn_edges_from_canonical(const float* y, const float* sc, cons
   const long long E = (long long)G * NF * NC;
   PF_REQUIRE(y && dst && E > 0 && F > 0 && mode >= 0 && mode <= 2 && (mode != 0 || perm),
              "pfsgnn_edges_from_canonical", "bad arguments");
+  if (mode == 1 && rowmajor && (F == 8 || F == 10 || F == 16)) {
+    const unsigned nb = (unsigned)((long long)G * ((NF + 63) / 64) * ((NC + FC_CT - 1) / FC_CT));
+    switch (F) {
+      case 8: hipLaunchKernelGGL(k_from_canonical_fm<8>, dim3(nb), dim3(256), 0,
+                                 as_stream(stream), y, sc, sh, G, NF, NC, dst); break;
+      case 10: hipLaunchKernelGGL(k_from_canonical_fm<10>, dim3(nb), dim3(256), 0,
+                                  as_stream(stream), y, sc, sh, G, NF, NC, dst); break;
+      default: hipLaunchKernelGGL(k_from_canonical_fm<16>, dim3(nb), dim3(256), 0,
+                                  as_stream(stream), y, sc, sh, G, NF, NC, dst); break;
+    }
+    return pf::check_launch("pfsgnn_edges_from_canonical");
+  }
   hipLaunchKernelGGL(k_from_canonical, dim3((unsigned)((E + 255) / 256)), dim3(256), 0,
                      as_stream(stream), y, sc, sh, E, NF, NC, F, mode, perm, rowmajor, dst);
   return pf::check_launch("pfsgnn_edges_from_canonical");
