@@ -292,14 +292,15 @@ __device__ __forceinline__ void chan_merge(double& C0, double& M0, double& Q0, d
   C0 = tot;
 }
 
-// merge per-block Welford partials -> mu, biased var (one wave per channel)
-__global__ __launch_bounds__(64) void k_moments_finalize(const float* __restrict__ part, int nb,
-                                                         int F, long long n,
-                                                         float* __restrict__ mu,
-                                                         float* __restrict__ var) {
-  const int k = blockIdx.x, lane = threadIdx.x;
+// merge per-block Welford partials -> mu, biased var (one 256-thread block per
+// channel: each thread merges a strided subset, then a fixed-order tree)
+__global__ __launch_bounds__(256) void k_moments_finalize(const float* __restrict__ part, int nb,
+                                                          int F, long long n,
+                                                          float* __restrict__ mu,
+                                                          float* __restrict__ var) {
+  const int k = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   double cnt = 0, mean = 0, m2 = 0;
-  for (int b = lane; b < nb; b += 64) {
+  for (int b = t; b < nb; b += 256) {
     const float* p = part + (size_t)b * (1 + 2 * F);
     chan_merge(cnt, mean, m2, p[0], p[1 + k], p[1 + F + k]);
   }
@@ -312,9 +313,14 @@ __global__ __launch_bounds__(64) void k_moments_finalize(const float* __restrict
     chan_merge(c1, m1, q1, c2, mm2, qq2);
     cnt = c1; mean = m1; m2 = q1;
   }
-  if (lane == 0) {
-    mu[k] = (float)mean;
-    var[k] = (float)(m2 / (double)n);
+  __shared__ double sh[4][3];
+  if (lane == 0) { sh[wave][0] = cnt; sh[wave][1] = mean; sh[wave][2] = m2; }
+  __syncthreads();
+  if (t == 0) {
+    double C0 = sh[0][0], M0 = sh[0][1], Q0 = sh[0][2];
+    for (int w = 1; w < 4; ++w) chan_merge(C0, M0, Q0, sh[w][0], sh[w][1], sh[w][2]);
+    mu[k] = (float)M0;
+    var[k] = (float)(Q0 / (double)n);
   }
 }
 
@@ -1148,7 +1154,7 @@ extern "C" int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe
   DISPATCH_F(F, hipLaunchKernelGGL(k_edge_mlp_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
                                    xe, xsc, xsh, Ps, PtT, W1, W2T, b2, y, part));
   tm_.end(); }
-  hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(64), 0, st, part, geo.nblocks, F, geo.E,
+  hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(256), 0, st, part, geo.nblocks, F, geo.E,
                      mu, var);
   return pf::check_launch("pfsgnn_edge_mlp_fwd");
 }

@@ -591,54 +591,83 @@ extern "C" int pfsgnn_bn_fwd(const float* X, int C, int N, const float* gamma, c
   return pf::check_launch("pfsgnn_bn_fwd");
 }
 
-// backward sums per channel: Sg = sum dY, Sgx = sum dY*xhat (one block per channel)
+// backward sums per channel: Sg = sum dY, Sgx = sum dY*xhat -- grid (C, S)
+// partials over node chunks; the apply kernel finishes them in fixed order
 __global__ __launch_bounds__(256) void k_bn_bwd_sums(const float* __restrict__ dY,
-                                                     const float* __restrict__ X, int N,
+                                                     const float* __restrict__ X, int N, int S,
                                                      const float* __restrict__ mu,
                                                      const float* __restrict__ var, float eps,
-                                                     float* __restrict__ sums) {
-  const int c = blockIdx.x;
+                                                     float* __restrict__ part) {
+  const int c = blockIdx.x, s = blockIdx.y;
+  const int chunk = (N + S - 1) / S;
+  const int n0 = s * chunk, n1 = min(N, n0 + chunk);
   const float m = mu[c], inv = 1.0f / sqrtf(var[c] + eps);
   float v[2] = {0.f, 0.f};
-  for (int n = threadIdx.x; n < N; n += 256) {
+  for (int n = n0 + threadIdx.x; n < n1; n += 256) {
     const float g = dY[(size_t)c * N + n];
     v[0] += g;
     v[1] += g * (X[(size_t)c * N + n] - m) * inv;
   }
   __shared__ float scratch[8];
   block_sum<2>(v, scratch);
-  if (threadIdx.x == 0) { sums[2 * c] = v[0]; sums[2 * c + 1] = v[1]; }
+  if (threadIdx.x == 0) {
+    part[((size_t)c * S + s) * 2] = v[0];
+    part[((size_t)c * S + s) * 2 + 1] = v[1];
+  }
 }
 
-__global__ void k_bn_bwd_apply(const float* __restrict__ dY, const float* __restrict__ X, int C,
-                               int N, const float* __restrict__ mu, const float* __restrict__ var,
-                               const float* __restrict__ gamma, float eps,
-                               const float* __restrict__ sums, float* __restrict__ dX,
-                               float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx < (size_t)C) {
-    dgamma[idx] += sums[2 * idx + 1];
-    dbeta[idx] += sums[2 * idx];
+// grid (C, ceil(N/1024)): every block re-derives its channel's two sums from
+// the S partials (fixed order), block (c, 0) also accumulates dgamma/dbeta
+__global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ dY,
+                                                      const float* __restrict__ X, int N, int S,
+                                                      const float* __restrict__ mu,
+                                                      const float* __restrict__ var,
+                                                      const float* __restrict__ gamma, float eps,
+                                                      const float* __restrict__ part,
+                                                      float* __restrict__ dX,
+                                                      float* __restrict__ dgamma,
+                                                      float* __restrict__ dbeta) {
+  const int c = blockIdx.x;
+  __shared__ float sums[2];
+  if (threadIdx.x == 0) {
+    float a = 0.f, b = 0.f;
+    for (int s = 0; s < S; ++s) {
+      a += part[((size_t)c * S + s) * 2];
+      b += part[((size_t)c * S + s) * 2 + 1];
+    }
+    sums[0] = a;
+    sums[1] = b;
+    if (blockIdx.y == 0) {
+      dgamma[c] += b;
+      dbeta[c] += a;
+    }
   }
-  if (idx >= (size_t)C * N) return;
-  const int c = (int)(idx / N);
-  const float inv = 1.0f / sqrtf(var[c] + eps);
-  const float xh = (X[idx] - mu[c]) * inv;
-  dX[idx] = gamma[c] * inv * (dY[idx] - sums[2 * c] / N - xh * (sums[2 * c + 1] / N));
+  __syncthreads();
+  const float inv = 1.0f / sqrtf(var[c] + eps), m = mu[c];
+  const float k0 = sums[0] / N, k1 = sums[1] / N, gi = gamma[c] * inv;
+  const int base = blockIdx.y * 1024;
+  for (int i = threadIdx.x; i < 1024; i += 256) {
+    const int n = base + i;
+    if (n < N) {
+      const size_t idx = (size_t)c * N + n;
+      const float xh = (X[idx] - m) * inv;
+      dX[idx] = gi * (dY[idx] - k0 - xh * k1);
+    }
+  }
 }
 
 extern "C" int pfsgnn_bn_bwd(const float* dY, const float* X, const float* mu, const float* var,
                              const float* gamma, float eps, int C, int N, float* dX, float* dgamma,
                              float* dbeta, void* ws, size_t ws_bytes, void* stream) {
   PF_REQUIRE(dY && X && dX && C > 0 && N > 0, "pfsgnn_bn_bwd", "bad arguments");
-  PF_REQUIRE(ws && ws_bytes >= (size_t)2 * C * sizeof(float), "pfsgnn_bn_bwd",
+  const int S = bn_splits(N);
+  PF_REQUIRE(ws && ws_bytes >= (size_t)2 * C * S * sizeof(float), "pfsgnn_bn_bwd",
              "workspace too small");
   hipStream_t st = as_stream(stream);
-  float* sums = reinterpret_cast<float*>(ws);
-  hipLaunchKernelGGL(k_bn_bwd_sums, dim3(C), dim3(256), 0, st, dY, X, N, mu, var, eps, sums);
-  const size_t tot = (size_t)C * N;
-  hipLaunchKernelGGL(k_bn_bwd_apply, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, dY, X,
-                     C, N, mu, var, gamma, eps, sums, dX, dgamma, dbeta);
+  float* part = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(k_bn_bwd_sums, dim3(C, S), dim3(256), 0, st, dY, X, N, S, mu, var, eps, part);
+  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(C, (N + 1023) / 1024), dim3(256), 0, st, dY, X, N, S, mu,
+                     var, gamma, eps, part, dX, dgamma, dbeta);
   return pf::check_launch("pfsgnn_bn_bwd");
 }
 
