@@ -648,9 +648,7 @@ __global__ __launch_bounds__(256) void k_source_bwd(
 #pragma unroll
       for (int k = 0; k < F; ++k) z = fmaf(W1f[h * C + k], x[k], z);
       zs[h] = z;
-      B[lane * WG2::LDB + h] = lrelu(z);
     }
-    B[lane * WG2::LDB + C] = 1.f;
     float gm[C];
 #pragma unroll
     for (int o = 0; o < C; ++o) {
@@ -661,8 +659,13 @@ __global__ __launch_bounds__(256) void k_source_bwd(
       const float q0 = fib[(C + o) * 64 + lane], q1 = fib[(2 * C + o) * 64 + lane],
                   q2 = fib[(3 * C + o) * 64 + lane], q3 = fib[(4 * C + o) * 64 + lane];
       gm[o] = fvalid ? fmaf(d, fmaf(d, fmaf(d, q3, q2), q1), q0) : 0.f;
-      A[lane * WG2::LDA + o] = gm[o];
     }
+    // staging rows written after the arithmetic (SMEM and LDS share lgkmcnt)
+#pragma unroll
+    for (int h = 0; h < C; ++h) B[lane * WG2::LDB + h] = lrelu(zs[h]);
+    B[lane * WG2::LDB + C] = 1.f;
+#pragma unroll
+    for (int o = 0; o < C; ++o) A[lane * WG2::LDA + o] = gm[o];
     wave_lds_sync();
     wg2.accum(region, lane);
     wave_lds_sync();
