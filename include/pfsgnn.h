@@ -40,6 +40,20 @@ const char* pfsgnn_version(void);
 const char* pfsgnn_last_error(void);
 size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F);
 
+/* Implementation of the per-edge kernels (process-wide, read at launch, so a
+ * captured graph keeps the path it was captured with):
+ *   PFSGNN_EDGE_MFMA (default) -- matrix cores (pfsgnn_mfma.hip): layer
+ *       contractions on v_mfma_f32_16x16x4_f32 (exact fp32 products), weight
+ *       gradients on v_mfma_f32_16x16x16_bf16 with split operands (bf16 hi +
+ *       lo, ~2^-16 relative per product, averaged over the edge sum);
+ *   PFSGNN_EDGE_VALU -- fp32 fmaf chains on the vector ALU (pfsgnn_edge.hip).
+ * Both produce the same outputs to fp32 rounding; node-level ops, reductions
+ * and the loss are shared. */
+#define PFSGNN_EDGE_VALU 0
+#define PFSGNN_EDGE_MFMA 1
+int pfsgnn_set_edge_path(int path);
+int pfsgnn_get_edge_path(void);
+
 /* Per-kernel HIP-event timing of the main edge/loss kernels (diagnostics for
  * bench.py; off by default, must stay off while a stream is captured).
  * Names: edge_mlp_fwd, source_fwd, target_fwd, target_bwd, source_bwd,

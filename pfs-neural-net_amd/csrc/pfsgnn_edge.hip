@@ -18,6 +18,7 @@
 // reduce, so a training step is bitwise reproducible.
 #include "pfsgnn_common.h"
 #include "../../include/pfsgnn.h"
+#include "pfsgnn_mfma.h"
 
 #include <algorithm>
 
@@ -1118,10 +1119,40 @@ void fiber_finish(const EdgeGeo& geo, int C, const float* dst, float* out, hipSt
                      geo.KS, len, out);
 }
 
+// per-class node table for the MFMA kernels: class-major, in their slot order
+const float* class_rows_p(const float* src, int C, const EdgeGeo& geo, Ws& w, hipStream_t st) {
+  if (!src) return nullptr;
+  float* dst = w.take((size_t)geo.NT * pfm::class_cols(C));
+  if (!dst) return nullptr;
+  pfm::class_rows_slot(src, C, geo.NT, dst, st);
+  return dst;
+}
+
+int g_path = PFSGNN_EDGE_MFMA;
+bool use_mfma() { return g_path == PFSGNN_EDGE_MFMA; }
+// MFMA blocks stage their class-table rows in LDS: at most MAX_CPS classes each
+EdgeGeo geo_mfma(int G, int NF, int NC) {
+  const long long groups = (long long)G * ((NF + 63) / 64);
+  const long long min_ks = (NC + pfm::MAX_CPS - 1) / pfm::MAX_CPS;
+  const long long target = std::max<long long>(pfm::TARGET_BLOCKS, groups * min_ks);
+  return make_geo(G, NF, NC, (int)std::min<long long>(target, 1ll << 30));
+}
+EdgeGeo geo_for(int G, int NF, int NC) {
+  return use_mfma() ? geo_mfma(G, NF, NC) : make_geo(G, NF, NC);
+}
+
 }  // namespace
 
-extern "C" size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F) {
-  const EdgeGeo geo = make_geo(G, NF, NC);
+extern "C" int pfsgnn_set_edge_path(int path) {
+  if (path != PFSGNN_EDGE_VALU && path != PFSGNN_EDGE_MFMA)
+    return pf::fail("pfsgnn_set_edge_path", "path must be PFSGNN_EDGE_VALU or PFSGNN_EDGE_MFMA");
+  g_path = path;
+  return 0;
+}
+extern "C" int pfsgnn_get_edge_path(void) { return g_path; }
+
+namespace {
+size_t edge_ws_floats(const EdgeGeo& geo, int G, int NC, int F) {
   const size_t nb = geo.nblocks, ks = geo.KS, NS = geo.NS;
   const size_t H = 4 * F, C = 2 * F;
   const size_t colp = (size_t)G * geo.NFG * NC;
@@ -1133,7 +1164,16 @@ extern "C" size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F) {
   edge = std::max(edge, nb * (C * (C + 1) + C * F + 2 * F) + colp * C + 4096);      // source bwd
   edge = std::max(edge, nb * (F * (H + 1) + H * F) + colp * H + ks * H * NS + 4096);  // edge bwd
   edge = std::max(edge, colp * 4 + ks * NS + nb * (F * (F + 1) + F + 1) + 4096);   // loss
-  edge += (size_t)geo.NT * (H + 2 * C) + 4 * H * H + 8 * 256;  // class_rows / transposed
+  edge += (size_t)geo.NT * (pfm::class_cols(H) + 2 * pfm::class_cols(C)) + 4 * H * H + 8 * 256;
+  return edge;
+}
+}  // namespace
+
+extern "C" size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F) {
+  // the larger of the two edge paths' partials (either may be selected later)
+  const EdgeGeo geo = make_geo(G, NF, NC);
+  const size_t edge = std::max(edge_ws_floats(geo, G, NC, F),
+                               edge_ws_floats(geo_mfma(G, NF, NC), G, NC, F));
   size_t node = (size_t)512 * 161 * 161 + 4096;                                     // wgrad splits
   size_t lay = (size_t)geo.E + 1024;                                                // layout counts
   return (std::max(std::max(edge, node), lay) + 64 * 16) * sizeof(float) + 16 * 256;
@@ -1146,10 +1186,20 @@ extern "C" int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe
                                    size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_edge_mlp_fwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(xe && Ps && Pt && W1 && W2 && b2 && y && mu && var, "pfsgnn_edge_mlp_fwd", "null");
-  const EdgeGeo geo = make_geo(G, NF, NC);
+  const EdgeGeo geo = geo_for(G, NF, NC);
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
   hipStream_t st = as_stream(stream);
   float* part = w.take((size_t)geo.nblocks * (1 + 2 * F));
+  if (use_mfma()) {
+    const float* PtP = class_rows_p(Pt, 4 * F, geo, w, st);
+    PF_REQUIRE(part && PtP, "pfsgnn_edge_mlp_fwd", "workspace too small");
+    { pf::Timer tm_("edge_mlp_fwd", st);
+    if (int rc = pfm::edge_mlp_fwd(geo, F, xe, xsc, xsh, Ps, PtP, W1, W2, b2, y, part, st)) return rc;
+    tm_.end(); }
+    hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(256), 0, st, part, geo.nblocks, F, geo.E,
+                       mu, var);
+    return pf::check_launch("pfsgnn_edge_mlp_fwd");
+  }
   const float* PtT = class_rows(Pt, 4 * F, geo, w, st);
   const float* W2T = transposed(W2, F, 4 * F, w, st);
   PF_REQUIRE(part && PtT && W2T, "pfsgnn_edge_mlp_fwd", "workspace too small");
@@ -1168,11 +1218,18 @@ extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, c
                                  void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_source_fwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(y && Qt && Ws1 && Ws2 && bs2 && mom && hs, "pfsgnn_source_fwd", "null");
-  const EdgeGeo geo = make_geo(G, NF, NC);
+  const EdgeGeo geo = geo_for(G, NF, NC);
   const int C = 2 * F;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
   hipStream_t st = as_stream(stream);
   float* partS = w.take((size_t)geo.KS * 4 * C * geo.NS);
+  if (use_mfma()) {
+    const float* QtP = class_rows_p(Qt, C, geo, w, st);
+    PF_REQUIRE(partS && QtP, "pfsgnn_source_fwd", "workspace too small");
+    pf::Timer tm_("source_fwd", st);
+    if (int rc = pfm::source_fwd(geo, F, y, sc, sh, QtP, Ws1, Ws2, bs2, partS, st)) return rc;
+    tm_.end();
+  } else {
   const float* QtT = class_rows(Qt, C, geo, w, st);
   const float* Ws2T = transposed(Ws2, C, C, w, st);
   PF_REQUIRE(partS && QtT && Ws2T, "pfsgnn_source_fwd", "workspace too small");
@@ -1180,6 +1237,7 @@ extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, c
   DISPATCH_F(F, hipLaunchKernelGGL(k_source_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
                                    sc, sh, QtT, Ws1, Ws2T, bs2, partS));
   tm_.end(); }
+  }
   const long long len = (long long)C * geo.NS;
   hipLaunchKernelGGL(k_source_finalize, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, st,
                      partS, geo.KS, geo.CPS, C, geo.NS, NC, mom, hs);
@@ -1191,14 +1249,18 @@ extern "C" int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, c
                                  void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_target_fwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(y && Rs && Wt1 && hsum, "pfsgnn_target_fwd", "null");
-  const EdgeGeo geo = make_geo(G, NF, NC);
+  const EdgeGeo geo = geo_for(G, NF, NC);
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
   float* part = w.take((size_t)G * geo.NFG * NC * 2 * F);
   PF_REQUIRE(part, "pfsgnn_target_fwd", "workspace too small");
   hipStream_t st = as_stream(stream);
   { pf::Timer tm_("target_fwd", st);
+  if (use_mfma()) {
+    if (int rc = pfm::target_fwd(geo, F, y, sc, sh, Rs, Wt1, part, st)) return rc;
+  } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
                                    sc, sh, Rs, Wt1, part));
+  }
   tm_.end(); }
   launch_reduce_columns(part, G, geo.NFG, NC, 2 * F, hsum, st);
   return pf::check_launch("pfsgnn_target_fwd");
@@ -1210,17 +1272,22 @@ extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, c
                                  void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_target_bwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(y && Rs && Wt1 && g_hsum && GzT && dWt1, "pfsgnn_target_bwd", "null");
-  const EdgeGeo geo = make_geo(G, NF, NC);
+  const EdgeGeo geo = geo_for(G, NF, NC);
   const int C = 2 * F;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
   hipStream_t st = as_stream(stream);
   float* part = w.take((size_t)geo.nblocks * C * F);
   float* gz = fiber_dst(geo, C, GzT, w);
-  const float* ghT = class_rows(g_hsum, C, geo, w, st);
+  const float* ghT = use_mfma() ? class_rows_p(g_hsum, C, geo, w, st)
+                                : class_rows(g_hsum, C, geo, w, st);
   PF_REQUIRE(part && gz && ghT, "pfsgnn_target_bwd", "workspace too small");
   { pf::Timer tm_("target_bwd", st);
+  if (use_mfma()) {
+    if (int rc = pfm::target_bwd(geo, F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part, st)) return rc;
+  } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
                                    sc, sh, Rs, Wt1, ghT, gz, gxe, part));
+  }
   tm_.end(); }
   fiber_finish(geo, C, gz, GzT, st);
   launch_reduce_rows(part, geo.nblocks, (size_t)C * F, F, C, F, dWt1 + F, C, 1, 1.f, st);
@@ -1241,7 +1308,7 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
   PF_REQUIRE((Rs == nullptr) == (Wt1 == nullptr) && (Rs == nullptr) == (g_hsum == nullptr),
              "pfsgnn_source_bwd", "Rs, Wt1, g_hsum must be given together");
   PF_REQUIRE(!mu1 || (inv1 && Sg && Sgx), "pfsgnn_source_bwd", "mu1 needs inv1, Sg, Sgx");
-  const EdgeGeo geo = make_geo(G, NF, NC);
+  const EdgeGeo geo = geo_for(G, NF, NC);
   const int C = 2 * F;
   const size_t nb = geo.nblocks;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
@@ -1250,14 +1317,21 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
   float* pCol = w.take((size_t)G * geo.NFG * NC * C);
   float* pBN = w.take(nb * 2 * F);
   hipStream_t st = as_stream(stream);
-  const float* QtT = class_rows(Qt, C, geo, w, st);
-  const float* ghT = class_rows(g_hsum, C, geo, w, st);
+  const bool mfma = use_mfma();
+  const float* QtT = mfma ? class_rows_p(Qt, C, geo, w, st) : class_rows(Qt, C, geo, w, st);
+  const float* ghT = mfma ? class_rows_p(g_hsum, C, geo, w, st) : class_rows(g_hsum, C, geo, w, st);
   PF_REQUIRE(pW2 && pW1 && pCol && pBN && QtT && (ghT || !g_hsum), "pfsgnn_source_bwd",
              "workspace too small");
   { pf::Timer tm_("source_bwd", st);
+  if (mfma) {
+    if (int rc = pfm::source_bwd(geo, F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT,
+                                 g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, st))
+      return rc;
+  } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_source_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
                                    sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT, g_next,
                                    mu1, inv1, g_tot, pW2, pW1, pCol, pBN));
+  }
   tm_.end(); }
   {
     RedDesc rd[5] = {{pW2, (int)nb, (size_t)C * (C + 1), C + 1, C, C, dWs2, C, 1, 1.f},
@@ -1305,7 +1379,7 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
   PF_REQUIRE(g_tot && alpha && gam0 && gam1 && y && xe && Ps && Pt && W1 && W2 && dW1 && dW2 &&
                  db2 && GzEs && GzEt,
              "pfsgnn_edge_mlp_bwd", "null");
-  const EdgeGeo geo = make_geo(G, NF, NC);
+  const EdgeGeo geo = geo_for(G, NF, NC);
   const int H = 4 * F;
   const size_t nb = geo.nblocks;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
@@ -1314,6 +1388,15 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
   float* pCol = w.take((size_t)G * geo.NFG * NC * H);
   float* gs = fiber_dst(geo, H, GzEs, w);
   hipStream_t st = as_stream(stream);
+  if (use_mfma()) {
+    const float* PtP = class_rows_p(Pt, H, geo, w, st);
+    PF_REQUIRE(pW2 && pW1 && pCol && gs && PtP, "pfsgnn_edge_mlp_bwd", "workspace too small");
+    pf::Timer tm_("edge_mlp_bwd", st);
+    if (int rc = pfm::edge_mlp_bwd(geo, F, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, PtP, W1,
+                                   W2, gxe, gs, pW2, pW1, pCol, st))
+      return rc;
+    tm_.end();
+  } else {
   const float* PtT = class_rows(Pt, H, geo, w, st);
   const float* W2T = transposed(W2, F, H, w, st);
   PF_REQUIRE(pW2 && pW1 && pCol && gs && PtT && W2T, "pfsgnn_edge_mlp_bwd", "workspace too small");
@@ -1322,6 +1405,7 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
                                    g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, PtT, W1, W2T, gxe,
                                    gs, pW2, pW1, pCol));
   tm_.end(); }
+  }
   fiber_finish(geo, H, gs, GzEs, st);
   {
     RedDesc rd[3] = {{pW2, (int)nb, (size_t)F * (H + 1), H + 1, F, H, dW2, H, 1, 1.f},

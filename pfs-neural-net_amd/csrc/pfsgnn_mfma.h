@@ -1,0 +1,47 @@
+// pfsgnn_mfma.h -- host launchers of the MFMA edge kernels (pfsgnn_mfma.hip).
+//
+// Same inputs, outputs and per-block partial formats as the fp32 VALU kernels
+// of pfsgnn_edge.hip, so the entry points in pfsgnn_edge.hip pick one or the
+// other per call (pfsgnn_set_edge_path) and share every finishing reduction.
+// Per-class node tables are passed class-major in the kernels' slot order
+// (class_rows_slot): a lane group reads each of its 4-row register tiles as
+// one float4.
+#pragma once
+#include "pfsgnn_common.h"
+
+namespace pfm {
+
+// grid of the MFMA kernels: 4 waves x 16 fibers per block (64 fibers, as the
+// fp32 kernels), KS class splits to about this many blocks
+static constexpr int TARGET_BLOCKS = 2048;
+// classes per block at most (the block's class-table rows are staged in LDS)
+static constexpr int MAX_CPS = 64;
+
+int edge_mlp_fwd(const EdgeGeo& geo, int F, const float* xe, const float* xsc, const float* xsh,
+                 const float* Ps, const float* PtS, const float* W1, const float* W2,
+                 const float* b2, float* y, float* part, hipStream_t st);
+int source_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
+               const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
+               float* partS, hipStream_t st);
+int target_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
+               const float* Rs, const float* Wt1, float* part, hipStream_t st);
+int target_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
+               const float* Rs, const float* Wt1, const float* ghS, float* gz, float* gxe,
+               float* part, hipStream_t st);
+int source_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
+               const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
+               const float* mean, const float* coef, const float* Rs, const float* Wt1,
+               const float* ghS, const float* g_next, const float* mu1, const float* inv1,
+               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN, hipStream_t st);
+int edge_mlp_bwd(const EdgeGeo& geo, int F, const float* g_tot, const float* alpha,
+                 const float* gam0, const float* gam1, const float* y, const float* xe,
+                 const float* xsc, const float* xsh, const float* Ps, const float* PtS,
+                 const float* W1, const float* W2, float* gxe, float* gs, float* pW2, float* pW1,
+                 float* pCol, hipStream_t st);
+
+// columns of a slot-ordered class table of a D-wide node tensor (16 per tile)
+int class_cols(int D);
+// [D][NT] node table -> class-major slot-ordered rows [NT][class_cols(D)]
+void class_rows_slot(const float* src, int D, long long NT, float* dst, hipStream_t st);
+
+}  // namespace pfm

@@ -1,0 +1,1176 @@
+// pfsgnn_mfma.hip -- the per-edge kernels of the message-passing block on the
+// matrix cores (the default edge path; pfsgnn_edge.hip holds the fp32 VALU one).
+//
+// Arithmetic.  Every layer-to-layer contraction of gnn.py's per-edge MLPs
+// (EdgeModel gnn.py:86-101, SModel / TModel message MLPs gnn.py:136, 188) and
+// of their backward runs on v_mfma_f32_16x16x4_f32: exact fp32 products, fp32
+// accumulation -- the numerics of an fmaf chain, i.e. of the fp32 VALU path.
+// (bf16 operands, even split hi+lo "bf16x3", are not accurate enough there:
+// SModel's skew / kurtosis features divide by std^3 / std^4 of the message
+// over a fiber's classes and amplify message rounding; measured 6 % gradient
+// deviation against fp64 on small graphs)  The weight
+// gradients -- sums over all edges of outer products -- use
+// v_mfma_f32_16x16x16_bf16 on split operands (v = bf16 hi + bf16 lo, products
+// hi*hi + hi*lo + lo*hi, fp32 accumulate): a product carries ~2^-16 relative
+// error with random sign, which averages out over the edge sum.
+//
+// Tile geometry.  Canonical edge order is class-major, e = (g*NC + c)*NF + f
+// (channel-major [C][E] tensors), as in pfsgnn_edge.hip.  A 256-thread block
+// owns 64 consecutive fibers of one graph and a range of classes; wave w owns
+// fibers 16w..16w+15 and walks EVERY class of the range, one 16-edge tile
+// (16 fibers x 1 class) per step.  In a tile the edge is the MFMA column
+// (lane & 15) and the feature the MFMA row.  A D-wide feature vector is spread
+// over the 4 lane groups g = lane >> 4 by the compact row map GM<D>: group g
+// holds rows g*RPG .. g*RPG + RPG-1 (RPG = ceil(D/4)) in register slots
+// s = 0..RPG-1, slot s being register s&3 of tile s>>2 (a floatx4 per tile).
+// That is the C/D layout of a 16x16 MFMA, and register s of a lane group is
+// exactly the B operand of the K-step that consumes input rows {g*RPG + s}:
+//     Y = W X   ->   y[t] += mfma_16x16x4(A = W[out row][g*RPG + s], B = x[s]),
+// so a layer's output feeds the next layer with no data movement, and an input
+// of D rows costs ceil(D/4) K-steps (10 -> 3, 20 -> 5, 40 -> 10) instead of
+// 4*ceil(D/16).  Consequences:
+//   * F-wide edge rows are loaded / stored as 64-byte row segments per lane
+//     group (16 consecutive fibers of one class), RPG_F instructions per tile;
+//   * per-fiber sums over classes stay in the lane's registers;
+//   * per-class sums over fibers are column sums of a tile, merged over the
+//     block's 4 waves through LDS in fixed order;
+//   * weight gradients sum over the tile's COLUMN index: the operand tiles go
+//     through a wave-private LDS image [edge][slot] read back transposed with
+//     ds_read_b64_tr_b16 (edge = MFMA K).
+// Edge rows are prefetched several classes ahead through a register ring
+// (class_stream).  Cross-block results go to the same per-block partials as
+// the VALU kernels and are finished by the same fixed-order reductions: a step
+// stays bitwise reproducible.
+#include "pfsgnn_mfma.h"
+
+#ifndef MF_DEPTH_FWD
+#define MF_DEPTH_FWD 4   // classes of edge rows in flight per wave (forward kernels)
+#endif
+#ifndef MF_DEPTH_BWD
+#define MF_DEPTH_BWD 2   // (backward kernels: more arrays per class, more registers)
+#endif
+
+namespace {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 b16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ floatx4 zero4() { return floatx4{0.f, 0.f, 0.f, 0.f}; }
+
+// ------------------------------------------------------------ row maps
+template <int D>
+struct GM {
+  static constexpr int RPG = (D + 3) / 4;       // rows per lane group
+  static constexpr int NT = (RPG + 3) / 4;      // floatx4 tiles per lane
+  // live registers of tile t
+  static constexpr int nreg(int t) { return RPG - 4 * t < 4 ? RPG - 4 * t : 4; }
+  // feature row of slot s in lane group g (-1: padding)
+  static __device__ __forceinline__ int row(int g, int s) {
+    const int h = g * RPG + s;
+    return (s < RPG && h < D) ? h : -1;
+  }
+  // feature row of MFMA row index i (= 4g + r) of tile t
+  static __device__ __forceinline__ int mrow(int t, int i) { return row(i >> 2, 4 * t + (i & 3)); }
+};
+
+// ------------------------------------------------------------ fp32 MFMA layer
+// y (+)= W x for a W of M x K rows (fn(out_row, in_row) gives the weight), on
+// v_mfma_f32_16x16x4_f32.  Lane (g, i) holds the A value of output row
+// mrow(t, i) and input row g*RPG_K + s of K-step s.  Long chains are split over
+// two accumulators (even / odd K-steps) to hide the 40-cycle MFMA latency.
+template <int M, int K>
+struct LayerF {
+  static constexpr int MT = GM<M>::NT, KS = GM<K>::RPG;
+  float a[MT][KS];
+  template <class Fn>
+  __device__ __forceinline__ void load(Fn fn, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int ro = GM<M>::mrow(t, i), ri = GM<K>::row(g, s);
+        a[t][s] = (ro >= 0 && ri >= 0) ? fn(ro, ri) : 0.f;
+      }
+  }
+  __device__ __forceinline__ void apply(const floatx4 (&x)[GM<K>::NT], floatx4 (&y)[MT]) const {
+    if constexpr (KS >= 6) {
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        floatx4 e = y[t], o = zero4();
+#pragma unroll
+        for (int s = 0; s < KS; s += 2) {
+          e = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][s], x[s >> 2][s & 3], e, 0, 0, 0);
+          if (s + 1 < KS)
+            o = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][s + 1], x[(s + 1) >> 2][(s + 1) & 3], o,
+                                                     0, 0, 0);
+        }
+        y[t] = e + o;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+          y[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][s], x[s >> 2][s & 3], y[t], 0, 0, 0);
+    }
+  }
+};
+
+// ------------------------------------------------------------ bf16x3 (wgrad)
+struct Fr {
+  s16x4 h, l;
+};
+__device__ __forceinline__ float bf_f(short s) {
+  return __builtin_bit_cast(float, ((uint32_t)(uint16_t)s) << 16);
+}
+// v = hi + lo (+ ~2^-17 |v|): hi = bf16_rne(v), lo = bf16_rne(v - hi)
+__device__ __forceinline__ Fr split(const floatx4& v) {
+  const b16x4 h = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  const s16x4 hs = __builtin_bit_cast(s16x4, h);
+  const b16x4 l = {(__bf16)(v[0] - bf_f(hs[0])), (__bf16)(v[1] - bf_f(hs[1])),
+                   (__bf16)(v[2] - bf_f(hs[2])), (__bf16)(v[3] - bf_f(hs[3]))};
+  return {hs, __builtin_bit_cast(s16x4, l)};
+}
+__device__ __forceinline__ floatx4 mf(s16x4 a, s16x4 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+// c += A B with A = Ah + Al, B = Bh + Bl (Al*Bl dropped); small terms first
+__device__ __forceinline__ floatx4 mma3(const Fr& a, const Fr& b, floatx4 c) {
+  c = mf(a.l, b.h, c);
+  c = mf(a.h, b.l, c);
+  return mf(a.h, b.h, c);
+}
+// bf16 1.0 in every element: B operand that sums an A image over its 16 edges
+__device__ __forceinline__ s16x4 ones16() {
+  return s16x4{(short)0x3F80, (short)0x3F80, (short)0x3F80, (short)0x3F80};
+}
+
+// Wave-private image of one 16x16 bf16 block, [16 edges][16 slots] (32-byte
+// rows, the four 8-byte chunks of row e XOR-swizzled by e>>2: conflict-free b64
+// writes and tr reads).  Lane (g, j) writes its slots 4g..4g+3 of edge j; a
+// ds_read_b64_tr_b16 hands lane (g, i) the slot-i column of edges 4g..4g+3:
+// an A operand A[slot][edge] or a B operand B[edge][slot], edge = MFMA K.
+#define IMG_SHORTS 256
+__device__ __forceinline__ void img_put(short* img, int lane, s16x4 v) {
+  const int g = lane >> 4, j = lane & 15;
+  *reinterpret_cast<s16x4*>(img + j * 16 + ((g ^ (j >> 2)) & 3) * 4) = v;
+}
+__device__ __forceinline__ s16x4 img_tr(const short* img, int lane) {
+  const int ii = lane & 15, gq = lane >> 4;
+  const int row = 4 * gq + (ii >> 2);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(img + row * 16 + (((ii & 3) ^ gq) & 3) * 4));
+}
+__device__ __forceinline__ void img_put2(short* img, int lane, const Fr& v) {
+  img_put(img, lane, v.h);
+  img_put(img + IMG_SHORTS, lane, v.l);
+}
+__device__ __forceinline__ Fr img_tr2(const short* img, int lane) {
+  return {img_tr(img, lane), img_tr(img + IMG_SHORTS, lane)};
+}
+// compiler-only ordering point between a wave's image writes and its reads
+// (one wave's LDS operations execute in order)
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
+// ------------------------------------------------------------ memory
+__device__ __forceinline__ float ldE(const float* p, uint32_t off) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(p) + off);
+}
+__device__ __forceinline__ void stE(float* p, uint32_t off, float v) {
+  *reinterpret_cast<float*>(reinterpret_cast<char*>(p) + off) = v;
+}
+
+// the lane's rows of an F-wide edge tensor at edge byte offset eo (slots with
+// no feature load row 0 again -- same 64-B segment -- and are masked later)
+template <int F>
+__device__ __forceinline__ floatx4 ld_frows(const float* p, uint32_t eo, uint32_t RB, int g) {
+  floatx4 v = zero4();
+#pragma unroll
+  for (int r = 0; r < GM<F>::RPG; ++r) {
+    const int k = GM<F>::row(g, r);
+    v[r] = ldE(p, eo + (uint32_t)(k < 0 ? 0 : k) * RB);
+  }
+  return v;
+}
+
+template <int F>
+__device__ __forceinline__ void st_frows(float* p, uint32_t eo, uint32_t RB, int g, bool valid,
+                                         const floatx4& v) {
+#pragma unroll
+  for (int r = 0; r < GM<F>::RPG; ++r) {
+    const int k = GM<F>::row(g, r);
+    if (valid && k >= 0) stE(p, eo + (uint32_t)k * RB, v[r]);
+  }
+}
+
+// per-feature constants of an F-wide block in the lane's slot order
+template <int F>
+__device__ __forceinline__ floatx4 ld_fconst(const float* p, int g, float dflt) {
+  floatx4 v = zero4();
+#pragma unroll
+  for (int r = 0; r < GM<F>::RPG; ++r) {
+    const int k = GM<F>::row(g, r);
+    v[r] = (p && k >= 0) ? p[k] : dflt;
+  }
+  return v;
+}
+
+// per-fiber rows of tile t of a channel-major node tensor [D][NS]
+template <int D>
+__device__ __forceinline__ floatx4 ld_node(const float* p, int t, int g, long long NS,
+                                           long long n, bool valid) {
+  floatx4 v = zero4();
+#pragma unroll
+  for (int r = 0; r < GM<D>::nreg(t); ++r) {
+    const int h = GM<D>::row(g, 4 * t + r);
+    v[r] = (p && valid && h >= 0) ? p[(long long)h * NS + n] : 0.f;
+  }
+  return v;
+}
+
+// The block's class rows [c0, c1) of a slot-ordered class table, staged in LDS
+// once (they are re-read for every tile of every wave); MF_MAX_CPS bounds the
+// class range of an MFMA block (pfm::MAX_CPS, geo_mfma in pfsgnn_edge.hip).
+#define MF_MAX_CPS 64
+template <int D>
+struct ClassRows {
+  static constexpr int CP = 16 * GM<D>::NT;
+  __device__ __forceinline__ static void stage(float* buf, const float* P, long long cn0, int ncl) {
+    const floatx4* src = reinterpret_cast<const floatx4*>(P + cn0 * CP);
+    floatx4* dst = reinterpret_cast<floatx4*>(buf);
+    for (int i = threadIdx.x; i < ncl * CP / 4; i += PF_BLOCK) dst[i] = src[i];
+  }
+  __device__ __forceinline__ static floatx4 get(const float* buf, int cl, int t, int g) {
+    return *reinterpret_cast<const floatx4*>(buf + cl * CP + 16 * t + 4 * g);
+  }
+};
+
+// constants of a D-wide vector (bias) in slot order
+template <int D>
+__device__ __forceinline__ floatx4 ld_vec(const float* p, int t, int g) {
+  floatx4 v = zero4();
+#pragma unroll
+  for (int r = 0; r < GM<D>::nreg(t); ++r) {
+    const int h = GM<D>::row(g, 4 * t + r);
+    v[r] = (p && h >= 0) ? p[h] : 0.f;
+  }
+  return v;
+}
+
+__device__ __forceinline__ float lrelu(float x) { return x > 0.f ? x : PF_LEAKY * x; }
+__device__ __forceinline__ float dlrelu(float z) { return z > 0.f ? 1.f : PF_LEAKY; }
+template <int D>
+__device__ __forceinline__ void lrelu_act(const floatx4 (&z)[GM<D>::NT], floatx4 (&a)[GM<D>::NT]) {
+#pragma unroll
+  for (int t = 0; t < GM<D>::NT; ++t) {
+    a[t] = zero4();
+#pragma unroll
+    for (int r = 0; r < GM<D>::nreg(t); ++r) a[t][r] = lrelu(z[t][r]);
+  }
+}
+
+// ------------------------------------------------------------ column sums
+template <int CTRL>
+__device__ __forceinline__ float dpp0(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// sum over the 16 lanes of each DPP row (= lane group); the total lands in the
+// row's lane 15 (row_shr 1, 2, 4, 8 with zero fill)
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp0<0x111>(v);
+  v += dpp0<0x112>(v);
+  v += dpp0<0x114>(v);
+  v += dpp0<0x118>(v);
+  return v;
+}
+
+// Per-class column partials of the block, chunked: each wave parks its 16-fiber
+// sums of COL_CH classes in buf[COL_CH][4][CW]; the block then writes the 4-wave
+// sums (fixed order) to part[(rowbase + c) * CW + h] ([G][NFG][NC][CW] layout).
+#define COL_CH 8
+template <int CW>
+__device__ __forceinline__ void col_flush(const float* buf, int nch, int cbase, float* part,
+                                          long long rowbase) {
+  for (int idx = threadIdx.x; idx < nch * CW; idx += PF_BLOCK) {
+    const int cc = idx / CW, h = idx - cc * CW;
+    const float* b = buf + cc * 4 * CW + h;
+    part[(rowbase + cbase + cc) * CW + h] = ((b[0] + b[CW]) + b[2 * CW]) + b[3 * CW];
+  }
+}
+
+// Sum a per-wave accumulator tile set over the block's 4 waves and write the
+// block partial.  acc[a] holds D[4g+r][j] of output tile a; rc(a, 4g + r, j)
+// gives the partial index of each element (negative = not an output).
+template <int NA, class RC>
+__device__ __forceinline__ void block_partial(const floatx4 (&acc)[NA], float* scratch, int len,
+                                              RC rc, float* part) {
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63, g = lane >> 4, j = lane & 15;
+  __syncthreads();
+  for (int idx = t; idx < 4 * len; idx += PF_BLOCK) scratch[idx] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int idx = rc(a, 4 * g + r, j);
+      if (idx >= 0) scratch[wave * len + idx] = acc[a][r];
+    }
+  __syncthreads();
+  for (int idx = t; idx < len; idx += PF_BLOCK)
+    part[idx] = ((scratch[idx] + scratch[len + idx]) + scratch[2 * len + idx]) + scratch[3 * len + idx];
+}
+
+// sum of v over the 16 lanes of each group (xor butterfly, identical in all 16)
+__device__ __forceinline__ float group_sum16(float v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 8);
+  return v;
+}
+
+// ------------------------------------------------------------ class stream
+// The edge rows of a wave's tiles are prefetched D classes ahead through a
+// register ring: D tiles' worth of 64-byte row loads stay in flight per wave.
+// load(c) returns the rows of class c; body(rows, c) consumes them.  The inner
+// loop is unrolled by D so the ring index is static.
+template <int D, class Load, class Body>
+__device__ __forceinline__ void class_stream(int c0, int c1, Load load, Body body) {
+  using R = decltype(load(c0));
+  R ring[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (c0 + d < c1) ring[d] = load(c0 + d);
+  for (int c = c0; c < c1; c += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int cc = c + d;
+      if (cc < c1) {
+        const R cur = ring[d];
+        if (cc + D < c1) ring[d] = load(cc + D);
+        body(cur, cc);
+      }
+    }
+  }
+}
+
+template <int NA>
+struct Rows {
+  floatx4 v[NA];
+};
+
+#define MF_GEO                                                                        \
+  const int t = threadIdx.x, lane = t & 63;                                           \
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);                            \
+  const int g4 = lane >> 4, j16 = lane & 15;                                          \
+  const int bx = blockIdx.x;                                                          \
+  const int ks = bx % geo.KS, grp = bx / geo.KS;                                      \
+  const int fg = grp % geo.NFG, gg = grp / geo.NFG;                                   \
+  const int f = fg * 64 + wave * 16 + j16;                                            \
+  const bool fvalid = f < geo.NF;                                                     \
+  const long long n = (long long)gg * geo.NF + (fvalid ? f : 0);                      \
+  const int c0 = ks * geo.CPS, c1 = min(geo.NC, c0 + geo.CPS);                        \
+  const long long NS = geo.NS;                                                        \
+  const uint32_t RB = (uint32_t)geo.E * 4u;                                           \
+  const uint32_t eo0 =                                                                \
+      (uint32_t)((((long long)gg * geo.NC) * geo.NF + (fvalid ? f : 0)) * 4);         \
+  const uint32_t eoc = (uint32_t)geo.NF * 4u;                                         \
+  const long long colbase = ((long long)gg * geo.NFG + fg) * geo.NC;                  \
+  (void)t; (void)n; (void)NS; (void)RB; (void)colbase; (void)j16;
+
+// x = valid ? (sc*raw + sh) : 0 on the lane's F slots
+template <int F>
+__device__ __forceinline__ floatx4 edge_in(const floatx4& raw, const bool (&fm)[4],
+                                           const float* sc, const floatx4& scv,
+                                           const floatx4& shv) {
+  floatx4 x = zero4();
+#pragma unroll
+  for (int r = 0; r < GM<F>::RPG; ++r) x[r] = fm[r] ? (sc ? fmaf(raw[r], scv[r], shv[r]) : raw[r]) : 0.f;
+  return x;
+}
+
+#define MF_FMASK(F)                                                                   \
+  bool fm[4];                                                                         \
+  _Pragma("unroll") for (int r = 0; r < 4; ++r) fm[r] = fvalid && GM<F>::row(g4, r) >= 0;
+
+// ============================================================ EdgeModel fwd
+// y = W2 lrelu(Ps[f] + Pt[c] + W1[:, 2F:3F] x) + b2 per edge (gnn.py:86-101 with
+// the node parts of the first Linear precomputed per node); Welford partials of
+// y per block for the (double) BatchNorm.
+template <int F>
+__global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float* __restrict__ xe,
+                                                       const float* __restrict__ xsc,
+                                                       const float* __restrict__ xsh,
+                                                       const float* __restrict__ Ps,
+                                                       const float* __restrict__ PtS,
+                                                       const float* __restrict__ W1,
+                                                       const float* __restrict__ W2,
+                                                       const float* __restrict__ b2,
+                                                       float* __restrict__ y,
+                                                       float* __restrict__ part) {
+  constexpr int H = 4 * F, NT = GM<H>::NT;
+  MF_GEO
+  __shared__ __attribute__((aligned(16))) float ptl[MF_MAX_CPS * ClassRows<H>::CP];
+  ClassRows<H>::stage(ptl, PtS, (long long)gg * geo.NC + c0, c1 - c0);
+  LayerF<H, F> L1;
+  L1.load([&](int h, int k) { return W1[h * 4 * F + 2 * F + k]; }, lane);
+  LayerF<F, H> L2;
+  L2.load([&](int o, int h) { return W2[o * H + h]; }, lane);
+  floatx4 ps[NT];
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt) ps[tt] = ld_node<H>(Ps, tt, g4, NS, n, fvalid);
+  const floatx4 bb = ld_fconst<F>(b2, g4, 0.f);
+  const floatx4 scv = ld_fconst<F>(xsc, g4, 1.f), shv = ld_fconst<F>(xsh, g4, 0.f);
+  MF_FMASK(F)
+
+  float cnt = 0.f;
+  floatx4 mean = zero4(), m2 = zero4();
+  __syncthreads();   // ptl
+  auto load = [&](int c) {
+    Rows<1> r;
+    r.v[0] = ld_frows<F>(xe, eo0 + (uint32_t)c * eoc, RB, g4);
+    return r;
+  };
+  class_stream<MF_DEPTH_FWD>(c0, c1, load, [&](const Rows<1>& rows, int c) {
+    const uint32_t eo = eo0 + (uint32_t)c * eoc;
+    const floatx4 x[1] = {edge_in<F>(rows.v[0], fm, xsc, scv, shv)};
+    floatx4 z[NT], a[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) z[tt] = ps[tt] + ClassRows<H>::get(ptl, c - c0, tt, g4);
+    L1.apply(x, z);
+    lrelu_act<H>(z, a);
+    floatx4 yo[1] = {bb};
+    L2.apply(a, yo);
+    st_frows<F>(y, eo, RB, g4, fvalid, yo[0]);
+    if (fvalid) {
+      cnt += 1.f;
+      const float rc = 1.0f / cnt;
+#pragma unroll
+      for (int r = 0; r < GM<F>::RPG; ++r) {
+        const float d = yo[0][r] - mean[r];
+        mean[r] = fmaf(d, rc, mean[r]);
+        m2[r] = fmaf(d, yo[0][r] - mean[r], m2[r]);
+      }
+    }
+  });
+  // Chan merge over the 16 fibers of the group, then over the 4 waves
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) {
+    const float cb = __shfl_xor(cnt, off);
+    const float tot = cnt + cb;
+    const float wb = tot > 0.f ? cb / tot : 0.f;
+    const float wab = tot > 0.f ? cnt * cb / tot : 0.f;
+#pragma unroll
+    for (int r = 0; r < GM<F>::RPG; ++r) {
+      const float mb = __shfl_xor(mean[r], off), qb = __shfl_xor(m2[r], off);
+      const float d = mb - mean[r];
+      mean[r] = fmaf(d, wb, mean[r]);
+      m2[r] = m2[r] + qb + d * d * wab;
+    }
+    cnt = tot;
+  }
+  __shared__ float shm[4][1 + 2 * F];
+  if (j16 == 0) {
+    if (g4 == 0) shm[wave][0] = cnt;
+#pragma unroll
+    for (int r = 0; r < GM<F>::RPG; ++r) {
+      const int k = GM<F>::row(g4, r);
+      if (k >= 0) { shm[wave][1 + k] = mean[r]; shm[wave][1 + F + k] = m2[r]; }
+    }
+  }
+  __syncthreads();
+  if (t < F) {
+    float C0 = shm[0][0], M0 = shm[0][1 + t], Q0 = shm[0][1 + F + t];
+    for (int w = 1; w < 4; ++w) {
+      const float cb = shm[w][0], mb = shm[w][1 + t], qb = shm[w][1 + F + t];
+      const float tot = C0 + cb;
+      if (tot > 0.f) {
+        const float d = mb - M0;
+        M0 = M0 + d * (cb / tot);
+        Q0 = Q0 + qb + d * d * (C0 * cb / tot);
+      }
+      C0 = tot;
+    }
+    float* p = part + (size_t)bx * (1 + 2 * F);
+    if (t == 0) p[0] = C0;
+    p[1 + t] = M0;
+    p[1 + F + t] = Q0;
+  }
+}
+
+// ============================================================ SModel fwd
+// message m = Ws2 lrelu(Qt[c] + Ws1[:, F:2F] x) + bs2 (gnn.py:136-137) and its
+// per-fiber centred moments over the class range by Pebay's one-pass update
+// (the wave walks every class of its 16 fibers: no cross-wave merge).
+template <int F>
+__global__ __launch_bounds__(256) void km_source_fwd(EdgeGeo geo, const float* __restrict__ y,
+                                                     const float* __restrict__ sc,
+                                                     const float* __restrict__ sh,
+                                                     const float* __restrict__ QtS,
+                                                     const float* __restrict__ Ws1,
+                                                     const float* __restrict__ Ws2,
+                                                     const float* __restrict__ bs2,
+                                                     float* __restrict__ partS) {
+  constexpr int C = 2 * F, NT = GM<C>::NT;
+  MF_GEO
+  __shared__ __attribute__((aligned(16))) float qtl[MF_MAX_CPS * ClassRows<C>::CP];
+  ClassRows<C>::stage(qtl, QtS, (long long)gg * geo.NC + c0, c1 - c0);
+  LayerF<C, F> L1;
+  L1.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
+  LayerF<C, C> L2;
+  L2.load([&](int o, int h) { return Ws2[o * C + h]; }, lane);
+  floatx4 bias[NT];
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt) bias[tt] = ld_vec<C>(bs2, tt, g4);
+  const floatx4 scv = ld_fconst<F>(sc, g4, 1.f), shv = ld_fconst<F>(sh, g4, 0.f);
+  MF_FMASK(F)
+
+  floatx4 S1[NT], S2[NT], S3[NT], S4[NT];  // mean | M2 | M3 | M4
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt) S1[tt] = S2[tt] = S3[tt] = S4[tt] = zero4();
+  float cnt = 0.f;
+  __syncthreads();   // qtl
+  auto load = [&](int c) {
+    Rows<1> r;
+    r.v[0] = ld_frows<F>(y, eo0 + (uint32_t)c * eoc, RB, g4);
+    return r;
+  };
+  class_stream<MF_DEPTH_FWD>(c0, c1, load, [&](const Rows<1>& rows, int c) {
+    const floatx4 x[1] = {edge_in<F>(rows.v[0], fm, sc, scv, shv)};
+    floatx4 z[NT], a[NT], m[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) z[tt] = ClassRows<C>::get(qtl, c - c0, tt, g4);
+    L1.apply(x, z);
+    lrelu_act<C>(z, a);
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) m[tt] = bias[tt];
+    L2.apply(a, m);
+    const float nold = cnt;
+    cnt += 1.f;
+    const float inv = 1.f / cnt, a3 = cnt - 2.f, a4 = cnt * cnt - 3.f * cnt + 3.f;
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+      for (int r = 0; r < GM<C>::nreg(tt); ++r) {
+        const float delta = m[tt][r] - S1[tt][r];
+        const float dn = delta * inv, dn2 = dn * dn, t1 = delta * dn * nold;
+        S4[tt][r] = fmaf(t1 * dn2, a4, fmaf(6.f * dn2, S2[tt][r], fmaf(-4.f * dn, S3[tt][r], S4[tt][r])));
+        S3[tt][r] = fmaf(t1 * dn, a3, fmaf(-3.f * dn, S2[tt][r], S3[tt][r]));
+        S2[tt][r] += t1;
+        S1[tt][r] += dn;
+      }
+  });
+  if (fvalid) {
+    float* dst = partS + (size_t)ks * 4 * C * NS + n;
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+      for (int r = 0; r < GM<C>::nreg(tt); ++r) {
+        const int o = GM<C>::row(g4, 4 * tt + r);
+        if (o >= 0) {
+          dst[(size_t)o * NS] = S1[tt][r];
+          dst[(size_t)(C + o) * NS] = S2[tt][r];
+          dst[(size_t)(2 * C + o) * NS] = S3[tt][r];
+          dst[(size_t)(3 * C + o) * NS] = S4[tt][r];
+        }
+      }
+  }
+}
+
+// ============================================================ TModel fwd
+// a = lrelu(Rs[f] + Wt1[:, F:2F] x) per edge and its per-class sum over fibers
+// (gnn.py:188-190; the second Linear runs after the sum, on the node side).
+template <int F>
+__global__ __launch_bounds__(256) void km_target_fwd(EdgeGeo geo, const float* __restrict__ y,
+                                                     const float* __restrict__ sc,
+                                                     const float* __restrict__ sh,
+                                                     const float* __restrict__ Rs,
+                                                     const float* __restrict__ Wt1,
+                                                     float* __restrict__ part) {
+  constexpr int C = 2 * F, NT = GM<C>::NT;
+  MF_GEO
+  __shared__ float colbuf[COL_CH * 4 * C];
+  LayerF<C, F> L1;
+  L1.load([&](int h, int k) { return Wt1[h * 2 * F + F + k]; }, lane);
+  floatx4 rs[NT];
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt) rs[tt] = ld_node<C>(Rs, tt, g4, NS, n, fvalid);
+  const floatx4 scv = ld_fconst<F>(sc, g4, 1.f), shv = ld_fconst<F>(sh, g4, 0.f);
+  MF_FMASK(F)
+
+  int cbase = c0;
+  auto load = [&](int c) {
+    Rows<1> r;
+    r.v[0] = ld_frows<F>(y, eo0 + (uint32_t)c * eoc, RB, g4);
+    return r;
+  };
+  class_stream<MF_DEPTH_FWD>(c0, c1, load, [&](const Rows<1>& rows, int c) {
+    const floatx4 x[1] = {edge_in<F>(rows.v[0], fm, sc, scv, shv)};
+    floatx4 z[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) z[tt] = rs[tt];
+    L1.apply(x, z);
+    const int cl = c - cbase;
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+      for (int r = 0; r < GM<C>::nreg(tt); ++r) {
+        const float s = row_sum16(fvalid ? lrelu(z[tt][r]) : 0.f);
+        const int h = GM<C>::row(g4, 4 * tt + r);
+        if (j16 == 15 && h >= 0) colbuf[(cl * 4 + wave) * C + h] = s;
+      }
+    if (cl == COL_CH - 1 || c == c1 - 1) {
+      __syncthreads();
+      col_flush<C>(colbuf, cl + 1, cbase, part, colbase);
+      __syncthreads();
+      cbase = c + 1;
+    }
+  });
+}
+
+// ============================================================ TModel bwd
+// g_z = g_hsum[c] * lrelu'(z) per edge; per-fiber sums of g_z (-> g_Rs), the
+// edge-input gradient Wt1[:, F:2F]^T g_z (optional) and dWt1[:, F:2F] += g_z x^T.
+template <int F>
+__global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* __restrict__ y,
+                                                     const float* __restrict__ sc,
+                                                     const float* __restrict__ sh,
+                                                     const float* __restrict__ Rs,
+                                                     const float* __restrict__ Wt1,
+                                                     const float* __restrict__ ghS,
+                                                     float* __restrict__ GzT,
+                                                     float* __restrict__ gxe,
+                                                     float* __restrict__ partW) {
+  constexpr int C = 2 * F, NT = GM<C>::NT;
+  constexpr int NIMG = NT + 1;  // g_z tiles | x
+  MF_GEO
+  __shared__ short imgs[4 * NIMG * 2 * IMG_SHORTS];
+  __shared__ float scratch[4 * C * F];
+  __shared__ __attribute__((aligned(16))) float ghl[MF_MAX_CPS * ClassRows<C>::CP];
+  ClassRows<C>::stage(ghl, ghS, (long long)gg * geo.NC + c0, c1 - c0);
+  short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
+  LayerF<C, F> L1;
+  L1.load([&](int h, int k) { return Wt1[h * 2 * F + F + k]; }, lane);
+  LayerF<F, C> LT;
+  LT.load([&](int k, int h) { return gxe ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
+  floatx4 rs[NT], accF[NT], accW[NT];
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt) {
+    rs[tt] = ld_node<C>(Rs, tt, g4, NS, n, fvalid);
+    accF[tt] = zero4();
+    accW[tt] = zero4();
+  }
+  const floatx4 scv = ld_fconst<F>(sc, g4, 1.f), shv = ld_fconst<F>(sh, g4, 0.f);
+  MF_FMASK(F)
+  __syncthreads();   // ghl
+
+  auto load = [&](int c) {
+    Rows<1> r;
+    r.v[0] = ld_frows<F>(y, eo0 + (uint32_t)c * eoc, RB, g4);
+    return r;
+  };
+  class_stream<MF_DEPTH_BWD>(c0, c1, load, [&](const Rows<1>& rows, int c) {
+    const uint32_t eo = eo0 + (uint32_t)c * eoc;
+    const floatx4 x[1] = {edge_in<F>(rows.v[0], fm, sc, scv, shv)};
+    floatx4 z[NT], gz[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) z[tt] = rs[tt];
+    L1.apply(x, z);
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+      const floatx4 gh = ClassRows<C>::get(ghl, c - c0, tt, g4);
+      gz[tt] = zero4();
+#pragma unroll
+      for (int r = 0; r < GM<C>::nreg(tt); ++r) gz[tt][r] = fvalid ? gh[r] * dlrelu(z[tt][r]) : 0.f;
+      accF[tt] += gz[tt];
+    }
+    if (gxe) {
+      floatx4 gx[1] = {zero4()};
+      LT.apply(gz, gx);
+      st_frows<F>(gxe, eo, RB, g4, fvalid, gx[0]);
+    }
+    lds_order();
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) img_put2(img + tt * 2 * IMG_SHORTS, lane, split(gz[tt]));
+    img_put2(img + NT * 2 * IMG_SHORTS, lane, split(x[0]));
+    lds_order();
+    const Fr tx = img_tr2(img + NT * 2 * IMG_SHORTS, lane);
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt)
+      accW[tt] = mma3(img_tr2(img + tt * 2 * IMG_SHORTS, lane), tx, accW[tt]);
+  });
+  if (fvalid) {
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+      for (int r = 0; r < GM<C>::nreg(tt); ++r) {
+        const int h = GM<C>::row(g4, 4 * tt + r);
+        if (h >= 0) GzT[(size_t)ks * C * NS + (size_t)h * NS + n] = accF[tt][r];
+      }
+  }
+  block_partial(accW, scratch, C * F, [&](int a, int s, int jj) {
+    const int h = GM<C>::mrow(a, s), k = GM<F>::mrow(0, jj);
+    return (h >= 0 && k >= 0) ? h * F + k : -1;
+  }, partW + (size_t)bx * C * F);
+}
+
+// ============================================================ SModel bwd (+T, +BN sums)
+// Per edge: recompute the message (gnn.py:136-137), g_m from the per-fiber
+// moment coefficients (d loss / d m is a cubic in m - mean), back through the
+// message MLP; plus TModel's recomputed input gradient, the downstream edge
+// gradient and the edge BatchNorm's two gradient sums.  dWs2 += g_m a^T,
+// dbs2 += g_m, dWs1[:, F:2F] += g_zs x^T, per-class sums of g_zs (-> g_Qt).
+template <int F>
+__global__ __launch_bounds__(256, 2) void km_source_bwd(
+    EdgeGeo geo, const float* __restrict__ y, const float* __restrict__ sc,
+    const float* __restrict__ sh, const float* __restrict__ QtS, const float* __restrict__ Ws1,
+    const float* __restrict__ Ws2, const float* __restrict__ bs2, const float* __restrict__ mean,
+    const float* __restrict__ coef, const float* __restrict__ Rs, const float* __restrict__ Wt1,
+    const float* __restrict__ ghS, const float* __restrict__ g_next,
+    const float* __restrict__ mu1, const float* __restrict__ inv1, float* __restrict__ g_tot,
+    float* __restrict__ partW2, float* __restrict__ partW1, float* __restrict__ partCol,
+    float* __restrict__ partBN) {
+  constexpr int C = 2 * F, NT = GM<C>::NT;
+  constexpr int NIMG = 3 * NT + 1;          // g_m | a | g_zs | x
+  constexpr int SCR = C * (C + 1) > C * F ? C * (C + 1) : C * F;
+  MF_GEO
+  __shared__ short imgs[4 * NIMG * 2 * IMG_SHORTS];
+  __shared__ float colbuf[COL_CH * 4 * C];
+  __shared__ float scratch[4 * SCR];
+  __shared__ __attribute__((aligned(16))) float qtl[MF_MAX_CPS * ClassRows<C>::CP];
+  __shared__ __attribute__((aligned(16))) float ghl[MF_MAX_CPS * ClassRows<C>::CP];
+  ClassRows<C>::stage(qtl, QtS, (long long)gg * geo.NC + c0, c1 - c0);
+  if (ghS) ClassRows<C>::stage(ghl, ghS, (long long)gg * geo.NC + c0, c1 - c0);
+  short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
+  short* im_gm = img;
+  short* im_a = img + NT * 2 * IMG_SHORTS;
+  short* im_gz = im_a + NT * 2 * IMG_SHORTS;
+  short* im_x = im_gz + NT * 2 * IMG_SHORTS;
+  const long long CNS = (long long)C * NS;
+  const bool tpart = Rs != nullptr;
+
+  LayerF<C, F> L1s, L1t;
+  L1s.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
+  L1t.load([&](int h, int k) { return tpart ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
+  LayerF<C, C> L2, L2T;
+  L2.load([&](int o, int h) { return Ws2[o * C + h]; }, lane);
+  L2T.load([&](int h, int o) { return Ws2[o * C + h]; }, lane);
+  LayerF<F, C> L1sT, L1tT;
+  L1sT.load([&](int k, int h) { return Ws1[h * 2 * F + F + k]; }, lane);
+  L1tT.load([&](int k, int h) { return tpart ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
+  floatx4 rs[NT], bias[NT], mn[NT], q0[NT], q1[NT], q2[NT], q3[NT];
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt) {
+    rs[tt] = ld_node<C>(Rs, tt, g4, NS, n, fvalid);
+    bias[tt] = ld_vec<C>(bs2, tt, g4);
+    mn[tt] = ld_node<C>(mean, tt, g4, NS, n, fvalid);
+    q0[tt] = ld_node<C>(coef, tt, g4, NS, n, fvalid);
+    q1[tt] = ld_node<C>(coef + CNS, tt, g4, NS, n, fvalid);
+    q2[tt] = ld_node<C>(coef + 2 * CNS, tt, g4, NS, n, fvalid);
+    q3[tt] = ld_node<C>(coef + 3 * CNS, tt, g4, NS, n, fvalid);
+  }
+  const floatx4 scv = ld_fconst<F>(sc, g4, 1.f), shv = ld_fconst<F>(sh, g4, 0.f);
+  const floatx4 m1v = ld_fconst<F>(mu1, g4, 0.f), i1v = ld_fconst<F>(inv1, g4, 0.f);
+  MF_FMASK(F)
+
+  floatx4 accW2[NT * NT], accW1[NT], accB[NT];
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt) {
+    accW1[tt] = zero4();
+    accB[tt] = zero4();
+#pragma unroll
+    for (int nb = 0; nb < NT; ++nb) accW2[tt * NT + nb] = zero4();
+  }
+  floatx4 sg = zero4(), sgx = zero4();
+  __syncthreads();   // qtl, ghl
+
+  int cbase = c0;
+  auto load = [&](int c) {
+    Rows<2> r;
+    const uint32_t eo = eo0 + (uint32_t)c * eoc;
+    r.v[0] = ld_frows<F>(y, eo, RB, g4);
+    r.v[1] = g_next ? ld_frows<F>(g_next, eo, RB, g4) : zero4();
+    return r;
+  };
+  class_stream<MF_DEPTH_BWD>(c0, c1, load, [&](const Rows<2>& rows, int c) {
+    const uint32_t eo = eo0 + (uint32_t)c * eoc;
+    const floatx4 yr = rows.v[0], gnr = rows.v[1];
+    const floatx4 x[1] = {edge_in<F>(yr, fm, sc, scv, shv)};
+    // ---- forward recompute: z_s, a_s, m
+    floatx4 zs[NT], as[NT], m[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) zs[tt] = ClassRows<C>::get(qtl, c - c0, tt, g4);
+    L1s.apply(x, zs);
+    lrelu_act<C>(zs, as);
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) m[tt] = bias[tt];
+    L2.apply(as, m);
+    floatx4 gm[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+      gm[tt] = zero4();
+#pragma unroll
+      for (int r = 0; r < GM<C>::nreg(tt); ++r) {
+        const float d = m[tt][r] - mn[tt][r];
+        gm[tt][r] = fvalid ? fmaf(d, fmaf(d, fmaf(d, q3[tt][r], q2[tt][r]), q1[tt][r]), q0[tt][r]) : 0.f;
+      }
+      accB[tt] += gm[tt];
+    }
+    // ---- backward through the message MLP
+    floatx4 gz[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) gz[tt] = zero4();
+    L2T.apply(gm, gz);
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+      for (int r = 0; r < GM<C>::nreg(tt); ++r) gz[tt][r] *= dlrelu(zs[tt][r]);
+    floatx4 g[1] = {zero4()};
+    L1sT.apply(gz, g);
+    if (tpart) {  // TModel's per-edge input gradient, recomputed (gnn.py:188-190)
+      floatx4 zt[NT];
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) zt[tt] = rs[tt];
+      L1t.apply(x, zt);
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) {
+        const floatx4 gh = ClassRows<C>::get(ghl, c - c0, tt, g4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) zt[tt][r] = (fvalid && r < GM<C>::nreg(tt)) ? gh[r] * dlrelu(zt[tt][r]) : 0.f;
+      }
+      L1tT.apply(zt, g);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) g[0][r] = fm[r] ? g[0][r] + (g_next ? gnr[r] : 0.f) : 0.f;
+    st_frows<F>(g_tot, eo, RB, g4, fvalid, g[0]);
+    if (mu1) {
+#pragma unroll
+      for (int r = 0; r < GM<F>::RPG; ++r) {
+        sg[r] += g[0][r];
+        sgx[r] = fmaf(g[0][r], (yr[r] - m1v[r]) * i1v[r], sgx[r]);
+      }
+    }
+    // ---- weight gradients (edge = K) through the transposed images
+    lds_order();
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+      img_put2(im_gm + tt * 2 * IMG_SHORTS, lane, split(gm[tt]));
+      img_put2(im_a + tt * 2 * IMG_SHORTS, lane, split(as[tt]));
+      img_put2(im_gz + tt * 2 * IMG_SHORTS, lane, split(gz[tt]));
+    }
+    img_put2(im_x, lane, split(x[0]));
+    lds_order();
+    const Fr tx = img_tr2(im_x, lane);
+    Fr ta[NT];
+#pragma unroll
+    for (int nb = 0; nb < NT; ++nb) ta[nb] = img_tr2(im_a + nb * 2 * IMG_SHORTS, lane);
+    const int cl = c - cbase;
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+      const Fr tgm = img_tr2(im_gm + tt * 2 * IMG_SHORTS, lane);
+#pragma unroll
+      for (int nb = 0; nb < NT; ++nb) accW2[tt * NT + nb] = mma3(tgm, ta[nb], accW2[tt * NT + nb]);
+      const Fr tgz = img_tr2(im_gz + tt * 2 * IMG_SHORTS, lane);
+      accW1[tt] = mma3(tgz, tx, accW1[tt]);
+      const floatx4 cs = mf(tgz.h, ones16(), mf(tgz.l, ones16(), zero4()));
+      if (j16 == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int h = GM<C>::mrow(tt, 4 * g4 + r);
+          if (h >= 0) colbuf[(cl * 4 + wave) * C + h] = cs[r];
+        }
+      }
+    }
+    if (cl == COL_CH - 1 || c == c1 - 1) {
+      __syncthreads();
+      col_flush<C>(colbuf, cl + 1, cbase, partCol, colbase);
+      __syncthreads();
+      cbase = c + 1;
+    }
+  });
+  block_partial(accW2, scratch, C * (C + 1), [&](int a, int s, int jj) {
+    const int o = GM<C>::mrow(a / NT, s), h = GM<C>::mrow(a % NT, jj);
+    return (o >= 0 && h >= 0) ? o * (C + 1) + h : -1;
+  }, partW2 + (size_t)bx * C * (C + 1));
+  // dbs2 (exact fp32 sums of g_m: a bias gradient cancels to ~0 through the
+  // BatchNorm that follows) -> column C of the same partial
+  {
+    __syncthreads();
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+      for (int r = 0; r < GM<C>::nreg(tt); ++r) {
+        const float v = group_sum16(accB[tt][r]);
+        const int o = GM<C>::row(g4, 4 * tt + r);
+        if (j16 == 0 && o >= 0) scratch[wave * C + o] = v;
+      }
+    __syncthreads();
+    if (t < C)
+      partW2[(size_t)bx * C * (C + 1) + t * (C + 1) + C] =
+          ((scratch[t] + scratch[C + t]) + scratch[2 * C + t]) + scratch[3 * C + t];
+  }
+  block_partial(accW1, scratch, C * F, [&](int a, int s, int jj) {
+    const int h = GM<C>::mrow(a, s), k = GM<F>::mrow(0, jj);
+    return (h >= 0 && k >= 0) ? h * F + k : -1;
+  }, partW1 + (size_t)bx * C * F);
+  if (mu1) {
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < GM<F>::RPG; ++r) {
+      const float a = group_sum16(sg[r]), b = group_sum16(sgx[r]);
+      const int k = GM<F>::row(g4, r);
+      if (j16 == 0 && k >= 0) { scratch[wave * 2 * F + k] = a; scratch[wave * 2 * F + F + k] = b; }
+    }
+    __syncthreads();
+    if (t < 2 * F)
+      partBN[(size_t)bx * 2 * F + t] =
+          ((scratch[t] + scratch[2 * F + t]) + scratch[4 * F + t]) + scratch[6 * F + t];
+  }
+}
+
+// ============================================================ EdgeModel bwd
+// g_y = alpha*g + gam0 + gam1*y (the double BatchNorm's backward, per channel),
+// then back through the edge MLP: dW2 += g_y a^T, db2 += g_y,
+// dW1[:, 2F:3F] += g_z x^T, per-fiber (-> g_Ps) and per-class (-> g_Pt) sums of
+// g_z, and the edge-input gradient W1[:, 2F:3F]^T g_z when the block has an
+// upstream edge input.
+template <int F>
+__global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
+    EdgeGeo geo, const float* __restrict__ g_tot, const float* __restrict__ alpha,
+    const float* __restrict__ gam0, const float* __restrict__ gam1, const float* __restrict__ y,
+    const float* __restrict__ xe, const float* __restrict__ xsc, const float* __restrict__ xsh,
+    const float* __restrict__ Ps, const float* __restrict__ PtS, const float* __restrict__ W1,
+    const float* __restrict__ W2, float* __restrict__ gxe, float* __restrict__ GzEs,
+    float* __restrict__ partW2, float* __restrict__ partW1, float* __restrict__ partCol) {
+  constexpr int H = 4 * F, NT = GM<H>::NT;
+  constexpr int NIMG = 1 + NT + NT + 1;          // g_y | a | g_z | x
+  constexpr int SCR = F * (H + 1) > H * F ? F * (H + 1) : H * F;
+  MF_GEO
+  __shared__ short imgs[4 * NIMG * 2 * IMG_SHORTS];
+  __shared__ float colbuf[COL_CH * 4 * H];
+  __shared__ float scratch[4 * SCR];
+  __shared__ __attribute__((aligned(16))) float ptl[MF_MAX_CPS * ClassRows<H>::CP];
+  ClassRows<H>::stage(ptl, PtS, (long long)gg * geo.NC + c0, c1 - c0);
+  short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
+  short* im_gy = img;
+  short* im_a = img + 2 * IMG_SHORTS;
+  short* im_gz = im_a + NT * 2 * IMG_SHORTS;
+  short* im_x = im_gz + NT * 2 * IMG_SHORTS;
+
+  LayerF<H, F> L1, L2T;
+  L1.load([&](int h, int k) { return W1[h * 4 * F + 2 * F + k]; }, lane);
+  L2T.load([&](int h, int o) { return W2[o * H + h]; }, lane);
+  LayerF<F, H> L1T;
+  L1T.load([&](int k, int h) { return gxe ? W1[h * 4 * F + 2 * F + k] : 0.f; }, lane);
+  floatx4 ps[NT], accF[NT], accW1[NT], accW2[NT];
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt) {
+    ps[tt] = ld_node<H>(Ps, tt, g4, NS, n, fvalid);
+    accF[tt] = zero4();
+    accW1[tt] = zero4();
+    accW2[tt] = zero4();
+  }
+  floatx4 accB = zero4();
+  const floatx4 alv = ld_fconst<F>(alpha, g4, 0.f), g0v = ld_fconst<F>(gam0, g4, 0.f),
+                g1v = ld_fconst<F>(gam1, g4, 0.f);
+  const floatx4 scv = ld_fconst<F>(xsc, g4, 1.f), shv = ld_fconst<F>(xsh, g4, 0.f);
+  MF_FMASK(F)
+  __syncthreads();   // ptl
+
+  int cbase = c0;
+  auto load = [&](int c) {
+    Rows<3> r;
+    const uint32_t eo = eo0 + (uint32_t)c * eoc;
+    r.v[0] = ld_frows<F>(g_tot, eo, RB, g4);
+    r.v[1] = ld_frows<F>(y, eo, RB, g4);
+    r.v[2] = ld_frows<F>(xe, eo, RB, g4);
+    return r;
+  };
+  class_stream<MF_DEPTH_BWD>(c0, c1, load, [&](const Rows<3>& rows, int c) {
+    const uint32_t eo = eo0 + (uint32_t)c * eoc;
+    floatx4 gy[1] = {zero4()};
+#pragma unroll
+    for (int r = 0; r < GM<F>::RPG; ++r)
+      gy[0][r] = fm[r] ? fmaf(g1v[r], rows.v[1][r], fmaf(alv[r], rows.v[0][r], g0v[r])) : 0.f;
+    accB += gy[0];
+    const floatx4 x[1] = {edge_in<F>(rows.v[2], fm, xsc, scv, shv)};
+    floatx4 z[NT], a[NT], gz[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+      z[tt] = ps[tt] + ClassRows<H>::get(ptl, c - c0, tt, g4);
+      gz[tt] = zero4();
+    }
+    L1.apply(x, z);
+    lrelu_act<H>(z, a);
+    L2T.apply(gy, gz);
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+#pragma unroll
+      for (int r = 0; r < GM<H>::nreg(tt); ++r) gz[tt][r] *= dlrelu(z[tt][r]);
+      accF[tt] += gz[tt];
+    }
+    if (gxe) {
+      floatx4 gx[1] = {zero4()};
+      L1T.apply(gz, gx);
+      st_frows<F>(gxe, eo, RB, g4, fvalid, gx[0]);
+    }
+    lds_order();
+    img_put2(im_gy, lane, split(gy[0]));
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+      img_put2(im_a + tt * 2 * IMG_SHORTS, lane, split(a[tt]));
+      img_put2(im_gz + tt * 2 * IMG_SHORTS, lane, split(gz[tt]));
+    }
+    img_put2(im_x, lane, split(x[0]));
+    lds_order();
+    const Fr tgy = img_tr2(im_gy, lane);
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt)
+      accW2[tt] = mma3(tgy, img_tr2(im_a + tt * 2 * IMG_SHORTS, lane), accW2[tt]);
+    const Fr tx = img_tr2(im_x, lane);
+    const int cl = c - cbase;
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+      const Fr tgz = img_tr2(im_gz + tt * 2 * IMG_SHORTS, lane);
+      accW1[tt] = mma3(tgz, tx, accW1[tt]);
+      const floatx4 cs = mf(tgz.h, ones16(), mf(tgz.l, ones16(), zero4()));
+      if (j16 == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int h = GM<H>::mrow(tt, 4 * g4 + r);
+          if (h >= 0) colbuf[(cl * 4 + wave) * H + h] = cs[r];
+        }
+      }
+    }
+    if (cl == COL_CH - 1 || c == c1 - 1) {
+      __syncthreads();
+      col_flush<H>(colbuf, cl + 1, cbase, partCol, colbase);
+      __syncthreads();
+      cbase = c + 1;
+    }
+  });
+  if (fvalid) {
+    float* dst = GzEs + (size_t)ks * H * NS + n;
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+      for (int r = 0; r < GM<H>::nreg(tt); ++r) {
+        const int h = GM<H>::row(g4, 4 * tt + r);
+        if (h >= 0) dst[(size_t)h * NS] = accF[tt][r];
+      }
+  }
+  block_partial(accW2, scratch, F * (H + 1), [&](int a, int s, int jj) {
+    const int o = GM<F>::mrow(0, s), h = GM<H>::mrow(a, jj);
+    return (o >= 0 && h >= 0) ? o * (H + 1) + h : -1;
+  }, partW2 + (size_t)bx * F * (H + 1));
+  {  // db2 (exact fp32 sums of g_y) -> column H of the same partial
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < GM<F>::RPG; ++r) {
+      const float v = group_sum16(accB[r]);
+      const int o = GM<F>::row(g4, r);
+      if (j16 == 0 && o >= 0) scratch[wave * F + o] = v;
+    }
+    __syncthreads();
+    if (t < F)
+      partW2[(size_t)bx * F * (H + 1) + t * (H + 1) + H] =
+          ((scratch[t] + scratch[F + t]) + scratch[2 * F + t]) + scratch[3 * F + t];
+  }
+  block_partial(accW1, scratch, H * F, [&](int a, int s, int jj) {
+    const int h = GM<H>::mrow(a, s), k = GM<F>::mrow(0, jj);
+    return (h >= 0 && k >= 0) ? h * F + k : -1;
+  }, partW1 + (size_t)bx * H * F);
+}
+
+// [D][NT] node table -> class-major slot-ordered rows [NT][16*GM<D>::NT]:
+// dst[cn][16t + 4g + r] = src[GM<D>::row(g, 4t + r)][cn] (0 for padding)
+__global__ void k_class_rows_slot(const float* __restrict__ src, int D, int RPG, int CP,
+                                  long long NT, float* __restrict__ dst) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // over NT*CP
+  if (idx >= NT * CP) return;
+  const long long cn = idx / CP;
+  const int q = (int)(idx - cn * CP);
+  const int tt = q >> 4, g = (q >> 2) & 3, r = q & 3;
+  const int s = 4 * tt + r, h = g * RPG + s;
+  dst[idx] = (s < RPG && h < D) ? src[(long long)h * NT + cn] : 0.f;
+}
+
+}  // namespace
+
+// ============================================================ host launchers
+#define MF_DISPATCH(F, ...)                                  \
+  switch (F) {                                               \
+    case 8: { constexpr int FF = 8; __VA_ARGS__; } break;    \
+    case 10: { constexpr int FF = 10; __VA_ARGS__; } break;  \
+    case 16: { constexpr int FF = 16; __VA_ARGS__; } break;  \
+    default: return pf::fail("pfsgnn mfma", "unsupported F");\
+  }
+
+namespace pfm {
+
+int class_cols(int D) { return 16 * (((D + 3) / 4 + 3) / 4); }
+
+void class_rows_slot(const float* src, int D, long long NT, float* dst, hipStream_t st) {
+  const int CP = class_cols(D);
+  const long long len = NT * CP;
+  hipLaunchKernelGGL(k_class_rows_slot, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, st, src,
+                     D, (D + 3) / 4, CP, NT, dst);
+}
+
+int edge_mlp_fwd(const EdgeGeo& geo, int F, const float* xe, const float* xsc, const float* xsh,
+                 const float* Ps, const float* PtS, const float* W1, const float* W2,
+                 const float* b2, float* y, float* part, hipStream_t st) {
+  MF_DISPATCH(F, hipLaunchKernelGGL(km_edge_mlp_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
+                                    xe, xsc, xsh, Ps, PtS, W1, W2, b2, y, part));
+  return 0;
+}
+
+int source_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
+               const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
+               float* partS, hipStream_t st) {
+  MF_DISPATCH(F, hipLaunchKernelGGL(km_source_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
+                                    y, sc, sh, QtS, Ws1, Ws2, bs2, partS));
+  return 0;
+}
+
+int target_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
+               const float* Rs, const float* Wt1, float* part, hipStream_t st) {
+  MF_DISPATCH(F, hipLaunchKernelGGL(km_target_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
+                                    y, sc, sh, Rs, Wt1, part));
+  return 0;
+}
+
+int target_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
+               const float* Rs, const float* Wt1, const float* ghS, float* gz, float* gxe,
+               float* part, hipStream_t st) {
+  MF_DISPATCH(F, hipLaunchKernelGGL(km_target_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
+                                    y, sc, sh, Rs, Wt1, ghS, gz, gxe, part));
+  return 0;
+}
+
+int source_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
+               const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
+               const float* mean, const float* coef, const float* Rs, const float* Wt1,
+               const float* ghS, const float* g_next, const float* mu1, const float* inv1,
+               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN, hipStream_t st) {
+  MF_DISPATCH(F, hipLaunchKernelGGL(km_source_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
+                                    y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghS,
+                                    g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN));
+  return 0;
+}
+
+int edge_mlp_bwd(const EdgeGeo& geo, int F, const float* g_tot, const float* alpha,
+                 const float* gam0, const float* gam1, const float* y, const float* xe,
+                 const float* xsc, const float* xsh, const float* Ps, const float* PtS,
+                 const float* W1, const float* W2, float* gxe, float* gs, float* pW2, float* pW1,
+                 float* pCol, hipStream_t st) {
+  MF_DISPATCH(F, hipLaunchKernelGGL(km_edge_mlp_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
+                                    g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, PtS, W1, W2,
+                                    gxe, gs, pW2, pW1, pCol));
+  return 0;
+}
+
+}  // namespace pfm

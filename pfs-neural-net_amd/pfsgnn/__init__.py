@@ -6,7 +6,7 @@ TModel, GlobalModel, Block, GNN) and the ``src/train.py`` objective
 (``softfloor``, ``loss_function``), computed by hand-written HIP kernels for
 gfx950 in ``libpfsgnn.so`` (C ABI: ``include/pfsgnn.h``).
 """
-from .native import NativeUnavailable, HipBackend  # noqa: F401
+from .native import NativeUnavailable, HipBackend, set_edge_path, get_edge_path  # noqa: F401
 from .gnn import (BipartiteData, Loader, Batch, MLP, EdgeModel, SModel, TModel,  # noqa: F401
                   GlobalModel, Block, GNN)
 from .train import softfloor, loss_function  # noqa: F401

@@ -33,6 +33,8 @@ _SIGS = {
     "pfsgnn_version": ([], ctypes.c_char_p),
     "pfsgnn_last_error": ([], ctypes.c_char_p),
     "pfsgnn_workspace_bytes": ([I, I, I, I], SZ),
+    "pfsgnn_set_edge_path": ([I], I),
+    "pfsgnn_get_edge_path": ([], I),
     "pfsgnn_timing_enable": ([I], I),
     "pfsgnn_timing_reset": ([], I),
     "pfsgnn_timing_query": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
@@ -81,7 +83,27 @@ def lib():
             fn.argtypes = args
             fn.restype = ret
         _lib = L
+        path = os.environ.get("PFSGNN_EDGE_PATH")
+        if path:
+            set_edge_path(path)
     return _lib
+
+
+EDGE_PATHS = {"valu": 0, "mfma": 1}
+
+
+def set_edge_path(path):
+    """Implementation of the per-edge kernels: "mfma" (default; matrix cores,
+    exact fp32 layer products) or "valu" (fp32 fmaf chains on the vector ALU).
+    Read at launch time; env PFSGNN_EDGE_PATH sets it when the library loads."""
+    if path not in EDGE_PATHS:
+        raise ValueError(f"edge path must be one of {sorted(EDGE_PATHS)}, got {path!r}")
+    _check(lib().pfsgnn_set_edge_path(EDGE_PATHS[path]), "pfsgnn_set_edge_path")
+
+
+def get_edge_path():
+    code = lib().pfsgnn_get_edge_path()
+    return {v: k for k, v in EDGE_PATHS.items()}[code]
 
 
 def exported_symbols():
