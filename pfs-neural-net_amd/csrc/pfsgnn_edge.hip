@@ -1119,22 +1119,18 @@ void fiber_finish(const EdgeGeo& geo, int C, const float* dst, float* out, hipSt
                      geo.KS, len, out);
 }
 
-// per-class node table for the MFMA kernels: class-major, in their slot order
-const float* class_rows_p(const float* src, int C, const EdgeGeo& geo, Ws& w, hipStream_t st) {
-  if (!src) return nullptr;
-  float* dst = w.take((size_t)geo.NT * pfm::class_cols(C));
-  if (!dst) return nullptr;
-  pfm::class_rows_slot(src, C, geo.NT, dst, st);
-  return dst;
-}
-
 int g_path = PFSGNN_EDGE_MFMA;
 bool use_mfma() { return g_path == PFSGNN_EDGE_MFMA; }
 // MFMA blocks stage their class-table rows in LDS: at most MAX_CPS classes each
 EdgeGeo geo_mfma(int G, int NF, int NC) {
   const long long groups = (long long)G * ((NF + 63) / 64);
   const long long min_ks = (NC + pfm::MAX_CPS - 1) / pfm::MAX_CPS;
-  const long long target = std::max<long long>(pfm::TARGET_BLOCKS, groups * min_ks);
+  static const long long tb = [] {  // tuning knob: PFSGNN_MFMA_BLOCKS (grid target)
+    const char* e = getenv("PFSGNN_MFMA_BLOCKS");
+    const long long v = e ? atoll(e) : 0;
+    return v > 0 ? v : (long long)pfm::TARGET_BLOCKS;
+  }();
+  const long long target = std::max<long long>(tb, groups * min_ks);
   return make_geo(G, NF, NC, (int)std::min<long long>(target, 1ll << 30));
 }
 EdgeGeo geo_for(int G, int NF, int NC) {
@@ -1164,7 +1160,7 @@ size_t edge_ws_floats(const EdgeGeo& geo, int G, int NC, int F) {
   edge = std::max(edge, nb * (C * (C + 1) + C * F + 2 * F) + colp * C + 4096);      // source bwd
   edge = std::max(edge, nb * (F * (H + 1) + H * F) + colp * H + ks * H * NS + 4096);  // edge bwd
   edge = std::max(edge, colp * 4 + ks * NS + nb * (F * (F + 1) + F + 1) + 4096);   // loss
-  edge += (size_t)geo.NT * (pfm::class_cols(H) + 2 * pfm::class_cols(C)) + 4 * H * H + 8 * 256;
+  edge += (size_t)geo.NT * (H + 2 * C) + 4 * H * H + 8 * 256;
   return edge;
 }
 }  // namespace
@@ -1191,10 +1187,9 @@ extern "C" int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe
   hipStream_t st = as_stream(stream);
   float* part = w.take((size_t)geo.nblocks * (1 + 2 * F));
   if (use_mfma()) {
-    const float* PtP = class_rows_p(Pt, 4 * F, geo, w, st);
-    PF_REQUIRE(part && PtP, "pfsgnn_edge_mlp_fwd", "workspace too small");
+    PF_REQUIRE(part, "pfsgnn_edge_mlp_fwd", "workspace too small");
     { pf::Timer tm_("edge_mlp_fwd", st);
-    if (int rc = pfm::edge_mlp_fwd(geo, F, xe, xsc, xsh, Ps, PtP, W1, W2, b2, y, part, st)) return rc;
+    if (int rc = pfm::edge_mlp_fwd(geo, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part, st)) return rc;
     tm_.end(); }
     hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(256), 0, st, part, geo.nblocks, F, geo.E,
                        mu, var);
@@ -1224,10 +1219,9 @@ extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, c
   hipStream_t st = as_stream(stream);
   float* partS = w.take((size_t)geo.KS * 4 * C * geo.NS);
   if (use_mfma()) {
-    const float* QtP = class_rows_p(Qt, C, geo, w, st);
-    PF_REQUIRE(partS && QtP, "pfsgnn_source_fwd", "workspace too small");
+    PF_REQUIRE(partS, "pfsgnn_source_fwd", "workspace too small");
     pf::Timer tm_("source_fwd", st);
-    if (int rc = pfm::source_fwd(geo, F, y, sc, sh, QtP, Ws1, Ws2, bs2, partS, st)) return rc;
+    if (int rc = pfm::source_fwd(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, partS, st)) return rc;
     tm_.end();
   } else {
   const float* QtT = class_rows(Qt, C, geo, w, st);
@@ -1278,7 +1272,7 @@ extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, c
   hipStream_t st = as_stream(stream);
   float* part = w.take((size_t)geo.nblocks * C * F);
   float* gz = fiber_dst(geo, C, GzT, w);
-  const float* ghT = use_mfma() ? class_rows_p(g_hsum, C, geo, w, st)
+  const float* ghT = use_mfma() ? g_hsum
                                 : class_rows(g_hsum, C, geo, w, st);
   PF_REQUIRE(part && gz && ghT, "pfsgnn_target_bwd", "workspace too small");
   { pf::Timer tm_("target_bwd", st);
@@ -1318,8 +1312,8 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
   float* pBN = w.take(nb * 2 * F);
   hipStream_t st = as_stream(stream);
   const bool mfma = use_mfma();
-  const float* QtT = mfma ? class_rows_p(Qt, C, geo, w, st) : class_rows(Qt, C, geo, w, st);
-  const float* ghT = mfma ? class_rows_p(g_hsum, C, geo, w, st) : class_rows(g_hsum, C, geo, w, st);
+  const float* QtT = mfma ? Qt : class_rows(Qt, C, geo, w, st);
+  const float* ghT = mfma ? g_hsum : class_rows(g_hsum, C, geo, w, st);
   PF_REQUIRE(pW2 && pW1 && pCol && pBN && QtT && (ghT || !g_hsum), "pfsgnn_source_bwd",
              "workspace too small");
   { pf::Timer tm_("source_bwd", st);
@@ -1389,10 +1383,9 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
   float* gs = fiber_dst(geo, H, GzEs, w);
   hipStream_t st = as_stream(stream);
   if (use_mfma()) {
-    const float* PtP = class_rows_p(Pt, H, geo, w, st);
-    PF_REQUIRE(pW2 && pW1 && pCol && gs && PtP, "pfsgnn_edge_mlp_bwd", "workspace too small");
+    PF_REQUIRE(pW2 && pW1 && pCol && gs, "pfsgnn_edge_mlp_bwd", "workspace too small");
     pf::Timer tm_("edge_mlp_bwd", st);
-    if (int rc = pfm::edge_mlp_bwd(geo, F, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, PtP, W1,
+    if (int rc = pfm::edge_mlp_bwd(geo, F, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1,
                                    W2, gxe, gs, pW2, pW1, pCol, st))
       return rc;
     tm_.end();

@@ -3,9 +3,8 @@
 // Same inputs, outputs and per-block partial formats as the fp32 VALU kernels
 // of pfsgnn_edge.hip, so the entry points in pfsgnn_edge.hip pick one or the
 // other per call (pfsgnn_set_edge_path) and share every finishing reduction.
-// Per-class node tables are passed class-major in the kernels' slot order
-// (class_rows_slot): a lane group reads each of its 4-row register tiles as
-// one float4.
+// Per-class node tables (Pt, Qt, g_hsum) are passed channel-major [D][NT] as
+// the node ops produce them; each block stages its class rows in LDS.
 #pragma once
 #include "pfsgnn_common.h"
 
@@ -38,10 +37,5 @@ int edge_mlp_bwd(const EdgeGeo& geo, int F, const float* g_tot, const float* alp
                  const float* xsc, const float* xsh, const float* Ps, const float* PtS,
                  const float* W1, const float* W2, float* gxe, float* gs, float* pW2, float* pW1,
                  float* pCol, hipStream_t st);
-
-// columns of a slot-ordered class table of a D-wide node tensor (16 per tile)
-int class_cols(int D);
-// [D][NT] node table -> class-major slot-ordered rows [NT][class_cols(D)]
-void class_rows_slot(const float* src, int D, long long NT, float* dst, hipStream_t st);
 
 }  // namespace pfm

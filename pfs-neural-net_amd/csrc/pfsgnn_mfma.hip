@@ -230,17 +230,21 @@ __device__ __forceinline__ floatx4 ld_node(const float* p, int t, int g, long lo
   return v;
 }
 
-// The block's class rows [c0, c1) of a slot-ordered class table, staged in LDS
-// once (they are re-read for every tile of every wave); MF_MAX_CPS bounds the
-// class range of an MFMA block (pfm::MAX_CPS, geo_mfma in pfsgnn_edge.hip).
+// The block's class rows [c0, c1) of a channel-major per-class node table
+// [D][NT], staged once in LDS in the kernels' slot order (they are re-read for
+// every tile of every wave): buf[cl][16t + 4g + r] = P[row(g, 4t + r)][cn0 + cl].
+// MF_MAX_CPS bounds the class range of an MFMA block (pfm::MAX_CPS, geo_mfma).
 #define MF_MAX_CPS 64
 template <int D>
 struct ClassRows {
   static constexpr int CP = 16 * GM<D>::NT;
-  __device__ __forceinline__ static void stage(float* buf, const float* P, long long cn0, int ncl) {
-    const floatx4* src = reinterpret_cast<const floatx4*>(P + cn0 * CP);
-    floatx4* dst = reinterpret_cast<floatx4*>(buf);
-    for (int i = threadIdx.x; i < ncl * CP / 4; i += PF_BLOCK) dst[i] = src[i];
+  __device__ __forceinline__ static void stage(float* buf, const float* P, long long NT,
+                                               long long cn0, int ncl) {
+    for (int i = threadIdx.x; i < ncl * CP; i += PF_BLOCK) {
+      const int cl = i / CP, q = i - cl * CP;
+      const int h = GM<D>::row((q >> 2) & 3, 4 * (q >> 4) + (q & 3));
+      buf[i] = h >= 0 ? P[(long long)h * NT + cn0 + cl] : 0.f;
+    }
   }
   __device__ __forceinline__ static floatx4 get(const float* buf, int cl, int t, int g) {
     return *reinterpret_cast<const floatx4*>(buf + cl * CP + 16 * t + 4 * g);
@@ -414,7 +418,7 @@ __global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float*
   constexpr int H = 4 * F, NT = GM<H>::NT;
   MF_GEO
   __shared__ __attribute__((aligned(16))) float ptl[MF_MAX_CPS * ClassRows<H>::CP];
-  ClassRows<H>::stage(ptl, PtS, (long long)gg * geo.NC + c0, c1 - c0);
+  ClassRows<H>::stage(ptl, PtS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
   LayerF<H, F> L1;
   L1.load([&](int h, int k) { return W1[h * 4 * F + 2 * F + k]; }, lane);
   LayerF<F, H> L2;
@@ -517,7 +521,7 @@ __global__ __launch_bounds__(256) void km_source_fwd(EdgeGeo geo, const float* _
   constexpr int C = 2 * F, NT = GM<C>::NT;
   MF_GEO
   __shared__ __attribute__((aligned(16))) float qtl[MF_MAX_CPS * ClassRows<C>::CP];
-  ClassRows<C>::stage(qtl, QtS, (long long)gg * geo.NC + c0, c1 - c0);
+  ClassRows<C>::stage(qtl, QtS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
   LayerF<C, F> L1;
   L1.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
   LayerF<C, C> L2;
@@ -650,7 +654,7 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
   __shared__ short imgs[4 * NIMG * 2 * IMG_SHORTS];
   __shared__ float scratch[4 * C * F];
   __shared__ __attribute__((aligned(16))) float ghl[MF_MAX_CPS * ClassRows<C>::CP];
-  ClassRows<C>::stage(ghl, ghS, (long long)gg * geo.NC + c0, c1 - c0);
+  ClassRows<C>::stage(ghl, ghS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
   short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
   LayerF<C, F> L1;
   L1.load([&](int h, int k) { return Wt1[h * 2 * F + F + k]; }, lane);
@@ -742,8 +746,8 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   __shared__ float scratch[4 * SCR];
   __shared__ __attribute__((aligned(16))) float qtl[MF_MAX_CPS * ClassRows<C>::CP];
   __shared__ __attribute__((aligned(16))) float ghl[MF_MAX_CPS * ClassRows<C>::CP];
-  ClassRows<C>::stage(qtl, QtS, (long long)gg * geo.NC + c0, c1 - c0);
-  if (ghS) ClassRows<C>::stage(ghl, ghS, (long long)gg * geo.NC + c0, c1 - c0);
+  ClassRows<C>::stage(qtl, QtS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
+  if (ghS) ClassRows<C>::stage(ghl, ghS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
   short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
   short* im_gm = img;
   short* im_a = img + NT * 2 * IMG_SHORTS;
@@ -953,7 +957,7 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
   __shared__ float colbuf[COL_CH * 4 * H];
   __shared__ float scratch[4 * SCR];
   __shared__ __attribute__((aligned(16))) float ptl[MF_MAX_CPS * ClassRows<H>::CP];
-  ClassRows<H>::stage(ptl, PtS, (long long)gg * geo.NC + c0, c1 - c0);
+  ClassRows<H>::stage(ptl, PtS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
   short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
   short* im_gy = img;
   short* im_a = img + 2 * IMG_SHORTS;
@@ -1085,19 +1089,6 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
   }, partW1 + (size_t)bx * H * F);
 }
 
-// [D][NT] node table -> class-major slot-ordered rows [NT][16*GM<D>::NT]:
-// dst[cn][16t + 4g + r] = src[GM<D>::row(g, 4t + r)][cn] (0 for padding)
-__global__ void k_class_rows_slot(const float* __restrict__ src, int D, int RPG, int CP,
-                                  long long NT, float* __restrict__ dst) {
-  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // over NT*CP
-  if (idx >= NT * CP) return;
-  const long long cn = idx / CP;
-  const int q = (int)(idx - cn * CP);
-  const int tt = q >> 4, g = (q >> 2) & 3, r = q & 3;
-  const int s = 4 * tt + r, h = g * RPG + s;
-  dst[idx] = (s < RPG && h < D) ? src[(long long)h * NT + cn] : 0.f;
-}
-
 }  // namespace
 
 // ============================================================ host launchers
@@ -1110,15 +1101,6 @@ __global__ void k_class_rows_slot(const float* __restrict__ src, int D, int RPG,
   }
 
 namespace pfm {
-
-int class_cols(int D) { return 16 * (((D + 3) / 4 + 3) / 4); }
-
-void class_rows_slot(const float* src, int D, long long NT, float* dst, hipStream_t st) {
-  const int CP = class_cols(D);
-  const long long len = NT * CP;
-  hipLaunchKernelGGL(k_class_rows_slot, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, st, src,
-                     D, (D + 3) / 4, CP, NT, dst);
-}
 
 int edge_mlp_fwd(const EdgeGeo& geo, int F, const float* xe, const float* xsc, const float* xsh,
                  const float* Ps, const float* PtS, const float* W1, const float* W2,
