@@ -27,6 +27,7 @@ import torch.distributed as dist  # noqa: E402
 
 NF, NC, FDIM = 2394, 128, 10
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense fp32-input MFMA (= fp32 vector peak)
 
 
 def parse():
@@ -74,6 +75,22 @@ def kernel_bytes_per_edge(F, first_block_excluded=False):
     }
 
 
+# per-edge algorithmic FLOPs (2 per real multiply-add of the unpadded layer
+# shapes); H = 4F hidden units of the EdgeModel MLP,
+# C = 2F of the S/T message MLPs.  source_bwd includes TModel's recomputed
+# input gradient; edge_mlp_bwd's input-gradient product is absent in block 0.
+def kernel_flops_per_edge(F, B):
+    H, C = 4 * F, 2 * F
+    return {
+        "edge_mlp_fwd": 2 * (H * F + F * H) + 4 * H,
+        "source_fwd": 2 * (C * F + C * C) + 4 * C + 14 * C,
+        "target_fwd": 2 * C * F + 4 * C,
+        "target_bwd": 2 * (C * F + C * F) + 3 * C,
+        "source_bwd": 2 * (C * F + C * C + C * C + F * C + C * F + F * C + C * C + C * F) + 12 * C,
+        "edge_mlp_bwd": 2 * (H * F + H * F + H * F + F * H) + 2 * (F * H) * (B - 1) / B + 8 * H,
+    }
+
+
 def pmc_traffic(kernel, E, F):
     """HBM bytes per launch of `kernel` from the latest committed PMC pass
     (profiles/<round>_traffic.json, made by tools/prof_pmc.sh +
@@ -86,7 +103,9 @@ def pmc_traffic(kernel, E, F):
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
-        key = f"k_{kernel}<{F}>"
+        from pfsgnn import native
+        pre = "km_" if native.get_edge_path() == "mfma" else "k_"
+        key = f"{pre}{kernel}<{F}>"
         if d.get("E") == E and d.get("F") == F and key in d.get("kernels", {}):
             return d["kernels"][key]["traffic_bytes"], os.path.basename(path)
     return None
@@ -247,11 +266,25 @@ def main():
         launches_bytes = (per_edge[dom] * (B - 1) + 3 * 4 * FDIM) * E / B
     avg_s = ms / n / 1e3
     achieved = launches_bytes / avg_s / 1e9
+    flops = kernel_flops_per_edge(FDIM, B).get(dom)
     tr = pmc_traffic(dom, E, FDIM)
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+    hbm = {"achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4)}
+    # both roofs of the dominant kernel; "bound" names the binding one (the
+    # larger fraction): the fp32-MFMA edge kernels do ~40 flop per HBM byte,
+    # well past the fp32 ridge point (157.3 TF/s / 8 TB/s ~ 20 flop/B)
+    mfma = None
+    if flops is not None:
+        tfs = flops * E / avg_s / 1e12
+        mfma = {"achieved": round(tfs, 2), "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": round(tfs / F32_MFMA_PEAK_TFS, 4), "flops_per_launch": int(flops * E)}
+    top = mfma if mfma is not None and mfma["frac"] > hbm["frac"] else hbm
+    roofline = {"bound": "mfma" if top is mfma else "hbm", "kernel": dom,
+                "achieved": top["achieved"], "peak": top["peak"], "unit": top["unit"],
+                "frac": top["frac"],
                 "traffic": None if tr is None else int(tr[0]),
                 "traffic_source": None if tr is None else f"profiles/{tr[1]} (PMC bytes per launch)",
+                "hbm": hbm, "mfma": mfma,
                 "avg_launch_us": round(avg_s * 1e6, 1), "launches": n,
                 "bytes_per_launch": int(launches_bytes),
                 "kernel_ms_per_step": {k: round(v[0] / prof_steps, 3) for k, v in kt.items()}}

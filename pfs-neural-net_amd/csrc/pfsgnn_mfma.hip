@@ -95,7 +95,9 @@ struct LayerF {
       }
   }
   __device__ __forceinline__ void apply(const floatx4 (&x)[GM<K>::NT], floatx4 (&y)[MT]) const {
-    if constexpr (KS >= 6) {
+    // one output tile: a lone dependent chain unless split; several tiles
+    // interleave their chains already
+    if constexpr (KS >= 6 || (MT == 1 && KS >= 4)) {
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
         floatx4 e = y[t], o = zero4();

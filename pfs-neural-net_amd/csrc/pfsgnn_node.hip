@@ -436,7 +436,7 @@ __global__ __launch_bounds__(512) void k_wgrad(const float* __restrict__ dY, int
 
 static int wgrad_blocks(int N) {
   int s = (N + 127) / 128;
-  return std::max(1, std::min(s, 512));
+  return std::max(1, std::min(s, 256));   // <= 2*RED_SEG: one reduce launch
 }
 
 extern "C" int pfsgnn_wgrad(const float* dY, int M, const float* X, int K, int N, int act_in,

@@ -16,4 +16,5 @@ for r in rows:
     disp[k].add(r["Dispatch_Id"])
 for k, v in sorted(agg.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", kv[1].get("FETCH_SIZE", 0))):
     n = len(disp[k])
-    print(k.split("(")[0][:40].ljust(40), n, " ".join(f"{c}={x / n:.4g}" for c, x in sorted(v.items())))
+    nm = k.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+    print(nm[:40].ljust(40), n, " ".join(f"{c}={x / n:.4g}" for c, x in sorted(v.items())))

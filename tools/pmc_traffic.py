@@ -21,12 +21,17 @@ E = int(sys.argv[3]) if len(sys.argv) > 3 else 16 * 2394 * 128
 F = int(sys.argv[4]) if len(sys.argv) > 4 else 10
 
 
+def kname(full):
+    """'void (anonymous namespace)::km_source_bwd<10>(EdgeGeo, ...)' -> 'km_source_bwd<10>'"""
+    return full.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+
+
 def per_dispatch(path, counter):
     agg, n = collections.defaultdict(float), collections.defaultdict(set)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        k = kname(r["Kernel_Name"])
         agg[k] += float(r["Counter_Value"])
         n[k].add(r["Dispatch_Id"])
     return {k: agg[k] / len(n[k]) * 1e3 for k in agg}   # KB -> bytes
