@@ -10,8 +10,8 @@ engine a torch-CPU emulation of the op set to check every hand-derived
 backward formula against the autograd oracle; the product never does.)
 
 Layouts (DESIGN.md §Data layout): node tensors are channel-major ``[C, N]``;
-edge tensors are channel-major ``[C, E]`` over the canonical fiber-major edge
-order ``e = (g*NF + f)*NC + c`` of a batch of G complete bipartite graphs.
+edge tensors are channel-major ``[C, E]`` over the canonical class-major edge
+order ``e = (g*NC + c)*NF + f`` of a batch of G complete bipartite graphs.
 Edge state is kept *lazily*: an EdgeModel output is its pre-norm value ``y``
 plus a per-channel affine ``(sc, sh)`` (xe_new = sc*y + sh) -- the triple
 ``xe3 = (y, sc, sh)``; consumers apply the affine on the fly, so inside the
