@@ -77,6 +77,57 @@ int pfsgnn_lin_t(const float* W, int ldw, int M, int K, const float* dY, int N,
 int pfsgnn_wgrad(const float* dY, int M, const float* X, int K, int N, int act_in,
                  float* dW, int lddw, float* db, float dbscale,
                  void* ws, size_t ws_bytes, void* stream);
+
+/* One row block of a virtually concatenated node input: the torch.cat of
+ * gnn.py:100 ([x_s[src], x_t[tgt], x_e, u[batch]]), :153 ([x, mean, std,
+ * skew, kurt, u[batch]]), :191 and :220, read in place instead of copied.
+ * x: `rows` channel-major rows.  per_graph == 0: x is [rows][N].
+ * per_graph > 0: x is [rows][N / per_graph] and node n reads column
+ * n / per_graph (the u[batch] broadcast; one value for all blocks of a list).
+ * col: the weight column that multiplies the block's first row.
+ * At most 4 blocks per list.                                                  */
+typedef struct {
+  const float* x;
+  int rows;
+  int col;
+  int per_graph;
+} pfsgnn_seg;
+
+/* pfsgnn_lin over a concatenated input: Y[m][n] (+)= sum over blocks s and
+ * their rows r of W[m][col_s + r] * act(x_s[r][n or n/per_graph]) + bscale*b[m] */
+int pfsgnn_lin_cat(const float* W, int ldw, int M, const pfsgnn_seg* segs, int nseg, int N,
+                   const float* b, float bscale, int act_in, float* Y, int add, void* stream);
+/* pfsgnn_wgrad over a concatenated input: dW[m][col_s + r] += sum_n dY[m][n] *
+ * act(x_s[r][n or n/per_graph]);  db[m] += dbscale * sum_n dY[m][n]            */
+int pfsgnn_wgrad_cat(const float* dY, int M, const pfsgnn_seg* segs, int nseg, int N,
+                     int act_in, float* dW, int lddw, float* db, float dbscale,
+                     void* ws, size_t ws_bytes, void* stream);
+
+/* Deferred weight gradients.  The node-level weight gradients of a backward
+ * pass (autograd's accumulation into .grad, train.py:140) are only read by the
+ * optimizer step, so their cross-block reductions can run together, after the
+ * backward: pfsgnn_wgrad_cat_part launches the per-block partials into `part`
+ * (pfsgnn_wgrad_part_bytes(M, K, N, has_db) bytes, owned by the caller until
+ * the reduction has run) and returns up to 5 reduction descriptors in red_out;
+ * pfsgnn_reduce_batch finishes any list of them in as few launches as the
+ * descriptors' output overlaps allow (fixed order: deterministic).          */
+typedef struct {
+  const float* part;
+  int nb;
+  size_t plen;
+  int ldp, rows, cols;
+  float* out;
+  int ldo, add;
+  float scale;
+} pfsgnn_red;
+
+size_t pfsgnn_wgrad_part_bytes(int M, int K, int N, int has_db);
+int pfsgnn_wgrad_cat_part(const float* dY, int M, const pfsgnn_seg* segs, int nseg, int N,
+                          int act_in, float* dW, int lddw, float* db, float dbscale,
+                          void* part, size_t part_bytes, pfsgnn_red* red_out, int* nred_out,
+                          void* stream);
+int pfsgnn_reduce_batch(const pfsgnn_red* reds, int n, void* stream);
+
 /* BatchNorm1d training forward over N rows (biased var for the output,
  * unbiased for the running update; rm/rv may be NULL). */
 int pfsgnn_bn_fwd(const float* X, int C, int N, const float* gamma, const float* beta,

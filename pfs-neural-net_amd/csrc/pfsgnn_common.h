@@ -230,7 +230,7 @@ struct RedDesc {
   int ldo, add;
   float scale;
 };
-#define PF_MAX_RED 4
+#define PF_MAX_RED 32
 void launch_reduce_multi(const RedDesc* d, int n, hipStream_t st);
 void launch_reduce_rows(const float* part, int nb, size_t plen, int ldp, int rows, int cols,
                         float* out, int ldo, int add, float scale, hipStream_t st);

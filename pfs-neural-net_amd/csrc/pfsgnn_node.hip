@@ -256,56 +256,160 @@ void launch_reduce_columns(const float* part, int G, int BPG, int NC, int C, flo
                      NC, C, out);
 }
 
+// ---------------------------------------------------------------- node inputs
+// A node-op input is up to PF_MAX_SEG row blocks of a virtual concatenation
+// (the torch.cat of gnn.py:100/136/153/188/191/220) -- never materialised.
+// Block s covers input rows [k0[s], k0[s+1]); its row k reads p[s] row
+// k - k0[s], either a [rows][N] node tensor or, when bc[s], a per-graph
+// [rows][N / npg] tensor whose column n / npg is broadcast to the npg nodes of
+// graph n / npg (the u[batch] gathers).  wcol[s] is the weight column of the
+// block's first row.  Unused blocks have k0 = INT_MAX.
+#define PF_MAX_SEG 4
+struct XSegs {
+  const float* p[PF_MAX_SEG];
+  int k0[PF_MAX_SEG + 1];
+  int wcol[PF_MAX_SEG];
+  int bc[PF_MAX_SEG];
+  int npg;
+};
+
+__device__ __forceinline__ int seg_of(const XSegs& S, int k) {
+  int s = 0;
+#pragma unroll
+  for (int i = 1; i < PF_MAX_SEG; ++i) s += k >= S.k0[i] ? 1 : 0;
+  return s;
+}
+
+// row k of the concatenation at node n (ng = n / npg)
+__device__ __forceinline__ float seg_load(const XSegs& S, int k, int n, int ng, int N, int Gc) {
+  const int s = seg_of(S, k);
+  const float* p = S.p[0];
+  int kb = S.k0[0], bc = S.bc[0];
+#pragma unroll
+  for (int i = 1; i < PF_MAX_SEG; ++i)
+    if (s == i) {
+      p = S.p[i];
+      kb = S.k0[i];
+      bc = S.bc[i];
+    }
+  return bc ? p[(size_t)(k - kb) * Gc + ng] : p[(size_t)(k - kb) * N + n];
+}
+
+__device__ __forceinline__ int seg_wcol(const XSegs& S, int k) {
+  const int s = seg_of(S, k);
+  int kb = S.k0[0], wc = S.wcol[0];
+#pragma unroll
+  for (int i = 1; i < PF_MAX_SEG; ++i)
+    if (s == i) {
+      kb = S.k0[i];
+      wc = S.wcol[i];
+    }
+  return wc + (k - kb);
+}
+
+static XSegs one_seg(const float* X, int wcol) {
+  XSegs S{};
+  S.p[0] = X;
+  S.k0[0] = 0;
+  S.wcol[0] = wcol;
+  for (int i = 1; i <= PF_MAX_SEG; ++i) S.k0[i] = INT_MAX;
+  S.npg = 0;
+  return S;
+}
+
+// Builds XSegs from the ABI's pfsgnn_seg list; returns the total row count or
+// -1 on a malformed list.
+static int make_segs(const pfsgnn_seg* segs, int nseg, int N, XSegs& S) {
+  if (!segs || nseg < 1 || nseg > PF_MAX_SEG) return -1;
+  S = XSegs{};
+  int k = 0, npg = 0;
+  for (int i = 0; i < nseg; ++i) {
+    if (!segs[i].x || segs[i].rows <= 0 || segs[i].col < 0 || segs[i].per_graph < 0) return -1;
+    if (segs[i].per_graph) {
+      if (N % segs[i].per_graph) return -1;
+      if (npg && npg != segs[i].per_graph) return -1;
+      npg = segs[i].per_graph;
+    }
+    S.p[i] = segs[i].x;
+    S.k0[i] = k;
+    S.wcol[i] = segs[i].col;
+    S.bc[i] = segs[i].per_graph ? 1 : 0;
+    k += segs[i].rows;
+  }
+  for (int i = nseg; i <= PF_MAX_SEG; ++i) S.k0[i] = INT_MAX;
+  S.npg = npg;
+  return k;
+}
+
 // ---------------------------------------------------------------- lin / lin_t
 // Y[Mo][N] (+)= op(W)[Mo][Ki] . act(X)[Ki][N] (+ bscale*b) (* lrelu'(Z)) on
 // v_mfma_f32_16x16x4_f32: a wave owns 16 node columns and every output row
 // (MT tiles of 16), the node column is the MFMA N index, the input channel
-// the K index.  op(W) is staged per block in LDS in K-chunks of 32 (rows =
-// output channel) -- W for lin, W^T for lin_t; the 8 X loads of a chunk are
-// issued together.
-#define GK 32
-template <int MT>
+// the K index.  Each lane first issues ALL its X loads (KSM >= ceil(Ki/4)
+// slots, held in registers), then the block stages the whole op(W) -- W for
+// lin, W^T for lin_t -- in LDS once ([MT*16][4*KSM+1], odd stride), so the X
+// latency overlaps the staging and the MFMA chain runs without a wait.
+template <int MT, int KSM>
 __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ W, int ldw, int trans,
-                                              int Mo, int Ki, const float* __restrict__ X, int N,
+                                              int Mo, int Ki, XSegs S, int N,
                                               const float* __restrict__ b, float bscale,
                                               int act_in, const float* __restrict__ Z,
                                               float* __restrict__ Y, int add) {
-  __shared__ float Ws[MT * 16][GK + 1];
+  extern __shared__ float Ws[];
+  // KSM K-steps of 4 always run (no per-step branch: the accumulators stay in
+  // AGPRs across the chain); rows Ki..4*KSM of op(W) and X are zero
+  constexpr int K4 = 4 * KSM, LDK = K4 + 1;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63, col = lane & 15, kq = lane >> 4;
   const int n = blockIdx.x * 64 + wave * 16 + col;
   const bool nv = n < N;
   const int nc = nv ? n : N - 1;
+  const int Gc = S.npg ? N / S.npg : 1, ng = S.npg ? nc / S.npg : 0;
+  float bv[KSM];
+#pragma unroll
+  for (int s = 0; s < KSM; ++s) {
+    const int kk = 4 * s + kq;
+    bv[s] = kk < Ki ? seg_load(S, kk, nc, ng, N, Gc) : 0.f;
+  }
+  // op(W) staging: 8 loads per thread in flight, then their LDS stores
+  const int MR = MT * 16, TOT = MR * K4;
+  for (int base = t; base < TOT; base += 8 * 256) {
+    float v[8];
+    int at[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int idx = base + u * 256;
+      int m, kk;
+      if (!trans) {
+        m = idx / K4;
+        kk = idx - m * K4;
+      } else {  // op(W) = W^T: walk W's rows so the reads stay contiguous
+        kk = idx / MR;
+        m = idx - kk * MR;
+      }
+      at[u] = idx < TOT ? m * LDK + kk : -1;
+      v[u] = 0.f;
+      if (idx < TOT && m < Mo && kk < Ki)
+        v[u] = trans ? W[(size_t)kk * ldw + m] : W[(size_t)m * ldw + seg_wcol(S, kk)];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (at[u] >= 0) Ws[at[u]] = v[u];
+  }
+  if (act_in) {
+#pragma unroll
+    for (int s = 0; s < KSM; ++s) bv[s] = lrelu(bv[s]);
+  }
+  __syncthreads();
   floatx4 acc[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int kc = 0; kc < Ki; kc += GK) {
-    const int kn = min(GK, Ki - kc);
-    __syncthreads();
-    for (int idx = t; idx < MT * 16 * GK; idx += 256) {
-      const int m = idx / GK, kk = idx - m * GK;
-      float v = 0.f;
-      if (m < Mo && kk < kn)
-        v = trans ? W[(size_t)(kc + kk) * ldw + m] : W[(size_t)m * ldw + kc + kk];
-      Ws[m][kk] = v;
-    }
-    __syncthreads();
-    float bv[GK / 4];
+  const float* wr = Ws + col * LDK + kq;
 #pragma unroll
-    for (int s = 0; s < GK / 4; ++s) {
-      const int kk = 4 * s + kq;
-      float v = 0.f;
-      if (kk < kn) v = X[(size_t)(kc + kk) * N + nc];
-      bv[s] = act_in ? lrelu(v) : v;
-    }
+  for (int s = 0; s < KSM; ++s) {
 #pragma unroll
-    for (int s = 0; s < GK / 4; ++s) {
-      if (4 * s < kn) {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ws[16 * mt + col][4 * s + kq], bv[s],
-                                                         acc[mt], 0, 0, 0);
-      }
-    }
+    for (int mt = 0; mt < MT; ++mt)
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[16 * mt * LDK + 4 * s], bv[s], acc[mt],
+                                                     0, 0, 0);
   }
   if (!nv) return;
 #pragma unroll
@@ -323,20 +427,63 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ W, int l
     }
 }
 
-static int launch_gemm(const float* W, int ldw, int trans, int Mo, int Ki, const float* X, int N,
+// K-step counts instantiated (Ki = 1..4, 9..12, 17..20, 29..32, 37..40, 97..100
+// and 157..160 run without padding steps: the encoders, F, 2F, 3F, 4F, 10F)
+#define PF_GEMM_KSM(X) X(1) X(3) X(5) X(8) X(10) X(16) X(25) X(40)
+static int gemm_ksm(int Ki) {
+  const int ks = (Ki + 3) / 4;
+  for (int v : {1, 3, 5, 8, 10, 16, 25, 40})
+    if (ks <= v) return v;
+  return -1;
+}
+
+template <int MT>
+static void gemm_attr() {
+#define PF_ATTR(KSM)                                                                       \
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm<MT, KSM>),               \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  PF_GEMM_KSM(PF_ATTR)
+#undef PF_ATTR
+}
+
+template <int MT>
+static void gemm_launch(int ksm, dim3 grid, size_t lds, hipStream_t st, const float* W, int ldw,
+                        int trans, int Mo, int Ki, const XSegs& S, int N, const float* b,
+                        float bscale, int act_in, const float* Z, float* Y, int add) {
+  switch (ksm) {
+#define PF_CASE(KSM)                                                                           \
+  case KSM:                                                                                    \
+    hipLaunchKernelGGL((k_gemm<MT, KSM>), grid, dim3(256), lds, st, W, ldw, trans, Mo, Ki, S, \
+                       N, b, bscale, act_in, Z, Y, add);                                       \
+    break;
+    PF_GEMM_KSM(PF_CASE)
+#undef PF_CASE
+  }
+}
+
+static int launch_gemm(const float* W, int ldw, int trans, int Mo, int Ki, const XSegs& S, int N,
                        const float* b, float bscale, int act_in, const float* Z, float* Y, int add,
                        hipStream_t st, const char* where) {
   const int MT = (Mo + 15) / 16;
-  dim3 grid((N + 63) / 64);
-#define PF_GEMM(T) \
-  case T: hipLaunchKernelGGL(k_gemm<T>, grid, dim3(256), 0, st, W, ldw, trans, Mo, Ki, X, N, b, \
-                             bscale, act_in, Z, Y, add); break;
-  switch (MT) {
-    PF_GEMM(1) PF_GEMM(2) PF_GEMM(3) PF_GEMM(4) PF_GEMM(5) PF_GEMM(6) PF_GEMM(7) PF_GEMM(8)
-    PF_GEMM(9) PF_GEMM(10) PF_GEMM(11)
-    default: return pf::fail(where, "output width > 176 not supported");
+  const int ksm = gemm_ksm(Ki);
+  if (ksm < 0) return pf::fail(where, "input width > 160 not supported");
+  if (MT > 11) return pf::fail(where, "output width > 176 not supported");
+  static bool attr_set = false;
+  if (!attr_set) {  // the widest op(W) (176 x 161) stages 113 KB of the CU's 160 KB LDS
+    gemm_attr<1>(); gemm_attr<2>(); gemm_attr<3>(); gemm_attr<4>(); gemm_attr<5>();
+    gemm_attr<6>(); gemm_attr<7>(); gemm_attr<8>(); gemm_attr<9>(); gemm_attr<10>();
+    gemm_attr<11>();
+    attr_set = true;
   }
-#undef PF_GEMM
+  const dim3 grid((N + 63) / 64);
+  const size_t lds = (size_t)MT * 16 * (4 * ksm + 1) * sizeof(float);
+  switch (MT) {
+#define PF_MT(T) \
+  case T: gemm_launch<T>(ksm, grid, lds, st, W, ldw, trans, Mo, Ki, S, N, b, bscale, act_in, Z, Y, add); break;
+    PF_MT(1) PF_MT(2) PF_MT(3) PF_MT(4) PF_MT(5) PF_MT(6) PF_MT(7) PF_MT(8) PF_MT(9) PF_MT(10)
+    PF_MT(11)
+#undef PF_MT
+  }
   return pf::check_launch(where);
 }
 
@@ -344,77 +491,160 @@ extern "C" int pfsgnn_lin(const float* W, int ldw, int M, int K, const float* X,
                           const float* b, float bscale, int act_in, float* Y, int add,
                           void* stream) {
   PF_REQUIRE(W && X && Y && M > 0 && K > 0 && N > 0, "pfsgnn_lin", "bad arguments");
-  return launch_gemm(W, ldw, 0, M, K, X, N, b, bscale, act_in, nullptr, Y, add,
+  return launch_gemm(W, ldw, 0, M, K, one_seg(X, 0), N, b, bscale, act_in, nullptr, Y, add,
                      as_stream(stream), "pfsgnn_lin");
+}
+
+extern "C" int pfsgnn_lin_cat(const float* W, int ldw, int M, const pfsgnn_seg* segs, int nseg,
+                              int N, const float* b, float bscale, int act_in, float* Y, int add,
+                              void* stream) {
+  PF_REQUIRE(W && Y && M > 0 && N > 0, "pfsgnn_lin_cat", "bad arguments");
+  XSegs S;
+  const int K = make_segs(segs, nseg, N, S);
+  PF_REQUIRE(K > 0, "pfsgnn_lin_cat", "bad segment list");
+  return launch_gemm(W, ldw, 0, M, K, S, N, b, bscale, act_in, nullptr, Y, add, as_stream(stream),
+                     "pfsgnn_lin_cat");
 }
 
 extern "C" int pfsgnn_lin_t(const float* W, int ldw, int M, int K, const float* dY, int N,
                             const float* Z, float* out, int add, void* stream) {
   PF_REQUIRE(W && dY && out && M > 0 && K > 0 && N > 0, "pfsgnn_lin_t", "bad arguments");
   // out[K][N] = W^T[K][M] . dY[M][N]
-  return launch_gemm(W, ldw, 1, K, M, dY, N, nullptr, 1.f, 0, Z, out, add, as_stream(stream),
-                     "pfsgnn_lin_t");
+  return launch_gemm(W, ldw, 1, K, M, one_seg(dY, 0), N, nullptr, 1.f, 0, Z, out, add,
+                     as_stream(stream), "pfsgnn_lin_t");
 }
 
 // ---------------------------------------------------------------- wgrad
-// dW[m][k] += sum_n dY[m][n] act(X[k][n]) and (optionally) db[m] += s*sum_n dY[m][n]
-// as one more column k = K of ones.  A block owns a node range; it stages 64
-// nodes at a time in LDS, transposed ([n][m], [n][k]: one coalesced read of
-// dY and X per block), and its 4 waves own output tiles wave, wave+4, ... of
-// the [M][K1] result, accumulated on v_mfma_f32_16x16x4_f32 with the node as
-// the K index.  Per-block partials + a fixed-order reduce (deterministic).
+// dW[m][col(k)] += sum_n dY[m][n] act(X[k][n]) and (optionally) db[m] +=
+// s*sum_n dY[m][n] as one more row k = K of ones.  A block owns a node range
+// and walks it in chunks of 64 nodes, staged ROW-major in LDS ([row][68]:
+// straight float4 copies of dY and X rows, no transpose).  The MFMA reduction
+// index is a permutation of the chunk's nodes -- step s of lane quad kq takes
+// node 16*kq + s for both operands -- so each lane reads its A and B values as
+// float4 runs (ds_read_b128; a 68-float row stride puts 16 rows on 64 distinct
+// banks).  The next chunk's global loads are issued before the current
+// chunk's MFMAs.  8 waves own output tiles wave, wave+8, ...; per-block
+// partials + a fixed-order reduce (deterministic).
 #define WG_WAVES 8
-// wave w owns output tiles w, w + 8, ... (TMAX slots) of the MT x KT grid
-template <int TMAX>
-__global__ __launch_bounds__(512) void k_wgrad(const float* __restrict__ dY, int M,
-                                               const float* __restrict__ X, int K, int K1,
-                                               int N, int act_in, int chunk,
+#define WG_LD 68
+// staged row kinds (per float4 item of a thread; fixed over the chunks)
+#define WG_DY 0
+#define WG_X 1
+#define WG_XBC 2
+#define WG_ONE 3
+#define WG_NONE 4
+template <int TMAX, int PER>
+__global__ __launch_bounds__(512) void k_wgrad(const float* __restrict__ dY, int M, XSegs S, int K,
+                                               int K1, int N, int act_in, int chunk, int vec,
                                                float* __restrict__ part) {
-  extern __shared__ float sm[];
-  const int LM = M | 1, LK = K1 | 1;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int MR = (M + 15) & ~15, KR = (K1 + 15) & ~15;
   float* Sd = sm;
-  float* Sx = sm + 64 * LM;
+  float* Sx = sm + MR * WG_LD;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63, col = lane & 15, kq = lane >> 4;
-  const int KT = (K1 + 15) / 16, NTILE = ((M + 15) / 16) * KT;
+  const int KT = KR / 16, NTILE = (MR / 16) * KT;
   const int n0 = blockIdx.x * chunk, n1 = min(N, n0 + chunk);
+  const int Gc = S.npg ? N / S.npg : 1;
   floatx4 acc[TMAX];
 #pragma unroll
   for (int j = 0; j < TMAX; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // padding rows (M..MR, K1..KR) are zero once; the chunk loop never writes them
+  for (int idx = t; idx < (MR - M) * WG_LD; idx += 64 * WG_WAVES) Sd[M * WG_LD + idx] = 0.f;
+  for (int idx = t; idx < (KR - K1) * WG_LD; idx += 64 * WG_WAVES) Sx[K1 * WG_LD + idx] = 0.f;
+  // item it = row (it >> 4: dY rows, then X rows, then the ones row) x float4 q
+  const int items = (M + K1) * 16;
+  const float* rp[PER];
+  int kind[PER];
+  float* lp[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int it = t + i * 64 * WG_WAVES, r = it >> 4, q = it & 15;
+    rp[i] = nullptr;
+    kind[i] = WG_NONE;
+    lp[i] = (r < M ? Sd + r * WG_LD : Sx + (r - M) * WG_LD) + 4 * q;
+    if (it >= items) continue;
+    if (r < M) {
+      rp[i] = dY + (size_t)r * N + 4 * q;
+      kind[i] = WG_DY;
+    } else if (r - M < K) {
+      const int k = r - M, s = seg_of(S, k);
+      const float* p = S.p[0];
+      int kb = S.k0[0], bc = S.bc[0];
+#pragma unroll
+      for (int u = 1; u < PF_MAX_SEG; ++u)
+        if (s == u) {
+          p = S.p[u];
+          kb = S.k0[u];
+          bc = S.bc[u];
+        }
+      rp[i] = bc ? p + (size_t)(k - kb) * Gc : p + (size_t)(k - kb) * N + 4 * q;
+      kind[i] = bc ? WG_XBC : WG_X;
+    } else {
+      kind[i] = WG_ONE;
+    }
+  }
+  auto fetch = [&](int c, int i) -> float4 {
+    const int q = (t + i * 64 * WG_WAVES) & 15;
+    const int nn = c + 4 * q;  // first node of the item
+    float4 v = {0.f, 0.f, 0.f, 0.f};
+    const int k = kind[i];
+    if (k == WG_DY || k == WG_X) {
+      const float* p = rp[i] + c;
+      if (vec && nn + 3 < n1) {
+        v = *reinterpret_cast<const float4*>(p);
+      } else {
+        v.x = nn < n1 ? p[0] : 0.f;
+        v.y = nn + 1 < n1 ? p[1] : 0.f;
+        v.z = nn + 2 < n1 ? p[2] : 0.f;
+        v.w = nn + 3 < n1 ? p[3] : 0.f;
+      }
+    } else if (k == WG_XBC) {
+      const float* p = rp[i];
+      v.x = nn < n1 ? p[nn / S.npg] : 0.f;
+      v.y = nn + 1 < n1 ? p[(nn + 1) / S.npg] : 0.f;
+      v.z = nn + 2 < n1 ? p[(nn + 2) / S.npg] : 0.f;
+      v.w = nn + 3 < n1 ? p[(nn + 3) / S.npg] : 0.f;
+    } else if (k == WG_ONE) {
+      v.x = nn < n1 ? 1.f : 0.f;
+      v.y = nn + 1 < n1 ? 1.f : 0.f;
+      v.z = nn + 2 < n1 ? 1.f : 0.f;
+      v.w = nn + 3 < n1 ? 1.f : 0.f;
+    }
+    if (act_in && (k == WG_X || k == WG_XBC)) {
+      v.x = lrelu(v.x); v.y = lrelu(v.y); v.z = lrelu(v.z); v.w = lrelu(v.w);
+    }
+    return v;
+  };
+  float4 buf[PER];
+  if (n0 < n1) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) buf[i] = fetch(n0, i);
+  }
   for (int c = n0; c < n1; c += 64) {
     __syncthreads();
-    for (int idx = t; idx < M * 64; idx += 64 * WG_WAVES) {
-      const int m = idx >> 6, nn = idx & 63;
-      Sd[nn * LM + m] = (c + nn < n1) ? dY[(size_t)m * N + c + nn] : 0.f;
-    }
-    for (int idx = t; idx < K1 * 64; idx += 64 * WG_WAVES) {
-      const int k = idx >> 6, nn = idx & 63;
-      float v = 0.f;
-      if (c + nn < n1) {
-        if (k < K) {
-          v = X[(size_t)k * N + c + nn];
-          if (act_in) v = lrelu(v);
-        } else {
-          v = 1.f;
-        }
-      }
-      Sx[nn * LK + k] = v;
-    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (kind[i] != WG_NONE) *reinterpret_cast<float4*>(lp[i]) = buf[i];
     __syncthreads();
+    if (c + 64 < n1) {  // next chunk's loads in flight during this chunk's MFMAs
+#pragma unroll
+      for (int i = 0; i < PER; ++i) buf[i] = fetch(c + 64, i);
+    }
 #pragma unroll
     for (int j = 0; j < TMAX; ++j) {
       const int tile = wave + WG_WAVES * j;
       if (tile < NTILE) {
         const int mt = tile / KT, kt = tile - mt * KT;
-        const int m = 16 * mt + col, k = 16 * kt + col;
-        const float* pa = Sd + (m < M ? m : 0);
-        const float* pb = Sx + (k < K1 ? k : 0);
-        const bool ma = m < M, mb = k < K1;
-#pragma unroll 4
-        for (int st = 0; st < 16; ++st) {
-          const int q = 4 * st + kq;
-          const float av = ma ? pa[q * LM] : 0.f;
-          const float bv = mb ? pb[q * LK] : 0.f;
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j], 0, 0, 0);
+        const float* pa = Sd + (16 * mt + col) * WG_LD + 16 * kq;
+        const float* pb = Sx + (16 * kt + col) * WG_LD + 16 * kq;
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const float4 a = *reinterpret_cast<const float4*>(pa + 4 * q4);
+          const float4 bq = *reinterpret_cast<const float4*>(pb + 4 * q4);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bq.x, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bq.y, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bq.z, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bq.w, acc[j], 0, 0, 0);
         }
       }
     }
@@ -439,50 +669,169 @@ static int wgrad_blocks(int N) {
   return std::max(1, std::min(s, 256));   // <= 2*RED_SEG: one reduce launch
 }
 
+static size_t wgrad_part_bytes(int M, int K1, int N) {
+  return (size_t)wgrad_blocks(N) * M * K1 * sizeof(float);
+}
+
+// Launches the per-block partials of dW (and db) into ws and describes the
+// reduction that finishes them (rd[0..*nr)); the caller launches it now or
+// batches it with others (pfsgnn_reduce_batch).
+static int wgrad_launch(const float* dY, int M, const XSegs& S, int nseg, int K, int N, int act_in,
+                        float* dW, int lddw, float* db, float dbscale, void* ws, size_t ws_bytes,
+                        hipStream_t st, const char* where, RedDesc* rd, int* nr_out) {
+  PF_REQUIRE(M <= 256 && K <= 256, where, "M, K too large");
+  const int nbk = wgrad_blocks(N);
+  const int K1 = K + (db ? 1 : 0);
+  const size_t need = wgrad_part_bytes(M, K1, N);
+  PF_REQUIRE(ws && ws_bytes >= need, where, "workspace too small");
+  const int chunk = ((N + nbk - 1) / nbk + 63) / 64 * 64;
+  const int nblk = (N + chunk - 1) / chunk;
+  float* part = reinterpret_cast<float*>(ws);
+  const int MR = (M + 15) & ~15, KR = (K1 + 15) & ~15;
+  const size_t lds = (size_t)(MR + KR) * WG_LD * sizeof(float);
+  const int ntile = (MR / 16) * (KR / 16);
+  // float4 staging when every row starts 16-byte aligned
+  bool vec = (N % 4 == 0) && ((uintptr_t)dY % 16 == 0);
+  for (int i = 0; i < nseg; ++i)
+    if (!S.bc[i] && (uintptr_t)S.p[i] % 16 != 0) vec = false;
+  const int items = (M + K1) * 16;
+  const int per = items <= 512 ? 1 : items <= 1024 ? 2 : items <= 2048 ? 4 : items <= 4096 ? 8 : 16;
+  PF_REQUIRE(items <= 16 * 64 * WG_WAVES, where, "M + K too large");
+  const int tm = ntile <= WG_WAVES ? 1 : ntile <= 2 * WG_WAVES ? 2 : ntile <= 4 * WG_WAVES ? 4
+               : ntile <= 8 * WG_WAVES ? 8 : ntile <= 16 * WG_WAVES ? 16 : -1;
+  PF_REQUIRE(tm > 0, where, "too many output tiles");
+  const dim3 grid(nblk), blk(64 * WG_WAVES);
+  bool launched = false;
+#define PF_WG(T, P)                                                                            \
+  {                                                                                            \
+    auto fn = &k_wgrad<T, P>;                                                                  \
+    static bool attr = false;                                                                  \
+    if (!attr) {                                                                               \
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn),                               \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=       \
+          hipSuccess)                                                                          \
+        return pf::fail(where, "hipFuncSetAttribute");                                         \
+      attr = true;                                                                             \
+    }                                                                                          \
+    if (tm == T && per == P) {                                                                 \
+      hipLaunchKernelGGL(fn, grid, blk, lds, st, dY, M, S, K, K1, N, act_in, chunk, (int)vec,  \
+                         part);                                                                \
+      launched = true;                                                                         \
+    }                                                                                          \
+  }
+#define PF_WG_P(T) PF_WG(T, 1) PF_WG(T, 2) PF_WG(T, 4) PF_WG(T, 8)
+  PF_WG_P(1) PF_WG_P(2) PF_WG_P(4) PF_WG_P(8) PF_WG_P(16) PF_WG(16, 16)
+#undef PF_WG_P
+#undef PF_WG
+  if (!launched) return pf::fail(where, "no kernel for this shape");
+  // the reduction: each input block's dW columns, plus db
+  int nr = 0;
+  for (int i = 0; i < nseg; ++i) {
+    const int k0 = S.k0[i], k1 = (i + 1 < nseg) ? S.k0[i + 1] : K;
+    rd[nr++] = {part + k0, nblk, (size_t)M * K1, K1, M, k1 - k0, dW + S.wcol[i], lddw, 1, 1.f};
+  }
+  if (db) rd[nr++] = {part + K, nblk, (size_t)M * K1, K1, M, 1, db, 1, 1, dbscale};
+  *nr_out = nr;
+  return pf::check_launch(where);
+}
+
+static int wgrad_impl(const float* dY, int M, const XSegs& S, int nseg, int K, int N, int act_in,
+                      float* dW, int lddw, float* db, float dbscale, void* ws, size_t ws_bytes,
+                      hipStream_t st, const char* where) {
+  RedDesc rd[PF_MAX_SEG + 1];
+  int nr = 0;
+  const int rc = wgrad_launch(dY, M, S, nseg, K, N, act_in, dW, lddw, db, dbscale, ws, ws_bytes,
+                              st, where, rd, &nr);
+  if (rc) return rc;
+  launch_reduce_multi(rd, nr, st);
+  return pf::check_launch(where);
+}
+
 extern "C" int pfsgnn_wgrad(const float* dY, int M, const float* X, int K, int N, int act_in,
                             float* dW, int lddw, float* db, float dbscale, void* ws,
                             size_t ws_bytes, void* stream) {
   PF_REQUIRE(dY && X && dW && M > 0 && K > 0 && N > 0, "pfsgnn_wgrad", "bad arguments");
-  PF_REQUIRE(M <= 256 && K <= 256, "pfsgnn_wgrad", "M, K too large");
+  return wgrad_impl(dY, M, one_seg(X, 0), 1, K, N, act_in, dW, lddw, db, dbscale, ws, ws_bytes,
+                    as_stream(stream), "pfsgnn_wgrad");
+}
+
+extern "C" int pfsgnn_wgrad_cat(const float* dY, int M, const pfsgnn_seg* segs, int nseg, int N,
+                                int act_in, float* dW, int lddw, float* db, float dbscale,
+                                void* ws, size_t ws_bytes, void* stream) {
+  PF_REQUIRE(dY && dW && M > 0 && N > 0, "pfsgnn_wgrad_cat", "bad arguments");
+  XSegs S;
+  const int K = make_segs(segs, nseg, N, S);
+  PF_REQUIRE(K > 0, "pfsgnn_wgrad_cat", "bad segment list");
+  return wgrad_impl(dY, M, S, nseg, K, N, act_in, dW, lddw, db, dbscale, ws, ws_bytes,
+                    as_stream(stream), "pfsgnn_wgrad_cat");
+}
+
+extern "C" size_t pfsgnn_wgrad_part_bytes(int M, int K, int N, int has_db) {
+  if (M <= 0 || K <= 0 || N <= 0) return 0;
+  return wgrad_part_bytes(M, K + (has_db ? 1 : 0), N);
+}
+
+extern "C" int pfsgnn_wgrad_cat_part(const float* dY, int M, const pfsgnn_seg* segs, int nseg,
+                                     int N, int act_in, float* dW, int lddw, float* db,
+                                     float dbscale, void* part, size_t part_bytes,
+                                     pfsgnn_red* red_out, int* nred_out, void* stream) {
+  PF_REQUIRE(dY && dW && M > 0 && N > 0 && red_out && nred_out, "pfsgnn_wgrad_cat_part",
+             "bad arguments");
+  XSegs S;
+  const int K = make_segs(segs, nseg, N, S);
+  PF_REQUIRE(K > 0, "pfsgnn_wgrad_cat_part", "bad segment list");
+  RedDesc rd[PF_MAX_SEG + 1];
+  int nr = 0;
+  const int rc = wgrad_launch(dY, M, S, nseg, K, N, act_in, dW, lddw, db, dbscale, part,
+                              part_bytes, as_stream(stream), "pfsgnn_wgrad_cat_part", rd, &nr);
+  if (rc) return rc;
+  for (int i = 0; i < nr; ++i)
+    red_out[i] = {rd[i].part, rd[i].nb, rd[i].plen, rd[i].ldp, rd[i].rows, rd[i].cols, rd[i].out,
+                  rd[i].ldo, rd[i].add, rd[i].scale};
+  *nred_out = nr;
+  return 0;
+}
+
+// Output rectangles of two reductions intersect?  Exact when both write rows
+// of the same row pitch without wrapping; conservative (true) otherwise.
+static bool red_overlap(const RedDesc& a, const RedDesc& b) {
+  const intptr_t ea = ((intptr_t)(a.rows - 1) * a.ldo + a.cols) * 4;
+  const intptr_t eb = ((intptr_t)(b.rows - 1) * b.ldo + b.cols) * 4;
+  const intptr_t pa = (intptr_t)a.out, pb = (intptr_t)b.out;
+  if (pa + ea <= pb || pb + eb <= pa) return false;  // disjoint address ranges
+  if (a.ldo != b.ldo || (pb - pa) % 4) return true;
+  const intptr_t d = (pb - pa) / 4;  // b's origin relative to a's, in floats
+  const intptr_t ld = a.ldo;
+  intptr_t dr = d / ld, dc = d % ld;
+  if (dc < 0) {
+    dc += ld;
+    dr -= 1;
+  }
+  if (a.cols > ld || dc + b.cols > ld) return true;
+  const bool rows_meet = dr < a.rows && dr + b.rows > 0;
+  const bool cols_meet = dc < a.cols && dc + b.cols > 0;
+  return rows_meet && cols_meet;
+}
+
+extern "C" int pfsgnn_reduce_batch(const pfsgnn_red* reds, int n, void* stream) {
+  PF_REQUIRE(n >= 0 && (reds || n == 0), "pfsgnn_reduce_batch", "bad arguments");
   hipStream_t st = as_stream(stream);
-  const int nbk = wgrad_blocks(N);
-  const int K1 = K + (db ? 1 : 0);
-  const size_t need = (size_t)nbk * M * K1 * sizeof(float);
-  PF_REQUIRE(ws && ws_bytes >= need, "pfsgnn_wgrad", "workspace too small");
-  const int chunk = ((N + nbk - 1) / nbk + 63) / 64 * 64;
-  const int nblk = (N + chunk - 1) / chunk;
-  float* part = reinterpret_cast<float*>(ws);
-  const size_t lds = (size_t)64 * ((M | 1) + (K1 | 1)) * sizeof(float);
-  const int ntile = ((M + 15) / 16) * ((K1 + 15) / 16);
-  static bool attr_set = false;
-  if (!attr_set) {  // Fdim 16 stages up to ~83 KB of the CU's 160 KB LDS
-    const void* fns[4] = {reinterpret_cast<const void*>(&k_wgrad<1>),
-                          reinterpret_cast<const void*>(&k_wgrad<2>),
-                          reinterpret_cast<const void*>(&k_wgrad<8>),
-                          reinterpret_cast<const void*>(&k_wgrad<16>)};
-    for (const void* f : fns)
-      if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
-          hipSuccess)
-        return pf::fail("pfsgnn_wgrad", "hipFuncSetAttribute");
-    attr_set = true;
+  std::vector<RedDesc> group;
+  for (int i = 0; i < n; ++i) {
+    const pfsgnn_red& r = reds[i];
+    PF_REQUIRE(r.part && r.out && r.nb > 0 && r.rows > 0 && r.cols > 0, "pfsgnn_reduce_batch",
+               "bad reduction");
+    const RedDesc d{r.part, r.nb, r.plen, r.ldp, r.rows, r.cols, r.out, r.ldo, r.add, r.scale};
+    bool clash = (int)group.size() == PF_MAX_RED;
+    for (const RedDesc& g : group) clash = clash || red_overlap(g, d);
+    if (clash) {  // a launch never holds two reductions into the same cells
+      launch_reduce_multi(group.data(), (int)group.size(), st);
+      group.clear();
+    }
+    group.push_back(d);
   }
-  const dim3 grid(nblk), blk(64 * WG_WAVES);
-  if (ntile <= WG_WAVES)
-    hipLaunchKernelGGL(k_wgrad<1>, grid, blk, lds, st, dY, M, X, K, K1, N, act_in, chunk, part);
-  else if (ntile <= 2 * WG_WAVES)
-    hipLaunchKernelGGL(k_wgrad<2>, grid, blk, lds, st, dY, M, X, K, K1, N, act_in, chunk, part);
-  else if (ntile <= 8 * WG_WAVES)
-    hipLaunchKernelGGL(k_wgrad<8>, grid, blk, lds, st, dY, M, X, K, K1, N, act_in, chunk, part);
-  else if (ntile <= 16 * WG_WAVES)
-    hipLaunchKernelGGL(k_wgrad<16>, grid, blk, lds, st, dY, M, X, K, K1, N, act_in, chunk, part);
-  else
-    return pf::fail("pfsgnn_wgrad", "too many output tiles");
-  {
-    RedDesc rd[2] = {{part, nblk, (size_t)M * K1, K1, M, K, dW, lddw, 1, 1.f},
-                     {part + K, nblk, (size_t)M * K1, K1, M, 1, db, 1, 1, dbscale}};
-    launch_reduce_multi(rd, db ? 2 : 1, st);
-  }
-  return pf::check_launch("pfsgnn_wgrad");
+  if (!group.empty()) launch_reduce_multi(group.data(), (int)group.size(), st);
+  return pf::check_launch("pfsgnn_reduce_batch");
 }
 
 // ---------------------------------------------------------------- batchnorm

@@ -75,6 +75,14 @@ def param_names(B, normed=True):
     return names
 
 
+def _seg_n(segs):
+    """Node count of a row-block list: the width of its first per-node block."""
+    for X, _, bc in segs:
+        if not bc:
+            return X.shape[1]
+    raise ValueError("a concatenated input needs at least one per-node block")
+
+
 class Engine:
     def __init__(self, backend, F, B=0, Fs=1, Ft=1, T=1, normed=True, bn_eps=1e-5,
                  bn_momentum=0.1, rms_eps=None):
@@ -87,10 +95,16 @@ class Engine:
 
     # ================================================================= MLP
     def mlp_fwd(self, P, pre, X):
-        """MLP (gnn.py:65): Linear -> LeakyReLU(0.1) -> Linear on [K, N]."""
+        """MLP (gnn.py:65): Linear -> LeakyReLU(0.1) -> Linear on [K, N].  X is a
+        tensor or, for the concatenated inputs of gnn.py:153/191/220, a list of
+        row blocks ``(tensor, weight column, per_graph)`` read in place (a
+        per_graph block is [rows, G], broadcast over each graph's nodes)."""
         be = self.be
         W1, b1, W2, b2 = P[pre + "0.weight"], P[pre + "0.bias"], P[pre + "2.weight"], P[pre + "2.bias"]
-        Z = be.lin(W1, 0, W1.shape[1], X, b=b1)
+        if isinstance(X, list):
+            Z = be.lin_cat(W1, X, _seg_n(X), b=b1)
+        else:
+            Z = be.lin(W1, 0, W1.shape[1], X, b=b1)
         Y = be.lin(W2, 0, W2.shape[1], Z, b=b2, act_in=True)
         return Y, (X, Z)
 
@@ -100,7 +114,10 @@ class Engine:
         W1, W2 = P[pre + "0.weight"], P[pre + "2.weight"]
         be.wgrad(dY, Z, Gr[pre + "2.weight"], db=Gr[pre + "2.bias"], act_in=True)
         dZ = be.lin_t(W2, 0, W2.shape[1], dY, z=Z)
-        be.wgrad(dZ, X, Gr[pre + "0.weight"], db=Gr[pre + "0.bias"])
+        if isinstance(X, list):
+            be.wgrad_cat(dZ, X, Gr[pre + "0.weight"], db=Gr[pre + "0.bias"])
+        else:
+            be.wgrad(dZ, X, Gr[pre + "0.weight"], db=Gr[pre + "0.bias"])
         return be.lin_t(W1, 0, W1.shape[1], dZ) if want_dx else None
 
     def _bn(self, P, BN, key, X):
@@ -128,8 +145,7 @@ class Engine:
         W1, b1 = P[pre + "0.weight"], P[pre + "0.bias"]
         W2, b2 = P[pre + "2.weight"], P[pre + "2.bias"]
         Ps = be.lin(W1, 0, F, xs)
-        Pt = be.lin(W1, F, F, xt, b=b1)
-        be.graph_bcast_add(Pt, be.lin(W1, 3 * F, F, u))
+        Pt = be.lin_cat(W1, [(xt, F, False), (u, 3 * F, True)], d.NT, b=b1)
         y, mu1, var1 = be.edge_mlp_fwd(d, xe3[0], xe3[1], xe3[2], Ps, Pt, W1, W2, b2)
         if self.normed:
             key = pre + "norm."
@@ -159,10 +175,11 @@ class Engine:
                                            Gr[pre + "2.bias"], want_gxe=want_gxe)
         be.wgrad(GzEs, st["xs"], dW1, col0=0)
         be.lin_t(W1, 0, F, GzEs, out=g_xs, add=True)
-        be.wgrad(GzEt, st["xt"], dW1, col0=F, db=Gr[pre + "0.bias"])
+        # x_t[tgt] and u[batch] columns in one pass (u's gradient sums over classes)
+        be.wgrad_cat(GzEt, [(st["xt"], F, False), (st["u"], 3 * F, True)], dW1,
+                     db=Gr[pre + "0.bias"])
         be.lin_t(W1, F, F, GzEt, out=g_xt, add=True)
         GzEu = be.graph_reduce(GzEt, G)
-        be.wgrad(GzEu, st["u"], dW1, col0=3 * F)
         be.lin_t(W1, 3 * F, F, GzEu, out=g_u, add=True)
         return g_xe
 
@@ -172,11 +189,10 @@ class Engine:
         Ws1, bs1 = P[pre + "node_mlp_1.0.weight"], P[pre + "node_mlp_1.0.bias"]
         Ws2, bs2 = P[pre + "node_mlp_1.2.weight"], P[pre + "node_mlp_1.2.bias"]
         Qt = be.lin(Ws1, 0, F, xt, b=bs1)
-        hS = be.empty(10 * F, d.NS)
-        hS[0:F].copy_(xs)
-        mom = be.source_fwd(d, xe3[0], xe3[1], xe3[2], Qt, Ws1, Ws2, bs2, hS[F:9 * F])
-        hS[9 * F:10 * F].zero_()
-        be.graph_bcast_add(hS[9 * F:10 * F], u)
+        hmom = be.empty(8 * F, d.NS)
+        mom = be.source_fwd(d, xe3[0], xe3[1], xe3[2], Qt, Ws1, Ws2, bs2, hmom)
+        # node_mlp_2 input [x, mean, std, skew, kurt, u[batch]] (gnn.py:153), in place
+        hS = [(xs, 0, False), (hmom, F, False), (u, 9 * F, True)]
         ys, sS = self.mlp_fwd(P, pre + "node_mlp_2.", hS)
         xs_new, bnS = self._bn(P, BN, pre + "norm.", ys)
         return dict(xs=xs, xt=xt, xe3=xe3, u=u, Qt=Qt, mom=mom, sS=sS, bnS=bnS, xs_new=xs_new)
@@ -210,11 +226,9 @@ class Engine:
         Wt2, bt2 = P[pre + "node_mlp_1.2.weight"], P[pre + "node_mlp_1.2.bias"]
         Rs = be.lin(Wt1, 0, F, xs, b=bt1)
         hsum = be.target_fwd(d, xe3[0], xe3[1], xe3[2], Rs, Wt1)
-        hT = be.empty(4 * F, d.NT)
-        hT[0:F].copy_(xt)
-        be.lin(Wt2, 0, 2 * F, hsum, b=bt2, bscale=float(d.NF), out=hT[F:3 * F])
-        hT[3 * F:4 * F].zero_()
-        be.graph_bcast_add(hT[3 * F:4 * F], u)
+        agg = be.lin(Wt2, 0, 2 * F, hsum, b=bt2, bscale=float(d.NF))
+        # node_mlp_2 input [x, agg, u[batch]] (gnn.py:191), in place
+        hT = [(xt, 0, False), (agg, F, False), (u, 3 * F, True)]
         yt, sT = self.mlp_fwd(P, pre + "node_mlp_2.", hT)
         xt_new, bnT = self._bn(P, BN, pre + "norm.", yt)
         return dict(xs=xs, xt=xt, xe3=xe3, u=u, Rs=Rs, hsum=hsum, sT=sT, bnT=bnT, xt_new=xt_new)
@@ -245,10 +259,9 @@ class Engine:
     # --- GlobalModel (gnn.py:208-223; its RMSNorm also runs twice)
     def global_fwd(self, P, d, pre, xs, xt, u):
         be, F, G = self.be, self.F, d.G
-        hU = be.empty(3 * F, G)
-        hU[0:F].copy_(u)
-        hU[F:2 * F].copy_(be.graph_reduce(xs, G, mean=True))
-        hU[2 * F:3 * F].copy_(be.graph_reduce(xt, G, mean=True))
+        # [u, mean x_s, mean x_t] (gnn.py:218-220), in place
+        hU = [(u, 0, False), (be.graph_reduce(xs, G, mean=True), F, False),
+              (be.graph_reduce(xt, G, mean=True), 2 * F, False)]
         v, sU = self.mlp_fwd(P, pre, hU)
         if self.normed:
             u_new, rms = be.rms2_fwd(v, P[pre + "norm.weight"], self._rms_eps(v))
@@ -297,11 +310,24 @@ class Engine:
         """Accumulates parameter gradients into ``Gr`` (same keys as ``P``).
         g_xe_out is [F, E] canonical, w.r.t. the final edge features."""
         d, be, F = ctx["d"], self.be, self.F
+        # node weight-gradient reductions are batched over the pass (flushed below)
+        be.defer_begin()
+        try:
+            self._backward(P, Gr, ctx, d, g_xs_out, g_xt_out, g_xe_out, g_u_out)
+        finally:
+            be.defer_flush()
+
+    def _backward(self, P, Gr, ctx, d, g_xs_out, g_xt_out, g_xe_out, g_u_out):
+        be, F = self.be, self.F
         g_xs, g_xt, g_xe, g_u = g_xs_out, g_xt_out, g_xe_out, g_u_out
         for b in reversed(range(self.B)):
             se, ss, stt, su = ctx["blocks"][b]
             p = f"mpb.{b}."
-            g_xs_in, g_xt_in, g_u_in = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
+            # the three input-gradient accumulators share one zeroed buffer (one fill)
+            acc = be.zeros(F * (d.NS + d.NT + d.G))
+            g_xs_in = acc[:F * d.NS].view(F, d.NS)
+            g_xt_in = acc[F * d.NS:F * (d.NS + d.NT)].view(F, d.NT)
+            g_u_in = acc[F * (d.NS + d.NT):].view(F, d.G)
             # gradients that are None are exactly zero: the models whose outputs
             # feed nothing downstream (the last block's S/T/Global under the
             # train.py objective) contribute nothing and are skipped
@@ -309,8 +335,11 @@ class Engine:
             live_s = live_t or g_xs is not None
             bnstat = (se["mu1"], se["inv1"]) if self.normed else None
             if live_s:
-                g_xs_new = be.zeros(F, d.NS) if g_xs is None else g_xs.clone()
-                g_xt_new = be.zeros(F, d.NT) if g_xt is None else g_xt.clone()
+                # below the last block g_xs / g_xt are this loop's own accumulators
+                # and are updated in place; the caller's gradients are copied
+                own = b < self.B - 1
+                g_xs_new = be.zeros(F, d.NS) if g_xs is None else (g_xs if own else g_xs.clone())
+                g_xt_new = be.zeros(F, d.NT) if g_xt is None else (g_xt if own else g_xt.clone())
                 if g_u is not None:
                     self.global_bwd(P, Gr, d, p + "global_model.", su, g_u, g_xs_new, g_xt_new,
                                     g_u_in)

@@ -29,6 +29,26 @@ FL = ctypes.c_float
 SZ = ctypes.c_size_t
 ULL = ctypes.c_ulonglong
 
+
+class Seg(ctypes.Structure):
+    """pfsgnn_seg (include/pfsgnn.h): one row block of a concatenated node input."""
+    _fields_ = [("x", ctypes.c_void_p), ("rows", ctypes.c_int), ("col", ctypes.c_int),
+                ("per_graph", ctypes.c_int)]
+
+
+SEGP = ctypes.POINTER(Seg)
+
+
+class Red(ctypes.Structure):
+    """pfsgnn_red (include/pfsgnn.h): one pending cross-block reduction."""
+    _fields_ = [("part", ctypes.c_void_p), ("nb", ctypes.c_int), ("plen", ctypes.c_size_t),
+                ("ldp", ctypes.c_int), ("rows", ctypes.c_int), ("cols", ctypes.c_int),
+                ("out", ctypes.c_void_p), ("ldo", ctypes.c_int), ("add", ctypes.c_int),
+                ("scale", ctypes.c_float)]
+
+
+REDP = ctypes.POINTER(Red)
+
 _SIGS = {
     "pfsgnn_version": ([], ctypes.c_char_p),
     "pfsgnn_last_error": ([], ctypes.c_char_p),
@@ -42,6 +62,12 @@ _SIGS = {
     "pfsgnn_lin": ([P, I, I, I, P, I, P, FL, I, P, I, P], I),
     "pfsgnn_lin_t": ([P, I, I, I, P, I, P, P, I, P], I),
     "pfsgnn_wgrad": ([P, I, P, I, I, I, P, I, P, FL, P, SZ, P], I),
+    "pfsgnn_lin_cat": ([P, I, I, SEGP, I, I, P, FL, I, P, I, P], I),
+    "pfsgnn_wgrad_cat": ([P, I, SEGP, I, I, I, P, I, P, FL, P, SZ, P], I),
+    "pfsgnn_wgrad_part_bytes": ([I, I, I, I], SZ),
+    "pfsgnn_wgrad_cat_part": ([P, I, SEGP, I, I, I, P, I, P, FL, P, SZ, REDP,
+                               ctypes.POINTER(ctypes.c_int), P], I),
+    "pfsgnn_reduce_batch": ([REDP, I, P], I),
     "pfsgnn_bn_fwd": ([P, I, I, P, P, P, P, FL, FL, P, P, P, P, SZ, P], I),
     "pfsgnn_bn_bwd": ([P, P, P, P, P, FL, I, I, P, P, P, P, SZ, P], I),
     "pfsgnn_graph_reduce": ([P, I, I, I, I, P, P], I),
@@ -217,13 +243,101 @@ class HipBackend:
               out.data_ptr(), int(add), _stream())
         return out
 
+    # ----------------------------------------------- deferred weight gradients
+    # Between defer_begin() and defer_flush(), wgrad/wgrad_cat only launch their
+    # per-block partials (into a private arena) and queue the reductions; the
+    # flush finishes them all in a few launches (pfsgnn_reduce_batch).  The
+    # engine defers over a backward pass: its weight gradients are read only by
+    # the optimizer.
+    def defer_begin(self):
+        self._defer = []
+        self._arena_off = 0
+
+    def defer_flush(self):
+        reds, self._defer = getattr(self, "_defer", None), None
+        if not reds:
+            return
+        arr = (Red * len(reds))(*reds)
+        _call("pfsgnn_reduce_batch", arr, len(reds), _stream())
+
+    def _arena_take(self, nbytes):
+        nbytes = (int(nbytes) + 255) & ~255
+        arena = getattr(self, "_arena", None)
+        if arena is None or self._arena_off + nbytes > arena.numel():
+            # grow: finish what the old arena holds first (warm-up steps size it
+            # before any graph capture)
+            pending = self._defer
+            if pending:
+                self._defer = pending
+                self.defer_flush()
+                self._defer = []
+            size = max(2 * (arena.numel() if arena is not None else 0), 64 << 20,
+                       2 * nbytes)
+            self._arena = torch.empty(size, dtype=torch.uint8, device=self.device)
+            self._arena_off = 0
+        off = self._arena_off
+        self._arena_off += nbytes
+        return self._arena.data_ptr() + off, nbytes
+
+    def _wgrad_deferred(self, dY, arr, nseg, N, act_in, dW, db, dbscale):
+        M = dY.shape[0]
+        K = sum(arr[i].rows for i in range(nseg))
+        part, nbytes = self._arena_take(lib().pfsgnn_wgrad_part_bytes(M, K, N, int(db is not None)))
+        reds = (Red * 5)()
+        nr = ctypes.c_int(0)
+        _call("pfsgnn_wgrad_cat_part", dY.data_ptr(), M, arr, nseg, N, int(act_in), dW.data_ptr(),
+              dW.shape[1], _ptr(db), float(dbscale), part, nbytes, reds, ctypes.byref(nr),
+              _stream())
+        self._defer.extend(reds[i] for i in range(nr.value))
+
     def wgrad(self, dY, X, dW, col0=0, db=None, act_in=False, dbscale=1.0):
         M, N = dY.shape
         K = X.shape[0]
         self._chk(dY, X, dW, db)
+        if getattr(self, "_defer", None) is not None:
+            self._wgrad_deferred(dY, self._segs([(X, col0, False)], N), 1, N, act_in, dW, db,
+                                 dbscale)
+            return
         ws, wsb = self._wsargs(getattr(self, "_dims", None))
         _call("pfsgnn_wgrad", dY.data_ptr(), M, X.data_ptr(), K, N, int(act_in),
               dW.data_ptr() + 4 * col0, dW.shape[1], _ptr(db), float(dbscale), ws, wsb, _stream())
+
+    def _segs(self, segs, N):
+        """[(X, col, per_graph)] -> ctypes pfsgnn_seg array; per_graph segments
+        are [rows, G] tensors broadcast over the N // G nodes of each graph."""
+        arr = (Seg * len(segs))()
+        for i, (X, col, bc) in enumerate(segs):
+            self._chk(X)
+            assert (N % X.shape[1] == 0) if bc else (X.shape[1] == N), (X.shape, N, bc)
+            arr[i].x = X.data_ptr()
+            arr[i].rows = X.shape[0]
+            arr[i].col = int(col)
+            arr[i].per_graph = N // X.shape[1] if bc else 0
+        return arr
+
+    def lin_cat(self, W, segs, N, b=None, act_in=False, out=None, add=False, bscale=1.0):
+        """Y (+)= sum_s W[:, col_s:col_s+rows_s] @ act(X_s[, broadcast per graph]) + bscale*b."""
+        M, ldw = W.shape
+        if out is None:
+            out = self.empty(M, N)
+            add = False
+        self._chk(W, b, out)
+        arr = self._segs(segs, N)
+        _call("pfsgnn_lin_cat", W.data_ptr(), ldw, M, arr, len(segs), N, _ptr(b), float(bscale),
+              int(act_in), out.data_ptr(), int(add), _stream())
+        return out
+
+    def wgrad_cat(self, dY, segs, dW, db=None, act_in=False, dbscale=1.0):
+        """dW[:, col_s:col_s+rows_s] += dY @ act(X_s)^T; db += dbscale * dY.sum(1)."""
+        M, N = dY.shape
+        self._chk(dY, dW, db)
+        arr = self._segs(segs, N)
+        if getattr(self, "_defer", None) is not None:
+            self._wgrad_deferred(dY, arr, len(segs), N, act_in, dW, db, dbscale)
+            return
+        ws, wsb = self._wsargs(getattr(self, "_dims", None))
+        _call("pfsgnn_wgrad_cat", dY.data_ptr(), M, arr, len(segs), N, int(act_in), dW.data_ptr(),
+              dW.shape[1], _ptr(db), float(dbscale), ws, wsb, _stream())
 
     def bn_fwd(self, X, gamma, beta, rm, rv, momentum, eps):
         C, N = X.shape

@@ -114,6 +114,39 @@ class EmuBackend:
         if db is not None:
             db += dbscale * dY.sum(1)
 
+    def defer_begin(self):  # weight-gradient batching is a no-op here
+        pass
+
+    def defer_flush(self):
+        pass
+
+    @staticmethod
+    def _expand(X, bc, N):
+        return X.repeat_interleave(N // X.shape[1], dim=1) if bc else X
+
+    def lin_cat(self, W, segs, N, b=None, act_in=False, out=None, add=False, bscale=1.0):
+        Y = 0
+        for X, col, bc in segs:
+            Xa = self._expand(lrelu(X) if act_in else X, bc, N)
+            Y = Y + W[:, col:col + X.shape[0]] @ Xa
+        if b is not None:
+            Y = Y + bscale * b[:, None]
+        if out is None:
+            return Y
+        if add:
+            out += Y
+        else:
+            out.copy_(Y)
+        return out
+
+    def wgrad_cat(self, dY, segs, dW, db=None, act_in=False, dbscale=1.0):
+        N = dY.shape[1]
+        for X, col, bc in segs:
+            Xa = self._expand(lrelu(X) if act_in else X, bc, N)
+            dW[:, col:col + X.shape[0]] += dY @ Xa.t()
+        if db is not None:
+            db += dbscale * dY.sum(1)
+
     def bn_fwd(self, X, gamma, beta, rm, rv, momentum, eps):
         n = X.shape[1]
         mu = X.mean(1)

@@ -140,7 +140,38 @@ def test_edge_ops(hb, prec, G, NF, NC, F):
         close(a, b, rtol=5e-4, name=nm)
 
 
-@pytest.mark.parametrize("G,NF,NC", [(1, 37, 12), (2, 50, 16), (1, 9, 128)])
+@pytest.mark.parametrize("G,NF,NC", [(1, 37, 12), (2, 50, 16), (3, 700, 4), (4, 1001, 3)])
+def test_concat_node_ops(hb, G, NF, NC):
+    """lin_cat / wgrad_cat (the in-place torch.cat inputs of gnn.py:100/153/191/220):
+    per-node blocks, a per-graph broadcast block and non-contiguous weight columns,
+    against the emulation (which materialises the concatenation)."""
+    gen = torch.Generator().manual_seed(11)
+    emu = EmuBackend()
+    N = G * NF
+    for rows, M in [((10, 80, 10), 100), ((10, 10), 40), ((3, 5, 7, 2), 20)]:
+        cols, c = [], 0
+        for k in rows:
+            cols.append(c)
+            c += k + 1  # a gap column between blocks: weight columns are not contiguous
+        K = c
+        segs_e = []
+        for i, k in enumerate(rows):
+            bc = i == len(rows) - 1
+            segs_e.append((r(k, G if bc else N, gen=gen), cols[i], bc))
+        segs_h = [(cuda(X), col, bc) for X, col, bc in segs_e]
+        W, b = r(M, K + 2, gen=gen), r(M, gen=gen)
+        close(hb.lin_cat(cuda(W), segs_h, N, b=cuda(b), act_in=True, bscale=2.0),
+              emu.lin_cat(W, segs_e, N, b=b, act_in=True, bscale=2.0), name=f"lin_cat{rows}")
+        dY = r(M, N, gen=gen)
+        dW_h, db_h = torch.zeros(M, K + 2, device="cuda"), torch.zeros(M, device="cuda")
+        dW_e, db_e = torch.zeros(M, K + 2, dtype=torch.float64), torch.zeros(M, dtype=torch.float64)
+        hb.wgrad_cat(cuda(dY), segs_h, dW_h, db=db_h, act_in=True, dbscale=0.5)
+        emu.wgrad_cat(dY, segs_e, dW_e, db=db_e, act_in=True, dbscale=0.5)
+        close(dW_h, dW_e, name=f"wgrad_cat{rows}"); close(db_h, db_e, name="db_cat")
+        assert (dW_h[:, [cl - 1 for cl in cols[1:]]] == 0).all(), "gap columns written"
+
+
+@pytest.mark.parametrize("G,NF,NC", [(1, 37, 12), (2, 50, 16), (1, 9, 128), (3, 700, 4)])
 def test_node_ops(hb, G, NF, NC):
     gen = torch.Generator().manual_seed(7)
     emu = EmuBackend()
