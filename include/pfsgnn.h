@@ -155,6 +155,16 @@ int pfsgnn_bn2_finalize(const float* mu1, const float* var1, const float* gamma,
                         const float* beta, float* rm, float* rv, int C, long long n,
                         float momentum, float eps, float* sc, float* sh, float* inv1,
                         float* inv2, void* stream);
+/* Eval-mode BatchNorm1d (running statistics, none updated) as one per-channel
+ * affine sc*y + sh: `times` = 2 for EdgeModel (gnn.py:101 + the Sequential
+ * child, replaces nn.BatchNorm1d.forward in eval), 1 for SModel/TModel
+ * (gnn.py:154, :192). */
+int pfsgnn_bn_eval_coef(const float* gamma, const float* beta, const float* rm,
+                        const float* rv, int C, float eps, int times, float* sc, float* sh,
+                        void* stream);
+/* Y[c][n] = sc[c]*X[c][n] + sh[c] over a channel-major [C][N] table */
+int pfsgnn_affine_rows(const float* X, int C, int N, const float* sc, const float* sh,
+                       float* Y, void* stream);
 /* its backward: g_y = alpha*g + gam0 + gam1*y from Sg = sum g, Sgx = sum g*xhat */
 int pfsgnn_bn2_bwd_coef(const float* Sg, const float* Sgx, const float* mu1, const float* var1,
                         const float* gamma, int C, long long n, float eps, float* alpha,

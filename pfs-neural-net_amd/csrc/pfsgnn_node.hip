@@ -1181,6 +1181,58 @@ extern "C" int pfsgnn_bn2_finalize(const float* mu1, const float* var1, const fl
   return pf::check_launch("pfsgnn_bn2_finalize");
 }
 
+// eval-mode BatchNorm1d (running statistics, nothing updated), applied
+// `times` times (2 for EdgeModel, gnn.py:101; 1 for S/T, gnn.py:154/192):
+// each application is y -> a*y + b with a = gamma/sqrt(rv+eps), b = beta - rm*a
+__global__ void k_bn_eval_coef(const float* __restrict__ gamma, const float* __restrict__ beta,
+                               const float* __restrict__ rm, const float* __restrict__ rv, int C,
+                               float eps, int times, float* __restrict__ sc,
+                               float* __restrict__ sh) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  const float a = gamma[c] / sqrtf(rv[c] + eps), b = beta[c] - rm[c] * a;
+  float s = 1.f, t = 0.f;
+  for (int i = 0; i < times; ++i) {
+    t = a * t + b;
+    s = a * s;
+  }
+  sc[c] = s;
+  sh[c] = t;
+}
+
+extern "C" int pfsgnn_bn_eval_coef(const float* gamma, const float* beta, const float* rm,
+                                   const float* rv, int C, float eps, int times, float* sc,
+                                   float* sh, void* stream) {
+  PF_REQUIRE(gamma && beta && rm && rv && sc && sh && C > 0 && C <= 64 && times >= 1 &&
+                 times <= 2,
+             "pfsgnn_bn_eval_coef", "bad arguments");
+  hipLaunchKernelGGL(k_bn_eval_coef, dim3(1), dim3(64), 0, as_stream(stream), gamma, beta, rm,
+                     rv, C, eps, times, sc, sh);
+  return pf::check_launch("pfsgnn_bn_eval_coef");
+}
+
+// Y[c][n] = sc[c]*X[c][n] + sh[c]; grid-stride over the flat [C][N] array
+__global__ __launch_bounds__(256) void k_affine_rows(const float* __restrict__ X, int C, int N,
+                                                     const float* __restrict__ sc,
+                                                     const float* __restrict__ sh,
+                                                     float* __restrict__ Y) {
+  const size_t tot = (size_t)C * N;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < tot; i += (size_t)gridDim.x * 256) {
+    const int c = (int)(i / (size_t)N);
+    Y[i] = fmaf(sc[c], X[i], sh[c]);
+  }
+}
+
+extern "C" int pfsgnn_affine_rows(const float* X, int C, int N, const float* sc, const float* sh,
+                                  float* Y, void* stream) {
+  PF_REQUIRE(X && Y && sc && sh && C > 0 && N > 0, "pfsgnn_affine_rows", "bad arguments");
+  const size_t tot = (size_t)C * N;
+  const unsigned blocks = (unsigned)std::min<size_t>((tot + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_affine_rows, dim3(blocks), dim3(256), 0, as_stream(stream), X, C, N, sc,
+                     sh, Y);
+  return pf::check_launch("pfsgnn_affine_rows");
+}
+
 __global__ void k_bn2_bwd_coef(const float* __restrict__ Sg, const float* __restrict__ Sgx,
                                const float* __restrict__ mu1, const float* __restrict__ var1,
                                const float* __restrict__ gamma, int C, long long n, float eps,

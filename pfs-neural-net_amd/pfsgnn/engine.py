@@ -92,6 +92,7 @@ class Engine:
         self.bn_eps = bn_eps
         self.bn_momentum = bn_momentum
         self.rms_eps = rms_eps
+        self.training = True
 
     # ================================================================= MLP
     def mlp_fwd(self, P, pre, X):
@@ -123,6 +124,12 @@ class Engine:
     def _bn(self, P, BN, key, X):
         if not self.normed:
             return X, None
+        if not self.training:
+            # eval: nn.BatchNorm1d on running statistics, applied once (gnn.py:154/192)
+            sc, sh = self.be.bn_eval_coef(P[key + "weight"], P[key + "bias"],
+                                          BN[key + "running_mean"], BN[key + "running_var"],
+                                          self.bn_eps, 1)
+            return self.be.affine_rows(X, sc, sh), None
         Y, mu, var = self.be.bn_fwd(X, P[key + "weight"], P[key + "bias"],
                                     BN.get(key + "running_mean"), BN.get(key + "running_var"),
                                     self.bn_momentum, self.bn_eps)
@@ -147,7 +154,13 @@ class Engine:
         Ps = be.lin(W1, 0, F, xs)
         Pt = be.lin_cat(W1, [(xt, F, False), (u, 3 * F, True)], d.NT, b=b1)
         y, mu1, var1 = be.edge_mlp_fwd(d, xe3[0], xe3[1], xe3[2], Ps, Pt, W1, W2, b2)
-        if self.normed:
+        if self.normed and not self.training:
+            # eval: both BatchNorm applications (gnn.py:101) on running statistics
+            key = pre + "norm."
+            sc, sh = be.bn_eval_coef(P[key + "weight"], P[key + "bias"], BN[key + "running_mean"],
+                                     BN[key + "running_var"], self.bn_eps, 2)
+            inv1 = None
+        elif self.normed:
             key = pre + "norm."
             sc, sh, inv1, _ = be.bn2_finalize(mu1, var1, P[key + "weight"], P[key + "bias"],
                                               BN.get(key + "running_mean"), BN.get(key + "running_var"),
@@ -286,12 +299,12 @@ class Engine:
         """GNN.forward (gnn.py:280-305).  xs_in [Fs, NS], xt_in [Ft, NT], xe_in [F, E],
         u_in [F, G] (channel-major).  Returns a context with the outputs
         (xs, xt, xe3, u) and everything backward needs."""
-        if not training:
-            raise NotImplementedError("eval-mode BatchNorm (running statistics) is not on the "
-                                      "training hot path; see DESIGN.md §Scope")
+        # eval (training=False): BatchNorm on running statistics, nothing updated;
+        # the context then serves inference only (backward refuses it)
+        self.training = training
         xs, s_enc = self.mlp_fwd(P, "encoder_s.", xs_in)
         xt, t_enc = self.mlp_fwd(P, "encoder_t.", xt_in)
-        ctx = {"d": d, "enc": (s_enc, t_enc), "blocks": []}
+        ctx = {"d": d, "enc": (s_enc, t_enc), "blocks": [], "training": training}
         xe3 = (xe_in, None, None)
         u = u_in
         for b in range(self.B):
@@ -310,6 +323,9 @@ class Engine:
         """Accumulates parameter gradients into ``Gr`` (same keys as ``P``).
         g_xe_out is [F, E] canonical, w.r.t. the final edge features."""
         d, be, F = ctx["d"], self.be, self.F
+        if not ctx.get("training", True):
+            raise NotImplementedError("backward through an eval-mode forward (BatchNorm on "
+                                      "running statistics) is not implemented")
         # node weight-gradient reductions are batched over the pass (flushed below)
         be.defer_begin()
         try:

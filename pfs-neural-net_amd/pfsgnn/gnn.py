@@ -331,6 +331,15 @@ def _engine_for(F, normed, B=0):
     return Engine(backend(), F=F, B=B, normed=normed)
 
 
+def _eval_guard(module):
+    """Eval mode (BatchNorm on running statistics) is inference only here."""
+    if not module.training and torch.is_grad_enabled() and any(
+            p.requires_grad for p in module.parameters()):
+        raise NotImplementedError(f"{type(module).__name__}.forward in eval mode runs inference "
+                                  "only (BatchNorm on running statistics, no backward): call it "
+                                  "under torch.no_grad()")
+
+
 # =================================================================== models
 class _MLPFn(torch.autograd.Function):
     @staticmethod
@@ -374,9 +383,10 @@ class _EdgeFn(torch.autograd.Function):
         F = module.Fdim
         d, lay = _graph_of(x_s, x_t, u, edge_index, F)
         eng = _engine_for(F, module.normed)
+        eng.training = module.training
         P, BN = module._flat_params(), module._bn_buffers()
         st = eng.edge_fwd(P, BN, d, "", _cm(x_s), _cm(x_t), (edges_in(edge_attr, lay), None, None), _cm(u))
-        if module.normed:
+        if module.normed and module.training:
             module._bump_batches(edge_keys=("norm.",))
         ctx.pf = (module, d, lay, st)
         return edges_out((st["y"], st["sc"], st["sh"]), lay, d)
@@ -408,6 +418,7 @@ class EdgeModel(MLP):
 
     def forward(self, x_s, x_t, edge_index, edge_attr, u):
         self._flat_sync()
+        _eval_guard(self)
         return _EdgeFn.apply(x_s, x_t, edge_attr, u, self[0].weight, self, edge_index)
 
 
@@ -417,9 +428,10 @@ class _SourceFn(torch.autograd.Function):
         F = module.Fdim
         d, lay = _graph_of(x_s, x_t, u, edge_index, F)
         eng = _engine_for(F, module.normed)
+        eng.training = module.training
         P, BN = module._flat_params(), module._bn_buffers()
         st = eng.source_fwd(P, BN, d, "", _cm(x_s), _cm(x_t), (edges_in(edge_attr, lay), None, None), _cm(u))
-        if module.normed:
+        if module.normed and module.training:
             module._bump_batches(node_keys=("norm.",))
         ctx.pf = (module, d, lay, st)
         return st["xs_new"].t()
@@ -450,6 +462,7 @@ class SModel(_ParamMixin, torch.nn.Module):
 
     def forward(self, x_s, x_t, edge_index, edge_attr, u):
         self._flat_sync()
+        _eval_guard(self)
         return _SourceFn.apply(x_s, x_t, edge_attr, u, self.node_mlp_1[0].weight, self, edge_index)
 
 
@@ -459,9 +472,10 @@ class _TargetFn(torch.autograd.Function):
         F = module.Fdim
         d, lay = _graph_of(x_s, x_t, u, edge_index, F)
         eng = _engine_for(F, module.normed)
+        eng.training = module.training
         P, BN = module._flat_params(), module._bn_buffers()
         st = eng.target_fwd(P, BN, d, "", _cm(x_s), _cm(x_t), (edges_in(edge_attr, lay), None, None), _cm(u))
-        if module.normed:
+        if module.normed and module.training:
             module._bump_batches(node_keys=("norm.",))
         ctx.pf = (module, d, lay, st)
         return st["xt_new"].t()
@@ -492,6 +506,7 @@ class TModel(_ParamMixin, torch.nn.Module):
 
     def forward(self, x_s, x_t, edge_index, edge_attr, u):
         self._flat_sync()
+        _eval_guard(self)
         return _TargetFn.apply(x_s, x_t, edge_attr, u, self.node_mlp_1[0].weight, self, edge_index)
 
 
@@ -611,19 +626,24 @@ class GNN(_FlatMixin, torch.nn.Module):
                       normed=self.normed)
 
     def forward(self, graph):
-        if not self.training:
-            raise NotImplementedError("GNN.forward in eval mode (BatchNorm running statistics) is "
-                                      "not implemented on the HIP path; the reference trains in "
-                                      "train mode (train.py:108)")
+        if not self.training and torch.is_grad_enabled() and any(
+                p.requires_grad for p in self.parameters()):
+            raise NotImplementedError("GNN.forward in eval mode runs inference only (BatchNorm "
+                                      "on running statistics, no backward): call it under "
+                                      "torch.no_grad()")
         for t in (graph.x_s, graph.x_t, graph.x_e, graph.x_u):
             if t is not None and t.requires_grad:
                 raise NotImplementedError("gradients w.r.t. the graph inputs are not computed")
         self._flat_sync()
         d, lay = geometry(graph.x_s, graph.x_t, graph.x_u, graph.edge_index, self.Fdim)
         xe_in = edges_in(graph.x_e, lay, cache=True)
-        anchor = self.encoder_s[0].weight
-        xs, xt, xe, u = _GNNFn.apply(anchor, self, d, lay, _cm(graph.x_s), _cm(graph.x_t),
-                                     xe_in, _cm(graph.x_u))
+        if self.training:
+            anchor = self.encoder_s[0].weight
+            xs, xt, xe, u = _GNNFn.apply(anchor, self, d, lay, _cm(graph.x_s), _cm(graph.x_t),
+                                         xe_in, _cm(graph.x_u))
+        else:
+            xs, xt, xe, u = self._forward_eval(d, lay, _cm(graph.x_s), _cm(graph.x_t), xe_in,
+                                               _cm(graph.x_u))
         out = BipartiteData.__new__(BipartiteData)
         out.edge_index, out.x_s, out.x_t, out.x_e, out.x_u = graph.edge_index, xs, xt, xe, u
         out.num_nodes = xt.size(0)
@@ -631,6 +651,15 @@ class GNN(_FlatMixin, torch.nn.Module):
         xe3, ectx = self.__dict__.pop("_pf_last")
         out._pf = (self, d, lay, xe, xe3, ectx)
         return out
+
+    def _forward_eval(self, d, lay, xs_in, xt_in, xe_in, u_in):
+        """GNN.forward in eval mode (gnn.py:280-305 with every BatchNorm1d on its
+        running statistics, none updated, num_batches_tracked unchanged)."""
+        P, BN = self._flat_params(), self._bn_buffers()
+        ectx = self._engine().forward(P, BN, d, xs_in, xt_in, xe_in, u_in, training=False)
+        xs, xt, xe3, u = ectx["out"]
+        self._pf_last = (xe3, ectx)
+        return xs.t(), xt.t(), edges_out(xe3, lay, d), u.t()
 
     def edge_prediction(self, x_e, scale=1):
         """gnn.py:307-312 (``round`` is the identity: ``self.train`` is a bound

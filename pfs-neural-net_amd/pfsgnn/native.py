@@ -75,6 +75,8 @@ _SIGS = {
     "pfsgnn_rms2_fwd": ([P, I, I, P, FL, P, P, P, P, P], I),
     "pfsgnn_rms2_bwd": ([P, P, P, P, P, P, I, I, FL, P, P, P, SZ, P], I),
     "pfsgnn_bn2_finalize": ([P, P, P, P, P, P, I, LL, FL, FL, P, P, P, P, P], I),
+    "pfsgnn_bn_eval_coef": ([P, P, P, P, I, FL, I, P, P, P], I),
+    "pfsgnn_affine_rows": ([P, I, I, P, P, P, P], I),
     "pfsgnn_bn2_bwd_coef": ([P, P, P, P, P, I, LL, FL, P, P, P, P, P, P], I),
     "pfsgnn_moment_coef": ([P, P, I, I, I, P, P], I),
     "pfsgnn_edge_mlp_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
@@ -404,6 +406,23 @@ class HipBackend:
               beta.data_ptr(), _ptr(rm), _ptr(rv), C, int(n), float(momentum), float(eps),
               sc.data_ptr(), sh.data_ptr(), inv1.data_ptr(), inv2.data_ptr(), _stream())
         return sc, sh, inv1, inv2
+
+    def bn_eval_coef(self, gamma, beta, rm, rv, eps, times):
+        """Eval-mode BatchNorm1d applied ``times`` times as (sc, sh)."""
+        C = gamma.shape[0]
+        self._chk(gamma, beta, rm, rv)
+        sc, sh = self.empty(C), self.empty(C)
+        _call("pfsgnn_bn_eval_coef", gamma.data_ptr(), beta.data_ptr(), rm.data_ptr(),
+              rv.data_ptr(), C, float(eps), int(times), sc.data_ptr(), sh.data_ptr(), _stream())
+        return sc, sh
+
+    def affine_rows(self, X, sc, sh):
+        C, N = X.shape
+        self._chk(X, sc, sh)
+        Y = self.empty(C, N)
+        _call("pfsgnn_affine_rows", X.data_ptr(), C, N, sc.data_ptr(), sh.data_ptr(),
+              Y.data_ptr(), _stream())
+        return Y
 
     def bn2_bwd_coef(self, Sg, Sgx, mu1, var1, gamma, n, eps, dgamma, dbeta):
         C = mu1.shape[0]

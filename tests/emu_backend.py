@@ -199,6 +199,17 @@ class EmuBackend:
         d1 = back(dY, Y1, r2)
         return back(d1, X, r1)
 
+    def bn_eval_coef(self, gamma, beta, rm, rv, eps, times):
+        a = gamma / torch.sqrt(rv.to(gamma.dtype) + eps)
+        b = beta - rm.to(gamma.dtype) * a
+        sc, sh = torch.ones_like(a), torch.zeros_like(a)
+        for _ in range(times):
+            sc, sh = a * sc, a * sh + b
+        return sc, sh
+
+    def affine_rows(self, X, sc, sh):
+        return X * sc[:, None] + sh[:, None]
+
     def bn2_finalize(self, mu1, var1, gamma, beta, rm, rv, n, momentum, eps):
         """EdgeModel's BatchNorm applied twice (gnn.py:101 -- ``super().forward``
         already runs ``self.norm`` as the Sequential's last child).  The second

@@ -72,3 +72,37 @@ def test_engine_unnormed_fp64():
     for name, prm in ref.named_parameters():
         gref = prm.grad if prm.grad is not None else torch.zeros_like(prm)
         assert (Gr[name] - gref).abs().max().item() <= 1e-8 * max(gref.abs().max().item(), 1.0), name
+
+
+@pytest.mark.parametrize("G,NF,NC,B", [(1, 9, 5, 2), (2, 6, 4, 1)])
+def test_engine_eval_mode_fp64(G, NF, NC, B):
+    """Eval-mode forward (every BatchNorm1d on running statistics, none
+    updated) vs the oracle in ``eval()``; running stats are first moved off
+    their init values by one training forward so the affine is non-trivial."""
+    model, graph = make_problem(G, NF, NC, B=B, seed=3)
+    model.train()
+    with torch.no_grad():
+        model(graph)
+    ref = copy.deepcopy(model).eval()
+    with torch.no_grad():
+        out = ref(graph)
+    be = EmuBackend()
+    eng = Engine(be, F=10, B=B, Fs=1, Ft=2, T=12, normed=True)
+    P = {k: v.detach().clone() for k, v in model.named_parameters()}
+    BN = {k: v.clone() for k, v in model.state_dict().items() if "running" in k}
+    BN0 = {k: v.clone() for k, v in BN.items()}
+    d = Dims(G, NF, NC, 10)
+    ctx = eng.forward(P, BN, d, graph.x_s.t().contiguous(), graph.x_t.t().contiguous(),
+                      to_canonical(graph.x_e, G, NF, NC), graph.x_u.t().contiguous(),
+                      training=False)
+    xs, xt, xe3, u = ctx["out"]
+    xe = be.edge_apply(d, *xe3)
+    assert torch.allclose(xs.t(), out.x_s, rtol=1e-9, atol=1e-9)
+    assert torch.allclose(xt.t(), out.x_t, rtol=1e-9, atol=1e-9)
+    assert torch.allclose(from_canonical(xe, G, NF, NC), out.x_e, rtol=1e-9, atol=1e-9)
+    assert torch.allclose(u.t(), out.x_u, rtol=1e-9, atol=1e-9)
+    for k in BN:
+        assert torch.equal(BN[k], BN0[k]), k
+    with pytest.raises(NotImplementedError):
+        eng.backward(P, {k: torch.zeros_like(v) for k, v in P.items()}, ctx,
+                     g_xe_out=torch.zeros_like(xe))

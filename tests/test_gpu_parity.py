@@ -220,3 +220,79 @@ def test_step_is_bitwise_deterministic():
         loss.backward()
         outs.append(torch.cat([p.grad.reshape(-1) for p in gnn.parameters()]).cpu())
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("G,NF,NC,B", [(1, 40, 12, 2), (2, 24, 16, 1)])
+def test_gnn_eval_forward_matches_oracle(G, NF, NC, B):
+    """model.eval() forward (BatchNorm on running statistics, none updated)
+    + the train.py loss under no_grad, vs the oracle in eval() in fp64/fp32."""
+    import pfsgnn
+    from pfsgnn.train import loss_function
+    model, graph = make_problem(G, NF, NC, B=B, seed=5 + G)
+    model.train()
+    with torch.no_grad():
+        model(graph)                     # moves the running stats off their init values
+    seed, sharp = 99, 8.0
+    res = {}
+    for dt in (torch.float64, torch.float32):
+        m = copy.deepcopy(model).to(dt).eval()
+        g = OGraph(graph.edge_index, graph.x_s.to(dt), graph.x_t.to(dt), graph.x_e.to(dt),
+                   graph.x_u.to(dt), graph.s_batch, graph.t_batch)
+        with torch.no_grad():
+            out = m(g)
+            uni = torch.as_tensor(uniform_numpy(seed, G * NF * NC), dtype=dt)
+            loss, _ = oracle_loss(m, out.x_e, g.x_t, G, NF, NC, pclass=0.1, pfiber=0.1,
+                                  sharpness=sharp, uniform=uni)
+        res[dt] = (out, loss)
+    gnn = pfsgnn.GNN(B=B, Fdim=10, T=12, F_s=1, F_t=2).cuda()
+    gnn.load_state_dict({k: v.float() for k, v in model.state_dict().items()})
+    gnn.eval()
+    sd0 = {k: v.clone() for k, v in gnn.state_dict().items()}
+    data = pfsgnn.BipartiteData(graph.edge_index, graph.x_s.float(), graph.x_t.float(),
+                                graph.x_e.float(), graph.x_u.float())
+    with pytest.raises(NotImplementedError):
+        gnn(data)                         # eval with grad enabled is refused loudly
+    with torch.no_grad():
+        out = gnn(data)
+        loss, _ = loss_function(out, graph.x_t.float().cuda(), pclass=0.1, pfiber=0.1,
+                                sharpness=sharp, seed=seed)
+    torch.cuda.synchronize()
+    (o64, l64), (o32, l32) = res[torch.float64], res[torch.float32]
+    for nm in ("x_e", "x_s", "x_t", "x_u"):
+        check("eval " + nm, getattr(out, nm), getattr(o64, nm), getattr(o32, nm))
+    check("eval loss", loss, l64, l32)
+    for k, v in gnn.state_dict().items():
+        assert torch.equal(v, sd0[k]), k
+
+
+@pytest.mark.parametrize("kind", ["edge", "source", "target"])
+def test_standalone_models_eval_match_oracle(kind):
+    import pfsgnn
+    pairs = {"edge": (ref_gnn.EdgeModel, pfsgnn.EdgeModel), "source": (ref_gnn.SModel, pfsgnn.SModel),
+             "target": (ref_gnn.TModel, pfsgnn.TModel)}
+    G, NF, NC = 2, 20, 16
+    mo, mh, ei, xs, xt, xe, u = _module_case(*pairs[kind], G, NF, NC, seed=4)
+    with torch.no_grad():
+        for n, b in mo.named_buffers():
+            if n.endswith("running_mean"):
+                b.copy_(torch.linspace(-0.5, 0.5, b.numel(), dtype=b.dtype))
+            elif n.endswith("running_var"):
+                b.copy_(torch.linspace(0.5, 2.0, b.numel(), dtype=b.dtype))
+    mh.load_state_dict({k: v.float() if v.is_floating_point() else v
+                        for k, v in mo.state_dict().items()})
+    sb = torch.arange(G).repeat_interleave(NF)
+    tb = torch.arange(G).repeat_interleave(NC)
+    res = {}
+    for dt in (torch.float64, torch.float32):
+        m = copy.deepcopy(mo).to(dt).eval()
+        ins = [t.to(dt) for t in (xs, xt, xe, u)]
+        with torch.no_grad():
+            res[dt] = m(ins[0], ins[1], ei, ins[2], ins[3], tb if kind == "target" else sb)
+    mh.eval()
+    sd0 = {k: v.clone() for k, v in mh.state_dict().items()}
+    with torch.no_grad():
+        outh = mh(*(t.float().cuda() for t in (xs, xt)), ei.cuda(), xe.float().cuda(),
+                  u.float().cuda())
+    check(kind + " eval out", outh, res[torch.float64], res[torch.float32])
+    for k, v in mh.state_dict().items():
+        assert torch.equal(v, sd0[k]), k
