@@ -370,30 +370,38 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ W, int l
     const int kk = 4 * s + kq;
     bv[s] = kk < Ki ? seg_load(S, kk, nc, ng, N, Gc) : 0.f;
   }
-  // op(W) staging: 8 loads per thread in flight, then their LDS stores
-  const int MR = MT * 16, TOT = MR * K4;
-  for (int base = t; base < TOT; base += 8 * 256) {
-    float v[8];
-    int at[8];
+  // op(W) staging: up to 48 loads per thread in flight (the whole op(W) in one
+  // L2 round trip for every shape up to 100 x 100), then their LDS stores; the
+  // (m, kk) split is recomputed for the stores instead of held in registers
+  constexpr int MR = MT * 16, TOT = MR * K4;
+  constexpr int PER = (TOT + 255) / 256, BATCH = PER < 48 ? PER : 48;
+  auto split = [&](int idx, int& m, int& kk) {
+    if (!trans) {
+      m = idx / K4;
+      kk = idx - m * K4;
+    } else {  // op(W) = W^T: walk W's rows so the reads stay contiguous
+      kk = idx / MR;
+      m = idx - kk * MR;
+    }
+  };
+  for (int base = t; base < TOT; base += BATCH * 256) {
+    float v[BATCH];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < BATCH; ++u) {
       const int idx = base + u * 256;
       int m, kk;
-      if (!trans) {
-        m = idx / K4;
-        kk = idx - m * K4;
-      } else {  // op(W) = W^T: walk W's rows so the reads stay contiguous
-        kk = idx / MR;
-        m = idx - kk * MR;
-      }
-      at[u] = idx < TOT ? m * LDK + kk : -1;
+      split(idx, m, kk);
       v[u] = 0.f;
       if (idx < TOT && m < Mo && kk < Ki)
         v[u] = trans ? W[(size_t)kk * ldw + m] : W[(size_t)m * ldw + seg_wcol(S, kk)];
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (at[u] >= 0) Ws[at[u]] = v[u];
+    for (int u = 0; u < BATCH; ++u) {
+      const int idx = base + u * 256;
+      int m, kk;
+      split(idx, m, kk);
+      if (idx < TOT) Ws[m * LDK + kk] = v[u];
+    }
   }
   if (act_in) {
 #pragma unroll
