@@ -3,6 +3,11 @@ complete bipartite graphs (BASELINE.json metric), plus the HBM roofline of the
 dominant kernel and the CPU oracle timed on the host.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--graphs G] [--blocks B]
+                    [--fibers NF] [--classes NC]
+
+Default workload: BASELINE.json's metric config (16 graphs of 2394x128 per
+GPU, 8 blocks).  configs[2] of BASELINE.json (a batch of 256 synthetic
+2394x16 graphs) is ``--classes 16 --graphs 256``.
 
 One process per GPU (torchrun for N > 1).  Each rank trains on its own G
 synthetic graphs (weak scaling); gradients are mean-all-reduced over RCCL once
@@ -25,7 +30,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-NF, NC, FDIM = 2394, 128, 10
+NF, NC, FDIM = 2394, 128, 10      # overridden by --fibers / --classes
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense fp32-input MFMA (= fp32 vector peak)
 
@@ -33,9 +38,11 @@ F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense fp32-input MFMA (= fp32 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--graphs", type=int, default=16, help="graphs per GPU")
+    ap.add_argument("--fibers", type=int, default=2394)
+    ap.add_argument("--classes", type=int, default=128)
     ap.add_argument("--blocks", type=int, default=8, help="message-passing rounds")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
@@ -117,7 +124,8 @@ def cpu_baseline(blocks, seconds):
     from harness import make_problem
     from noise_ref import uniform_numpy
     from oracle.ref_train import loss_function as oracle_loss
-    threads = min(16, os.cpu_count() or 1)
+    # train.py:15-19: the reference runs on every host core os.cpu_count() reports
+    threads = os.cpu_count() or 1
     torch.set_num_threads(threads)
     model, graph = make_problem(1, NF, NC, B=blocks, seed=0, dtype=torch.float32)
     model.train()
@@ -135,13 +143,21 @@ def cpu_baseline(blocks, seconds):
         el = time.perf_counter() - t0
         if el >= seconds or steps >= 50:
             break
+    try:
+        share = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        share = threads
     return {"value": steps * NF * NC / el, "unit": "edges/s", "cores": threads, "kind": "port",
             "sample": f"{steps} training step(s) of one {NF}x{NC} graph, {blocks} blocks, "
-                      f"oracle/ (torch CPU fp32, {threads} threads), {el:.1f}s"}
+                      f"oracle/ (torch CPU fp32, {threads} threads = os.cpu_count() as "
+                      f"train.py:15-19 sets; {share} CPUs in this process's affinity mask), "
+                      f"{el:.1f}s"}
 
 
 def main():
+    global NF, NC
     args = parse()
+    NF, NC = args.fibers, args.classes
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -162,7 +178,7 @@ def main():
     import pfsgnn
     from pfsgnn import config, native
     from pfsgnn.train import loss_function
-    from pfsgnn.distributed import allreduce_gradients, broadcast_parameters
+    from pfsgnn.distributed import allreduce_gradients, broadcast_parameters, sync_buffers
     config.device = device
 
     G, B = args.graphs, args.blocks
@@ -191,6 +207,7 @@ def main():
         loss = fwd_bwd()
         allreduce_gradients(gnn)
         opt.step()
+        sync_buffers(gnn)          # DDP broadcast_buffers semantics (no-op at N=1)
         return loss
 
     for i in range(args.warmup):
@@ -219,6 +236,7 @@ def main():
             if world > 1:
                 allreduce_gradients(gnn)
                 opt.step()
+                sync_buffers(gnn)
             return static_loss
 
         step()
@@ -294,8 +312,11 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(B, args.cpu_seconds)
         value = world * E * args.steps / elapsed
+        metric = "training-step edges/sec on 2394\u00d7128 bipartite batches; % HBM roofline"
+        if (NF, NC) != (2394, 128):
+            metric = f"training-step edges/sec on {NF}\u00d7{NC} bipartite batches; % HBM roofline"
         line = {
-            "metric": "training-step edges/sec on 2394x128 bipartite batches; % HBM roofline",
+            "metric": metric,
             "value": value, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",

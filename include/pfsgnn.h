@@ -53,6 +53,10 @@ size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F);
 #define PFSGNN_EDGE_MFMA 1
 int pfsgnn_set_edge_path(int path);
 int pfsgnn_get_edge_path(void);
+/* Grid the current edge path launches for a batch (host-only query, for tests
+ * and diagnostics): info[0] = KS class splits, [1] = classes per split,
+ * [2] = blocks per edge kernel, [3] = 64-fiber groups per graph. */
+int pfsgnn_edge_grid(int G, int NF, int NC, int* info);
 
 /* Per-kernel HIP-event timing of the main edge/loss kernels (diagnostics for
  * bench.py; off by default, must stay off while a stream is captured).
@@ -278,11 +282,15 @@ int pfsgnn_edges_from_canonical(const float* y, const float* sc, const float* sh
                                 float* dst, void* stream);
 
 /* ---------------------------------------------------------------- optimiser
- * torch.optim.Adam (amsgrad=False, maximize=False) over one flat buffer.
- * step_dev (optional, device float) overrides `step` (capturable form). */
+ * torch.optim.Adam (amsgrad=False, maximize=False) over one flat buffer
+ * (replaces optimizer.step(), train.py:111/141).  step_dev (optional, device
+ * float) overrides `step` (capturable form).  live (optional, device byte
+ * per element): elements with live[i] == 0 belong to parameters whose .grad
+ * the reference leaves None (unused by the loss); torch.optim.Adam skips
+ * those, so they are left untouched (matters when weight_decay != 0). */
 int pfsgnn_adam(float* p, const float* g, float* m, float* v, long long n, int step,
                 const float* step_dev, float lr, float beta1, float beta2, float eps,
-                float weight_decay, void* stream);
+                float weight_decay, const unsigned char* live, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1147,6 +1147,16 @@ extern "C" int pfsgnn_set_edge_path(int path) {
 }
 extern "C" int pfsgnn_get_edge_path(void) { return g_path; }
 
+extern "C" int pfsgnn_edge_grid(int G, int NF, int NC, int* info) {
+  PF_REQUIRE(G > 0 && NF > 0 && NC > 0 && info, "pfsgnn_edge_grid", "bad arguments");
+  const EdgeGeo geo = geo_for(G, NF, NC);
+  info[0] = geo.KS;
+  info[1] = geo.CPS;
+  info[2] = geo.nblocks;
+  info[3] = geo.NFG;
+  return 0;
+}
+
 namespace {
 size_t edge_ws_floats(const EdgeGeo& geo, int G, int NC, int F) {
   const size_t nb = geo.nblocks, ks = geo.KS, NS = geo.NS;

@@ -151,6 +151,12 @@ __global__ void k_loss_class_reduce(const float* __restrict__ part, int G, int N
   tvar[idx] = NF > 1 ? (float)(Q0 / (double)(NF - 1)) : NAN;  // torch.var, correction=1
 }
 
+// torch.min propagates NaN (train.py:53: a class with N_i = 0 gives 0/0);
+// fminf would drop it
+__device__ __forceinline__ float nan_min(float a, float b) {
+  return (a != a) ? a : ((b != b) ? b : (b < a ? b : a));
+}
+
 // one block per graph: train.py:53-71 and the per-node gradient coefficients
 __global__ __launch_bounds__(256) void k_loss_finalize(
     int NF, int NC, int NT, const float* __restrict__ n_prime, const float* __restrict__ fiber_time,
@@ -167,12 +173,12 @@ __global__ __launch_bounds__(256) void k_loss_finalize(
     const long long cn = (long long)g * NC + c;
     const float Ni = ci[NT + cn] / nfields;
     const float comp = n_prime[cn] / Ni;
-    mn = fminf(mn, comp);
+    mn = nan_min(mn, comp);
   }
   smin[t] = mn;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
-    if (t < s) smin[t] = fminf(smin[t], smin[t + s]);
+    if (t < s) smin[t] = nan_min(smin[t], smin[t + s]);
     __syncthreads();
   }
   const float umin = smin[0];

@@ -1315,9 +1315,12 @@ extern "C" int pfsgnn_moment_coef(const float* mom, const float* gst, int C, int
 __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                        float* __restrict__ v, long long n, float neg_step0, float beta1, float beta2,
                        float bc2_sqrt0, float eps, float wd, float lr,
-                       const float* __restrict__ step_dev) {
+                       const float* __restrict__ step_dev, const unsigned char* __restrict__ live) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  // a parameter whose .grad the reference leaves None is skipped by
+  // torch.optim.Adam: no decay, moments and value untouched
+  if (live && !live[i]) return;
   float neg_step = neg_step0, bc2_sqrt = bc2_sqrt0;
   if (step_dev) {  // capturable form: the step count lives on the device
     const double st = (double)*step_dev;
@@ -1339,7 +1342,7 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
 
 extern "C" int pfsgnn_adam(float* p, const float* g, float* m, float* v, long long n, int step,
                            const float* step_dev, float lr, float beta1, float beta2, float eps,
-                           float weight_decay, void* stream) {
+                           float weight_decay, const unsigned char* live, void* stream) {
   PF_REQUIRE(p && g && m && v && n > 0 && (step >= 1 || step_dev), "pfsgnn_adam",
              "bad arguments");
   const int st = step >= 1 ? step : 1;
@@ -1349,6 +1352,6 @@ extern "C" int pfsgnn_adam(float* p, const float* g, float* m, float* v, long lo
   const float bc2_sqrt = (float)std::sqrt(bc2);
   hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream),
                      p, g, m, v, n, neg_step, beta1, beta2, bc2_sqrt, eps, weight_decay, lr,
-                     step_dev);
+                     step_dev, live);
   return pf::check_launch("pfsgnn_adam");
 }

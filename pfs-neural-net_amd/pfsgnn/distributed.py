@@ -5,8 +5,14 @@ shards across ranks with no data-path collective: every rank runs the fused
 step on its own graphs, and the only exchange is ONE all-reduce (mean) of the
 flat gradient buffer (~40k floats for the reference model) per step, over
 RCCL (backend "nccl" on ROCm) on xGMI -- it is latency-bound, so a single
-bucket is the right size.  BatchNorm statistics stay per rank (no SyncBN), as
-torch DDP does by default.
+bucket is the right size.
+
+BatchNorm: the batch statistics a forward normalises with are per rank (no
+SyncBN), as under torch DDP.  The running statistics (and
+num_batches_tracked) follow DDP's default ``broadcast_buffers=True``: rank
+0's buffers are broadcast to every rank once per step (``sync_buffers``, one
+collective on a packed buffer), so eval-mode inference and checkpoints do not
+depend on the rank.
 """
 import os
 
@@ -40,6 +46,28 @@ def broadcast_parameters(model, src=0):
             dist.broadcast(p.data, src)
     for b in model.buffers():
         dist.broadcast(b, src)
+
+
+def sync_buffers(model, src=0):
+    """DDP's broadcast_buffers=True: every rank takes rank `src`'s BatchNorm
+    running statistics and batch counters (one broadcast of a packed buffer)."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return
+    bufs = [b for b in model.buffers()]
+    if not bufs:
+        return
+    fl = [b for b in bufs if b.dtype == torch.float32]
+    it = [b for b in bufs if b.dtype != torch.float32]
+    for group in (fl, it):
+        if not group:
+            continue
+        packed = torch.cat([b.reshape(-1) for b in group])
+        dist.broadcast(packed, src)
+        off = 0
+        for b in group:
+            n = b.numel()
+            b.copy_(packed[off:off + n].view_as(b))
+            off += n
 
 
 def allreduce_gradients(model):

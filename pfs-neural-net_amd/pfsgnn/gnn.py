@@ -24,6 +24,8 @@ from ``BipartiteData.__inc__``) with ``x_u`` of shape [G, F]; ``u[g]`` is
 broadcast to the edges / nodes of graph g and the GlobalModel means are
 per graph.  With G == 1 this is exactly the reference.
 """
+import weakref
+
 import torch
 
 from . import config
@@ -105,8 +107,42 @@ class Loader(torch.utils.data.Dataset):
 
 
 # ==================================================================== layout
-_LAYOUT_CACHE = {}
-_EDGE_CACHE = {}
+class _TensorCache:
+    """Results cached per live tensor OBJECT and its in-place version counter.
+
+    Keys are ``id(tensor)`` plus a weak reference that must still resolve to
+    that same object: a freed tensor whose address (or id) the allocator hands
+    to a new tensor never hits a stale entry, and an in-place write bumps
+    ``_version`` and misses.  (Keying on ``data_ptr`` would silently reuse
+    the previous batch's layout or features whenever the caching allocator
+    recycles a block of the same size.)"""
+
+    def __init__(self, cap):
+        self.cap = cap
+        self.d = {}
+
+    def get(self, t, extra):
+        e = self.d.get(id(t))
+        if e is None:
+            return None
+        ref, ver, ex, val = e
+        if ref() is not t or ver != t._version or ex != extra:
+            return None
+        return val
+
+    def put(self, t, extra, val):
+        if len(self.d) >= self.cap:
+            self.d = {k: e for k, e in self.d.items() if e[0]() is not None}
+            if len(self.d) >= self.cap:
+                self.d.clear()
+        self.d[id(t)] = (weakref.ref(t), t._version, extra, val)
+
+    def clear(self):
+        self.d.clear()
+
+
+_LAYOUT_CACHE = _TensorCache(32)
+_EDGE_CACHE = _TensorCache(4)
 
 
 class Layout:
@@ -119,10 +155,6 @@ class Layout:
         self.perm = perm if mode == Layout.PERM else None
         self.fiber_major = fiber_major    # caller order == train.py's positional order
 
-    @property
-    def key(self):
-        return (self.mode, None if self.perm is None else self.perm.data_ptr())
-
 
 def geometry(x_s, x_t, x_u, edge_index, F):
     """(Dims, Layout) for a batch."""
@@ -133,8 +165,8 @@ def geometry(x_s, x_t, x_u, edge_index, F):
     NF, NC = S // G, T // G
     d = Dims(G, NF, NC, F)
     E = int(edge_index.size(1))
-    key = (edge_index.data_ptr(), edge_index._version, E, G, NF, NC)
-    hit = _LAYOUT_CACHE.get(key)
+    key = (E, G, NF, NC)
+    hit = _LAYOUT_CACHE.get(edge_index, key)
     if hit is None:
         if E != d.E:
             raise NotImplementedError(
@@ -147,9 +179,7 @@ def geometry(x_s, x_t, x_u, edge_index, F):
                                       "(fiber, class) pair is missing, repeated, or crosses graphs)")
         mode = Layout.CANONICAL if identity else (Layout.FIBER_MAJOR if fm else Layout.PERM)
         hit = Layout(G, NF, NC, mode, perm, fiber_major=fm)
-        if len(_LAYOUT_CACHE) > 32:
-            _LAYOUT_CACHE.clear()
-        _LAYOUT_CACHE[key] = hit
+        _LAYOUT_CACHE.put(edge_index, key, hit)
     return d, hit
 
 
@@ -158,14 +188,14 @@ def edges_in(x_e, lay, cache=False):
     if (lay.mode == Layout.CANONICAL and x_e.dtype == torch.float32 and x_e.is_cuda
             and x_e.t().is_contiguous()):
         return x_e.t()
-    key = (x_e.data_ptr(), x_e._version, tuple(x_e.shape), lay.key)
-    if cache and key in _EDGE_CACHE:
-        return _EDGE_CACHE[key]
+    key = (tuple(x_e.shape), lay)      # the Layout object itself (identity compare)
+    if cache:
+        hit = _EDGE_CACHE.get(x_e, key)
+        if hit is not None:
+            return hit
     out = backend().edges_to_canonical(x_e, lay)
     if cache:
-        if len(_EDGE_CACHE) > 4:
-            _EDGE_CACHE.clear()
-        _EDGE_CACHE[key] = out
+        _EDGE_CACHE.put(x_e, key, out)
     return out
 
 
@@ -296,6 +326,18 @@ class _FlatMixin(_ParamMixin):
                     p.grad = sl.view(p.shape)
         return {n: p.grad for n, p in self.named_parameters()}
 
+    def _recording_grads(self):
+        return _GradRecorder(self._flat_grads())
+
+    def _mark_live(self, names):
+        """Parameters a backward wrote (the ones the reference's autograd would
+        give a .grad); FusedAdam skips the others when weight_decay != 0."""
+        params = dict(self.named_parameters())
+        for n in names:
+            p = params.get(n)
+            if p is not None:
+                p._pf_live = True
+
     def zero_grad(self, set_to_none=True):
         """Zero the flat gradient buffer in one kernel and keep every ``p.grad``
         attached to it (the buffer the fused backward accumulates into, the
@@ -304,6 +346,8 @@ class _FlatMixin(_ParamMixin):
         them exactly unchanged, as the reference's skipped None grads do.  No
         host sync and no reallocation, so the step can be graph-captured."""
         gflat = getattr(self, "_pf_gflat", None)
+        for p in self.parameters():
+            p._pf_live = False          # the reference's zero_grad leaves every .grad None
         if gflat is not None:
             params = [p for _, p in self.named_parameters()]
             if len(params) == len(self._pf_off) and all(
@@ -577,7 +621,15 @@ class Block(torch.nn.Module):
 # ====================================================================== GNN
 class _GNNFn(torch.autograd.Function):
     """The whole GNN.forward as one fused engine call; its backward is the
-    engine's hand-fused block backward (engine.Engine.backward)."""
+    engine's hand-fused block backward (engine.Engine.backward).
+
+    The final edge features are NOT an output: they stay in the engine's lazy
+    canonical state (y, sc, sh).  In their place the function returns a 0-dim
+    ``token`` that every consumer of the edge state takes as its autograd
+    input -- the fused loss (train._LossFn) or the caller-order ``x_e`` view
+    (_EdgesOutFn, built only if ``out.x_e`` is read).  Consumers hand their
+    canonical [F, E] gradient over through the context, so nothing is ever
+    converted to the caller's order unless the caller asks for it."""
 
     @staticmethod
     def forward(ctx, anchor, model, d, lay, xs_in, xt_in, xe_in, u_in):
@@ -591,22 +643,79 @@ class _GNNFn(torch.autograd.Function):
         xs, xt, xe3, u = ectx["out"]
         ctx.pf = (model, d, lay, ectx)
         model._pf_last = (xe3, ectx)
-        x_e = edges_out(xe3, lay, d)
-        return xs.t(), xt.t(), x_e, u.t()
+        token = xs.new_zeros(())
+        return xs.t(), xt.t(), token, u.t()
 
     @staticmethod
-    def backward(ctx, g_xs, g_xt, g_xe, g_u):
+    def backward(ctx, g_xs, g_xt, g_token, g_u):
         model, d, lay, ectx = ctx.pf
-        P, Gr = model._flat_params(), model._flat_grads()
+        P, Gr = model._flat_params(), model._recording_grads()
         cm = (lambda g: None if g is None else g.t().contiguous())
-        gc = grad_edges_in(g_xe, lay)
-        # a fused consumer of x_e (train._LossFn) hands its gradient over in the
-        # canonical order instead of round-tripping it through the caller's order
-        handed = ectx.pop("g_xe_canonical", None)
-        if handed is not None:
-            gc = handed if gc is None else gc + handed
+        # consumers of the edge state hand their gradient over in canonical order
+        gc = ectx.pop("g_xe_canonical", None)
         model._engine().backward(P, Gr, ectx, gc, cm(g_xs), cm(g_xt), cm(g_u))
+        model._mark_live(Gr.used)
         return (None,) * 8
+
+
+class _EdgesOutFn(torch.autograd.Function):
+    """Caller-order ``x_e`` [E, F] of a GNN output, materialised on first read
+    from the lazy canonical state; its gradient goes back to _GNNFn through
+    the shared context (canonical order), the token gets a zero."""
+
+    @staticmethod
+    def forward(ctx, token, ectx, xe3, lay, d):
+        ctx.pf = (ectx, lay)
+        return edges_out(xe3, lay, d)
+
+    @staticmethod
+    def backward(ctx, g):
+        ectx, lay = ctx.pf
+        gc = grad_edges_in(g, lay)
+        if gc is not None:
+            gc = gc.contiguous()
+            prev = ectx.get("g_xe_canonical")
+            ectx["g_xe_canonical"] = gc if prev is None else prev + gc
+        return g.new_zeros(()), None, None, None, None
+
+
+class _GradRecorder(dict):
+    """Parameter-gradient dict that records which entries a backward wrote
+    (the parameters autograd would give a .grad in the reference)."""
+
+    def __init__(self, d):
+        super().__init__(d)
+        self.used = set()
+
+    def __getitem__(self, k):
+        self.used.add(k)
+        return super().__getitem__(k)
+
+
+class GNNOutput(BipartiteData):
+    """The BipartiteData GNN.forward returns (gnn.py:305).  ``x_e`` is built on
+    first read (caller's edge order); the fused loss never reads it."""
+
+    @property
+    def x_e(self):
+        v = self.__dict__.get("_x_e_val")
+        if v is None:
+            mk = self.__dict__.get("_x_e_make")
+            if mk is None:
+                return None
+            v = mk()
+            self.__dict__["_x_e_val"] = v
+        return v
+
+    @x_e.setter
+    def x_e(self, v):
+        self.__dict__["_x_e_val"] = v
+        self.__dict__["_x_e_make"] = None
+        if "_pf" in self.__dict__:        # replaced by the caller: the fused loss
+            self.__dict__["_pf_replaced"] = True   # must not read the engine state
+
+    def to(self, device):
+        return BipartiteData(self.edge_index, self.x_s, self.x_t, self.x_e, self.x_u).to(device)
 
 
 class GNN(_FlatMixin, torch.nn.Module):
@@ -637,19 +746,24 @@ class GNN(_FlatMixin, torch.nn.Module):
         self._flat_sync()
         d, lay = geometry(graph.x_s, graph.x_t, graph.x_u, graph.edge_index, self.Fdim)
         xe_in = edges_in(graph.x_e, lay, cache=True)
+        out = GNNOutput.__new__(GNNOutput)
         if self.training:
             anchor = self.encoder_s[0].weight
-            xs, xt, xe, u = _GNNFn.apply(anchor, self, d, lay, _cm(graph.x_s), _cm(graph.x_t),
-                                         xe_in, _cm(graph.x_u))
+            xs, xt, token, u = _GNNFn.apply(anchor, self, d, lay, _cm(graph.x_s), _cm(graph.x_t),
+                                            xe_in, _cm(graph.x_u))
+            xe3, ectx = self.__dict__.pop("_pf_last")
+            out._x_e_make = lambda: _EdgesOutFn.apply(token, ectx, xe3, lay, d)
         else:
-            xs, xt, xe, u = self._forward_eval(d, lay, _cm(graph.x_s), _cm(graph.x_t), xe_in,
-                                               _cm(graph.x_u))
-        out = BipartiteData.__new__(BipartiteData)
-        out.edge_index, out.x_s, out.x_t, out.x_e, out.x_u = graph.edge_index, xs, xt, xe, u
+            xs, xt, u = self._forward_eval(d, lay, _cm(graph.x_s), _cm(graph.x_t), xe_in,
+                                           _cm(graph.x_u))
+            xe3, ectx = self.__dict__.pop("_pf_last")
+            token = None
+            out._x_e_make = lambda: edges_out(xe3, lay, d)
+        out._x_e_val = None
+        out.edge_index, out.x_s, out.x_t, out.x_u = graph.edge_index, xs, xt, u
         out.num_nodes = xt.size(0)
         # lets train.loss_function fuse on the lazy final edge state (y, sc, sh)
-        xe3, ectx = self.__dict__.pop("_pf_last")
-        out._pf = (self, d, lay, xe, xe3, ectx)
+        out._pf = (self, d, lay, token, xe3, ectx)
         return out
 
     def _forward_eval(self, d, lay, xs_in, xt_in, xe_in, u_in):
@@ -659,7 +773,7 @@ class GNN(_FlatMixin, torch.nn.Module):
         ectx = self._engine().forward(P, BN, d, xs_in, xt_in, xe_in, u_in, training=False)
         xs, xt, xe3, u = ectx["out"]
         self._pf_last = (xe3, ectx)
-        return xs.t(), xt.t(), edges_out(xe3, lay, d), u.t()
+        return xs.t(), xt.t(), u.t()
 
     def edge_prediction(self, x_e, scale=1):
         """gnn.py:307-312 (``round`` is the identity: ``self.train`` is a bound

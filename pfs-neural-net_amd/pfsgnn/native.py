@@ -55,6 +55,7 @@ _SIGS = {
     "pfsgnn_workspace_bytes": ([I, I, I, I], SZ),
     "pfsgnn_set_edge_path": ([I], I),
     "pfsgnn_get_edge_path": ([], I),
+    "pfsgnn_edge_grid": ([I, I, I, ctypes.POINTER(ctypes.c_int)], I),
     "pfsgnn_timing_enable": ([I], I),
     "pfsgnn_timing_reset": ([], I),
     "pfsgnn_timing_query": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
@@ -93,7 +94,7 @@ _SIGS = {
     "pfsgnn_layout_analyze": ([P, LL, I, I, I, P, P, P, SZ, P], I),
     "pfsgnn_edges_to_canonical": ([P, I, I, I, I, I, P, P, P], I),
     "pfsgnn_edges_from_canonical": ([P, P, P, I, I, I, I, I, P, I, P, P], I),
-    "pfsgnn_adam": ([P, P, P, P, LL, I, P, FL, FL, FL, FL, FL, P], I),
+    "pfsgnn_adam": ([P, P, P, P, LL, I, P, FL, FL, FL, FL, FL, P, P], I),
 }
 
 
@@ -132,6 +133,13 @@ def set_edge_path(path):
 def get_edge_path():
     code = lib().pfsgnn_get_edge_path()
     return {v: k for k, v in EDGE_PATHS.items()}[code]
+
+
+def edge_grid(G, NF, NC):
+    """Grid of the current edge path for a batch: dict(KS, CPS, nblocks, NFG)."""
+    info = (ctypes.c_int * 4)()
+    _check(lib().pfsgnn_edge_grid(int(G), int(NF), int(NC), info), "pfsgnn_edge_grid")
+    return dict(KS=info[0], CPS=info[1], nblocks=info[2], NFG=info[3])
 
 
 def exported_symbols():
@@ -192,6 +200,10 @@ class HipBackend:
         self.dtype = torch.float32
         self._ws = None
         self._ws_key = None
+        # buffers replaced by a larger one stay alive: a HIP graph captured
+        # while they were current keeps their addresses baked in, and a replay
+        # must never write into memory the allocator has handed out again
+        self._retired = []
 
     # ------------------------------------------------------------ memory
     def empty(self, *shape):
@@ -207,6 +219,8 @@ class HipBackend:
         need = lib().pfsgnn_workspace_bytes(d.G, d.NF, d.NC, d.F) if d is not None else 0
         need = max(need, 16 << 20)
         if self._ws is None or self._ws.numel() < need:
+            if self._ws is not None:
+                self._retired.append(self._ws)
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         return self._ws
 
@@ -275,6 +289,8 @@ class HipBackend:
                 self._defer = []
             size = max(2 * (arena.numel() if arena is not None else 0), 64 << 20,
                        2 * nbytes)
+            if arena is not None:
+                self._retired.append(arena)     # see __init__: never freed
             self._arena = torch.empty(size, dtype=torch.uint8, device=self.device)
             self._arena_off = 0
         off = self._arena_off
@@ -612,10 +628,13 @@ class HipBackend:
               lay.NC, F, lay.mode, _ptr(lay.perm), int(rowmajor), out.data_ptr(), _stream())
         return out
 
-    def adam(self, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay):
+    def adam(self, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, live=None):
         """``step``: int, or a device float tensor holding the (already
-        incremented) step count (capturable form)."""
+        incremented) step count (capturable form).  ``live``: optional device
+        uint8 mask; elements with 0 are skipped (parameters without a grad)."""
         self._chk(p, g, m, v)
+        if live is not None:
+            assert live.dtype == torch.uint8 and live.is_cuda and live.numel() == p.numel()
         if isinstance(step, torch.Tensor):
             if not step.is_cuda or step.dtype != torch.float32 or step.numel() != 1:
                 raise ValueError("a tensor step must be one float32 on the device")
@@ -624,4 +643,4 @@ class HipBackend:
             sval, sptr = int(step), None
         _call("pfsgnn_adam", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
               sval, sptr, float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
-              _stream())
+              _ptr(live), _stream())

@@ -40,6 +40,30 @@ class FusedAdam(torch.optim.Optimizer):
                         maximize=False, capturable=capturable)
         super().__init__(params, defaults)
         self._flat = {}
+        self._masks = {}
+
+    def _live_mask(self, gi, group, n):
+        """None if every parameter of the group got a gradient this step, else a
+        device uint8 mask over the flat buffer: torch.optim.Adam skips the
+        parameters whose .grad the reference leaves None (p._pf_live False,
+        set by pfsgnn.GNN's backward) -- which only changes the update when
+        weight_decay != 0 (zero grads with zero moments leave p unchanged)."""
+        if group["weight_decay"] == 0.0:
+            return None
+        live = tuple(bool(getattr(p, "_pf_live", True)) for p in group["params"])
+        if all(live):
+            return None
+        key = (gi, live)
+        m = self._masks.get(key)
+        if m is None:
+            host = torch.zeros(n, dtype=torch.uint8)
+            _, offs = _flat_base([p.detach() for p in group["params"]])
+            for p, off, on in zip(group["params"], offs, live):
+                if on:
+                    host[off:off + p.numel()] = 1
+            m = host.to(group["params"][0].device)
+            self._masks[key] = m
+        return m
 
     def _group_flat(self, gi, group):
         ps = group["params"]
@@ -85,21 +109,23 @@ class FusedAdam(torch.optim.Optimizer):
             flat = self._group_flat(gi, group)
             if flat is not None:
                 p, g, m, v = flat
+                live = self._live_mask(gi, group, p.numel())
                 st0 = self.state[group["params"][0]]
                 if group.get("capturable", False):
                     step_t = st0["step"]          # one device tensor shared by the group
                     step_t.add_(1.0)
                     be.adam(p, g, m, v, step_t, group["lr"], beta1, beta2, group["eps"],
-                            group["weight_decay"])
+                            group["weight_decay"], live=live)
                     continue
                 step = int(st0["step"]) + 1
                 be.adam(p, g, m, v, step, group["lr"], beta1, beta2, group["eps"],
-                        group["weight_decay"])
+                        group["weight_decay"], live=live)
                 for q in group["params"]:
                     self.state[q]["step"].fill_(float(step))
                 continue
             for q in group["params"]:
-                if q.grad is None:
+                if q.grad is None or (group["weight_decay"] != 0.0
+                                      and not getattr(q, "_pf_live", True)):
                     continue
                 st = self.state[q]
                 if "exp_avg" not in st:

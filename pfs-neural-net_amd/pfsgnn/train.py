@@ -46,14 +46,15 @@ def softfloor(x, sharpness=20, noiselevel=0.3):
 
 class _LossFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x_e, anchor, model, d, ectx, xe3, ci, sharpness, seed, pclass, pfiber,
-                want_time):
+    def forward(ctx, token, anchor, model, d, ectx, xe3, ci, sharpness, seed, pclass, pfiber,
+                want_time, noiselevel):
         eng = model._engine()
         P = model._flat_params()
         loss, diag, lctx = eng.loss_forward(P, d, xe3, ci, sharpness, seed, pclass=pclass,
                                             pfiber=pfiber, total_time=float(config.TOTAL_TIME),
                                             nfields=float(config.NFIELDS), wutils=config.wutils,
-                                            wvar=config.wvar, want_time=want_time)
+                                            wvar=config.wvar, want_time=want_time,
+                                            noiselevel=noiselevel)
         ctx.pf = (model, d, ectx, lctx)
         outs = (diag["utils"], diag["n_prime"], diag["fiber_time"], diag["variance"])
         ctx.mark_non_differentiable(*outs)
@@ -65,13 +66,14 @@ class _LossFn(torch.autograd.Function):
     def backward(ctx, g_loss, *unused):
         model, d, ectx, lctx = ctx.pf
         eng = model._engine()
-        P, Gr = model._flat_params(), model._flat_grads()
+        P, Gr = model._flat_params(), model._recording_grads()
         gc = eng.loss_backward(P, Gr, lctx, gscale=g_loss)
+        model._mark_live(Gr.used)
         # hand the canonical [F, E] gradient straight to the GNN's backward
-        # (gnn._GNNFn.backward); autograd sees a stride-0 zero placeholder
+        # (gnn._GNNFn.backward); the edge-state token gets a zero
         prev = ectx.get("g_xe_canonical")
         ectx["g_xe_canonical"] = gc if prev is None else prev + gc
-        return (gc.new_zeros(()).expand(d.E, d.F),) + (None,) * 11
+        return (gc.new_zeros(()),) + (None,) * 12
 
 
 def _class_info_cm(class_info, d):
@@ -82,7 +84,7 @@ def _class_info_cm(class_info, d):
 
 
 def loss_function(graph, class_info, pclass=0.1, pfiber=1.0, sharpness=0.5, finaloutput=False,
-                  *, gnn=None, seed=None):
+                  *, gnn=None, seed=None, noiselevel=0.3):
     """train.py:29-80.  ``graph`` is the output of ``GNN.forward``; ``class_info``
     is [NC, 2] (T_i, N_i) per class -- [G*NC, 2] for a batch of G graphs, whose
     loss is the sum of the per-graph losses.  The reference reads the model
@@ -91,12 +93,16 @@ def loss_function(graph, class_info, pclass=0.1, pfiber=1.0, sharpness=0.5, fina
     (train.py:94), on which train.py:40 and :67 rely.  ``seed`` (softfloor's
     noise): None draws one from torch's CPU generator; an int; or a device
     int64 tensor read in-kernel (a captured step then draws fresh noise per
-    replay when the tensor is advanced on the device)."""
-    pf = getattr(graph, "_pf", None)
-    if pf is None or pf[3] is not graph.x_e:
+    replay when the tensor is advanced on the device).  ``noiselevel`` is
+    softfloor's (train.py:21, fixed at 0.3 by the reference's call)."""
+    pf = graph.__dict__.get("_pf")
+    if pf is None or graph.__dict__.get("_pf_replaced"):
         raise NotImplementedError("loss_function needs the BipartiteData returned by "
                                   "pfsgnn.GNN.forward (the fused loss reads its edge state)")
-    model, d, lay, x_e, xe3, ectx = pf
+    model, d, lay, token, xe3, ectx = pf
+    if token is None:
+        raise NotImplementedError("loss_function needs a training-mode GNN.forward "
+                                  "(train.py:108 trains in train mode)")
     if gnn is not None and gnn is not model:
         raise ValueError("graph was produced by a different GNN than `gnn`")
     if not lay.fiber_major:
@@ -107,8 +113,8 @@ def loss_function(graph, class_info, pclass=0.1, pfiber=1.0, sharpness=0.5, fina
         seed = draw_seed()
     elif not isinstance(seed, torch.Tensor):
         seed = int(seed)
-    outs = _LossFn.apply(x_e, model.encoder_s[0].weight, model, d, ectx, xe3, ci, float(sharpness),
-                         seed, float(pclass), float(pfiber), bool(finaloutput))
+    outs = _LossFn.apply(token, model.encoder_s[0].weight, model, d, ectx, xe3, ci, float(sharpness),
+                         seed, float(pclass), float(pfiber), bool(finaloutput), float(noiselevel))
     loss, utils_g, n_prime, fiber_time, variance = outs[:5]
     if not finaloutput:
         return loss, utils_g.sum() if d.G > 1 else utils_g[0]

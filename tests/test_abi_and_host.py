@@ -87,3 +87,37 @@ def test_noise_reference_is_uniform():
     assert u.min() >= 0.0 and u.max() < 1.0
     assert abs(u.mean() - 0.5) < 0.005 and abs(u.var() - 1 / 12) < 0.002
     assert (uniform_numpy(7, 10) == u[:10]).all() and (uniform_numpy(8, 10) != u[:10]).any()
+
+
+def test_edge_grid_query_is_host_only(lib):
+    from pfsgnn import native
+    g = native.edge_grid(16, 2394, 128)
+    assert g == dict(KS=4, CPS=32, nblocks=2432, NFG=38)
+    assert native.edge_grid(256, 2394, 16)["KS"] == 1
+
+
+def test_tensor_cache_keys_on_object_not_address():
+    """A freed tensor's cache entry must never serve a new tensor, even one the
+    allocator places at the same address; in-place writes invalidate."""
+    import gc
+    from pfsgnn.gnn import _TensorCache
+    c = _TensorCache(4)
+    a = torch.zeros(1000)
+    c.put(a, ("k",), "A")
+    assert c.get(a, ("k",)) == "A"
+    assert c.get(a, ("other",)) is None
+    a.add_(1)                                    # bumps _version
+    assert c.get(a, ("k",)) is None
+    c.put(a, ("k",), "A2")
+    ptr = a.data_ptr()
+    del a
+    gc.collect()
+    for _ in range(50):                          # try to land on the same block
+        b = torch.zeros(1000)
+        if b.data_ptr() == ptr:
+            break
+    assert c.get(b, ("k",)) is None
+    for i in range(10):                          # capacity: dead entries purged first
+        t = torch.zeros(3)
+        c.put(t, (), i)
+    assert len(c.d) <= 4

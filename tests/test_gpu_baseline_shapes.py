@@ -1,0 +1,160 @@
+"""Parity and property checks at the BASELINE.json shapes (2394-fiber graphs).
+
+Oracle parity (full training step: GNN forward + train.py loss + backward +
+BatchNorm running statistics, the same ``check`` bar as test_gpu_parity):
+  * configs[1]: one complete 2394x16 graph, B=3 blocks (train.py:90-111 shape);
+  * the metric shape: a batch of G=2 complete 2394x128 graphs, B=8 blocks.
+
+Full-size properties (the oracle would take minutes at these sizes):
+  * configs[2]: a batch of 256 graphs of 2394x16, and the bench batch of 16
+    graphs of 2394x128 (B=8): finite outputs, a bitwise-repeatable step, and
+    -- with BatchNorm off, so the graphs of a batch do not interact -- batch
+    loss and parameter gradients equal to the sums over per-graph (G=1) runs.
+
+Code paths reached (asserted below through ``pfsgnn_edge_grid``, MFMA path):
+  * NF = 2394 = 37*64 + 26: every case has a partial 26-fiber tail group;
+  * 2394x128, G=2: KS = 26 class splits, 1976 blocks per edge kernel, so the
+    per-block weight-gradient partials take the two-stage (nb > 256)
+    in-place segment reduction (pfsgnn_node.hip k_reduce_seg);
+  * 2394x16, G=1: KS = 4, 152 blocks (single-stage reduction);
+  * 2394x16, G=256: KS = 1 (per-fiber outputs written directly), 9728 blocks;
+  * 2394x128, G=16 (the bench batch): KS = 4, 2432 blocks.
+"""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from harness import make_problem  # noqa: E402
+from test_gpu_parity import check, oracle_step, ours_step  # noqa: E402
+
+NF = 2394
+
+
+@pytest.fixture(params=["mfma", "valu"])
+def prec(request):
+    import pfsgnn
+    pfsgnn.set_edge_path(request.param)
+    yield request.param
+    pfsgnn.set_edge_path("mfma")
+
+
+def _grid(G, NC):
+    from pfsgnn import native
+    return native.edge_grid(G, NF, NC)
+
+
+@pytest.mark.parametrize("G,NC,B,sharp,grid", [
+    (1, 16, 3, 12.0, dict(KS=4, nblocks=152)),
+    (2, 128, 8, 10.0, dict(KS=26, nblocks=1976)),
+])
+def test_training_step_matches_oracle_at_baseline_shape(G, NC, B, sharp, grid, prec):
+    if prec == "mfma":
+        got = _grid(G, NC)
+        assert got["NFG"] == 38 and NF % 64 == 26
+        for k, v in grid.items():
+            assert got[k] == v, (k, got)
+    model, graph = make_problem(G, NF, NC, B=B, seed=100 + NC)
+    seed = 4242 + NC
+    m64, o64, l64 = oracle_step(model, graph, G, NF, NC, seed, sharp, torch.float64)
+    m32, o32, l32 = oracle_step(model, graph, G, NF, NC, seed, sharp, torch.float32)
+    gnn, out, loss = ours_step(model, graph, G, NF, NC, B, seed, sharp)
+    check("loss", loss, l64, l32)
+    check("x_e", out.x_e, o64.x_e, o32.x_e)
+    check("x_s", out.x_s, o64.x_s, o32.x_s)
+    check("x_t", out.x_t, o64.x_t, o32.x_t)
+    check("x_u", out.x_u, o64.x_u, o32.x_u)
+    p64, p32 = dict(m64.named_parameters()), dict(m32.named_parameters())
+    for name, p in gnn.named_parameters():
+        r64 = p64[name].grad if p64[name].grad is not None else torch.zeros_like(p64[name])
+        r32 = p32[name].grad if p32[name].grad is not None else torch.zeros_like(p32[name])
+        check("grad " + name, p.grad, r64, r32)
+    b64, b32 = m64.state_dict(), m32.state_dict()
+    for k, v in gnn.state_dict().items():
+        if "running" in k:
+            check(k, v.double(), b64[k].double(), b32[k].double())
+        elif "num_batches" in k:
+            assert int(v) == int(b64[k]), k
+
+
+def _synthetic(G, NC, seed, normed):
+    """bench.py-style batch: G train.py-shaped graphs (train.py:88-104)."""
+    import pfsgnn
+    gen = torch.Generator().manual_seed(seed)
+    Ti = torch.randint(2, 13, (G * NC, 1), generator=gen).float()
+    Ni = torch.randint(1000, 100000, (G * NC, 1), generator=gen).float()
+    ci = torch.cat([Ti, Ni], 1)
+    x_s = torch.arange(NF, dtype=torch.float).repeat(G).reshape(-1, 1)
+    e = torch.arange(G * NF * NC)
+    edge_index = torch.stack([e // NC, (e // (NF * NC)) * NC + e % NC])
+    x_e = 2.0 + 8.0 * torch.rand(G * NF * NC, 10, generator=gen)
+    x_u = torch.zeros(G, 10)
+    torch.manual_seed(seed)
+    gnn = pfsgnn.GNN(B=8, Fdim=10, T=NC, F_s=1, F_t=2, normed=normed).cuda()
+    return gnn, (edge_index, x_s, ci, x_e, x_u)
+
+
+def _run(gnn, parts, noiselevel=0.3):
+    import pfsgnn
+    from pfsgnn.train import loss_function
+    edge_index, x_s, ci, x_e, x_u = parts
+    data = pfsgnn.BipartiteData(edge_index, x_s, ci, x_e, x_u)
+    gnn.zero_grad()
+    out = gnn(data)
+    loss, _ = loss_function(out, ci.cuda(), pclass=0.1, pfiber=0.1, sharpness=10.0, seed=9,
+                            noiselevel=noiselevel)
+    loss.backward()
+    torch.cuda.synchronize()
+    grads = torch.cat([p.grad.reshape(-1) for p in gnn.parameters()]).clone()
+    return loss.detach().clone(), grads, out
+
+
+@pytest.mark.parametrize("G,NC,grid", [(256, 16, dict(KS=1, nblocks=9728)),
+                                       (16, 128, dict(KS=4, nblocks=2432))])
+def test_full_size_step_finite_and_repeatable(G, NC, grid):
+    import pfsgnn
+    pfsgnn.set_edge_path("mfma")
+    got = _grid(G, NC)
+    for k, v in grid.items():
+        assert got[k] == v, (k, got)
+    gnn, parts = _synthetic(G, NC, seed=7, normed=True)
+    sd = copy.deepcopy(gnn.state_dict())
+    l1, g1, out = _run(gnn, parts)
+    assert torch.isfinite(l1).item()
+    assert torch.isfinite(g1).all().item()
+    for t in (out.x_s, out.x_t, out.x_u):
+        assert torch.isfinite(t).all().item()
+    assert torch.isfinite(out.x_e).all().item()
+    gnn.load_state_dict(sd)
+    l2, g2, _ = _run(gnn, parts)
+    assert torch.equal(l1, l2)
+    assert torch.equal(g1, g2)
+
+
+@pytest.mark.parametrize("G,NC", [(256, 16), (16, 128)])
+def test_full_size_batch_decomposes_into_graphs(G, NC):
+    """normed=False: graphs of a batch share nothing but the parameters, so the
+    batch loss / gradients are the sums over each graph run alone (G=1).
+    softfloor's noise is keyed by the edge's position in the batch, so it is
+    switched off (noiselevel=0) for this property."""
+    import pfsgnn
+    pfsgnn.set_edge_path("mfma")
+    gnn, parts = _synthetic(G, NC, seed=11, normed=False)
+    lb, gb, _ = _run(gnn, parts, noiselevel=0.0)
+    edge_index, x_s, ci, x_e, x_u = parts
+    E1 = NF * NC
+    ls, gs = torch.zeros((), dtype=torch.float64, device="cuda"), torch.zeros_like(gb, dtype=torch.float64)
+    e = torch.arange(E1)
+    ei1 = torch.stack([e // NC, e % NC])
+    for g in range(G):
+        p1 = (ei1, x_s[g * NF:(g + 1) * NF], ci[g * NC:(g + 1) * NC], x_e[g * E1:(g + 1) * E1],
+              x_u[g:g + 1])
+        l1, g1, _ = _run(gnn, p1, noiselevel=0.0)
+        ls += l1.double()
+        gs += g1.double()
+    # fp32 sums in a different order: relative to the scale of each quantity
+    assert abs(lb.double().item() - ls.item()) <= 1e-4 * max(1.0, abs(ls.item())), (lb, ls)
+    err = (gb.double() - gs).abs().max().item()
+    assert err <= 1e-4 * gs.abs().max().item(), err
