@@ -118,15 +118,39 @@ def pmc_traffic(kernel, E, F):
     return None
 
 
+def cpu_share():
+    """CPUs this process may actually run on: os.cpu_count() capped by the
+    affinity mask and by a cgroup-v2 CPU quota (a container's share of a large
+    host).  Threads beyond the share oversubscribe it and slow torch's CPU
+    kernels down by orders of magnitude."""
+    host = os.cpu_count() or 1
+    n = host
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return host, n
+
+
 def cpu_baseline(blocks, seconds):
     """The CPU oracle (oracle/, torch on the host cores) timed on a bounded sample
     of the same workload: ONE 2394x128 graph, full training step incl. Adam."""
     from harness import make_problem
     from noise_ref import uniform_numpy
     from oracle.ref_train import loss_function as oracle_loss
-    # train.py:15-19: the reference runs on every host core os.cpu_count() reports
-    threads = os.cpu_count() or 1
+    # train.py:15-19 sets torch's threads to os.cpu_count(); on a container
+    # share of a large host that count is the host's, so the threads are capped
+    # at the CPUs this process may use (both numbers are reported)
+    host, threads = cpu_share()
     torch.set_num_threads(threads)
+    print(f"[bench] cpu baseline: {threads} threads (os.cpu_count() = {host})",
+          file=sys.stderr, flush=True)
     model, graph = make_problem(1, NF, NC, B=blocks, seed=0, dtype=torch.float32)
     model.train()
     opt = torch.optim.Adam(model.parameters(), lr=5e-4)
@@ -141,17 +165,14 @@ def cpu_baseline(blocks, seconds):
         opt.step()
         steps += 1
         el = time.perf_counter() - t0
+        print(f"[bench] cpu baseline step {steps}: {el:.1f}s", file=sys.stderr, flush=True)
         if el >= seconds or steps >= 50:
             break
-    try:
-        share = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        share = threads
     return {"value": steps * NF * NC / el, "unit": "edges/s", "cores": threads, "kind": "port",
+            "host_cpus": host,
             "sample": f"{steps} training step(s) of one {NF}x{NC} graph, {blocks} blocks, "
-                      f"oracle/ (torch CPU fp32, {threads} threads = os.cpu_count() as "
-                      f"train.py:15-19 sets; {share} CPUs in this process's affinity mask), "
-                      f"{el:.1f}s"}
+                      f"oracle/ (torch CPU fp32, {threads} threads: os.cpu_count() = {host} as "
+                      f"train.py:15-19 sets, capped at this process's CPU share), {el:.1f}s"}
 
 
 def main():
@@ -251,6 +272,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if rank == 0:
+        print(f"[bench] {args.steps} timed steps: {elapsed:.2f}s", file=sys.stderr, flush=True)
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -101,8 +101,11 @@ def loss_function(graph, class_info, pclass=0.1, pfiber=1.0, sharpness=0.5, fina
                                   "pfsgnn.GNN.forward (the fused loss reads its edge state)")
     model, d, lay, token, xe3, ectx = pf
     if token is None:
-        raise NotImplementedError("loss_function needs a training-mode GNN.forward "
-                                  "(train.py:108 trains in train mode)")
+        # eval-mode forward: the loss is inference-only (no backward through it)
+        if torch.is_grad_enabled():
+            raise NotImplementedError("loss_function on an eval-mode GNN.forward runs under "
+                                      "torch.no_grad() only (train.py:108 trains in train mode)")
+        token = xe3[0].new_zeros(())
     if gnn is not None and gnn is not model:
         raise ValueError("graph was produced by a different GNN than `gnn`")
     if not lay.fiber_major:

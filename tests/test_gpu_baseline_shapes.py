@@ -79,7 +79,7 @@ def test_training_step_matches_oracle_at_baseline_shape(G, NC, B, sharp, grid, p
             assert int(v) == int(b64[k]), k
 
 
-def _synthetic(G, NC, seed, normed):
+def _synthetic(G, NC, seed, normed, B=8):
     """bench.py-style batch: G train.py-shaped graphs (train.py:88-104)."""
     import pfsgnn
     gen = torch.Generator().manual_seed(seed)
@@ -92,7 +92,7 @@ def _synthetic(G, NC, seed, normed):
     x_e = 2.0 + 8.0 * torch.rand(G * NF * NC, 10, generator=gen)
     x_u = torch.zeros(G, 10)
     torch.manual_seed(seed)
-    gnn = pfsgnn.GNN(B=8, Fdim=10, T=NC, F_s=1, F_t=2, normed=normed).cuda()
+    gnn = pfsgnn.GNN(B=B, Fdim=10, T=NC, F_s=1, F_t=2, normed=normed).cuda()
     return gnn, (edge_index, x_s, ci, x_e, x_u)
 
 
@@ -138,11 +138,15 @@ def test_full_size_batch_decomposes_into_graphs(G, NC):
     """normed=False: graphs of a batch share nothing but the parameters, so the
     batch loss / gradients are the sums over each graph run alone (G=1).
     softfloor's noise is keyed by the edge's position in the batch, so it is
-    switched off (noiselevel=0) for this property."""
+    switched off (noiselevel=0) for this property.  Without normalisation the
+    activations grow by orders of magnitude per block (x_t reaches ~1e9 after 8
+    blocks on these inputs, and the fp32 kurtosis overflows in the reference's
+    arithmetic as well), so the unnormalised stack here is B=2 blocks deep."""
     import pfsgnn
     pfsgnn.set_edge_path("mfma")
-    gnn, parts = _synthetic(G, NC, seed=11, normed=False)
+    gnn, parts = _synthetic(G, NC, seed=11, normed=False, B=2)
     lb, gb, _ = _run(gnn, parts, noiselevel=0.0)
+    assert torch.isfinite(lb).item() and torch.isfinite(gb).all().item()
     edge_index, x_s, ci, x_e, x_u = parts
     E1 = NF * NC
     ls, gs = torch.zeros((), dtype=torch.float64, device="cuda"), torch.zeros_like(gb, dtype=torch.float64)
@@ -152,6 +156,7 @@ def test_full_size_batch_decomposes_into_graphs(G, NC):
         p1 = (ei1, x_s[g * NF:(g + 1) * NF], ci[g * NC:(g + 1) * NC], x_e[g * E1:(g + 1) * E1],
               x_u[g:g + 1])
         l1, g1, _ = _run(gnn, p1, noiselevel=0.0)
+        assert torch.isfinite(g1).all().item(), g
         ls += l1.double()
         gs += g1.double()
     # fp32 sums in a different order: relative to the scale of each quantity

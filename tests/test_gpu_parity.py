@@ -66,10 +66,10 @@ def oracle_step(model, graph, G, NF, NC, seed, sharp, dtype):
     return m, out, loss
 
 
-def ours_step(model, graph, G, NF, NC, B, seed, sharp):
+def ours_step(model, graph, G, NF, NC, B, seed, sharp, normed=True):
     import pfsgnn
     from pfsgnn.train import loss_function
-    gnn = pfsgnn.GNN(B=B, Fdim=10, T=12, F_s=1, F_t=2).cuda()
+    gnn = pfsgnn.GNN(B=B, Fdim=10, T=12, F_s=1, F_t=2, normed=normed).cuda()
     gnn.load_state_dict({k: v.float() for k, v in model.state_dict().items()})
     gnn.train()
     data = pfsgnn.BipartiteData(graph.edge_index, graph.x_s.float(), graph.x_t.float(), graph.x_e.float(),
@@ -82,14 +82,17 @@ def ours_step(model, graph, G, NF, NC, B, seed, sharp):
     return gnn, out, loss
 
 
-@pytest.mark.parametrize("G,NF,NC,B,sharp", [(1, 40, 12, 2, 12.0), (2, 24, 16, 2, 5.0),
-                                              (1, 16, 128, 1, 20.0), (3, 10, 7, 3, 0.0)])
-def test_gnn_training_step_matches_oracle(G, NF, NC, B, sharp):
-    model, graph = make_problem(G, NF, NC, B=B, seed=G + NF + NC)
+@pytest.mark.parametrize("G,NF,NC,B,sharp,normed", [
+    (1, 40, 12, 2, 12.0, True), (2, 24, 16, 2, 5.0, True), (1, 16, 128, 1, 20.0, True),
+    (3, 10, 7, 3, 0.0, True),
+    # GNN(normed=False): every norm is the identity (gnn.py:84/121/173/206)
+    (2, 24, 16, 2, 5.0, False), (1, 70, 16, 3, 10.0, False)])
+def test_gnn_training_step_matches_oracle(G, NF, NC, B, sharp, normed):
+    model, graph = make_problem(G, NF, NC, B=B, seed=G + NF + NC, normed=normed)
     seed = 777 + NC
     m64, o64, l64 = oracle_step(model, graph, G, NF, NC, seed, sharp, torch.float64)
     m32, o32, l32 = oracle_step(model, graph, G, NF, NC, seed, sharp, torch.float32)
-    gnn, out, loss = ours_step(model, graph, G, NF, NC, B, seed, sharp)
+    gnn, out, loss = ours_step(model, graph, G, NF, NC, B, seed, sharp, normed=normed)
     check("loss", loss, l64, l32)
     check("x_e", out.x_e, o64.x_e, o32.x_e)
     check("x_s", out.x_s, o64.x_s, o32.x_s)
