@@ -141,8 +141,47 @@ int pfsgnn_bn_bwd(const float* dY, const float* X, const float* mu, const float*
                   const float* gamma, float eps, int C, int N,
                   float* dX, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
                   void* stream);
+/* Fused node MLP (gnn.py:65-71: Linear -> LeakyReLU(0.1) -> Linear) over N
+ * nodes, optionally followed by a training-mode BatchNorm1d (SModel gnn.py:154,
+ * TModel gnn.py:192):
+ *   Z  = W1 . cat(segs) + b1      [H][N] pre-activation (saved for backward; may be NULL)
+ *   Yp = W2 . lrelu(Z) + b2       [O][N]
+ *   gamma != NULL: Y = BatchNorm1d(Yp) (biased var), mu/var [O] out, running stats
+ *                  rm/rv (may be NULL) updated with the unbiased variance.
+ * The blocks of `segs` must cover weight columns 0..K in order (col = running
+ * row offset).  K, H <= 112; O <= 16.  Two launches with BatchNorm, one without.
+ * ws >= pfsgnn_mlp_ws_bytes(N).  Replaces the reference's MLP.forward +
+ * BatchNorm1d.forward (gnn.py:69-71, 154, 192, 223, 297-298). */
+size_t pfsgnn_mlp_ws_bytes(int N);
+int pfsgnn_mlp_fwd(const pfsgnn_seg* segs, int nseg, int N, const float* W1, int ldw1, int H,
+                   const float* b1, const float* W2, int O, const float* b2, float* Z, float* Yp,
+                   const float* gamma, const float* beta, float* rm, float* rv, float momentum,
+                   float eps, float* Y, float* mu, float* var, void* ws, size_t ws_bytes,
+                   void* stream);
+/* One row block of an input-gradient output: rows `rows` of dX go to x
+ * ([rows][N], overwritten, or accumulated when add != 0); x == NULL drops them. */
+typedef struct {
+  float* x;
+  int rows;
+  int add;
+} pfsgnn_oseg;
+/* Its backward (autograd of the same modules, train.py:140), input side:
+ *   gamma != NULL: dYp = BatchNorm1d backward of dY (dgamma += sum dY*xhat,
+ *                  dbeta += sum dY), written to dYp [O][N];  else dYp := dY;
+ *   dZ = (W2^T dYp) * lrelu'(Z)   written to dZ [H][N];
+ *   dX = W1^T dZ                  into the `outs` blocks (covering K rows; nout = 0 skips dX).
+ * The weight gradients are pfsgnn_wgrad(dYp, Z, act_in=1) and
+ * pfsgnn_wgrad_cat(dZ, segs) (deferred-reduction friendly).                   */
+int pfsgnn_mlp_bwd(const float* dY, int N, const float* Yp, const float* mu, const float* var,
+                   const float* gamma, float eps, float* dgamma, float* dbeta, const float* Z,
+                   const float* W1, int ldw1, int H, int K, const float* W2, int O, float* dYp,
+                   float* dZ, const pfsgnn_oseg* outs, int nout, void* ws, size_t ws_bytes,
+                   void* stream);
 /* out[c][g] = sum (or mean) over the n nodes of graph g of X[c][g*n + i] */
 int pfsgnn_graph_reduce(const float* X, int C, int G, int n, int mean, float* out, void* stream);
+/* the same, accumulated: out[c][g] += sum (or mean) ... (u[batch] gradients, gnn.py:100/153/191) */
+int pfsgnn_graph_reduce_add(const float* X, int C, int G, int n, int mean, float* out,
+                            void* stream);
 /* out[c][g*n + i] += scale * src[c][g] */
 int pfsgnn_graph_bcast_add(float* out, int C, int G, int n, const float* src, float scale,
                            void* stream);

@@ -1,0 +1,761 @@
+// pfsgnn_mlp.hip -- fused node-level MLPs (gnn.py:65-71, Linear -> LeakyReLU(0.1)
+// -> Linear) with the BatchNorm1d that follows them in SModel / TModel
+// (gnn.py:154, 192), on v_mfma_f32_16x16x4_f32 (exact fp32 products).
+//
+// Forward  (pfsgnn_mlp_fwd): Z = W1 cat(X) + b1, Yp = W2 lrelu(Z) + b2, Welford
+//   partials of Yp per block; then one launch finishes the BatchNorm statistics
+//   (every block merges the partials in the same fixed order) and writes
+//   Y = BN(Yp).  Two launches for what was lin_cat + lin + stats + finalize + apply.
+// Backward (pfsgnn_mlp_bwd): BatchNorm sums (one launch), then per node
+//   dYp = BN'(dY), dZ = (W2^T dYp) * lrelu'(Z), dX = W1^T dZ written (or added)
+//   straight into the caller's gradient blocks.  The weight gradients stay
+//   pfsgnn_wgrad(_cat) calls on (dYp, lrelu Z) and (dZ, X).
+//
+// Geometry.  Node n is the MFMA column; a wave owns 16 nodes, a block 64 per
+// chunk and walks chunks grid-stride (persistent), so the weights are staged
+// in LDS once per block.  All widths are padded to M tiles of 16 (K, H <= 16M,
+// O <= 16).  Layer chaining needs no data movement: the D layout of a tile
+// (lane group q holds rows 16t + 4q + r in register r) is the B operand of the
+// next layer's K-step (t, r), whose A operand is the permuted weight image.
+#include "pfsgnn_common.h"
+#include "../../include/pfsgnn.h"
+
+#include <algorithm>
+#include <climits>
+
+namespace {
+
+constexpr int NM_SEG = 4;
+
+// concatenated input rows (gnn.py:153 [x, mean, std, skew, kurt, u[batch]] etc.)
+struct InSegs {
+  const float* p[NM_SEG];
+  int k0[NM_SEG + 1];  // first row of each block; INT_MAX past the last
+  int pg[NM_SEG];      // 1: per-graph block [rows][Gc], node n reads column n / npg
+  int npg, Gc;
+};
+
+// gradient output rows: block s covers rows [k0[s], k0[s+1]); p == nullptr drops them
+struct OutSegs {
+  float* p[NM_SEG];
+  int k0[NM_SEG + 1];
+  int add[NM_SEG];
+};
+
+// Address of row k of the concatenated input at node n (k wave-uniform: the
+// block selection is scalar, the node offset per lane)
+__device__ __forceinline__ const float* in_ptr(const InSegs& S, int k, int n, int ng, int N) {
+  const float* p = S.p[0];
+  int kb = 0, pg = S.pg[0];
+  if (k >= S.k0[1]) { p = S.p[1]; kb = S.k0[1]; pg = S.pg[1]; }
+  if (k >= S.k0[2]) { p = S.p[2]; kb = S.k0[2]; pg = S.pg[2]; }
+  if (k >= S.k0[3]) { p = S.p[3]; kb = S.k0[3]; pg = S.pg[3]; }
+  return pg ? p + (size_t)(k - kb) * S.Gc + ng : p + (size_t)(k - kb) * N + n;
+}
+
+// async global -> LDS copy of one float per lane: LDS row base (wave-uniform)
+// + 4*lane, no VGPR destination (global_load_lds_dword)
+__device__ __forceinline__ void glds4(const float* src, float* lds_row) {
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_row, 4, 0, 0);
+}
+
+// Row k of the input gradient for the 64 nodes of a chunk (k wave-uniform)
+__device__ __forceinline__ void out_row(const OutSegs& S, int k, int n, int N, float v) {
+  float* p = S.p[0];
+  int kb = 0, add = S.add[0];
+  if (k >= S.k0[1]) { p = S.p[1]; kb = S.k0[1]; add = S.add[1]; }
+  if (k >= S.k0[2]) { p = S.p[2]; kb = S.k0[2]; add = S.add[2]; }
+  if (k >= S.k0[3]) { p = S.p[3]; kb = S.k0[3]; add = S.add[3]; }
+  if (!p) return;
+  float* q = p + (size_t)(k - kb) * N + n;
+  *q = add ? *q + v : v;
+}
+
+// node tables of a chunk staged in LDS as [row][XS_LD]: a wave's 16-node
+// column block for rows k = 4s + q puts lane groups q = 0..3 on disjoint
+// 16-bank ranges (stride 80 = 16 mod 32)
+constexpr int XS_LD = 80;
+
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+constexpr int PART_LEN = 33;  // BN forward partial: count, mean[16], M2[16]
+
+// ============================================================ forward
+template <int M>
+__global__ __launch_bounds__(256, (M <= 3 ? 2 : 1)) void k_mlp_fwd(InSegs S, int K, int N,
+                                                    const float* __restrict__ W1, int ldw1, int H,
+                                                    const float* __restrict__ b1,
+                                                    const float* __restrict__ W2, int O,
+                                                    const float* __restrict__ b2,
+                                                    float* __restrict__ Z, float* __restrict__ Yp,
+                                                    float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  floatx4* A1 = reinterpret_cast<floatx4*>(sm);  // [M][M][64]: W1 per (tile, 4 K-steps)
+  floatx4* A2 = A1 + M * M * 64;                 // [M][64]: W2 per hidden tile
+  float* B1 = reinterpret_cast<float*>(A2 + M * 64);
+  float* B2 = B1 + 16 * M;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, col = lane & 15, kq = lane >> 4;
+  {  // weight images: every load of the thread in flight at once (a load ->
+     // store loop would pay one L2 round trip per element)
+    float v[M * M], w[M];
+#pragma unroll
+    for (int i = 0; i < M * M; ++i) {
+      const int idx = t + 256 * i;
+      const int j = idx & 3, l = (idx >> 2) & 63, q = (idx >> 8) % M, mt = (idx >> 8) / M;
+      const int row = 16 * mt + (l & 15), k = 4 * (4 * q + j) + (l >> 4);
+      v[i] = (row < H && k < K) ? W1[(size_t)row * ldw1 + k] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const int idx = t + 256 * i;
+      const int r = idx & 3, l = (idx >> 2) & 63, mt = idx >> 8;
+      const int o = l & 15, h = 16 * mt + 4 * (l >> 4) + r;
+      w[i] = (o < O && h < H) ? W2[(size_t)o * H + h] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < M * M; ++i) sm[t + 256 * i] = v[i];
+#pragma unroll
+    for (int i = 0; i < M; ++i) reinterpret_cast<float*>(A2)[t + 256 * i] = w[i];
+  }
+  for (int i = t; i < 16 * M; i += 256) B1[i] = i < H ? b1[i] : 0.f;
+  if (t < 16) B2[t] = t < O ? b2[t] : 0.f;
+
+  // chunk input rows [16M][XS_LD], double-buffered: chunk c+1 streams in with
+  // global_load_lds while chunk c is multiplied (rows >= K stay zero)
+  float* Xs0 = B2 + 16;
+  constexpr int XSZ = 16 * M * XS_LD;
+  for (int i = t; i < 2 * XSZ; i += 256) Xs0[i] = 0.f;
+  const int nch = (N + 63) / 64;
+  const int wu = __builtin_amdgcn_readfirstlane(wave);
+  auto issue = [&](int ch, int buf) {
+    const int n = ch * 64 + lane;
+    const int nc = n < N ? n : N - 1;
+    const int ng = S.npg ? nc / S.npg : 0;
+    float* dst = Xs0 + buf * XSZ;
+    for (int k = wu; k < K; k += 4) glds4(in_ptr(S, k, nc, ng, N), dst + k * XS_LD);
+  };
+  float cnt = 0.f, mean[4] = {0.f, 0.f, 0.f, 0.f}, m2[4] = {0.f, 0.f, 0.f, 0.f};
+  if ((int)blockIdx.x < nch) {
+    __syncthreads();                               // zero fill before the first copy
+    issue(blockIdx.x, 0);
+  }
+  int it = 0;
+  for (int ch = blockIdx.x; ch < nch; ch += gridDim.x, ++it) {
+    const int buf = it & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of chunk ch landed
+    __syncthreads();                                    // ... and every other wave's
+    if (ch + (int)gridDim.x < nch) issue(ch + gridDim.x, buf ^ 1);
+    const float* Xs = Xs0 + buf * XSZ;
+    const int n = ch * 64 + wave * 16 + col;
+    const bool nv = n < N;
+    // the weight images are re-read from LDS every chunk: an opaque offset keeps
+    // the compiler from hoisting M*M float4 loop invariants into registers
+    int lo = 0;
+    asm volatile("" : "+v"(lo));
+    const floatx4* A1c = A1 + lo;
+    const floatx4* A2c = A2 + lo;
+    const float* xr = Xs + lo + kq * XS_LD + wave * 16 + col;
+    floatx4 acc[M];
+#pragma unroll
+    for (int mt = 0; mt < M; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // K-step group q: its M weight float4s and 4 input values are read first
+    // (the next group's reads are issued before this group's MFMAs), and the
+    // MFMAs run across the M independent accumulators (no dependent back-to-back)
+    floatx4 an[M];
+    float xn[4];
+#pragma unroll
+    for (int mt = 0; mt < M; ++mt) an[mt] = A1c[mt * M * 64 + lane];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xn[j] = xr[(4 * j) * XS_LD];
+#pragma unroll
+    for (int q = 0; q < M; ++q) {
+      floatx4 a[M];
+      float x[4];
+#pragma unroll
+      for (int mt = 0; mt < M; ++mt) a[mt] = an[mt];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = xn[j];
+      if (q + 1 < M) {
+#pragma unroll
+        for (int mt = 0; mt < M; ++mt) an[mt] = A1c[(mt * M + q + 1) * 64 + lane];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xn[j] = xr[(4 * (4 * (q + 1) + j)) * XS_LD];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int mt = 0; mt < M; ++mt) acc[mt] = mfma4(a[mt][j], x[j], acc[mt]);
+    }
+    floatx4 ye = floatx4{0.f, 0.f, 0.f, 0.f}, yo = ye;
+    floatx4 act[M], w2[M];
+#pragma unroll
+    for (int mt = 0; mt < M; ++mt) {
+      w2[mt] = A2c[mt * 64 + lane];
+      const floatx4 bb = *reinterpret_cast<const floatx4*>(B1 + 16 * mt + 4 * kq);
+      const floatx4 z = acc[mt] + bb;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int h = 16 * mt + 4 * kq + r;
+        if (Z && nv && h < H) Z[(size_t)h * N + n] = z[r];
+        act[mt][r] = lrelu(z[r]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int mt = 0; mt < M; ++mt) {
+        floatx4& y = (mt & 1) ? yo : ye;
+        y = mfma4(w2[mt][r], act[mt][r], y);
+      }
+    const floatx4 bo = *reinterpret_cast<const floatx4*>(B2 + 4 * kq);
+    const floatx4 y = ye + yo + bo;
+    if (nv) {
+      cnt += 1.f;
+      const float rc = 1.f / cnt;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = 4 * kq + r;
+        if (o < O) {
+          Yp[(size_t)o * N + n] = y[r];
+          const float d = y[r] - mean[r];
+          mean[r] = fmaf(d, rc, mean[r]);
+          m2[r] = fmaf(d, y[r] - mean[r], m2[r]);
+        }
+      }
+    }
+  }
+  if (!part) return;
+  // Chan merge over the 16 nodes of each lane group, then over the 4 waves
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) {
+    const float cb = __shfl_xor(cnt, off);
+    const float tot = cnt + cb;
+    const float wb = tot > 0.f ? cb / tot : 0.f;
+    const float wab = tot > 0.f ? cnt * cb / tot : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float mb = __shfl_xor(mean[r], off), qb = __shfl_xor(m2[r], off);
+      const float d = mb - mean[r];
+      mean[r] = fmaf(d, wb, mean[r]);
+      m2[r] = m2[r] + qb + d * d * wab;
+    }
+    cnt = tot;
+  }
+  __shared__ float shm[4][PART_LEN];
+  __syncthreads();
+  if (col == 0) {
+    if (kq == 0) shm[wave][0] = cnt;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      shm[wave][1 + 4 * kq + r] = mean[r];
+      shm[wave][17 + 4 * kq + r] = m2[r];
+    }
+  }
+  __syncthreads();
+  if (t < 16) {
+    float C0 = shm[0][0], M0 = shm[0][1 + t], Q0 = shm[0][17 + t];
+    for (int w = 1; w < 4; ++w) {
+      const float cb = shm[w][0], mb = shm[w][1 + t], qb = shm[w][17 + t];
+      const float tot = C0 + cb;
+      if (tot > 0.f) {
+        const float d = mb - M0;
+        M0 = M0 + d * (cb / tot);
+        Q0 = Q0 + qb + d * d * (C0 * cb / tot);
+      }
+      C0 = tot;
+    }
+    float* p = part + (size_t)blockIdx.x * PART_LEN;
+    if (t == 0) p[0] = C0;
+    p[1 + t] = M0;
+    p[17 + t] = Q0;
+  }
+}
+
+// BatchNorm1d training forward from the MLP's per-block partials: every block
+// merges them in the same fixed order (double), block 0 writes mu / var and
+// updates the running statistics (unbiased variance), all apply the norm.
+__global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__ part, int nb,
+                                                       int O, int N, const float* __restrict__ Yp,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float eps,
+                                                       float* __restrict__ rm,
+                                                       float* __restrict__ rv, float momentum,
+                                                       float* __restrict__ Y,
+                                                       float* __restrict__ mu,
+                                                       float* __restrict__ var) {
+  __shared__ double acc[16][16][3];
+  __shared__ float cf[4][16];
+  const int t = threadIdx.x, c = t & 15, u = t >> 4;
+  double C0 = 0.0, M0 = 0.0, Q0 = 0.0;
+  constexpr int PB = 32;  // partials per thread: nb <= 512 (the MLP grid)
+  float pc[PB], pm[PB], pq[PB];
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {  // every load in flight before the merge chain
+    const int b = u + 16 * i;
+    const float* p = part + (size_t)(b < nb ? b : 0) * PART_LEN;
+    pc[i] = b < nb ? p[0] : 0.f;
+    pm[i] = b < nb ? p[1 + c] : 0.f;
+    pq[i] = b < nb ? p[17 + c] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const double cb = pc[i], mb = pm[i], qb = pq[i];
+    const double tot = C0 + cb;
+    if (tot > 0.0) {
+      const double d = mb - M0;
+      M0 += d * (cb / tot);
+      Q0 += qb + d * d * (C0 * cb / tot);
+    }
+    C0 = tot;
+  }
+  acc[u][c][0] = C0;
+  acc[u][c][1] = M0;
+  acc[u][c][2] = Q0;
+  __syncthreads();
+  if (t < 16) {
+    double Cc = 0.0, Mc = 0.0, Qc = 0.0;
+    for (int s = 0; s < 16; ++s) {
+      const double cb = acc[s][t][0], mb = acc[s][t][1], qb = acc[s][t][2];
+      const double tot = Cc + cb;
+      if (tot > 0.0) {
+        const double d = mb - Mc;
+        Mc += d * (cb / tot);
+        Qc += qb + d * d * (Cc * cb / tot);
+      }
+      Cc = tot;
+    }
+    const double v = Qc / (double)N;
+    const float muf = (float)Mc, vf = (float)v;
+    const bool live = t < O;
+    cf[0][t] = muf;
+    cf[1][t] = 1.0f / sqrtf(vf + eps);
+    cf[2][t] = live ? gamma[t] : 0.f;
+    cf[3][t] = live ? beta[t] : 0.f;
+    if (blockIdx.x == 0 && live) {
+      mu[t] = muf;
+      var[t] = vf;
+      if (rm) {
+        const double unb = N > 1 ? Qc / (double)(N - 1) : v;
+        rm[t] = (float)((1.0 - momentum) * rm[t] + momentum * Mc);
+        rv[t] = (float)((1.0 - momentum) * rv[t] + momentum * unb);
+      }
+    }
+  }
+  __syncthreads();
+  const size_t tot = (size_t)O * N;
+  for (size_t i = (size_t)blockIdx.x * 256 + t; i < tot; i += (size_t)gridDim.x * 256) {
+    const int o = (int)(i / (size_t)N);
+    Y[i] = (Yp[i] - cf[0][o]) * cf[1][o] * cf[2][o] + cf[3][o];
+  }
+}
+
+// ============================================================ backward
+// BatchNorm backward sums per block: Sg[c] = sum dY, Sgx[c] = sum dY * xhat.
+constexpr int SUM_LEN = 32;
+__global__ __launch_bounds__(256) void k_bn_sums_part(const float* __restrict__ dY,
+                                                      const float* __restrict__ Yp, int O, int N,
+                                                      const float* __restrict__ mu,
+                                                      const float* __restrict__ var, float eps,
+                                                      float* __restrict__ part) {
+  const int t = threadIdx.x;
+  float sg[16], sx[16], mc[16], ic[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    sg[c] = sx[c] = 0.f;
+    mc[c] = c < O ? mu[c] : 0.f;
+    ic[c] = c < O ? 1.0f / sqrtf(var[c] + eps) : 0.f;
+  }
+  for (int n = blockIdx.x * 256 + t; n < N; n += gridDim.x * 256) {
+    float g[16], y[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      g[c] = c < O ? dY[(size_t)c * N + n] : 0.f;
+      y[c] = c < O ? Yp[(size_t)c * N + n] : 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      sg[c] += g[c];
+      sx[c] += g[c] * ((y[c] - mc[c]) * ic[c]);
+    }
+  }
+  __shared__ float scratch[4 * 32];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    sg[c] = wave_sum(sg[c]);
+    sx[c] = wave_sum(sx[c]);
+  }
+  const int wave = t >> 6, lane = t & 63;
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      scratch[wave * 32 + c] = sg[c];
+      scratch[wave * 32 + 16 + c] = sx[c];
+    }
+  }
+  __syncthreads();
+  if (t < 32)
+    part[(size_t)blockIdx.x * SUM_LEN + t] =
+        ((scratch[t] + scratch[32 + t]) + scratch[64 + t]) + scratch[96 + t];
+}
+
+template <int M>
+__global__ __launch_bounds__(256, (M <= 3 ? 2 : 1)) void k_mlp_bwd(
+    int K, int N, int H, int O, const float* __restrict__ dY, const float* __restrict__ Yp,
+    const float* __restrict__ spart, int nsp, const float* __restrict__ mu,
+    const float* __restrict__ var, const float* __restrict__ gamma, float eps,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, const float* __restrict__ Z,
+    const float* __restrict__ W1, int ldw1, const float* __restrict__ W2,
+    float* __restrict__ dYp, float* __restrict__ dZ, OutSegs outs, int want_dx) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  floatx4* T2 = reinterpret_cast<floatx4*>(sm);  // [M][64]: W2^T per hidden tile
+  floatx4* T1 = T2 + M * 64;                     // [M][M][64]: W1^T per (input tile, hidden tile)
+  float* BC = reinterpret_cast<float*>(T1 + M * M * 64);  // [5][16] BN backward coefficients
+  float* DXs = BC + 80;                                     // [16M][XS_LD] chunk input gradient
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, col = lane & 15, kq = lane >> 4;
+  {  // weight images, all loads in flight at once (see k_mlp_fwd)
+    float w[M], v[M * M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const int idx = t + 256 * i;
+      const int r = idx & 3, l = (idx >> 2) & 63, mt = idx >> 8;
+      const int o = 4 * (l >> 4) + r, h = 16 * mt + (l & 15);
+      w[i] = (o < O && h < H) ? W2[(size_t)o * H + h] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < M * M; ++i) {
+      const int idx = t + 256 * i;
+      const int r = idx & 3, l = (idx >> 2) & 63, mt = (idx >> 8) % M, mk = (idx >> 8) / M;
+      const int h = 16 * mt + 4 * (l >> 4) + r, k = 16 * mk + (l & 15);
+      v[i] = (want_dx && h < H && k < K) ? W1[(size_t)h * ldw1 + k] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i) sm[t + 256 * i] = w[i];
+    float* t1 = reinterpret_cast<float*>(T1);
+#pragma unroll
+    for (int i = 0; i < M * M; ++i) t1[t + 256 * i] = v[i];
+  }
+  const bool bn = spart != nullptr;
+  if (bn) {
+    __shared__ float ss[16][SUM_LEN];
+    const int c = t & 31, u = t >> 5;  // 8 subsets of the partial list per sum
+    float v[32];  // nsp <= 256: every load in flight, then a fixed-order sum
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int b = u + 8 * i;
+      v[i] = b < nsp ? spart[(size_t)b * SUM_LEN + c] : 0.f;
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) s += v[i];
+    ss[u][c] = s;
+    __syncthreads();
+    if (t < 16) {
+      float sg = 0.f, sx = 0.f;
+      for (int i = 0; i < 8; ++i) {
+        sg += ss[i][t];
+        sx += ss[i][16 + t];
+      }
+      const bool live = t < O;
+      const float inv = live ? 1.0f / sqrtf(var[t] + eps) : 0.f;
+      BC[t] = live ? gamma[t] * inv : 0.f;       // gi
+      BC[16 + t] = sg / (float)N;                // k0
+      BC[32 + t] = sx / (float)N;                // k1
+      BC[48 + t] = live ? mu[t] : 0.f;
+      BC[64 + t] = inv;
+      if (blockIdx.x == 0 && live) {
+        dgamma[t] += sx;
+        dbeta[t] += sg;
+      }
+    }
+  }
+  __syncthreads();
+  float gi[4], k0[4], k1[4], mm[4], iv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int o = 4 * kq + r;
+    gi[r] = bn ? BC[o] : 1.f;
+    k0[r] = bn ? BC[16 + o] : 0.f;
+    k1[r] = bn ? BC[32 + o] : 0.f;
+    mm[r] = bn ? BC[48 + o] : 0.f;
+    iv[r] = bn ? BC[64 + o] : 0.f;
+  }
+
+  const int nch = (N + 63) / 64;
+  const int wu = __builtin_amdgcn_readfirstlane(wave);
+  float gv[4], yv[4], zv[4 * M];
+  auto load = [&](int ch) {
+    const int n = ch * 64 + wave * 16 + col;
+    const bool nv = n < N;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = 4 * kq + r;
+      gv[r] = (nv && o < O) ? dY[(size_t)o * N + n] : 0.f;
+      yv[r] = (bn && nv && o < O) ? Yp[(size_t)o * N + n] : 0.f;
+    }
+#pragma unroll
+    for (int mt = 0; mt < M; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int h = 16 * mt + 4 * kq + r;
+        zv[4 * mt + r] = (nv && h < H) ? Z[(size_t)h * N + n] : 0.f;
+      }
+  };
+  int ch = blockIdx.x;
+  if (ch < nch) load(ch);
+  for (; ch < nch; ch += gridDim.x) {
+    float g[4], y[4], z[4 * M];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { g[r] = gv[r]; y[r] = yv[r]; }
+#pragma unroll
+    for (int s = 0; s < 4 * M; ++s) z[s] = zv[s];
+    if (ch + (int)gridDim.x < nch) load(ch + gridDim.x);
+    const int n = ch * 64 + wave * 16 + col;
+    const bool nv = n < N;
+    int lo = 0;  // opaque: weight images re-read from LDS per chunk (see k_mlp_fwd)
+    asm volatile("" : "+v"(lo));
+    const floatx4* T1c = T1 + lo;
+    const floatx4* T2c = T2 + lo;
+    float gp[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = 4 * kq + r;
+      gp[r] = bn ? gi[r] * (g[r] - k0[r] - (y[r] - mm[r]) * iv[r] * k1[r]) : g[r];
+      if (o >= O) gp[r] = 0.f;
+      if (bn && dYp && nv && o < O) dYp[(size_t)o * N + n] = gp[r];
+    }
+    floatx4 dz[M];
+    {
+      floatx4 w[M];
+#pragma unroll
+      for (int mt = 0; mt < M; ++mt) {
+        w[mt] = T2c[mt * 64 + lane];
+        dz[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int mt = 0; mt < M; ++mt) dz[mt] = mfma4(w[mt][r], gp[r], dz[mt]);
+    }
+#pragma unroll
+    for (int mt = 0; mt < M; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int h = 16 * mt + 4 * kq + r;
+        dz[mt][r] *= dlrelu(z[4 * mt + r]);
+        if (nv && h < H) dZ[(size_t)h * N + n] = dz[mt][r];
+      }
+    if (want_dx) {
+      __syncthreads();                             // previous chunk's stores from DXs done
+      // dX = W1^T dZ: K-step group mt (hidden tile) over the M output tiles, its
+      // weight float4s read one group ahead, independent accumulators back to back
+      floatx4 dx[M], wn[M];
+#pragma unroll
+      for (int mk = 0; mk < M; ++mk) {
+        dx[mk] = floatx4{0.f, 0.f, 0.f, 0.f};
+        wn[mk] = T1c[(mk * M) * 64 + lane];
+      }
+#pragma unroll
+      for (int mt = 0; mt < M; ++mt) {
+        floatx4 w[M];
+#pragma unroll
+        for (int mk = 0; mk < M; ++mk) w[mk] = wn[mk];
+        if (mt + 1 < M) {
+#pragma unroll
+          for (int mk = 0; mk < M; ++mk) wn[mk] = T1c[(mk * M + mt + 1) * 64 + lane];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int mk = 0; mk < M; ++mk) dx[mk] = mfma4(w[mk][r], dz[mt][r], dx[mk]);
+      }
+#pragma unroll
+      for (int mk = 0; mk < M; ++mk) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = 16 * mk + 4 * kq + r;
+          if (k < K) DXs[k * XS_LD + wave * 16 + col] = dx[mk][r];
+        }
+      }
+      __syncthreads();
+      // rows wu, wu + 4, ...: one coalesced 256-byte row per wave-instruction,
+      // the output block (and its add flag) wave-uniform
+      const int n2 = ch * 64 + lane;
+      if (n2 < N) {
+        for (int k = wu; k < K; k += 4) out_row(outs, k, n2, N, DXs[k * XS_LD + lane]);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------ host side
+int tiles_for(int K, int H) {
+  const int m = (std::max(K, H) + 15) / 16;
+  for (int v : {1, 2, 3, 4, 5, 7})
+    if (m <= v) return v;
+  return -1;
+}
+
+template <class Fn>
+int with_tiles(int m, Fn fn) {
+  switch (m) {
+    case 1: return fn(std::integral_constant<int, 1>{});
+    case 2: return fn(std::integral_constant<int, 2>{});
+    case 3: return fn(std::integral_constant<int, 3>{});
+    case 4: return fn(std::integral_constant<int, 4>{});
+    case 5: return fn(std::integral_constant<int, 5>{});
+    case 7: return fn(std::integral_constant<int, 7>{});
+  }
+  return -1;
+}
+
+size_t fwd_lds(int m) {
+  return ((size_t)m * m * 256 + (size_t)m * 256 + 16 * m + 16 + (size_t)2 * 16 * m * XS_LD) * 4;
+}
+size_t bwd_lds(int m) {
+  return ((size_t)m * 256 + (size_t)m * m * 256 + 80 + (size_t)16 * m * XS_LD) * 4;
+}
+
+// blocks per CU: the M <= 3 kernels fit 2 (registers, LDS), the wider ones
+// run one 4-wave block per CU with up to 512 registers per lane
+int grid_for(int N, int m, size_t lds) {
+  const int nch = (N + 63) / 64;
+  const int per_cu = (m <= 3 && lds <= 72 * 1024) ? 2 : 1;
+  return std::max(1, std::min(nch, 256 * per_cu));
+}
+
+// pfsgnn_seg list -> InSegs (blocks must be contiguous in the weight columns)
+int make_in(const pfsgnn_seg* segs, int nseg, int N, InSegs& S) {
+  if (!segs || nseg < 1 || nseg > NM_SEG) return -1;
+  S = InSegs{};
+  int k = 0, npg = 0;
+  for (int i = 0; i < nseg; ++i) {
+    const pfsgnn_seg& g = segs[i];
+    if (!g.x || g.rows <= 0 || g.col != k || g.per_graph < 0) return -1;
+    if (g.per_graph) {
+      if (N % g.per_graph || (npg && npg != g.per_graph)) return -1;
+      npg = g.per_graph;
+    }
+    S.p[i] = g.x;
+    S.k0[i] = k;
+    S.pg[i] = g.per_graph ? 1 : 0;
+    k += g.rows;
+  }
+  for (int i = nseg; i <= NM_SEG; ++i) S.k0[i] = INT_MAX;
+  for (int i = nseg; i < NM_SEG; ++i) S.p[i] = S.p[0];
+  S.npg = npg;
+  S.Gc = npg ? N / npg : 1;
+  return k;
+}
+
+}  // namespace
+
+extern "C" size_t pfsgnn_mlp_ws_bytes(int N) {
+  return align256((size_t)512 * PART_LEN * sizeof(float)) +
+         align256((size_t)256 * SUM_LEN * sizeof(float)) + (N > 0 ? 0 : 0);
+}
+
+extern "C" int pfsgnn_mlp_fwd(const pfsgnn_seg* segs, int nseg, int N, const float* W1, int ldw1,
+                              int H, const float* b1, const float* W2, int O, const float* b2,
+                              float* Z, float* Yp, const float* gamma, const float* beta,
+                              float* rm, float* rv, float momentum, float eps, float* Y,
+                              float* mu, float* var, void* ws, size_t ws_bytes, void* stream) {
+  const char* where = "pfsgnn_mlp_fwd";
+  PF_REQUIRE(W1 && b1 && W2 && b2 && Yp && N > 0 && H > 0 && O > 0 && O <= 16, where,
+             "bad arguments");
+  InSegs S;
+  const int K = make_in(segs, nseg, N, S);
+  PF_REQUIRE(K > 0, where, "bad segment list (blocks must cover weight columns 0..K in order)");
+  const int m = tiles_for(K, H);
+  PF_REQUIRE(m > 0, where, "K, H > 112 not supported");
+  const bool bn = gamma != nullptr;
+  PF_REQUIRE(!bn || (beta && Y && mu && var && N > 1), where,
+             "BatchNorm needs beta, Y, mu, var and more than one node");
+  PF_REQUIRE(ws && ws_bytes >= pfsgnn_mlp_ws_bytes(N), where, "workspace too small");
+  hipStream_t st = as_stream(stream);
+  const size_t lds = fwd_lds(m);
+  const int grid = grid_for(N, m, lds);
+  float* part = bn ? reinterpret_cast<float*>(ws) : nullptr;
+  const int rc = with_tiles(m, [&](auto mc) {
+    constexpr int MM = decltype(mc)::value;
+    static size_t attr = 0;  // dynamic LDS above the 64 KB default must be opted into
+    if (lds > 65536 && attr < lds) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mlp_fwd<MM>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return -3;
+      attr = lds;
+    }
+    hipLaunchKernelGGL(k_mlp_fwd<MM>, dim3(grid), dim3(256), lds, st, S, K, N, W1, ldw1, H, b1,
+                       W2, O, b2, Z, Yp, part);
+    return 0;
+  });
+  PF_REQUIRE(rc != -3, where, "hipFuncSetAttribute (dynamic LDS) failed");
+  PF_REQUIRE(rc == 0, where, "no kernel for this width");
+  if (bn) {
+    const int ag = std::max(1, std::min(256, (int)(((size_t)O * N + 1023) / 1024)));
+    hipLaunchKernelGGL(k_bn_apply_part, dim3(ag), dim3(256), 0, st, part, grid, O, N, Yp, gamma,
+                       beta, eps, rm, rv, momentum, Y, mu, var);
+  }
+  return pf::check_launch(where);
+}
+
+extern "C" int pfsgnn_mlp_bwd(const float* dY, int N, const float* Yp, const float* mu,
+                              const float* var, const float* gamma, float eps, float* dgamma,
+                              float* dbeta, const float* Z, const float* W1, int ldw1, int H,
+                              int K, const float* W2, int O, float* dYp, float* dZ,
+                              const pfsgnn_oseg* outs, int nout, void* ws, size_t ws_bytes,
+                              void* stream) {
+  const char* where = "pfsgnn_mlp_bwd";
+  PF_REQUIRE(dY && Z && W1 && W2 && dZ && N > 0 && H > 0 && K > 0 && O > 0 && O <= 16, where,
+             "bad arguments");
+  const bool bn = gamma != nullptr;
+  PF_REQUIRE(!bn || (Yp && mu && var && dgamma && dbeta && dYp), where,
+             "BatchNorm backward needs Yp, mu, var, dgamma, dbeta and dYp");
+  PF_REQUIRE(nout >= 0 && nout <= NM_SEG && (nout == 0 || outs), where, "bad output list");
+  OutSegs OS{};
+  int k = 0;
+  for (int i = 0; i < nout; ++i) {
+    PF_REQUIRE(outs[i].rows > 0, where, "bad output block");
+    OS.p[i] = outs[i].x;
+    OS.k0[i] = k;
+    OS.add[i] = outs[i].add;
+    k += outs[i].rows;
+  }
+  PF_REQUIRE(nout == 0 || k == K, where, "output blocks must cover the K input rows");
+  for (int i = nout; i <= NM_SEG; ++i) OS.k0[i] = INT_MAX;
+  const int m = tiles_for(K, H);
+  PF_REQUIRE(m > 0, where, "K, H > 112 not supported");
+  PF_REQUIRE(ws && ws_bytes >= pfsgnn_mlp_ws_bytes(N), where, "workspace too small");
+  hipStream_t st = as_stream(stream);
+  float* spart = nullptr;
+  int nsp = 0;
+  if (bn) {
+    spart = reinterpret_cast<float*>(static_cast<char*>(ws) +
+                                      align256((size_t)512 * PART_LEN * sizeof(float)));
+    nsp = std::max(1, std::min(256, (N + 255) / 256));
+    hipLaunchKernelGGL(k_bn_sums_part, dim3(nsp), dim3(256), 0, st, dY, Yp, O, N, mu, var, eps,
+                       spart);
+  }
+  const size_t lds = bwd_lds(m);
+  const int grid = grid_for(N, m, lds);
+  const int want_dx = nout > 0 ? 1 : 0;
+  const int rc = with_tiles(m, [&](auto mc) {
+    constexpr int MM = decltype(mc)::value;
+    static size_t attr = 0;  // dynamic LDS above the 64 KB default must be opted into
+    if (lds > 65536 && attr < lds) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mlp_bwd<MM>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return -3;
+      attr = lds;
+    }
+    hipLaunchKernelGGL(k_mlp_bwd<MM>, dim3(grid), dim3(256), lds, st, K, N, H, O, dY, Yp, spart,
+                       nsp, mu, var, gamma, eps, dgamma, dbeta, Z, W1, ldw1, W2, dYp, dZ, OS,
+                       want_dx);
+    return 0;
+  });
+  PF_REQUIRE(rc != -3, where, "hipFuncSetAttribute (dynamic LDS) failed");
+  PF_REQUIRE(rc == 0, where, "no kernel for this width");
+  return pf::check_launch(where);
+}

@@ -1030,7 +1030,7 @@ extern "C" int pfsgnn_bn_bwd(const float* dY, const float* X, const float* mu, c
 
 // ---------------------------------------------------------------- graph ops
 __global__ void k_graph_reduce(const float* __restrict__ X, int C, int G, int n, int mean,
-                               float* __restrict__ out) {
+                               float* __restrict__ out, int add) {
   const int cg = blockIdx.x;  // c*G + g
   const int c = cg / G, g = cg - c * G;
   float v[1] = {0.f};
@@ -1038,15 +1038,27 @@ __global__ void k_graph_reduce(const float* __restrict__ X, int C, int G, int n,
   for (int i = threadIdx.x; i < n; i += 256) v[0] += p[i];
   __shared__ float scratch[4];
   block_sum<1>(v, scratch);
-  if (threadIdx.x == 0) out[(size_t)c * G + g] = mean ? v[0] / (float)n : v[0];
+  if (threadIdx.x == 0) {
+    const float r = mean ? v[0] / (float)n : v[0];
+    float* o = out + (size_t)c * G + g;
+    *o = add ? *o + r : r;
+  }
 }
 
 extern "C" int pfsgnn_graph_reduce(const float* X, int C, int G, int n, int mean, float* out,
                                    void* stream) {
   PF_REQUIRE(X && out && C > 0 && G > 0 && n > 0, "pfsgnn_graph_reduce", "bad arguments");
   hipLaunchKernelGGL(k_graph_reduce, dim3(C * G), dim3(256), 0, as_stream(stream), X, C, G, n,
-                     mean, out);
+                     mean, out, 0);
   return pf::check_launch("pfsgnn_graph_reduce");
+}
+
+extern "C" int pfsgnn_graph_reduce_add(const float* X, int C, int G, int n, int mean, float* out,
+                                       void* stream) {
+  PF_REQUIRE(X && out && C > 0 && G > 0 && n > 0, "pfsgnn_graph_reduce_add", "bad arguments");
+  hipLaunchKernelGGL(k_graph_reduce, dim3(C * G), dim3(256), 0, as_stream(stream), X, C, G, n,
+                     mean, out, 1);
+  return pf::check_launch("pfsgnn_graph_reduce_add");
 }
 
 __global__ void k_graph_bcast_add(float* __restrict__ out, int C, int G, int n,

@@ -83,6 +83,15 @@ def _seg_n(segs):
     raise ValueError("a concatenated input needs at least one per-node block")
 
 
+def _fused_mlp_ok(W1, W2, segs):
+    """Shapes the fused node-MLP op takes (include/pfsgnn.h pfsgnn_mlp_fwd)."""
+    K = sum(X.shape[0] for X, _, _ in segs)
+    cols_in_order = all(col == sum(X.shape[0] for X, _, _ in segs[:i])
+                        for i, (_, col, _) in enumerate(segs))
+    return (W2.shape[0] <= 16 and W1.shape[0] <= 112 and K <= 112 and len(segs) <= 4
+            and cols_in_order)
+
+
 class Engine:
     def __init__(self, backend, F, B=0, Fs=1, Ft=1, T=1, normed=True, bn_eps=1e-5,
                  bn_momentum=0.1, rms_eps=None):
@@ -95,52 +104,91 @@ class Engine:
         self.training = True
 
     # ================================================================= MLP
-    def mlp_fwd(self, P, pre, X):
-        """MLP (gnn.py:65): Linear -> LeakyReLU(0.1) -> Linear on [K, N].  X is a
-        tensor or, for the concatenated inputs of gnn.py:153/191/220, a list of
-        row blocks ``(tensor, weight column, per_graph)`` read in place (a
-        per_graph block is [rows, G], broadcast over each graph's nodes)."""
+    def mlp_fwd(self, P, pre, X, bnkey=None, BN=None):
+        """MLP (gnn.py:65): Linear -> LeakyReLU(0.1) -> Linear on [K, N], as ONE
+        fused op, optionally followed by the module's BatchNorm1d (``bnkey``,
+        gnn.py:154/192).  X is a tensor or, for the concatenated inputs of
+        gnn.py:153/191/220, a list of row blocks ``(tensor, weight column,
+        per_graph)`` read in place (a per_graph block is [rows, G], broadcast
+        over each graph's nodes).  Returns (Y, saved)."""
         be = self.be
         W1, b1, W2, b2 = P[pre + "0.weight"], P[pre + "0.bias"], P[pre + "2.weight"], P[pre + "2.bias"]
-        if isinstance(X, list):
-            Z = be.lin_cat(W1, X, _seg_n(X), b=b1)
-        else:
-            Z = be.lin(W1, 0, W1.shape[1], X, b=b1)
-        Y = be.lin(W2, 0, W2.shape[1], Z, b=b2, act_in=True)
-        return Y, (X, Z)
+        segs = X if isinstance(X, list) else [(X, 0, False)]
+        N = _seg_n(segs)
+        norm = bnkey is not None and self.normed
+        if not _fused_mlp_ok(W1, W2, segs):
+            return self._mlp_fwd_ops(P, BN, pre, segs, N, bnkey if norm else None)
+        if norm and self.training:
+            bn = (P[bnkey + "weight"], P[bnkey + "bias"], BN.get(bnkey + "running_mean"),
+                  BN.get(bnkey + "running_var"), self.bn_momentum, self.bn_eps)
+            Y, Z, Yp, mu, var = be.mlp_fwd(segs, N, W1, b1, W2, b2, bn=bn)
+            return Y, (segs, Z, (Yp, mu, var, bnkey))
+        Y, Z, _, _, _ = be.mlp_fwd(segs, N, W1, b1, W2, b2, save_z=self.training)
+        if norm:
+            # eval: nn.BatchNorm1d on running statistics, applied once (gnn.py:154/192)
+            sc, sh = be.bn_eval_coef(P[bnkey + "weight"], P[bnkey + "bias"],
+                                     BN[bnkey + "running_mean"], BN[bnkey + "running_var"],
+                                     self.bn_eps, 1)
+            Y = be.affine_rows(Y, sc, sh)
+        return Y, (segs, Z, None)
 
-    def mlp_bwd(self, P, Gr, pre, dY, saved, want_dx=True):
+    def mlp_bwd(self, P, Gr, pre, dY, saved, outs=()):
+        """Backward of mlp_fwd: the input gradient goes to ``outs`` = [(tensor or
+        None, rows, add)] over the K input rows (empty: none wanted); the weight
+        gradients accumulate into Gr."""
         be = self.be
-        X, Z = saved
+        if saved[0] == "ops":
+            return self._mlp_bwd_ops(P, Gr, pre, dY, saved, outs)
+        segs, Z, bns = saved
         W1, W2 = P[pre + "0.weight"], P[pre + "2.weight"]
+        K = sum(X.shape[0] for X, _, _ in segs)
+        bn = None
+        if bns is not None:
+            Yp, mu, var, key = bns
+            bn = (Yp, mu, var, P[key + "weight"], self.bn_eps, Gr[key + "weight"], Gr[key + "bias"])
+        dYp, dZ = be.mlp_bwd(dY, Z, W1, W2, K, bn=bn, outs=list(outs))
+        be.wgrad(dYp, Z, Gr[pre + "2.weight"], db=Gr[pre + "2.bias"], act_in=True)
+        be.wgrad_cat(dZ, segs, Gr[pre + "0.weight"], db=Gr[pre + "0.bias"])
+
+    # MLPs outside the fused op's shapes (output > 16 or a width > 112: Fdim 16's
+    # SModel node_mlp_2, a node_prediction decoder over many classes) run as
+    # separate Linear ops
+    def _mlp_fwd_ops(self, P, BN, pre, segs, N, bnkey):
+        be = self.be
+        W1, b1, W2, b2 = P[pre + "0.weight"], P[pre + "0.bias"], P[pre + "2.weight"], P[pre + "2.bias"]
+        Z = be.lin_cat(W1, segs, N, b=b1)
+        Y = be.lin(W2, 0, W2.shape[1], Z, b=b2, act_in=True)
+        bns = None
+        if bnkey is not None:
+            if self.training:
+                Yn, mu, var = be.bn_fwd(Y, P[bnkey + "weight"], P[bnkey + "bias"],
+                                        BN.get(bnkey + "running_mean"), BN.get(bnkey + "running_var"),
+                                        self.bn_momentum, self.bn_eps)
+                bns = (Y, mu, var, bnkey)
+                Y = Yn
+            else:
+                sc, sh = be.bn_eval_coef(P[bnkey + "weight"], P[bnkey + "bias"],
+                                         BN[bnkey + "running_mean"], BN[bnkey + "running_var"],
+                                         self.bn_eps, 1)
+                Y = be.affine_rows(Y, sc, sh)
+        return Y, ("ops", segs, Z, bns)
+
+    def _mlp_bwd_ops(self, P, Gr, pre, dY, saved, outs):
+        be = self.be
+        _, segs, Z, bns = saved
+        W1, W2 = P[pre + "0.weight"], P[pre + "2.weight"]
+        if bns is not None:
+            Yp, mu, var, key = bns
+            dY = be.bn_bwd(dY, Yp, mu, var, P[key + "weight"], self.bn_eps, Gr[key + "weight"],
+                           Gr[key + "bias"])
         be.wgrad(dY, Z, Gr[pre + "2.weight"], db=Gr[pre + "2.bias"], act_in=True)
         dZ = be.lin_t(W2, 0, W2.shape[1], dY, z=Z)
-        if isinstance(X, list):
-            be.wgrad_cat(dZ, X, Gr[pre + "0.weight"], db=Gr[pre + "0.bias"])
-        else:
-            be.wgrad(dZ, X, Gr[pre + "0.weight"], db=Gr[pre + "0.bias"])
-        return be.lin_t(W1, 0, W1.shape[1], dZ) if want_dx else None
-
-    def _bn(self, P, BN, key, X):
-        if not self.normed:
-            return X, None
-        if not self.training:
-            # eval: nn.BatchNorm1d on running statistics, applied once (gnn.py:154/192)
-            sc, sh = self.be.bn_eval_coef(P[key + "weight"], P[key + "bias"],
-                                          BN[key + "running_mean"], BN[key + "running_var"],
-                                          self.bn_eps, 1)
-            return self.be.affine_rows(X, sc, sh), None
-        Y, mu, var = self.be.bn_fwd(X, P[key + "weight"], P[key + "bias"],
-                                    BN.get(key + "running_mean"), BN.get(key + "running_var"),
-                                    self.bn_momentum, self.bn_eps)
-        return Y, (X, mu, var)
-
-    def _bn_bwd(self, P, Gr, key, dY, saved):
-        if saved is None:
-            return dY
-        X, mu, var = saved
-        return self.be.bn_bwd(dY, X, mu, var, P[key + "weight"], self.bn_eps,
-                              Gr[key + "weight"], Gr[key + "bias"])
+        be.wgrad_cat(dZ, segs, Gr[pre + "0.weight"], db=Gr[pre + "0.bias"])
+        r = 0
+        for t, rows, add in outs:
+            if t is not None:
+                be.lin_t(W1, r, rows, dZ, out=t, add=add)
+            r += rows
 
     def _rms_eps(self, t):
         return self.rms_eps if self.rms_eps is not None else torch.finfo(t.dtype).eps
@@ -204,20 +252,21 @@ class Engine:
         Qt = be.lin(Ws1, 0, F, xt, b=bs1)
         hmom = be.empty(8 * F, d.NS)
         mom = be.source_fwd(d, xe3[0], xe3[1], xe3[2], Qt, Ws1, Ws2, bs2, hmom)
-        # node_mlp_2 input [x, mean, std, skew, kurt, u[batch]] (gnn.py:153), in place
+        # node_mlp_2 input [x, mean, std, skew, kurt, u[batch]] (gnn.py:153), in place,
+        # + its BatchNorm1d (gnn.py:154) in the same fused op
         hS = [(xs, 0, False), (hmom, F, False), (u, 9 * F, True)]
-        ys, sS = self.mlp_fwd(P, pre + "node_mlp_2.", hS)
-        xs_new, bnS = self._bn(P, BN, pre + "norm.", ys)
-        return dict(xs=xs, xt=xt, xe3=xe3, u=u, Qt=Qt, mom=mom, sS=sS, bnS=bnS, xs_new=xs_new)
+        xs_new, sS = self.mlp_fwd(P, pre + "node_mlp_2.", hS, pre + "norm.", BN)
+        return dict(xs=xs, xt=xt, xe3=xe3, u=u, Qt=Qt, mom=mom, sS=sS, xs_new=xs_new)
 
     def source_node_bwd(self, P, Gr, d, pre, st, g_xs_new, g_xs, g_u):
         """Node half of the SModel backward; returns the per-fiber moment coefficients."""
         be, F, G = self.be, self.F, d.G
-        g_ys = self._bn_bwd(P, Gr, pre + "norm.", g_xs_new, st["bnS"])
-        g_hS = self.mlp_bwd(P, Gr, pre + "node_mlp_2.", g_ys, st["sS"])
-        g_xs += g_hS[0:F]
-        g_u += be.graph_reduce(g_hS[9 * F:10 * F], G)
-        return be.moment_coef(st["mom"], g_hS[F:9 * F], d.NC)
+        gst = be.empty(8 * F, d.NS)          # d loss / d [mean, std, skew, kurt]
+        gu = be.empty(F, d.NS)               # d loss / d u[batch], per fiber
+        self.mlp_bwd(P, Gr, pre + "node_mlp_2.", g_xs_new, st["sS"],
+                     outs=[(g_xs, F, True), (gst, 8 * F, False), (gu, F, False)])
+        be.graph_reduce(gu, G, out=g_u)
+        return be.moment_coef(st["mom"], gst, d.NC)
 
     def source_edge_bwd(self, P, Gr, d, pre, st, coef, tpart, g_next, bnstat, g_xt):
         be, F = self.be, self.F
@@ -240,19 +289,18 @@ class Engine:
         Rs = be.lin(Wt1, 0, F, xs, b=bt1)
         hsum = be.target_fwd(d, xe3[0], xe3[1], xe3[2], Rs, Wt1)
         agg = be.lin(Wt2, 0, 2 * F, hsum, b=bt2, bscale=float(d.NF))
-        # node_mlp_2 input [x, agg, u[batch]] (gnn.py:191), in place
+        # node_mlp_2 input [x, agg, u[batch]] (gnn.py:191), in place, + BatchNorm1d
         hT = [(xt, 0, False), (agg, F, False), (u, 3 * F, True)]
-        yt, sT = self.mlp_fwd(P, pre + "node_mlp_2.", hT)
-        xt_new, bnT = self._bn(P, BN, pre + "norm.", yt)
-        return dict(xs=xs, xt=xt, xe3=xe3, u=u, Rs=Rs, hsum=hsum, sT=sT, bnT=bnT, xt_new=xt_new)
+        xt_new, sT = self.mlp_fwd(P, pre + "node_mlp_2.", hT, pre + "norm.", BN)
+        return dict(xs=xs, xt=xt, xe3=xe3, u=u, Rs=Rs, hsum=hsum, sT=sT, xt_new=xt_new)
 
     def target_node_bwd(self, P, Gr, d, pre, st, g_xt_new, g_xt, g_u):
         be, F, G = self.be, self.F, d.G
-        g_yt = self._bn_bwd(P, Gr, pre + "norm.", g_xt_new, st["bnT"])
-        g_hT = self.mlp_bwd(P, Gr, pre + "node_mlp_2.", g_yt, st["sT"])
-        g_xt += g_hT[0:F]
-        g_agg = g_hT[F:3 * F]
-        g_u += be.graph_reduce(g_hT[3 * F:4 * F], G)
+        g_agg = be.empty(2 * F, d.NT)
+        gu = be.empty(F, d.NT)
+        self.mlp_bwd(P, Gr, pre + "node_mlp_2.", g_xt_new, st["sT"],
+                     outs=[(g_xt, F, True), (g_agg, 2 * F, False), (gu, F, False)])
+        be.graph_reduce(gu, G, out=g_u)
         Wt2 = P[pre + "node_mlp_1.2.weight"]
         be.wgrad(g_agg, st["hsum"], Gr[pre + "node_mlp_1.2.weight"],
                  db=Gr[pre + "node_mlp_1.2.bias"], dbscale=float(d.NF))
@@ -289,10 +337,11 @@ class Engine:
                               self._rms_eps(st["v"]), Gr[pre + "norm.weight"])
         else:
             g_v = g_u_new
-        g_hU = self.mlp_bwd(P, Gr, pre, g_v, st["sU"])
-        g_u += g_hU[0:F]
-        be.graph_bcast_add(g_xs, g_hU[F:2 * F], 1.0 / d.NF)
-        be.graph_bcast_add(g_xt, g_hU[2 * F:3 * F], 1.0 / d.NC)
+        g_ms, g_mt = be.empty(F, d.G), be.empty(F, d.G)
+        self.mlp_bwd(P, Gr, pre, g_v, st["sU"], outs=[(g_u, F, True), (g_ms, F, False),
+                                                      (g_mt, F, False)])
+        be.graph_bcast_add(g_xs, g_ms, 1.0 / d.NF)
+        be.graph_bcast_add(g_xt, g_mt, 1.0 / d.NC)
 
     # ============================================================ GNN path
     def forward(self, P, BN, d, xs_in, xt_in, xe_in, u_in, training=True):
@@ -377,8 +426,8 @@ class Engine:
                                  g_xs_in, g_xt_in, g_u_in)
             g_xs, g_xt, g_u = g_xs_in, g_xt_in, g_u_in
         s_enc, t_enc = ctx["enc"]
-        self.mlp_bwd(P, Gr, "encoder_s.", g_xs, s_enc, want_dx=False)
-        self.mlp_bwd(P, Gr, "encoder_t.", g_xt, t_enc, want_dx=False)
+        self.mlp_bwd(P, Gr, "encoder_s.", g_xs, s_enc)
+        self.mlp_bwd(P, Gr, "encoder_t.", g_xt, t_enc)
 
     # ================================================================ loss
     def loss_forward(self, P, d, xe3, ci, sharpness, seed, pclass=0.1, pfiber=0.1, total_time=42.0,

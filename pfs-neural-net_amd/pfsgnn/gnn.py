@@ -401,7 +401,10 @@ class _MLPFn(torch.autograd.Function):
         eng = _engine_for(module[0].out_features, True)
         P = module._flat_params()
         Gr = module._flat_grads()
-        dx = eng.mlp_bwd(P, Gr, "", gy.t().contiguous(), ctx.saved_pf, want_dx=True)
+        be = backend()
+        K = module[0].in_features
+        dx = be.empty(K, gy.shape[0])
+        eng.mlp_bwd(P, Gr, "", gy.t().contiguous(), ctx.saved_pf, outs=[(dx, K, False)])
         return dx.t(), None, None
 
 

@@ -49,6 +49,14 @@ class Red(ctypes.Structure):
 
 REDP = ctypes.POINTER(Red)
 
+
+class OSeg(ctypes.Structure):
+    """pfsgnn_oseg (include/pfsgnn.h): one row block of an input-gradient output."""
+    _fields_ = [("x", ctypes.c_void_p), ("rows", ctypes.c_int), ("add", ctypes.c_int)]
+
+
+OSEGP = ctypes.POINTER(OSeg)
+
 _SIGS = {
     "pfsgnn_version": ([], ctypes.c_char_p),
     "pfsgnn_last_error": ([], ctypes.c_char_p),
@@ -71,7 +79,13 @@ _SIGS = {
     "pfsgnn_reduce_batch": ([REDP, I, P], I),
     "pfsgnn_bn_fwd": ([P, I, I, P, P, P, P, FL, FL, P, P, P, P, SZ, P], I),
     "pfsgnn_bn_bwd": ([P, P, P, P, P, FL, I, I, P, P, P, P, SZ, P], I),
+    "pfsgnn_mlp_ws_bytes": ([I], SZ),
+    "pfsgnn_mlp_fwd": ([SEGP, I, I, P, I, I, P, P, I, P, P, P, P, P, P, P, FL, FL, P, P, P, P,
+                        SZ, P], I),
+    "pfsgnn_mlp_bwd": ([P, I, P, P, P, P, FL, P, P, P, P, I, I, I, P, I, P, P, OSEGP, I, P, SZ,
+                        P], I),
     "pfsgnn_graph_reduce": ([P, I, I, I, I, P, P], I),
+    "pfsgnn_graph_reduce_add": ([P, I, I, I, I, P, P], I),
     "pfsgnn_graph_bcast_add": ([P, I, I, I, P, FL, P], I),
     "pfsgnn_rms2_fwd": ([P, I, I, P, FL, P, P, P, P, P], I),
     "pfsgnn_rms2_bwd": ([P, P, P, P, P, P, I, I, FL, P, P, P, SZ, P], I),
@@ -357,6 +371,62 @@ class HipBackend:
         _call("pfsgnn_wgrad_cat", dY.data_ptr(), M, arr, len(segs), N, int(act_in), dW.data_ptr(),
               dW.shape[1], _ptr(db), float(dbscale), ws, wsb, _stream())
 
+    # ------------------------------------------------------- fused node MLPs
+    def mlp_fwd(self, segs, N, W1, b1, W2, b2, bn=None, save_z=True):
+        """MLP (gnn.py:65) over a concatenated node input (+ training BatchNorm1d
+        when ``bn`` = (gamma, beta, running_mean, running_var, momentum, eps)).
+        Returns (Y, Z, Yp, mu, var): Y the module output, Z the saved
+        pre-activation, Yp the pre-norm output (Y itself without bn)."""
+        H, ldw1 = W1.shape
+        O = W2.shape[0]
+        self._chk(W1, b1, W2, b2)
+        arr = self._segs(segs, N)
+        Z = self.empty(H, N) if save_z else None
+        Yp = self.empty(O, N)
+        g = bt = rm = rv = None
+        mom, eps = 0.0, 0.0
+        Y = mu = var = None
+        if bn is not None:
+            g, bt, rm, rv, mom, eps = bn
+            self._chk(g, bt, rm, rv)
+            Y, mu, var = self.empty(O, N), self.empty(O), self.empty(O)
+        ws, wsb = self._wsargs(getattr(self, "_dims", None))
+        _call("pfsgnn_mlp_fwd", arr, len(segs), N, W1.data_ptr(), ldw1, H, b1.data_ptr(),
+              W2.data_ptr(), O, b2.data_ptr(), _ptr(Z), Yp.data_ptr(), _ptr(g), _ptr(bt), _ptr(rm),
+              _ptr(rv), float(mom), float(eps), _ptr(Y), _ptr(mu), _ptr(var), ws, wsb, _stream())
+        return (Yp if Y is None else Y), Z, Yp, mu, var
+
+    def mlp_bwd(self, dY, Z, W1, W2, K, bn=None, outs=()):
+        """Input side of the MLP(+BN) backward.  ``bn`` = (Yp, mu, var, gamma, eps,
+        dgamma, dbeta) or None; ``outs`` = [(tensor or None, rows, add)] covering
+        the K input rows (empty: no input gradient).  Returns (dYp, dZ)."""
+        H, ldw1 = W1.shape
+        O, N = dY.shape
+        dY = dY.contiguous()
+        self._chk(dY, Z, W1, W2)
+        dZ = self.empty(H, N)
+        Yp = mu = var = g = dg = db = None
+        eps = 0.0
+        dYp = dY
+        if bn is not None:
+            Yp, mu, var, g, eps, dg, db = bn
+            self._chk(Yp, mu, var, g, dg, db)
+            dYp = self.empty(O, N)
+        arr = (OSeg * max(1, len(outs)))()
+        for i, (t, rows, add) in enumerate(outs):
+            if t is not None:
+                self._chk(t)
+                assert t.shape == (rows, N), (t.shape, rows, N)
+            arr[i].x = None if t is None else t.data_ptr()
+            arr[i].rows = int(rows)
+            arr[i].add = int(bool(add))
+        ws, wsb = self._wsargs(getattr(self, "_dims", None))
+        _call("pfsgnn_mlp_bwd", dY.data_ptr(), N, _ptr(Yp), _ptr(mu), _ptr(var), _ptr(g),
+              float(eps), _ptr(dg), _ptr(db), Z.data_ptr(), W1.data_ptr(), ldw1, H, int(K),
+              W2.data_ptr(), O, None if bn is None else dYp.data_ptr(), dZ.data_ptr(), arr,
+              len(outs), ws, wsb, _stream())
+        return dYp, dZ
+
     def bn_fwd(self, X, gamma, beta, rm, rv, momentum, eps):
         C, N = X.shape
         Y, mu, var = self.empty(C, N), self.empty(C), self.empty(C)
@@ -378,10 +448,16 @@ class HipBackend:
               dbeta.data_ptr(), ws, wsb, _stream())
         return dX
 
-    def graph_reduce(self, X, G, mean=False):
+    def graph_reduce(self, X, G, mean=False, out=None):
+        """Per-graph sum (mean) of a node table; with ``out`` it is accumulated."""
         C, N = X.shape
-        out = self.empty(C, G)
         self._chk(X)
+        if out is not None:
+            self._chk(out)
+            _call("pfsgnn_graph_reduce_add", X.data_ptr(), C, G, N // G, int(mean),
+                  out.data_ptr(), _stream())
+            return out
+        out = self.empty(C, G)
         _call("pfsgnn_graph_reduce", X.data_ptr(), C, G, N // G, int(mean), out.data_ptr(),
               _stream())
         return out

@@ -147,6 +147,35 @@ class EmuBackend:
         if db is not None:
             db += dbscale * dY.sum(1)
 
+    def mlp_fwd(self, segs, N, W1, b1, W2, b2, bn=None, save_z=True):
+        Z = b1[:, None] + 0
+        for X, col, bc in segs:
+            Z = Z + W1[:, col:col + X.shape[0]] @ self._expand(X, bc, N)
+        Yp = W2 @ lrelu(Z) + b2[:, None]
+        if bn is None:
+            return Yp, Z, Yp, None, None
+        g, bt, rm, rv, mom, eps = bn
+        Y, mu, var = self.bn_fwd(Yp, g, bt, rm, rv, mom, eps)
+        return Y, Z, Yp, mu, var
+
+    def mlp_bwd(self, dY, Z, W1, W2, K, bn=None, outs=()):
+        dYp = dY
+        if bn is not None:
+            Yp, mu, var, g, eps, dg, db = bn
+            dYp = self.bn_bwd(dY, Yp, mu, var, g, eps, dg, db)
+        dZ = (W2.t() @ dYp) * dlrelu(Z)
+        if outs:
+            dX = W1[:, :K].t() @ dZ
+            r = 0
+            for t, rows, add in outs:
+                if t is not None:
+                    if add:
+                        t += dX[r:r + rows]
+                    else:
+                        t.copy_(dX[r:r + rows])
+                r += rows
+        return dYp, dZ
+
     def bn_fwd(self, X, gamma, beta, rm, rv, momentum, eps):
         n = X.shape[1]
         mu = X.mean(1)
@@ -167,10 +196,14 @@ class EmuBackend:
         dbeta += Sg
         return (gamma * inv)[:, None] * (dY - Sg[:, None] / n - xh * (Sgx / n)[:, None])
 
-    def graph_reduce(self, X, G, mean=False):
+    def graph_reduce(self, X, G, mean=False, out=None):
         C, N = X.shape
         R = X.reshape(C, G, N // G).sum(2)
-        return R / (N // G) if mean else R
+        R = R / (N // G) if mean else R
+        if out is not None:
+            out += R
+            return out
+        return R
 
     def graph_bcast_add(self, out, src, scale=1.0):
         C, N = out.shape

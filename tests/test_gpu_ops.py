@@ -347,3 +347,68 @@ def test_layout_modes(hb, G, NF, NC):
         bad[1, 0] = NC * (G - 1)
         assert not hb.layout_analyze(bad.cuda(), G, NF, NC)[1]
     assert torch.equal(from_canonical(xc_ref, G, NF, NC), x)
+
+
+# fused node MLP (+ BatchNorm1d): (K split into blocks, H, O, N, G, bn) -- the
+# SModel / TModel / GlobalModel / encoder shapes at Fdim 8/10/16, N not a
+# multiple of 64, per-graph u blocks, one wave-chunk and many
+MLP_CASES = [
+    ([10, 80, 10], 100, 10, 38 * 64 + 26, 16, True),     # SModel node_mlp_2, Fdim 10
+    ([8, 64, 8], 80, 8, 1000, 4, True),                 # Fdim 8
+    ([16, 32, 16], 64, 16, 777, 3, True),               # TModel node_mlp_2, Fdim 16
+    ([12, 88, 12], 112, 16, 300, 4, True),              # the widest fused shape
+    ([10, 20, 10], 40, 10, 2048, 16, True),             # TModel node_mlp_2
+    ([10, 10, 10], 30, 10, 16, 16, False),              # GlobalModel MLP over G columns
+    ([1], 10, 10, 5000, 1, False),                      # encoder_s
+    ([2], 10, 10, 130, 1, False),                       # encoder_t
+]
+
+
+@pytest.mark.parametrize("blocks,H,O,N,G,bn", MLP_CASES)
+def test_mlp_fused(hb, blocks, H, O, N, G, bn):
+    """pfsgnn_mlp_fwd / pfsgnn_mlp_bwd (+ the BatchNorm1d) and the weight
+    gradients taken from their saved tensors, vs the float64 emulation."""
+    gen = torch.Generator().manual_seed(N + H + O)
+    emu = EmuBackend()
+    K = sum(blocks)
+    last_pg = len(blocks) == 3 and G > 1 and N % G == 0 and N > G
+    X = []
+    col = 0
+    for i, rows in enumerate(blocks):
+        pg = last_pg and i == len(blocks) - 1
+        X.append((r(rows, G if pg else N, gen=gen), col, pg))
+        col += rows
+    W1, b1 = r(H, K, scale=0.2, gen=gen), r(H, scale=0.3, gen=gen)
+    W2, b2 = r(O, H, scale=0.2, gen=gen), r(O, gen=gen)
+    g, bt = r(O, gen=gen) * 0.2 + 1, r(O, gen=gen) * 0.1
+    rm, rv = r(O, gen=gen) * 0.1, r(O, gen=gen).abs() + 0.5
+    dY = r(O, N, gen=gen)
+    res = {}
+    for be, conv in ((emu, lambda t: t.clone()), (hb, cuda)):
+        segs = [(conv(t), c, pg) for t, c, pg in X]
+        w = [conv(t) for t in (W1, b1, W2, b2)]
+        bnp = (conv(g), conv(bt), conv(rm), conv(rv), 0.1, 1e-5) if bn else None
+        Y, Z, Yp, mu, var = be.mlp_fwd(segs, N, *w, bn=bnp)
+        dg, db = conv(torch.zeros(O)), conv(torch.zeros(O))
+        bnb = (Yp, mu, var, bnp[0], 1e-5, dg, db) if bn else None
+        outs, bufs = [], []
+        for t, c, pg in X:
+            buf = conv(torch.full((t.shape[0], N), 0.5))
+            bufs.append(buf)
+            outs.append((buf, t.shape[0], c == 0))      # first block accumulates
+        dYp, dZ = be.mlp_bwd(conv(dY), Z, w[0], w[2], K, bn=bnb, outs=outs)
+        dW1, db1 = conv(torch.zeros(H, K)), conv(torch.zeros(H))
+        dW2, db2 = conv(torch.zeros(O, H)), conv(torch.zeros(O))
+        be.wgrad(dYp, Z, dW2, db=db2, act_in=True)
+        be.wgrad_cat(dZ, segs, dW1, db=db1)
+        res[be.name] = dict(Y=Y, Z=Z, dYp=dYp, dZ=dZ, dW1=dW1, db1=db1, dW2=dW2, db2=db2,
+                            **{f"dX{i}": b for i, b in enumerate(bufs)},
+                            **({"mu": mu, "var": var, "rm": bnp[2], "rv": bnp[3], "dg": dg,
+                                "db": db} if bn else {}))
+    for k, v in res["emu"].items():
+        atol = 1e-6
+        if k in ("db2", "db"):
+            # sums of the BatchNorm-backward gradient cancel to ~0 analytically:
+            # judged against the fp32 rounding of the sum of |terms|
+            atol += 1e-6 * res["emu"]["dYp"].abs().sum(1).max().item()
+        close(res["hip"][k], v, rtol=5e-5, atol=atol, name=k)
