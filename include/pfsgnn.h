@@ -42,15 +42,18 @@ size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F);
 
 /* Implementation of the per-edge kernels (process-wide, read at launch, so a
  * captured graph keeps the path it was captured with):
- *   PFSGNN_EDGE_MFMA (default) -- matrix cores (pfsgnn_mfma.hip): layer
- *       contractions on v_mfma_f32_16x16x4_f32 (exact fp32 products), weight
- *       gradients on v_mfma_f32_16x16x16_bf16 with split operands (bf16 hi +
- *       lo, ~2^-16 relative per product, averaged over the edge sum);
+ *   PFSGNN_EDGE_MFMA (default) -- matrix cores (pfsgnn_mfma.hip): forward
+ *       layer contractions and their backward recompute on
+ *       v_mfma_f32_16x16x4_f32 (exact fp32 products); the backward's gradient
+ *       chains (W^T g) and the weight gradients on v_mfma_f32_16x16x16_bf16
+ *       with split operands (bf16 hi + lo, ~2^-16 relative per product);
+ *   PFSGNN_EDGE_MFMA_F32 -- the same with the gradient chains in exact fp32;
  *   PFSGNN_EDGE_VALU -- fp32 fmaf chains on the vector ALU (pfsgnn_edge.hip).
- * Both produce the same outputs to fp32 rounding; node-level ops, reductions
- * and the loss are shared. */
+ * All produce the same outputs to the parity tolerance; node-level ops,
+ * reductions and the loss are shared. */
 #define PFSGNN_EDGE_VALU 0
 #define PFSGNN_EDGE_MFMA 1
+#define PFSGNN_EDGE_MFMA_F32 2
 int pfsgnn_set_edge_path(int path);
 int pfsgnn_get_edge_path(void);
 /* Grid the current edge path launches for a batch (host-only query, for tests

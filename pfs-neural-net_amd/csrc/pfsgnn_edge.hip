@@ -1120,7 +1120,9 @@ void fiber_finish(const EdgeGeo& geo, int C, const float* dst, float* out, hipSt
 }
 
 int g_path = PFSGNN_EDGE_MFMA;
-bool use_mfma() { return g_path == PFSGNN_EDGE_MFMA; }
+bool use_mfma() { return g_path != PFSGNN_EDGE_VALU; }
+// bf16x3 gradient chains in the MFMA backward kernels (PFSGNN_EDGE_MFMA)
+bool use_b3() { return g_path == PFSGNN_EDGE_MFMA; }
 // MFMA blocks stage their class-table rows in LDS: at most MAX_CPS classes each
 EdgeGeo geo_mfma(int G, int NF, int NC) {
   const long long groups = (long long)G * ((NF + 63) / 64);
@@ -1140,8 +1142,9 @@ EdgeGeo geo_for(int G, int NF, int NC) {
 }  // namespace
 
 extern "C" int pfsgnn_set_edge_path(int path) {
-  if (path != PFSGNN_EDGE_VALU && path != PFSGNN_EDGE_MFMA)
-    return pf::fail("pfsgnn_set_edge_path", "path must be PFSGNN_EDGE_VALU or PFSGNN_EDGE_MFMA");
+  if (path != PFSGNN_EDGE_VALU && path != PFSGNN_EDGE_MFMA && path != PFSGNN_EDGE_MFMA_F32)
+    return pf::fail("pfsgnn_set_edge_path",
+                    "path must be PFSGNN_EDGE_VALU, PFSGNN_EDGE_MFMA or PFSGNN_EDGE_MFMA_F32");
   g_path = path;
   return 0;
 }
@@ -1287,7 +1290,7 @@ extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, c
   PF_REQUIRE(part && gz && ghT, "pfsgnn_target_bwd", "workspace too small");
   { pf::Timer tm_("target_bwd", st);
   if (use_mfma()) {
-    if (int rc = pfm::target_bwd(geo, F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part, st)) return rc;
+    if (int rc = pfm::target_bwd(geo, F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part, use_b3(), st)) return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
                                    sc, sh, Rs, Wt1, ghT, gz, gxe, part));
@@ -1329,7 +1332,7 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
   { pf::Timer tm_("source_bwd", st);
   if (mfma) {
     if (int rc = pfm::source_bwd(geo, F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT,
-                                 g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, st))
+                                 g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, use_b3(), st))
       return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_source_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
@@ -1396,7 +1399,7 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
     PF_REQUIRE(pW2 && pW1 && pCol && gs, "pfsgnn_edge_mlp_bwd", "workspace too small");
     pf::Timer tm_("edge_mlp_bwd", st);
     if (int rc = pfm::edge_mlp_bwd(geo, F, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1,
-                                   W2, gxe, gs, pW2, pW1, pCol, st))
+                                   W2, gxe, gs, pW2, pW1, pCol, use_b3(), st))
       return rc;
     tm_.end();
   } else {

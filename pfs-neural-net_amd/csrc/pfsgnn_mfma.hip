@@ -43,6 +43,8 @@
 // stays bitwise reproducible.
 #include "pfsgnn_mfma.h"
 
+#include <type_traits>
+
 #ifndef MF_DEPTH_FWD
 #define MF_DEPTH_FWD 4   // classes of edge rows in flight per wave (forward kernels)
 #endif
@@ -148,6 +150,42 @@ __device__ __forceinline__ floatx4 mma3(const Fr& a, const Fr& b, floatx4 c) {
 __device__ __forceinline__ s16x4 ones16() {
   return s16x4{(short)0x3F80, (short)0x3F80, (short)0x3F80, (short)0x3F80};
 }
+
+// ------------------------------------------------------------ bf16x3 layer
+// y (+)= W x for the GRADIENT chains of the backward kernels (PFSGNN_EDGE_MFMA):
+// v_mfma_f32_16x16x16_bf16 on split operands, ~2^-16 relative per product
+// (the forward values and their recompute stay exact fp32: LayerF).  K-step
+// u of v_mfma_f32_16x16x16 takes the 4 slots 4u..4u+3 of every lane group, so
+// a D-row input costs GM<D>::NT steps (20 -> 2, 40 -> 3) instead of
+// GM<D>::RPG fp32 steps (5, 10); the input is the lane's own floatx4 tiles,
+// split once (the same splits feed the weight-gradient images).
+template <int M, int K>
+struct LayerB3 {
+  static constexpr int MT = GM<M>::NT, KT = GM<K>::NT;
+  Fr a[MT][KT];
+  template <class Fn>
+  __device__ __forceinline__ void load(Fn fn, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+        floatx4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ro = GM<M>::mrow(t, i), ri = GM<K>::row(g, 4 * u + j);
+          v[j] = (ro >= 0 && ri >= 0) ? fn(ro, ri) : 0.f;
+        }
+        a[t][u] = split(v);
+      }
+  }
+  __device__ __forceinline__ void apply(const Fr (&x)[KT], floatx4 (&y)[MT]) const {
+#pragma unroll
+    for (int u = 0; u < KT; ++u)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) y[t] = mma3(a[t][u], x[u], y[t]);
+  }
+};
 
 // Wave-private image of one 16x16 bf16 block, [16 edges][16 slots] (32-byte
 // rows, the four 8-byte chunks of row e XOR-swizzled by e>>2: conflict-free b64
@@ -640,7 +678,7 @@ __global__ __launch_bounds__(256) void km_target_fwd(EdgeGeo geo, const float* _
 // ============================================================ TModel bwd
 // g_z = g_hsum[c] * lrelu'(z) per edge; per-fiber sums of g_z (-> g_Rs), the
 // edge-input gradient Wt1[:, F:2F]^T g_z (optional) and dWt1[:, F:2F] += g_z x^T.
-template <int F>
+template <int F, bool B3>
 __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* __restrict__ y,
                                                      const float* __restrict__ sc,
                                                      const float* __restrict__ sh,
@@ -660,7 +698,7 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
   short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
   LayerF<C, F> L1;
   L1.load([&](int h, int k) { return Wt1[h * 2 * F + F + k]; }, lane);
-  LayerF<F, C> LT;
+  std::conditional_t<B3, LayerB3<F, C>, LayerF<F, C>> LT;
   LT.load([&](int k, int h) { return gxe ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
   floatx4 rs[NT], accF[NT], accW[NT];
 #pragma unroll
@@ -693,14 +731,17 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
       for (int r = 0; r < GM<C>::nreg(tt); ++r) gz[tt][r] = fvalid ? gh[r] * dlrelu(z[tt][r]) : 0.f;
       accF[tt] += gz[tt];
     }
+    Fr sgz[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) sgz[tt] = split(gz[tt]);
     if (gxe) {
       floatx4 gx[1] = {zero4()};
-      LT.apply(gz, gx);
+      if constexpr (B3) LT.apply(sgz, gx); else LT.apply(gz, gx);
       st_frows<F>(gxe, eo, RB, g4, fvalid, gx[0]);
     }
     lds_order();
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) img_put2(img + tt * 2 * IMG_SHORTS, lane, split(gz[tt]));
+    for (int tt = 0; tt < NT; ++tt) img_put2(img + tt * 2 * IMG_SHORTS, lane, sgz[tt]);
     img_put2(img + NT * 2 * IMG_SHORTS, lane, split(x[0]));
     lds_order();
     const Fr tx = img_tr2(img + NT * 2 * IMG_SHORTS, lane);
@@ -729,7 +770,7 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
 // message MLP; plus TModel's recomputed input gradient, the downstream edge
 // gradient and the edge BatchNorm's two gradient sums.  dWs2 += g_m a^T,
 // dbs2 += g_m, dWs1[:, F:2F] += g_zs x^T, per-class sums of g_zs (-> g_Qt).
-template <int F>
+template <int F, bool B3>
 __global__ __launch_bounds__(256, 2) void km_source_bwd(
     EdgeGeo geo, const float* __restrict__ y, const float* __restrict__ sc,
     const float* __restrict__ sh, const float* __restrict__ QtS, const float* __restrict__ Ws1,
@@ -761,10 +802,12 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   LayerF<C, F> L1s, L1t;
   L1s.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
   L1t.load([&](int h, int k) { return tpart ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
-  LayerF<C, C> L2, L2T;
+  LayerF<C, C> L2;
   L2.load([&](int o, int h) { return Ws2[o * C + h]; }, lane);
+  // gradient chains: bf16x3 (PFSGNN_EDGE_MFMA) or exact fp32 (PFSGNN_EDGE_MFMA_F32)
+  std::conditional_t<B3, LayerB3<C, C>, LayerF<C, C>> L2T;
   L2T.load([&](int h, int o) { return Ws2[o * C + h]; }, lane);
-  LayerF<F, C> L1sT, L1tT;
+  std::conditional_t<B3, LayerB3<F, C>, LayerF<F, C>> L1sT, L1tT;
   L1sT.load([&](int k, int h) { return Ws1[h * 2 * F + F + k]; }, lane);
   L1tT.load([&](int k, int h) { return tpart ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
   floatx4 rs[NT], bias[NT], mn[NT], q0[NT], q1[NT], q2[NT], q3[NT];
@@ -825,17 +868,23 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
       }
       accB[tt] += gm[tt];
     }
-    // ---- backward through the message MLP
+    // ---- backward through the message MLP (the operand splits also feed the
+    // weight-gradient images below)
+    Fr sgm[NT], sgz[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) sgm[tt] = split(gm[tt]);
     floatx4 gz[NT];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) gz[tt] = zero4();
-    L2T.apply(gm, gz);
+    if constexpr (B3) L2T.apply(sgm, gz); else L2T.apply(gm, gz);
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt)
+    for (int tt = 0; tt < NT; ++tt) {
 #pragma unroll
       for (int r = 0; r < GM<C>::nreg(tt); ++r) gz[tt][r] *= dlrelu(zs[tt][r]);
+      sgz[tt] = split(gz[tt]);
+    }
     floatx4 g[1] = {zero4()};
-    L1sT.apply(gz, g);
+    if constexpr (B3) L1sT.apply(sgz, g); else L1sT.apply(gz, g);
     if (tpart) {  // TModel's per-edge input gradient, recomputed (gnn.py:188-190)
       floatx4 zt[NT];
 #pragma unroll
@@ -847,7 +896,14 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
 #pragma unroll
         for (int r = 0; r < 4; ++r) zt[tt][r] = (fvalid && r < GM<C>::nreg(tt)) ? gh[r] * dlrelu(zt[tt][r]) : 0.f;
       }
-      L1tT.apply(zt, g);
+      if constexpr (B3) {
+        Fr szt[NT];
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) szt[tt] = split(zt[tt]);
+        L1tT.apply(szt, g);
+      } else {
+        L1tT.apply(zt, g);
+      }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) g[0][r] = fm[r] ? g[0][r] + (g_next ? gnr[r] : 0.f) : 0.f;
@@ -863,9 +919,9 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     lds_order();
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      img_put2(im_gm + tt * 2 * IMG_SHORTS, lane, split(gm[tt]));
+      img_put2(im_gm + tt * 2 * IMG_SHORTS, lane, sgm[tt]);
       img_put2(im_a + tt * 2 * IMG_SHORTS, lane, split(as[tt]));
-      img_put2(im_gz + tt * 2 * IMG_SHORTS, lane, split(gz[tt]));
+      img_put2(im_gz + tt * 2 * IMG_SHORTS, lane, sgz[tt]);
     }
     img_put2(im_x, lane, split(x[0]));
     lds_order();
@@ -943,7 +999,7 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
 // dW1[:, 2F:3F] += g_z x^T, per-fiber (-> g_Ps) and per-class (-> g_Pt) sums of
 // g_z, and the edge-input gradient W1[:, 2F:3F]^T g_z when the block has an
 // upstream edge input.
-template <int F>
+template <int F, bool B3>
 __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
     EdgeGeo geo, const float* __restrict__ g_tot, const float* __restrict__ alpha,
     const float* __restrict__ gam0, const float* __restrict__ gam1, const float* __restrict__ y,
@@ -966,10 +1022,12 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
   short* im_gz = im_a + NT * 2 * IMG_SHORTS;
   short* im_x = im_gz + NT * 2 * IMG_SHORTS;
 
-  LayerF<H, F> L1, L2T;
+  LayerF<H, F> L1;
   L1.load([&](int h, int k) { return W1[h * 4 * F + 2 * F + k]; }, lane);
+  // gradient chains: bf16x3 (PFSGNN_EDGE_MFMA) or exact fp32 (PFSGNN_EDGE_MFMA_F32)
+  std::conditional_t<B3, LayerB3<H, F>, LayerF<H, F>> L2T;
   L2T.load([&](int h, int o) { return W2[o * H + h]; }, lane);
-  LayerF<F, H> L1T;
+  std::conditional_t<B3, LayerB3<F, H>, LayerF<F, H>> L1T;
   L1T.load([&](int k, int h) { return gxe ? W1[h * 4 * F + 2 * F + k] : 0.f; }, lane);
   floatx4 ps[NT], accF[NT], accW1[NT], accW2[NT];
 #pragma unroll
@@ -1011,24 +1069,27 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
     }
     L1.apply(x, z);
     lrelu_act<H>(z, a);
-    L2T.apply(gy, gz);
+    const Fr sgy[1] = {split(gy[0])};
+    if constexpr (B3) L2T.apply(sgy, gz); else L2T.apply(gy, gz);
+    Fr sgz[NT];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
 #pragma unroll
       for (int r = 0; r < GM<H>::nreg(tt); ++r) gz[tt][r] *= dlrelu(z[tt][r]);
       accF[tt] += gz[tt];
+      sgz[tt] = split(gz[tt]);
     }
     if (gxe) {
       floatx4 gx[1] = {zero4()};
-      L1T.apply(gz, gx);
+      if constexpr (B3) L1T.apply(sgz, gx); else L1T.apply(gz, gx);
       st_frows<F>(gxe, eo, RB, g4, fvalid, gx[0]);
     }
     lds_order();
-    img_put2(im_gy, lane, split(gy[0]));
+    img_put2(im_gy, lane, sgy[0]);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
       img_put2(im_a + tt * 2 * IMG_SHORTS, lane, split(a[tt]));
-      img_put2(im_gz + tt * 2 * IMG_SHORTS, lane, split(gz[tt]));
+      img_put2(im_gz + tt * 2 * IMG_SHORTS, lane, sgz[tt]);
     }
     img_put2(im_x, lane, split(x[0]));
     lds_order();
@@ -1129,9 +1190,13 @@ int target_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const
 
 int target_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* Rs, const float* Wt1, const float* ghS, float* gz, float* gxe,
-               float* part, hipStream_t st) {
-  MF_DISPATCH(F, hipLaunchKernelGGL(km_target_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
-                                    y, sc, sh, Rs, Wt1, ghS, gz, gxe, part));
+               float* part, bool b3, hipStream_t st) {
+  if (b3)
+    MF_DISPATCH(F, hipLaunchKernelGGL((km_target_bwd<FF, true>), dim3(geo.nblocks), dim3(256), 0,
+                                      st, geo, y, sc, sh, Rs, Wt1, ghS, gz, gxe, part))
+  else
+    MF_DISPATCH(F, hipLaunchKernelGGL((km_target_bwd<FF, false>), dim3(geo.nblocks), dim3(256), 0,
+                                      st, geo, y, sc, sh, Rs, Wt1, ghS, gz, gxe, part))
   return 0;
 }
 
@@ -1139,10 +1204,16 @@ int source_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
                const float* mean, const float* coef, const float* Rs, const float* Wt1,
                const float* ghS, const float* g_next, const float* mu1, const float* inv1,
-               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN, hipStream_t st) {
-  MF_DISPATCH(F, hipLaunchKernelGGL(km_source_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
-                                    y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghS,
-                                    g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN));
+               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN, bool b3,
+               hipStream_t st) {
+  if (b3)
+    MF_DISPATCH(F, hipLaunchKernelGGL((km_source_bwd<FF, true>), dim3(geo.nblocks), dim3(256), 0,
+                                      st, geo, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+                                      ghS, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN))
+  else
+    MF_DISPATCH(F, hipLaunchKernelGGL((km_source_bwd<FF, false>), dim3(geo.nblocks), dim3(256), 0,
+                                      st, geo, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+                                      ghS, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN))
   return 0;
 }
 
@@ -1150,10 +1221,15 @@ int edge_mlp_bwd(const EdgeGeo& geo, int F, const float* g_tot, const float* alp
                  const float* gam0, const float* gam1, const float* y, const float* xe,
                  const float* xsc, const float* xsh, const float* Ps, const float* PtS,
                  const float* W1, const float* W2, float* gxe, float* gs, float* pW2, float* pW1,
-                 float* pCol, hipStream_t st) {
-  MF_DISPATCH(F, hipLaunchKernelGGL(km_edge_mlp_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
-                                    g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, PtS, W1, W2,
-                                    gxe, gs, pW2, pW1, pCol));
+                 float* pCol, bool b3, hipStream_t st) {
+  if (b3)
+    MF_DISPATCH(F, hipLaunchKernelGGL((km_edge_mlp_bwd<FF, true>), dim3(geo.nblocks), dim3(256), 0,
+                                      st, geo, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, PtS,
+                                      W1, W2, gxe, gs, pW2, pW1, pCol))
+  else
+    MF_DISPATCH(F, hipLaunchKernelGGL((km_edge_mlp_bwd<FF, false>), dim3(geo.nblocks), dim3(256),
+                                      0, st, geo, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps,
+                                      PtS, W1, W2, gxe, gs, pW2, pW1, pCol))
   return 0;
 }
 

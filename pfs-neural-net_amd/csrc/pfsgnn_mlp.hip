@@ -203,12 +203,13 @@ __global__ __launch_bounds__(256, (M <= 3 ? 2 : 1)) void k_mlp_fwd(InSegs S, int
         act[mt][r] = lrelu(z[r]);
       }
     }
+    // two accumulators (even / odd hidden tiles), each in K order
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int mt = 0; mt < M; mt += 2)
 #pragma unroll
-      for (int mt = 0; mt < M; ++mt) {
-        floatx4& y = (mt & 1) ? yo : ye;
-        y = mfma4(w2[mt][r], act[mt][r], y);
+      for (int r = 0; r < 4; ++r) {
+        ye = mfma4(w2[mt][r], act[mt][r], ye);
+        if (mt + 1 < M) yo = mfma4(w2[mt + 1][r], act[mt + 1][r], yo);
       }
     const floatx4 bo = *reinterpret_cast<const floatx4*>(B2 + 4 * kq);
     const floatx4 y = ye + yo + bo;

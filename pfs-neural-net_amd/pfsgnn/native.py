@@ -132,12 +132,13 @@ def lib():
     return _lib
 
 
-EDGE_PATHS = {"valu": 0, "mfma": 1}
+EDGE_PATHS = {"valu": 0, "mfma": 1, "mfma32": 2}
 
 
 def set_edge_path(path):
     """Implementation of the per-edge kernels: "mfma" (default; matrix cores,
-    exact fp32 layer products) or "valu" (fp32 fmaf chains on the vector ALU).
+    exact fp32 forward products, bf16x3 gradient chains), "mfma32" (matrix
+    cores, every layer product exact fp32) or "valu" (fp32 fmaf chains).
     Read at launch time; env PFSGNN_EDGE_PATH sets it when the library loads."""
     if path not in EDGE_PATHS:
         raise ValueError(f"edge path must be one of {sorted(EDGE_PATHS)}, got {path!r}")

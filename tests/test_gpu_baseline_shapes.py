@@ -33,7 +33,7 @@ from test_gpu_parity import check, oracle_step, ours_step  # noqa: E402
 NF = 2394
 
 
-@pytest.fixture(params=["mfma", "valu"])
+@pytest.fixture(params=["mfma", "mfma32", "valu"])
 def prec(request):
     import pfsgnn
     pfsgnn.set_edge_path(request.param)

@@ -44,7 +44,7 @@ def dims(G, NF, NC, F=10):
     return Dims(G, NF, NC, F), EDims(G, NF, NC, F)
 
 
-@pytest.fixture(params=["mfma", "valu"])
+@pytest.fixture(params=["mfma", "mfma32", "valu"])
 def prec(request):
     import pfsgnn
     pfsgnn.set_edge_path(request.param)

@@ -1,14 +1,17 @@
 """HBM traffic per launch of the edge kernels from rocprofv3 FETCH_SIZE /
 WRITE_SIZE passes (tools/prof_pmc.sh), written to profiles/<name>_traffic.json.
 
-FETCH_SIZE / WRITE_SIZE are in KB per dispatch.  WRITE_SIZE reads dword stores
-exactly (MI355X_MICROARCH.md, HBM section).  FETCH_SIZE under-reports wide
-coalesced reads on gfx950 and is uncalibrated for other widths, so it is
-calibrated on OUR access pattern: k_edge_bn_sums reads exactly the two edge
-tensors g and y (2*F*4 bytes per edge, 4-byte-per-lane coalesced rows, the
-pattern of every edge kernel) and nothing else of size.
+Units and corrections (MI355X_MICROARCH.md §HBM, and our own calibration in
+profiles/r02_fetch_calibration.json, made by tools/fetch_calib.hip +
+tools/calib_pmc.sh on known byte counts past the Infinity Cache):
+  * FETCH_SIZE / WRITE_SIZE are KiB per dispatch;
+  * WRITE_SIZE is exact for 4- and 16-byte-per-lane stores;
+  * FETCH_SIZE reads 1/2 of a fully coalesced stream (4 or 16 B/lane alike)
+    and 0.625 of the edge kernels' own pattern (16-lane groups reading 64-byte
+    runs of different channel rows): reads are corrected by 1/0.625 = 1.6;
+    the guide's 2.0 (upper bound) is reported beside it.
 
-    python tools/pmc_traffic.py gpurun_out/pmc3 r01 [E F]
+    python tools/pmc_traffic.py gpurun_out/pmc_xxx r02b128 [E F B]
 """
 import collections
 import csv
@@ -16,9 +19,14 @@ import json
 import os
 import sys
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 d, name = sys.argv[1], sys.argv[2]
 E = int(sys.argv[3]) if len(sys.argv) > 3 else 16 * 2394 * 128
 F = int(sys.argv[4]) if len(sys.argv) > 4 else 10
+B = int(sys.argv[5]) if len(sys.argv) > 5 else 8
+cal = json.load(open(os.path.join(ROOT, "profiles", "r02_fetch_calibration.json")))
+read_cal = cal["edge_read_correction"]
 
 
 def kname(full):
@@ -34,25 +42,45 @@ def per_dispatch(path, counter):
         k = kname(r["Kernel_Name"])
         agg[k] += float(r["Counter_Value"])
         n[k].add(r["Dispatch_Id"])
-    return {k: agg[k] / len(n[k]) * 1e3 for k in agg}   # KB -> bytes
+    return {k: agg[k] / len(n[k]) * 1024.0 for k in agg}   # KiB -> bytes
+
+
+def algorithmic(kernel):
+    """Algorithmic bytes per launch (bench.py:kernel_bytes_per_edge x E)."""
+    import bench
+    per = bench.kernel_bytes_per_edge(F)
+    base = kernel.split("<")[0].replace("km_", "").replace("k_", "")
+    if base not in per:
+        return None
+    if base == "edge_mlp_bwd":          # block 0 writes no input gradient
+        return (per[base] * (B - 1) + 3 * 4 * F) * E / B
+    return per[base] * E
 
 
 fetch = per_dispatch(os.path.join(d, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
 write = per_dispatch(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE")
-cal_key = [k for k in fetch if k.startswith("k_edge_bn_sums")][0]
-read_cal = (2 * F * 4 * E) / fetch[cal_key]
-out = {"E": E, "F": F, "calibration_kernel": cal_key, "read_calibration": read_cal,
-       "note": "traffic_bytes = FETCH_SIZE*read_calibration + WRITE_SIZE, per launch", "kernels": {}}
+out = {"E": E, "F": F, "read_calibration": read_cal,
+       "calibration": "profiles/r02_fetch_calibration.json (rdrows pattern)",
+       "note": "traffic_bytes = FETCH_SIZE*read_calibration + WRITE_SIZE per launch; "
+               "traffic_bytes_guide2x uses the guide's 2.0 read correction (upper bound)",
+       "kernels": {}}
 for k in sorted(fetch):
     if "<" not in k:
         continue
     fb, wb = fetch[k], write.get(k, 0.0)
-    out["kernels"][k] = {"fetch_bytes_raw": fb, "write_bytes": wb,
-                         "traffic_bytes": fb * read_cal + wb}
-os.makedirs("profiles", exist_ok=True)
-path = os.path.join("profiles", f"{name}_traffic.json")
+    alg = algorithmic(k)
+    rec = {"fetch_bytes_raw": fb, "write_bytes": wb, "traffic_bytes": fb * read_cal + wb,
+           "traffic_bytes_guide2x": fb * 2.0 + wb}
+    if alg:
+        rec["algorithmic_bytes"] = alg
+        rec["traffic_over_algorithmic"] = round(rec["traffic_bytes"] / alg, 3)
+        rec["traffic_over_algorithmic_guide2x"] = round(rec["traffic_bytes_guide2x"] / alg, 3)
+    out["kernels"][k] = rec
+os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+path = os.path.join(ROOT, "profiles", f"{name}_traffic.json")
 json.dump(out, open(path, "w"), indent=1)
 for k, v in out["kernels"].items():
-    print(f"{k:28s} traffic {v['traffic_bytes'] / 1e6:8.1f} MB/launch "
-          f"(fetch raw {v['fetch_bytes_raw'] / 1e6:7.1f}, write {v['write_bytes'] / 1e6:7.1f})")
+    if "algorithmic_bytes" in v:
+        print(f"{k:26s} traffic {v['traffic_bytes'] / 1e6:8.1f} MB/launch (x{v['traffic_over_algorithmic']:.2f} "
+              f"of algorithmic {v['algorithmic_bytes'] / 1e6:.1f}; guide 2x: x{v['traffic_over_algorithmic_guide2x']:.2f})")
 print("read calibration", read_cal, "->", path)
