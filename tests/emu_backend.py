@@ -488,6 +488,42 @@ class EmuBackend:
         Gv = torch.full_like(tvar, gscale * (-wvar) * 2.0 / (NF - 1))
         return loss, utils, variance, Gn.reshape(-1), Gf.reshape(-1), Gv
 
+    # ------------------------------------------------------------ layout
+    # (emulation of pfsgnn_layout_analyze / pfsgnn_edges_{to,from}_canonical:
+    # perm[i] = canonical index of the caller's edge i)
+    def layout_analyze(self, edge_index, G, NF, NC):
+        src, tgt = edge_index[0].long().cpu(), edge_index[1].long().cpu()
+        g = src // NF
+        ok = bool(((tgt // NC) == g).all()) and bool((src < G * NF).all())
+        perm = (g * NC + tgt % NC) * NF + src % NF
+        E = G * NF * NC
+        complete = ok and perm.numel() == E and torch.equal(torch.sort(perm).values, torch.arange(E))
+        fm = torch.equal(perm, self._fm_perm(G, NF, NC)) if complete else False
+        ident = torch.equal(perm, torch.arange(E)) if complete else False
+        return perm, complete, fm, ident
+
+    @staticmethod
+    def _fm_perm(G, NF, NC):
+        i = torch.arange(G * NF * NC)
+        g, f, c = i // (NF * NC), (i // NC) % NF, i % NC
+        return (g * NC + c) * NF + f
+
+    def _perm_of(self, lay):
+        if lay.mode == 2:                      # Layout.CANONICAL
+            return torch.arange(lay.G * lay.NF * lay.NC)
+        if lay.mode == 1:                      # Layout.FIBER_MAJOR
+            return self._fm_perm(lay.G, lay.NF, lay.NC)
+        return lay.perm
+
+    def edges_to_canonical(self, x, lay):
+        out = torch.zeros(x.shape[1], x.shape[0], dtype=self.dtype)
+        out[:, self._perm_of(lay)] = x.to(self.dtype).t()
+        return out
+
+    def edges_from_canonical(self, y, sc, sh, lay, rowmajor=True):
+        u = _aff(y, sc, sh)[:, self._perm_of(lay)]
+        return u.t().contiguous() if rowmajor else u.contiguous()
+
     # ------------------------------------------------------------ misc
     def noise_uniform(self, seed, E):
         from noise_ref import uniform_numpy
