@@ -180,6 +180,14 @@ int pfsgnn_mlp_bwd(const float* dY, int N, const float* Yp, const float* mu, con
                    const float* W1, int ldw1, int H, int K, const float* W2, int O, float* dYp,
                    float* dZ, const pfsgnn_oseg* outs, int nout, void* ws, size_t ws_bytes,
                    void* stream);
+/* ---------------------------------------------------------- graph building
+ * edge_index (int64 [2][E], E = G*NF*NC) of G complete bipartite graphs, fiber
+ * ids g*NF + f, class ids g*NC + c.  order 0: fiber-major (train.py:94
+ * cartesian_prod; graph.py:49's sort by source, ties in construction order);
+ * order 1: class-major (graph.py:41-45 construction order).  Replaces
+ * to_Graph's host loops (graph.py:40-51). */
+int pfsgnn_build_complete(int G, int NF, int NC, int order, long long* edge_index, void* stream);
+
 /* out[c][g] = sum (or mean) over the n nodes of graph g of X[c][g*n + i] */
 int pfsgnn_graph_reduce(const float* X, int C, int G, int n, int mean, float* out, void* stream);
 /* the same, accumulated: out[c][g] += sum (or mean) ... (u[batch] gradients, gnn.py:100/153/191) */

@@ -84,6 +84,7 @@ _SIGS = {
                         SZ, P], I),
     "pfsgnn_mlp_bwd": ([P, I, P, P, P, P, FL, P, P, P, P, I, I, I, P, I, P, P, OSEGP, I, P, SZ,
                         P], I),
+    "pfsgnn_build_complete": ([I, I, I, I, P, P], I),
     "pfsgnn_graph_reduce": ([P, I, I, I, I, P, P], I),
     "pfsgnn_graph_reduce_add": ([P, I, I, I, I, P, P], I),
     "pfsgnn_graph_bcast_add": ([P, I, I, I, P, FL, P], I),
@@ -674,6 +675,15 @@ class HipBackend:
               dWd1.data_ptr(), dbd1.data_ptr(), dWd2.data_ptr(), dbd2.data_ptr(), gxe.data_ptr(),
               ws, wsb, _stream())
         return gxe
+
+    # ------------------------------------------------------------ graph building
+    def build_complete(self, G, NF, NC, order=0):
+        """edge_index [2, G*NF*NC] int64 of G complete bipartite graphs on the
+        device; order 0 fiber-major (train.py:94), 1 class-major (graph.py:41)."""
+        ei = torch.empty(2, G * NF * NC, dtype=torch.int64, device=self.device)
+        _call("pfsgnn_build_complete", int(G), int(NF), int(NC), int(order), ei.data_ptr(),
+              _stream())
+        return ei
 
     # ------------------------------------------------------------ layout / optim
     def layout_analyze(self, edge_index, G, NF, NC):

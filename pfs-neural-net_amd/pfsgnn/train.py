@@ -137,7 +137,8 @@ def complete_graph(class_info, nfibers, fdim, lo=2.0, hi=10.0):
     class_info = torch.as_tensor(class_info, dtype=torch.float, device=config.device)
     nclasses = class_info.shape[0]
     x_s = torch.arange(nfibers, dtype=torch.float, device=config.device).reshape(-1, 1)
-    edge_index = torch.cartesian_prod(torch.arange(nfibers), torch.arange(nclasses)).to(config.device).T
+    # torch.cartesian_prod's fiber-major order, built on the device
+    edge_index = backend().build_complete(1, nfibers, nclasses, order=0)
     x_e = lo + (hi - lo) * torch.rand(size=(nfibers * nclasses, fdim)).to(config.device)
     x_u = torch.zeros(1, fdim).to(config.device)
     return BipartiteData(edge_index=edge_index, x_s=x_s, x_t=class_info, x_e=x_e, x_u=x_u)
