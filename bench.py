@@ -31,6 +31,17 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 NF, NC, FDIM = 2394, 128, 10      # overridden by --fibers / --classes
+# what each edge path computes in (include/pfsgnn.h); the
+# node level, reductions, BatchNorm statistics and the loss are fp32 in all
+PRECISION = {
+    "mfma": "fp32 MFMA forward contractions and recompute; backward gradient chains and weight "
+            "gradients bf16x3 (~2^-16 relative per product); fp32 accumulation and edge state",
+    "mfma32": "every per-edge contraction exact fp32 MFMA; weight gradients bf16x3",
+    "valu": "fp32 fmaf chains on the vector ALU; weight gradients bf16x3 MFMA",
+    "bf16y": "mfma32 arithmetic with the edge state rounded to bf16",
+    "bf16m": "every per-edge contraction a single bf16 MFMA, fp32 accumulation and edge state",
+    "bf16": "single-bf16 MFMA contractions and bf16 edge state (BASELINE configs[4])",
+}
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense fp32-input MFMA (= fp32 vector peak)
 
@@ -48,6 +59,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every kernel from Python instead of replaying a captured HIP graph")
+    ap.add_argument("--edge-path", default=os.environ.get("PFSGNN_EDGE_PATH", "mfma"),
+                    help="per-edge kernel precision: mfma (default: fp32 forward, bf16x3 "
+                         "gradient chains), mfma32, valu, bf16y, bf16m, bf16 (configs[4])")
     return ap.parse_args()
 
 
@@ -111,7 +125,7 @@ def pmc_traffic(kernel, E, F):
         except (OSError, ValueError):
             continue
         from pfsgnn import native
-        pre = "km_" if native.get_edge_path() == "mfma" else "k_"
+        pre = "k_" if native.get_edge_path() == "valu" else "km_"
         key = f"{pre}{kernel}<{F}>"
         if d.get("E") == E and d.get("F") == F and key in d.get("kernels", {}):
             return d["kernels"][key]["traffic_bytes"], os.path.basename(path)
@@ -203,6 +217,7 @@ def main():
     config.device = device
 
     G, B = args.graphs, args.blocks
+    native.set_edge_path(args.edge_path)
     torch.manual_seed(0)
     gnn = pfsgnn.GNN(B=B, Fdim=FDIM, T=NC, F_s=1, F_t=2).to(device)
     gnn.train()
@@ -342,8 +357,10 @@ def main():
             "metric": metric,
             "value": value, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if args.edge_path in ("bf16", "bf16m") else "f32",
             "data": "synthetic",
+            "precision": PRECISION[args.edge_path],
             "config": {"workload": f"{G} complete bipartite {NF}x{NC} graphs per GPU, {B} "
                                    f"message-passing blocks, Fdim {FDIM}; full training step "
                                    f"(GNN fwd + train.py loss + bwd + Adam)",

@@ -48,12 +48,21 @@ size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F);
  *       chains (W^T g) and the weight gradients on v_mfma_f32_16x16x16_bf16
  *       with split operands (bf16 hi + lo, ~2^-16 relative per product);
  *   PFSGNN_EDGE_MFMA_F32 -- the same with the gradient chains in exact fp32;
- *   PFSGNN_EDGE_VALU -- fp32 fmaf chains on the vector ALU (pfsgnn_edge.hip).
- * All produce the same outputs to the parity tolerance; node-level ops,
- * reductions and the loss are shared. */
+ *   PFSGNN_EDGE_VALU -- fp32 fmaf chains on the vector ALU (pfsgnn_edge.hip);
+ *   PFSGNN_EDGE_BF16Y -- MFMA_F32 arithmetic with the edge state y rounded to
+ *       bf16 where it is stored (the numerics of bf16 edge-state storage);
+ *   PFSGNN_EDGE_BF16 -- every per-edge contraction a single bf16 MFMA (fp32
+ *       accumulation) + bf16 edge state (BASELINE configs[4]; Fdim 10);
+ *   PFSGNN_EDGE_BF16_MFMA -- the bf16 contractions with the fp32 edge state.
+ * The fp32-class paths (MFMA, MFMA_F32, VALU) produce the same outputs to the
+ * parity tolerance; the bf16 paths' deviation is measured, not bounded
+ * (DESIGN.md §Numerics).  Node-level ops, reductions and the loss are shared. */
 #define PFSGNN_EDGE_VALU 0
 #define PFSGNN_EDGE_MFMA 1
 #define PFSGNN_EDGE_MFMA_F32 2
+#define PFSGNN_EDGE_BF16Y 3
+#define PFSGNN_EDGE_BF16 4
+#define PFSGNN_EDGE_BF16_MFMA 5
 int pfsgnn_set_edge_path(int path);
 int pfsgnn_get_edge_path(void);
 /* Grid the current edge path launches for a batch (host-only query, for tests

@@ -1121,8 +1121,12 @@ void fiber_finish(const EdgeGeo& geo, int C, const float* dst, float* out, hipSt
 
 int g_path = PFSGNN_EDGE_MFMA;
 bool use_mfma() { return g_path != PFSGNN_EDGE_VALU; }
-// bf16x3 gradient chains in the MFMA backward kernels (PFSGNN_EDGE_MFMA)
-bool use_b3() { return g_path == PFSGNN_EDGE_MFMA; }
+// precision of the MFMA kernels' contractions (pfsgnn_mfma.h) and bf16 edge state
+int mf_prec() {
+  return g_path == PFSGNN_EDGE_MFMA ? 1
+         : (g_path == PFSGNN_EDGE_BF16 || g_path == PFSGNN_EDGE_BF16_MFMA) ? 2 : 0;
+}
+int mf_bfy() { return g_path == PFSGNN_EDGE_BF16Y || g_path == PFSGNN_EDGE_BF16 ? 1 : 0; }
 // MFMA blocks stage their class-table rows in LDS: at most MAX_CPS classes each
 EdgeGeo geo_mfma(int G, int NF, int NC) {
   const long long groups = (long long)G * ((NF + 63) / 64);
@@ -1142,9 +1146,9 @@ EdgeGeo geo_for(int G, int NF, int NC) {
 }  // namespace
 
 extern "C" int pfsgnn_set_edge_path(int path) {
-  if (path != PFSGNN_EDGE_VALU && path != PFSGNN_EDGE_MFMA && path != PFSGNN_EDGE_MFMA_F32)
+  if (path < PFSGNN_EDGE_VALU || path > PFSGNN_EDGE_BF16_MFMA)
     return pf::fail("pfsgnn_set_edge_path",
-                    "path must be PFSGNN_EDGE_VALU, PFSGNN_EDGE_MFMA or PFSGNN_EDGE_MFMA_F32");
+                    "path must be PFSGNN_EDGE_VALU, _MFMA, _MFMA_F32, _BF16Y, _BF16 or _BF16_MFMA");
   g_path = path;
   return 0;
 }
@@ -1202,7 +1206,7 @@ extern "C" int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe
   if (use_mfma()) {
     PF_REQUIRE(part, "pfsgnn_edge_mlp_fwd", "workspace too small");
     { pf::Timer tm_("edge_mlp_fwd", st);
-    if (int rc = pfm::edge_mlp_fwd(geo, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part, st)) return rc;
+    if (int rc = pfm::edge_mlp_fwd(geo, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part, mf_prec(), mf_bfy(), st)) return rc;
     tm_.end(); }
     hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(256), 0, st, part, geo.nblocks, F, geo.E,
                        mu, var);
@@ -1234,7 +1238,7 @@ extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, c
   if (use_mfma()) {
     PF_REQUIRE(partS, "pfsgnn_source_fwd", "workspace too small");
     pf::Timer tm_("source_fwd", st);
-    if (int rc = pfm::source_fwd(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, partS, st)) return rc;
+    if (int rc = pfm::source_fwd(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, partS, mf_prec(), st)) return rc;
     tm_.end();
   } else {
   const float* QtT = class_rows(Qt, C, geo, w, st);
@@ -1263,7 +1267,7 @@ extern "C" int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, c
   hipStream_t st = as_stream(stream);
   { pf::Timer tm_("target_fwd", st);
   if (use_mfma()) {
-    if (int rc = pfm::target_fwd(geo, F, y, sc, sh, Rs, Wt1, part, st)) return rc;
+    if (int rc = pfm::target_fwd(geo, F, y, sc, sh, Rs, Wt1, part, mf_prec(), st)) return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
                                    sc, sh, Rs, Wt1, part));
@@ -1290,7 +1294,7 @@ extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, c
   PF_REQUIRE(part && gz && ghT, "pfsgnn_target_bwd", "workspace too small");
   { pf::Timer tm_("target_bwd", st);
   if (use_mfma()) {
-    if (int rc = pfm::target_bwd(geo, F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part, use_b3(), st)) return rc;
+    if (int rc = pfm::target_bwd(geo, F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part, mf_prec(), st)) return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
                                    sc, sh, Rs, Wt1, ghT, gz, gxe, part));
@@ -1332,7 +1336,7 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
   { pf::Timer tm_("source_bwd", st);
   if (mfma) {
     if (int rc = pfm::source_bwd(geo, F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT,
-                                 g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, use_b3(), st))
+                                 g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, mf_prec(), st))
       return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_source_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
@@ -1399,7 +1403,7 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
     PF_REQUIRE(pW2 && pW1 && pCol && gs, "pfsgnn_edge_mlp_bwd", "workspace too small");
     pf::Timer tm_("edge_mlp_bwd", st);
     if (int rc = pfm::edge_mlp_bwd(geo, F, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1,
-                                   W2, gxe, gs, pW2, pW1, pCol, use_b3(), st))
+                                   W2, gxe, gs, pW2, pW1, pCol, mf_prec(), st))
       return rc;
     tm_.end();
   } else {

@@ -11,34 +11,35 @@
 namespace pfm {
 
 // grid of the MFMA kernels: 4 waves x 16 fibers per block (64 fibers, as the
-// fp32 kernels), KS class splits to about this many blocks.  `b3`: the
-// backward kernels run their gradient chains in bf16x3 (PFSGNN_EDGE_MFMA)
-// instead of exact fp32 (PFSGNN_EDGE_MFMA_F32)
+// fp32 kernels), KS class splits to about this many blocks.  `prec`: 0 exact
+// fp32 contractions, 1 bf16x3 gradient chains in the backward kernels, 2 single
+// bf16 everywhere (pfsgnn_mfma.hip, PREC); `bfy`: round the edge state y to
+// bf16 at its store (bf16 edge-state numerics)
 static constexpr int TARGET_BLOCKS = 2048;
 // classes per block at most (the block's class-table rows are staged in LDS)
 static constexpr int MAX_CPS = 64;
 
 int edge_mlp_fwd(const EdgeGeo& geo, int F, const float* xe, const float* xsc, const float* xsh,
                  const float* Ps, const float* PtS, const float* W1, const float* W2,
-                 const float* b2, float* y, float* part, hipStream_t st);
+                 const float* b2, float* y, float* part, int prec, int bfy, hipStream_t st);
 int source_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
-               float* partS, hipStream_t st);
+               float* partS, int prec, hipStream_t st);
 int target_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
-               const float* Rs, const float* Wt1, float* part, hipStream_t st);
+               const float* Rs, const float* Wt1, float* part, int prec, hipStream_t st);
 int target_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* Rs, const float* Wt1, const float* ghS, float* gz, float* gxe,
-               float* part, bool b3, hipStream_t st);
+               float* part, int prec, hipStream_t st);
 int source_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
                const float* mean, const float* coef, const float* Rs, const float* Wt1,
                const float* ghS, const float* g_next, const float* mu1, const float* inv1,
-               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN, bool b3,
+               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN, int prec,
                hipStream_t st);
 int edge_mlp_bwd(const EdgeGeo& geo, int F, const float* g_tot, const float* alpha,
                  const float* gam0, const float* gam1, const float* y, const float* xe,
                  const float* xsc, const float* xsh, const float* Ps, const float* PtS,
                  const float* W1, const float* W2, float* gxe, float* gs, float* pW2, float* pW1,
-                 float* pCol, bool b3, hipStream_t st);
+                 float* pCol, int prec, hipStream_t st);
 
 }  // namespace pfm

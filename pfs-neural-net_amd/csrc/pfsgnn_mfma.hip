@@ -187,6 +187,60 @@ struct LayerB3 {
   }
 };
 
+// ------------------------------------------------------------ bf16 layer
+// y (+)= W x with every product a single v_mfma_f32_16x16x16_bf16 on bf16
+// operands (RNE), fp32 accumulation: the "bf16" edge path (BASELINE configs[4],
+// PFSGNN_EDGE_BF16) -- one MFMA per K-tile where LayerF issues GM<K>::RPG.
+__device__ __forceinline__ s16x4 hi4(const floatx4& v) {
+  const b16x4 h = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  return __builtin_bit_cast(s16x4, h);
+}
+template <int M, int K>
+struct LayerB1 {
+  static constexpr int MT = GM<M>::NT, KT = GM<K>::NT;
+  s16x4 a[MT][KT];
+  template <class Fn>
+  __device__ __forceinline__ void load(Fn fn, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+        floatx4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ro = GM<M>::mrow(t, i), ri = GM<K>::row(g, 4 * u + j);
+          v[j] = (ro >= 0 && ri >= 0) ? fn(ro, ri) : 0.f;
+        }
+        a[t][u] = hi4(v);
+      }
+  }
+  __device__ __forceinline__ void apply(const Fr (&x)[KT], floatx4 (&y)[MT]) const {
+#pragma unroll
+    for (int u = 0; u < KT; ++u)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) y[t] = mf(a[t][u], x[u].h, y[t]);
+  }
+  __device__ __forceinline__ void apply(const floatx4 (&x)[KT], floatx4 (&y)[MT]) const {
+#pragma unroll
+    for (int u = 0; u < KT; ++u) {
+      const s16x4 xb = hi4(x[u]);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) y[t] = mf(a[t][u], xb, y[t]);
+    }
+  }
+};
+
+// Precision of the per-edge contractions (PREC, per edge path):
+//   0 exact fp32 everywhere (PFSGNN_EDGE_MFMA_F32, _BF16Y);
+//   1 forward fp32, backward gradient chains bf16x3 (PFSGNN_EDGE_MFMA);
+//   2 every contraction single bf16 (PFSGNN_EDGE_BF16).
+template <int PREC, int M, int K>
+using FwdLayer = std::conditional_t<PREC == 2, LayerB1<M, K>, LayerF<M, K>>;
+template <int PREC, int M, int K>
+using GradLayer = std::conditional_t<PREC == 0, LayerF<M, K>,
+                                     std::conditional_t<PREC == 1, LayerB3<M, K>, LayerB1<M, K>>>;
+
 // Wave-private image of one 16x16 bf16 block, [16 edges][16 slots] (32-byte
 // rows, the four 8-byte chunks of row e XOR-swizzled by e>>2: conflict-free b64
 // writes and tr reads).  Lane (g, j) writes its slots 4g..4g+3 of edge j; a
@@ -444,7 +498,7 @@ __device__ __forceinline__ floatx4 edge_in(const floatx4& raw, const bool (&fm)[
 // y = W2 lrelu(Ps[f] + Pt[c] + W1[:, 2F:3F] x) + b2 per edge (gnn.py:86-101 with
 // the node parts of the first Linear precomputed per node); Welford partials of
 // y per block for the (double) BatchNorm.
-template <int F>
+template <int F, int PREC>
 __global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float* __restrict__ xe,
                                                        const float* __restrict__ xsc,
                                                        const float* __restrict__ xsh,
@@ -454,14 +508,14 @@ __global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float*
                                                        const float* __restrict__ W2,
                                                        const float* __restrict__ b2,
                                                        float* __restrict__ y,
-                                                       float* __restrict__ part) {
+                                                       float* __restrict__ part, int bfy) {
   constexpr int H = 4 * F, NT = GM<H>::NT;
   MF_GEO
   __shared__ __attribute__((aligned(16))) float ptl[MF_MAX_CPS * ClassRows<H>::CP];
   ClassRows<H>::stage(ptl, PtS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
-  LayerF<H, F> L1;
+  FwdLayer<PREC, H, F> L1;
   L1.load([&](int h, int k) { return W1[h * 4 * F + 2 * F + k]; }, lane);
-  LayerF<F, H> L2;
+  FwdLayer<PREC, F, H> L2;
   L2.load([&](int o, int h) { return W2[o * H + h]; }, lane);
   floatx4 ps[NT];
 #pragma unroll
@@ -488,6 +542,12 @@ __global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float*
     lrelu_act<H>(z, a);
     floatx4 yo[1] = {bb};
     L2.apply(a, yo);
+    if (bfy) {  // the edge state at bf16 (PFSGNN_EDGE_BF16Y / _BF16): every consumer
+                // reads exactly what a bf16 store would hold
+      const s16x4 h = hi4(yo[0]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) yo[0][r] = bf_f(h[r]);
+    }
     st_frows<F>(y, eo, RB, g4, fvalid, yo[0]);
     if (fvalid) {
       cnt += 1.f;
@@ -549,7 +609,7 @@ __global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float*
 // message m = Ws2 lrelu(Qt[c] + Ws1[:, F:2F] x) + bs2 (gnn.py:136-137) and its
 // per-fiber centred moments over the class range by Pebay's one-pass update
 // (the wave walks every class of its 16 fibers: no cross-wave merge).
-template <int F>
+template <int F, int PREC>
 __global__ __launch_bounds__(256) void km_source_fwd(EdgeGeo geo, const float* __restrict__ y,
                                                      const float* __restrict__ sc,
                                                      const float* __restrict__ sh,
@@ -562,9 +622,9 @@ __global__ __launch_bounds__(256) void km_source_fwd(EdgeGeo geo, const float* _
   MF_GEO
   __shared__ __attribute__((aligned(16))) float qtl[MF_MAX_CPS * ClassRows<C>::CP];
   ClassRows<C>::stage(qtl, QtS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
-  LayerF<C, F> L1;
+  FwdLayer<PREC, C, F> L1;
   L1.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
-  LayerF<C, C> L2;
+  FwdLayer<PREC, C, C> L2;
   L2.load([&](int o, int h) { return Ws2[o * C + h]; }, lane);
   floatx4 bias[NT];
 #pragma unroll
@@ -627,7 +687,7 @@ __global__ __launch_bounds__(256) void km_source_fwd(EdgeGeo geo, const float* _
 // ============================================================ TModel fwd
 // a = lrelu(Rs[f] + Wt1[:, F:2F] x) per edge and its per-class sum over fibers
 // (gnn.py:188-190; the second Linear runs after the sum, on the node side).
-template <int F>
+template <int F, int PREC>
 __global__ __launch_bounds__(256) void km_target_fwd(EdgeGeo geo, const float* __restrict__ y,
                                                      const float* __restrict__ sc,
                                                      const float* __restrict__ sh,
@@ -637,7 +697,7 @@ __global__ __launch_bounds__(256) void km_target_fwd(EdgeGeo geo, const float* _
   constexpr int C = 2 * F, NT = GM<C>::NT;
   MF_GEO
   __shared__ float colbuf[COL_CH * 4 * C];
-  LayerF<C, F> L1;
+  FwdLayer<PREC, C, F> L1;
   L1.load([&](int h, int k) { return Wt1[h * 2 * F + F + k]; }, lane);
   floatx4 rs[NT];
 #pragma unroll
@@ -678,7 +738,7 @@ __global__ __launch_bounds__(256) void km_target_fwd(EdgeGeo geo, const float* _
 // ============================================================ TModel bwd
 // g_z = g_hsum[c] * lrelu'(z) per edge; per-fiber sums of g_z (-> g_Rs), the
 // edge-input gradient Wt1[:, F:2F]^T g_z (optional) and dWt1[:, F:2F] += g_z x^T.
-template <int F, bool B3>
+template <int F, int PREC>
 __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* __restrict__ y,
                                                      const float* __restrict__ sc,
                                                      const float* __restrict__ sh,
@@ -696,9 +756,9 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
   __shared__ __attribute__((aligned(16))) float ghl[MF_MAX_CPS * ClassRows<C>::CP];
   ClassRows<C>::stage(ghl, ghS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
   short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
-  LayerF<C, F> L1;
+  FwdLayer<PREC == 2 ? 2 : 0, C, F> L1;
   L1.load([&](int h, int k) { return Wt1[h * 2 * F + F + k]; }, lane);
-  std::conditional_t<B3, LayerB3<F, C>, LayerF<F, C>> LT;
+  GradLayer<PREC, F, C> LT;
   LT.load([&](int k, int h) { return gxe ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
   floatx4 rs[NT], accF[NT], accW[NT];
 #pragma unroll
@@ -736,7 +796,7 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
     for (int tt = 0; tt < NT; ++tt) sgz[tt] = split(gz[tt]);
     if (gxe) {
       floatx4 gx[1] = {zero4()};
-      if constexpr (B3) LT.apply(sgz, gx); else LT.apply(gz, gx);
+      if constexpr (PREC >= 1) LT.apply(sgz, gx); else LT.apply(gz, gx);
       st_frows<F>(gxe, eo, RB, g4, fvalid, gx[0]);
     }
     lds_order();
@@ -770,7 +830,7 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
 // message MLP; plus TModel's recomputed input gradient, the downstream edge
 // gradient and the edge BatchNorm's two gradient sums.  dWs2 += g_m a^T,
 // dbs2 += g_m, dWs1[:, F:2F] += g_zs x^T, per-class sums of g_zs (-> g_Qt).
-template <int F, bool B3>
+template <int F, int PREC>
 __global__ __launch_bounds__(256, 2) void km_source_bwd(
     EdgeGeo geo, const float* __restrict__ y, const float* __restrict__ sc,
     const float* __restrict__ sh, const float* __restrict__ QtS, const float* __restrict__ Ws1,
@@ -799,15 +859,15 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   const long long CNS = (long long)C * NS;
   const bool tpart = Rs != nullptr;
 
-  LayerF<C, F> L1s, L1t;
+  FwdLayer<PREC == 2 ? 2 : 0, C, F> L1s, L1t;
   L1s.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
   L1t.load([&](int h, int k) { return tpart ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
-  LayerF<C, C> L2;
+  FwdLayer<PREC == 2 ? 2 : 0, C, C> L2;
   L2.load([&](int o, int h) { return Ws2[o * C + h]; }, lane);
-  // gradient chains: bf16x3 (PFSGNN_EDGE_MFMA) or exact fp32 (PFSGNN_EDGE_MFMA_F32)
-  std::conditional_t<B3, LayerB3<C, C>, LayerF<C, C>> L2T;
+  // gradient chains: exact fp32, bf16x3 or bf16 by PREC
+  GradLayer<PREC, C, C> L2T;
   L2T.load([&](int h, int o) { return Ws2[o * C + h]; }, lane);
-  std::conditional_t<B3, LayerB3<F, C>, LayerF<F, C>> L1sT, L1tT;
+  GradLayer<PREC, F, C> L1sT, L1tT;
   L1sT.load([&](int k, int h) { return Ws1[h * 2 * F + F + k]; }, lane);
   L1tT.load([&](int k, int h) { return tpart ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
   floatx4 rs[NT], bias[NT], mn[NT], q0[NT], q1[NT], q2[NT], q3[NT];
@@ -876,7 +936,7 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     floatx4 gz[NT];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) gz[tt] = zero4();
-    if constexpr (B3) L2T.apply(sgm, gz); else L2T.apply(gm, gz);
+    if constexpr (PREC >= 1) L2T.apply(sgm, gz); else L2T.apply(gm, gz);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
 #pragma unroll
@@ -884,7 +944,7 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
       sgz[tt] = split(gz[tt]);
     }
     floatx4 g[1] = {zero4()};
-    if constexpr (B3) L1sT.apply(sgz, g); else L1sT.apply(gz, g);
+    if constexpr (PREC >= 1) L1sT.apply(sgz, g); else L1sT.apply(gz, g);
     if (tpart) {  // TModel's per-edge input gradient, recomputed (gnn.py:188-190)
       floatx4 zt[NT];
 #pragma unroll
@@ -896,7 +956,7 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
 #pragma unroll
         for (int r = 0; r < 4; ++r) zt[tt][r] = (fvalid && r < GM<C>::nreg(tt)) ? gh[r] * dlrelu(zt[tt][r]) : 0.f;
       }
-      if constexpr (B3) {
+      if constexpr (PREC >= 1) {
         Fr szt[NT];
 #pragma unroll
         for (int tt = 0; tt < NT; ++tt) szt[tt] = split(zt[tt]);
@@ -999,7 +1059,7 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
 // dW1[:, 2F:3F] += g_z x^T, per-fiber (-> g_Ps) and per-class (-> g_Pt) sums of
 // g_z, and the edge-input gradient W1[:, 2F:3F]^T g_z when the block has an
 // upstream edge input.
-template <int F, bool B3>
+template <int F, int PREC>
 __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
     EdgeGeo geo, const float* __restrict__ g_tot, const float* __restrict__ alpha,
     const float* __restrict__ gam0, const float* __restrict__ gam1, const float* __restrict__ y,
@@ -1022,12 +1082,12 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
   short* im_gz = im_a + NT * 2 * IMG_SHORTS;
   short* im_x = im_gz + NT * 2 * IMG_SHORTS;
 
-  LayerF<H, F> L1;
+  FwdLayer<PREC == 2 ? 2 : 0, H, F> L1;
   L1.load([&](int h, int k) { return W1[h * 4 * F + 2 * F + k]; }, lane);
-  // gradient chains: bf16x3 (PFSGNN_EDGE_MFMA) or exact fp32 (PFSGNN_EDGE_MFMA_F32)
-  std::conditional_t<B3, LayerB3<H, F>, LayerF<H, F>> L2T;
+  // gradient chains: exact fp32, bf16x3 or bf16 by PREC
+  GradLayer<PREC, H, F> L2T;
   L2T.load([&](int h, int o) { return W2[o * H + h]; }, lane);
-  std::conditional_t<B3, LayerB3<F, H>, LayerF<F, H>> L1T;
+  GradLayer<PREC, F, H> L1T;
   L1T.load([&](int k, int h) { return gxe ? W1[h * 4 * F + 2 * F + k] : 0.f; }, lane);
   floatx4 ps[NT], accF[NT], accW1[NT], accW2[NT];
 #pragma unroll
@@ -1070,7 +1130,7 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
     L1.apply(x, z);
     lrelu_act<H>(z, a);
     const Fr sgy[1] = {split(gy[0])};
-    if constexpr (B3) L2T.apply(sgy, gz); else L2T.apply(gy, gz);
+    if constexpr (PREC >= 1) L2T.apply(sgy, gz); else L2T.apply(gy, gz);
     Fr sgz[NT];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
@@ -1081,7 +1141,7 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
     }
     if (gxe) {
       floatx4 gx[1] = {zero4()};
-      if constexpr (B3) L1T.apply(sgz, gx); else L1T.apply(gz, gx);
+      if constexpr (PREC >= 1) L1T.apply(sgz, gx); else L1T.apply(gz, gx);
       st_frows<F>(gxe, eo, RB, g4, fvalid, gx[0]);
     }
     lds_order();
@@ -1155,48 +1215,51 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
 }  // namespace
 
 // ============================================================ host launchers
-#define MF_DISPATCH(F, ...)                                  \
-  switch (F) {                                               \
-    case 8: { constexpr int FF = 8; __VA_ARGS__; } break;    \
-    case 10: { constexpr int FF = 10; __VA_ARGS__; } break;  \
-    case 16: { constexpr int FF = 16; __VA_ARGS__; } break;  \
-    default: return pf::fail("pfsgnn mfma", "unsupported F");\
+// Instantiations: Fdim 8, 10, 16 for the fp32 / bf16x3 precisions (PREC 0, 1);
+// the single-bf16 path (PREC 2, BASELINE configs[4]) at Fdim 10.
+#define MF_CASE(FF, PP, K, ...)                                                   \
+  case FF * 4 + PP: {                                                             \
+    hipLaunchKernelGGL((K<FF, PP>), dim3(geo.nblocks), dim3(256), 0, st, geo,     \
+                       __VA_ARGS__);                                              \
+  } break;
+#define MF_LAUNCH(F, P, K, ...)                                                   \
+  switch ((F) * 4 + (P)) {                                                        \
+    MF_CASE(8, 0, K, __VA_ARGS__) MF_CASE(8, 1, K, __VA_ARGS__)                  \
+    MF_CASE(10, 0, K, __VA_ARGS__) MF_CASE(10, 1, K, __VA_ARGS__)                \
+    MF_CASE(10, 2, K, __VA_ARGS__)                                                \
+    MF_CASE(16, 0, K, __VA_ARGS__) MF_CASE(16, 1, K, __VA_ARGS__)                \
+    default: return pf::fail("pfsgnn mfma", "unsupported Fdim for this edge path"); \
   }
 
 namespace pfm {
 
+// forward kernels only distinguish single-bf16 (2) from fp32 (0, 1)
+static inline int fwd_prec(int prec) { return prec == 2 ? 2 : 0; }
+
 int edge_mlp_fwd(const EdgeGeo& geo, int F, const float* xe, const float* xsc, const float* xsh,
                  const float* Ps, const float* PtS, const float* W1, const float* W2,
-                 const float* b2, float* y, float* part, hipStream_t st) {
-  MF_DISPATCH(F, hipLaunchKernelGGL(km_edge_mlp_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
-                                    xe, xsc, xsh, Ps, PtS, W1, W2, b2, y, part));
+                 const float* b2, float* y, float* part, int prec, int bfy, hipStream_t st) {
+  MF_LAUNCH(F, fwd_prec(prec), km_edge_mlp_fwd, xe, xsc, xsh, Ps, PtS, W1, W2, b2, y, part, bfy)
   return 0;
 }
 
 int source_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
-               float* partS, hipStream_t st) {
-  MF_DISPATCH(F, hipLaunchKernelGGL(km_source_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
-                                    y, sc, sh, QtS, Ws1, Ws2, bs2, partS));
+               float* partS, int prec, hipStream_t st) {
+  MF_LAUNCH(F, fwd_prec(prec), km_source_fwd, y, sc, sh, QtS, Ws1, Ws2, bs2, partS)
   return 0;
 }
 
 int target_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
-               const float* Rs, const float* Wt1, float* part, hipStream_t st) {
-  MF_DISPATCH(F, hipLaunchKernelGGL(km_target_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
-                                    y, sc, sh, Rs, Wt1, part));
+               const float* Rs, const float* Wt1, float* part, int prec, hipStream_t st) {
+  MF_LAUNCH(F, fwd_prec(prec), km_target_fwd, y, sc, sh, Rs, Wt1, part)
   return 0;
 }
 
 int target_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* Rs, const float* Wt1, const float* ghS, float* gz, float* gxe,
-               float* part, bool b3, hipStream_t st) {
-  if (b3)
-    MF_DISPATCH(F, hipLaunchKernelGGL((km_target_bwd<FF, true>), dim3(geo.nblocks), dim3(256), 0,
-                                      st, geo, y, sc, sh, Rs, Wt1, ghS, gz, gxe, part))
-  else
-    MF_DISPATCH(F, hipLaunchKernelGGL((km_target_bwd<FF, false>), dim3(geo.nblocks), dim3(256), 0,
-                                      st, geo, y, sc, sh, Rs, Wt1, ghS, gz, gxe, part))
+               float* part, int prec, hipStream_t st) {
+  MF_LAUNCH(F, prec, km_target_bwd, y, sc, sh, Rs, Wt1, ghS, gz, gxe, part)
   return 0;
 }
 
@@ -1204,16 +1267,10 @@ int source_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
                const float* mean, const float* coef, const float* Rs, const float* Wt1,
                const float* ghS, const float* g_next, const float* mu1, const float* inv1,
-               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN, bool b3,
+               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN, int prec,
                hipStream_t st) {
-  if (b3)
-    MF_DISPATCH(F, hipLaunchKernelGGL((km_source_bwd<FF, true>), dim3(geo.nblocks), dim3(256), 0,
-                                      st, geo, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
-                                      ghS, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN))
-  else
-    MF_DISPATCH(F, hipLaunchKernelGGL((km_source_bwd<FF, false>), dim3(geo.nblocks), dim3(256), 0,
-                                      st, geo, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
-                                      ghS, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN))
+  MF_LAUNCH(F, prec, km_source_bwd, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghS,
+            g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN)
   return 0;
 }
 
@@ -1221,15 +1278,9 @@ int edge_mlp_bwd(const EdgeGeo& geo, int F, const float* g_tot, const float* alp
                  const float* gam0, const float* gam1, const float* y, const float* xe,
                  const float* xsc, const float* xsh, const float* Ps, const float* PtS,
                  const float* W1, const float* W2, float* gxe, float* gs, float* pW2, float* pW1,
-                 float* pCol, bool b3, hipStream_t st) {
-  if (b3)
-    MF_DISPATCH(F, hipLaunchKernelGGL((km_edge_mlp_bwd<FF, true>), dim3(geo.nblocks), dim3(256), 0,
-                                      st, geo, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, PtS,
-                                      W1, W2, gxe, gs, pW2, pW1, pCol))
-  else
-    MF_DISPATCH(F, hipLaunchKernelGGL((km_edge_mlp_bwd<FF, false>), dim3(geo.nblocks), dim3(256),
-                                      0, st, geo, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps,
-                                      PtS, W1, W2, gxe, gs, pW2, pW1, pCol))
+                 float* pCol, int prec, hipStream_t st) {
+  MF_LAUNCH(F, prec, km_edge_mlp_bwd, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, PtS, W1, W2,
+            gxe, gs, pW2, pW1, pCol)
   return 0;
 }
 

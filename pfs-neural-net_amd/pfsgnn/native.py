@@ -133,13 +133,16 @@ def lib():
     return _lib
 
 
-EDGE_PATHS = {"valu": 0, "mfma": 1, "mfma32": 2}
+EDGE_PATHS = {"valu": 0, "mfma": 1, "mfma32": 2, "bf16y": 3, "bf16": 4, "bf16m": 5}
 
 
 def set_edge_path(path):
     """Implementation of the per-edge kernels: "mfma" (default; matrix cores,
     exact fp32 forward products, bf16x3 gradient chains), "mfma32" (matrix
-    cores, every layer product exact fp32) or "valu" (fp32 fmaf chains).
+    cores, every layer product exact fp32), "valu" (fp32 fmaf chains), "bf16y"
+    (mfma32 with the edge state rounded to bf16), "bf16m" (single-bf16 MFMA
+    contractions) or "bf16" (bf16m + bf16 edge state; BASELINE configs[4],
+    Fdim 10).
     Read at launch time; env PFSGNN_EDGE_PATH sets it when the library loads."""
     if path not in EDGE_PATHS:
         raise ValueError(f"edge path must be one of {sorted(EDGE_PATHS)}, got {path!r}")
