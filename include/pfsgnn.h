@@ -237,6 +237,64 @@ int pfsgnn_bn2_bwd_coef(const float* Sg, const float* Sgx, const float* mu1, con
  * (mean, c2, c3, c4); gst [4C][NS] = dL/d(mean, std, skew, kurt). */
 int pfsgnn_moment_coef(const float* mom, const float* gst, int C, int NS, int n,
                        float* coef, void* stream);
+/* the same for a general graph: fiber s's count is fib_ptr[s+1] - fib_ptr[s]
+ * (clamped at 1, as torch_scatter's mean; gnn.py:140-144) */
+int pfsgnn_moment_coef_seg(const float* mom, const float* gst, int C, int NS, const int* fib_ptr,
+                           float* coef, void* stream);
+
+/* ------------------------------------------------ general (sparse) bipartite graphs
+ * The reference's data model takes any edge_index (gnn.py:7-47; PyG batching
+ * gnn.py:32-47) and its scatters reduce over arbitrary src / tgt (gnn.py:140-144
+ * per fiber, gnn.py:190 per class).  A batch that is not complete bipartite is
+ * laid out once by pfsgnn_sparse_layout; every edge tensor of the step is then
+ * channel-major [C][E] in "position" order (edges sorted stably by fiber), and
+ * the per-edge MLPs run as node-table gathers + pfsgnn_lin over E columns, the
+ * scatters as the deterministic segment kernels below (block per segment,
+ * fixed-order trees: bitwise reproducible run to run).  int32 indices: E, G*NF,
+ * G*NC < 2^31.  (Replaces torch_scatter.scatter / x[src] / x[tgt] of gnn.py:100,
+ * 136-144, 188-190 for such graphs.) */
+size_t pfsgnn_sparse_layout_ws_bytes(long long E);
+/* edge_index int64 [2][E] (row 0 fiber ids g*NF+f, row 1 class ids g*NC+c).
+ * Outputs (device int32): src_p/tgt_p [E] fiber / class of each position,
+ * user_of [E] the caller's edge at each position, fib_ptr [G*NF+1] (CSR by
+ * fiber over positions), cls_ord [E] positions sorted stably by class and
+ * cls_ptr [G*NC+1] (CSR by class over cls_ord).  status[0] != 0 after the call
+ * iff some edge is out of range or joins nodes of different graphs (the
+ * caller must reject the batch). */
+int pfsgnn_sparse_layout(const long long* edge_index, long long E, int G, int NF, int NC,
+                         int* src_p, int* tgt_p, int* user_of, int* fib_ptr, int* cls_ord,
+                         int* cls_ptr, int* status, void* ws, size_t ws_bytes, void* stream);
+/* out[c][e] = X[c][idx[e]] (mode 0), += X[c][idx[e]] (mode 1), or
+ * X[c][idx[e]] * lrelu'(Z[c][e]) (mode 2); X is a node table [C][N] */
+int pfsgnn_gather_cols(const float* X, int C, int N, const int* idx, long long E, const float* Z,
+                       int mode, float* out, void* stream);
+/* out[c][s] (+)= sum over the segment's positions p in [ptr[s], ptr[s+1]) of
+ * act(X[c][ord ? ord[p] : p]); act = lrelu (0.1) if `act`, identity otherwise */
+int pfsgnn_segment_sum(const float* X, int C, long long E, const int* ord, const int* ptr,
+                       int nseg, int act, float* out, int add, void* stream);
+/* SModel moments per fiber (gnn.py:140-151): mom [4][C][nseg] = (mean, c2, c3,
+ * c4) and the node_mlp_2 inputs hs [4C][nseg] = (mean, std, skew, kurt);
+ * an empty fiber gives zeros and std = sqrt(1e-6), as the reference's
+ * scatter-mean + nan_to_num do */
+int pfsgnn_segment_moments(const float* M, int C, long long E, const int* ptr, int nseg,
+                           float* mom, float* hs, void* stream);
+/* gm[c][e] = C0 + d(C1 + d(C2 + d C3)), d = M[c][e] - mean[c][seg[e]],
+ * coefficients coef [4][C][nseg] from pfsgnn_moment_coef_seg */
+int pfsgnn_segment_moment_grad(const float* M, int C, long long E, const int* seg,
+                               const float* mean, const float* coef, int nseg, float* gm,
+                               void* stream);
+/* per-channel batch statistics of a [C][N] table (C <= 256): mean and biased
+ * variance (the EdgeModel BatchNorm's, gnn.py:101) */
+size_t pfsgnn_rows_ws_bytes(int C, long long N);
+int pfsgnn_rows_stats(const float* X, int C, long long N, float* mu, float* var, void* ws,
+                      size_t ws_bytes, void* stream);
+/* Sg[c] = sum_n g, Sgx[c] = sum_n g (y - mu) inv (the double BatchNorm's gradient sums) */
+int pfsgnn_rows_bn_sums(const float* g, const float* y, int C, long long N, const float* mu,
+                        const float* inv, float* Sg, float* Sgx, void* ws, size_t ws_bytes,
+                        void* stream);
+/* out[c][n] = alpha[c] g[c][n] + gam1[c] y[c][n] + gam0[c]; out may alias g or y */
+int pfsgnn_rows_axpby(const float* g, const float* y, int C, long long N, const float* alpha,
+                      const float* gam1, const float* gam0, float* out, void* stream);
 
 /* ---------------------------------------------------------------- edge ops */
 

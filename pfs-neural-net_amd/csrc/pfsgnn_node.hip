@@ -1290,10 +1290,15 @@ extern "C" int pfsgnn_bn2_bwd_coef(const float* Sg, const float* Sgx, const floa
 
 // ---------------------------------------------------------------- moments
 __global__ void k_moment_coef(const float* __restrict__ mom, const float* __restrict__ gst, int C,
-                              int NS, int n, float* __restrict__ coef) {
+                              int NS, int n, const int* __restrict__ ptr,
+                              float* __restrict__ coef) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // over C*NS
   const size_t CN = (size_t)C * NS;
   if (idx >= CN) return;
+  if (ptr) {  // general graph: this fiber's degree (count clamped at 1, as scatter mean)
+    const int s = (int)(idx % NS);
+    n = max(ptr[s + 1] - ptr[s], 1);
+  }
   const float c2 = mom[CN + idx], c3 = mom[2 * CN + idx], c4 = mom[3 * CN + idx];
   const float gmean = gst[idx], gstd = gst[CN + idx], gskew = gst[2 * CN + idx],
               gkurt = gst[3 * CN + idx];
@@ -1317,8 +1322,18 @@ extern "C" int pfsgnn_moment_coef(const float* mom, const float* gst, int C, int
              "bad arguments");
   const size_t tot = (size_t)C * NS;
   hipLaunchKernelGGL(k_moment_coef, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
-                     as_stream(stream), mom, gst, C, NS, n, coef);
+                     as_stream(stream), mom, gst, C, NS, n, nullptr, coef);
   return pf::check_launch("pfsgnn_moment_coef");
+}
+
+extern "C" int pfsgnn_moment_coef_seg(const float* mom, const float* gst, int C, int NS,
+                                      const int* fib_ptr, float* coef, void* stream) {
+  PF_REQUIRE(mom && gst && coef && fib_ptr && C > 0 && NS > 0, "pfsgnn_moment_coef_seg",
+             "bad arguments");
+  const size_t tot = (size_t)C * NS;
+  hipLaunchKernelGGL(k_moment_coef, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), mom, gst, C, NS, 1, fib_ptr, coef);
+  return pf::check_launch("pfsgnn_moment_coef_seg");
 }
 
 // ---------------------------------------------------------------- adam

@@ -1,0 +1,419 @@
+// pfsgnn_sparse.hip -- general (non-complete) bipartite graphs.
+//
+// The reference's data model takes any edge_index (gnn.py:32-63), and its
+// scatters reduce over arbitrary src / tgt (gnn.py:140-144 per fiber, 190 per
+// class).  A general batch is laid out once (pfsgnn_sparse_layout): edges
+// sorted stably by fiber (CSR by fiber: fib_ptr) -- every edge tensor of the
+// step lives in that order -- plus the positions sorted stably by class (CSR
+// by class: cls_ord / cls_ptr).  The per-edge MLPs then run as gathers of the
+// per-node parts + the node-level Linear kernels over E columns, and the
+// scatters as deterministic segment kernels (block per segment, fixed-order
+// tree: bitwise reproducible), all in this file:
+//   gather_cols      per-edge copy / add / (x) lrelu' of node-table columns
+//   segment_sum      per-fiber or per-class sums (optionally of lrelu(x))
+//   segment_moments  per-fiber mean + central moments -> SModel features
+//   segment_moment_grad  d loss / d message from the per-fiber coefficients
+//   rows_stats / rows_bn_sums / rows_axpby   the EdgeModel BatchNorm pieces
+#include "pfsgnn_common.h"
+#include "../../include/pfsgnn.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+
+namespace {
+
+// ------------------------------------------------------------ layout
+__global__ void k_sp_prepare(const long long* __restrict__ ei, long long E, int G, int NF, int NC,
+                             int* __restrict__ key, int* __restrict__ val,
+                             int* __restrict__ bad) {
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < E;
+       e += (long long)gridDim.x * 256) {
+    const long long s = ei[e], t = ei[E + e];
+    const bool ok = s >= 0 && s < (long long)G * NF && t >= 0 && t < (long long)G * NC &&
+                    s / NF == t / NC;
+    if (!ok) bad[0] = 1;  // any writer: a flag, the value is the same
+    key[e] = ok ? (int)s : 0;
+    val[e] = (int)e;
+  }
+}
+
+// after the sort by fiber: user_of[p] = the caller's edge at position p
+__global__ void k_sp_scatter(const long long* __restrict__ ei, long long E,
+                             const int* __restrict__ user_of, int* __restrict__ tgt_p,
+                             int* __restrict__ iota) {
+  for (long long p = (long long)blockIdx.x * 256 + threadIdx.x; p < E;
+       p += (long long)gridDim.x * 256) {
+    tgt_p[p] = (int)ei[E + user_of[p]];
+    iota[p] = (int)p;
+  }
+}
+
+// ptr[k] = first position whose (sorted) key is >= k, k = 0..n
+__global__ void k_sp_ptr(const int* __restrict__ keys, long long E, int n, int* __restrict__ ptr) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k > n) return;
+  long long lo = 0, hi = E;
+  while (lo < hi) {
+    const long long mid = (lo + hi) >> 1;
+    if (keys[mid] < k) lo = mid + 1; else hi = mid;
+  }
+  ptr[k] = (int)lo;
+}
+
+// ------------------------------------------------------------ gathers
+// mode 0: out[c][e] = X[c][idx[e]];  1: out += X[c][idx[e]];
+// mode 2: out = X[c][idx[e]] * lrelu'(Z[c][e])
+__global__ __launch_bounds__(256) void k_gather_cols(const float* __restrict__ X, int C, int N,
+                                                     const int* __restrict__ idx, long long E,
+                                                     const float* __restrict__ Z, int mode,
+                                                     float* __restrict__ out) {
+  const long long tot = (long long)C * E;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < tot;
+       i += (long long)gridDim.x * 256) {
+    const long long c = i / E, e = i - c * E;
+    const float v = X[c * N + idx[e]];
+    if (mode == 0) out[i] = v;
+    else if (mode == 1) out[i] += v;
+    else out[i] = v * dlrelu(Z[i]);
+  }
+}
+
+// ------------------------------------------------------------ segment sums
+// block per segment: 256 threads stride over the segment's edges (fixed
+// assignment), a fixed-order LDS tree per channel (deterministic)
+__global__ __launch_bounds__(256) void k_segment_sum(const float* __restrict__ X, int C, long long E,
+                                                     const int* __restrict__ ord,
+                                                     const int* __restrict__ ptr, int act,
+                                                     float* __restrict__ out, int nseg, int add) {
+  const int s = blockIdx.x, t = threadIdx.x;
+  const int p0 = ptr[s], p1 = ptr[s + 1];
+  __shared__ float red[256];
+  for (int c = 0; c < C; ++c) {
+    float v = 0.f;
+    for (int p = p0 + t; p < p1; p += 256) {
+      const long long e = ord ? ord[p] : p;
+      const float x = X[(long long)c * E + e];
+      v += act ? lrelu(x) : x;
+    }
+    red[t] = v;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (t < w) red[t] += red[t + w];
+      __syncthreads();
+    }
+    if (t == 0) {
+      float* o = out + (long long)c * nseg + s;
+      *o = add ? *o + red[0] : red[0];
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------ moments
+// thread per (segment, channel): mean, then the central moments over the
+// segment (two passes, double accumulation), as torch_scatter's mean (count
+// clamped at 1) and gnn.py:140-144; empty segments give mean 0, moments 0
+__global__ __launch_bounds__(256) void k_segment_moments(const float* __restrict__ M, int C,
+                                                         long long E,
+                                                         const int* __restrict__ ptr, int nseg,
+                                                         float* __restrict__ mom,
+                                                         float* __restrict__ hs) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;  // c * nseg + s
+  const long long CN = (long long)C * nseg;
+  if (idx >= CN) return;
+  const int c = (int)(idx / nseg), s = (int)(idx - (long long)c * nseg);
+  const int p0 = ptr[s], p1 = ptr[s + 1];
+  const float* m = M + (long long)c * E;
+  double sum = 0.0;
+  for (int p = p0; p < p1; ++p) sum += m[p];
+  const double n = p1 > p0 ? (double)(p1 - p0) : 1.0;
+  const double mean = sum / n;
+  double s2 = 0.0, s3 = 0.0, s4 = 0.0;
+  for (int p = p0; p < p1; ++p) {
+    const double d = (double)m[p] - mean, d2 = d * d;
+    s2 += d2;
+    s3 += d2 * d;
+    s4 += d2 * d2;
+  }
+  const float c2 = (float)(s2 / n), c3 = (float)(s3 / n), c4 = (float)(s4 / n);
+  mom[idx] = (float)mean;
+  mom[CN + idx] = c2;
+  mom[2 * CN + idx] = c3;
+  mom[3 * CN + idx] = c4;
+  const float var = c2 > 0.f ? c2 : 0.01f * c2;  // F.leaky_relu (slope 0.01), gnn.py:141
+  const float sd = sqrtf(var + 1e-6f);
+  hs[idx] = (float)mean;
+  hs[CN + idx] = sd;
+  hs[2 * CN + idx] = c3 / (sd * sd * sd);
+  hs[3 * CN + idx] = c4 / ((sd * sd) * (sd * sd));
+}
+
+// g_m[c][e] = C0 + d (C1 + d (C2 + d C3)), d = m - mean, per-fiber coefficients
+__global__ __launch_bounds__(256) void k_segment_moment_grad(const float* __restrict__ M, int C,
+                                                             long long E,
+                                                             const int* __restrict__ seg,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ coef,
+                                                             int nseg, float* __restrict__ gm) {
+  const long long tot = (long long)C * E, CN = (long long)C * nseg;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < tot;
+       i += (long long)gridDim.x * 256) {
+    const long long c = i / E, e = i - c * E;
+    const long long j = c * nseg + seg[e];
+    const float d = M[i] - mean[j];
+    gm[i] = fmaf(d, fmaf(d, fmaf(d, coef[3 * CN + j], coef[2 * CN + j]), coef[CN + j]), coef[j]);
+  }
+}
+
+// ------------------------------------------------------------ row statistics
+// per-(channel, chunk) Welford partials -> per-channel mean / biased variance
+__global__ __launch_bounds__(256) void k_rows_stats_part(const float* __restrict__ X, long long N,
+                                                         int S, float* __restrict__ part) {
+  const int c = blockIdx.x, sidx = blockIdx.y, t = threadIdx.x;
+  const long long chunk = (N + S - 1) / S;
+  const long long n0 = (long long)sidx * chunk, n1 = std::min<long long>(N, n0 + chunk);
+  float cnt = 0.f, mean = 0.f, m2 = 0.f;
+  for (long long n = n0 + t; n < n1; n += 256) {
+    const float x = X[(long long)c * N + n];
+    cnt += 1.f;
+    const float d = x - mean;
+    mean += d / cnt;
+    m2 += d * (x - mean);
+  }
+  __shared__ float sc[256], sm[256], sq[256];
+  sc[t] = cnt; sm[t] = mean; sq[t] = m2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) {
+      const float ca = sc[t], cb = sc[t + w], tot = ca + cb;
+      if (tot > 0.f) {
+        const float d = sm[t + w] - sm[t];
+        sm[t] = sm[t] + d * (cb / tot);
+        sq[t] = sq[t] + sq[t + w] + d * d * (ca * cb / tot);
+      }
+      sc[t] = tot;
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    float* p = part + ((long long)c * S + sidx) * 3;
+    p[0] = sc[0]; p[1] = sm[0]; p[2] = sq[0];
+  }
+}
+
+__global__ void k_rows_stats_fin(const float* __restrict__ part, int C, int S, long long N,
+                                 float* __restrict__ mu, float* __restrict__ var) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  double n = 0, mean = 0, m2 = 0;
+  for (int s = 0; s < S; ++s) {
+    const float* p = part + ((long long)c * S + s) * 3;
+    const double cb = p[0], tot = n + cb;
+    if (tot > 0) {
+      const double d = p[1] - mean;
+      mean += d * (cb / tot);
+      m2 += p[2] + d * d * (n * cb / tot);
+    }
+    n = tot;
+  }
+  mu[c] = (float)mean;
+  var[c] = (float)(m2 / (double)N);
+}
+
+// Sg[c] = sum_n g, Sgx[c] = sum_n g * (y - mu) * inv  (block partials, fixed order)
+__global__ __launch_bounds__(256) void k_rows_bn_sums_part(const float* __restrict__ g,
+                                                           const float* __restrict__ y,
+                                                           long long N, int S,
+                                                           const float* __restrict__ mu,
+                                                           const float* __restrict__ inv,
+                                                           float* __restrict__ part) {
+  const int c = blockIdx.x, sidx = blockIdx.y, t = threadIdx.x;
+  const long long chunk = (N + S - 1) / S;
+  const long long n0 = (long long)sidx * chunk, n1 = std::min<long long>(N, n0 + chunk);
+  const float m = mu[c], iv = inv[c];
+  float a = 0.f, b = 0.f;
+  for (long long n = n0 + t; n < n1; n += 256) {
+    const float gv = g[(long long)c * N + n];
+    a += gv;
+    b += gv * ((y[(long long)c * N + n] - m) * iv);
+  }
+  __shared__ float ra[256], rb[256];
+  ra[t] = a; rb[t] = b;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) { ra[t] += ra[t + w]; rb[t] += rb[t + w]; }
+    __syncthreads();
+  }
+  if (t == 0) {
+    part[((long long)c * S + sidx) * 2] = ra[0];
+    part[((long long)c * S + sidx) * 2 + 1] = rb[0];
+  }
+}
+
+__global__ void k_rows_bn_sums_fin(const float* __restrict__ part, int C, int S,
+                                   float* __restrict__ Sg, float* __restrict__ Sgx) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+  for (int s = 0; s < S; ++s) {
+    a += part[((long long)c * S + s) * 2];
+    b += part[((long long)c * S + s) * 2 + 1];
+  }
+  Sg[c] = a;
+  Sgx[c] = b;
+}
+
+// out may alias g or y (elementwise)
+__global__ __launch_bounds__(256) void k_rows_axpby(const float* g, const float* y, int C,
+                                                    long long N,
+                                                    const float* __restrict__ alpha,
+                                                    const float* __restrict__ gam1,
+                                                    const float* __restrict__ gam0, float* out) {
+  const long long tot = (long long)C * N;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < tot;
+       i += (long long)gridDim.x * 256) {
+    const int c = (int)(i / N);
+    out[i] = fmaf(gam1[c], y[i], fmaf(alpha[c], g[i], gam0[c]));
+  }
+}
+
+unsigned grid_of(long long n) { return (unsigned)std::max<long long>(1, std::min<long long>((n + 255) / 256, 8192)); }
+int row_splits(long long N) { return (int)std::max<long long>(1, std::min<long long>(64, (N + 8191) / 8192)); }
+
+}  // namespace
+
+// ================================================================ ABI
+extern "C" size_t pfsgnn_sparse_layout_ws_bytes(long long E) {
+  if (E <= 0 || E >= INT32_MAX) return 256;
+  size_t tmp = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const int*)nullptr, (int*)nullptr,
+                                           (const int*)nullptr, (int*)nullptr, (int)E);
+  return align256(tmp) + 4 * align256((size_t)E * sizeof(int)) + 256;
+}
+
+static int key_bits(int n) {  // keys are 0..n-1
+  int b = 1;
+  while (b < 31 && (1 << b) < n) ++b;
+  return b;
+}
+
+extern "C" int pfsgnn_sparse_layout(const long long* edge_index, long long E, int G, int NF, int NC,
+                                    int* src_p, int* tgt_p, int* user_of, int* fib_ptr,
+                                    int* cls_ord, int* cls_ptr, int* status, void* ws,
+                                    size_t ws_bytes, void* stream) {
+  const char* where = "pfsgnn_sparse_layout";
+  PF_REQUIRE(edge_index && E > 0 && E < INT32_MAX && G > 0 && NF > 0 && NC > 0 && src_p &&
+                 tgt_p && user_of && fib_ptr && cls_ord && cls_ptr && status,
+             where, "bad arguments");
+  PF_REQUIRE((long long)G * NF < INT32_MAX && (long long)G * NC < INT32_MAX, where,
+             "too many nodes for int32 indices");
+  PF_REQUIRE(ws && ws_bytes >= pfsgnn_sparse_layout_ws_bytes(E), where, "workspace too small");
+  hipStream_t st = as_stream(stream);
+  char* w = static_cast<char*>(ws);
+  const size_t eb = align256((size_t)E * sizeof(int));
+  int* key = reinterpret_cast<int*>(w);
+  int* val = reinterpret_cast<int*>(w + eb);
+  int* iota = reinterpret_cast<int*>(w + 2 * eb);
+  int* ckey = reinterpret_cast<int*>(w + 3 * eb);
+  void* tmp = w + 4 * eb;
+  size_t tmpb = ws_bytes - 4 * eb;
+  const int NS = G * NF, NT = G * NC;
+  if (hipMemsetAsync(status, 0, sizeof(int), st) != hipSuccess) return pf::fail(where, "memset");
+  hipLaunchKernelGGL(k_sp_prepare, dim3(grid_of(E)), dim3(256), 0, st, edge_index, E, G, NF, NC,
+                     key, val, status);
+  // stable LSD radix sorts: the edges by fiber (ties keep the caller's order),
+  // then the fiber-sorted positions by class (ties keep position order)
+  if (hipcub::DeviceRadixSort::SortPairs(tmp, tmpb, key, src_p, val, user_of, (int)E, 0,
+                                         key_bits(NS), st) != hipSuccess)
+    return pf::fail(where, "radix sort (fibers)");
+  hipLaunchKernelGGL(k_sp_scatter, dim3(grid_of(E)), dim3(256), 0, st, edge_index, E, user_of,
+                     tgt_p, iota);
+  if (hipcub::DeviceRadixSort::SortPairs(tmp, tmpb, tgt_p, ckey, iota, cls_ord, (int)E, 0,
+                                         key_bits(NT), st) != hipSuccess)
+    return pf::fail(where, "radix sort (classes)");
+  hipLaunchKernelGGL(k_sp_ptr, dim3((NS + 256) / 256), dim3(256), 0, st, src_p, E, NS, fib_ptr);
+  hipLaunchKernelGGL(k_sp_ptr, dim3((NT + 256) / 256), dim3(256), 0, st, ckey, E, NT, cls_ptr);
+  return pf::check_launch(where);
+}
+
+extern "C" int pfsgnn_gather_cols(const float* X, int C, int N, const int* idx, long long E,
+                                  const float* Z, int mode, float* out, void* stream) {
+  PF_REQUIRE(X && idx && out && C > 0 && N > 0 && E > 0 && mode >= 0 && mode <= 2 &&
+                 (mode != 2 || Z),
+             "pfsgnn_gather_cols", "bad arguments");
+  hipLaunchKernelGGL(k_gather_cols, dim3(grid_of((long long)C * E)), dim3(256), 0,
+                     as_stream(stream), X, C, N, idx, E, Z, mode, out);
+  return pf::check_launch("pfsgnn_gather_cols");
+}
+
+extern "C" int pfsgnn_segment_sum(const float* X, int C, long long E, const int* ord,
+                                  const int* ptr, int nseg, int act, float* out, int add,
+                                  void* stream) {
+  PF_REQUIRE(X && ptr && out && C > 0 && E > 0 && nseg > 0, "pfsgnn_segment_sum",
+             "bad arguments");
+  hipLaunchKernelGGL(k_segment_sum, dim3(nseg), dim3(256), 0, as_stream(stream), X, C, E, ord, ptr,
+                     act, out, nseg, add);
+  return pf::check_launch("pfsgnn_segment_sum");
+}
+
+extern "C" int pfsgnn_segment_moments(const float* M, int C, long long E, const int* ptr, int nseg,
+                                      float* mom, float* hs, void* stream) {
+  PF_REQUIRE(M && ptr && mom && hs && C > 0 && E > 0 && nseg > 0, "pfsgnn_segment_moments",
+             "bad arguments");
+  hipLaunchKernelGGL(k_segment_moments, dim3(grid_of((long long)C * nseg)), dim3(256), 0,
+                     as_stream(stream), M, C, E, ptr, nseg, mom, hs);
+  return pf::check_launch("pfsgnn_segment_moments");
+}
+
+extern "C" int pfsgnn_segment_moment_grad(const float* M, int C, long long E, const int* seg,
+                                          const float* mean, const float* coef, int nseg,
+                                          float* gm, void* stream) {
+  PF_REQUIRE(M && seg && mean && coef && gm && C > 0 && E > 0 && nseg > 0,
+             "pfsgnn_segment_moment_grad", "bad arguments");
+  hipLaunchKernelGGL(k_segment_moment_grad, dim3(grid_of((long long)C * E)), dim3(256), 0,
+                     as_stream(stream), M, C, E, seg, mean, coef, nseg, gm);
+  return pf::check_launch("pfsgnn_segment_moment_grad");
+}
+
+extern "C" size_t pfsgnn_rows_ws_bytes(int C, long long N) {
+  return align256((size_t)C * row_splits(N) * 3 * sizeof(float));
+}
+
+extern "C" int pfsgnn_rows_stats(const float* X, int C, long long N, float* mu, float* var,
+                                 void* ws, size_t ws_bytes, void* stream) {
+  PF_REQUIRE(X && mu && var && C > 0 && C <= 256 && N > 0, "pfsgnn_rows_stats", "bad arguments");
+  PF_REQUIRE(ws && ws_bytes >= pfsgnn_rows_ws_bytes(C, N), "pfsgnn_rows_stats",
+             "workspace too small");
+  const int S = row_splits(N);
+  hipStream_t st = as_stream(stream);
+  float* part = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(k_rows_stats_part, dim3(C, S), dim3(256), 0, st, X, N, S, part);
+  hipLaunchKernelGGL(k_rows_stats_fin, dim3(1), dim3(256), 0, st, part, C, S, N, mu, var);
+  return pf::check_launch("pfsgnn_rows_stats");
+}
+
+extern "C" int pfsgnn_rows_bn_sums(const float* g, const float* y, int C, long long N,
+                                   const float* mu, const float* inv, float* Sg, float* Sgx,
+                                   void* ws, size_t ws_bytes, void* stream) {
+  PF_REQUIRE(g && y && mu && inv && Sg && Sgx && C > 0 && C <= 256 && N > 0,
+             "pfsgnn_rows_bn_sums", "bad arguments");
+  PF_REQUIRE(ws && ws_bytes >= pfsgnn_rows_ws_bytes(C, N), "pfsgnn_rows_bn_sums",
+             "workspace too small");
+  const int S = row_splits(N);
+  hipStream_t st = as_stream(stream);
+  float* part = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(k_rows_bn_sums_part, dim3(C, S), dim3(256), 0, st, g, y, N, S, mu, inv, part);
+  hipLaunchKernelGGL(k_rows_bn_sums_fin, dim3(1), dim3(256), 0, st, part, C, S, Sg, Sgx);
+  return pf::check_launch("pfsgnn_rows_bn_sums");
+}
+
+extern "C" int pfsgnn_rows_axpby(const float* g, const float* y, int C, long long N,
+                                 const float* alpha, const float* gam1, const float* gam0,
+                                 float* out, void* stream) {
+  PF_REQUIRE(g && y && alpha && gam1 && gam0 && out && C > 0 && N > 0, "pfsgnn_rows_axpby",
+             "bad arguments");
+  hipLaunchKernelGGL(k_rows_axpby, dim3(grid_of((long long)C * N)), dim3(256), 0,
+                     as_stream(stream), g, y, C, N, alpha, gam1, gam0, out);
+  return pf::check_launch("pfsgnn_rows_axpby");
+}

@@ -11,7 +11,8 @@ backward formula against the autograd oracle; the product never does.)
 
 Layouts (DESIGN.md §Data layout): node tensors are channel-major ``[C, N]``;
 edge tensors are channel-major ``[C, E]`` over the canonical class-major edge
-order ``e = (g*NC + c)*NF + f`` of a batch of G complete bipartite graphs.
+order ``e = (g*NC + c)*NF + f`` of a batch of G complete bipartite graphs
+(a general batch: its position order, edges sorted by fiber -- pfsgnn.sparse).
 Edge state is kept *lazily*: an EdgeModel output is its pre-norm value ``y``
 plus a per-channel affine ``(sc, sh)`` (xe_new = sc*y + sh) -- the triple
 ``xe3 = (y, sc, sh)``; consumers apply the affine on the fly, so inside the
@@ -36,16 +37,20 @@ import torch
 
 
 class Dims:
-    """Batch geometry: G graphs of NF fibers x NC classes, feature width F."""
+    """Batch geometry: G graphs of NF fibers x NC classes, feature width F.
+    ``sp``: None for complete bipartite graphs (E = G*NF*NC, the fused edge
+    kernels), or the pfsgnn.sparse.SparseGeo of a general batch of E edges."""
 
-    def __init__(self, G, NF, NC, F):
+    def __init__(self, G, NF, NC, F, sp=None):
         self.G, self.NF, self.NC, self.F = int(G), int(NF), int(NC), int(F)
-        self.E = self.G * self.NF * self.NC
+        self.sp = sp
+        self.E = self.G * self.NF * self.NC if sp is None else sp.E
         self.NS = self.G * self.NF
         self.NT = self.G * self.NC
 
     def __repr__(self):
-        return f"Dims(G={self.G}, NF={self.NF}, NC={self.NC}, F={self.F}, E={self.E})"
+        kind = "" if self.sp is None else ", general"
+        return f"Dims(G={self.G}, NF={self.NF}, NC={self.NC}, F={self.F}, E={self.E}{kind})"
 
 
 def param_names(B, normed=True):
@@ -266,7 +271,8 @@ class Engine:
         self.mlp_bwd(P, Gr, pre + "node_mlp_2.", g_xs_new, st["sS"],
                      outs=[(g_xs, F, True), (gst, 8 * F, False), (gu, F, False)])
         be.graph_reduce(gu, G, out=g_u)
-        return be.moment_coef(st["mom"], gst, d.NC)
+        # messages per fiber: NC on complete graphs, the fiber degree otherwise
+        return be.moment_coef(st["mom"], gst, d.NC if d.sp is None else d.sp.fib_ptr)
 
     def source_edge_bwd(self, P, Gr, d, pre, st, coef, tpart, g_next, bnstat, g_xt):
         be, F = self.be, self.F
@@ -288,7 +294,12 @@ class Engine:
         Wt2, bt2 = P[pre + "node_mlp_1.2.weight"], P[pre + "node_mlp_1.2.bias"]
         Rs = be.lin(Wt1, 0, F, xs, b=bt1)
         hsum = be.target_fwd(d, xe3[0], xe3[1], xe3[2], Rs, Wt1)
-        agg = be.lin(Wt2, 0, 2 * F, hsum, b=bt2, bscale=float(d.NF))
+        if d.sp is None:
+            agg = be.lin(Wt2, 0, 2 * F, hsum, b=bt2, bscale=float(d.NF))
+        else:
+            # the bias of the summed messages is deg(c) * b2 (gnn.py:190)
+            agg = be.lin(Wt2, 0, 2 * F, hsum)
+            be.lin(bt2.view(-1, 1), 0, 1, d.sp.deg_t, out=agg, add=True)
         # node_mlp_2 input [x, agg, u[batch]] (gnn.py:191), in place, + BatchNorm1d
         hT = [(xt, 0, False), (agg, F, False), (u, 3 * F, True)]
         xt_new, sT = self.mlp_fwd(P, pre + "node_mlp_2.", hT, pre + "norm.", BN)
@@ -302,8 +313,12 @@ class Engine:
                      outs=[(g_xt, F, True), (g_agg, 2 * F, False), (gu, F, False)])
         be.graph_reduce(gu, G, out=g_u)
         Wt2 = P[pre + "node_mlp_1.2.weight"]
-        be.wgrad(g_agg, st["hsum"], Gr[pre + "node_mlp_1.2.weight"],
-                 db=Gr[pre + "node_mlp_1.2.bias"], dbscale=float(d.NF))
+        if d.sp is None:
+            be.wgrad(g_agg, st["hsum"], Gr[pre + "node_mlp_1.2.weight"],
+                     db=Gr[pre + "node_mlp_1.2.bias"], dbscale=float(d.NF))
+        else:
+            be.wgrad(g_agg, st["hsum"], Gr[pre + "node_mlp_1.2.weight"])
+            be.wgrad(g_agg, d.sp.deg_t, Gr[pre + "node_mlp_1.2.bias"].view(-1, 1))
         return be.lin_t(Wt2, 0, 2 * F, g_agg)
 
     def target_edge_bwd(self, P, Gr, d, pre, st, g_hsum, want_gxe, g_xs):

@@ -17,7 +17,9 @@ once (cached per tensor).  train.py's fiber-major order ((g*NF + f)*NC + c,
 train.py:94) is mapped arithmetically; any other order (``graphs/graph-0.pt``:
 each fiber's classes come out of an unstable argsort) through a permutation.
 Results are always reported in the caller's edge order.
-Graphs that are not complete bipartite are rejected loudly.
+Any other edge_index (ragged degrees, missing or repeated pairs) runs on the
+general-graph path (pfsgnn.sparse: CSR by fiber / class, DESIGN.md §General
+graphs); edges that leave their graph are rejected loudly.
 
 Batching: G graphs collated PyG-style (``Batch.from_data_list``, increments
 from ``BipartiteData.__inc__``) with ``x_u`` of shape [G, F]; ``u[g]`` is
@@ -146,41 +148,45 @@ _EDGE_CACHE = _TensorCache(4)
 
 
 class Layout:
-    """How the caller's edge order maps onto the canonical class-major order
-    (the ``mode`` argument of pfsgnn_edges_{to,from}_canonical)."""
+    """How the caller's edge order maps onto the kernels' edge order (the
+    ``mode`` argument of pfsgnn_edges_{to,from}_canonical).  A general batch
+    (``sp`` set) is a PERM layout over its E positions (G=1, NF=E, NC=1 in the
+    ABI's terms) whose permutation is the position -> caller-edge map."""
     PERM, FIBER_MAJOR, CANONICAL = 0, 1, 2
 
-    def __init__(self, G, NF, NC, mode, perm=None, fiber_major=False):
+    def __init__(self, G, NF, NC, mode, perm=None, fiber_major=False, sp=None):
         self.G, self.NF, self.NC, self.mode = G, NF, NC, mode
         self.perm = perm if mode == Layout.PERM else None
         self.fiber_major = fiber_major    # caller order == train.py's positional order
+        self.sp = sp
 
 
 def geometry(x_s, x_t, x_u, edge_index, F):
-    """(Dims, Layout) for a batch."""
+    """(Dims, Layout) for a batch: complete bipartite graphs run on the fused
+    edge kernels; any other edge_index (gnn.py:7-47 takes one) on the general
+    path (pfsgnn.sparse), laid out once per edge_index tensor."""
     G = 1 if x_u is None else int(x_u.size(0))
     S, T = int(x_s.size(0)), int(x_t.size(0))
     if S % G or T % G:
         raise ValueError(f"x_s ({S}) / x_t ({T}) rows are not a multiple of the {G} graphs in x_u")
     NF, NC = S // G, T // G
-    d = Dims(G, NF, NC, F)
     E = int(edge_index.size(1))
+    if E == 0:
+        raise ValueError("edge_index has no edges")
     key = (E, G, NF, NC)
     hit = _LAYOUT_CACHE.get(edge_index, key)
     if hit is None:
-        if E != d.E:
-            raise NotImplementedError(
-                f"edge_index has {E} edges; the HIP kernels need a batch of complete bipartite "
-                f"graphs (G*NF*NC = {d.E}).  General sparse bipartite graphs are a later row of "
-                "the scope (DESIGN.md §Scope)")
-        perm, complete, fm, identity = backend().layout_analyze(edge_index, G, NF, NC)
-        if not complete:
-            raise NotImplementedError("edge_index is not a complete bipartite batch (some "
-                                      "(fiber, class) pair is missing, repeated, or crosses graphs)")
-        mode = Layout.CANONICAL if identity else (Layout.FIBER_MAJOR if fm else Layout.PERM)
-        hit = Layout(G, NF, NC, mode, perm, fiber_major=fm)
+        complete = False
+        if E == G * NF * NC:
+            perm, complete, fm, identity = backend().layout_analyze(edge_index, G, NF, NC)
+        if complete:
+            mode = Layout.CANONICAL if identity else (Layout.FIBER_MAJOR if fm else Layout.PERM)
+            hit = Layout(G, NF, NC, mode, perm, fiber_major=fm)
+        else:
+            sp = backend().sparse_layout(edge_index, G, NF, NC)
+            hit = Layout(1, E, 1, Layout.PERM, sp.user_of, sp=sp)
         _LAYOUT_CACHE.put(edge_index, key, hit)
-    return d, hit
+    return Dims(G, NF, NC, F, sp=hit.sp), hit
 
 
 def edges_in(x_e, lay, cache=False):

@@ -13,6 +13,8 @@ import os
 
 import torch
 
+from .sparse import SparseEdgeOps, SparseGeo
+
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpfsgnn.so")
 
 
@@ -95,6 +97,17 @@ _SIGS = {
     "pfsgnn_affine_rows": ([P, I, I, P, P, P, P], I),
     "pfsgnn_bn2_bwd_coef": ([P, P, P, P, P, I, LL, FL, P, P, P, P, P, P], I),
     "pfsgnn_moment_coef": ([P, P, I, I, I, P, P], I),
+    "pfsgnn_moment_coef_seg": ([P, P, I, I, P, P, P], I),
+    "pfsgnn_sparse_layout_ws_bytes": ([LL], SZ),
+    "pfsgnn_sparse_layout": ([P, LL, I, I, I, P, P, P, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_gather_cols": ([P, I, I, P, LL, P, I, P, P], I),
+    "pfsgnn_segment_sum": ([P, I, LL, P, P, I, I, P, I, P], I),
+    "pfsgnn_segment_moments": ([P, I, LL, P, I, P, P, P], I),
+    "pfsgnn_segment_moment_grad": ([P, I, LL, P, P, P, I, P, P], I),
+    "pfsgnn_rows_ws_bytes": ([I, LL], SZ),
+    "pfsgnn_rows_stats": ([P, I, LL, P, P, P, SZ, P], I),
+    "pfsgnn_rows_bn_sums": ([P, P, I, LL, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_rows_axpby": ([P, P, I, LL, P, P, P, P, P], I),
     "pfsgnn_edge_mlp_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_source_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_target_fwd": ([I, I, I, I, P, P, P, P, P, P, P, SZ, P], I),
@@ -223,6 +236,7 @@ class HipBackend:
         # while they were current keeps their addresses baked in, and a replay
         # must never write into memory the allocator has handed out again
         self._retired = []
+        self._sp = SparseEdgeOps(self)
 
     # ------------------------------------------------------------ memory
     def empty(self, *shape):
@@ -530,10 +544,17 @@ class HipBackend:
         return a, g0, g1
 
     def moment_coef(self, mom, gst, n):
+        """``n``: the messages per fiber -- an int (complete graphs: NC), or a
+        general graph's fiber CSR pointer (int32 [NS+1] device tensor)."""
         _, C, NS = mom.shape
         coef = self.empty(4, C, NS)
         gst = gst.contiguous()
         self._chk(mom, gst)
+        if isinstance(n, torch.Tensor):
+            assert n.dtype == torch.int32 and n.is_cuda and n.numel() == NS + 1
+            _call("pfsgnn_moment_coef_seg", mom.data_ptr(), gst.data_ptr(), C, NS, n.data_ptr(),
+                  coef.data_ptr(), _stream())
+            return coef
         _call("pfsgnn_moment_coef", mom.data_ptr(), gst.data_ptr(), C, NS, int(n), coef.data_ptr(),
               _stream())
         return coef
@@ -543,6 +564,8 @@ class HipBackend:
         self._dims = d
 
     def edge_mlp_fwd(self, d, xe, xsc, xsh, Ps, Pt, W1, W2, b2):
+        if d.sp is not None:
+            return self._sp.edge_mlp_fwd(d, xe, xsc, xsh, Ps, Pt, W1, W2, b2)
         self._set_dims(d)
         y, mu, var = self.empty(d.F, d.E), self.empty(d.F), self.empty(d.F)
         self._chk(xe, Ps, Pt, W1, W2, b2)
@@ -553,6 +576,8 @@ class HipBackend:
         return y, mu, var
 
     def source_fwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, hs_out):
+        if d.sp is not None:
+            return self._sp.source_fwd(d, y, sc, sh, Qt, Ws1, Ws2, bs2, hs_out)
         mom = self.empty(4, 2 * d.F, d.NS)
         self._chk(y, Qt, Ws1, Ws2, bs2, hs_out)
         ws, wsb = self._wsargs(d)
@@ -562,6 +587,8 @@ class HipBackend:
         return mom
 
     def target_fwd(self, d, y, sc, sh, Rs, Wt1):
+        if d.sp is not None:
+            return self._sp.target_fwd(d, y, sc, sh, Rs, Wt1)
         hsum = self.empty(2 * d.F, d.NT)
         ws, wsb = self._wsargs(d)
         _call("pfsgnn_target_fwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
@@ -569,6 +596,8 @@ class HipBackend:
         return hsum
 
     def target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False):
+        if d.sp is not None:
+            return self._sp.target_bwd(d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=want_gxe)
         GzT = self.empty(2 * d.F, d.NS)
         gxe = self.empty(d.F, d.E) if want_gxe else None
         g_hsum = g_hsum.contiguous()
@@ -580,6 +609,9 @@ class HipBackend:
 
     def source_bwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next, bnstat,
                    dWs1, dWs2, dbs2):
+        if d.sp is not None:
+            return self._sp.source_bwd(d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next,
+                                       bnstat, dWs1, dWs2, dbs2)
         g_tot = self.empty(d.F, d.E)
         GzS = self.empty(2 * d.F, d.NT)
         Rs = Wt1 = g_hsum = None
@@ -602,6 +634,8 @@ class HipBackend:
         return g_tot, GzS, Sg, Sgx
 
     def edge_bn_grad_sums(self, d, g, y, mu1, inv1):
+        if d.sp is not None:
+            return self._sp.edge_bn_grad_sums(d, g, y, mu1, inv1)
         Sg, Sgx = self.empty(d.F), self.empty(d.F)
         ws, wsb = self._wsargs(d)
         _call("pfsgnn_edge_bn_grad_sums", d.G, d.NF, d.NC, d.F, g.data_ptr(), y.data_ptr(),
@@ -610,6 +644,9 @@ class HipBackend:
 
     def edge_mlp_bwd(self, d, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1, W2,
                      dW1, dW2, db2, want_gxe=True):
+        if d.sp is not None:
+            return self._sp.edge_mlp_bwd(d, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1,
+                                         W2, dW1, dW2, db2, want_gxe=want_gxe)
         gxe = self.empty(d.F, d.E) if want_gxe else None
         GzEs, GzEt = self.empty(4 * d.F, d.NS), self.empty(4 * d.F, d.NT)
         ws, wsb = self._wsargs(d)
@@ -621,6 +658,8 @@ class HipBackend:
         return gxe, GzEs, GzEt
 
     def edge_apply(self, d, y, sc, sh):
+        if d.sp is not None:
+            return self._sp.edge_apply(d, y, sc, sh)
         out = self.empty(d.F, d.E)
         _call("pfsgnn_edges_from_canonical", y.data_ptr(), _ptr(sc), _ptr(sh), d.G, d.NF, d.NC,
               d.F, 2, None, 0, out.data_ptr(), _stream())
@@ -687,6 +726,104 @@ class HipBackend:
         _call("pfsgnn_build_complete", int(G), int(NF), int(NC), int(order), ei.data_ptr(),
               _stream())
         return ei
+
+    # ------------------------------------------------------------ general graphs
+    def sparse_layout(self, edge_index, G, NF, NC):
+        """CSR layout of a batch that is not complete bipartite (pfsgnn.sparse).
+        Raises ValueError if an edge is out of range or crosses graphs."""
+        E = int(edge_index.shape[1])
+        ei = edge_index.to(device=self.device, dtype=torch.int64).contiguous()
+        i32 = dict(dtype=torch.int32, device=self.device)
+        src_p, tgt_p, user_of, cls_ord = (torch.empty(E, **i32) for _ in range(4))
+        fib_ptr = torch.empty(G * NF + 1, **i32)
+        cls_ptr = torch.empty(G * NC + 1, **i32)
+        status = torch.empty(1, **i32)
+        ws = torch.empty(lib().pfsgnn_sparse_layout_ws_bytes(E), dtype=torch.uint8,
+                         device=self.device)
+        _call("pfsgnn_sparse_layout", ei.data_ptr(), E, int(G), int(NF), int(NC), src_p.data_ptr(),
+              tgt_p.data_ptr(), user_of.data_ptr(), fib_ptr.data_ptr(), cls_ord.data_ptr(),
+              cls_ptr.data_ptr(), status.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+        if int(status.item()) != 0:
+            raise ValueError("edge_index has an edge out of range or joining nodes of different "
+                             f"graphs (G={G}, NF={NF}, NC={NC}; gnn.py:32-47 batching)")
+        deg_t = (cls_ptr[1:] - cls_ptr[:-1]).to(torch.float32).reshape(1, -1).contiguous()
+        return SparseGeo(E, src_p, tgt_p, user_of, fib_ptr, cls_ord, cls_ptr, deg_t)
+
+    def gather_cols(self, X, idx, mode=0, out=None, Z=None):
+        """out[c][e] (=, +=) X[c][idx[e]]; mode 2: X[c][idx[e]] * lrelu'(Z[c][e])."""
+        C, N = X.shape
+        E = idx.numel()
+        if out is None:
+            assert mode != 1
+            out = self.empty(C, E)
+        self._chk(X, Z, out)
+        assert idx.dtype == torch.int32 and out.shape == (C, E)
+        _call("pfsgnn_gather_cols", X.data_ptr(), C, N, idx.data_ptr(), E, _ptr(Z), int(mode),
+              out.data_ptr(), _stream())
+        return out
+
+    def segment_sum(self, X, ord, ptr, nseg, act=False, out=None, add=False):
+        C, E = X.shape
+        if out is None:
+            out, add = self.empty(C, nseg), False
+        self._chk(X, out)
+        assert ptr.numel() == nseg + 1
+        _call("pfsgnn_segment_sum", X.data_ptr(), C, E, _ptr(ord), ptr.data_ptr(), int(nseg),
+              int(act), out.data_ptr(), int(add), _stream())
+        return out
+
+    def segment_moments(self, M, ptr, nseg, hs_out):
+        C, E = M.shape
+        mom = self.empty(4, C, nseg)
+        self._chk(M, hs_out)
+        assert hs_out.shape == (4 * C, nseg)
+        _call("pfsgnn_segment_moments", M.data_ptr(), C, E, ptr.data_ptr(), int(nseg),
+              mom.data_ptr(), hs_out.data_ptr(), _stream())
+        return mom
+
+    def segment_moment_grad(self, M, seg, mean, coef):
+        C, E = M.shape
+        nseg = mean.shape[1]
+        mean, coef = mean.contiguous(), coef.contiguous()
+        self._chk(M, mean, coef)
+        gm = self.empty(C, E)
+        _call("pfsgnn_segment_moment_grad", M.data_ptr(), C, E, seg.data_ptr(), mean.data_ptr(),
+              coef.data_ptr(), int(nseg), gm.data_ptr(), _stream())
+        return gm
+
+    def _rows_ws(self, C, N):
+        nb = lib().pfsgnn_rows_ws_bytes(int(C), int(N))
+        ws = self.workspace(getattr(self, "_dims", None))
+        if ws.numel() < nb:
+            return torch.empty(nb, dtype=torch.uint8, device=self.device)
+        return ws
+
+    def rows_stats(self, X):
+        C, N = X.shape
+        self._chk(X)
+        mu, var = self.empty(C), self.empty(C)
+        ws = self._rows_ws(C, N)
+        _call("pfsgnn_rows_stats", X.data_ptr(), C, N, mu.data_ptr(), var.data_ptr(),
+              ws.data_ptr(), ws.numel(), _stream())
+        return mu, var
+
+    def rows_bn_sums(self, g, y, mu, inv):
+        C, N = y.shape
+        self._chk(g, y, mu, inv)
+        Sg, Sgx = self.empty(C), self.empty(C)
+        ws = self._rows_ws(C, N)
+        _call("pfsgnn_rows_bn_sums", g.data_ptr(), y.data_ptr(), C, N, mu.data_ptr(),
+              inv.data_ptr(), Sg.data_ptr(), Sgx.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+        return Sg, Sgx
+
+    def rows_axpby(self, g, y, alpha, gam1, gam0, out=None):
+        """out = alpha*g + gam1*y + gam0 per channel (out may be g or y)."""
+        C, N = y.shape
+        out = self.empty(C, N) if out is None else out
+        self._chk(g, y, alpha, gam1, gam0, out)
+        _call("pfsgnn_rows_axpby", g.data_ptr(), y.data_ptr(), C, N, alpha.data_ptr(),
+              gam1.data_ptr(), gam0.data_ptr(), out.data_ptr(), _stream())
+        return out
 
     # ------------------------------------------------------------ layout / optim
     def layout_analyze(self, edge_index, G, NF, NC):

@@ -32,12 +32,8 @@ def dlrelu(z, s=SLOPE):
     return torch.where(z > 0, torch.ones_like(z), torch.full_like(z, s))
 
 
-class Dims:
-    def __init__(self, G, NF, NC, F):
-        self.G, self.NF, self.NC, self.F = G, NF, NC, F
-        self.E = G * NF * NC
-        self.NS = G * NF
-        self.NT = G * NC
+from pfsgnn.engine import Dims  # noqa: E402,F401  (re-exported for the tests)
+from pfsgnn.sparse import SparseEdgeOps, SparseGeo  # noqa: E402
 
 
 def _edge_index(d, device):
@@ -72,6 +68,7 @@ class EmuBackend:
     def __init__(self, dtype=torch.float64):
         self.dtype = dtype
         self.device = torch.device("cpu")
+        self._sp = SparseEdgeOps(self)
 
     def empty(self, *shape):
         return torch.empty(*shape, dtype=self.dtype)
@@ -278,6 +275,8 @@ class EmuBackend:
         return alpha, gam0, gam1
 
     def moment_coef(self, mom, gst, n):
+        if isinstance(n, torch.Tensor):          # general graph: fiber CSR pointer
+            n = (n[1:] - n[:-1]).clamp(min=1).to(mom.dtype)
         """SModel moment backward (gnn.py:140-153) as per-fiber coefficients of
         g_m = C0 + d*(C1 + d*(C2 + d*C3)), d = m - mean.  gst = d(loss)/d
         [mean; std; skew; kurt] ([8F, NS])."""
@@ -294,6 +293,8 @@ class EmuBackend:
 
     # ------------------------------------------------------------ edge ops
     def edge_mlp_fwd(self, d, xe, xsc, xsh, Ps, Pt, W1, W2, b2):
+        if d.sp is not None:
+            return self._sp.edge_mlp_fwd(d, xe, xsc, xsh, Ps, Pt, W1, W2, b2)
         fib, cls = _edge_index(d, xe.device)
         F = d.F
         x = _aff(xe, xsc, xsh)
@@ -307,6 +308,8 @@ class EmuBackend:
         """Per-fiber centred moments of the SModel message (gnn.py:136-151).
         Returns mom [4, 2F, NS] = (mean, c2, c3, c4); writes the MLP inputs
         (mean, std, skew, kurt) into hs_out [8F, NS]."""
+        if d.sp is not None:
+            return self._sp.source_fwd(d, y, sc, sh, Qt, Ws1, Ws2, bs2, hs_out)
         fib, cls = _edge_index(d, y.device)
         F = d.F
         x = _aff(y, sc, sh)
@@ -327,6 +330,8 @@ class EmuBackend:
         return torch.stack([mean, c2, c3, c4])
 
     def target_fwd(self, d, y, sc, sh, Rs, Wt1):
+        if d.sp is not None:
+            return self._sp.target_fwd(d, y, sc, sh, Rs, Wt1)
         fib, cls = _edge_index(d, y.device)
         F = d.F
         x = _aff(y, sc, sh)
@@ -335,6 +340,8 @@ class EmuBackend:
         return _seg(at, cls, d.NT)
 
     def target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False):
+        if d.sp is not None:
+            return self._sp.target_bwd(d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=want_gxe)
         fib, cls = _edge_index(d, y.device)
         F = d.F
         x = _aff(y, sc, sh)
@@ -349,6 +356,8 @@ class EmuBackend:
                    bnstat, dWs1, dWs2, dbs2):
         """Returns (g_tot [F,E], GzS [2F, NT], Sg, Sgx).  ``coef`` = [4, 2F, NS]
         (C0..C3 of g_m = C0 + d*(C1 + d*(C2 + d*C3)), d = m - mean)."""
+        if d.sp is not None:
+            return self._sp.source_bwd(d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next, bnstat, dWs1, dWs2, dbs2)
         fib, cls = _edge_index(d, y.device)
         F = d.F
         x = _aff(y, sc, sh)
@@ -379,11 +388,15 @@ class EmuBackend:
         return g, GzS, Sg, Sgx
 
     def edge_bn_grad_sums(self, d, g, y, mu1, inv1):
+        if d.sp is not None:
+            return self._sp.edge_bn_grad_sums(d, g, y, mu1, inv1)
         xh = (y - mu1[:, None]) * inv1[:, None]
         return g.sum(1), (g * xh).sum(1)
 
     def edge_mlp_bwd(self, d, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1, W2,
                      dW1, dW2, db2, want_gxe=True):
+        if d.sp is not None:
+            return self._sp.edge_mlp_bwd(d, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1, W2, dW1, dW2, db2, want_gxe=want_gxe)
         fib, cls = _edge_index(d, y.device)
         F = d.F
         gy = alpha[:, None] * g_tot + gam0[:, None] + gam1[:, None] * y
@@ -400,6 +413,8 @@ class EmuBackend:
         return gxe, GzEs, GzEt
 
     def edge_apply(self, d, y, sc, sh):
+        if d.sp is not None:
+            return self._sp.edge_apply(d, y, sc, sh)
         return _aff(y, sc, sh).clone()
 
     # ------------------------------------------------------------ loss ops
@@ -509,6 +524,11 @@ class EmuBackend:
         return (g * NC + c) * NF + f
 
     def _perm_of(self, lay):
+        sp = getattr(lay, "sp", None)
+        if sp is not None:                     # general graph: caller edge -> position
+            inv = torch.empty_like(sp.user_of)
+            inv[sp.user_of] = torch.arange(sp.E)
+            return inv
         if lay.mode == 2:                      # Layout.CANONICAL
             return torch.arange(lay.G * lay.NF * lay.NC)
         if lay.mode == 1:                      # Layout.FIBER_MAJOR
@@ -523,6 +543,86 @@ class EmuBackend:
     def edges_from_canonical(self, y, sc, sh, lay, rowmajor=True):
         u = _aff(y, sc, sh)[:, self._perm_of(lay)]
         return u.t().contiguous() if rowmajor else u.contiguous()
+
+    # ------------------------------------------------------------ general graphs
+    # (emulation of pfsgnn_sparse_layout and the primitives of pfsgnn.sparse)
+    def sparse_layout(self, edge_index, G, NF, NC):
+        src, tgt = edge_index[0].long().cpu(), edge_index[1].long().cpu()
+        E = src.numel()
+        if not (bool((src >= 0).all()) and bool((src < G * NF).all()) and bool((tgt >= 0).all())
+                and bool((tgt < G * NC).all()) and bool(((src // NF) == (tgt // NC)).all())):
+            raise ValueError("edge_index has an edge out of range or joining nodes of different graphs")
+        user_of = torch.sort(src, stable=True).indices
+        src_p, tgt_p = src[user_of], tgt[user_of]
+        cls_ord = torch.sort(tgt_p, stable=True).indices
+        fib_ptr = torch.searchsorted(src_p, torch.arange(G * NF + 1))
+        cls_ptr = torch.searchsorted(tgt_p[cls_ord], torch.arange(G * NC + 1))
+        deg_t = (cls_ptr[1:] - cls_ptr[:-1]).to(self.dtype).reshape(1, -1)
+        return SparseGeo(E, src_p, tgt_p, user_of, fib_ptr, cls_ord, cls_ptr, deg_t)
+
+    def gather_cols(self, X, idx, mode=0, out=None, Z=None):
+        v = X[:, idx.long()]
+        if mode == 2:
+            v = v * dlrelu(Z)
+        if out is None:
+            return v
+        if mode == 1:
+            out += v
+        else:
+            out.copy_(v)
+        return out
+
+    def segment_sum(self, X, ord, ptr, nseg, act=False, out=None, add=False):
+        C, E = X.shape
+        cnt = (ptr[1:] - ptr[:-1]).long()
+        seg = torch.repeat_interleave(torch.arange(nseg), cnt)
+        pos = torch.arange(E) if ord is None else ord.long()
+        r = _seg((lrelu(X) if act else X)[:, pos], seg, nseg)
+        if out is None:
+            return r
+        if add:
+            out += r
+        else:
+            out.copy_(r)
+        return out
+
+    def segment_moments(self, M, ptr, nseg, hs_out):
+        C, E = M.shape
+        cnt = (ptr[1:] - ptr[:-1]).long()
+        seg = torch.repeat_interleave(torch.arange(nseg), cnt)
+        n = cnt.clamp(min=1).to(M.dtype)
+        mean = _seg(M, seg, nseg) / n
+        dd = M - mean[:, seg]
+        c2 = _seg(dd ** 2, seg, nseg) / n
+        c3 = _seg(dd ** 3, seg, nseg) / n
+        c4 = _seg(dd ** 4, seg, nseg) / n
+        var = torch.where(c2 > 0, c2, 0.01 * c2)
+        std = torch.sqrt(var + 1e-6)
+        hs_out[0:C] = mean
+        hs_out[C:2 * C] = std
+        hs_out[2 * C:3 * C] = c3 / std ** 3
+        hs_out[3 * C:4 * C] = c4 / std ** 4
+        return torch.stack([mean, c2, c3, c4])
+
+    def segment_moment_grad(self, M, seg, mean, coef):
+        seg = seg.long()
+        dd = M - mean[:, seg]
+        return coef[0][:, seg] + dd * (coef[1][:, seg] + dd * (coef[2][:, seg] + dd * coef[3][:, seg]))
+
+    def rows_stats(self, X):
+        mu = X.mean(1)
+        return mu, ((X - mu[:, None]) ** 2).mean(1)
+
+    def rows_bn_sums(self, g, y, mu, inv):
+        xh = (y - mu[:, None]) * inv[:, None]
+        return g.sum(1), (g * xh).sum(1)
+
+    def rows_axpby(self, g, y, alpha, gam1, gam0, out=None):
+        r = alpha[:, None] * g + gam1[:, None] * y + gam0[:, None]
+        if out is None:
+            return r
+        out.copy_(r)
+        return out
 
     # ------------------------------------------------------------ misc
     def noise_uniform(self, seed, E):

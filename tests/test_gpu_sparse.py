@@ -1,0 +1,178 @@
+"""General (non-complete) bipartite graphs on the GPU (pfsgnn.sparse +
+pfsgnn_sparse.hip) against the emulated op set and the CPU oracle.
+
+* pfsgnn_sparse_layout: every output equal to the emulation's (stable sorts:
+  exact);
+* the primitives (gather, segment sums with empty segments, moments, moment
+  gradient, row statistics): fp32 vs the float64 emulation;
+* the product modules (pfsgnn.GNN, as a user calls them) on random ragged
+  graphs -- empty fibers and classes, repeated pairs, shuffled caller order,
+  batches of graphs -- vs the float64 oracle, with the fp32 error level of the
+  oracle itself (two edge orders) as in tests/test_gpu_parity.py; the
+  objective is a random linear functional of every output (x_s, x_t, x_e, u);
+* bitwise reproducibility of a step (deterministic segment trees).
+"""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from emu_backend import EmuBackend  # noqa: E402
+from oracle.ref_gnn import Graph as OGraph  # noqa: E402
+from test_sparse_emu import sparse_problem, sparse_edges  # noqa: E402
+
+TOL_K = 16.0
+TOL_REL = 3e-5        # every op of the general path is exact-fp32 arithmetic
+
+
+def _hb():
+    from pfsgnn.gnn import backend
+    return backend()
+
+
+def check(name, ours, r64, r32s):
+    ours = ours.detach().double().cpu()
+    r64 = r64.detach().double().cpu()
+    scale = r64.abs().max().item()
+    ref_err = max((t.detach().double().cpu() - r64).abs().max().item() for t in r32s)
+    err = (ours - r64).abs().max().item()
+    bound = max(TOL_K * ref_err, TOL_REL * scale, 1e-6)
+    assert err <= bound, f"{name}: err {err:.3e} > bound {bound:.3e} (oracle32 {ref_err:.3e}, scale {scale:.3e})"
+
+
+@pytest.mark.parametrize("G,NF,NC,density,dup", [(1, 9, 5, 0.6, 0), (3, 70, 40, 0.3, 17),
+                                                  (2, 300, 9, 0.05, 5)])
+def test_sparse_layout_matches_emulation(G, NF, NC, density, dup):
+    gen = torch.Generator().manual_seed(G + NF)
+    ei = sparse_edges(G, NF, NC, density, gen, dup=dup)
+    a = _hb().sparse_layout(ei.cuda(), G, NF, NC)
+    b = EmuBackend().sparse_layout(ei, G, NF, NC)
+    for k in ("src_p", "tgt_p", "user_of", "fib_ptr", "cls_ord", "cls_ptr"):
+        assert torch.equal(getattr(a, k).long().cpu(), getattr(b, k).long()), k
+    assert torch.equal(a.deg_t.cpu().double(), b.deg_t)
+
+
+def test_sparse_layout_rejects_cross_graph_edges():
+    with pytest.raises(ValueError):
+        _hb().sparse_layout(torch.tensor([[0, 1], [0, 5]]).cuda(), 2, 3, 4)
+    with pytest.raises(ValueError):
+        _hb().sparse_layout(torch.tensor([[0, 7], [0, 1]]).cuda(), 2, 3, 4)
+
+
+def test_sparse_primitives_vs_emulation():
+    hb, em = _hb(), EmuBackend()
+    gen = torch.Generator().manual_seed(3)
+    G, NF, NC, C = 2, 50, 30, 20
+    ei = sparse_edges(G, NF, NC, 0.3, gen, dup=9)
+    sa, sb = hb.sparse_layout(ei.cuda(), G, NF, NC), em.sparse_layout(ei, G, NF, NC)
+    E = sb.E
+    X = torch.randn(C, E, generator=gen, dtype=torch.float64)
+    Z = torch.randn(C, E, generator=gen, dtype=torch.float64)
+    Ns = torch.randn(C, G * NF, generator=gen, dtype=torch.float64)
+    Nt = torch.randn(C, G * NC, generator=gen, dtype=torch.float64)
+    c = lambda t: t.float().cuda().contiguous()  # noqa: E731
+
+    def close(a, b, tol=2e-5):
+        b = b.double()
+        assert (a.double().cpu() - b).abs().max().item() <= tol * max(b.abs().max().item(), 1.0)
+
+    close(hb.gather_cols(c(Ns), sa.src_p), em.gather_cols(Ns, sb.src_p))
+    close(hb.gather_cols(c(Nt), sa.tgt_p, mode=2, Z=c(Z)), em.gather_cols(Nt, sb.tgt_p, mode=2, Z=Z))
+    acc = c(X)
+    hb.gather_cols(c(Nt), sa.tgt_p, mode=1, out=acc)
+    close(acc, X + Nt[:, sb.tgt_p])
+    close(hb.segment_sum(c(X), None, sa.fib_ptr, G * NF), em.segment_sum(X, None, sb.fib_ptr, G * NF))
+    close(hb.segment_sum(c(X), sa.cls_ord, sa.cls_ptr, G * NC, act=True),
+          em.segment_sum(X, sb.cls_ord, sb.cls_ptr, G * NC, act=True))
+    hs_a, hs_b = hb.empty(4 * C, G * NF), torch.empty(4 * C, G * NF, dtype=torch.float64)
+    ma = hb.segment_moments(c(X), sa.fib_ptr, G * NF, hs_a)
+    mb = em.segment_moments(X, sb.fib_ptr, G * NF, hs_b)
+    close(ma, mb, 1e-4)
+    close(hs_a, hs_b, 1e-4)
+    coef = torch.randn(4, C, G * NF, generator=gen, dtype=torch.float64)
+    close(hb.segment_moment_grad(c(X), sa.src_p, c(mb[0]), c(coef)),
+          em.segment_moment_grad(X, sb.src_p, mb[0], coef), 1e-4)
+    mu, var = hb.rows_stats(c(X))
+    mu2, var2 = em.rows_stats(X)
+    close(mu, mu2)
+    close(var, var2)
+    inv = 1.0 / torch.sqrt(var2 + 1e-5)
+    sg, sgx = hb.rows_bn_sums(c(Z), c(X), c(mu2), c(inv))
+    sg2, sgx2 = em.rows_bn_sums(Z, X, mu2, inv)
+    close(sg, sg2, 1e-4)
+    close(sgx, sgx2, 1e-4)
+    al, g1, g0 = (torch.randn(C, generator=gen, dtype=torch.float64) for _ in range(3))
+    close(hb.rows_axpby(c(Z), c(X), c(al), c(g1), c(g0)), em.rows_axpby(Z, X, al, g1, g0))
+
+
+def _oracle(model, graph, w, dtype, reverse=False):
+    m = copy.deepcopy(model).to(dtype)
+    m.train()
+    ei, xe, we = graph.edge_index, graph.x_e, w[2]
+    if reverse:
+        ei, xe, we = ei.flip(1), xe.flip(0), we.flip(0)
+    out = m(OGraph(ei, graph.x_s.to(dtype), graph.x_t.to(dtype), xe.to(dtype), graph.x_u.to(dtype),
+                   graph.s_batch, graph.t_batch))
+    loss = ((out.x_s * w[0].to(dtype)).sum() + (out.x_t * w[1].to(dtype)).sum()
+            + (out.x_e * we.to(dtype)).sum() + (out.x_u * w[3].to(dtype)).sum())
+    loss.backward()
+    if reverse:
+        out.x_e = out.x_e.flip(0)
+    return m, out
+
+
+def _ours(model, graph, w, B, normed=True):
+    import pfsgnn
+    gnn = pfsgnn.GNN(B=B, Fdim=10, T=12, F_s=1, F_t=2, normed=normed).cuda()
+    gnn.load_state_dict({k: v.float() for k, v in model.state_dict().items()})
+    gnn.train()
+    data = pfsgnn.BipartiteData(graph.edge_index, graph.x_s.float(), graph.x_t.float(),
+                                graph.x_e.float(), graph.x_u.float())
+    gnn.zero_grad()
+    out = gnn(data)
+    wc = [t.float().cuda() for t in w]
+    loss = ((out.x_s * wc[0]).sum() + (out.x_t * wc[1]).sum() + (out.x_e * wc[2]).sum()
+            + (out.x_u * wc[3]).sum())
+    loss.backward()
+    torch.cuda.synchronize()
+    return gnn, out
+
+
+def _weights(graph, G, NF, NC, gen, F=10):
+    E = graph.edge_index.shape[1]
+    return [torch.randn(n, F, generator=gen, dtype=torch.float64) for n in (G * NF, G * NC, E, G)]
+
+
+@pytest.mark.parametrize("G,NF,NC,density,B,dup,normed", [
+    (1, 40, 12, 0.5, 2, 3, True), (2, 24, 16, 0.3, 2, 0, True), (3, 10, 7, 0.7, 3, 4, True),
+    (1, 300, 64, 0.08, 2, 0, True), (2, 24, 16, 0.4, 2, 2, False)])
+def test_sparse_gnn_matches_oracle(G, NF, NC, density, B, dup, normed):
+    model, graph, gen = sparse_problem(G, NF, NC, density, B=B, seed=G + NF, dup=dup, normed=normed)
+    w = _weights(graph, G, NF, NC, gen)
+    m64, o64 = _oracle(model, graph, w, torch.float64)
+    r32 = [_oracle(model, graph, w, torch.float32, reverse=rv) for rv in (False, True)]
+    gnn, out = _ours(model, graph, w, B, normed=normed)
+    for nm in ("x_e", "x_s", "x_t", "x_u"):
+        check(nm, getattr(out, nm), getattr(o64, nm), [getattr(r[1], nm) for r in r32])
+    p64 = dict(m64.named_parameters())
+    p32 = [dict(r[0].named_parameters()) for r in r32]
+    for name, p in gnn.named_parameters():
+        z = torch.zeros_like(p64[name])
+        check("grad " + name, p.grad, p64[name].grad if p64[name].grad is not None else z,
+              [q[name].grad if q[name].grad is not None else z.float() for q in p32])
+    b64 = m64.state_dict()
+    for k, v in gnn.state_dict().items():
+        if "running" in k or "num_batches" in k:
+            check(k, v.double(), b64[k].double(), [r[0].state_dict()[k].double() for r in r32])
+
+
+def test_sparse_step_is_bitwise_reproducible():
+    model, graph, gen = sparse_problem(2, 200, 50, 0.2, B=2, seed=9, dup=11)
+    w = _weights(graph, 2, 200, 50, gen)
+    g1, o1 = _ours(model, graph, w, 2)
+    g2, o2 = _ours(model, graph, w, 2)
+    assert torch.equal(o1.x_e, o2.x_e) and torch.equal(o1.x_s, o2.x_s)
+    for (n, a), (_, b) in zip(g1.named_parameters(), g2.named_parameters()):
+        assert torch.equal(a.grad, b.grad), n
