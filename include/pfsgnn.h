@@ -143,6 +143,29 @@ int pfsgnn_wgrad_cat_part(const float* dY, int M, const pfsgnn_seg* segs, int ns
                           void* part, size_t part_bytes, pfsgnn_red* red_out, int* nred_out,
                           void* stream);
 int pfsgnn_reduce_batch(const pfsgnn_red* reds, int n, void* stream);
+/* A backward pass's weight gradients in a few launches: each job is one
+ * pfsgnn_wgrad_cat (dW[:, col_s..] += dY . act(x_s)^T, db += dbscale * sum dY);
+ * jobs of the same kernel shape share a launch, then every reduction runs
+ * batched.  Per job the result is bitwise that of pfsgnn_wgrad_cat.  The
+ * inputs must be unchanged since the job was formed (the host defers jobs over
+ * a backward pass: the gradients of nn.Linear weights in gnn.py:65-71, read by
+ * the optimizer only, train.py:140-141).  `part`: a scratch arena of
+ * pfsgnn_wgrad_multi_bytes(jobs, n) bytes. */
+typedef struct {
+  const float* dY;
+  int M;
+  const pfsgnn_seg* segs;
+  int nseg;
+  int N;
+  int act_in;
+  float* dW;
+  int lddw;
+  float* db;
+  float dbscale;
+} pfsgnn_wgrad_job;
+size_t pfsgnn_wgrad_multi_bytes(const pfsgnn_wgrad_job* jobs, int n);
+int pfsgnn_wgrad_multi(const pfsgnn_wgrad_job* jobs, int n, void* part, size_t part_bytes,
+                       void* stream);
 
 /* BatchNorm1d training forward over N rows (biased var for the output,
  * unbiased for the running update; rm/rv may be NULL). */

@@ -287,47 +287,46 @@ __global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__
                                                        float* __restrict__ Y,
                                                        float* __restrict__ mu,
                                                        float* __restrict__ var) {
-  __shared__ double acc[16][16][3];
+  __shared__ double acc[16][16][2];
+  __shared__ double mean_s[16];
   __shared__ float cf[4][16];
   const int t = threadIdx.x, c = t & 15, u = t >> 4;
-  double C0 = 0.0, M0 = 0.0, Q0 = 0.0;
   constexpr int PB = 32;  // partials per thread: nb <= 512 (the MLP grid)
   float pc[PB], pm[PB], pq[PB];
 #pragma unroll
-  for (int i = 0; i < PB; ++i) {  // every load in flight before the merge chain
+  for (int i = 0; i < PB; ++i) {  // every load in flight before the sums
     const int b = u + 16 * i;
     const float* p = part + (size_t)(b < nb ? b : 0) * PART_LEN;
     pc[i] = b < nb ? p[0] : 0.f;
     pm[i] = b < nb ? p[1 + c] : 0.f;
     pq[i] = b < nb ? p[17 + c] : 0.f;
   }
+  // the partials combined in closed form (fixed order, no serial chain of
+  // divisions): mean = sum c_b m_b / N, M2 = sum (q_b + c_b (m_b - mean)^2)
+  double S = 0.0;
 #pragma unroll
-  for (int i = 0; i < PB; ++i) {
-    const double cb = pc[i], mb = pm[i], qb = pq[i];
-    const double tot = C0 + cb;
-    if (tot > 0.0) {
-      const double d = mb - M0;
-      M0 += d * (cb / tot);
-      Q0 += qb + d * d * (C0 * cb / tot);
-    }
-    C0 = tot;
-  }
-  acc[u][c][0] = C0;
-  acc[u][c][1] = M0;
-  acc[u][c][2] = Q0;
+  for (int i = 0; i < PB; ++i) S += (double)pc[i] * (double)pm[i];
+  acc[u][c][0] = S;
   __syncthreads();
   if (t < 16) {
-    double Cc = 0.0, Mc = 0.0, Qc = 0.0;
-    for (int s = 0; s < 16; ++s) {
-      const double cb = acc[s][t][0], mb = acc[s][t][1], qb = acc[s][t][2];
-      const double tot = Cc + cb;
-      if (tot > 0.0) {
-        const double d = mb - Mc;
-        Mc += d * (cb / tot);
-        Qc += qb + d * d * (Cc * cb / tot);
-      }
-      Cc = tot;
-    }
+    double St = 0.0;
+    for (int s = 0; s < 16; ++s) St += acc[s][t][0];
+    mean_s[t] = St / (double)N;
+  }
+  __syncthreads();
+  const double mean = mean_s[c];
+  double Q = 0.0;
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const double d = (double)pm[i] - mean;
+    Q += (double)pq[i] + (double)pc[i] * d * d;
+  }
+  acc[u][c][1] = Q;
+  __syncthreads();
+  if (t < 16) {
+    double Qc = 0.0;
+    for (int s = 0; s < 16; ++s) Qc += acc[s][t][1];
+    const double Mc = mean_s[t];
     const double v = Qc / (double)N;
     const float muf = (float)Mc, vf = (float)v;
     const bool live = t < O;
@@ -346,10 +345,11 @@ __global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__
     }
   }
   __syncthreads();
-  const size_t tot = (size_t)O * N;
-  for (size_t i = (size_t)blockIdx.x * 256 + t; i < tot; i += (size_t)gridDim.x * 256) {
-    const int o = (int)(i / (size_t)N);
-    Y[i] = (Yp[i] - cf[0][o]) * cf[1][o] * cf[2][o] + cf[3][o];
+  for (int o = 0; o < O; ++o) {
+    const float m = cf[0][o], a = cf[1][o] * cf[2][o], b = cf[3][o];
+    const float* yp = Yp + (size_t)o * N;
+    float* y = Y + (size_t)o * N;
+    for (int n = blockIdx.x * 256 + t; n < N; n += gridDim.x * 256) y[n] = (yp[n] - m) * a + b;
   }
 }
 

@@ -542,16 +542,16 @@ extern "C" int pfsgnn_lin_t(const float* W, int ldw, int M, int K, const float* 
 #define WG_ONE 3
 #define WG_NONE 4
 template <int TMAX, int PER>
-__global__ __launch_bounds__(512) void k_wgrad(const float* __restrict__ dY, int M, XSegs S, int K,
-                                               int K1, int N, int act_in, int chunk, int vec,
-                                               float* __restrict__ part) {
+__device__ __forceinline__ void wgrad_block(const float* __restrict__ dY, int M, const XSegs& S,
+                                            int K, int K1, int N, int act_in, int chunk, int vec,
+                                            float* __restrict__ part, int bid) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int MR = (M + 15) & ~15, KR = (K1 + 15) & ~15;
   float* Sd = sm;
   float* Sx = sm + MR * WG_LD;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63, col = lane & 15, kq = lane >> 4;
   const int KT = KR / 16, NTILE = (MR / 16) * KT;
-  const int n0 = blockIdx.x * chunk, n1 = min(N, n0 + chunk);
+  const int n0 = bid * chunk, n1 = min(N, n0 + chunk);
   const int Gc = S.npg ? N / S.npg : 1;
   floatx4 acc[TMAX];
 #pragma unroll
@@ -666,10 +666,43 @@ __global__ __launch_bounds__(512) void k_wgrad(const float* __restrict__ dY, int
       for (int r = 0; r < 4; ++r) {
         const int m = 16 * mt + 4 * kq + r, k = 16 * kt + col;
         if (m < M && k < K1)
-          part[(size_t)blockIdx.x * M * K1 + (size_t)m * K1 + k] = acc[j][r];
+          part[(size_t)bid * M * K1 + (size_t)m * K1 + k] = acc[j][r];
       }
     }
   }
+}
+
+template <int TMAX, int PER>
+__global__ __launch_bounds__(512) void k_wgrad(const float* __restrict__ dY, int M, XSegs S, int K,
+                                               int K1, int N, int act_in, int chunk, int vec,
+                                               float* __restrict__ part) {
+  wgrad_block<TMAX, PER>(dY, M, S, K, K1, N, act_in, chunk, vec, part, blockIdx.x);
+}
+
+// Several independent weight gradients in one launch (pfsgnn_wgrad_multi):
+// job j owns blocks [blk0_j, blk0_j + nblk_j); the table rides in the kernel
+// arguments and a block selects its job with constant indices (uniform).
+#define WG_MULTI 8
+struct WgJob {
+  const float* dY;
+  XSegs S;
+  float* part;
+  int M, K, K1, N, act_in, chunk, vec, blk0;
+};
+struct WgTable {
+  WgJob j[WG_MULTI];
+  int njob;
+};
+
+template <int TMAX, int PER>
+__global__ __launch_bounds__(512) void k_wgrad_multi(WgTable T) {
+  const int b = blockIdx.x;
+  WgJob J = T.j[0];
+#pragma unroll
+  for (int u = 1; u < WG_MULTI; ++u)
+    if (u < T.njob && b >= T.j[u].blk0) J = T.j[u];
+  wgrad_block<TMAX, PER>(J.dY, J.M, J.S, J.K, J.K1, J.N, J.act_in, J.chunk, J.vec, J.part,
+                         b - J.blk0);
 }
 
 static int wgrad_blocks(int N) {
@@ -681,65 +714,91 @@ static size_t wgrad_part_bytes(int M, int K1, int N) {
   return (size_t)wgrad_blocks(N) * M * K1 * sizeof(float);
 }
 
+// Launch geometry of one weight gradient (shared by the single and the
+// batched launches).
+struct WgPlan {
+  int K1, nblk, chunk, tm, per, vec;
+  size_t lds, part_bytes;
+};
+
+static int wgrad_plan(const float* dY, int M, const XSegs& S, int nseg, int K, int N, bool has_db,
+                      const char* where, WgPlan& P) {
+  PF_REQUIRE(M <= 256 && K <= 256, where, "M, K too large");
+  const int nbk = wgrad_blocks(N);
+  P.K1 = K + (has_db ? 1 : 0);
+  P.chunk = ((N + nbk - 1) / nbk + 63) / 64 * 64;
+  P.nblk = (N + P.chunk - 1) / P.chunk;
+  P.part_bytes = (size_t)P.nblk * M * P.K1 * sizeof(float);
+  const int MR = (M + 15) & ~15, KR = (P.K1 + 15) & ~15;
+  P.lds = (size_t)(MR + KR) * WG_LD * sizeof(float);
+  const int ntile = (MR / 16) * (KR / 16);
+  // float4 staging when every row starts 16-byte aligned
+  bool vec = (N % 4 == 0) && ((uintptr_t)dY % 16 == 0);
+  for (int i = 0; i < nseg; ++i)
+    if (!S.bc[i] && (uintptr_t)S.p[i] % 16 != 0) vec = false;
+  P.vec = vec ? 1 : 0;
+  const int items = (M + P.K1) * 16;
+  P.per = items <= 512 ? 1 : items <= 1024 ? 2 : items <= 2048 ? 4 : items <= 4096 ? 8 : 16;
+  PF_REQUIRE(items <= 16 * 64 * WG_WAVES, where, "M + K too large");
+  P.tm = ntile <= WG_WAVES ? 1 : ntile <= 2 * WG_WAVES ? 2 : ntile <= 4 * WG_WAVES ? 4
+       : ntile <= 8 * WG_WAVES ? 8 : ntile <= 16 * WG_WAVES ? 16 : -1;
+  PF_REQUIRE(P.tm > 0, where, "too many output tiles");
+  return 0;
+}
+
+// the reductions finishing one weight gradient's partials: each input block's
+// dW columns, plus db
+static int wgrad_reds(const XSegs& S, int nseg, int K, int M, const WgPlan& P, float* part,
+                      float* dW, int lddw, float* db, float dbscale, RedDesc* rd) {
+  int nr = 0;
+  for (int i = 0; i < nseg; ++i) {
+    const int k0 = S.k0[i], k1 = (i + 1 < nseg) ? S.k0[i + 1] : K;
+    rd[nr++] = {part + k0, P.nblk, (size_t)M * P.K1, P.K1, M, k1 - k0, dW + S.wcol[i], lddw, 1,
+                1.f};
+  }
+  if (db) rd[nr++] = {part + K, P.nblk, (size_t)M * P.K1, P.K1, M, 1, db, 1, 1, dbscale};
+  return nr;
+}
+
+// Dynamic LDS above 64 KB needs the attribute once per instantiation.
+template <typename Fn>
+static bool wg_allow_lds(Fn fn) {
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+}
+
+#define PF_WG_ALL(X) \
+  X(1, 1) X(1, 2) X(1, 4) X(1, 8) X(2, 1) X(2, 2) X(2, 4) X(2, 8) X(4, 1) X(4, 2) X(4, 4) \
+  X(4, 8) X(8, 1) X(8, 2) X(8, 4) X(8, 8) X(16, 1) X(16, 2) X(16, 4) X(16, 8) X(16, 16)
+
 // Launches the per-block partials of dW (and db) into ws and describes the
 // reduction that finishes them (rd[0..*nr)); the caller launches it now or
 // batches it with others (pfsgnn_reduce_batch).
 static int wgrad_launch(const float* dY, int M, const XSegs& S, int nseg, int K, int N, int act_in,
                         float* dW, int lddw, float* db, float dbscale, void* ws, size_t ws_bytes,
                         hipStream_t st, const char* where, RedDesc* rd, int* nr_out) {
-  PF_REQUIRE(M <= 256 && K <= 256, where, "M, K too large");
-  const int nbk = wgrad_blocks(N);
-  const int K1 = K + (db ? 1 : 0);
-  const size_t need = wgrad_part_bytes(M, K1, N);
-  PF_REQUIRE(ws && ws_bytes >= need, where, "workspace too small");
-  const int chunk = ((N + nbk - 1) / nbk + 63) / 64 * 64;
-  const int nblk = (N + chunk - 1) / chunk;
+  WgPlan P;
+  if (int rc = wgrad_plan(dY, M, S, nseg, K, N, db != nullptr, where, P)) return rc;
+  PF_REQUIRE(ws && ws_bytes >= P.part_bytes, where, "workspace too small");
   float* part = reinterpret_cast<float*>(ws);
-  const int MR = (M + 15) & ~15, KR = (K1 + 15) & ~15;
-  const size_t lds = (size_t)(MR + KR) * WG_LD * sizeof(float);
-  const int ntile = (MR / 16) * (KR / 16);
-  // float4 staging when every row starts 16-byte aligned
-  bool vec = (N % 4 == 0) && ((uintptr_t)dY % 16 == 0);
-  for (int i = 0; i < nseg; ++i)
-    if (!S.bc[i] && (uintptr_t)S.p[i] % 16 != 0) vec = false;
-  const int items = (M + K1) * 16;
-  const int per = items <= 512 ? 1 : items <= 1024 ? 2 : items <= 2048 ? 4 : items <= 4096 ? 8 : 16;
-  PF_REQUIRE(items <= 16 * 64 * WG_WAVES, where, "M + K too large");
-  const int tm = ntile <= WG_WAVES ? 1 : ntile <= 2 * WG_WAVES ? 2 : ntile <= 4 * WG_WAVES ? 4
-               : ntile <= 8 * WG_WAVES ? 8 : ntile <= 16 * WG_WAVES ? 16 : -1;
-  PF_REQUIRE(tm > 0, where, "too many output tiles");
-  const dim3 grid(nblk), blk(64 * WG_WAVES);
+  const dim3 grid(P.nblk), blk(64 * WG_WAVES);
   bool launched = false;
-#define PF_WG(T, P)                                                                            \
-  {                                                                                            \
-    auto fn = &k_wgrad<T, P>;                                                                  \
+#define PF_WG(T, PP)                                                                           \
+  if (P.tm == T && P.per == PP) {                                                              \
+    auto fn = &k_wgrad<T, PP>;                                                                 \
     static bool attr = false;                                                                  \
     if (!attr) {                                                                               \
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn),                               \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=       \
-          hipSuccess)                                                                          \
-        return pf::fail(where, "hipFuncSetAttribute");                                         \
+      if (!wg_allow_lds(fn)) return pf::fail(where, "hipFuncSetAttribute");                    \
       attr = true;                                                                             \
     }                                                                                          \
-    if (tm == T && per == P) {                                                                 \
-      hipLaunchKernelGGL(fn, grid, blk, lds, st, dY, M, S, K, K1, N, act_in, chunk, (int)vec,  \
-                         part);                                                                \
-      launched = true;                                                                         \
-    }                                                                                          \
+    hipLaunchKernelGGL(fn, grid, blk, P.lds, st, dY, M, S, K, P.K1, N, act_in, P.chunk, P.vec, \
+                       part);                                                                  \
+    launched = true;                                                                           \
   }
-#define PF_WG_P(T) PF_WG(T, 1) PF_WG(T, 2) PF_WG(T, 4) PF_WG(T, 8)
-  PF_WG_P(1) PF_WG_P(2) PF_WG_P(4) PF_WG_P(8) PF_WG_P(16) PF_WG(16, 16)
-#undef PF_WG_P
+  PF_WG_ALL(PF_WG)
 #undef PF_WG
   if (!launched) return pf::fail(where, "no kernel for this shape");
-  // the reduction: each input block's dW columns, plus db
-  int nr = 0;
-  for (int i = 0; i < nseg; ++i) {
-    const int k0 = S.k0[i], k1 = (i + 1 < nseg) ? S.k0[i + 1] : K;
-    rd[nr++] = {part + k0, nblk, (size_t)M * K1, K1, M, k1 - k0, dW + S.wcol[i], lddw, 1, 1.f};
-  }
-  if (db) rd[nr++] = {part + K, nblk, (size_t)M * K1, K1, M, 1, db, 1, 1, dbscale};
-  *nr_out = nr;
+  *nr_out = wgrad_reds(S, nseg, K, M, P, part, dW, lddw, db, dbscale, rd);
   return pf::check_launch(where);
 }
 
@@ -798,6 +857,112 @@ extern "C" int pfsgnn_wgrad_cat_part(const float* dY, int M, const pfsgnn_seg* s
                   rd[i].ldo, rd[i].add, rd[i].scale};
   *nred_out = nr;
   return 0;
+}
+
+// ------------------------------------------------- batched weight gradients
+// Many independent weight gradients (a backward pass's worth, deferred by the
+// host) in a few launches: jobs with the same kernel shape share a launch (up
+// to WG_MULTI per launch), then all their reductions go through the batched
+// reduce.  Per job the partials and the reduction order are those of
+// pfsgnn_wgrad_cat: results are bitwise identical.
+static int wgrad_job_prep(const pfsgnn_wgrad_job& jb, XSegs& S, int& K, WgPlan& P,
+                          const char* where) {
+  PF_REQUIRE(jb.dY && jb.dW && jb.M > 0 && jb.N > 0, where, "bad job");
+  K = make_segs(jb.segs, jb.nseg, jb.N, S);
+  PF_REQUIRE(K > 0, where, "bad segment list");
+  return wgrad_plan(jb.dY, jb.M, S, jb.nseg, K, jb.N, jb.db != nullptr, where, P);
+}
+
+extern "C" size_t pfsgnn_wgrad_multi_bytes(const pfsgnn_wgrad_job* jobs, int n) {
+  size_t tot = 0;
+  for (int i = 0; i < n; ++i) {
+    XSegs S;
+    int K;
+    WgPlan P;
+    if (wgrad_job_prep(jobs[i], S, K, P, "pfsgnn_wgrad_multi_bytes")) return 0;
+    tot += align256(P.part_bytes);
+  }
+  return tot + 256;
+}
+
+extern "C" int pfsgnn_wgrad_multi(const pfsgnn_wgrad_job* jobs, int n, void* part,
+                                  size_t part_bytes, void* stream) {
+  const char* where = "pfsgnn_wgrad_multi";
+  PF_REQUIRE(n >= 0 && (jobs || n == 0), where, "bad arguments");
+  if (n == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  std::vector<WgJob> J(n);
+  std::vector<WgPlan> PL(n);
+  std::vector<RedDesc> reds;
+  size_t off = 0;
+  char* base = static_cast<char*>(part);
+  for (int i = 0; i < n; ++i) {
+    int K;
+    if (int rc = wgrad_job_prep(jobs[i], J[i].S, K, PL[i], where)) return rc;
+    PF_REQUIRE(part && off + PL[i].part_bytes <= part_bytes, where, "partial arena too small");
+    float* p = reinterpret_cast<float*>(base + off);
+    off += align256(PL[i].part_bytes);
+    const pfsgnn_wgrad_job& jb = jobs[i];
+    J[i].dY = jb.dY;
+    J[i].part = p;
+    J[i].M = jb.M;
+    J[i].K = K;
+    J[i].K1 = PL[i].K1;
+    J[i].N = jb.N;
+    J[i].act_in = jb.act_in;
+    J[i].chunk = PL[i].chunk;
+    J[i].vec = PL[i].vec;
+    RedDesc rd[PF_MAX_SEG + 1];
+    const int nr = wgrad_reds(J[i].S, jb.nseg, K, jb.M, PL[i], p, jb.dW, jb.lddw, jb.db,
+                              jb.dbscale, rd);
+    reds.insert(reds.end(), rd, rd + nr);
+  }
+  // group by kernel shape, in job order; launch WG_MULTI at a time
+  std::vector<bool> done(n, false);
+  for (int i = 0; i < n; ++i) {
+    if (done[i]) continue;
+    std::vector<int> grp;
+    for (int k = i; k < n; ++k)
+      if (!done[k] && PL[k].tm == PL[i].tm && PL[k].per == PL[i].per) {
+        grp.push_back(k);
+        done[k] = true;
+      }
+    for (size_t g0 = 0; g0 < grp.size(); g0 += WG_MULTI) {
+      WgTable T{};
+      int blocks = 0;
+      size_t lds = 0;
+      const int m = (int)std::min<size_t>(WG_MULTI, grp.size() - g0);
+      for (int u = 0; u < m; ++u) {
+        T.j[u] = J[grp[g0 + u]];
+        T.j[u].blk0 = blocks;
+        blocks += PL[grp[g0 + u]].nblk;
+        lds = std::max(lds, PL[grp[g0 + u]].lds);
+      }
+      T.njob = m;
+      bool launched = false;
+      const int tm = PL[i].tm, per = PL[i].per;
+#define PF_WGM(TT, PP)                                                                    \
+  if (tm == TT && per == PP) {                                                            \
+    auto fn = &k_wgrad_multi<TT, PP>;                                                     \
+    static bool attr = false;                                                             \
+    if (!attr) {                                                                          \
+      if (!wg_allow_lds(fn)) return pf::fail(where, "hipFuncSetAttribute");               \
+      attr = true;                                                                        \
+    }                                                                                     \
+    hipLaunchKernelGGL(fn, dim3(blocks), dim3(64 * WG_WAVES), lds, st, T);                \
+    launched = true;                                                                      \
+  }
+      PF_WG_ALL(PF_WGM)
+#undef PF_WGM
+      if (!launched) return pf::fail(where, "no kernel for this shape");
+    }
+  }
+  // the reductions, batched (a launch never holds two into the same cells)
+  std::vector<pfsgnn_red> rr(reds.size());
+  for (size_t i = 0; i < reds.size(); ++i)
+    rr[i] = {reds[i].part, reds[i].nb, reds[i].plen, reds[i].ldp, reds[i].rows, reds[i].cols,
+             reds[i].out, reds[i].ldo, reds[i].add, reds[i].scale};
+  return pfsgnn_reduce_batch(rr.data(), (int)rr.size(), stream);
 }
 
 // Output rectangles of two reductions intersect?  Exact when both write rows

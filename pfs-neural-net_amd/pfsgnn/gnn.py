@@ -335,6 +335,35 @@ class _FlatMixin(_ParamMixin):
     def _recording_grads(self):
         return _GradRecorder(self._flat_grads())
 
+    def _bump_batches(self, edge_keys=(), node_keys=()):
+        """num_batches_tracked += 2 (edge BatchNorms, applied twice) / += 1 for
+        every BatchNorm of a forward, as ONE device add: the counters are
+        views of one int64 buffer (re-made if a buffer was replaced, e.g. by
+        ``.to()`` or ``load_state_dict`` assigning new tensors)."""
+        key = (tuple(edge_keys), tuple(node_keys))
+        names = [k + "num_batches_tracked" for k in key[0] + key[1]]
+        cache = self.__dict__.get("_pf_nbt")
+        bufs = None
+        if cache is not None and cache[0] == key:
+            flat = cache[1]
+            bufs = dict(self.named_buffers())
+            if any(bufs[n].data_ptr() != flat.data_ptr() + 8 * i or bufs[n].device != flat.device
+                   for i, n in enumerate(names)):
+                cache = None
+        else:
+            cache = None
+        if cache is None:
+            bufs = bufs or dict(self.named_buffers())
+            flat = torch.stack([bufs[n].detach().reshape(()) for n in names]).contiguous()
+            for i, n in enumerate(names):
+                mod = self.get_submodule(n.rsplit(".", 1)[0])
+                mod._buffers["num_batches_tracked"] = flat[i]
+            inc = torch.tensor([2] * len(key[0]) + [1] * len(key[1]), dtype=flat.dtype,
+                               device=flat.device)
+            cache = (key, flat, inc)
+            self.__dict__["_pf_nbt"] = cache
+        cache[1].add_(cache[2])
+
     def _mark_live(self, names):
         """Parameters a backward wrote (the ones the reference's autograd would
         give a .grad); FusedAdam skips the others when weight_decay != 0."""

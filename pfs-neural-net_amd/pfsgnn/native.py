@@ -59,6 +59,16 @@ class OSeg(ctypes.Structure):
 
 OSEGP = ctypes.POINTER(OSeg)
 
+
+class WgJob(ctypes.Structure):
+    """pfsgnn_wgrad_job (include/pfsgnn.h): one deferred weight gradient."""
+    _fields_ = [("dY", ctypes.c_void_p), ("M", ctypes.c_int), ("segs", SEGP), ("nseg", ctypes.c_int),
+                ("N", ctypes.c_int), ("act_in", ctypes.c_int), ("dW", ctypes.c_void_p),
+                ("lddw", ctypes.c_int), ("db", ctypes.c_void_p), ("dbscale", ctypes.c_float)]
+
+
+WGJP = ctypes.POINTER(WgJob)
+
 _SIGS = {
     "pfsgnn_version": ([], ctypes.c_char_p),
     "pfsgnn_last_error": ([], ctypes.c_char_p),
@@ -79,6 +89,8 @@ _SIGS = {
     "pfsgnn_wgrad_cat_part": ([P, I, SEGP, I, I, I, P, I, P, FL, P, SZ, REDP,
                                ctypes.POINTER(ctypes.c_int), P], I),
     "pfsgnn_reduce_batch": ([REDP, I, P], I),
+    "pfsgnn_wgrad_multi_bytes": ([WGJP, I], SZ),
+    "pfsgnn_wgrad_multi": ([WGJP, I, P, SZ, P], I),
     "pfsgnn_bn_fwd": ([P, I, I, P, P, P, P, FL, FL, P, P, P, P, SZ, P], I),
     "pfsgnn_bn_bwd": ([P, P, P, P, P, FL, I, I, P, P, P, P, SZ, P], I),
     "pfsgnn_mlp_ws_bytes": ([I], SZ),
@@ -293,61 +305,47 @@ class HipBackend:
         return out
 
     # ----------------------------------------------- deferred weight gradients
-    # Between defer_begin() and defer_flush(), wgrad/wgrad_cat only launch their
-    # per-block partials (into a private arena) and queue the reductions; the
-    # flush finishes them all in a few launches (pfsgnn_reduce_batch).  The
-    # engine defers over a backward pass: its weight gradients are read only by
-    # the optimizer.
+    # Between defer_begin() and defer_flush(), wgrad/wgrad_cat only record a
+    # job; the flush computes them all in a few launches (pfsgnn_wgrad_multi:
+    # jobs of one kernel shape share a launch, the reductions are batched).
+    # The engine defers over a backward pass: its weight gradients are read
+    # only by the optimizer, and the jobs' inputs are activations and
+    # gradients that no later op of the pass writes (engine.Engine.backward).
     def defer_begin(self):
-        self._defer = []
-        self._arena_off = 0
+        self._jobs = []
 
     def defer_flush(self):
-        reds, self._defer = getattr(self, "_defer", None), None
-        if not reds:
+        jobs, self._jobs = getattr(self, "_jobs", None), None
+        if not jobs:
             return
-        arr = (Red * len(reds))(*reds)
-        _call("pfsgnn_reduce_batch", arr, len(reds), _stream())
-
-    def _arena_take(self, nbytes):
-        nbytes = (int(nbytes) + 255) & ~255
+        arr = (WgJob * len(jobs))()
+        for i, (job, _keep) in enumerate(jobs):
+            arr[i] = job
+        need = lib().pfsgnn_wgrad_multi_bytes(arr, len(jobs))
+        if need == 0:
+            raise RuntimeError("pfsgnn_wgrad_multi_bytes: " + lib().pfsgnn_last_error().decode())
         arena = getattr(self, "_arena", None)
-        if arena is None or self._arena_off + nbytes > arena.numel():
-            # grow: finish what the old arena holds first (warm-up steps size it
-            # before any graph capture)
-            pending = self._defer
-            if pending:
-                self._defer = pending
-                self.defer_flush()
-                self._defer = []
-            size = max(2 * (arena.numel() if arena is not None else 0), 64 << 20,
-                       2 * nbytes)
+        if arena is None or arena.numel() < need:
+            # grown during warm-up, before any graph capture; a replaced arena
+            # stays alive (see __init__)
             if arena is not None:
-                self._retired.append(arena)     # see __init__: never freed
-            self._arena = torch.empty(size, dtype=torch.uint8, device=self.device)
-            self._arena_off = 0
-        off = self._arena_off
-        self._arena_off += nbytes
-        return self._arena.data_ptr() + off, nbytes
+                self._retired.append(arena)
+            self._arena = arena = torch.empty(max(need, 64 << 20), dtype=torch.uint8,
+                                              device=self.device)
+        _call("pfsgnn_wgrad_multi", arr, len(jobs), arena.data_ptr(), arena.numel(), _stream())
 
-    def _wgrad_deferred(self, dY, arr, nseg, N, act_in, dW, db, dbscale):
-        M = dY.shape[0]
-        K = sum(arr[i].rows for i in range(nseg))
-        part, nbytes = self._arena_take(lib().pfsgnn_wgrad_part_bytes(M, K, N, int(db is not None)))
-        reds = (Red * 5)()
-        nr = ctypes.c_int(0)
-        _call("pfsgnn_wgrad_cat_part", dY.data_ptr(), M, arr, nseg, N, int(act_in), dW.data_ptr(),
-              dW.shape[1], _ptr(db), float(dbscale), part, nbytes, reds, ctypes.byref(nr),
-              _stream())
-        self._defer.extend(reds[i] for i in range(nr.value))
+    def _wgrad_job(self, dY, arr, nseg, N, act_in, dW, db, dbscale, keep):
+        job = WgJob(dY.data_ptr(), dY.shape[0], arr, nseg, N, int(act_in), dW.data_ptr(),
+                    dW.shape[1], _ptr(db), float(dbscale))
+        self._jobs.append((job, (arr, dY, dW, db) + tuple(keep)))
 
     def wgrad(self, dY, X, dW, col0=0, db=None, act_in=False, dbscale=1.0):
         M, N = dY.shape
         K = X.shape[0]
         self._chk(dY, X, dW, db)
-        if getattr(self, "_defer", None) is not None:
-            self._wgrad_deferred(dY, self._segs([(X, col0, False)], N), 1, N, act_in, dW, db,
-                                 dbscale)
+        if getattr(self, "_jobs", None) is not None:
+            self._wgrad_job(dY, self._segs([(X, col0, False)], N), 1, N, act_in, dW, db, dbscale,
+                            (X,))
             return
         ws, wsb = self._wsargs(getattr(self, "_dims", None))
         _call("pfsgnn_wgrad", dY.data_ptr(), M, X.data_ptr(), K, N, int(act_in),
@@ -383,8 +381,9 @@ class HipBackend:
         M, N = dY.shape
         self._chk(dY, dW, db)
         arr = self._segs(segs, N)
-        if getattr(self, "_defer", None) is not None:
-            self._wgrad_deferred(dY, arr, len(segs), N, act_in, dW, db, dbscale)
+        if getattr(self, "_jobs", None) is not None:
+            self._wgrad_job(dY, arr, len(segs), N, act_in, dW, db, dbscale,
+                            tuple(X for X, _, _ in segs))
             return
         ws, wsb = self._wsargs(getattr(self, "_dims", None))
         _call("pfsgnn_wgrad_cat", dY.data_ptr(), M, arr, len(segs), N, int(act_in), dW.data_ptr(),

@@ -15,7 +15,8 @@ which = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 
 
 def name(s):
-    s = re.sub(r"\(.*", "", s).replace("void ", "").replace("(anonymous namespace)::", "")
+    s = s.replace("void ", "").replace("(anonymous namespace)::", "")
+    s = re.sub(r"\(.*", "", s)
     m = re.search(r"(Fill|CUDAFunctorOnSelf_add|CUDAFunctor_add|direct_copy|MulFunctor|reduce_kernel)", s)
     if s.startswith("at::native") and m:
         s = "torch_" + m.group(1)
