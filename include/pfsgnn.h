@@ -164,6 +164,16 @@ typedef struct {
   float dbscale;
 } pfsgnn_wgrad_job;
 size_t pfsgnn_wgrad_multi_bytes(const pfsgnn_wgrad_job* jobs, int n);
+/* Deferred weight-gradient reductions of the fused edge backward kernels
+ * (pfsgnn_target_bwd, _source_bwd, _edge_mlp_bwd): between _begin and _end
+ * their per-block weight partials go to `arena` (bump-allocated) and their
+ * reductions are queued; _end launches them all, batched.  A kernel whose
+ * partials do not fit reduces at once, as with no pass open.
+ * pfsgnn_defer_need: the arena bytes the last pass asked for (size the next
+ * one).  Results are bitwise those of immediate reductions. */
+int pfsgnn_defer_begin(void* arena, size_t bytes);
+int pfsgnn_defer_end(void* stream);
+size_t pfsgnn_defer_need(void);
 int pfsgnn_wgrad_multi(const pfsgnn_wgrad_job* jobs, int n, void* part, size_t part_bytes,
                        void* stream);
 
@@ -225,6 +235,13 @@ int pfsgnn_graph_reduce(const float* X, int C, int G, int n, int mean, float* ou
 /* the same, accumulated: out[c][g] += sum (or mean) ... (u[batch] gradients, gnn.py:100/153/191) */
 int pfsgnn_graph_reduce_add(const float* X, int C, int G, int n, int mean, float* out,
                             void* stream);
+/* GlobalModel's two node means (gnn.py:218-219) in one launch:
+ * out[c][g] = mean of X1[c][g*n1 ..], out[C + c][g] = mean of X2[c][g*n2 ..] */
+int pfsgnn_graph_mean2(const float* X1, int n1, const float* X2, int n2, int C, int G,
+                       float* out, void* stream);
+/* its backward: out1[c][g*n1 + i] += s1*src[c][g], out2[c][g*n2 + i] += s2*src[C + c][g] */
+int pfsgnn_graph_bcast_add2(float* out1, int n1, float s1, float* out2, int n2, float s2, int C,
+                            int G, const float* src, void* stream);
 /* out[c][g*n + i] += scale * src[c][g] */
 int pfsgnn_graph_bcast_add(float* out, int C, int G, int n, const float* src, float scale,
                            void* stream);
@@ -328,6 +345,15 @@ int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe, const flo
                         const float* xsh, const float* Ps, const float* Pt, const float* W1,
                         const float* W2, const float* b2, float* y, float* mu, float* var,
                         void* ws, size_t ws_bytes, void* stream);
+/* the same + the double BatchNorm's finalize (pfsgnn_bn2_finalize's outputs
+ * sc, sh, inv1, inv2 and running-stat updates) in the moments pass: the
+ * EdgeModel training forward in one call (gnn.py:99-101) */
+int pfsgnn_edge_mlp_fwd_bn(int G, int NF, int NC, int F, const float* xe, const float* xsc,
+                           const float* xsh, const float* Ps, const float* Pt, const float* W1,
+                           const float* W2, const float* b2, float* y, float* mu, float* var,
+                           const float* gamma, const float* beta, float* rm, float* rv,
+                           float momentum, float eps, float* sc, float* sh, float* inv1,
+                           float* inv2, void* ws, size_t ws_bytes, void* stream);
 /* SModel per-edge message + per-fiber centred moments (gnn.py:136-151).
  * mom [4][2F][NS]; hs [8F][NS] receives (mean, std, skew, kurt). */
 int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,

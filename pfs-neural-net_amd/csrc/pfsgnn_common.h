@@ -51,6 +51,34 @@ class Timer {
 __device__ __forceinline__ float lrelu(float x) { return x > 0.f ? x : PF_LEAKY * x; }
 __device__ __forceinline__ float dlrelu(float z) { return z > 0.f ? 1.f : PF_LEAKY; }
 
+// ------------------------------------------------------------ double BatchNorm
+// EdgeModel's BatchNorm applied twice (gnn.py:101) from the batch moments
+// (m, v) of channel c: xe_new = sc*y + sh, and both running-stat updates.
+__device__ __forceinline__ void bn2_coef(const float* gamma, const float* beta, float* rm,
+                                         float* rv, int c, long long n, float momentum, float eps,
+                                         float m, float v, float* sc, float* sh, float* inv1o,
+                                         float* inv2o) {
+  const float g = gamma[c], bt = beta[c];
+  const float inv1 = 1.0f / sqrtf(v + eps);
+  const float rho = v * inv1 * inv1;
+  const float v2 = g * g * rho;
+  const float inv2 = 1.0f / sqrtf(v2 + eps);
+  const float s = g * g * inv1 * inv2;
+  sc[c] = s;
+  sh[c] = bt - m * s;
+  inv1o[c] = inv1;
+  inv2o[c] = inv2;
+  if (rm) {
+    const float f = n > 1 ? (float)((double)n / (double)(n - 1)) : 1.f;
+    float a = (1.f - momentum) * rm[c] + momentum * m;
+    float b = (1.f - momentum) * rv[c] + momentum * (v * f);
+    a = (1.f - momentum) * a + momentum * bt;
+    b = (1.f - momentum) * b + momentum * (v2 * f);
+    rm[c] = a;
+    rv[c] = b;
+  }
+}
+
 // ------------------------------------------------------------ edge geometry
 // Canonical edge order is class-major, e = (g*NC + c)*NF + f.  A block of 4
 // waves owns 64 consecutive fibers (lane = fiber) of one graph -- fiber group
@@ -232,6 +260,14 @@ struct RedDesc {
 };
 #define PF_MAX_RED 32
 void launch_reduce_multi(const RedDesc* d, int n, hipStream_t st);
+// Deferred weight-gradient reductions (pfsgnn_defer_begin / _end): while a
+// pass is open, the edge backward kernels put their weight partials in the
+// caller's arena and queue the reductions; nullptr when closed or full (the
+// caller then reduces at once, as outside a pass).
+namespace pf {
+float* defer_take(size_t nfloats);
+void defer_push(const RedDesc* d, int n);
+}  // namespace pf
 void launch_reduce_rows(const float* part, int nb, size_t plen, int ldp, int rows, int cols,
                         float* out, int ldo, int add, float scale, hipStream_t st);
 // Column partials [G][NFG][NC][C] -> channel-major node tensor out[C][G*NC].

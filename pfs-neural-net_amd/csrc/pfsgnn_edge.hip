@@ -295,10 +295,21 @@ __device__ __forceinline__ void chan_merge(double& C0, double& M0, double& Q0, d
 
 // merge per-block Welford partials -> mu, biased var (one 256-thread block per
 // channel: each thread merges a strided subset, then a fixed-order tree)
+// With `bn` (EdgeModel training forward): also the double BatchNorm's affine
+// and running statistics of channel k, as pfsgnn_bn2_finalize computes them.
+struct Bn2Args {
+  const float* gamma;
+  const float* beta;
+  float* rm;
+  float* rv;
+  float momentum, eps;
+  float *sc, *sh, *inv1, *inv2;
+};
+
 __global__ __launch_bounds__(256) void k_moments_finalize(const float* __restrict__ part, int nb,
                                                           int F, long long n,
                                                           float* __restrict__ mu,
-                                                          float* __restrict__ var) {
+                                                          float* __restrict__ var, Bn2Args bn) {
   const int k = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   double cnt = 0, mean = 0, m2 = 0;
   for (int b = t; b < nb; b += 256) {
@@ -320,8 +331,11 @@ __global__ __launch_bounds__(256) void k_moments_finalize(const float* __restric
   if (t == 0) {
     double C0 = sh[0][0], M0 = sh[0][1], Q0 = sh[0][2];
     for (int w = 1; w < 4; ++w) chan_merge(C0, M0, Q0, sh[w][0], sh[w][1], sh[w][2]);
-    mu[k] = (float)M0;
-    var[k] = (float)(Q0 / (double)n);
+    const float m = (float)M0, v = (float)(Q0 / (double)n);
+    mu[k] = m;
+    var[k] = v;
+    if (bn.gamma) bn2_coef(bn.gamma, bn.beta, bn.rm, bn.rv, k, n, bn.momentum, bn.eps, m, v,
+                           bn.sc, bn.sh, bn.inv1, bn.inv2);
   }
 }
 
@@ -1192,11 +1206,10 @@ extern "C" size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F) {
   return (std::max(std::max(edge, node), lay) + 64 * 16) * sizeof(float) + 16 * 256;
 }
 
-extern "C" int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe,
-                                   const float* xsc, const float* xsh, const float* Ps,
-                                   const float* Pt, const float* W1, const float* W2,
-                                   const float* b2, float* y, float* mu, float* var, void* ws,
-                                   size_t ws_bytes, void* stream) {
+static int edge_mlp_fwd_impl(int G, int NF, int NC, int F, const float* xe, const float* xsc,
+                             const float* xsh, const float* Ps, const float* Pt, const float* W1,
+                             const float* W2, const float* b2, float* y, float* mu, float* var,
+                             Bn2Args bn, void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_edge_mlp_fwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(xe && Ps && Pt && W1 && W2 && b2 && y && mu && var, "pfsgnn_edge_mlp_fwd", "null");
   const EdgeGeo geo = geo_for(G, NF, NC);
@@ -1209,7 +1222,7 @@ extern "C" int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe
     if (int rc = pfm::edge_mlp_fwd(geo, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part, mf_prec(), mf_bfy(), st)) return rc;
     tm_.end(); }
     hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(256), 0, st, part, geo.nblocks, F, geo.E,
-                       mu, var);
+                       mu, var, bn);
     return pf::check_launch("pfsgnn_edge_mlp_fwd");
   }
   const float* PtT = class_rows(Pt, 4 * F, geo, w, st);
@@ -1220,8 +1233,32 @@ extern "C" int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe
                                    xe, xsc, xsh, Ps, PtT, W1, W2T, b2, y, part));
   tm_.end(); }
   hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(256), 0, st, part, geo.nblocks, F, geo.E,
-                     mu, var);
+                     mu, var, bn);
   return pf::check_launch("pfsgnn_edge_mlp_fwd");
+}
+
+extern "C" int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe,
+                                   const float* xsc, const float* xsh, const float* Ps,
+                                   const float* Pt, const float* W1, const float* W2,
+                                   const float* b2, float* y, float* mu, float* var, void* ws,
+                                   size_t ws_bytes, void* stream) {
+  return edge_mlp_fwd_impl(G, NF, NC, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, mu, var, Bn2Args{},
+                           ws, ws_bytes, stream);
+}
+
+extern "C" int pfsgnn_edge_mlp_fwd_bn(int G, int NF, int NC, int F, const float* xe,
+                                      const float* xsc, const float* xsh, const float* Ps,
+                                      const float* Pt, const float* W1, const float* W2,
+                                      const float* b2, float* y, float* mu, float* var,
+                                      const float* gamma, const float* beta, float* rm, float* rv,
+                                      float momentum, float eps, float* sc, float* sh,
+                                      float* inv1, float* inv2, void* ws, size_t ws_bytes,
+                                      void* stream) {
+  PF_REQUIRE(gamma && beta && sc && sh && inv1 && inv2 && (!rm == !rv),
+             "pfsgnn_edge_mlp_fwd_bn", "null");
+  return edge_mlp_fwd_impl(G, NF, NC, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, mu, var,
+                           Bn2Args{gamma, beta, rm, rv, momentum, eps, sc, sh, inv1, inv2}, ws,
+                           ws_bytes, stream);
 }
 
 extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
@@ -1287,7 +1324,9 @@ extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, c
   const int C = 2 * F;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
   hipStream_t st = as_stream(stream);
-  float* part = w.take((size_t)geo.nblocks * C * F);
+  float* part = pf::defer_take((size_t)geo.nblocks * C * F);
+  const bool defer = part != nullptr;
+  if (!defer) part = w.take((size_t)geo.nblocks * C * F);
   float* gz = fiber_dst(geo, C, GzT, w);
   const float* ghT = use_mfma() ? g_hsum
                                 : class_rows(g_hsum, C, geo, w, st);
@@ -1301,7 +1340,9 @@ extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, c
   }
   tm_.end(); }
   fiber_finish(geo, C, gz, GzT, st);
-  launch_reduce_rows(part, geo.nblocks, (size_t)C * F, F, C, F, dWt1 + F, C, 1, 1.f, st);
+  const RedDesc rd{part, geo.nblocks, (size_t)C * F, F, C, F, dWt1 + F, C, 1, 1.f};
+  if (defer) pf::defer_push(&rd, 1);
+  else launch_reduce_multi(&rd, 1, st);
   return pf::check_launch("pfsgnn_target_bwd");
 }
 
@@ -1323,8 +1364,10 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
   const int C = 2 * F;
   const size_t nb = geo.nblocks;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
-  float* pW2 = w.take(nb * C * (C + 1));
-  float* pW1 = w.take(nb * C * F);
+  float* pW2 = pf::defer_take(nb * C * (C + 1) + nb * C * F);
+  const bool defer = pW2 != nullptr;
+  if (!defer) pW2 = w.take(nb * C * (C + 1) + nb * C * F);
+  float* pW1 = pW2 ? pW2 + nb * C * (C + 1) : nullptr;
   float* pCol = w.take((size_t)G * geo.NFG * NC * C);
   float* pBN = w.take(nb * 2 * F);
   hipStream_t st = as_stream(stream);
@@ -1345,12 +1388,20 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
   }
   tm_.end(); }
   {
-    RedDesc rd[5] = {{pW2, (int)nb, (size_t)C * (C + 1), C + 1, C, C, dWs2, C, 1, 1.f},
+    RedDesc rd[5] = {{pBN, (int)nb, (size_t)2 * F, F, 1, F, Sg, F, 0, 1.f},
+                     {pBN + F, (int)nb, (size_t)2 * F, F, 1, F, Sgx, F, 0, 1.f},
+                     {pW2, (int)nb, (size_t)C * (C + 1), C + 1, C, C, dWs2, C, 1, 1.f},
                      {pW2 + C, (int)nb, (size_t)C * (C + 1), C + 1, C, 1, dbs2, 1, 1, 1.f},
-                     {pW1, (int)nb, (size_t)C * F, F, C, F, dWs1 + F, C, 1, 1.f},
-                     {pBN, (int)nb, (size_t)2 * F, F, 1, F, Sg, F, 0, 1.f},
-                     {pBN + F, (int)nb, (size_t)2 * F, F, 1, F, Sgx, F, 0, 1.f}};
-    launch_reduce_multi(rd, mu1 ? 5 : 3, st);
+                     {pW1, (int)nb, (size_t)C * F, F, C, F, dWs1 + F, C, 1, 1.f}};
+    // the BatchNorm sums are read at once (bn2_bwd_coef); the weight
+    // gradients only by the optimizer
+    const RedDesc* now = mu1 ? rd : rd + 2;
+    int nnow = mu1 ? 5 : 3;
+    if (defer) {
+      pf::defer_push(rd + 2, 3);
+      nnow -= 3;
+    }
+    if (nnow) launch_reduce_multi(now, nnow, st);
   }
   launch_reduce_columns(pCol, G, geo.NFG, NC, C, GzS, st);
   return pf::check_launch("pfsgnn_source_bwd");
@@ -1394,8 +1445,10 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
   const int H = 4 * F;
   const size_t nb = geo.nblocks;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
-  float* pW2 = w.take(nb * F * (H + 1));
-  float* pW1 = w.take(nb * H * F);
+  float* pW2 = pf::defer_take(nb * F * (H + 1) + nb * H * F);
+  const bool defer = pW2 != nullptr;
+  if (!defer) pW2 = w.take(nb * F * (H + 1) + nb * H * F);
+  float* pW1 = pW2 ? pW2 + nb * F * (H + 1) : nullptr;
   float* pCol = w.take((size_t)G * geo.NFG * NC * H);
   float* gs = fiber_dst(geo, H, GzEs, w);
   hipStream_t st = as_stream(stream);
@@ -1421,7 +1474,8 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
     RedDesc rd[3] = {{pW2, (int)nb, (size_t)F * (H + 1), H + 1, F, H, dW2, H, 1, 1.f},
                      {pW2 + H, (int)nb, (size_t)F * (H + 1), H + 1, F, 1, db2, 1, 1, 1.f},
                      {pW1, (int)nb, (size_t)H * F, F, H, F, dW1 + 2 * F, H, 1, 1.f}};
-    launch_reduce_multi(rd, 3, st);
+    if (defer) pf::defer_push(rd, 3);
+    else launch_reduce_multi(rd, 3, st);
   }
   launch_reduce_columns(pCol, G, geo.NFG, NC, H, GzEt, st);
   return pf::check_launch("pfsgnn_edge_mlp_bwd");

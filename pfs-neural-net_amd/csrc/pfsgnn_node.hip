@@ -965,6 +965,58 @@ extern "C" int pfsgnn_wgrad_multi(const pfsgnn_wgrad_job* jobs, int n, void* par
   return pfsgnn_reduce_batch(rr.data(), (int)rr.size(), stream);
 }
 
+// ------------------------------------------------- deferred reductions
+namespace pf {
+namespace {
+struct DeferCtx {
+  char* base = nullptr;
+  size_t cap = 0, off = 0, need = 0;
+  bool on = false;
+  std::vector<RedDesc> q;
+};
+DeferCtx g_defer;
+}  // namespace
+
+float* defer_take(size_t nfloats) {
+  DeferCtx& D = g_defer;
+  if (!D.on) return nullptr;
+  const size_t b = align256(nfloats * sizeof(float));
+  D.need += b;
+  if (D.off + b > D.cap) return nullptr;
+  float* r = reinterpret_cast<float*>(D.base + D.off);
+  D.off += b;
+  return r;
+}
+
+void defer_push(const RedDesc* d, int n) { g_defer.q.insert(g_defer.q.end(), d, d + n); }
+}  // namespace pf
+
+extern "C" int pfsgnn_defer_begin(void* arena, size_t bytes) {
+  pf::DeferCtx& D = pf::g_defer;
+  PF_REQUIRE(!D.on, "pfsgnn_defer_begin", "a deferred pass is already open");
+  D.base = static_cast<char*>(arena);
+  D.cap = arena ? bytes : 0;
+  D.off = D.need = 0;
+  D.q.clear();
+  D.on = true;
+  return 0;
+}
+
+extern "C" size_t pfsgnn_defer_need(void) { return pf::g_defer.need; }
+
+extern "C" int pfsgnn_defer_end(void* stream) {
+  pf::DeferCtx& D = pf::g_defer;
+  PF_REQUIRE(D.on, "pfsgnn_defer_end", "no deferred pass is open");
+  D.on = false;
+  std::vector<pfsgnn_red> rr(D.q.size());
+  for (size_t i = 0; i < D.q.size(); ++i) {
+    const RedDesc& r = D.q[i];
+    rr[i] = {r.part, r.nb, r.plen, r.ldp, r.rows, r.cols, r.out, r.ldo, r.add, r.scale};
+  }
+  D.q.clear();
+  return pfsgnn_reduce_batch(rr.data(), (int)rr.size(), stream);
+}
+
 // Output rectangles of two reductions intersect?  Exact when both write rows
 // of the same row pitch without wrapping; conservative (true) otherwise.
 static bool red_overlap(const RedDesc& a, const RedDesc& b) {
@@ -1226,6 +1278,56 @@ extern "C" int pfsgnn_graph_reduce_add(const float* X, int C, int G, int n, int 
   return pf::check_launch("pfsgnn_graph_reduce_add");
 }
 
+// Two per-graph means in one launch (GlobalModel's x_s.mean / x_t.mean,
+// gnn.py:218-219): out rows [0, C) from X1 (n1 nodes per graph), [C, 2C) from X2.
+__global__ void k_graph_mean2(const float* __restrict__ X1, int n1, const float* __restrict__ X2,
+                              int n2, int C, int G, float* __restrict__ out) {
+  const int cg = blockIdx.x, which = blockIdx.y;
+  const int c = cg / G, g = cg - c * G;
+  const int n = which ? n2 : n1;
+  const float* p = (which ? X2 : X1) + (size_t)c * G * n + (size_t)g * n;
+  float v[1] = {0.f};
+  for (int i = threadIdx.x; i < n; i += 256) v[0] += p[i];
+  __shared__ float scratch[4];
+  block_sum<1>(v, scratch);
+  if (threadIdx.x == 0) out[(size_t)(which * C + c) * G + g] = v[0] / (float)n;
+}
+
+extern "C" int pfsgnn_graph_mean2(const float* X1, int n1, const float* X2, int n2, int C, int G,
+                                  float* out, void* stream) {
+  PF_REQUIRE(X1 && X2 && out && C > 0 && G > 0 && n1 > 0 && n2 > 0, "pfsgnn_graph_mean2",
+             "bad arguments");
+  hipLaunchKernelGGL(k_graph_mean2, dim3(C * G, 2), dim3(256), 0, as_stream(stream), X1, n1, X2,
+                     n2, C, G, out);
+  return pf::check_launch("pfsgnn_graph_mean2");
+}
+
+// Its backward in one launch: out1[c][g*n1 + i] += s1 src[c][g], out2 likewise
+// with src rows [C, 2C).
+__global__ void k_graph_bcast_add2(float* __restrict__ out1, int n1, float s1,
+                                   float* __restrict__ out2, int n2, float s2, int C, int G,
+                                   const float* __restrict__ src) {
+  const size_t t1 = (size_t)C * G * n1, t2 = (size_t)C * G * n2;
+  size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < t1) {
+    const size_t c = idx / ((size_t)G * n1), g = (idx - c * G * n1) / n1;
+    out1[idx] += s1 * src[c * G + g];
+  } else if ((idx -= t1) < t2) {
+    const size_t c = idx / ((size_t)G * n2), g = (idx - c * G * n2) / n2;
+    out2[idx] += s2 * src[(C + c) * G + g];
+  }
+}
+
+extern "C" int pfsgnn_graph_bcast_add2(float* out1, int n1, float s1, float* out2, int n2,
+                                       float s2, int C, int G, const float* src, void* stream) {
+  PF_REQUIRE(out1 && out2 && src && C > 0 && G > 0 && n1 > 0 && n2 > 0,
+             "pfsgnn_graph_bcast_add2", "bad arguments");
+  const size_t tot = (size_t)C * G * ((size_t)n1 + n2);
+  hipLaunchKernelGGL(k_graph_bcast_add2, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), out1, n1, s1, out2, n2, s2, C, G, src);
+  return pf::check_launch("pfsgnn_graph_bcast_add2");
+}
+
 __global__ void k_graph_bcast_add(float* __restrict__ out, int C, int G, int n,
                                   const float* __restrict__ src, float scale) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1334,25 +1436,7 @@ __global__ void k_bn2_finalize(const float* __restrict__ mu1, const float* __res
                                float* __restrict__ inv2o) {
   const int c = threadIdx.x;
   if (c >= C) return;
-  const float g = gamma[c], bt = beta[c], m = mu1[c], v = var1[c];
-  const float inv1 = 1.0f / sqrtf(v + eps);
-  const float rho = v * inv1 * inv1;
-  const float v2 = g * g * rho;
-  const float inv2 = 1.0f / sqrtf(v2 + eps);
-  const float s = g * g * inv1 * inv2;
-  sc[c] = s;
-  sh[c] = bt - m * s;
-  inv1o[c] = inv1;
-  inv2o[c] = inv2;
-  if (rm) {
-    const float f = n > 1 ? (float)((double)n / (double)(n - 1)) : 1.f;
-    float a = (1.f - momentum) * rm[c] + momentum * m;
-    float b = (1.f - momentum) * rv[c] + momentum * (v * f);
-    a = (1.f - momentum) * a + momentum * bt;
-    b = (1.f - momentum) * b + momentum * (v2 * f);
-    rm[c] = a;
-    rv[c] = b;
-  }
+  bn2_coef(gamma, beta, rm, rv, c, n, momentum, eps, mu1[c], var1[c], sc, sh, inv1o, inv2o);
 }
 
 extern "C" int pfsgnn_bn2_finalize(const float* mu1, const float* var1, const float* gamma,

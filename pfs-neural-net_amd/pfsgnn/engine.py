@@ -206,6 +206,15 @@ class Engine:
         W2, b2 = P[pre + "2.weight"], P[pre + "2.bias"]
         Ps = be.lin(W1, 0, F, xs)
         Pt = be.lin_cat(W1, [(xt, F, False), (u, 3 * F, True)], d.NT, b=b1)
+        if self.normed and self.training:
+            # the double BatchNorm's finalize rides in the moments pass
+            key = pre + "norm."
+            y, mu1, var1, sc, sh, inv1 = be.edge_mlp_fwd_bn(
+                d, xe3[0], xe3[1], xe3[2], Ps, Pt, W1, W2, b2,
+                (P[key + "weight"], P[key + "bias"], BN.get(key + "running_mean"),
+                 BN.get(key + "running_var"), self.bn_momentum, self.bn_eps))
+            return dict(xs=xs, xt=xt, xe3=xe3, u=u, Ps=Ps, Pt=Pt, y=y, mu1=mu1, var1=var1,
+                        sc=sc, sh=sh, inv1=inv1)
         y, mu1, var1 = be.edge_mlp_fwd(d, xe3[0], xe3[1], xe3[2], Ps, Pt, W1, W2, b2)
         if self.normed and not self.training:
             # eval: both BatchNorm applications (gnn.py:101) on running statistics
@@ -213,11 +222,6 @@ class Engine:
             sc, sh = be.bn_eval_coef(P[key + "weight"], P[key + "bias"], BN[key + "running_mean"],
                                      BN[key + "running_var"], self.bn_eps, 2)
             inv1 = None
-        elif self.normed:
-            key = pre + "norm."
-            sc, sh, inv1, _ = be.bn2_finalize(mu1, var1, P[key + "weight"], P[key + "bias"],
-                                              BN.get(key + "running_mean"), BN.get(key + "running_var"),
-                                              d.E, self.bn_momentum, self.bn_eps)
         else:
             sc = sh = inv1 = None
         return dict(xs=xs, xt=xt, xe3=xe3, u=u, Ps=Ps, Pt=Pt, y=y, mu1=mu1, var1=var1,
@@ -336,8 +340,7 @@ class Engine:
     def global_fwd(self, P, d, pre, xs, xt, u):
         be, F, G = self.be, self.F, d.G
         # [u, mean x_s, mean x_t] (gnn.py:218-220), in place
-        hU = [(u, 0, False), (be.graph_reduce(xs, G, mean=True), F, False),
-              (be.graph_reduce(xt, G, mean=True), 2 * F, False)]
+        hU = [(u, 0, False), (be.graph_mean2(xs, xt, G), F, False)]
         v, sU = self.mlp_fwd(P, pre, hU)
         if self.normed:
             u_new, rms = be.rms2_fwd(v, P[pre + "norm.weight"], self._rms_eps(v))
@@ -352,11 +355,9 @@ class Engine:
                               self._rms_eps(st["v"]), Gr[pre + "norm.weight"])
         else:
             g_v = g_u_new
-        g_ms, g_mt = be.empty(F, d.G), be.empty(F, d.G)
-        self.mlp_bwd(P, Gr, pre, g_v, st["sU"], outs=[(g_u, F, True), (g_ms, F, False),
-                                                      (g_mt, F, False)])
-        be.graph_bcast_add(g_xs, g_ms, 1.0 / d.NF)
-        be.graph_bcast_add(g_xt, g_mt, 1.0 / d.NC)
+        g_m = be.empty(2 * F, d.G)          # d loss / d [mean x_s; mean x_t]
+        self.mlp_bwd(P, Gr, pre, g_v, st["sU"], outs=[(g_u, F, True), (g_m, 2 * F, False)])
+        be.graph_bcast_add2(g_xs, 1.0 / d.NF, g_xt, 1.0 / d.NC, g_m)
 
     # ============================================================ GNN path
     def forward(self, P, BN, d, xs_in, xt_in, xe_in, u_in, training=True):

@@ -681,7 +681,7 @@ class _GNNFn(torch.autograd.Function):
         xs, xt, xe3, u = ectx["out"]
         ctx.pf = (model, d, lay, ectx)
         model._pf_last = (xe3, ectx)
-        token = xs.new_zeros(())
+        token = xs.new_empty(())            # connectivity only: its value is never read
         return xs.t(), xt.t(), token, u.t()
 
     @staticmethod
@@ -714,7 +714,7 @@ class _EdgesOutFn(torch.autograd.Function):
             gc = gc.contiguous()
             prev = ectx.get("g_xe_canonical")
             ectx["g_xe_canonical"] = gc if prev is None else prev + gc
-        return g.new_zeros(()), None, None, None, None
+        return None, None, None, None, None
 
 
 class _GradRecorder(dict):

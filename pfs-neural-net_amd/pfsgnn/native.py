@@ -91,6 +91,9 @@ _SIGS = {
     "pfsgnn_reduce_batch": ([REDP, I, P], I),
     "pfsgnn_wgrad_multi_bytes": ([WGJP, I], SZ),
     "pfsgnn_wgrad_multi": ([WGJP, I, P, SZ, P], I),
+    "pfsgnn_defer_begin": ([P, SZ], I),
+    "pfsgnn_defer_end": ([P], I),
+    "pfsgnn_defer_need": ([], SZ),
     "pfsgnn_bn_fwd": ([P, I, I, P, P, P, P, FL, FL, P, P, P, P, SZ, P], I),
     "pfsgnn_bn_bwd": ([P, P, P, P, P, FL, I, I, P, P, P, P, SZ, P], I),
     "pfsgnn_mlp_ws_bytes": ([I], SZ),
@@ -102,6 +105,8 @@ _SIGS = {
     "pfsgnn_graph_reduce": ([P, I, I, I, I, P, P], I),
     "pfsgnn_graph_reduce_add": ([P, I, I, I, I, P, P], I),
     "pfsgnn_graph_bcast_add": ([P, I, I, I, P, FL, P], I),
+    "pfsgnn_graph_mean2": ([P, I, P, I, I, I, P, P], I),
+    "pfsgnn_graph_bcast_add2": ([P, I, FL, P, I, FL, I, I, P, P], I),
     "pfsgnn_rms2_fwd": ([P, I, I, P, FL, P, P, P, P, P], I),
     "pfsgnn_rms2_bwd": ([P, P, P, P, P, P, I, I, FL, P, P, P, SZ, P], I),
     "pfsgnn_bn2_finalize": ([P, P, P, P, P, P, I, LL, FL, FL, P, P, P, P, P], I),
@@ -121,6 +126,7 @@ _SIGS = {
     "pfsgnn_rows_bn_sums": ([P, P, I, LL, P, P, P, P, P, SZ, P], I),
     "pfsgnn_rows_axpby": ([P, P, I, LL, P, P, P, P, P], I),
     "pfsgnn_edge_mlp_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_edge_mlp_fwd_bn": ([I, I, I, I] + [P] * 15 + [FL, FL, P, P, P, P, P, SZ, P], I),
     "pfsgnn_source_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_target_fwd": ([I, I, I, I, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_target_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
@@ -311,11 +317,27 @@ class HipBackend:
     # The engine defers over a backward pass: its weight gradients are read
     # only by the optimizer, and the jobs' inputs are activations and
     # gradients that no later op of the pass writes (engine.Engine.backward).
+    # The fused edge backward kernels' own weight reductions are deferred the
+    # same way inside the library (pfsgnn_defer_begin / _end), their partials
+    # in a second arena sized by the previous pass (warm-up sizes it before
+    # any graph capture; a pass that does not fit reduces at once).
     def defer_begin(self):
         self._jobs = []
+        ea = getattr(self, "_earena", None)
+        _call("pfsgnn_defer_begin", None if ea is None else ea.data_ptr(),
+              0 if ea is None else ea.numel())
 
     def defer_flush(self):
         jobs, self._jobs = getattr(self, "_jobs", None), None
+        if jobs is None:
+            return
+        _call("pfsgnn_defer_end", _stream())
+        need = lib().pfsgnn_defer_need()
+        ea = getattr(self, "_earena", None)
+        if need and (ea is None or ea.numel() < need):
+            if ea is not None:
+                self._retired.append(ea)
+            self._earena = torch.empty(need + (1 << 20), dtype=torch.uint8, device=self.device)
         if not jobs:
             return
         arr = (WgJob * len(jobs))()
@@ -489,6 +511,22 @@ class HipBackend:
               float(scale), _stream())
         return out
 
+    def graph_mean2(self, X1, X2, G):
+        """[2C, G]: per-graph means of X1 (rows 0..C) and X2 (rows C..2C)."""
+        C = X1.shape[0]
+        self._chk(X1, X2)
+        out = self.empty(2 * C, G)
+        _call("pfsgnn_graph_mean2", X1.data_ptr(), X1.shape[1] // G, X2.data_ptr(),
+              X2.shape[1] // G, C, G, out.data_ptr(), _stream())
+        return out
+
+    def graph_bcast_add2(self, out1, s1, out2, s2, src):
+        C, G = src.shape[0] // 2, src.shape[1]
+        src = src.contiguous()
+        self._chk(out1, out2, src)
+        _call("pfsgnn_graph_bcast_add2", out1.data_ptr(), out1.shape[1] // G, float(s1),
+              out2.data_ptr(), out2.shape[1] // G, float(s2), C, G, src.data_ptr(), _stream())
+
     def rms2_fwd(self, X, w, eps):
         C, G = X.shape
         Y, y1, r1, r2 = self.empty(C, G), self.empty(C, G), self.empty(G), self.empty(G)
@@ -573,6 +611,27 @@ class HipBackend:
               Ps.data_ptr(), Pt.data_ptr(), W1.data_ptr(), W2.data_ptr(), b2.data_ptr(),
               y.data_ptr(), mu.data_ptr(), var.data_ptr(), ws, wsb, _stream())
         return y, mu, var
+
+    def edge_mlp_fwd_bn(self, d, xe, xsc, xsh, Ps, Pt, W1, W2, b2, bn):
+        """edge_mlp_fwd + bn2_finalize in one call; ``bn`` = (gamma, beta,
+        running_mean, running_var, momentum, eps).  -> y, mu1, var1, sc, sh, inv1."""
+        gamma, beta, rm, rv, momentum, eps = bn
+        if d.sp is not None:
+            y, mu, var = self._sp.edge_mlp_fwd(d, xe, xsc, xsh, Ps, Pt, W1, W2, b2)
+            sc, sh, inv1, _ = self.bn2_finalize(mu, var, gamma, beta, rm, rv, d.E, momentum, eps)
+            return y, mu, var, sc, sh, inv1
+        self._set_dims(d)
+        F = d.F
+        y, mu, var = self.empty(F, d.E), self.empty(F), self.empty(F)
+        sc, sh, inv1, inv2 = self.empty(F), self.empty(F), self.empty(F), self.empty(F)
+        self._chk(xe, Ps, Pt, W1, W2, b2, gamma, beta, rm, rv)
+        ws, wsb = self._wsargs(d)
+        _call("pfsgnn_edge_mlp_fwd_bn", d.G, d.NF, d.NC, F, xe.data_ptr(), _ptr(xsc), _ptr(xsh),
+              Ps.data_ptr(), Pt.data_ptr(), W1.data_ptr(), W2.data_ptr(), b2.data_ptr(),
+              y.data_ptr(), mu.data_ptr(), var.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+              _ptr(rm), _ptr(rv), float(momentum), float(eps), sc.data_ptr(), sh.data_ptr(),
+              inv1.data_ptr(), inv2.data_ptr(), ws, wsb, _stream())
+        return y, mu, var, sc, sh, inv1
 
     def source_fwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, hs_out):
         if d.sp is not None:

@@ -48,6 +48,7 @@ class _LossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, token, anchor, model, d, ectx, xe3, ci, sharpness, seed, pclass, pfiber,
                 want_time, noiselevel):
+        ctx.set_materialize_grads(False)   # the diagnostics get no gradient: no zero fills
         eng = model._engine()
         P = model._flat_params()
         loss, diag, lctx = eng.loss_forward(P, d, xe3, ci, sharpness, seed, pclass=pclass,
@@ -65,15 +66,17 @@ class _LossFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_loss, *unused):
         model, d, ectx, lctx = ctx.pf
+        if g_loss is None:
+            return (None,) * 13
         eng = model._engine()
         P, Gr = model._flat_params(), model._recording_grads()
         gc = eng.loss_backward(P, Gr, lctx, gscale=g_loss)
         model._mark_live(Gr.used)
         # hand the canonical [F, E] gradient straight to the GNN's backward
-        # (gnn._GNNFn.backward); the edge-state token gets a zero
+        # (gnn._GNNFn.backward); the edge-state token gets none
         prev = ectx.get("g_xe_canonical")
         ectx["g_xe_canonical"] = gc if prev is None else prev + gc
-        return (gc.new_zeros(()),) + (None,) * 12
+        return (None,) * 13
 
 
 def _class_info_cm(class_info, d):
@@ -105,7 +108,7 @@ def loss_function(graph, class_info, pclass=0.1, pfiber=1.0, sharpness=0.5, fina
         if torch.is_grad_enabled():
             raise NotImplementedError("loss_function on an eval-mode GNN.forward runs under "
                                       "torch.no_grad() only (train.py:108 trains in train mode)")
-        token = xe3[0].new_zeros(())
+        token = xe3[0].new_empty(())
     if gnn is not None and gnn is not model:
         raise ValueError("graph was produced by a different GNN than `gnn`")
     if not lay.fiber_major:

@@ -208,6 +208,14 @@ class EmuBackend:
         out += (src * scale).repeat_interleave(N // G, dim=1)
         return out
 
+    def graph_mean2(self, X1, X2, G):
+        return torch.cat([self.graph_reduce(X1, G, mean=True), self.graph_reduce(X2, G, mean=True)])
+
+    def graph_bcast_add2(self, out1, s1, out2, s2, src):
+        C = src.shape[0] // 2
+        self.graph_bcast_add(out1, src[:C], s1)
+        self.graph_bcast_add(out2, src[C:], s2)
+
     def rms2_fwd(self, X, w, eps):
         def one(x):
             r = torch.rsqrt((x * x).mean(0, keepdim=True) + eps)
@@ -303,6 +311,12 @@ class EmuBackend:
         mu = y.mean(1)
         var = ((y - mu[:, None]) ** 2).mean(1)
         return y, mu, var
+
+    def edge_mlp_fwd_bn(self, d, xe, xsc, xsh, Ps, Pt, W1, W2, b2, bn):
+        gamma, beta, rm, rv, momentum, eps = bn
+        y, mu, var = self.edge_mlp_fwd(d, xe, xsc, xsh, Ps, Pt, W1, W2, b2)
+        sc, sh, inv1, _ = self.bn2_finalize(mu, var, gamma, beta, rm, rv, d.E, momentum, eps)
+        return y, mu, var, sc, sh, inv1
 
     def source_fwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, hs_out):
         """Per-fiber centred moments of the SModel message (gnn.py:136-151).
