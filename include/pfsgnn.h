@@ -222,6 +222,30 @@ int pfsgnn_mlp_bwd(const float* dY, int N, const float* Yp, const float* mu, con
                    const float* W1, int ldw1, int H, int K, const float* W2, int O, float* dYp,
                    float* dZ, const pfsgnn_oseg* outs, int nout, void* ws, size_t ws_bytes,
                    void* stream);
+/* Several independent small products in one launch: each job is a
+ * pfsgnn_lin_cat (trans 0: Y[M][N] (+)= W . act(x_segs) + bscale*b) or a
+ * pfsgnn_lin_t (trans 1: Y[M][N] (+)= W^T[M][K] . segs[0] (* lrelu'(Z)), W
+ * of K rows).  Jobs must not write the same Y.  K <= 40, M <= 64 (the
+ * per-block node parts of gnn.py:100/136/188's first Linear layers and their
+ * input gradients). */
+typedef struct {
+  const float* W;
+  int ldw;
+  int trans;
+  int M;
+  int K;
+  const pfsgnn_seg* segs;
+  int nseg;
+  int N;
+  const float* b;
+  float bscale;
+  int act_in;
+  const float* Z;
+  float* Y;
+  int add;
+} pfsgnn_gemm_job;
+int pfsgnn_gemm_multi(const pfsgnn_gemm_job* jobs, int n, void* stream);
+
 /* ---------------------------------------------------------- graph building
  * edge_index (int64 [2][E], E = G*NF*NC) of G complete bipartite graphs, fiber
  * ids g*NF + f, class ids g*NC + c.  order 0: fiber-major (train.py:94
@@ -383,6 +407,19 @@ int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, const float*
                       const float* mu1, const float* inv1, float* g_tot, float* GzS,
                       float* dWs1, float* dWs2, float* dbs2, float* Sg, float* Sgx,
                       void* ws, size_t ws_bytes, void* stream);
+/* the same with the edge BatchNorm's backward finished in the same call: in
+ * place of Sg / Sgx it writes pfsgnn_bn2_bwd_coef's alpha, gam0, gam1 and
+ * accumulates dgamma / dbeta (gamma, var1: that BatchNorm's weight and batch
+ * variance; n = E) */
+int pfsgnn_source_bwd_bn(int G, int NF, int NC, int F, const float* y, const float* sc,
+                         const float* sh, const float* Qt, const float* Ws1, const float* Ws2,
+                         const float* bs2, const float* mean, const float* coef, const float* Rs,
+                         const float* Wt1, const float* g_hsum, const float* g_next,
+                         const float* mu1, const float* inv1, const float* var1,
+                         const float* gamma, long long n, float eps, float* g_tot, float* GzS,
+                         float* dWs1, float* dWs2, float* dbs2, float* alpha, float* gam0,
+                         float* gam1, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
+                         void* stream);
 /* Sg = sum g, Sgx = sum g*(y-mu1)*inv1 (standalone EdgeModel backward). */
 int pfsgnn_edge_bn_grad_sums(int G, int NF, int NC, int F, const float* g, const float* y,
                              const float* mu1, const float* inv1, float* Sg, float* Sgx,

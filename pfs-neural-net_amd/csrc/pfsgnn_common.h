@@ -79,6 +79,27 @@ __device__ __forceinline__ void bn2_coef(const float* gamma, const float* beta, 
   }
 }
 
+// its backward as g_y = alpha*g + gam0 + gam1*y from Sg = sum g, Sgx = sum g*xhat
+__device__ __forceinline__ void bn2_bwd_coef_one(int c, float Sg, float Sgx, const float* mu1,
+                                                 const float* var1, const float* gamma,
+                                                 long long n, float eps, float* alpha,
+                                                 float* gam0, float* gam1, float* dgamma,
+                                                 float* dbeta) {
+  const float g = gamma[c], v = var1[c];
+  const float inv1 = 1.0f / sqrtf(v + eps);
+  const float rho = v * inv1 * inv1;
+  const float inv2 = 1.0f / sqrtf(g * g * rho + eps);
+  const float k = g * inv2;
+  const float M = Sgx / (float)n;
+  const float a = g * inv1 * k;
+  const float g1 = -a * M * (k * k + 1.f - k * k * rho) * inv1;
+  alpha[c] = a;
+  gam1[c] = g1;
+  gam0[c] = -a * Sg / (float)n - g1 * mu1[c];
+  dgamma[c] += k * Sgx * (2.f - k * k * rho);
+  dbeta[c] += Sg;
+}
+
 // ------------------------------------------------------------ edge geometry
 // Canonical edge order is class-major, e = (g*NC + c)*NF + f.  A block of 4
 // waves owns 64 consecutive fibers (lane = fiber) of one graph -- fiber group

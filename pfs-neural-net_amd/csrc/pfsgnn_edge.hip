@@ -293,8 +293,23 @@ __device__ __forceinline__ void chan_merge(double& C0, double& M0, double& Q0, d
   C0 = tot;
 }
 
-// merge per-block Welford partials -> mu, biased var (one 256-thread block per
-// channel: each thread merges a strided subset, then a fixed-order tree)
+// merge per-block Welford partials -> mu, biased var: one 256-thread block per
+// channel, the partials combined in closed form in double (no serial chain of
+// divisions): mean = sum c_b m_b / n, M2 = sum q_b + c_b (m_b - mean)^2, each
+// sum over a fixed assignment of partials to threads + a fixed-order tree.
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+  const int t = threadIdx.x;
+  red[t] = v;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) red[t] += red[t + w];
+    __syncthreads();
+  }
+  const double r = red[0];
+  __syncthreads();
+  return r;
+}
+
 // With `bn` (EdgeModel training forward): also the double BatchNorm's affine
 // and running statistics of channel k, as pfsgnn_bn2_finalize computes them.
 struct Bn2Args {
@@ -306,31 +321,56 @@ struct Bn2Args {
   float *sc, *sh, *inv1, *inv2;
 };
 
+#define MF_PB 8   // partials per thread (nb <= 2048: the edge grids)
 __global__ __launch_bounds__(256) void k_moments_finalize(const float* __restrict__ part, int nb,
                                                           int F, long long n,
                                                           float* __restrict__ mu,
                                                           float* __restrict__ var, Bn2Args bn) {
-  const int k = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  double cnt = 0, mean = 0, m2 = 0;
-  for (int b = t; b < nb; b += 256) {
-    const float* p = part + (size_t)b * (1 + 2 * F);
-    chan_merge(cnt, mean, m2, p[0], p[1 + k], p[1 + F + k]);
+  const int k = blockIdx.x, t = threadIdx.x;
+  __shared__ double red[256];
+  float pc[MF_PB], pm[MF_PB], pq[MF_PB];
+  double S = 0.0, Q = 0.0;
+  for (int b0 = 0; b0 < nb; b0 += 256 * MF_PB) {   // one round for nb <= 2048
+#pragma unroll
+    for (int i = 0; i < MF_PB; ++i) {
+      const int b = b0 + t + 256 * i;
+      const float* p = part + (size_t)(b < nb ? b : 0) * (1 + 2 * F);
+      pc[i] = b < nb ? p[0] : 0.f;
+      pm[i] = b < nb ? p[1 + k] : 0.f;
+      pq[i] = b < nb ? p[1 + F + k] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < MF_PB; ++i) S += (double)pc[i] * (double)pm[i];
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    const double cb = __shfl_xor(cnt, o), mb = __shfl_xor(mean, o), qb = __shfl_xor(m2, o);
-    double c1 = cnt, m1 = mean, q1 = m2;
-    if (lane & o) { c1 = cb; m1 = mb; q1 = qb; }
-    const double c2 = (lane & o) ? cnt : cb, mm2 = (lane & o) ? mean : mb,
-                 qq2 = (lane & o) ? m2 : qb;
-    chan_merge(c1, m1, q1, c2, mm2, qq2);
-    cnt = c1; mean = m1; m2 = q1;
+  const double M0 = block_sum_d(S, red) / (double)n;
+  for (int b0 = 0; b0 < nb; b0 += 256 * MF_PB) {
+    if (b0 > 0) {  // (re-read when the partials did not fit one round)
+#pragma unroll
+      for (int i = 0; i < MF_PB; ++i) {
+        const int b = b0 + t + 256 * i;
+        const float* p = part + (size_t)(b < nb ? b : 0) * (1 + 2 * F);
+        pc[i] = b < nb ? p[0] : 0.f;
+        pm[i] = b < nb ? p[1 + k] : 0.f;
+        pq[i] = b < nb ? p[1 + F + k] : 0.f;
+      }
+    } else if (nb > 256 * MF_PB) {
+#pragma unroll
+      for (int i = 0; i < MF_PB; ++i) {
+        const int b = t + 256 * i;
+        const float* p = part + (size_t)b * (1 + 2 * F);
+        pc[i] = p[0];
+        pm[i] = p[1 + k];
+        pq[i] = p[1 + F + k];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MF_PB; ++i) {
+      const double d = (double)pm[i] - M0;
+      Q += (double)pq[i] + (double)pc[i] * d * d;
+    }
   }
-  __shared__ double sh[4][3];
-  if (lane == 0) { sh[wave][0] = cnt; sh[wave][1] = mean; sh[wave][2] = m2; }
-  __syncthreads();
+  const double Q0 = block_sum_d(Q, red);
   if (t == 0) {
-    double C0 = sh[0][0], M0 = sh[0][1], Q0 = sh[0][2];
-    for (int w = 1; w < 4; ++w) chan_merge(C0, M0, Q0, sh[w][0], sh[w][1], sh[w][2]);
     const float m = (float)M0, v = (float)(Q0 / (double)n);
     mu[k] = m;
     var[k] = v;
@@ -1346,6 +1386,54 @@ extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, c
   return pf::check_launch("pfsgnn_target_bwd");
 }
 
+// The edge BatchNorm's two gradient sums straight from source_bwd's block
+// partials, and its backward coefficients, in one launch: block k sums channel
+// k over the nb partials (fixed order) and finishes like pfsgnn_bn2_bwd_coef.
+struct Bn2Bwd {
+  const float* gamma;
+  const float* mu1;
+  const float* var1;
+  long long n;
+  float eps;
+  float *alpha, *gam0, *gam1, *dgamma, *dbeta;
+};
+
+__global__ __launch_bounds__(256) void k_bn2_coef_part(const float* __restrict__ part, int nb,
+                                                       int F, Bn2Bwd bb, float* __restrict__ Sg,
+                                                       float* __restrict__ Sgx) {
+  const int k = blockIdx.x, t = threadIdx.x;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
+  int b = t;
+  for (; b + 768 < nb; b += 1024) {  // 4 partials in flight per thread and sum
+    const float* p = part + (size_t)b * 2 * F + k;
+    const size_t st = (size_t)256 * 2 * F;
+    a0 += p[0]; b0 += p[F];
+    a1 += p[st]; b1 += p[st + F];
+    a2 += p[2 * st]; b2 += p[2 * st + F];
+    a3 += p[3 * st]; b3 += p[3 * st + F];
+  }
+  for (; b < nb; b += 256) {
+    a0 += part[(size_t)b * 2 * F + k];
+    b0 += part[(size_t)b * 2 * F + F + k];
+  }
+  float v[2] = {(a0 + a1) + (a2 + a3), (b0 + b1) + (b2 + b3)};
+  __shared__ float scratch[8];
+  block_sum<2>(v, scratch);
+  if (t == 0) {
+    if (Sg) { Sg[k] = v[0]; Sgx[k] = v[1]; }
+    bn2_bwd_coef_one(k, v[0], v[1], bb.mu1, bb.var1, bb.gamma, bb.n, bb.eps, bb.alpha, bb.gam0,
+                     bb.gam1, bb.dgamma, bb.dbeta);
+  }
+}
+
+static int source_bwd_impl(int G, int NF, int NC, int F, const float* y, const float* sc,
+                           const float* sh, const float* Qt, const float* Ws1, const float* Ws2,
+                           const float* bs2, const float* mean, const float* coef, const float* Rs,
+                           const float* Wt1, const float* g_hsum, const float* g_next,
+                           const float* mu1, const float* inv1, float* g_tot, float* GzS,
+                           float* dWs1, float* dWs2, float* dbs2, float* Sg, float* Sgx,
+                           const Bn2Bwd* bb, void* ws, size_t ws_bytes, void* stream);
+
 extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                                  const float* sh, const float* Qt, const float* Ws1,
                                  const float* Ws2, const float* bs2, const float* mean,
@@ -1354,12 +1442,43 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
                                  const float* inv1, float* g_tot, float* GzS, float* dWs1,
                                  float* dWs2, float* dbs2, float* Sg, float* Sgx, void* ws,
                                  size_t ws_bytes, void* stream) {
+  return source_bwd_impl(G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, g_hsum,
+                         g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, Sg, Sgx, nullptr, ws,
+                         ws_bytes, stream);
+}
+
+extern "C" int pfsgnn_source_bwd_bn(int G, int NF, int NC, int F, const float* y, const float* sc,
+                                    const float* sh, const float* Qt, const float* Ws1,
+                                    const float* Ws2, const float* bs2, const float* mean,
+                                    const float* coef, const float* Rs, const float* Wt1,
+                                    const float* g_hsum, const float* g_next, const float* mu1,
+                                    const float* inv1, const float* var1, const float* gamma,
+                                    long long n, float eps, float* g_tot, float* GzS, float* dWs1,
+                                    float* dWs2, float* dbs2, float* alpha, float* gam0,
+                                    float* gam1, float* dgamma, float* dbeta, void* ws,
+                                    size_t ws_bytes, void* stream) {
+  PF_REQUIRE(mu1 && inv1 && var1 && gamma && n > 0 && alpha && gam0 && gam1 && dgamma && dbeta,
+             "pfsgnn_source_bwd_bn", "null");
+  const Bn2Bwd bb{gamma, mu1, var1, n, eps, alpha, gam0, gam1, dgamma, dbeta};
+  return source_bwd_impl(G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, g_hsum,
+                         g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, nullptr, nullptr, &bb,
+                         ws, ws_bytes, stream);
+}
+
+static int source_bwd_impl(int G, int NF, int NC, int F, const float* y, const float* sc,
+                           const float* sh, const float* Qt, const float* Ws1, const float* Ws2,
+                           const float* bs2, const float* mean, const float* coef, const float* Rs,
+                           const float* Wt1, const float* g_hsum, const float* g_next,
+                           const float* mu1, const float* inv1, float* g_tot, float* GzS,
+                           float* dWs1, float* dWs2, float* dbs2, float* Sg, float* Sgx,
+                           const Bn2Bwd* bb, void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_source_bwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(y && Qt && Ws1 && Ws2 && bs2 && mean && coef && g_tot && GzS && dWs1 && dWs2 && dbs2,
              "pfsgnn_source_bwd", "null");
   PF_REQUIRE((Rs == nullptr) == (Wt1 == nullptr) && (Rs == nullptr) == (g_hsum == nullptr),
              "pfsgnn_source_bwd", "Rs, Wt1, g_hsum must be given together");
-  PF_REQUIRE(!mu1 || (inv1 && Sg && Sgx), "pfsgnn_source_bwd", "mu1 needs inv1, Sg, Sgx");
+  PF_REQUIRE(!mu1 || (inv1 && ((Sg && Sgx) || bb)), "pfsgnn_source_bwd",
+             "mu1 needs inv1, Sg, Sgx");
   const EdgeGeo geo = geo_for(G, NF, NC);
   const int C = 2 * F;
   const size_t nb = geo.nblocks;
@@ -1395,13 +1514,17 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
                      {pW1, (int)nb, (size_t)C * F, F, C, F, dWs1 + F, C, 1, 1.f}};
     // the BatchNorm sums are read at once (bn2_bwd_coef); the weight
     // gradients only by the optimizer
-    const RedDesc* now = mu1 ? rd : rd + 2;
-    int nnow = mu1 ? 5 : 3;
+    const bool sums = mu1 && !bb;   // BN sums by the generic reduce
+    const RedDesc* now = sums ? rd : rd + 2;
+    int nnow = sums ? 5 : 3;
     if (defer) {
       pf::defer_push(rd + 2, 3);
       nnow -= 3;
     }
     if (nnow) launch_reduce_multi(now, nnow, st);
+    if (bb)
+      hipLaunchKernelGGL(k_bn2_coef_part, dim3(F), dim3(256), 0, st, pBN, (int)nb, F, *bb, Sg,
+                         Sgx);
   }
   launch_reduce_columns(pCol, G, geo.NFG, NC, C, GzS, st);
   return pf::check_launch("pfsgnn_source_bwd");

@@ -350,17 +350,17 @@ static int make_segs(const pfsgnn_seg* segs, int nseg, int N, XSegs& S) {
 // lin, W^T for lin_t -- in LDS once ([MT*16][4*KSM+1], odd stride), so the X
 // latency overlaps the staging and the MFMA chain runs without a wait.
 template <int MT, int KSM>
-__global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ W, int ldw, int trans,
-                                              int Mo, int Ki, XSegs S, int N,
-                                              const float* __restrict__ b, float bscale,
-                                              int act_in, const float* __restrict__ Z,
-                                              float* __restrict__ Y, int add) {
+__device__ __forceinline__ void gemm_block(const float* __restrict__ W, int ldw, int trans, int Mo,
+                                           int Ki, const XSegs& S, int N,
+                                           const float* __restrict__ b, float bscale, int act_in,
+                                           const float* __restrict__ Z, float* __restrict__ Y,
+                                           int add, int bid) {
   extern __shared__ float Ws[];
   // KSM K-steps of 4 always run (no per-step branch: the accumulators stay in
   // AGPRs across the chain); rows Ki..4*KSM of op(W) and X are zero
   constexpr int K4 = 4 * KSM, LDK = K4 + 1;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63, col = lane & 15, kq = lane >> 4;
-  const int n = blockIdx.x * 64 + wave * 16 + col;
+  const int n = bid * 64 + wave * 16 + col;
   const bool nv = n < N;
   const int nc = nv ? n : N - 1;
   const int Gc = S.npg ? N / S.npg : 1, ng = S.npg ? nc / S.npg : 0;
@@ -374,33 +374,35 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ W, int l
   // L2 round trip for every shape up to 100 x 100), then their LDS stores; the
   // (m, kk) split is recomputed for the stores instead of held in registers
   constexpr int MR = MT * 16, TOT = MR * K4;
-  constexpr int PER = (TOT + 255) / 256, BATCH = PER < 48 ? PER : 48;
-  auto split = [&](int idx, int& m, int& kk) {
+  // (a power-of-two batch: odd-sized register arrays here went to scratch)
+  constexpr int PER = (TOT + 255) / 256;
+  constexpr int BATCH = PER <= 1 ? 1 : PER <= 2 ? 2 : PER <= 4 ? 4 : PER <= 8 ? 8 : PER <= 16 ? 16 : 32;
+  // (m, kk) of staging item idx, returned by value (reference out-parameters
+  // here were kept in scratch memory)
+  auto split = [&](int idx) -> int2 {
     if (!trans) {
-      m = idx / K4;
-      kk = idx - m * K4;
-    } else {  // op(W) = W^T: walk W's rows so the reads stay contiguous
-      kk = idx / MR;
-      m = idx - kk * MR;
+      const int m = idx / K4;
+      return make_int2(m, idx - m * K4);
     }
+    // op(W) = W^T: walk W's rows so the reads stay contiguous
+    const int kk = idx / MR;
+    return make_int2(idx - kk * MR, kk);
   };
   for (int base = t; base < TOT; base += BATCH * 256) {
     float v[BATCH];
 #pragma unroll
     for (int u = 0; u < BATCH; ++u) {
       const int idx = base + u * 256;
-      int m, kk;
-      split(idx, m, kk);
+      const int2 mk = split(idx);
       v[u] = 0.f;
-      if (idx < TOT && m < Mo && kk < Ki)
-        v[u] = trans ? W[(size_t)kk * ldw + m] : W[(size_t)m * ldw + seg_wcol(S, kk)];
+      if (idx < TOT && mk.x < Mo && mk.y < Ki)
+        v[u] = trans ? W[(size_t)mk.y * ldw + mk.x] : W[(size_t)mk.x * ldw + seg_wcol(S, mk.y)];
     }
 #pragma unroll
     for (int u = 0; u < BATCH; ++u) {
       const int idx = base + u * 256;
-      int m, kk;
-      split(idx, m, kk);
-      if (idx < TOT) Ws[m * LDK + kk] = v[u];
+      const int2 mk = split(idx);
+      if (idx < TOT) Ws[mk.x * LDK + mk.y] = v[u];
     }
   }
   if (act_in) {
@@ -433,6 +435,46 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ W, int l
         *o = add ? (*o + v) : v;
       }
     }
+}
+
+template <int MT, int KSM>
+__global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ W, int ldw, int trans,
+                                              int Mo, int Ki, XSegs S, int N,
+                                              const float* __restrict__ b, float bscale,
+                                              int act_in, const float* __restrict__ Z,
+                                              float* __restrict__ Y, int add) {
+  gemm_block<MT, KSM>(W, ldw, trans, Mo, Ki, S, N, b, bscale, act_in, Z, Y, add, blockIdx.x);
+}
+
+// Several independent small products in one launch (pfsgnn_gemm_multi): job j
+// owns blocks [blk0_j, blk0_j + ceil(N_j / 64)); the table rides in the kernel
+// arguments; the instantiation covers the widest job (MT, KSM), narrower jobs
+// run zero padding.
+#define GM_MULTI 4
+struct GemmJob {
+  const float* W;
+  XSegs S;
+  const float* b;
+  const float* Z;
+  float* Y;
+  int ldw, trans, Mo, Ki, N, act_in, add, blk0;
+  float bscale;
+};
+struct GemmTable {
+  GemmJob j[GM_MULTI];
+  int njob;
+};
+
+template <int MT, int KSM>
+__global__ __launch_bounds__(256) void k_gemm_multi(GemmTable T) {
+  const int bx = blockIdx.x;
+  int jj = 0;
+#pragma unroll
+  for (int u = 1; u < GM_MULTI; ++u)
+    if (u < T.njob && bx >= T.j[u].blk0) jj = u;
+  const GemmJob& J = T.j[jj];   // read in place from the kernel arguments
+  gemm_block<MT, KSM>(J.W, J.ldw, J.trans, J.Mo, J.Ki, J.S, J.N, J.b, J.bscale, J.act_in, J.Z,
+                      J.Y, J.add, bx - J.blk0);
 }
 
 // K-step counts instantiated (Ki = 1..4, 9..12, 17..20, 29..32, 37..40, 97..100
@@ -520,6 +562,79 @@ extern "C" int pfsgnn_lin_t(const float* W, int ldw, int M, int K, const float* 
   // out[K][N] = W^T[K][M] . dY[M][N]
   return launch_gemm(W, ldw, 1, K, M, one_seg(dY, 0), N, nullptr, 1.f, 0, Z, out, add,
                      as_stream(stream), "pfsgnn_lin_t");
+}
+
+// Batched small products (the node-side Linear layers of one block that have
+// no data dependence on each other): up to GM_MULTI jobs per launch, each a
+// pfsgnn_lin_cat (trans 0) or pfsgnn_lin_t (trans 1); same per-output
+// arithmetic as the single launches (zero padding adds exact zeros).
+#define PF_GMM_ALL(X) \
+  X(1, 3) X(1, 5) X(1, 10) X(2, 3) X(2, 5) X(2, 10) X(3, 3) X(3, 5) X(3, 10) X(4, 3) X(4, 5) \
+  X(4, 10)
+extern "C" int pfsgnn_gemm_multi(const pfsgnn_gemm_job* jobs, int n, void* stream) {
+  const char* where = "pfsgnn_gemm_multi";
+  PF_REQUIRE(n >= 0 && (jobs || n == 0), where, "bad arguments");
+  hipStream_t st = as_stream(stream);
+  static bool attr = false;
+  if (!attr) {
+#define PF_GMA(T, K)                                                                           \
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_multi<T, K>),                \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    PF_GMM_ALL(PF_GMA)
+#undef PF_GMA
+    attr = true;
+  }
+  for (int i0 = 0; i0 < n; i0 += GM_MULTI) {
+    const int m = std::min(GM_MULTI, n - i0);
+    GemmTable T{};
+    int blocks = 0, mt = 1, ks = 3;
+    for (int u = 0; u < m; ++u) {
+      const pfsgnn_gemm_job& jb = jobs[i0 + u];
+      PF_REQUIRE(jb.W && jb.Y && jb.M > 0 && jb.N > 0 && (jb.trans == 0 || jb.trans == 1), where,
+                 "bad job");
+      GemmJob& J = T.j[u];
+      int Ki;
+      if (jb.trans) {
+        PF_REQUIRE(jb.nseg == 1 && jb.segs && jb.segs[0].x && !jb.segs[0].per_graph, where,
+                   "lin_t job takes one plain input block");
+        J.S = one_seg(jb.segs[0].x, 0);
+        Ki = jb.K;
+      } else {
+        Ki = make_segs(jb.segs, jb.nseg, jb.N, J.S);
+        PF_REQUIRE(Ki > 0, where, "bad segment list");
+      }
+      PF_REQUIRE(Ki <= 40 && jb.M <= 64, where, "job wider than the batched kernels (K 40, M 64)");
+      J.W = jb.W;
+      J.b = jb.b;
+      J.Z = jb.Z;
+      J.Y = jb.Y;
+      J.ldw = jb.ldw;
+      J.trans = jb.trans;
+      J.Mo = jb.M;
+      J.Ki = Ki;
+      J.N = jb.N;
+      J.act_in = jb.act_in;
+      J.add = jb.add;
+      J.bscale = jb.bscale;
+      J.blk0 = blocks;
+      blocks += (jb.N + 63) / 64;
+      mt = std::max(mt, (jb.M + 15) / 16);
+      const int k4 = (Ki + 3) / 4;
+      ks = std::max(ks, k4 <= 3 ? 3 : k4 <= 5 ? 5 : 10);
+    }
+    T.njob = m;
+    const size_t lds = (size_t)mt * 16 * (4 * ks + 1) * sizeof(float);
+    bool launched = false;
+#define PF_GMM(TT, KK)                                                                       \
+  if (!launched && mt == TT && ks == KK) {                                                   \
+    hipLaunchKernelGGL((k_gemm_multi<TT, KK>), dim3(blocks), dim3(256), lds, st, T);         \
+    launched = true;                                                                         \
+  }
+    PF_GMM_ALL(PF_GMM)
+#undef PF_GMM
+    PF_REQUIRE(launched, where, "no kernel for this shape");
+  }
+  return pf::check_launch(where);
 }
 
 // ---------------------------------------------------------------- wgrad
@@ -697,10 +812,11 @@ struct WgTable {
 template <int TMAX, int PER>
 __global__ __launch_bounds__(512) void k_wgrad_multi(WgTable T) {
   const int b = blockIdx.x;
-  WgJob J = T.j[0];
+  int jj = 0;
 #pragma unroll
   for (int u = 1; u < WG_MULTI; ++u)
-    if (u < T.njob && b >= T.j[u].blk0) J = T.j[u];
+    if (u < T.njob && b >= T.j[u].blk0) jj = u;
+  const WgJob& J = T.j[jj];   // read in place from the kernel arguments (a copy spills)
   wgrad_block<TMAX, PER>(J.dY, J.M, J.S, J.K, J.K1, J.N, J.act_in, J.chunk, J.vec, J.part,
                          b - J.blk0);
 }
@@ -1510,19 +1626,7 @@ __global__ void k_bn2_bwd_coef(const float* __restrict__ Sg, const float* __rest
                                float* __restrict__ dbeta) {
   const int c = threadIdx.x;
   if (c >= C) return;
-  const float g = gamma[c], v = var1[c];
-  const float inv1 = 1.0f / sqrtf(v + eps);
-  const float rho = v * inv1 * inv1;
-  const float inv2 = 1.0f / sqrtf(g * g * rho + eps);
-  const float k = g * inv2;
-  const float M = Sgx[c] / (float)n;
-  const float a = g * inv1 * k;
-  const float g1 = -a * M * (k * k + 1.f - k * k * rho) * inv1;
-  alpha[c] = a;
-  gam1[c] = g1;
-  gam0[c] = -a * Sg[c] / (float)n - g1 * mu1[c];
-  dgamma[c] += k * Sgx[c] * (2.f - k * k * rho);
-  dbeta[c] += Sg[c];
+  bn2_bwd_coef_one(c, Sg[c], Sgx[c], mu1, var1, gamma, n, eps, alpha, gam0, gam1, dgamma, dbeta);
 }
 
 extern "C" int pfsgnn_bn2_bwd_coef(const float* Sg, const float* Sgx, const float* mu1,

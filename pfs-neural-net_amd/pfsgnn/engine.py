@@ -200,12 +200,29 @@ class Engine:
 
     # ========================================================= model pieces
     # --- EdgeModel (gnn.py:86-101)
-    def edge_fwd(self, P, BN, d, pre, xs, xt, xe3, u):
+    def node_parts(self, P, d, pe, ps, xs, xt, u):
+        """The node parts of a block's first per-edge Linear layers that depend
+        only on the block's inputs -- EdgeModel's Ps, Pt (gnn.py:100) and
+        SModel's Qt (gnn.py:136) -- as one batched launch."""
+        F = self.F
+        W1, b1 = P[pe + "0.weight"], P[pe + "0.bias"]
+        Ws1, bs1 = P[ps + "node_mlp_1.0.weight"], P[ps + "node_mlp_1.0.bias"]
+        if 4 * F > 64:
+            return None
+        return self.be.linear_batch([
+            ("cat", W1, [(xs, 0, False)], d.NS, None),
+            ("cat", W1, [(xt, F, False), (u, 3 * F, True)], d.NT, b1),
+            ("cat", Ws1, [(xt, 0, False)], d.NT, bs1)])
+
+    def edge_fwd(self, P, BN, d, pre, xs, xt, xe3, u, parts=None):
         be, F = self.be, self.F
         W1, b1 = P[pre + "0.weight"], P[pre + "0.bias"]
         W2, b2 = P[pre + "2.weight"], P[pre + "2.bias"]
-        Ps = be.lin(W1, 0, F, xs)
-        Pt = be.lin_cat(W1, [(xt, F, False), (u, 3 * F, True)], d.NT, b=b1)
+        if parts is not None:
+            Ps, Pt = parts
+        else:
+            Ps = be.lin(W1, 0, F, xs)
+            Pt = be.lin_cat(W1, [(xt, F, False), (u, 3 * F, True)], d.NT, b=b1)
         if self.normed and self.training:
             # the double BatchNorm's finalize rides in the moments pass
             key = pre + "norm."
@@ -227,14 +244,19 @@ class Engine:
         return dict(xs=xs, xt=xt, xe3=xe3, u=u, Ps=Ps, Pt=Pt, y=y, mu1=mu1, var1=var1,
                     sc=sc, sh=sh, inv1=inv1)
 
-    def edge_bwd(self, P, Gr, d, pre, st, g_tot, Sg, Sgx, want_gxe, g_xs, g_xt, g_u):
-        """g_tot: d loss / d xe_new (canonical [F, E]); Sg/Sgx its BatchNorm sums.
+    def edge_bn_coef(self, P, Gr, d, pre, st, Sg, Sgx):
+        """The double BatchNorm's backward coefficients from its gradient sums."""
+        key = pre + "norm."
+        return self.be.bn2_bwd_coef(Sg, Sgx, st["mu1"], st["var1"], P[key + "weight"], d.E,
+                                    self.bn_eps, Gr[key + "weight"], Gr[key + "bias"])
+
+    def edge_bwd(self, P, Gr, d, pre, st, g_tot, bnc, want_gxe, g_xs, g_xt, g_u):
+        """g_tot: d loss / d xe_new (canonical [F, E]); bnc: the BatchNorm's
+        backward coefficients (alpha, gam0, gam1) (edge_bn_coef), None if unnormed.
         Adds the node-input gradients into g_xs / g_xt / g_u; returns d loss / d xe_in."""
         be, F, G = self.be, self.F, d.G
         if self.normed:
-            key = pre + "norm."
-            alpha, gam0, gam1 = be.bn2_bwd_coef(Sg, Sgx, st["mu1"], st["var1"], P[key + "weight"],
-                                                d.E, self.bn_eps, Gr[key + "weight"], Gr[key + "bias"])
+            alpha, gam0, gam1 = bnc
         else:
             alpha, gam0, gam1 = be.ones(F), be.zeros(F), be.zeros(F)
         W1, W2 = P[pre + "0.weight"], P[pre + "2.weight"]
@@ -244,21 +266,25 @@ class Engine:
                                            st["Ps"], st["Pt"], W1, W2, dW1, Gr[pre + "2.weight"],
                                            Gr[pre + "2.bias"], want_gxe=want_gxe)
         be.wgrad(GzEs, st["xs"], dW1, col0=0)
-        be.lin_t(W1, 0, F, GzEs, out=g_xs, add=True)
         # x_t[tgt] and u[batch] columns in one pass (u's gradient sums over classes)
         be.wgrad_cat(GzEt, [(st["xt"], F, False), (st["u"], 3 * F, True)], dW1,
                      db=Gr[pre + "0.bias"])
-        be.lin_t(W1, F, F, GzEt, out=g_xt, add=True)
+        if 4 * F <= 40:      # the two node-input gradients in one launch
+            be.linear_batch([("t", W1, 0, F, GzEs, g_xs, True), ("t", W1, F, F, GzEt, g_xt, True)])
+        else:
+            be.lin_t(W1, 0, F, GzEs, out=g_xs, add=True)
+            be.lin_t(W1, F, F, GzEt, out=g_xt, add=True)
         GzEu = be.graph_reduce(GzEt, G)
         be.lin_t(W1, 3 * F, F, GzEu, out=g_u, add=True)
         return g_xe
 
     # --- SModel (gnn.py:123-154)
-    def source_fwd(self, P, BN, d, pre, xs, xt, xe3, u):
+    def source_fwd(self, P, BN, d, pre, xs, xt, xe3, u, Qt=None):
         be, F = self.be, self.F
         Ws1, bs1 = P[pre + "node_mlp_1.0.weight"], P[pre + "node_mlp_1.0.bias"]
         Ws2, bs2 = P[pre + "node_mlp_1.2.weight"], P[pre + "node_mlp_1.2.bias"]
-        Qt = be.lin(Ws1, 0, F, xt, b=bs1)
+        if Qt is None:
+            Qt = be.lin(Ws1, 0, F, xt, b=bs1)
         hmom = be.empty(8 * F, d.NS)
         mom = be.source_fwd(d, xe3[0], xe3[1], xe3[2], Qt, Ws1, Ws2, bs2, hmom)
         # node_mlp_2 input [x, mean, std, skew, kurt, u[batch]] (gnn.py:153), in place,
@@ -278,18 +304,30 @@ class Engine:
         # messages per fiber: NC on complete graphs, the fiber degree otherwise
         return be.moment_coef(st["mom"], gst, d.NC if d.sp is None else d.sp.fib_ptr)
 
-    def source_edge_bwd(self, P, Gr, d, pre, st, coef, tpart, g_next, bnstat, g_xt):
+    def source_edge_bwd(self, P, Gr, d, pre, st, coef, tpart, g_next, bnstat, g_xt, se=None,
+                        epre=None):
+        """SModel edge backward; with the upstream EdgeModel's state ``se`` (and
+        its prefix) the edge BatchNorm's backward coefficients come out of the
+        same call -> (g_tot, (alpha, gam0, gam1)); else -> (g_tot, Sg, Sgx)."""
         be, F = self.be, self.F
         Ws1, Ws2 = P[pre + "node_mlp_1.0.weight"], P[pre + "node_mlp_1.2.weight"]
         y, sc, sh = st["xe3"]
-        g_tot, GzS, Sg, Sgx = be.source_bwd(
+        bn2 = None
+        if se is not None and bnstat is not None:
+            key = epre + "norm."
+            bn2 = (P[key + "weight"], se["var1"], d.E, self.bn_eps, Gr[key + "weight"],
+                   Gr[key + "bias"])
+        out = be.source_bwd(
             d, y, sc, sh, st["Qt"], Ws1, Ws2, P[pre + "node_mlp_1.2.bias"], st["mom"][0], coef,
             tpart, g_next, bnstat, Gr[pre + "node_mlp_1.0.weight"], Gr[pre + "node_mlp_1.2.weight"],
-            Gr[pre + "node_mlp_1.2.bias"])
+            Gr[pre + "node_mlp_1.2.bias"], bn2=bn2)
+        g_tot, GzS = out[0], out[1]
         be.wgrad(GzS, st["xt"], Gr[pre + "node_mlp_1.0.weight"], col0=0,
                  db=Gr[pre + "node_mlp_1.0.bias"])
         be.lin_t(Ws1, 0, F, GzS, out=g_xt, add=True)
-        return g_tot, Sg, Sgx
+        if bn2 is not None:
+            return g_tot, out[4]
+        return g_tot, out[2], out[3]
 
     # --- TModel (gnn.py:175-192)
     def target_fwd(self, P, BN, d, pre, xs, xt, xe3, u):
@@ -374,9 +412,12 @@ class Engine:
         u = u_in
         for b in range(self.B):
             p = f"mpb.{b}."
-            se = self.edge_fwd(P, BN, d, p + "edge_model.", xs, xt, xe3, u)
+            parts = self.node_parts(P, d, p + "edge_model.", p + "s_model.", xs, xt, u)
+            se = self.edge_fwd(P, BN, d, p + "edge_model.", xs, xt, xe3, u,
+                               parts=None if parts is None else parts[:2])
             xe3n = (se["y"], se["sc"], se["sh"])
-            ss = self.source_fwd(P, BN, d, p + "s_model.", xs, xt, xe3n, u)
+            ss = self.source_fwd(P, BN, d, p + "s_model.", xs, xt, xe3n, u,
+                                 Qt=None if parts is None else parts[2])
             stt = self.target_fwd(P, BN, d, p + "t_model.", ss["xs_new"], xt, xe3n, u)
             su = self.global_fwd(P, d, p + "global_model.", ss["xs_new"], stt["xt_new"], u)
             ctx["blocks"].append((se, ss, stt, su))
@@ -431,14 +472,17 @@ class Engine:
                     self.target_edge_bwd(P, Gr, d, p + "t_model.", stt, g_hsum, False, g_xs_new)
                     tpart = (stt["Rs"], P[p + "t_model.node_mlp_1.0.weight"], g_hsum)
                 coef = self.source_node_bwd(P, Gr, d, p + "s_model.", ss, g_xs_new, g_xs_in, g_u_in)
-                g_tot, Sg, Sgx = self.source_edge_bwd(P, Gr, d, p + "s_model.", ss, coef, tpart,
-                                                      g_xe, bnstat, g_xt_in)
+                g_tot, *bnc = self.source_edge_bwd(P, Gr, d, p + "s_model.", ss, coef, tpart,
+                                                   g_xe, bnstat, g_xt_in, se=se,
+                                                   epre=p + "edge_model.")
+                bnc = bnc[0] if self.normed else None
             else:
                 g_tot = be.zeros(F, d.E) if g_xe is None else g_xe
-                Sg = Sgx = None
+                bnc = None
                 if self.normed:
                     Sg, Sgx = be.edge_bn_grad_sums(d, g_tot, se["y"], *bnstat)
-            g_xe = self.edge_bwd(P, Gr, d, p + "edge_model.", se, g_tot, Sg, Sgx, b > 0,
+                    bnc = self.edge_bn_coef(P, Gr, d, p + "edge_model.", se, Sg, Sgx)
+            g_xe = self.edge_bwd(P, Gr, d, p + "edge_model.", se, g_tot, bnc, b > 0,
                                  g_xs_in, g_xt_in, g_u_in)
             g_xs, g_xt, g_u = g_xs_in, g_xt_in, g_u_in
         s_enc, t_enc = ctx["enc"]

@@ -481,11 +481,12 @@ class _EdgeFn(torch.autograd.Function):
         P, Gr = module._flat_params(), module._flat_grads()
         gc = grad_edges_in(g, lay)
         gc = be.zeros(F, d.E) if gc is None else gc.contiguous()
-        Sg = Sgx = None
+        bnc = None
         if module.normed:
             Sg, Sgx = be.edge_bn_grad_sums(d, gc, st["y"], st["mu1"], st["inv1"])
+            bnc = eng.edge_bn_coef(P, Gr, d, "", st, Sg, Sgx)
         g_xs, g_xt, g_u = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
-        g_xe = eng.edge_bwd(P, Gr, d, "", st, gc, Sg, Sgx, True, g_xs, g_xt, g_u)
+        g_xe = eng.edge_bwd(P, Gr, d, "", st, gc, bnc, True, g_xs, g_xt, g_u)
         return g_xs.t(), g_xt.t(), grad_edges_out(g_xe, lay), g_u.t(), None, None, None
 
 
@@ -526,7 +527,7 @@ class _SourceFn(torch.autograd.Function):
         P, Gr = module._flat_params(), module._flat_grads()
         g_xs, g_xt, g_u = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
         coef = eng.source_node_bwd(P, Gr, d, "", st, g.t().contiguous(), g_xs, g_u)
-        g_tot, _, _ = eng.source_edge_bwd(P, Gr, d, "", st, coef, None, None, None, g_xt)
+        g_tot = eng.source_edge_bwd(P, Gr, d, "", st, coef, None, None, None, g_xt)[0]
         return g_xs.t(), g_xt.t(), grad_edges_out(g_tot, lay), g_u.t(), None, None, None
 
 

@@ -69,6 +69,18 @@ class WgJob(ctypes.Structure):
 
 WGJP = ctypes.POINTER(WgJob)
 
+
+class GemmJob(ctypes.Structure):
+    """pfsgnn_gemm_job (include/pfsgnn.h): one product of a batched launch."""
+    _fields_ = [("W", ctypes.c_void_p), ("ldw", ctypes.c_int), ("trans", ctypes.c_int),
+                ("M", ctypes.c_int), ("K", ctypes.c_int), ("segs", SEGP), ("nseg", ctypes.c_int),
+                ("N", ctypes.c_int), ("b", ctypes.c_void_p), ("bscale", ctypes.c_float),
+                ("act_in", ctypes.c_int), ("Z", ctypes.c_void_p), ("Y", ctypes.c_void_p),
+                ("add", ctypes.c_int)]
+
+
+GMJP = ctypes.POINTER(GemmJob)
+
 _SIGS = {
     "pfsgnn_version": ([], ctypes.c_char_p),
     "pfsgnn_last_error": ([], ctypes.c_char_p),
@@ -90,6 +102,7 @@ _SIGS = {
                                ctypes.POINTER(ctypes.c_int), P], I),
     "pfsgnn_reduce_batch": ([REDP, I, P], I),
     "pfsgnn_wgrad_multi_bytes": ([WGJP, I], SZ),
+    "pfsgnn_gemm_multi": ([GMJP, I, P], I),
     "pfsgnn_wgrad_multi": ([WGJP, I, P, SZ, P], I),
     "pfsgnn_defer_begin": ([P, SZ], I),
     "pfsgnn_defer_end": ([P], I),
@@ -131,6 +144,7 @@ _SIGS = {
     "pfsgnn_target_fwd": ([I, I, I, I, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_target_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_source_bwd": ([I, I, I, I] + [P] * 22 + [P, SZ, P], I),
+    "pfsgnn_source_bwd_bn": ([I, I, I, I] + [P] * 17 + [LL, FL] + [P] * 10 + [P, SZ, P], I),
     "pfsgnn_edge_bn_grad_sums": ([I, I, I, I, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_edge_mlp_bwd": ([I, I, I, I] + [P] * 18 + [P, SZ, P], I),
     "pfsgnn_loss_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, FL, FL, ULL, P, P, P, P, P, P, P, SZ, P], I),
@@ -309,6 +323,38 @@ class HipBackend:
         _call("pfsgnn_lin_t", W.data_ptr() + 4 * col0, ldw, M, ncol, dY.data_ptr(), N, _ptr(z),
               out.data_ptr(), int(add), _stream())
         return out
+
+    def linear_batch(self, ops):
+        """Independent small products in one launch (pfsgnn_gemm_multi).  ops:
+        ("cat", W, segs, N, b) -> Y = W . cat(segs) + b (a new [M, N] tensor), or
+        ("t", W, col0, ncol, dY, out, add) -> out (+)= W[:, col0:col0+ncol]^T dY.
+        Returns the outputs in order."""
+        arr = (GemmJob * len(ops))()
+        keep, outs = [], []
+        for i, op in enumerate(ops):
+            if op[0] == "cat":
+                _, W, segs, N, b = op
+                M, ldw = W.shape
+                Y = self.empty(M, N)
+                sg = self._segs(segs, N)
+                self._chk(W, b)
+                arr[i] = GemmJob(W.data_ptr(), ldw, 0, M, 0, sg, len(segs), N, _ptr(b), 1.0, 0,
+                                 None, Y.data_ptr(), 0)
+                keep.append(sg)
+            else:
+                _, W, col0, ncol, dY, Y, add = op
+                Mw, ldw = W.shape
+                N = dY.shape[1]
+                if Y is None:
+                    Y, add = self.empty(ncol, N), False
+                self._chk(W, dY, Y)
+                sg = self._segs([(dY, 0, False)], N)
+                arr[i] = GemmJob(W.data_ptr() + 4 * col0, ldw, 1, ncol, Mw, sg, 1, N, None, 1.0,
+                                 0, None, Y.data_ptr(), int(add))
+                keep.append(sg)
+            outs.append(Y)
+        _call("pfsgnn_gemm_multi", arr, len(ops), _stream())
+        return outs
 
     # ----------------------------------------------- deferred weight gradients
     # Between defer_begin() and defer_flush(), wgrad/wgrad_cat only record a
@@ -666,10 +712,18 @@ class HipBackend:
         return GzT, gxe
 
     def source_bwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next, bnstat,
-                   dWs1, dWs2, dbs2):
+                   dWs1, dWs2, dbs2, bn2=None):
+        """-> (g_tot, GzS, Sg, Sgx).  With ``bn2`` = (gamma, var1, n, eps, dgamma,
+        dbeta) (and ``bnstat``) the edge BatchNorm's backward is finished in the
+        same call: -> (g_tot, GzS, None, None, (alpha, gam0, gam1))."""
         if d.sp is not None:
-            return self._sp.source_bwd(d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next,
-                                       bnstat, dWs1, dWs2, dbs2)
+            out = self._sp.source_bwd(d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next,
+                                      bnstat, dWs1, dWs2, dbs2)
+            if bn2 is None:
+                return out
+            gamma, var1, n, eps, dg, db = bn2
+            cf = self.bn2_bwd_coef(out[2], out[3], bnstat[0], var1, gamma, n, eps, dg, db)
+            return out[0], out[1], None, None, cf
         g_tot = self.empty(d.F, d.E)
         GzS = self.empty(2 * d.F, d.NT)
         Rs = Wt1 = g_hsum = None
@@ -679,16 +733,26 @@ class HipBackend:
         mu1 = inv1 = Sg = Sgx = None
         if bnstat is not None:
             mu1, inv1 = bnstat
-            Sg, Sgx = self.empty(d.F), self.empty(d.F)
+            if bn2 is None:
+                Sg, Sgx = self.empty(d.F), self.empty(d.F)
         mean = mean.contiguous()
         if g_next is not None:
             g_next = g_next.contiguous()
         ws, wsb = self._wsargs(d)
-        _call("pfsgnn_source_bwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
-              Qt.data_ptr(), Ws1.data_ptr(), Ws2.data_ptr(), bs2.data_ptr(), mean.data_ptr(),
-              coef.data_ptr(), _ptr(Rs), _ptr(Wt1), _ptr(g_hsum), _ptr(g_next), _ptr(mu1),
-              _ptr(inv1), g_tot.data_ptr(), GzS.data_ptr(), dWs1.data_ptr(), dWs2.data_ptr(),
-              dbs2.data_ptr(), _ptr(Sg), _ptr(Sgx), ws, wsb, _stream())
+        head = (d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh), Qt.data_ptr(),
+                Ws1.data_ptr(), Ws2.data_ptr(), bs2.data_ptr(), mean.data_ptr(), coef.data_ptr(),
+                _ptr(Rs), _ptr(Wt1), _ptr(g_hsum), _ptr(g_next), _ptr(mu1), _ptr(inv1))
+        if bn2 is not None:
+            assert bnstat is not None
+            gamma, var1, n, eps, dg, db = bn2
+            a, g0, g1 = self.empty(d.F), self.empty(d.F), self.empty(d.F)
+            _call("pfsgnn_source_bwd_bn", *head, var1.data_ptr(), gamma.data_ptr(), int(n),
+                  float(eps), g_tot.data_ptr(), GzS.data_ptr(), dWs1.data_ptr(), dWs2.data_ptr(),
+                  dbs2.data_ptr(), a.data_ptr(), g0.data_ptr(), g1.data_ptr(), dg.data_ptr(),
+                  db.data_ptr(), ws, wsb, _stream())
+            return g_tot, GzS, None, None, (a, g0, g1)
+        _call("pfsgnn_source_bwd", *head, g_tot.data_ptr(), GzS.data_ptr(), dWs1.data_ptr(),
+              dWs2.data_ptr(), dbs2.data_ptr(), _ptr(Sg), _ptr(Sgx), ws, wsb, _stream())
         return g_tot, GzS, Sg, Sgx
 
     def edge_bn_grad_sums(self, d, g, y, mu1, inv1):

@@ -111,6 +111,17 @@ class EmuBackend:
         if db is not None:
             db += dbscale * dY.sum(1)
 
+    def linear_batch(self, ops):
+        outs = []
+        for op in ops:
+            if op[0] == "cat":
+                _, W, segs, N, b = op
+                outs.append(self.lin_cat(W, segs, N, b=b))
+            else:
+                _, W, col0, ncol, dY, Y, add = op
+                outs.append(self.lin_t(W, col0, ncol, dY, out=Y, add=add))
+        return outs
+
     def defer_begin(self):  # weight-gradient batching is a no-op here
         pass
 
@@ -367,7 +378,17 @@ class EmuBackend:
         return GzT, gxe
 
     def source_bwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next,
-                   bnstat, dWs1, dWs2, dbs2):
+                   bnstat, dWs1, dWs2, dbs2, bn2=None):
+        out = self._source_bwd(d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next,
+                               bnstat, dWs1, dWs2, dbs2)
+        if bn2 is None:
+            return out
+        gamma, var1, n, eps, dg, db = bn2
+        cf = self.bn2_bwd_coef(out[2], out[3], bnstat[0], var1, gamma, n, eps, dg, db)
+        return out[0], out[1], None, None, cf
+
+    def _source_bwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next,
+                    bnstat, dWs1, dWs2, dbs2):
         """Returns (g_tot [F,E], GzS [2F, NT], Sg, Sgx).  ``coef`` = [4, 2F, NS]
         (C0..C3 of g_m = C0 + d*(C1 + d*(C2 + d*C3)), d = m - mean)."""
         if d.sp is not None:

@@ -412,3 +412,29 @@ def test_mlp_fused(hb, blocks, H, O, N, G, bn):
             # judged against the fp32 rounding of the sum of |terms|
             atol += 1e-6 * res["emu"]["dYp"].abs().sum(1).max().item()
         close(res["hip"][k], v, rtol=5e-5, atol=atol, name=k)
+
+
+def test_linear_batch_matches_single_launches():
+    """pfsgnn_gemm_multi (node parts / input gradients batched) against the
+    single-launch pfsgnn_lin_cat / pfsgnn_lin_t: bitwise equal."""
+    from pfsgnn.gnn import backend
+    hb = backend()
+    g = torch.Generator().manual_seed(5)
+    r = lambda *s: torch.randn(*s, generator=g).cuda()  # noqa: E731
+    F, G, NS, NT = 10, 3, 3 * 301, 3 * 37
+    W1, b1, Ws1, bs1 = r(4 * F, 4 * F), r(4 * F), r(2 * F, 2 * F), r(2 * F)
+    xs, xt, u = r(F, NS), r(F, NT), r(F, G)
+    outs = hb.linear_batch([("cat", W1, [(xs, 0, False)], NS, None),
+                            ("cat", W1, [(xt, F, False), (u, 3 * F, True)], NT, b1),
+                            ("cat", Ws1, [(xt, 0, False)], NT, bs1)])
+    ref = [hb.lin(W1, 0, F, xs), hb.lin_cat(W1, [(xt, F, False), (u, 3 * F, True)], NT, b=b1),
+           hb.lin(Ws1, 0, F, xt, b=bs1)]
+    for a, b in zip(outs, ref):
+        assert torch.equal(a, b)
+    gs, gt = r(4 * F, NS), r(4 * F, NT)
+    ys, yt = r(F, NS), r(F, NT)
+    ys2, yt2 = ys.clone(), yt.clone()
+    hb.linear_batch([("t", W1, 0, F, gs, ys, True), ("t", W1, F, F, gt, yt, True)])
+    hb.lin_t(W1, 0, F, gs, out=ys2, add=True)
+    hb.lin_t(W1, F, F, gt, out=yt2, add=True)
+    assert torch.equal(ys, ys2) and torch.equal(yt, yt2)
