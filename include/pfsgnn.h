@@ -86,6 +86,14 @@ int pfsgnn_timing_query(const char* name, double* total_ms, long long* count);
 /* Y[m][n] (+)= sum_k W[m][k] * act(X[k][n]) + bscale*b[m]; act = lrelu if act_in */
 int pfsgnn_lin(const float* W, int ldw, int M, int K, const float* X, int N,
                const float* b, float bscale, int act_in, float* Y, int add, void* stream);
+/* pfsgnn_lin + per-column gathers in the epilogue:
+ * Y[m][n] (+)= (W . act(X))[m][n] + bscale*b[m] + G1[m][idx1[n]] + G2[m][idx2[n]]
+ * (G1/G2 [M][ld] node tables or NULL) -- the general-graph path's first
+ * per-edge Linear, gnn.py:100/136/188, with its node parts gathered per edge */
+int pfsgnn_lin_gather(const float* W, int ldw, int M, int K, const float* X, int N,
+                      const float* b, float bscale, int act_in, float* Y, int add,
+                      const float* G1, const int* idx1, int ld1, const float* G2, const int* idx2,
+                      int ld2, void* stream);
 /* out[k][n] (+)= (sum_m W[m][k] dY[m][n]) * (Z ? lrelu'(Z[k][n]) : 1) */
 int pfsgnn_lin_t(const float* W, int ldw, int M, int K, const float* dY, int N,
                  const float* Z, float* out, int add, void* stream);
@@ -333,11 +341,12 @@ int pfsgnn_sparse_layout(const long long* edge_index, long long E, int G, int NF
 int pfsgnn_gather_cols(const float* X, int C, int N, const int* idx, long long E, const float* Z,
                        int mode, float* out, void* stream);
 /* out[c][s] (+)= sum over the segment's positions p in [ptr[s], ptr[s+1]) of
- * act(X[c][ord ? ord[p] : p]); act = lrelu (0.1) if `act`, identity otherwise */
+ * act(X[c][ord ? ord[p] : p]); act = lrelu (0.1) if `act`, identity otherwise;
+ * C <= 64 (one wave per segment, every channel in registers) */
 int pfsgnn_segment_sum(const float* X, int C, long long E, const int* ord, const int* ptr,
                        int nseg, int act, float* out, int add, void* stream);
-/* SModel moments per fiber (gnn.py:140-151): mom [4][C][nseg] = (mean, c2, c3,
- * c4) and the node_mlp_2 inputs hs [4C][nseg] = (mean, std, skew, kurt);
+/* SModel moments per fiber (gnn.py:140-151), C <= 32: mom [4][C][nseg] = (mean,
+ * c2, c3, c4) and the node_mlp_2 inputs hs [4C][nseg] = (mean, std, skew, kurt);
  * an empty fiber gives zeros and std = sqrt(1e-6), as the reference's
  * scatter-mean + nan_to_num do */
 int pfsgnn_segment_moments(const float* M, int C, long long E, const int* ptr, int nseg,

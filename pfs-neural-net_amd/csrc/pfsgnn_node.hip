@@ -349,12 +349,21 @@ static int make_segs(const pfsgnn_seg* segs, int nseg, int N, XSegs& S) {
 // slots, held in registers), then the block stages the whole op(W) -- W for
 // lin, W^T for lin_t -- in LDS once ([MT*16][4*KSM+1], odd stride), so the X
 // latency overlaps the staging and the MFMA chain runs without a wait.
+// Optional epilogue gathers of lin: Y[m][n] += g[j][m*ld[j] + idx[j][n]] --
+// per-node tables indexed per column (the general-graph path adds the gathered
+// node parts of a first Linear, gnn.py:100/136/188, in the same pass)
+struct GatherAdd {
+  const float* g[2];
+  const int* idx[2];
+  int ld[2];
+};
+
 template <int MT, int KSM>
 __device__ __forceinline__ void gemm_block(const float* __restrict__ W, int ldw, int trans, int Mo,
                                            int Ki, const XSegs& S, int N,
                                            const float* __restrict__ b, float bscale, int act_in,
                                            const float* __restrict__ Z, float* __restrict__ Y,
-                                           int add, int bid) {
+                                           int add, int bid, const GatherAdd& GA) {
   extern __shared__ float Ws[];
   // KSM K-steps of 4 always run (no per-step branch: the accumulators stay in
   // AGPRs across the chain); rows Ki..4*KSM of op(W) and X are zero
@@ -405,15 +414,15 @@ __device__ __forceinline__ void gemm_block(const float* __restrict__ W, int ldw,
       if (idx < TOT) Ws[mk.x * LDK + mk.y] = v[u];
     }
   }
+  __syncthreads();
+  const float* wr = Ws + col * LDK + kq;
   if (act_in) {
 #pragma unroll
     for (int s = 0; s < KSM; ++s) bv[s] = lrelu(bv[s]);
   }
-  __syncthreads();
   floatx4 acc[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const float* wr = Ws + col * LDK + kq;
 #pragma unroll
   for (int s = 0; s < KSM; ++s) {
 #pragma unroll
@@ -422,6 +431,10 @@ __device__ __forceinline__ void gemm_block(const float* __restrict__ W, int ldw,
                                                      0, 0, 0);
   }
   if (!nv) return;
+  // (epilogue gathers only in the small shapes that take them)
+  constexpr bool GATH = MT <= 4 && KSM <= 16;
+  const int gi0 = GATH && GA.g[0] ? GA.idx[0][n] : 0;
+  const int gi1 = GATH && GA.g[1] ? GA.idx[1][n] : 0;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -430,6 +443,8 @@ __device__ __forceinline__ void gemm_block(const float* __restrict__ W, int ldw,
       if (row < Mo) {
         float v = acc[mt][r];
         if (b) v += bscale * b[row];
+        if (GATH && GA.g[0]) v += GA.g[0][(size_t)row * GA.ld[0] + gi0];
+        if (GATH && GA.g[1]) v += GA.g[1][(size_t)row * GA.ld[1] + gi1];
         if (Z) v *= dlrelu(Z[(size_t)row * N + n]);
         float* o = Y + (size_t)row * N + n;
         *o = add ? (*o + v) : v;
@@ -442,8 +457,8 @@ __global__ __launch_bounds__(256) void k_gemm(const float* __restrict__ W, int l
                                               int Mo, int Ki, XSegs S, int N,
                                               const float* __restrict__ b, float bscale,
                                               int act_in, const float* __restrict__ Z,
-                                              float* __restrict__ Y, int add) {
-  gemm_block<MT, KSM>(W, ldw, trans, Mo, Ki, S, N, b, bscale, act_in, Z, Y, add, blockIdx.x);
+                                              float* __restrict__ Y, int add, GatherAdd GA) {
+  gemm_block<MT, KSM>(W, ldw, trans, Mo, Ki, S, N, b, bscale, act_in, Z, Y, add, blockIdx.x, GA);
 }
 
 // Several independent small products in one launch (pfsgnn_gemm_multi): job j
@@ -473,8 +488,9 @@ __global__ __launch_bounds__(256) void k_gemm_multi(GemmTable T) {
   for (int u = 1; u < GM_MULTI; ++u)
     if (u < T.njob && bx >= T.j[u].blk0) jj = u;
   const GemmJob& J = T.j[jj];   // read in place from the kernel arguments
+  const GatherAdd none{};
   gemm_block<MT, KSM>(J.W, J.ldw, J.trans, J.Mo, J.Ki, J.S, J.N, J.b, J.bscale, J.act_in, J.Z,
-                      J.Y, J.add, bx - J.blk0);
+                      J.Y, J.add, bx - J.blk0, none);
 }
 
 // K-step counts instantiated (Ki = 1..4, 9..12, 17..20, 29..32, 37..40, 97..100
@@ -499,12 +515,13 @@ static void gemm_attr() {
 template <int MT>
 static void gemm_launch(int ksm, dim3 grid, size_t lds, hipStream_t st, const float* W, int ldw,
                         int trans, int Mo, int Ki, const XSegs& S, int N, const float* b,
-                        float bscale, int act_in, const float* Z, float* Y, int add) {
+                        float bscale, int act_in, const float* Z, float* Y, int add,
+                        const GatherAdd& GA) {
   switch (ksm) {
 #define PF_CASE(KSM)                                                                           \
   case KSM:                                                                                    \
     hipLaunchKernelGGL((k_gemm<MT, KSM>), grid, dim3(256), lds, st, W, ldw, trans, Mo, Ki, S, \
-                       N, b, bscale, act_in, Z, Y, add);                                       \
+                       N, b, bscale, act_in, Z, Y, add, GA);                                   \
     break;
     PF_GEMM_KSM(PF_CASE)
 #undef PF_CASE
@@ -513,7 +530,7 @@ static void gemm_launch(int ksm, dim3 grid, size_t lds, hipStream_t st, const fl
 
 static int launch_gemm(const float* W, int ldw, int trans, int Mo, int Ki, const XSegs& S, int N,
                        const float* b, float bscale, int act_in, const float* Z, float* Y, int add,
-                       hipStream_t st, const char* where) {
+                       hipStream_t st, const char* where, const GatherAdd& GA = GatherAdd{}) {
   const int MT = (Mo + 15) / 16;
   const int ksm = gemm_ksm(Ki);
   if (ksm < 0) return pf::fail(where, "input width > 160 not supported");
@@ -529,7 +546,7 @@ static int launch_gemm(const float* W, int ldw, int trans, int Mo, int Ki, const
   const size_t lds = (size_t)MT * 16 * (4 * ksm + 1) * sizeof(float);
   switch (MT) {
 #define PF_MT(T) \
-  case T: gemm_launch<T>(ksm, grid, lds, st, W, ldw, trans, Mo, Ki, S, N, b, bscale, act_in, Z, Y, add); break;
+  case T: gemm_launch<T>(ksm, grid, lds, st, W, ldw, trans, Mo, Ki, S, N, b, bscale, act_in, Z, Y, add, GA); break;
     PF_MT(1) PF_MT(2) PF_MT(3) PF_MT(4) PF_MT(5) PF_MT(6) PF_MT(7) PF_MT(8) PF_MT(9) PF_MT(10)
     PF_MT(11)
 #undef PF_MT
@@ -543,6 +560,19 @@ extern "C" int pfsgnn_lin(const float* W, int ldw, int M, int K, const float* X,
   PF_REQUIRE(W && X && Y && M > 0 && K > 0 && N > 0, "pfsgnn_lin", "bad arguments");
   return launch_gemm(W, ldw, 0, M, K, one_seg(X, 0), N, b, bscale, act_in, nullptr, Y, add,
                      as_stream(stream), "pfsgnn_lin");
+}
+
+extern "C" int pfsgnn_lin_gather(const float* W, int ldw, int M, int K, const float* X, int N,
+                                 const float* b, float bscale, int act_in, float* Y, int add,
+                                 const float* G1, const int* idx1, int ld1, const float* G2,
+                                 const int* idx2, int ld2, void* stream) {
+  PF_REQUIRE(W && X && Y && M > 0 && K > 0 && N > 0 && (!G1 || idx1) && (!G2 || idx2),
+             "pfsgnn_lin_gather", "bad arguments");
+  PF_REQUIRE((!G1 && !G2) || (M <= 64 && K <= 64), "pfsgnn_lin_gather",
+             "gathers need M, K <= 64");
+  const GatherAdd GA{{G1, G2}, {idx1, idx2}, {ld1, ld2}};
+  return launch_gemm(W, ldw, 0, M, K, one_seg(X, 0), N, b, bscale, act_in, nullptr, Y, add,
+                     as_stream(stream), "pfsgnn_lin_gather", GA);
 }
 
 extern "C" int pfsgnn_lin_cat(const float* W, int ldw, int M, const pfsgnn_seg* segs, int nseg,

@@ -62,107 +62,140 @@ __global__ void k_sp_ptr(const int* __restrict__ keys, long long E, int n, int* 
 }
 
 // ------------------------------------------------------------ gathers
-// mode 0: out[c][e] = X[c][idx[e]];  1: out += X[c][idx[e]];
-// mode 2: out = X[c][idx[e]] * lrelu'(Z[c][e])
+// thread per position e (idx[e] read once), every channel: coalesced writes
+// out[c][e]; mode 0: = X[c][idx[e]], 1: += X[c][idx[e]], 2: = X[c][idx[e]] *
+// lrelu'(Z[c][e])
 __global__ __launch_bounds__(256) void k_gather_cols(const float* __restrict__ X, int C, int N,
                                                      const int* __restrict__ idx, long long E,
                                                      const float* __restrict__ Z, int mode,
                                                      float* __restrict__ out) {
-  const long long tot = (long long)C * E;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < tot;
-       i += (long long)gridDim.x * 256) {
-    const long long c = i / E, e = i - c * E;
-    const float v = X[c * N + idx[e]];
-    if (mode == 0) out[i] = v;
-    else if (mode == 1) out[i] += v;
-    else out[i] = v * dlrelu(Z[i]);
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < E;
+       e += (long long)gridDim.x * 256) {
+    const float* xr = X + idx[e];
+    for (int c = 0; c < C; ++c) {
+      const float v = xr[(size_t)c * N];
+      const size_t i = (size_t)c * E + e;
+      if (mode == 0) out[i] = v;
+      else if (mode == 1) out[i] += v;
+      else out[i] = v * dlrelu(Z[i]);
+    }
   }
 }
 
 // ------------------------------------------------------------ segment sums
-// block per segment: 256 threads stride over the segment's edges (fixed
-// assignment), a fixed-order LDS tree per channel (deterministic)
+// one wave per segment: lane l takes positions p0 + l, p0 + l + 64, ... and
+// keeps every channel's running sum in registers (CM >= C); a fixed DPP tree
+// per channel finishes it (deterministic).  Fiber segments are contiguous
+// runs of positions (coalesced); class segments gather through ord.
+template <int CM>
 __global__ __launch_bounds__(256) void k_segment_sum(const float* __restrict__ X, int C, long long E,
                                                      const int* __restrict__ ord,
                                                      const int* __restrict__ ptr, int act,
                                                      float* __restrict__ out, int nseg, int add) {
-  const int s = blockIdx.x, t = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= nseg) return;  // the whole wave
   const int p0 = ptr[s], p1 = ptr[s + 1];
-  __shared__ float red[256];
-  for (int c = 0; c < C; ++c) {
-    float v = 0.f;
-    for (int p = p0 + t; p < p1; p += 256) {
-      const long long e = ord ? ord[p] : p;
-      const float x = X[(long long)c * E + e];
-      v += act ? lrelu(x) : x;
-    }
-    red[t] = v;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-      if (t < w) red[t] += red[t + w];
-      __syncthreads();
-    }
-    if (t == 0) {
-      float* o = out + (long long)c * nseg + s;
-      *o = add ? *o + red[0] : red[0];
-    }
-    __syncthreads();
+  float acc[CM];
+#pragma unroll
+  for (int c = 0; c < CM; ++c) acc[c] = 0.f;
+  for (int p = p0 + lane; p < p1; p += 64) {
+    const size_t e = ord ? (size_t)ord[p] : (size_t)p;
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+      if (c < C) {
+        const float x = X[(size_t)c * E + e];
+        acc[c] += act ? lrelu(x) : x;
+      }
   }
+#pragma unroll
+  for (int c = 0; c < CM; ++c)
+    if (c < C) {
+      const float v = wave_sum(acc[c]);
+      if (lane == 0) {
+        float* o = out + (size_t)c * nseg + s;
+        *o = add ? *o + v : v;
+      }
+    }
 }
 
 // ------------------------------------------------------------ moments
-// thread per (segment, channel): mean, then the central moments over the
-// segment (two passes, double accumulation), as torch_scatter's mean (count
-// clamped at 1) and gnn.py:140-144; empty segments give mean 0, moments 0
+// one wave per fiber segment (contiguous positions): the mean, then the
+// central moments (two passes over the segment, fp32 as the reference's
+// scatter means, gnn.py:140-144); torch_scatter's mean clamps the count at 1,
+// so an empty segment gives mean 0 and moments 0
+template <int CM>
 __global__ __launch_bounds__(256) void k_segment_moments(const float* __restrict__ M, int C,
                                                          long long E,
                                                          const int* __restrict__ ptr, int nseg,
                                                          float* __restrict__ mom,
                                                          float* __restrict__ hs) {
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;  // c * nseg + s
-  const long long CN = (long long)C * nseg;
-  if (idx >= CN) return;
-  const int c = (int)(idx / nseg), s = (int)(idx - (long long)c * nseg);
+  const int lane = threadIdx.x & 63;
+  const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= nseg) return;
   const int p0 = ptr[s], p1 = ptr[s + 1];
-  const float* m = M + (long long)c * E;
-  double sum = 0.0;
-  for (int p = p0; p < p1; ++p) sum += m[p];
-  const double n = p1 > p0 ? (double)(p1 - p0) : 1.0;
-  const double mean = sum / n;
-  double s2 = 0.0, s3 = 0.0, s4 = 0.0;
-  for (int p = p0; p < p1; ++p) {
-    const double d = (double)m[p] - mean, d2 = d * d;
-    s2 += d2;
-    s3 += d2 * d;
-    s4 += d2 * d2;
-  }
-  const float c2 = (float)(s2 / n), c3 = (float)(s3 / n), c4 = (float)(s4 / n);
-  mom[idx] = (float)mean;
-  mom[CN + idx] = c2;
-  mom[2 * CN + idx] = c3;
-  mom[3 * CN + idx] = c4;
-  const float var = c2 > 0.f ? c2 : 0.01f * c2;  // F.leaky_relu (slope 0.01), gnn.py:141
-  const float sd = sqrtf(var + 1e-6f);
-  hs[idx] = (float)mean;
-  hs[CN + idx] = sd;
-  hs[2 * CN + idx] = c3 / (sd * sd * sd);
-  hs[3 * CN + idx] = c4 / ((sd * sd) * (sd * sd));
+  const float inv_n = 1.0f / (float)(p1 > p0 ? p1 - p0 : 1);
+  float mean[CM];
+#pragma unroll
+  for (int c = 0; c < CM; ++c) mean[c] = 0.f;
+  for (int p = p0 + lane; p < p1; p += 64)
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+      if (c < C) mean[c] += M[(size_t)c * E + p];
+#pragma unroll
+  for (int c = 0; c < CM; ++c)
+    if (c < C) mean[c] = wave_sum(mean[c]) * inv_n;
+  float s2[CM], s3[CM], s4[CM];
+#pragma unroll
+  for (int c = 0; c < CM; ++c) s2[c] = s3[c] = s4[c] = 0.f;
+  for (int p = p0 + lane; p < p1; p += 64)
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+      if (c < C) {
+        const float d = M[(size_t)c * E + p] - mean[c], d2 = d * d;
+        s2[c] += d2;
+        s3[c] += d2 * d;
+        s4[c] += d2 * d2;
+      }
+  const size_t CN = (size_t)C * nseg;
+#pragma unroll
+  for (int c = 0; c < CM; ++c)
+    if (c < C) {
+      const float c2 = wave_sum(s2[c]) * inv_n, c3 = wave_sum(s3[c]) * inv_n,
+                  c4 = wave_sum(s4[c]) * inv_n;
+      if (lane == 0) {
+        const size_t idx = (size_t)c * nseg + s;
+        mom[idx] = mean[c];
+        mom[CN + idx] = c2;
+        mom[2 * CN + idx] = c3;
+        mom[3 * CN + idx] = c4;
+        const float var = c2 > 0.f ? c2 : 0.01f * c2;  // F.leaky_relu (slope 0.01), gnn.py:141
+        const float sd = sqrtf(var + 1e-6f);
+        hs[idx] = mean[c];
+        hs[CN + idx] = sd;
+        hs[2 * CN + idx] = c3 / (sd * sd * sd);
+        hs[3 * CN + idx] = c4 / ((sd * sd) * (sd * sd));
+      }
+    }
 }
 
 // g_m[c][e] = C0 + d (C1 + d (C2 + d C3)), d = m - mean, per-fiber coefficients
+// (thread per position, every channel)
 __global__ __launch_bounds__(256) void k_segment_moment_grad(const float* __restrict__ M, int C,
                                                              long long E,
                                                              const int* __restrict__ seg,
                                                              const float* __restrict__ mean,
                                                              const float* __restrict__ coef,
                                                              int nseg, float* __restrict__ gm) {
-  const long long tot = (long long)C * E, CN = (long long)C * nseg;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < tot;
-       i += (long long)gridDim.x * 256) {
-    const long long c = i / E, e = i - c * E;
-    const long long j = c * nseg + seg[e];
-    const float d = M[i] - mean[j];
-    gm[i] = fmaf(d, fmaf(d, fmaf(d, coef[3 * CN + j], coef[2 * CN + j]), coef[CN + j]), coef[j]);
+  const size_t CN = (size_t)C * nseg;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < E;
+       e += (long long)gridDim.x * 256) {
+    const int sg = seg[e];
+    for (int c = 0; c < C; ++c) {
+      const size_t i = (size_t)c * E + e, j = (size_t)c * nseg + sg;
+      const float d = M[i] - mean[j];
+      gm[i] = fmaf(d, fmaf(d, fmaf(d, coef[3 * CN + j], coef[2 * CN + j]), coef[CN + j]), coef[j]);
+    }
   }
 }
 
@@ -264,18 +297,18 @@ __global__ void k_rows_bn_sums_fin(const float* __restrict__ part, int C, int S,
   Sgx[c] = b;
 }
 
-// out may alias g or y (elementwise)
+// out may alias g or y (elementwise); thread per column, every channel
 __global__ __launch_bounds__(256) void k_rows_axpby(const float* g, const float* y, int C,
                                                     long long N,
                                                     const float* __restrict__ alpha,
                                                     const float* __restrict__ gam1,
                                                     const float* __restrict__ gam0, float* out) {
-  const long long tot = (long long)C * N;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < tot;
-       i += (long long)gridDim.x * 256) {
-    const int c = (int)(i / N);
-    out[i] = fmaf(gam1[c], y[i], fmaf(alpha[c], g[i], gam0[c]));
-  }
+  for (long long n = (long long)blockIdx.x * 256 + threadIdx.x; n < N;
+       n += (long long)gridDim.x * 256)
+    for (int c = 0; c < C; ++c) {
+      const size_t i = (size_t)c * N + n;
+      out[i] = fmaf(gam1[c], y[i], fmaf(alpha[c], g[i], gam0[c]));
+    }
 }
 
 unsigned grid_of(long long n) { return (unsigned)std::max<long long>(1, std::min<long long>((n + 255) / 256, 8192)); }
@@ -342,27 +375,41 @@ extern "C" int pfsgnn_gather_cols(const float* X, int C, int N, const int* idx, 
   PF_REQUIRE(X && idx && out && C > 0 && N > 0 && E > 0 && mode >= 0 && mode <= 2 &&
                  (mode != 2 || Z),
              "pfsgnn_gather_cols", "bad arguments");
-  hipLaunchKernelGGL(k_gather_cols, dim3(grid_of((long long)C * E)), dim3(256), 0,
-                     as_stream(stream), X, C, N, idx, E, Z, mode, out);
+  hipLaunchKernelGGL(k_gather_cols, dim3(grid_of(E)), dim3(256), 0, as_stream(stream), X, C, N,
+                     idx, E, Z, mode, out);
   return pf::check_launch("pfsgnn_gather_cols");
 }
 
 extern "C" int pfsgnn_segment_sum(const float* X, int C, long long E, const int* ord,
                                   const int* ptr, int nseg, int act, float* out, int add,
                                   void* stream) {
-  PF_REQUIRE(X && ptr && out && C > 0 && E > 0 && nseg > 0, "pfsgnn_segment_sum",
-             "bad arguments");
-  hipLaunchKernelGGL(k_segment_sum, dim3(nseg), dim3(256), 0, as_stream(stream), X, C, E, ord, ptr,
-                     act, out, nseg, add);
+  PF_REQUIRE(X && ptr && out && C > 0 && C <= 64 && E > 0 && nseg > 0, "pfsgnn_segment_sum",
+             "bad arguments (C <= 64)");
+  const dim3 grid((nseg + 3) / 4);
+  hipStream_t st = as_stream(stream);
+  if (C <= 16)
+    hipLaunchKernelGGL(k_segment_sum<16>, grid, dim3(256), 0, st, X, C, E, ord, ptr, act, out, nseg, add);
+  else if (C <= 24)
+    hipLaunchKernelGGL(k_segment_sum<24>, grid, dim3(256), 0, st, X, C, E, ord, ptr, act, out, nseg, add);
+  else if (C <= 40)
+    hipLaunchKernelGGL(k_segment_sum<40>, grid, dim3(256), 0, st, X, C, E, ord, ptr, act, out, nseg, add);
+  else
+    hipLaunchKernelGGL(k_segment_sum<64>, grid, dim3(256), 0, st, X, C, E, ord, ptr, act, out, nseg, add);
   return pf::check_launch("pfsgnn_segment_sum");
 }
 
 extern "C" int pfsgnn_segment_moments(const float* M, int C, long long E, const int* ptr, int nseg,
                                       float* mom, float* hs, void* stream) {
-  PF_REQUIRE(M && ptr && mom && hs && C > 0 && E > 0 && nseg > 0, "pfsgnn_segment_moments",
-             "bad arguments");
-  hipLaunchKernelGGL(k_segment_moments, dim3(grid_of((long long)C * nseg)), dim3(256), 0,
-                     as_stream(stream), M, C, E, ptr, nseg, mom, hs);
+  PF_REQUIRE(M && ptr && mom && hs && C > 0 && C <= 32 && E > 0 && nseg > 0,
+             "pfsgnn_segment_moments", "bad arguments (C <= 32)");
+  const dim3 grid((nseg + 3) / 4);
+  hipStream_t st = as_stream(stream);
+  if (C <= 16)
+    hipLaunchKernelGGL(k_segment_moments<16>, grid, dim3(256), 0, st, M, C, E, ptr, nseg, mom, hs);
+  else if (C <= 20)
+    hipLaunchKernelGGL(k_segment_moments<20>, grid, dim3(256), 0, st, M, C, E, ptr, nseg, mom, hs);
+  else
+    hipLaunchKernelGGL(k_segment_moments<32>, grid, dim3(256), 0, st, M, C, E, ptr, nseg, mom, hs);
   return pf::check_launch("pfsgnn_segment_moments");
 }
 
@@ -371,8 +418,8 @@ extern "C" int pfsgnn_segment_moment_grad(const float* M, int C, long long E, co
                                           float* gm, void* stream) {
   PF_REQUIRE(M && seg && mean && coef && gm && C > 0 && E > 0 && nseg > 0,
              "pfsgnn_segment_moment_grad", "bad arguments");
-  hipLaunchKernelGGL(k_segment_moment_grad, dim3(grid_of((long long)C * E)), dim3(256), 0,
-                     as_stream(stream), M, C, E, seg, mean, coef, nseg, gm);
+  hipLaunchKernelGGL(k_segment_moment_grad, dim3(grid_of(E)), dim3(256), 0, as_stream(stream), M,
+                     C, E, seg, mean, coef, nseg, gm);
   return pf::check_launch("pfsgnn_segment_moment_grad");
 }
 
@@ -413,7 +460,7 @@ extern "C" int pfsgnn_rows_axpby(const float* g, const float* y, int C, long lon
                                  float* out, void* stream) {
   PF_REQUIRE(g && y && alpha && gam1 && gam0 && out && C > 0 && N > 0, "pfsgnn_rows_axpby",
              "bad arguments");
-  hipLaunchKernelGGL(k_rows_axpby, dim3(grid_of((long long)C * N)), dim3(256), 0,
-                     as_stream(stream), g, y, C, N, alpha, gam1, gam0, out);
+  hipLaunchKernelGGL(k_rows_axpby, dim3(grid_of(N)), dim3(256), 0, as_stream(stream), g, y, C, N,
+                     alpha, gam1, gam0, out);
   return pf::check_launch("pfsgnn_rows_axpby");
 }

@@ -94,6 +94,7 @@ _SIGS = {
                              ctypes.POINTER(ctypes.c_longlong)], I),
     "pfsgnn_lin": ([P, I, I, I, P, I, P, FL, I, P, I, P], I),
     "pfsgnn_lin_t": ([P, I, I, I, P, I, P, P, I, P], I),
+    "pfsgnn_lin_gather": ([P, I, I, I, P, I, P, FL, I, P, I, P, P, I, P, P, I, P], I),
     "pfsgnn_wgrad": ([P, I, P, I, I, I, P, I, P, FL, P, SZ, P], I),
     "pfsgnn_lin_cat": ([P, I, I, SEGP, I, I, P, FL, I, P, I, P], I),
     "pfsgnn_wgrad_cat": ([P, I, SEGP, I, I, I, P, I, P, FL, P, SZ, P], I),
@@ -311,6 +312,23 @@ class HipBackend:
         self._chk(W, X, b, out)
         _call("pfsgnn_lin", W.data_ptr() + 4 * col0, ldw, M, ncol, X.data_ptr(), N, _ptr(b),
               float(bscale), int(act_in), out.data_ptr(), int(add), _stream())
+        return out
+
+    def lin_gather(self, W, col0, ncol, X, gathers, b=None):
+        """W[:, col0:col0+ncol] . X + b + sum_j G_j[:, idx_j] (up to two
+        (G [M, ld], idx int32 [N]) pairs), one launch."""
+        M, ldw = W.shape
+        N = X.shape[1]
+        out = self.empty(M, N)
+        self._chk(W, X, b, out)
+        g = list(gathers) + [(None, None)] * (2 - len(gathers))
+        for G, idx in gathers:
+            self._chk(G)
+            assert idx.dtype == torch.int32 and idx.numel() == N and G.shape[0] == M
+        _call("pfsgnn_lin_gather", W.data_ptr() + 4 * col0, ldw, M, ncol, X.data_ptr(), N, _ptr(b),
+              1.0, 0, out.data_ptr(), 0, _ptr(g[0][0]), _ptr(g[0][1]),
+              0 if g[0][0] is None else g[0][0].shape[1], _ptr(g[1][0]), _ptr(g[1][1]),
+              0 if g[1][0] is None else g[1][0].shape[1], _stream())
         return out
 
     def lin_t(self, W, col0, ncol, dY, z=None, out=None, add=False):

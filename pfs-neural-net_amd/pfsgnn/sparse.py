@@ -14,10 +14,10 @@ the fused op it replaces:
   edges sorted stably by fiber, so each fiber's messages are one contiguous
   run (``fib_ptr``) and the per-fiber moments need no index;
 * the first Linear of every per-edge MLP is split as in the fused path: the
-  node parts (Ps, Pt, Qt, Rs) are gathered per edge (``pfsgnn_gather_cols``),
-  the edge-feature part is one ``pfsgnn_lin`` over E columns;
-* per-fiber and per-class sums are ``pfsgnn_segment_sum`` (block per segment,
-  fixed-order tree: bitwise reproducible);
+  edge-feature part is one ``pfsgnn_lin_gather`` over E columns whose
+  epilogue adds the node parts (Ps, Pt, Qt, Rs) gathered per edge;
+* per-fiber and per-class sums are ``pfsgnn_segment_sum`` (one wave per
+  segment, every channel in registers, fixed DPP tree: bitwise reproducible);
 * TModel's ``scatter(MLP(msg), tgt, 'sum')`` keeps the second Linear after the
   sum, with its bias scaled by each class's degree (engine.target_fwd).
 
@@ -25,6 +25,8 @@ Intermediates the fused kernels recompute in registers (z1, zs, zt) are
 recomputed here too, as [C, E] tables, so forward and backward keep the
 fused path's saved state (y, sc, sh) and nothing else per edge.
 """
+import weakref
+
 import torch
 
 
@@ -50,31 +52,43 @@ class SparseEdgeOps:
 
     def __init__(self, be):
         self.be = be
+        self._xcache = {}
 
     # ------------------------------------------------------------ helpers
     def _x(self, xe, sc, sh):
-        """The lazy edge state materialised: xe_new = sc*y + sh per channel."""
-        return xe if sc is None else self.be.affine_rows(xe, sc, sh)
+        """The lazy edge state materialised: xe_new = sc*y + sh per channel.
+        Each state is read by up to five ops of a step (S/T forward, their
+        backward, the next EdgeModel backward): it is materialised once and
+        kept while its (y, sc, sh) tensors live (weak references)."""
+        if sc is None:
+            return xe
+        key = (id(xe), id(sc), id(sh))
+        hit = self._xcache.get(key)
+        if hit is not None:
+            ry, rs, rh, x, ver = hit
+            if ry() is xe and rs() is sc and rh() is sh and ver == (xe._version, sc._version,
+                                                                    sh._version):
+                return x
+        # drop the states that died (their x would otherwise stay allocated)
+        self._xcache = {k: v for k, v in self._xcache.items()
+                        if v[0]() is not None and v[1]() is not None and v[2]() is not None}
+        x = self.be.affine_rows(xe, sc, sh)
+        self._xcache[key] = (weakref.ref(xe), weakref.ref(sc), weakref.ref(sh), x,
+                             (xe._version, sc._version, sh._version))
+        return x
 
     def _z1(self, d, x, Ps, Pt, W1):
         """EdgeModel first Linear (gnn.py:100): Ps[:, src] + Pt[:, tgt] + W1[:, 2F:3F] x."""
         be, F, sp = self.be, d.F, d.sp
-        z1 = be.lin(W1, 2 * F, F, x)
-        be.gather_cols(Ps, sp.src_p, mode=1, out=z1)
-        be.gather_cols(Pt, sp.tgt_p, mode=1, out=z1)
-        return z1
+        return be.lin_gather(W1, 2 * F, F, x, [(Ps, sp.src_p), (Pt, sp.tgt_p)])
 
     def _zs(self, d, x, Qt, Ws1):
         """SModel node_mlp_1 first Linear (gnn.py:136): Qt[:, tgt] + Ws1[:, F:2F] x."""
-        z = self.be.lin(Ws1, d.F, d.F, x)
-        self.be.gather_cols(Qt, d.sp.tgt_p, mode=1, out=z)
-        return z
+        return self.be.lin_gather(Ws1, d.F, d.F, x, [(Qt, d.sp.tgt_p)])
 
     def _zt(self, d, x, Rs, Wt1):
         """TModel node_mlp_1 first Linear (gnn.py:188): Rs[:, src] + Wt1[:, F:2F] x."""
-        z = self.be.lin(Wt1, d.F, d.F, x)
-        self.be.gather_cols(Rs, d.sp.src_p, mode=1, out=z)
-        return z
+        return self.be.lin_gather(Wt1, d.F, d.F, x, [(Rs, d.sp.src_p)])
 
     # ------------------------------------------------------------ forward
     def edge_mlp_fwd(self, d, xe, xsc, xsh, Ps, Pt, W1, W2, b2):

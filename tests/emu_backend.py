@@ -93,6 +93,12 @@ class EmuBackend:
             out.copy_(Y)
         return out
 
+    def lin_gather(self, W, col0, ncol, X, gathers, b=None):
+        Y = self.lin(W, col0, ncol, X, b=b)
+        for G, idx in gathers:
+            Y = Y + G[:, idx.long()]
+        return Y
+
     def lin_t(self, W, col0, ncol, dY, z=None, out=None, add=False):
         R = W[:, col0:col0 + ncol].t() @ dY
         if z is not None:

@@ -1,0 +1,79 @@
+"""Throughput of the general-graph path (pfsgnn.sparse) next to the fused
+complete-graph path, on the bench geometry (GPU box).
+
+The objective is a fixed random linear functional of the GNN outputs (x_s,
+x_t, x_e, u) -- train.py's loss needs complete fiber-major graphs -- and the
+step is zero_grad + GNN forward + objective + backward + FusedAdam, eager,
+synchronised around the timed steps.
+
+    python tools/sparse_bench.py [G] [NF] [NC] [B] [steps]
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "pfs-neural-net_amd")):
+    sys.path.insert(0, p)
+import torch  # noqa: E402
+
+import pfsgnn  # noqa: E402
+from pfsgnn import config  # noqa: E402
+
+G = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+NF = int(sys.argv[2]) if len(sys.argv) > 2 else 2394
+NC = int(sys.argv[3]) if len(sys.argv) > 3 else 128
+B = int(sys.argv[4]) if len(sys.argv) > 4 else 8
+STEPS = int(sys.argv[5]) if len(sys.argv) > 5 else 10
+F = 10
+config.device = torch.device("cuda")
+gen = torch.Generator().manual_seed(0)
+
+
+def edges(density):
+    if density >= 1.0:
+        e = torch.arange(G * NF * NC)
+        return torch.stack([e // NC, (e // (NF * NC)) * NC + e % NC])
+    keep = torch.rand(G, NF, NC, generator=gen) < density
+    g, f, c = torch.nonzero(keep, as_tuple=True)
+    p = torch.randperm(g.numel(), generator=gen)
+    return torch.stack([(g * NF + f)[p], (g * NC + c)[p]])
+
+
+def run(density, label):
+    torch.manual_seed(0)
+    ei = edges(density)
+    E = ei.shape[1]
+    xs = torch.arange(NF, dtype=torch.float).repeat(G).reshape(-1, 1)
+    xt = torch.cat([torch.randint(2, 13, (G * NC, 1), generator=gen).float(),
+                    torch.randint(1000, 100000, (G * NC, 1), generator=gen).float()], 1)
+    xe = 2.0 + 8.0 * torch.rand(E, F, generator=gen)
+    data = pfsgnn.BipartiteData(ei, xs, xt, xe, torch.zeros(G, F))
+    gnn = pfsgnn.GNN(B=B, Fdim=F, T=NC, F_s=1, F_t=2).cuda()
+    gnn.train()
+    opt = pfsgnn.FusedAdam(gnn.parameters(), lr=1e-4)
+    w = [torch.randn(n, F, device="cuda") * 1e-3 for n in (G * NF, G * NC, E, G)]
+
+    def step():
+        gnn.zero_grad()
+        out = gnn(data)
+        loss = ((out.x_s * w[0]).sum() + (out.x_t * w[1]).sum() + (out.x_e * w[2]).sum()
+                + (out.x_u * w[3]).sum())
+        loss.backward()
+        opt.step()
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(STEPS):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) / STEPS * 1e3
+    print(f"{label:34s} E={E:9d}  {ms:8.2f} ms/step  {E / ms / 1e3:8.1f} M edges/s", flush=True)
+
+
+dens = [float(x) for x in os.environ.get("SPARSE_DENSITIES", "1.0,0.999,0.3,0.05").split(",")]
+for dd in dens:
+    run(dd, "complete (fused edge kernels)" if dd >= 1.0 else
+        f"{100 * dd:g}% dense (general path)")
