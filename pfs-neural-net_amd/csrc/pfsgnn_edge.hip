@@ -16,6 +16,7 @@
 //     v_mfma_f32_16x16x4_f32 (exact fp32 products) with the edge as the K index.
 // Every cross-block result goes through per-block partials and a fixed-order
 // reduce, so a training step is bitwise reproducible.
+#include <cmath>
 #include "pfsgnn_common.h"
 #include "../../include/pfsgnn.h"
 #include "pfsgnn_mfma.h"
@@ -1187,11 +1188,31 @@ EdgeGeo geo_mfma(int G, int NF, int NC) {
   const long long min_ks = (NC + pfm::MAX_CPS - 1) / pfm::MAX_CPS;
   static const long long tb = [] {  // tuning knob: PFSGNN_MFMA_BLOCKS (grid target)
     const char* e = getenv("PFSGNN_MFMA_BLOCKS");
-    const long long v = e ? atoll(e) : 0;
-    return v > 0 ? v : (long long)pfm::TARGET_BLOCKS;
+    return e ? atoll(e) : 0ll;
   }();
-  const long long target = std::max<long long>(tb, groups * min_ks);
-  return make_geo(G, NF, NC, (int)std::min<long long>(target, 1ll << 30));
+  if (tb > 0)
+    return make_geo(G, NF, NC, (int)std::min<long long>(std::max(tb, groups * min_ks), 1ll << 30));
+  // Class splits near TARGET_BLOCKS, picked for the fewest idle slots in the
+  // last dispatch round: the backward kernels hold 2 blocks per CU, the forward
+  // ones 4 (registers), so a grid of nb blocks runs ceil(nb / cap) rounds at
+  // cap = 512 / 1024 and the last one may be mostly empty (2432 blocks at the
+  // bench shape: 79 % of the forward slots busy; 3040: 99 %).  Weighted by the
+  // kernels' share of the edge time (backward ~60 %).
+  auto eff = [](double nb, double cap) { return nb / cap / std::ceil(nb / cap); };
+  const long long k0 = std::max(min_ks, (pfm::TARGET_BLOCKS + groups - 1) / groups);
+  EdgeGeo best = make_geo(G, NF, NC, (int)std::min<long long>(groups * k0, 1ll << 30));
+  // (another split count only for a clear gain: more splits cost partials)
+  auto score = [&](const EdgeGeo& g) {
+    return 0.6 * eff(g.nblocks, 512.0) + 0.4 * eff(g.nblocks, 1024.0);
+  };
+  double best_s = score(best) * 1.03;
+  for (long long k = std::max(min_ks, k0 - 1); k <= k0 + 2; ++k) {
+    const EdgeGeo g = make_geo(G, NF, NC, (int)std::min<long long>(groups * k, 1ll << 30));
+    if (g.KS < min_ks || g.KS == best.KS) continue;
+    const double sc = score(g);
+    if (sc > best_s) { best_s = sc; best = g; }
+  }
+  return best;
 }
 EdgeGeo geo_for(int G, int NF, int NC) {
   return use_mfma() ? geo_mfma(G, NF, NC) : make_geo(G, NF, NC);

@@ -146,6 +146,27 @@ __device__ __forceinline__ floatx4 mma3(const Fr& a, const Fr& b, floatx4 c) {
   c = mf(a.h, b.l, c);
   return mf(a.h, b.h, c);
 }
+// the 16x16x32 form: lane (g, i) holds A[i][k = 8g + q], B[k = 8g + q][i], q = 0..7;
+// slot q of a K-tile pair is slot q & 3 of tile q >> 2, so a pair of 16x16x16
+// operands concatenates into one 16x16x32 operand with the same k <-> slot map
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 b16x8 __attribute__((ext_vector_type(8)));
+struct Fr8 {
+  s16x8 h, l;
+};
+__device__ __forceinline__ s16x8 cat8(s16x4 a, s16x4 b) {
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ Fr8 cat(const Fr& a, const Fr& b) { return {cat8(a.h, b.h), cat8(a.l, b.l)}; }
+__device__ __forceinline__ floatx4 mf8(s16x8 a, s16x8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b16x8, a),
+                                                 __builtin_bit_cast(b16x8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ floatx4 mma3w(const Fr8& a, const Fr8& b, floatx4 c) {
+  c = mf8(a.l, b.h, c);
+  c = mf8(a.h, b.l, c);
+  return mf8(a.h, b.h, c);
+}
 // bf16 1.0 in every element: B operand that sums an A image over its 16 edges
 __device__ __forceinline__ s16x4 ones16() {
   return s16x4{(short)0x3F80, (short)0x3F80, (short)0x3F80, (short)0x3F80};
@@ -161,13 +182,20 @@ __device__ __forceinline__ s16x4 ones16() {
 // split once (the same splits feed the weight-gradient images).
 template <int M, int K>
 struct LayerB3 {
-  static constexpr int MT = GM<M>::NT, KT = GM<K>::NT;
-  Fr a[MT][KT];
+  static constexpr int MT = GM<M>::NT, KT = GM<K>::NT, KP = (KT + 1) / 2;
+  // K-tile pairs on v_mfma_f32_16x16x32_bf16 (twice the K of the 16x16x16 form
+  // in the same cycles: tools/mfma_cycles.hip; pairing checked bitwise by
+  // tools/mfma_pair_check.hip); an odd last K-tile is paired with zeros.  (A
+  // 16x16x16 finishing a chain of 16x16x32s on the same accumulator gave wrong
+  // sums on gfx950 -- the edge op tests at F = 10, K = 40 -- so a chain stays
+  // on the one MFMA form.)
+  Fr8 ap[MT][KP];
   template <class Fn>
   __device__ __forceinline__ void load(Fn fn, int lane) {
     const int g = lane >> 4, i = lane & 15;
 #pragma unroll
-    for (int t = 0; t < MT; ++t)
+    for (int t = 0; t < MT; ++t) {
+      Fr a[KT];
 #pragma unroll
       for (int u = 0; u < KT; ++u) {
         floatx4 v;
@@ -176,14 +204,19 @@ struct LayerB3 {
           const int ro = GM<M>::mrow(t, i), ri = GM<K>::row(g, 4 * u + j);
           v[j] = (ro >= 0 && ri >= 0) ? fn(ro, ri) : 0.f;
         }
-        a[t][u] = split(v);
+        a[u] = split(v);
       }
+#pragma unroll
+      for (int p = 0; p < KP; ++p) ap[t][p] = cat(a[2 * p], 2 * p + 1 < KT ? a[2 * p + 1] : Fr{});
+    }
   }
   __device__ __forceinline__ void apply(const Fr (&x)[KT], floatx4 (&y)[MT]) const {
 #pragma unroll
-    for (int u = 0; u < KT; ++u)
+    for (int p = 0; p < KP; ++p) {
+      const Fr8 xp = cat(x[2 * p], 2 * p + 1 < KT ? x[2 * p + 1] : Fr{});
 #pragma unroll
-      for (int t = 0; t < MT; ++t) y[t] = mma3(a[t][u], x[u], y[t]);
+      for (int t = 0; t < MT; ++t) y[t] = mma3w(ap[t][p], xp, y[t]);
+    }
   }
 };
 
@@ -197,13 +230,15 @@ __device__ __forceinline__ s16x4 hi4(const floatx4& v) {
 }
 template <int M, int K>
 struct LayerB1 {
-  static constexpr int MT = GM<M>::NT, KT = GM<K>::NT;
-  s16x4 a[MT][KT];
+  static constexpr int MT = GM<M>::NT, KT = GM<K>::NT, KP = (KT + 1) / 2;
+  // K-tile pairs on v_mfma_f32_16x16x32_bf16, an odd last K-tile paired with zeros
+  s16x8 ap[MT][KP];
   template <class Fn>
   __device__ __forceinline__ void load(Fn fn, int lane) {
     const int g = lane >> 4, i = lane & 15;
 #pragma unroll
-    for (int t = 0; t < MT; ++t)
+    for (int t = 0; t < MT; ++t) {
+      s16x4 a[KT];
 #pragma unroll
       for (int u = 0; u < KT; ++u) {
         floatx4 v;
@@ -212,21 +247,26 @@ struct LayerB1 {
           const int ro = GM<M>::mrow(t, i), ri = GM<K>::row(g, 4 * u + j);
           v[j] = (ro >= 0 && ri >= 0) ? fn(ro, ri) : 0.f;
         }
-        a[t][u] = hi4(v);
+        a[u] = hi4(v);
       }
+#pragma unroll
+      for (int p = 0; p < KP; ++p) ap[t][p] = cat8(a[2 * p], 2 * p + 1 < KT ? a[2 * p + 1] : s16x4{});
+    }
   }
   __device__ __forceinline__ void apply(const Fr (&x)[KT], floatx4 (&y)[MT]) const {
 #pragma unroll
-    for (int u = 0; u < KT; ++u)
+    for (int p = 0; p < KP; ++p) {
+      const s16x8 xp = cat8(x[2 * p].h, 2 * p + 1 < KT ? x[2 * p + 1].h : s16x4{});
 #pragma unroll
-      for (int t = 0; t < MT; ++t) y[t] = mf(a[t][u], x[u].h, y[t]);
+      for (int t = 0; t < MT; ++t) y[t] = mf8(ap[t][p], xp, y[t]);
+    }
   }
   __device__ __forceinline__ void apply(const floatx4 (&x)[KT], floatx4 (&y)[MT]) const {
 #pragma unroll
-    for (int u = 0; u < KT; ++u) {
-      const s16x4 xb = hi4(x[u]);
+    for (int p = 0; p < KP; ++p) {
+      const s16x8 xp = cat8(hi4(x[2 * p]), 2 * p + 1 < KT ? hi4(x[2 * p + 1]) : s16x4{});
 #pragma unroll
-      for (int t = 0; t < MT; ++t) y[t] = mf(a[t][u], xb, y[t]);
+      for (int t = 0; t < MT; ++t) y[t] = mf8(ap[t][p], xp, y[t]);
     }
   }
 };

@@ -18,7 +18,8 @@ Code paths reached (asserted below through ``pfsgnn_edge_grid``, MFMA path):
     in-place segment reduction (pfsgnn_node.hip k_reduce_seg);
   * 2394x16, G=1: KS = 4, 152 blocks (single-stage reduction);
   * 2394x16, G=256: KS = 1 (per-fiber outputs written directly), 9728 blocks;
-  * 2394x128, G=16 (the bench batch): KS = 4, 2432 blocks.
+  * 2394x128, G=16 (the bench batch): KS = 5, 3040 blocks (the split count
+    that fills the last dispatch round, geo_mfma).
 """
 import copy
 
@@ -112,7 +113,7 @@ def _run(gnn, parts, noiselevel=0.3):
 
 
 @pytest.mark.parametrize("G,NC,grid", [(256, 16, dict(KS=1, nblocks=9728)),
-                                       (16, 128, dict(KS=4, nblocks=2432))])
+                                       (16, 128, dict(KS=5, nblocks=3040))])
 def test_full_size_step_finite_and_repeatable(G, NC, grid):
     import pfsgnn
     pfsgnn.set_edge_path("mfma")
