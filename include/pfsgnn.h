@@ -284,6 +284,27 @@ int pfsgnn_rms2_fwd(const float* X, int C, int G, const float* w, float eps,
 int pfsgnn_rms2_bwd(const float* dY, const float* X, const float* w, const float* y1,
                     const float* r1, const float* r2, int C, int G, float eps,
                     float* dX, float* dw, void* ws, size_t ws_bytes, void* stream);
+/* The whole GlobalModel (gnn.py:208-223) in one call (a wide means launch,
+ * then a block per graph): means[c][g] / means[F + c][g] = per-graph means of xs / xt
+ * (n1 / n2 nodes per graph), Z [H][G] = W1 [u; means] + b1, V [F][G] =
+ * W2 lrelu(Z) + b2 (the MLP, W1 [H][3F], W2 [F][H]), Y = RMSNorm applied
+ * twice with weight w (y1, r1, r2 saved as pfsgnn_rms2_fwd); w == NULL: Y = V
+ * (unnormed).  3F, H <= 192.  Two launches for graph_mean2 + mlp + rms2_fwd. */
+int pfsgnn_global_fwd(const float* xs, int n1, const float* xt, int n2, const float* u, int F,
+                      int G, const float* W1, int H, const float* b1, const float* W2,
+                      const float* b2, const float* w, float eps, float* means, float* Z, float* V,
+                      float* Y, float* y1, float* r1, float* r2, void* stream);
+/* Its backward (train.py:140's autograd through gnn.py:218-223): gV [F][G] =
+ * d loss / d V, dZ [H][G] = d loss / d Z (both kept for the weight gradients),
+ * dwp [F][G] the per-graph RMSNorm weight gradient (the caller sums over g),
+ * gU [F][G] += d loss / d u, gm [2F][G] = d loss / d means, then
+ * gxs[c][g*n1 + i] += s1 * gm[c][g], gxt[c][g*n2 + i] += s2 * gm[F + c][g]
+ * (s = 1/n for the mean).  Two launches. */
+int pfsgnn_global_bwd(const float* dY, const float* V, const float* w, const float* y1,
+                      const float* r1, const float* r2, int F, int G, const float* Z, int H,
+                      const float* W1, const float* W2, float* gV, float* dZ, float* dwp,
+                      float* gU, float* gm, float* gxs, int n1, float s1, float* gxt, int n2,
+                      float s2, void* stream);
 /* EdgeModel's BatchNorm applied twice (gnn.py:101): from the batch moments
  * (mu1, var1) of y give xe_new = sc*y + sh; updates running stats twice. */
 int pfsgnn_bn2_finalize(const float* mu1, const float* var1, const float* gamma,
@@ -394,28 +415,33 @@ int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, const float*
                       const float* bs2, float* mom, float* hs, void* ws, size_t ws_bytes,
                       void* stream);
 /* TModel per-edge message, summed per class before its second Linear
- * (gnn.py:188-190): hsum[:,c] = sum_f lrelu(Rs[:,f] + Wt1[:,F:2F] x). */
+ * (gnn.py:188-190): hsum[:,c] = sum_f lrelu(Rs[:,f] + Wt1[:,F:2F] x); with Wt2
+ * (optional, [2F][2F]) also that Linear in the same call's reduction epilogue:
+ * agg[:,c] = Wt2 hsum[:,c] + bscale*bt2. */
 int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                       const float* sh, const float* Rs, const float* Wt1, float* hsum,
+                      const float* Wt2, const float* bt2, float bscale, float* agg,
                       void* ws, size_t ws_bytes, void* stream);
 /* TModel edge backward: GzT[:,f] = sum_c g_z; dWt1[:,F:2F] += sum g_z x^T;
- * optional gxe = Wt1[:,F:2F]^T g_z (standalone TModel only). */
+ * optional gxe = Wt1[:,F:2F]^T g_z (standalone TModel only); optional g_xs
+ * += Wt1[:,0:F]^T GzT (the x_s[src] input gradient, in the reduction epilogue). */
 int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                       const float* sh, const float* Rs, const float* Wt1, const float* g_hsum,
-                      float* GzT, float* dWt1, float* gxe, void* ws, size_t ws_bytes,
-                      void* stream);
+                      float* GzT, float* dWt1, float* gxe, float* g_xs, void* ws,
+                      size_t ws_bytes, void* stream);
 /* SModel edge backward fused with TModel's per-edge input gradient, the
  * downstream edge gradient and the edge BatchNorm's two gradient sums:
  * g_tot = Ws1e^T g_zs + [Wt1e^T g_zt] + [g_next]; GzS per class;
  * dWs1[:,F:2F], dWs2, dbs2 accumulated; Sg/Sgx = sums of g_tot, g_tot*xhat
- * (xhat = (y-mu1)*inv1) when mu1 != NULL.  Rs/Wt1/g_hsum may be NULL. */
+ * (xhat = (y-mu1)*inv1) when mu1 != NULL.  Rs/Wt1/g_hsum may be NULL.
+ * Optional g_xt += Ws1[:,0:F]^T GzS (x_t[tgt] input gradient, reduction epilogue). */
 int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                       const float* sh, const float* Qt, const float* Ws1, const float* Ws2,
                       const float* bs2, const float* mean, const float* coef, const float* Rs,
                       const float* Wt1, const float* g_hsum, const float* g_next,
                       const float* mu1, const float* inv1, float* g_tot, float* GzS,
                       float* dWs1, float* dWs2, float* dbs2, float* Sg, float* Sgx,
-                      void* ws, size_t ws_bytes, void* stream);
+                      float* g_xt, void* ws, size_t ws_bytes, void* stream);
 /* the same with the edge BatchNorm's backward finished in the same call: in
  * place of Sg / Sgx it writes pfsgnn_bn2_bwd_coef's alpha, gam0, gam1 and
  * accumulates dgamma / dbeta (gamma, var1: that BatchNorm's weight and batch
@@ -427,21 +453,24 @@ int pfsgnn_source_bwd_bn(int G, int NF, int NC, int F, const float* y, const flo
                          const float* mu1, const float* inv1, const float* var1,
                          const float* gamma, long long n, float eps, float* g_tot, float* GzS,
                          float* dWs1, float* dWs2, float* dbs2, float* alpha, float* gam0,
-                         float* gam1, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
-                         void* stream);
+                         float* gam1, float* dgamma, float* dbeta, float* g_xt, void* ws,
+                         size_t ws_bytes, void* stream);
 /* Sg = sum g, Sgx = sum g*(y-mu1)*inv1 (standalone EdgeModel backward). */
 int pfsgnn_edge_bn_grad_sums(int G, int NF, int NC, int F, const float* g, const float* y,
                              const float* mu1, const float* inv1, float* Sg, float* Sgx,
                              void* ws, size_t ws_bytes, void* stream);
 /* EdgeModel per-edge MLP backward.  g_y = alpha*g_tot + gam0 + gam1*y;
  * gxe (optional) = W1[:,2F:3F]^T g_z1; GzEs [4F][NS], GzEt [4F][NT] are
- * the per-fiber / per-class sums of g_z1; dW1[:,2F:3F], dW2, db2 accumulated. */
+ * the per-fiber / per-class sums of g_z1; dW1[:,2F:3F], dW2, db2 accumulated.
+ * Optional, in the reductions' epilogues (gnn.py:100's node-input gradients):
+ * g_xs += W1[:,0:F]^T GzEs, g_xt += W1[:,F:2F]^T GzEt, Vu [F][NT] =
+ * W1[:,3F:4F]^T GzEt (the caller sums it per graph into g_u). */
 int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_tot, const float* alpha,
                         const float* gam0, const float* gam1, const float* y, const float* xe,
                         const float* xsc, const float* xsh, const float* Ps, const float* Pt,
                         const float* W1, const float* W2, float* dW1, float* dW2, float* db2,
-                        float* gxe, float* GzEs, float* GzEt, void* ws, size_t ws_bytes,
-                        void* stream);
+                        float* gxe, float* GzEs, float* GzEt, float* g_xs, float* g_xt,
+                        float* Vu, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- loss
  * train.py:29-80: decoder_e (gnn.py:307) + softplus + softfloor (train.py:21)

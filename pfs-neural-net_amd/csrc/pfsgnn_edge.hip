@@ -1104,6 +1104,160 @@ __global__ void k_reduce_fiber(const float* __restrict__ part, int KS, long long
   out[idx] = s;
 }
 
+// A linear epilogue of a node-side reduction: for every node q of the reduced
+// C-row table S, out[k][q] (+)= sum_i Wk(k, i) S[i][q] (+ bscale b[k]), k < nk,
+// with Wk(k, i) = W[i*ldw + k] (trans: a lin_t, the node-input gradient of a
+// first Linear's column block) or W[k*ldw + i] (a lin).  It replaces the
+// separate pfsgnn_lin / _lin_t launch that used to follow the reduction.
+struct NodeLin {
+  const float* W;  // nullptr: no epilogue
+  int ldw, trans, nk, add;
+  const float* b;
+  float bscale;
+  float* out;
+  long long ldo;
+};
+
+// The epilogues' weight blocks staged in LDS as ws[e][k][i] = Wk(k, i) (k < nk
+// <= NL_MAXK): issued before the partial sums, so their latency overlaps them.
+#define NL_MAXK 32
+template <int C>
+__device__ __forceinline__ void stage_lin(const NodeLin& L0, const NodeLin& L1, float* ws) {
+  for (int e = 0; e < 2; ++e) {
+    const NodeLin& L = e ? L1 : L0;
+    if (!L.W) continue;
+    for (int idx = threadIdx.x; idx < L.nk * C; idx += blockDim.x) {
+      const int k = idx / C, i = idx - k * C;
+      ws[e * NL_MAXK * C + idx] =
+          L.trans ? L.W[(size_t)i * L.ldw + k] : L.W[(size_t)k * L.ldw + i];
+    }
+  }
+}
+
+// sum KS per-fiber partials [KS][C][NS] -> out[C][NS] (in k order, as
+// k_reduce_fiber; KS == 1: out is the input and only the epilogues run), + up
+// to two epilogues.  A block owns 64 fibers (lane = fiber, coalesced rows);
+// wave w sums channels w, w+4, ...; the epilogues read the block's sums and
+// the staged weights from LDS.
+template <int C>
+__global__ __launch_bounds__(256) void k_reduce_fiber_lin(const float* __restrict__ part, int KS,
+                                                          long long NS, float* __restrict__ out,
+                                                          NodeLin L0, NodeLin L1) {
+  static_assert(C % 4 == 0, "C must be a multiple of 4");
+  constexpr int CPW = C / 4;
+  __shared__ float res[C][65];
+  __shared__ float ws[2 * NL_MAXK * C];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const long long n0 = (long long)blockIdx.x * 64, n = n0 + lane;
+  const bool v = n < NS;
+  const long long nc = v ? n : NS - 1;   // clamped: every load unconditional
+  const long long len = (long long)C * NS;
+  stage_lin<C>(L0, L1, ws);
+  float a[CPW];
+#pragma unroll
+  for (int j = 0; j < CPW; ++j) a[j] = 0.f;
+  for (int k = 0; k < KS; ++k) {
+    float x[CPW];
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) x[j] = part[(size_t)k * len + (size_t)(w + 4 * j) * NS + nc];
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) a[j] += x[j];
+  }
+#pragma unroll
+  for (int j = 0; j < CPW; ++j) {
+    const int c = w + 4 * j;
+    res[c][lane] = a[j];
+    if (v && KS > 1) out[(size_t)c * NS + n] = a[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const NodeLin& L = e ? L1 : L0;
+    if (!L.W) continue;
+    const float* wk = ws + e * NL_MAXK * C;
+    for (int idx = t; idx < 64 * L.nk; idx += 256) {
+      const int k = idx >> 6, o = idx & 63;
+      if (n0 + o >= NS) continue;
+      float acc = L.b ? L.bscale * L.b[k] : 0.f;
+#pragma unroll
+      for (int i = 0; i < C; ++i) acc = fmaf(wk[k * C + i], res[i][o], acc);
+      float* op = L.out + (size_t)k * L.ldo + n0 + o;
+      *op = L.add ? *op + acc : acc;
+    }
+  }
+}
+
+// per-class sums over the BPG fiber groups of each graph, bitwise as
+// k_reduce_columns (out[i][g*NC + c] = sum_b part[((g*BPG + b)*NC + c)*C + i]:
+// 16 partial lanes per output, two accumulators each, fixed-order combine), for
+// 4 whole classes per block, + up to two epilogues on those classes' columns
+template <int C>
+__global__ __launch_bounds__(256) void k_reduce_columns_lin(const float* __restrict__ part, int G,
+                                                            int BPG, int NC,
+                                                            float* __restrict__ out, NodeLin L0,
+                                                            NodeLin L1) {
+  constexpr int CPB = 4, NO = CPB * C, NP = NO / 16;   // outputs, 16-output passes
+  static_assert(NO % 16 == 0, "4C must be a multiple of 16");
+  __shared__ float sh[NP][16][17];
+  __shared__ float res[NO];
+  __shared__ float ws[2 * NL_MAXK * C];
+  const int t = threadIdx.x, o = t & 15, pl = t >> 4;
+  const long long NT = (long long)G * NC, q0 = (long long)blockIdx.x * CPB;
+  stage_lin<C>(L0, L1, ws);
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int idx = p * 16 + o, cl = idx / C, i = idx - cl * C;
+    const long long q = min(q0 + cl, NT - 1);   // clamped: loads unconditional
+    const long long g = q / NC, c = q - g * NC;
+    const float* pp = part + ((size_t)g * BPG * NC + c) * C + i;
+    float s0 = 0.f, s1 = 0.f;
+    int b = pl;
+    for (; b + 16 < BPG; b += 32) {
+      s0 += pp[(size_t)b * NC * C];
+      s1 += pp[(size_t)(b + 16) * NC * C];
+    }
+    if (b < BPG) s0 += pp[(size_t)b * NC * C];
+    sh[p][pl][o] = s0 + s1;
+  }
+  __syncthreads();
+  for (int idx = t; idx < NO; idx += 256) {
+    const int p = idx >> 4, oo = idx & 15;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += sh[p][k][oo];
+    res[idx] = s;
+    const int cl = idx / C, i = idx - cl * C;
+    if (q0 + cl < NT) out[(size_t)i * NT + q0 + cl] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const NodeLin& L = e ? L1 : L0;
+    if (!L.W) continue;
+    const float* wk = ws + e * NL_MAXK * C;
+    for (int idx = t; idx < CPB * L.nk; idx += 256) {
+      const int k = idx / CPB, cl = idx - k * CPB;
+      const long long q = q0 + cl;
+      if (q >= NT) continue;
+      float acc = L.b ? L.bscale * L.b[k] : 0.f;
+#pragma unroll
+      for (int i = 0; i < C; ++i) acc = fmaf(wk[k * C + i], res[cl * C + i], acc);
+      float* op = L.out + (size_t)k * L.ldo + q;
+      *op = L.add ? *op + acc : acc;
+    }
+  }
+}
+
+#define DISPATCH_C(C, ...)                                            \
+  switch (C) {                                                        \
+    case 16: { constexpr int CC = 16; __VA_ARGS__; } break;           \
+    case 20: { constexpr int CC = 20; __VA_ARGS__; } break;           \
+    case 32: { constexpr int CC = 32; __VA_ARGS__; } break;           \
+    case 40: { constexpr int CC = 40; __VA_ARGS__; } break;           \
+    case 64: { constexpr int CC = 64; __VA_ARGS__; } break;           \
+    default: return pf::fail("dispatch", "unsupported node width");   \
+  }
+
 // per-class node table [C][NT] -> class-major rows [NT][C] (scalar-loadable)
 __global__ void k_class_rows(const float* __restrict__ src, int C, long long NT,
                              float* __restrict__ dst) {
@@ -1172,6 +1326,37 @@ void fiber_finish(const EdgeGeo& geo, int C, const float* dst, float* out, hipSt
   const long long len = (long long)C * geo.NS;
   hipLaunchKernelGGL(k_reduce_fiber, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, st, dst,
                      geo.KS, len, out);
+}
+
+// the reductions with their linear epilogues (NodeLin); no epilogue: the plain
+// reductions above
+NodeLin no_lin() { return NodeLin{nullptr, 0, 0, 0, 0, nullptr, 0.f, nullptr, 0}; }
+NodeLin lin_t_add(const float* W, int ldw, int col0, int nk, float* out, long long ldo) {
+  return NodeLin{W ? W + col0 : nullptr, ldw, 1, nk, 1, nullptr, 0.f, out, ldo};
+}
+int fiber_finish_lin(const EdgeGeo& geo, int C, const float* dst, float* out, const NodeLin& L0,
+                     const NodeLin& L1, hipStream_t st) {
+  if (L0.nk > NL_MAXK || L1.nk > NL_MAXK) return pf::fail("fiber_finish_lin", "nk > 32");
+  if (!L0.W && !L1.W) {
+    fiber_finish(geo, C, dst, out, st);
+    return 0;
+  }
+  const float* src = geo.KS == 1 ? out : dst;
+  DISPATCH_C(C, hipLaunchKernelGGL(k_reduce_fiber_lin<CC>, dim3((unsigned)((geo.NS + 63) / 64)),
+                                   dim3(256), 0, st, src, geo.KS, geo.NS, out, L0, L1));
+  return 0;
+}
+int columns_lin(const float* part, int G, int BPG, int NC, int C, float* out, const NodeLin& L0,
+                const NodeLin& L1, hipStream_t st) {
+  if (L0.nk > NL_MAXK || L1.nk > NL_MAXK) return pf::fail("columns_lin", "nk > 32");
+  if (!L0.W && !L1.W) {
+    launch_reduce_columns(part, G, BPG, NC, C, out, st);
+    return 0;
+  }
+  DISPATCH_C(C, hipLaunchKernelGGL(k_reduce_columns_lin<CC>,
+                                   dim3((unsigned)(((long long)G * NC + 3) / 4)), dim3(256), 0,
+                                   st, part, G, BPG, NC, out, L0, L1));
+  return 0;
 }
 
 int g_path = PFSGNN_EDGE_MFMA;
@@ -1355,6 +1540,7 @@ extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, c
 
 extern "C" int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                                  const float* sh, const float* Rs, const float* Wt1, float* hsum,
+                                 const float* Wt2, const float* bt2, float bscale, float* agg,
                                  void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_target_fwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(y && Rs && Wt1 && hsum, "pfsgnn_target_fwd", "null");
@@ -1371,14 +1557,18 @@ extern "C" int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, c
                                    sc, sh, Rs, Wt1, part));
   }
   tm_.end(); }
-  launch_reduce_columns(part, G, geo.NFG, NC, 2 * F, hsum, st);
+  PF_REQUIRE(!Wt2 || agg, "pfsgnn_target_fwd", "Wt2 needs agg");
+  // agg = Wt2 hsum + bscale bt2 (gnn.py:188-190, the second Linear after the sum)
+  const NodeLin La = Wt2 ? NodeLin{Wt2, 2 * F, 0, 2 * F, 0, bt2, bscale, agg, (long long)G * NC}
+                         : no_lin();
+  if (int rc = columns_lin(part, G, geo.NFG, NC, 2 * F, hsum, La, no_lin(), st)) return rc;
   return pf::check_launch("pfsgnn_target_fwd");
 }
 
 extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                                  const float* sh, const float* Rs, const float* Wt1,
                                  const float* g_hsum, float* GzT, float* dWt1, float* gxe,
-                                 void* ws, size_t ws_bytes, void* stream) {
+                                 float* g_xs, void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_target_bwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(y && Rs && Wt1 && g_hsum && GzT && dWt1, "pfsgnn_target_bwd", "null");
   const EdgeGeo geo = geo_for(G, NF, NC);
@@ -1400,7 +1590,11 @@ extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, c
                                    sc, sh, Rs, Wt1, ghT, gz, gxe, part));
   }
   tm_.end(); }
-  fiber_finish(geo, C, gz, GzT, st);
+  // g_xs += Wt1[:, 0:F]^T GzT (gnn.py:188, the x_s[src] input gradient)
+  if (int rc = fiber_finish_lin(geo, C, gz, GzT, lin_t_add(g_xs ? Wt1 : nullptr, 2 * F, 0, F, g_xs,
+                                                           geo.NS),
+                                no_lin(), st))
+    return rc;
   const RedDesc rd{part, geo.nblocks, (size_t)C * F, F, C, F, dWt1 + F, C, 1, 1.f};
   if (defer) pf::defer_push(&rd, 1);
   else launch_reduce_multi(&rd, 1, st);
@@ -1453,7 +1647,7 @@ static int source_bwd_impl(int G, int NF, int NC, int F, const float* y, const f
                            const float* Wt1, const float* g_hsum, const float* g_next,
                            const float* mu1, const float* inv1, float* g_tot, float* GzS,
                            float* dWs1, float* dWs2, float* dbs2, float* Sg, float* Sgx,
-                           const Bn2Bwd* bb, void* ws, size_t ws_bytes, void* stream);
+                           const Bn2Bwd* bb, float* g_xt, void* ws, size_t ws_bytes, void* stream);
 
 extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                                  const float* sh, const float* Qt, const float* Ws1,
@@ -1461,11 +1655,11 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
                                  const float* coef, const float* Rs, const float* Wt1,
                                  const float* g_hsum, const float* g_next, const float* mu1,
                                  const float* inv1, float* g_tot, float* GzS, float* dWs1,
-                                 float* dWs2, float* dbs2, float* Sg, float* Sgx, void* ws,
-                                 size_t ws_bytes, void* stream) {
+                                 float* dWs2, float* dbs2, float* Sg, float* Sgx, float* g_xt,
+                                 void* ws, size_t ws_bytes, void* stream) {
   return source_bwd_impl(G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, g_hsum,
-                         g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, Sg, Sgx, nullptr, ws,
-                         ws_bytes, stream);
+                         g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, Sg, Sgx, nullptr, g_xt,
+                         ws, ws_bytes, stream);
 }
 
 extern "C" int pfsgnn_source_bwd_bn(int G, int NF, int NC, int F, const float* y, const float* sc,
@@ -1476,14 +1670,14 @@ extern "C" int pfsgnn_source_bwd_bn(int G, int NF, int NC, int F, const float* y
                                     const float* inv1, const float* var1, const float* gamma,
                                     long long n, float eps, float* g_tot, float* GzS, float* dWs1,
                                     float* dWs2, float* dbs2, float* alpha, float* gam0,
-                                    float* gam1, float* dgamma, float* dbeta, void* ws,
-                                    size_t ws_bytes, void* stream) {
+                                    float* gam1, float* dgamma, float* dbeta, float* g_xt,
+                                    void* ws, size_t ws_bytes, void* stream) {
   PF_REQUIRE(mu1 && inv1 && var1 && gamma && n > 0 && alpha && gam0 && gam1 && dgamma && dbeta,
              "pfsgnn_source_bwd_bn", "null");
   const Bn2Bwd bb{gamma, mu1, var1, n, eps, alpha, gam0, gam1, dgamma, dbeta};
   return source_bwd_impl(G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, g_hsum,
                          g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, nullptr, nullptr, &bb,
-                         ws, ws_bytes, stream);
+                         g_xt, ws, ws_bytes, stream);
 }
 
 static int source_bwd_impl(int G, int NF, int NC, int F, const float* y, const float* sc,
@@ -1492,7 +1686,7 @@ static int source_bwd_impl(int G, int NF, int NC, int F, const float* y, const f
                            const float* Wt1, const float* g_hsum, const float* g_next,
                            const float* mu1, const float* inv1, float* g_tot, float* GzS,
                            float* dWs1, float* dWs2, float* dbs2, float* Sg, float* Sgx,
-                           const Bn2Bwd* bb, void* ws, size_t ws_bytes, void* stream) {
+                           const Bn2Bwd* bb, float* g_xt, void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_source_bwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(y && Qt && Ws1 && Ws2 && bs2 && mean && coef && g_tot && GzS && dWs1 && dWs2 && dbs2,
              "pfsgnn_source_bwd", "null");
@@ -1547,7 +1741,11 @@ static int source_bwd_impl(int G, int NF, int NC, int F, const float* y, const f
       hipLaunchKernelGGL(k_bn2_coef_part, dim3(F), dim3(256), 0, st, pBN, (int)nb, F, *bb, Sg,
                          Sgx);
   }
-  launch_reduce_columns(pCol, G, geo.NFG, NC, C, GzS, st);
+  // g_xt += Ws1[:, 0:F]^T GzS (gnn.py:136, the x_t[tgt] input gradient)
+  if (int rc = columns_lin(pCol, G, geo.NFG, NC, C, GzS,
+                           lin_t_add(g_xt ? Ws1 : nullptr, 2 * F, 0, F, g_xt, geo.NT), no_lin(),
+                           st))
+    return rc;
   return pf::check_launch("pfsgnn_source_bwd");
 }
 
@@ -1579,7 +1777,8 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
                                    const float* y, const float* xe, const float* xsc,
                                    const float* xsh, const float* Ps, const float* Pt,
                                    const float* W1, const float* W2, float* dW1, float* dW2,
-                                   float* db2, float* gxe, float* GzEs, float* GzEt, void* ws,
+                                   float* db2, float* gxe, float* GzEs, float* GzEt,
+                                   float* g_xs, float* g_xt, float* Vu, void* ws,
                                    size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_edge_mlp_bwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(g_tot && alpha && gam0 && gam1 && y && xe && Ps && Pt && W1 && W2 && dW1 && dW2 &&
@@ -1613,7 +1812,13 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
                                    gs, pW2, pW1, pCol));
   tm_.end(); }
   }
-  fiber_finish(geo, H, gs, GzEs, st);
+  // node-input gradients of the first Linear (gnn.py:100): g_xs += W1[:, 0:F]^T GzEs,
+  // g_xt += W1[:, F:2F]^T GzEt, and Vu = W1[:, 3F:4F]^T GzEt per class (the
+  // caller sums it per graph into g_u)
+  if (int rc = fiber_finish_lin(geo, H, gs, GzEs,
+                                lin_t_add(g_xs ? W1 : nullptr, 4 * F, 0, F, g_xs, geo.NS),
+                                no_lin(), st))
+    return rc;
   {
     RedDesc rd[3] = {{pW2, (int)nb, (size_t)F * (H + 1), H + 1, F, H, dW2, H, 1, 1.f},
                      {pW2 + H, (int)nb, (size_t)F * (H + 1), H + 1, F, 1, db2, 1, 1, 1.f},
@@ -1621,6 +1826,10 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
     if (defer) pf::defer_push(rd, 3);
     else launch_reduce_multi(rd, 3, st);
   }
-  launch_reduce_columns(pCol, G, geo.NFG, NC, H, GzEt, st);
+  NodeLin Lu = lin_t_add(Vu ? W1 : nullptr, 4 * F, 3 * F, F, Vu, geo.NT);
+  Lu.add = 0;
+  if (int rc = columns_lin(pCol, G, geo.NFG, NC, H, GzEt,
+                           lin_t_add(g_xt ? W1 : nullptr, 4 * F, F, F, g_xt, geo.NT), Lu, st))
+    return rc;
   return pf::check_launch("pfsgnn_edge_mlp_bwd");
 }

@@ -1573,6 +1573,166 @@ extern "C" int pfsgnn_rms2_bwd(const float* dY, const float* X, const float* w, 
   return pf::check_launch("pfsgnn_rms2_bwd");
 }
 
+// ---------------------------------------------------------------- GlobalModel, fused
+// GlobalModel (gnn.py:208-223): the node means (gnn.py:218-219) by the wide
+// k_graph_mean2, then one block per graph does the MLP(3F -> H -> F) on
+// [u, mean x_s, mean x_t] and the double RMSNorm (the arithmetic of k_rms2_fwd,
+// serial over the F features): two launches for what was mean2 + mlp + rms2.
+constexpr int GL_MAXK = 192;  // 3F and H <= 192 (F <= 64)
+__global__ __launch_bounds__(256) void k_global_fwd(
+    const float* __restrict__ xs, int n1, const float* __restrict__ xt, int n2,
+    const float* __restrict__ u, int F, int G, const float* __restrict__ W1, int H,
+    const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
+    const float* __restrict__ w, float eps, float* __restrict__ means, float* __restrict__ Z,
+    float* __restrict__ V, float* __restrict__ Y, float* __restrict__ y1,
+    float* __restrict__ r1, float* __restrict__ r2) {
+  __shared__ float h[GL_MAXK], z[GL_MAXK], v[GL_MAXK];
+  const int g = blockIdx.x, t = threadIdx.x;
+  const int K = 3 * F;
+  (void)xs; (void)xt; (void)n1; (void)n2;
+  if (t < F) h[t] = u[(size_t)t * G + g];
+  else if (t < K) h[t] = means[(size_t)(t - F) * G + g];
+  __syncthreads();
+  for (int j = t; j < H; j += 256) {
+    float acc = b1[j];
+    for (int k = 0; k < K; ++k) acc = fmaf(W1[(size_t)j * K + k], h[k], acc);
+    z[j] = acc;
+    Z[(size_t)j * G + g] = acc;
+  }
+  __syncthreads();
+  for (int o = t; o < F; o += 256) {
+    float acc = b2[o];
+    for (int j = 0; j < H; ++j) acc = fmaf(W2[(size_t)o * H + j], lrelu(z[j]), acc);
+    v[o] = acc;
+    V[(size_t)o * G + g] = acc;
+  }
+  __syncthreads();
+  if (!w) {  // unnormed GNN: u_new = v
+    if (t < F) Y[(size_t)t * G + g] = v[t];
+    return;
+  }
+  if (t == 0) {
+    float s = 0.f;
+    for (int c = 0; c < F; ++c) s += v[c] * v[c];
+    const float a = rsqrtf(s / F + eps);
+    float s2 = 0.f;
+    for (int c = 0; c < F; ++c) {
+      const float q = v[c] * a * w[c];
+      h[c] = q;
+      y1[(size_t)c * G + g] = q;
+      s2 += q * q;
+    }
+    const float b = rsqrtf(s2 / F + eps);
+    for (int c = 0; c < F; ++c) Y[(size_t)c * G + g] = h[c] * b * w[c];
+    r1[g] = a;
+    r2[g] = b;
+  }
+}
+
+// Its backward, one block per graph: the double RMSNorm backward (k_rms2_bwd's
+// arithmetic; dw per graph into dwp [F][G], summed by the caller), then
+// dZ = (W2^T gV) lrelu'(Z), dh = W1^T dZ, gU += dh[0:F], gm = dh[F:3F]; the
+// wide k_graph_bcast_add2 then broadcasts gm over the graphs' nodes (gnn.py:
+// 218-219).  Two launches for rms2_bwd + reduce + mlp_bwd + graph_bcast_add2.
+__global__ __launch_bounds__(256) void k_global_bwd(
+    const float* __restrict__ dY, const float* __restrict__ V, const float* __restrict__ w,
+    const float* __restrict__ y1, const float* __restrict__ r1, const float* __restrict__ r2,
+    int F, int G, const float* __restrict__ Z, int H, const float* __restrict__ W1,
+    const float* __restrict__ W2, float* __restrict__ gV, float* __restrict__ dZ,
+    float* __restrict__ dwp, float* __restrict__ gU, float* __restrict__ gm) {
+  __shared__ float gv[GL_MAXK], dz[GL_MAXK], dh[GL_MAXK], d1[GL_MAXK];
+  __shared__ float sdy[GL_MAXK], sy1[GL_MAXK], sv[GL_MAXK], sw[GL_MAXK], sdw[GL_MAXK];
+  const int g = blockIdx.x, t = threadIdx.x;
+  const int K = 3 * F;
+  // the graph's vectors staged in parallel; the serial RMSNorm math reads LDS
+  if (t < F) {
+    sdy[t] = dY[(size_t)t * G + g];
+    if (w) {
+      sy1[t] = y1[(size_t)t * G + g];
+      sv[t] = V[(size_t)t * G + g];
+      sw[t] = w[t];
+    }
+  }
+  __syncthreads();
+  if (!w) {
+    if (t < F) gv[t] = sdy[t];
+  } else if (t == 0) {
+    const float a = r1[g], b = r2[g];
+    float dot = 0.f;
+    for (int c = 0; c < F; ++c) {
+      const float dy = sdy[c], x = sy1[c];
+      sdw[c] = dy * x * b;
+      dot += dy * sw[c] * x;
+    }
+    float dot2 = 0.f;
+    for (int c = 0; c < F; ++c) {
+      const float dy = sdy[c], x1 = sy1[c];
+      const float q = b * dy * sw[c] - x1 * b * b * b * dot / F;
+      d1[c] = q;
+      const float x0 = sv[c];
+      sdw[c] += q * x0 * a;
+      dot2 += q * sw[c] * x0;
+    }
+    for (int c = 0; c < F; ++c) {
+      const float x0 = sv[c];
+      gv[c] = a * d1[c] * sw[c] - x0 * a * a * a * dot2 / F;
+    }
+  }
+  __syncthreads();
+  if (w && t < F) dwp[(size_t)t * G + g] = sdw[t];
+  if (t < F) gV[(size_t)t * G + g] = gv[t];
+  for (int j = t; j < H; j += 256) {
+    float acc = 0.f;
+    for (int o = 0; o < F; ++o) acc = fmaf(W2[(size_t)o * H + j], gv[o], acc);
+    const float q = acc * dlrelu(Z[(size_t)j * G + g]);
+    dz[j] = q;
+    dZ[(size_t)j * G + g] = q;
+  }
+  __syncthreads();
+  for (int k = t; k < K; k += 256) {
+    float acc = 0.f;
+    for (int j = 0; j < H; ++j) acc = fmaf(W1[(size_t)j * K + k], dz[j], acc);
+    dh[k] = acc;
+  }
+  __syncthreads();
+  if (t < F) gU[(size_t)t * G + g] += dh[t];
+  else if (t < K) gm[(size_t)(t - F) * G + g] = dh[t];
+}
+
+extern "C" int pfsgnn_global_fwd(const float* xs, int n1, const float* xt, int n2, const float* u,
+                                 int F, int G, const float* W1, int H, const float* b1,
+                                 const float* W2, const float* b2, const float* w, float eps,
+                                 float* means, float* Z, float* V, float* Y, float* y1, float* r1,
+                                 float* r2, void* stream) {
+  PF_REQUIRE(xs && xt && u && W1 && b1 && W2 && b2 && means && Z && V && Y && F > 0 && G > 0 &&
+                 n1 > 0 && n2 > 0 && H > 0 && 3 * F <= GL_MAXK && H <= GL_MAXK,
+             "pfsgnn_global_fwd", "bad arguments (3F, H <= 192)");
+  PF_REQUIRE(!w || (y1 && r1 && r2), "pfsgnn_global_fwd", "RMSNorm needs y1, r1, r2");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(k_graph_mean2, dim3(F * G, 2), dim3(256), 0, st, xs, n1, xt, n2, F, G, means);
+  hipLaunchKernelGGL(k_global_fwd, dim3(G), dim3(256), 0, st, xs, n1, xt, n2, u, F, G, W1, H, b1,
+                     W2, b2, w, eps, means, Z, V, Y, y1, r1, r2);
+  return pf::check_launch("pfsgnn_global_fwd");
+}
+
+extern "C" int pfsgnn_global_bwd(const float* dY, const float* V, const float* w, const float* y1,
+                                 const float* r1, const float* r2, int F, int G, const float* Z,
+                                 int H, const float* W1, const float* W2, float* gV, float* dZ,
+                                 float* dwp, float* gU, float* gm, float* gxs, int n1, float s1,
+                                 float* gxt, int n2, float s2, void* stream) {
+  PF_REQUIRE(dY && V && Z && W1 && W2 && gV && dZ && gU && gm && gxs && gxt && F > 0 && G > 0 &&
+                 n1 > 0 && n2 > 0 && H > 0 && 3 * F <= GL_MAXK && H <= GL_MAXK,
+             "pfsgnn_global_bwd", "bad arguments (3F, H <= 192)");
+  PF_REQUIRE(!w || (y1 && r1 && r2 && dwp), "pfsgnn_global_bwd", "RMSNorm needs y1, r1, r2, dwp");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(k_global_bwd, dim3(G), dim3(256), 0, st, dY, V, w, y1, r1, r2, F, G, Z, H, W1,
+                     W2, gV, dZ, dwp, gU, gm);
+  const size_t tot = (size_t)F * G * ((size_t)n1 + n2);
+  hipLaunchKernelGGL(k_graph_bcast_add2, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st,
+                     gxs, n1, s1, gxt, n2, s2, F, G, gm);
+  return pf::check_launch("pfsgnn_global_bwd");
+}
+
 // ---------------------------------------------------------------- BN x2 (edges)
 __global__ void k_bn2_finalize(const float* __restrict__ mu1, const float* __restrict__ var1,
                                const float* __restrict__ gamma, const float* __restrict__ beta,

@@ -262,20 +262,17 @@ class Engine:
         W1, W2 = P[pre + "0.weight"], P[pre + "2.weight"]
         xe, xsc, xsh = st["xe3"]
         dW1 = Gr[pre + "0.weight"]
-        g_xe, GzEs, GzEt = be.edge_mlp_bwd(d, g_tot, alpha, gam0, gam1, st["y"], xe, xsc, xsh,
-                                           st["Ps"], st["Pt"], W1, W2, dW1, Gr[pre + "2.weight"],
-                                           Gr[pre + "2.bias"], want_gxe=want_gxe)
+        # the node-input gradients g_xs += W1s^T GzEs, g_xt += W1t^T GzEt ride in
+        # the op's per-fiber / per-class reductions; Vu = W1u^T GzEt per class
+        g_xe, GzEs, GzEt, Vu = be.edge_mlp_bwd(d, g_tot, alpha, gam0, gam1, st["y"], xe, xsc, xsh,
+                                               st["Ps"], st["Pt"], W1, W2, dW1,
+                                               Gr[pre + "2.weight"], Gr[pre + "2.bias"],
+                                               want_gxe=want_gxe, nodes=(g_xs, g_xt))
         be.wgrad(GzEs, st["xs"], dW1, col0=0)
         # x_t[tgt] and u[batch] columns in one pass (u's gradient sums over classes)
         be.wgrad_cat(GzEt, [(st["xt"], F, False), (st["u"], 3 * F, True)], dW1,
                      db=Gr[pre + "0.bias"])
-        if 4 * F <= 40:      # the two node-input gradients in one launch
-            be.linear_batch([("t", W1, 0, F, GzEs, g_xs, True), ("t", W1, F, F, GzEt, g_xt, True)])
-        else:
-            be.lin_t(W1, 0, F, GzEs, out=g_xs, add=True)
-            be.lin_t(W1, F, F, GzEt, out=g_xt, add=True)
-        GzEu = be.graph_reduce(GzEt, G)
-        be.lin_t(W1, 3 * F, F, GzEu, out=g_u, add=True)
+        be.graph_reduce(Vu, G, out=g_u)      # g_u += W1u^T (sum of GzEt over each graph)
         return g_xe
 
     # --- SModel (gnn.py:123-154)
@@ -320,11 +317,10 @@ class Engine:
         out = be.source_bwd(
             d, y, sc, sh, st["Qt"], Ws1, Ws2, P[pre + "node_mlp_1.2.bias"], st["mom"][0], coef,
             tpart, g_next, bnstat, Gr[pre + "node_mlp_1.0.weight"], Gr[pre + "node_mlp_1.2.weight"],
-            Gr[pre + "node_mlp_1.2.bias"], bn2=bn2)
+            Gr[pre + "node_mlp_1.2.bias"], bn2=bn2, g_xt=g_xt)  # + g_xt += Ws1x^T GzS
         g_tot, GzS = out[0], out[1]
         be.wgrad(GzS, st["xt"], Gr[pre + "node_mlp_1.0.weight"], col0=0,
                  db=Gr[pre + "node_mlp_1.0.bias"])
-        be.lin_t(Ws1, 0, F, GzS, out=g_xt, add=True)
         if bn2 is not None:
             return g_tot, out[4]
         return g_tot, out[2], out[3]
@@ -335,10 +331,12 @@ class Engine:
         Wt1, bt1 = P[pre + "node_mlp_1.0.weight"], P[pre + "node_mlp_1.0.bias"]
         Wt2, bt2 = P[pre + "node_mlp_1.2.weight"], P[pre + "node_mlp_1.2.bias"]
         Rs = be.lin(Wt1, 0, F, xs, b=bt1)
-        hsum = be.target_fwd(d, xe3[0], xe3[1], xe3[2], Rs, Wt1)
         if d.sp is None:
-            agg = be.lin(Wt2, 0, 2 * F, hsum, b=bt2, bscale=float(d.NF))
+            # the second Linear after the per-class sum, in the op's reduction epilogue
+            hsum, agg = be.target_fwd(d, xe3[0], xe3[1], xe3[2], Rs, Wt1,
+                                      agg=(Wt2, bt2, float(d.NF)))
         else:
+            hsum = be.target_fwd(d, xe3[0], xe3[1], xe3[2], Rs, Wt1)
             # the bias of the summed messages is deg(c) * b2 (gnn.py:190)
             agg = be.lin(Wt2, 0, 2 * F, hsum)
             be.lin(bt2.view(-1, 1), 0, 1, d.sp.deg_t, out=agg, add=True)
@@ -368,15 +366,24 @@ class Engine:
         Wt1 = P[pre + "node_mlp_1.0.weight"]
         y, sc, sh = st["xe3"]
         GzT, gxe = be.target_bwd(d, y, sc, sh, st["Rs"], Wt1, g_hsum,
-                                 Gr[pre + "node_mlp_1.0.weight"], want_gxe=want_gxe)
+                                 Gr[pre + "node_mlp_1.0.weight"], want_gxe=want_gxe,
+                                 g_xs=g_xs)          # + g_xs += Wt1s^T GzT
         be.wgrad(GzT, st["xs"], Gr[pre + "node_mlp_1.0.weight"], col0=0,
                  db=Gr[pre + "node_mlp_1.0.bias"])
-        be.lin_t(Wt1, 0, F, GzT, out=g_xs, add=True)
         return gxe
 
     # --- GlobalModel (gnn.py:208-223; its RMSNorm also runs twice)
     def global_fwd(self, P, d, pre, xs, xt, u):
         be, F, G = self.be, self.F, d.G
+        W1 = P[pre + "0.weight"]
+        if 3 * F <= 192 and W1.shape[0] <= 192:
+            # the whole model of each graph in one op (means, MLP, RMSNorm x2)
+            w = P[pre + "norm.weight"] if self.normed else None
+            u_new, means, Z, v, rms = be.global_fwd(
+                xs, xt, u, W1, P[pre + "0.bias"], P[pre + "2.weight"], P[pre + "2.bias"], w,
+                self._rms_eps(u) if w is not None else 0.0, G)
+            sU = ([(u, 0, False), (means, F, False)], Z, None)
+            return dict(sU=sU, v=v, rms=rms, u_new=u_new, fused=True)
         # [u, mean x_s, mean x_t] (gnn.py:218-220), in place
         hU = [(u, 0, False), (be.graph_mean2(xs, xt, G), F, False)]
         v, sU = self.mlp_fwd(P, pre, hU)
@@ -388,6 +395,16 @@ class Engine:
 
     def global_bwd(self, P, Gr, d, pre, st, g_u_new, g_xs, g_xt, g_u):
         be, F = self.be, self.F
+        if st.get("fused"):
+            pre_w = pre + "norm.weight"
+            segs, Z, _ = st["sU"]
+            W1, W2 = P[pre + "0.weight"], P[pre + "2.weight"]
+            g_v, dZ = be.global_bwd(g_u_new, st["v"], P[pre_w] if self.normed else None, st["rms"],
+                                    self._rms_eps(st["v"]), Gr[pre_w] if self.normed else None,
+                                    Z, W1, W2, g_u, g_xs, 1.0 / d.NF, g_xt, 1.0 / d.NC)
+            be.wgrad(g_v, Z, Gr[pre + "2.weight"], db=Gr[pre + "2.bias"], act_in=True)
+            be.wgrad_cat(dZ, segs, Gr[pre + "0.weight"], db=Gr[pre + "0.bias"])
+            return
         if self.normed:
             g_v = be.rms2_bwd(g_u_new, st["v"], P[pre + "norm.weight"], st["rms"],
                               self._rms_eps(st["v"]), Gr[pre + "norm.weight"])

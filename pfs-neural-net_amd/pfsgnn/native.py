@@ -123,6 +123,9 @@ _SIGS = {
     "pfsgnn_graph_bcast_add2": ([P, I, FL, P, I, FL, I, I, P, P], I),
     "pfsgnn_rms2_fwd": ([P, I, I, P, FL, P, P, P, P, P], I),
     "pfsgnn_rms2_bwd": ([P, P, P, P, P, P, I, I, FL, P, P, P, SZ, P], I),
+    "pfsgnn_global_fwd": ([P, I, P, I, P, I, I, P, I, P, P, P, P, FL] + [P] * 7 + [P], I),
+    "pfsgnn_global_bwd": ([P, P, P, P, P, P, I, I, P, I, P, P, P, P, P, P, P, P, I, FL, P, I,
+                           FL, P], I),
     "pfsgnn_bn2_finalize": ([P, P, P, P, P, P, I, LL, FL, FL, P, P, P, P, P], I),
     "pfsgnn_bn_eval_coef": ([P, P, P, P, I, FL, I, P, P, P], I),
     "pfsgnn_affine_rows": ([P, I, I, P, P, P, P], I),
@@ -142,12 +145,12 @@ _SIGS = {
     "pfsgnn_edge_mlp_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_edge_mlp_fwd_bn": ([I, I, I, I] + [P] * 15 + [FL, FL, P, P, P, P, P, SZ, P], I),
     "pfsgnn_source_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
-    "pfsgnn_target_fwd": ([I, I, I, I, P, P, P, P, P, P, P, SZ, P], I),
-    "pfsgnn_target_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
-    "pfsgnn_source_bwd": ([I, I, I, I] + [P] * 22 + [P, SZ, P], I),
-    "pfsgnn_source_bwd_bn": ([I, I, I, I] + [P] * 17 + [LL, FL] + [P] * 10 + [P, SZ, P], I),
+    "pfsgnn_target_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, P, P, SZ, P], I),
+    "pfsgnn_target_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_source_bwd": ([I, I, I, I] + [P] * 23 + [P, SZ, P], I),
+    "pfsgnn_source_bwd_bn": ([I, I, I, I] + [P] * 17 + [LL, FL] + [P] * 11 + [P, SZ, P], I),
     "pfsgnn_edge_bn_grad_sums": ([I, I, I, I, P, P, P, P, P, P, P, SZ, P], I),
-    "pfsgnn_edge_mlp_bwd": ([I, I, I, I] + [P] * 18 + [P, SZ, P], I),
+    "pfsgnn_edge_mlp_bwd": ([I, I, I, I] + [P] * 21 + [P, SZ, P], I),
     "pfsgnn_loss_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, FL, FL, ULL, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_loss_finalize": ([I, I, I, P, P, P, P, FL, FL, FL, FL, FL, FL, P, P, P, P, P, P, P], I),
     "pfsgnn_loss_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, FL, FL, ULL, P, P, P, P, P, P,
@@ -611,6 +614,51 @@ class HipBackend:
               wsb, _stream())
         return dX
 
+    def global_fwd(self, xs, xt, u, W1, b1, W2, b2, w, eps, G):
+        """The whole GlobalModel forward (gnn.py:208-223), one call (two launches).  w: the
+        RMSNorm weight or None (unnormed).  -> (u_new, means [2F, G], Z, V, rms)."""
+        F = u.shape[0]
+        H = W1.shape[0]
+        assert W1.shape[1] == 3 * F and W2.shape == (F, H)
+        self._chk(xs, xt, u, W1, b1, W2, b2, w)
+        means, Z, V, Y = self.empty(2 * F, G), self.empty(H, G), self.empty(F, G), self.empty(F, G)
+        rms = (self.empty(F, G), self.empty(G), self.empty(G)) if w is not None else None
+        y1, r1, r2 = rms if rms is not None else (None, None, None)
+        _call("pfsgnn_global_fwd", xs.data_ptr(), xs.shape[1] // G, xt.data_ptr(), xt.shape[1] // G,
+              u.data_ptr(), F, G, W1.data_ptr(), H, b1.data_ptr(), W2.data_ptr(), b2.data_ptr(),
+              _ptr(w), float(eps), means.data_ptr(), Z.data_ptr(), V.data_ptr(), Y.data_ptr(),
+              _ptr(y1), _ptr(r1), _ptr(r2), _stream())
+        return Y, means, Z, V, rms
+
+    def _ones_row(self, n):
+        c = getattr(self, "_ones_cache", None)
+        if c is None:
+            c = self._ones_cache = {}
+        if n not in c:
+            c[n] = self.ones(1, n)
+        return c[n]
+
+    def global_bwd(self, dY, V, w, rms, eps, dw, Z, W1, W2, g_u, g_xs, s1, g_xt, s2):
+        """Backward of global_fwd, one call (two launches; + the RMSNorm weight gradient as a
+        deferred weight-gradient job).  Accumulates into g_u, g_xs, g_xt and dw;
+        -> (gV, dZ) for the MLP's weight gradients."""
+        F, G = V.shape
+        H = W1.shape[0]
+        dY = dY.contiguous()
+        self._chk(dY, V, w, Z, W1, W2, g_u, g_xs, g_xt)
+        gV, dZ, gm = self.empty(F, G), self.empty(H, G), self.empty(2 * F, G)
+        dwp = self.empty(F, G) if w is not None else None
+        y1, r1, r2 = rms if rms is not None else (None, None, None)
+        _call("pfsgnn_global_bwd", dY.data_ptr(), V.data_ptr(), _ptr(w), _ptr(y1), _ptr(r1),
+              _ptr(r2), F, G, Z.data_ptr(), H, W1.data_ptr(), W2.data_ptr(), gV.data_ptr(),
+              dZ.data_ptr(), _ptr(dwp), g_u.data_ptr(), gm.data_ptr(), g_xs.data_ptr(),
+              g_xs.shape[1] // G,
+              float(s1), g_xt.data_ptr(), g_xt.shape[1] // G, float(s2), _stream())
+        if w is not None:
+            # dw[c] += sum_g dwp[c][g]: a [F, G] x [1, G]^T weight-gradient job
+            self.wgrad(dwp, self._ones_row(G), dw.view(F, 1))
+        return gV, dZ
+
     def bn2_finalize(self, mu1, var1, gamma, beta, rm, rv, n, momentum, eps):
         C = mu1.shape[0]
         sc, sh, inv1, inv2 = self.empty(C), self.empty(C), self.empty(C), self.empty(C)
@@ -708,35 +756,57 @@ class HipBackend:
               hs_out.data_ptr(), ws, wsb, _stream())
         return mom
 
-    def target_fwd(self, d, y, sc, sh, Rs, Wt1):
+    def target_fwd(self, d, y, sc, sh, Rs, Wt1, agg=None):
+        """-> hsum; with ``agg`` = (Wt2, bt2, bscale) -> (hsum, Wt2 hsum + bscale bt2),
+        the second Linear done in the class reduction's epilogue."""
         if d.sp is not None:
-            return self._sp.target_fwd(d, y, sc, sh, Rs, Wt1)
+            hsum = self._sp.target_fwd(d, y, sc, sh, Rs, Wt1)
+            if agg is None:
+                return hsum
+            Wt2, bt2, bscale = agg
+            return hsum, self.lin(Wt2, 0, Wt2.shape[1], hsum, b=bt2, bscale=bscale)
         hsum = self.empty(2 * d.F, d.NT)
+        Wt2 = bt2 = A = None
+        bscale = 1.0
+        if agg is not None:
+            Wt2, bt2, bscale = agg
+            self._chk(Wt2, bt2)
+            assert Wt2.shape == (2 * d.F, 2 * d.F)
+            A = self.empty(2 * d.F, d.NT)
         ws, wsb = self._wsargs(d)
         _call("pfsgnn_target_fwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
-              Rs.data_ptr(), Wt1.data_ptr(), hsum.data_ptr(), ws, wsb, _stream())
-        return hsum
+              Rs.data_ptr(), Wt1.data_ptr(), hsum.data_ptr(), _ptr(Wt2), _ptr(bt2),
+              float(bscale), _ptr(A), ws, wsb, _stream())
+        return hsum if agg is None else (hsum, A)
 
-    def target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False):
+    def target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False, g_xs=None):
+        """-> (GzT, gxe); with ``g_xs``: g_xs += Wt1[:, :F]^T GzT as well."""
         if d.sp is not None:
-            return self._sp.target_bwd(d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=want_gxe)
+            out = self._sp.target_bwd(d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=want_gxe)
+            if g_xs is not None:
+                self.lin_t(Wt1, 0, d.F, out[0], out=g_xs, add=True)
+            return out
+        self._chk(g_xs)
         GzT = self.empty(2 * d.F, d.NS)
         gxe = self.empty(d.F, d.E) if want_gxe else None
         g_hsum = g_hsum.contiguous()
         ws, wsb = self._wsargs(d)
         _call("pfsgnn_target_bwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
               Rs.data_ptr(), Wt1.data_ptr(), g_hsum.data_ptr(), GzT.data_ptr(), dWt1.data_ptr(),
-              _ptr(gxe), ws, wsb, _stream())
+              _ptr(gxe), _ptr(g_xs), ws, wsb, _stream())
         return GzT, gxe
 
     def source_bwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next, bnstat,
-                   dWs1, dWs2, dbs2, bn2=None):
+                   dWs1, dWs2, dbs2, bn2=None, g_xt=None):
         """-> (g_tot, GzS, Sg, Sgx).  With ``bn2`` = (gamma, var1, n, eps, dgamma,
         dbeta) (and ``bnstat``) the edge BatchNorm's backward is finished in the
-        same call: -> (g_tot, GzS, None, None, (alpha, gam0, gam1))."""
+        same call: -> (g_tot, GzS, None, None, (alpha, gam0, gam1)).  With
+        ``g_xt``: g_xt += Ws1[:, :F]^T GzS as well."""
         if d.sp is not None:
             out = self._sp.source_bwd(d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next,
                                       bnstat, dWs1, dWs2, dbs2)
+            if g_xt is not None:
+                self.lin_t(Ws1, 0, d.F, out[1], out=g_xt, add=True)
             if bn2 is None:
                 return out
             gamma, var1, n, eps, dg, db = bn2
@@ -767,10 +837,11 @@ class HipBackend:
             _call("pfsgnn_source_bwd_bn", *head, var1.data_ptr(), gamma.data_ptr(), int(n),
                   float(eps), g_tot.data_ptr(), GzS.data_ptr(), dWs1.data_ptr(), dWs2.data_ptr(),
                   dbs2.data_ptr(), a.data_ptr(), g0.data_ptr(), g1.data_ptr(), dg.data_ptr(),
-                  db.data_ptr(), ws, wsb, _stream())
+                  db.data_ptr(), _ptr(g_xt), ws, wsb, _stream())
             return g_tot, GzS, None, None, (a, g0, g1)
         _call("pfsgnn_source_bwd", *head, g_tot.data_ptr(), GzS.data_ptr(), dWs1.data_ptr(),
-              dWs2.data_ptr(), dbs2.data_ptr(), _ptr(Sg), _ptr(Sgx), ws, wsb, _stream())
+              dWs2.data_ptr(), dbs2.data_ptr(), _ptr(Sg), _ptr(Sgx), _ptr(g_xt), ws, wsb,
+              _stream())
         return g_tot, GzS, Sg, Sgx
 
     def edge_bn_grad_sums(self, d, g, y, mu1, inv1):
@@ -783,19 +854,33 @@ class HipBackend:
         return Sg, Sgx
 
     def edge_mlp_bwd(self, d, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1, W2,
-                     dW1, dW2, db2, want_gxe=True):
+                     dW1, dW2, db2, want_gxe=True, nodes=None):
+        """-> (gxe, GzEs, GzEt); with ``nodes`` = (g_xs, g_xt) the first Linear's
+        node-input gradients are added in the reductions' epilogues and the
+        result is (gxe, GzEs, GzEt, Vu), Vu = W1[:, 3F:4F]^T GzEt per class."""
         if d.sp is not None:
-            return self._sp.edge_mlp_bwd(d, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1,
-                                         W2, dW1, dW2, db2, want_gxe=want_gxe)
+            out = self._sp.edge_mlp_bwd(d, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1,
+                                        W2, dW1, dW2, db2, want_gxe=want_gxe)
+            if nodes is None:
+                return out
+            F = d.F
+            self.lin_t(W1, 0, F, out[1], out=nodes[0], add=True)
+            self.lin_t(W1, F, F, out[2], out=nodes[1], add=True)
+            return out + (self.lin_t(W1, 3 * F, F, out[2]),)
         gxe = self.empty(d.F, d.E) if want_gxe else None
         GzEs, GzEt = self.empty(4 * d.F, d.NS), self.empty(4 * d.F, d.NT)
+        g_xs = g_xt = Vu = None
+        if nodes is not None:
+            g_xs, g_xt = nodes
+            self._chk(g_xs, g_xt)
+            Vu = self.empty(d.F, d.NT)
         ws, wsb = self._wsargs(d)
         _call("pfsgnn_edge_mlp_bwd", d.G, d.NF, d.NC, d.F, g_tot.data_ptr(), alpha.data_ptr(),
               gam0.data_ptr(), gam1.data_ptr(), y.data_ptr(), xe.data_ptr(), _ptr(xsc), _ptr(xsh),
               Ps.data_ptr(), Pt.data_ptr(), W1.data_ptr(), W2.data_ptr(), dW1.data_ptr(),
-              dW2.data_ptr(), db2.data_ptr(), _ptr(gxe), GzEs.data_ptr(), GzEt.data_ptr(), ws, wsb,
-              _stream())
-        return gxe, GzEs, GzEt
+              dW2.data_ptr(), db2.data_ptr(), _ptr(gxe), GzEs.data_ptr(), GzEt.data_ptr(),
+              _ptr(g_xs), _ptr(g_xt), _ptr(Vu), ws, wsb, _stream())
+        return (gxe, GzEs, GzEt) if nodes is None else (gxe, GzEs, GzEt, Vu)
 
     def edge_apply(self, d, y, sc, sh):
         if d.sp is not None:

@@ -233,6 +233,23 @@ class EmuBackend:
         self.graph_bcast_add(out1, src[:C], s1)
         self.graph_bcast_add(out2, src[C:], s2)
 
+    def global_fwd(self, xs, xt, u, W1, b1, W2, b2, w, eps, G):
+        F = u.shape[0]
+        means = self.graph_mean2(xs, xt, G)
+        V, Z, _, _, _ = self.mlp_fwd([(u, 0, False), (means, F, False)], G, W1, b1, W2, b2)
+        if w is None:
+            return V, means, Z, V, None
+        Y, rms = self.rms2_fwd(V, w, eps)
+        return Y, means, Z, V, rms
+
+    def global_bwd(self, dY, V, w, rms, eps, dw, Z, W1, W2, g_u, g_xs, s1, g_xt, s2):
+        F, G = V.shape
+        gV = dY if w is None else self.rms2_bwd(dY, V, w, rms, eps, dw)
+        g_m = self.empty(2 * F, G)
+        _, dZ = self.mlp_bwd(gV, Z, W1, W2, 3 * F, outs=[(g_u, F, True), (g_m, 2 * F, False)])
+        self.graph_bcast_add2(g_xs, s1, g_xt, s2, g_m)
+        return gV, dZ
+
     def rms2_fwd(self, X, w, eps):
         def one(x):
             r = torch.rsqrt((x * x).mean(0, keepdim=True) + eps)
@@ -360,7 +377,14 @@ class EmuBackend:
         hs_out[3 * C:4 * C] = c4 / std ** 4
         return torch.stack([mean, c2, c3, c4])
 
-    def target_fwd(self, d, y, sc, sh, Rs, Wt1):
+    def target_fwd(self, d, y, sc, sh, Rs, Wt1, agg=None):
+        hsum = self._target_fwd(d, y, sc, sh, Rs, Wt1)
+        if agg is None:
+            return hsum
+        Wt2, bt2, bscale = agg
+        return hsum, self.lin(Wt2, 0, Wt2.shape[1], hsum, b=bt2, bscale=bscale)
+
+    def _target_fwd(self, d, y, sc, sh, Rs, Wt1):
         if d.sp is not None:
             return self._sp.target_fwd(d, y, sc, sh, Rs, Wt1)
         fib, cls = _edge_index(d, y.device)
@@ -370,7 +394,13 @@ class EmuBackend:
         at = lrelu(zt)
         return _seg(at, cls, d.NT)
 
-    def target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False):
+    def target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False, g_xs=None):
+        out = self._target_bwd(d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=want_gxe)
+        if g_xs is not None:
+            self.lin_t(Wt1, 0, d.F, out[0], out=g_xs, add=True)
+        return out
+
+    def _target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False):
         if d.sp is not None:
             return self._sp.target_bwd(d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=want_gxe)
         fib, cls = _edge_index(d, y.device)
@@ -384,9 +414,11 @@ class EmuBackend:
         return GzT, gxe
 
     def source_bwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next,
-                   bnstat, dWs1, dWs2, dbs2, bn2=None):
+                   bnstat, dWs1, dWs2, dbs2, bn2=None, g_xt=None):
         out = self._source_bwd(d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next,
                                bnstat, dWs1, dWs2, dbs2)
+        if g_xt is not None:
+            self.lin_t(Ws1, 0, d.F, out[1], out=g_xt, add=True)
         if bn2 is None:
             return out
         gamma, var1, n, eps, dg, db = bn2
@@ -435,7 +467,18 @@ class EmuBackend:
         return g.sum(1), (g * xh).sum(1)
 
     def edge_mlp_bwd(self, d, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1, W2,
-                     dW1, dW2, db2, want_gxe=True):
+                     dW1, dW2, db2, want_gxe=True, nodes=None):
+        out = self._edge_mlp_bwd(d, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1, W2,
+                                 dW1, dW2, db2, want_gxe=want_gxe)
+        if nodes is None:
+            return out
+        F = d.F
+        self.lin_t(W1, 0, F, out[1], out=nodes[0], add=True)
+        self.lin_t(W1, F, F, out[2], out=nodes[1], add=True)
+        return out + (self.lin_t(W1, 3 * F, F, out[2]),)
+
+    def _edge_mlp_bwd(self, d, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1, W2,
+                      dW1, dW2, db2, want_gxe=True):
         if d.sp is not None:
             return self._sp.edge_mlp_bwd(d, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1, W2, dW1, dW2, db2, want_gxe=want_gxe)
         fib, cls = _edge_index(d, y.device)

@@ -438,3 +438,37 @@ def test_linear_batch_matches_single_launches():
     hb.lin_t(W1, 0, F, gs, out=ys2, add=True)
     hb.lin_t(W1, F, F, gt, out=yt2, add=True)
     assert torch.equal(ys, ys2) and torch.equal(yt, yt2)
+
+
+@pytest.mark.parametrize("G,n1,n2,F,normed", [(1, 37, 12, 10, True), (16, 2394, 128, 10, True),
+                                                (3, 300, 7, 16, True), (5, 21, 5, 8, False)])
+def test_global_fused(hb, G, n1, n2, F, normed):
+    """pfsgnn_global_fwd / _bwd (the whole GlobalModel, gnn.py:208-223, one
+    launch each) vs the composed emulation (graph means, MLP, RMSNorm x2)."""
+    emu = EmuBackend()
+    gen = torch.Generator().manual_seed(G * 7 + F)
+    xs, xt, u = r(F, G * n1, gen=gen), r(F, G * n2, gen=gen), r(F, G, gen=gen)
+    W1, b1 = r(3 * F, 3 * F, scale=0.3, gen=gen), r(3 * F, gen=gen)
+    W2, b2 = r(F, 3 * F, scale=0.3, gen=gen), r(F, gen=gen)
+    w = r(F, gen=gen).abs() + 0.5 if normed else None
+    eps = float(torch.finfo(torch.float32).eps)
+    oh = hb.global_fwd(cuda(xs), cuda(xt), cuda(u), cuda(W1), cuda(b1), cuda(W2), cuda(b2),
+                       cuda(w), eps, G)
+    oe = emu.global_fwd(xs, xt, u, W1, b1, W2, b2, w, eps, G)
+    for a, b, nm in zip(oh[:4], oe[:4], ("Y", "means", "Z", "V")):
+        close(a, b, name=nm)
+    dY = r(F, G, gen=gen)
+    gu_e, gxs_e, gxt_e = r(F, G, gen=gen), r(F, G * n1, gen=gen), r(F, G * n2, gen=gen)
+    gu_h, gxs_h, gxt_h = cuda(gu_e), cuda(gxs_e), cuda(gxt_e)
+    dw_h = torch.zeros(F, device="cuda") if normed else None
+    dw_e = torch.zeros(F, dtype=torch.float64) if normed else None
+    gh = hb.global_bwd(cuda(dY), oh[3], cuda(w), oh[4], eps, dw_h, oh[2], cuda(W1), cuda(W2),
+                       gu_h, gxs_h, 1.0 / n1, gxt_h, 1.0 / n2)
+    ge = emu.global_bwd(dY, oe[3], w, oe[4], eps, dw_e, oe[2], W1, W2, gu_e, gxs_e, 1.0 / n1,
+                        gxt_e, 1.0 / n2)
+    torch.cuda.synchronize()
+    close(gh[0], ge[0], rtol=1e-3, name="gV"); close(gh[1], ge[1], rtol=1e-3, name="dZ")
+    close(gu_h, gu_e, rtol=1e-3, name="g_u")
+    close(gxs_h, gxs_e, rtol=1e-3, name="g_xs"); close(gxt_h, gxt_e, rtol=1e-3, name="g_xt")
+    if normed:
+        close(dw_h, dw_e, rtol=1e-3, name="dw")
