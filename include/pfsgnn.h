@@ -267,6 +267,10 @@ int pfsgnn_graph_reduce(const float* X, int C, int G, int n, int mean, float* ou
 /* the same, accumulated: out[c][g] += sum (or mean) ... (u[batch] gradients, gnn.py:100/153/191) */
 int pfsgnn_graph_reduce_add(const float* X, int C, int G, int n, int mean, float* out,
                             void* stream);
+/* m (1..4) per-graph sums into one accumulator, one launch: out[c][g] +=
+ * sum_j sum_i X[j][c][g*n[j] + i] (the u[batch] gradients of gnn.py:100/153/191). */
+int pfsgnn_graph_reduce_multi(const float* const* X, const int* n, int m, int C, int G,
+                              float* out, void* stream);
 /* GlobalModel's two node means (gnn.py:218-219) in one launch:
  * out[c][g] = mean of X1[c][g*n1 ..], out[C + c][g] = mean of X2[c][g*n2 ..] */
 int pfsgnn_graph_mean2(const float* X1, int n1, const float* X2, int n2, int C, int G,

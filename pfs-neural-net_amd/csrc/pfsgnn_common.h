@@ -146,6 +146,55 @@ __device__ __forceinline__ float wave_sum(float v) {
   return (a + b) + (c + d);
 }
 
+// (na, mean, M2, M3, M4) <- merge with (nb, ...)   [Pebay 2008, eq. 3.1 ff.]
+template <typename T>
+__device__ __forceinline__ void pebay_merge(T na, T& ma, T& M2a, T& M3a, T& M4a, T nb, T mb,
+                                            T M2b, T M3b, T M4b) {
+  const T n = na + nb;
+  const T d = mb - ma, d2 = d * d, nanb = na * nb;
+  const T in = T(1) / n, in2 = in * in;
+  M4a = M4a + M4b + d2 * d2 * nanb * (na * na - nanb + nb * nb) * in2 * in +
+        T(6) * d2 * (na * na * M2b + nb * nb * M2a) * in2 + T(4) * d * (na * M3b - nb * M3a) * in;
+  M3a = M3a + M3b + d2 * d * nanb * (na - nb) * in2 + T(3) * d * (na * M2b - nb * M2a) * in;
+  M2a = M2a + M2b + d2 * nanb * in;
+  ma = ma + d * nb * in;
+}
+
+// SModel's per-fiber moments of element idx = c*NS + n from the KS class-split
+// Pebay partials partS [KS][4][C][NS] (merged in k order, in double), written
+// as mom [4][C][NS] = (mean, M2/n, M3/n, M4/n) and hs [4C][NS] = (mean, std,
+// skew, kurt) with gnn.py:140-151's leaky variance and eps
+__device__ __forceinline__ void source_finalize_one(const float* __restrict__ partS, int KS,
+                                                    int CPS, int C, long long NS, int NC,
+                                                    long long idx, float* __restrict__ mom,
+                                                    float* __restrict__ hs) {
+  const long long CNS = (long long)C * NS;
+  double na = 0, mean = 0, M2 = 0, M3 = 0, M4 = 0;
+  for (int k = 0; k < KS; ++k) {
+    const float* p = partS + (size_t)k * 4 * CNS + idx;
+    const double nb = (double)(min(NC, (k + 1) * CPS) - k * CPS);
+    if (nb <= 0) break;
+    if (na == 0) {
+      mean = p[0]; M2 = p[CNS]; M3 = p[2 * CNS]; M4 = p[3 * CNS];
+    } else {
+      pebay_merge<double>(na, mean, M2, M3, M4, nb, p[0], p[CNS], p[2 * CNS], p[3 * CNS]);
+    }
+    na += nb;
+  }
+  const double invn = 1.0 / (double)NC;
+  const float c2 = (float)(M2 * invn), c3 = (float)(M3 * invn), c4 = (float)(M4 * invn);
+  mom[idx] = (float)mean;
+  mom[CNS + idx] = c2;
+  mom[2 * CNS + idx] = c3;
+  mom[3 * CNS + idx] = c4;
+  const float var = c2 > 0.f ? c2 : 0.01f * c2;  // F.leaky_relu (slope 0.01), gnn.py:141
+  const float sd = sqrtf(var + 1e-6f);
+  hs[idx] = (float)mean;
+  hs[CNS + idx] = sd;
+  hs[2 * CNS + idx] = c3 / (sd * sd * sd);
+  hs[3 * CNS + idx] = c4 / ((sd * sd) * (sd * sd));
+}
+
 // ------------------------------------------------------------ reductions
 // Sum NV values over the whole 256-thread block into out[0..NV) (LDS), valid
 // after the call for every thread.  `scratch` >= 4*NV floats.

@@ -409,20 +409,6 @@ __device__ __forceinline__ void source_message(const float (&x)[F], const float*
   }
 }
 
-// (na, mean, M2, M3, M4) <- merge with (nb, ...)   [Pebay 2008, eq. 3.1 ff.]
-template <typename T>
-__device__ __forceinline__ void pebay_merge(T na, T& ma, T& M2a, T& M3a, T& M4a, T nb, T mb,
-                                            T M2b, T M3b, T M4b) {
-  const T n = na + nb;
-  const T d = mb - ma, d2 = d * d, nanb = na * nb;
-  const T in = T(1) / n, in2 = in * in;
-  M4a = M4a + M4b + d2 * d2 * nanb * (na * na - nanb + nb * nb) * in2 * in +
-        T(6) * d2 * (na * na * M2b + nb * nb * M2a) * in2 + T(4) * d * (na * M3b - nb * M3a) * in;
-  M3a = M3a + M3b + d2 * d * nanb * (na - nb) * in2 + T(3) * d * (na * M2b - nb * M2a) * in;
-  M2a = M2a + M2b + d2 * nanb * in;
-  ma = ma + d * nb * in;
-}
-
 template <int F>
 __global__ __launch_bounds__(256) void k_source_fwd(EdgeGeo geo, const float* __restrict__ y,
                                                     const float* __restrict__ sc,
@@ -509,32 +495,7 @@ __global__ void k_source_finalize(const float* __restrict__ partS, int KS, int C
                                   long long NS, int NC, float* __restrict__ mom,
                                   float* __restrict__ hs) {
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // over C*NS
-  const long long CNS = (long long)C * NS;
-  if (idx >= CNS) return;
-  double na = 0, mean = 0, M2 = 0, M3 = 0, M4 = 0;
-  for (int k = 0; k < KS; ++k) {
-    const float* p = partS + (size_t)k * 4 * CNS + idx;
-    const double nb = (double)(min(NC, (k + 1) * CPS) - k * CPS);
-    if (nb <= 0) break;
-    if (na == 0) {
-      mean = p[0]; M2 = p[CNS]; M3 = p[2 * CNS]; M4 = p[3 * CNS];
-    } else {
-      pebay_merge<double>(na, mean, M2, M3, M4, nb, p[0], p[CNS], p[2 * CNS], p[3 * CNS]);
-    }
-    na += nb;
-  }
-  const double invn = 1.0 / (double)NC;
-  const float c2 = (float)(M2 * invn), c3 = (float)(M3 * invn), c4 = (float)(M4 * invn);
-  mom[idx] = (float)mean;
-  mom[CNS + idx] = c2;
-  mom[2 * CNS + idx] = c3;
-  mom[3 * CNS + idx] = c4;
-  const float var = c2 > 0.f ? c2 : 0.01f * c2;  // F.leaky_relu (slope 0.01), gnn.py:141
-  const float sd = sqrtf(var + 1e-6f);
-  hs[idx] = (float)mean;
-  hs[CNS + idx] = sd;
-  hs[2 * CNS + idx] = c3 / (sd * sd * sd);
-  hs[3 * CNS + idx] = c4 / ((sd * sd) * (sd * sd));
+  if (idx < (long long)C * NS) source_finalize_one(partS, KS, CPS, C, NS, NC, idx, mom, hs);
 }
 
 // ============================================================ TModel fwd

@@ -1424,6 +1424,43 @@ extern "C" int pfsgnn_graph_reduce_add(const float* X, int C, int G, int n, int 
   return pf::check_launch("pfsgnn_graph_reduce_add");
 }
 
+// Several per-graph sums into one accumulator in one launch (the u[batch]
+// gradients of a block's SModel, TModel and EdgeModel, gnn.py:100/153/191):
+// out[c][g] += sum_j sum_i X_j[c][g*n_j + i], j in order, one block per (c, g).
+#define GR_MAX 4
+struct GrPack {
+  const float* x[GR_MAX];
+  int n[GR_MAX];
+};
+__global__ void k_graph_reduce_multi(GrPack pk, int m, int C, int G, float* __restrict__ out) {
+  const int cg = blockIdx.x;  // c*G + g
+  const int c = cg / G, g = cg - c * G;
+  float v[1] = {0.f};
+  for (int j = 0; j < m; ++j) {
+    const int n = pk.n[j];
+    const float* p = pk.x[j] + (size_t)c * G * n + (size_t)g * n;
+    for (int i = threadIdx.x; i < n; i += 256) v[0] += p[i];
+  }
+  __shared__ float scratch[4];
+  block_sum<1>(v, scratch);
+  if (threadIdx.x == 0) out[(size_t)c * G + g] += v[0];
+}
+
+extern "C" int pfsgnn_graph_reduce_multi(const float* const* X, const int* n, int m, int C, int G,
+                                         float* out, void* stream) {
+  PF_REQUIRE(X && n && out && m >= 1 && m <= GR_MAX && C > 0 && G > 0,
+             "pfsgnn_graph_reduce_multi", "bad arguments (1..4 inputs)");
+  GrPack pk{};
+  for (int j = 0; j < m; ++j) {
+    PF_REQUIRE(X[j] && n[j] > 0, "pfsgnn_graph_reduce_multi", "bad input");
+    pk.x[j] = X[j];
+    pk.n[j] = n[j];
+  }
+  hipLaunchKernelGGL(k_graph_reduce_multi, dim3(C * G), dim3(256), 0, as_stream(stream), pk, m, C,
+                     G, out);
+  return pf::check_launch("pfsgnn_graph_reduce_multi");
+}
+
 // Two per-graph means in one launch (GlobalModel's x_s.mean / x_t.mean,
 // gnn.py:218-219): out rows [0, C) from X1 (n1 nodes per graph), [C, 2C) from X2.
 __global__ void k_graph_mean2(const float* __restrict__ X1, int n1, const float* __restrict__ X2,

@@ -195,6 +195,22 @@ class Engine:
                 be.lin_t(W1, r, rows, dZ, out=t, add=add)
             r += rows
 
+    def _gu_add(self, X, G, g_u):
+        """g_u += per-graph sums of X (a u[batch] gradient, gnn.py:100/153/191);
+        inside a backward block they are batched into one launch (_gu_flush)."""
+        pend = getattr(self, "_gu_pend", None)
+        if pend is not None:
+            pend.append((X, g_u))
+        else:
+            self.be.graph_reduce(X, G, out=g_u)
+
+    def _gu_flush(self, G):
+        pend, self._gu_pend = getattr(self, "_gu_pend", None) or [], []
+        for i in range(0, len(pend), 4):
+            part = pend[i:i + 4]
+            assert all(t is part[0][1] for _, t in part)
+            self.be.graph_reduce_multi([X for X, _ in part], G, part[0][1])
+
     def _rms_eps(self, t):
         return self.rms_eps if self.rms_eps is not None else torch.finfo(t.dtype).eps
 
@@ -272,7 +288,7 @@ class Engine:
         # x_t[tgt] and u[batch] columns in one pass (u's gradient sums over classes)
         be.wgrad_cat(GzEt, [(st["xt"], F, False), (st["u"], 3 * F, True)], dW1,
                      db=Gr[pre + "0.bias"])
-        be.graph_reduce(Vu, G, out=g_u)      # g_u += W1u^T (sum of GzEt over each graph)
+        self._gu_add(Vu, G, g_u)             # g_u += W1u^T (sum of GzEt over each graph)
         return g_xe
 
     # --- SModel (gnn.py:123-154)
@@ -297,7 +313,7 @@ class Engine:
         gu = be.empty(F, d.NS)               # d loss / d u[batch], per fiber
         self.mlp_bwd(P, Gr, pre + "node_mlp_2.", g_xs_new, st["sS"],
                      outs=[(g_xs, F, True), (gst, 8 * F, False), (gu, F, False)])
-        be.graph_reduce(gu, G, out=g_u)
+        self._gu_add(gu, G, g_u)
         # messages per fiber: NC on complete graphs, the fiber degree otherwise
         return be.moment_coef(st["mom"], gst, d.NC if d.sp is None else d.sp.fib_ptr)
 
@@ -351,7 +367,7 @@ class Engine:
         gu = be.empty(F, d.NT)
         self.mlp_bwd(P, Gr, pre + "node_mlp_2.", g_xt_new, st["sT"],
                      outs=[(g_xt, F, True), (g_agg, 2 * F, False), (gu, F, False)])
-        be.graph_reduce(gu, G, out=g_u)
+        self._gu_add(gu, G, g_u)
         Wt2 = P[pre + "node_mlp_1.2.weight"]
         if d.sp is None:
             be.wgrad(g_agg, st["hsum"], Gr[pre + "node_mlp_1.2.weight"],
@@ -454,11 +470,13 @@ class Engine:
         try:
             self._backward(P, Gr, ctx, d, g_xs_out, g_xt_out, g_xe_out, g_u_out)
         finally:
+            self._gu_pend = None
             be.defer_flush()
 
     def _backward(self, P, Gr, ctx, d, g_xs_out, g_xt_out, g_xe_out, g_u_out):
         be, F = self.be, self.F
         g_xs, g_xt, g_xe, g_u = g_xs_out, g_xt_out, g_xe_out, g_u_out
+        self._gu_pend = []
         for b in reversed(range(self.B)):
             se, ss, stt, su = ctx["blocks"][b]
             p = f"mpb.{b}."
@@ -501,6 +519,7 @@ class Engine:
                     bnc = self.edge_bn_coef(P, Gr, d, p + "edge_model.", se, Sg, Sgx)
             g_xe = self.edge_bwd(P, Gr, d, p + "edge_model.", se, g_tot, bnc, b > 0,
                                  g_xs_in, g_xt_in, g_u_in)
+            self._gu_flush(d.G)                  # the block's u[batch] gradients, one launch
             g_xs, g_xt, g_u = g_xs_in, g_xt_in, g_u_in
         s_enc, t_enc = ctx["enc"]
         self.mlp_bwd(P, Gr, "encoder_s.", g_xs, s_enc)

@@ -119,6 +119,7 @@ _SIGS = {
     "pfsgnn_graph_reduce": ([P, I, I, I, I, P, P], I),
     "pfsgnn_graph_reduce_add": ([P, I, I, I, I, P, P], I),
     "pfsgnn_graph_bcast_add": ([P, I, I, I, P, FL, P], I),
+    "pfsgnn_graph_reduce_multi": ([P, P, I, I, I, P, P], I),
     "pfsgnn_graph_mean2": ([P, I, P, I, I, I, P, P], I),
     "pfsgnn_graph_bcast_add2": ([P, I, FL, P, I, FL, I, I, P, P], I),
     "pfsgnn_rms2_fwd": ([P, I, I, P, FL, P, P, P, P, P], I),
@@ -567,6 +568,17 @@ class HipBackend:
         out = self.empty(C, G)
         _call("pfsgnn_graph_reduce", X.data_ptr(), C, G, N // G, int(mean), out.data_ptr(),
               _stream())
+        return out
+
+    def graph_reduce_multi(self, Xs, G, out):
+        """out[c][g] += per-graph sums of every X in Xs (one launch)."""
+        self._chk(out, *Xs)
+        m = len(Xs)
+        arr = (ctypes.c_void_p * m)(*[X.data_ptr() for X in Xs])
+        ns = (ctypes.c_int * m)(*[X.shape[1] // G for X in Xs])
+        for X in Xs:
+            assert X.shape[0] == out.shape[0] and X.shape[1] % G == 0
+        _call("pfsgnn_graph_reduce_multi", arr, ns, m, out.shape[0], G, out.data_ptr(), _stream())
         return out
 
     def graph_bcast_add(self, out, src, scale=1.0):

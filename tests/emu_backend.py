@@ -219,6 +219,11 @@ class EmuBackend:
             return out
         return R
 
+    def graph_reduce_multi(self, Xs, G, out):
+        for X in Xs:
+            self.graph_reduce(X, G, out=out)
+        return out
+
     def graph_bcast_add(self, out, src, scale=1.0):
         C, N = out.shape
         G = src.shape[1]
