@@ -983,6 +983,17 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
       for (int r = 0; r < GM<C>::nreg(tt); ++r) gz[tt][r] *= dlrelu(zs[tt][r]);
       sgz[tt] = split(gz[tt]);
     }
+    // the weight-gradient images are written first: their LDS latency hides
+    // behind the input-gradient chains below
+    lds_order();
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+      img_put2(im_gm + tt * 2 * IMG_SHORTS, lane, sgm[tt]);
+      img_put2(im_a + tt * 2 * IMG_SHORTS, lane, split(as[tt]));
+      img_put2(im_gz + tt * 2 * IMG_SHORTS, lane, sgz[tt]);
+    }
+    img_put2(im_x, lane, split(x[0]));
+    lds_order();
     floatx4 g[1] = {zero4()};
     if constexpr (PREC >= 1) L1sT.apply(sgz, g); else L1sT.apply(gz, g);
     if (tpart) {  // TModel's per-edge input gradient, recomputed (gnn.py:188-190)
@@ -1016,14 +1027,6 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
       }
     }
     // ---- weight gradients (edge = K) through the transposed images
-    lds_order();
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt) {
-      img_put2(im_gm + tt * 2 * IMG_SHORTS, lane, sgm[tt]);
-      img_put2(im_a + tt * 2 * IMG_SHORTS, lane, split(as[tt]));
-      img_put2(im_gz + tt * 2 * IMG_SHORTS, lane, sgz[tt]);
-    }
-    img_put2(im_x, lane, split(x[0]));
     lds_order();
     const Fr tx = img_tr2(im_x, lane);
     Fr ta[NT];
@@ -1179,11 +1182,8 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
       accF[tt] += gz[tt];
       sgz[tt] = split(gz[tt]);
     }
-    if (gxe) {
-      floatx4 gx[1] = {zero4()};
-      if constexpr (PREC >= 1) L1T.apply(sgz, gx); else L1T.apply(gz, gx);
-      st_frows<F>(gxe, eo, RB, g4, fvalid, gx[0]);
-    }
+    // the weight-gradient images are written first: their LDS latency hides
+    // behind the edge-input gradient chain below
     lds_order();
     img_put2(im_gy, lane, sgy[0]);
 #pragma unroll
@@ -1193,6 +1193,11 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
     }
     img_put2(im_x, lane, split(x[0]));
     lds_order();
+    if (gxe) {
+      floatx4 gx[1] = {zero4()};
+      if constexpr (PREC >= 1) L1T.apply(sgz, gx); else L1T.apply(gz, gx);
+      st_frows<F>(gxe, eo, RB, g4, fvalid, gx[0]);
+    }
     const Fr tgy = img_tr2(im_gy, lane);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt)
