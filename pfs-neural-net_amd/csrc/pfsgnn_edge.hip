@@ -322,7 +322,7 @@ struct Bn2Args {
   float *sc, *sh, *inv1, *inv2;
 };
 
-#define MF_PB 8   // partials per thread (nb <= 2048: the edge grids)
+#define MF_PB 16  // partials per thread (nb <= 4096 in one round: the edge grids)
 __global__ __launch_bounds__(256) void k_moments_finalize(const float* __restrict__ part, int nb,
                                                           int F, long long n,
                                                           float* __restrict__ mu,
