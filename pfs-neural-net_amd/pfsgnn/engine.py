@@ -477,11 +477,14 @@ class Engine:
         be, F = self.be, self.F
         g_xs, g_xt, g_xe, g_u = g_xs_out, g_xt_out, g_xe_out, g_u_out
         self._gu_pend = []
+        stride = (F * (d.NS + d.NT + d.G) + 63) // 64 * 64     # 256-byte aligned slices
+        acc_all = be.zeros(self.B * stride)
         for b in reversed(range(self.B)):
             se, ss, stt, su = ctx["blocks"][b]
             p = f"mpb.{b}."
-            # the three input-gradient accumulators share one zeroed buffer (one fill)
-            acc = be.zeros(F * (d.NS + d.NT + d.G))
+            # the three input-gradient accumulators of every block share one
+            # buffer zeroed once per backward pass (one fill, not one per block)
+            acc = acc_all[b * stride:b * stride + F * (d.NS + d.NT + d.G)]
             g_xs_in = acc[:F * d.NS].view(F, d.NS)
             g_xt_in = acc[F * d.NS:F * (d.NS + d.NT)].view(F, d.NT)
             g_u_in = acc[F * (d.NS + d.NT):].view(F, d.G)
