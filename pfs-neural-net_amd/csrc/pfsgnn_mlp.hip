@@ -98,6 +98,23 @@ __global__ __launch_bounds__(256, (M <= 3 ? 2 : 1)) void k_mlp_fwd(InSegs S, int
   float* B1 = reinterpret_cast<float*>(A2 + M * 64);
   float* B2 = B1 + 16 * M;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, col = lane & 15, kq = lane >> 4;
+  // chunk input rows [16M][XS_LD], double-buffered: chunk c+1 streams in with
+  // global_load_lds while chunk c is multiplied.  The first chunk's copy is
+  // issued before the weight images are staged (its latency overlaps theirs);
+  // only the padding rows >= K, which no copy writes, are zeroed.
+  float* Xs0 = B2 + 16;
+  constexpr int XSZ = 16 * M * XS_LD;
+  const int nch = (N + 63) / 64;
+  const int wu = __builtin_amdgcn_readfirstlane(wave);
+  auto issue = [&](int ch, int buf) {
+    const int n = ch * 64 + lane;
+    const int nc = n < N ? n : N - 1;
+    const int ng = S.npg ? nc / S.npg : 0;
+    float* dst = Xs0 + buf * XSZ;
+    for (int k = wu; k < K; k += 4) glds4(in_ptr(S, k, nc, ng, N), dst + k * XS_LD);
+  };
+  if ((int)blockIdx.x < nch) issue(blockIdx.x, 0);
+  for (int i = K * XS_LD + t; i < XSZ; i += 256) Xs0[i] = Xs0[XSZ + i] = 0.f;
   {  // weight images: every load of the thread in flight at once (a load ->
      // store loop would pay one L2 round trip per element)
     float v[M * M], w[M];
@@ -123,25 +140,7 @@ __global__ __launch_bounds__(256, (M <= 3 ? 2 : 1)) void k_mlp_fwd(InSegs S, int
   for (int i = t; i < 16 * M; i += 256) B1[i] = i < H ? b1[i] : 0.f;
   if (t < 16) B2[t] = t < O ? b2[t] : 0.f;
 
-  // chunk input rows [16M][XS_LD], double-buffered: chunk c+1 streams in with
-  // global_load_lds while chunk c is multiplied (rows >= K stay zero)
-  float* Xs0 = B2 + 16;
-  constexpr int XSZ = 16 * M * XS_LD;
-  for (int i = t; i < 2 * XSZ; i += 256) Xs0[i] = 0.f;
-  const int nch = (N + 63) / 64;
-  const int wu = __builtin_amdgcn_readfirstlane(wave);
-  auto issue = [&](int ch, int buf) {
-    const int n = ch * 64 + lane;
-    const int nc = n < N ? n : N - 1;
-    const int ng = S.npg ? nc / S.npg : 0;
-    float* dst = Xs0 + buf * XSZ;
-    for (int k = wu; k < K; k += 4) glds4(in_ptr(S, k, nc, ng, N), dst + k * XS_LD);
-  };
   float cnt = 0.f, mean[4] = {0.f, 0.f, 0.f, 0.f}, m2[4] = {0.f, 0.f, 0.f, 0.f};
-  if ((int)blockIdx.x < nch) {
-    __syncthreads();                               // zero fill before the first copy
-    issue(blockIdx.x, 0);
-  }
   int it = 0;
   for (int ch = blockIdx.x; ch < nch; ch += gridDim.x, ++it) {
     const int buf = it & 1;
