@@ -6,6 +6,7 @@
 // per-graph broadcast of u (gnn.py:100/153/191).  Node tensors are small
 // (G*NF fibers, G*NC classes) and L2-resident; the hot path is the edge ops.
 #include "pfsgnn_common.h"
+#include <cstdlib>
 #include "../../include/pfsgnn.h"
 
 #include <algorithm>
@@ -852,8 +853,13 @@ __global__ __launch_bounds__(512) void k_wgrad_multi(WgTable T) {
 }
 
 static int wgrad_blocks(int N) {
+  static const int cap = [] {   // tuning knob: PFSGNN_WG_BLOCKS (blocks per weight gradient)
+    const char* e = std::getenv("PFSGNN_WG_BLOCKS");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? std::min(v, 256) : 256;
+  }();
   int s = (N + 127) / 128;
-  return std::max(1, std::min(s, 256));   // <= 2*RED_SEG: one reduce launch
+  return std::max(1, std::min(s, cap));   // <= 2*RED_SEG: one reduce launch
 }
 
 static size_t wgrad_part_bytes(int M, int K1, int N) {
