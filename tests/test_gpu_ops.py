@@ -472,3 +472,67 @@ def test_global_fused(hb, G, n1, n2, F, normed):
     close(gxs_h, gxs_e, rtol=1e-3, name="g_xs"); close(gxt_h, gxt_e, rtol=1e-3, name="g_xt")
     if normed:
         close(dw_h, dw_e, rtol=1e-3, name="dw")
+
+
+@pytest.mark.parametrize("G,NF,NC,F", EDGE_CASES)
+def test_edge_ops_node_epilogues(hb, G, NF, NC, F):
+    """The node-side Linear epilogues of the edge ops' reductions (TModel's
+    second Linear after the class sum; the first Linears' node-input gradients
+    g_xs / g_xt / Vu) against the emulation's separate products, at every Fdim
+    (reduction widths 16, 20, 32, 40, 64) and with KS = 1 and KS > 1 grids."""
+    gen = torch.Generator().manual_seed(7 + G * 1000 + NF * 10 + NC + F)
+
+    def q(t, step):
+        return torch.round(t / step) * step
+    emu = EmuBackend()
+    d, de = dims(G, NF, NC, F)
+    E, NS, NT = d.E, d.NS, d.NT
+    y = q(r(F, E, scale=2, gen=gen), 1 / 4)
+    sc, sh = q(r(F, gen=gen) * 0.3 + 1, 1 / 8), q(r(F, gen=gen), 1 / 8)
+    # target_fwd + agg
+    Rs, Wt1 = q(r(2 * F, NS, gen=gen), 1 / 256), q(r(2 * F, 2 * F, scale=0.3, gen=gen), 1 / 64)
+    Wt2, bt2 = r(2 * F, 2 * F, scale=0.3, gen=gen), r(2 * F, gen=gen)
+    hs_h, agg_h = hb.target_fwd(d, cuda(y), cuda(sc), cuda(sh), cuda(Rs), cuda(Wt1),
+                                agg=(cuda(Wt2), cuda(bt2), float(NF)))
+    hs_e, agg_e = emu.target_fwd(de, y, sc, sh, Rs, Wt1, agg=(Wt2, bt2, float(NF)))
+    close(hs_h, hs_e, name="hsum"); close(agg_h, agg_e, name="agg")
+    # target_bwd + g_xs
+    g_hsum = r(2 * F, NT, gen=gen)
+    dW_h, dW_e = torch.zeros(2 * F, 2 * F, device="cuda"), torch.zeros(2 * F, 2 * F, dtype=torch.float64)
+    gxs_e = r(F, NS, gen=gen)
+    gxs_h = cuda(gxs_e)
+    GzT_h, _ = hb.target_bwd(d, cuda(y), cuda(sc), cuda(sh), cuda(Rs), cuda(Wt1), cuda(g_hsum), dW_h,
+                             g_xs=gxs_h)
+    GzT_e, _ = emu.target_bwd(de, y, sc, sh, Rs, Wt1, g_hsum, dW_e, g_xs=gxs_e)
+    close(GzT_h, GzT_e, name="GzT"); close(gxs_h, gxs_e, rtol=5e-4, name="g_xs(T)")
+    # source_bwd + g_xt
+    Qt = q(r(2 * F, NT, gen=gen), 1 / 256)
+    Ws1, Ws2, bs2 = q(r(2 * F, 2 * F, scale=0.3, gen=gen), 1 / 64), r(2 * F, 2 * F, scale=0.3, gen=gen), r(2 * F, gen=gen)
+    mean = r(2 * F, NS, gen=gen)
+    coef = r(4, 2 * F, NS, gen=gen) * torch.tensor([1, 0.3, 0.1, 0.03], dtype=torch.float64)[:, None, None]
+    gr_h = [torch.zeros(2 * F, 2 * F, device="cuda"), torch.zeros(2 * F, 2 * F, device="cuda"), torch.zeros(2 * F, device="cuda")]
+    gr_e = [torch.zeros(2 * F, 2 * F, dtype=torch.float64), torch.zeros(2 * F, 2 * F, dtype=torch.float64), torch.zeros(2 * F, dtype=torch.float64)]
+    gxt_e = r(F, NT, gen=gen)
+    gxt_h = cuda(gxt_e)
+    oh = hb.source_bwd(d, cuda(y), cuda(sc), cuda(sh), cuda(Qt), cuda(Ws1), cuda(Ws2), cuda(bs2), cuda(mean),
+                       cuda(coef), None, None, None, *gr_h, g_xt=gxt_h)
+    oe = emu.source_bwd(de, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, None, None, None, *gr_e, g_xt=gxt_e)
+    close(oh[1], oe[1], rtol=5e-4, name="GzS"); close(gxt_h, gxt_e, rtol=5e-4, name="g_xt(S)")
+    # edge_mlp_bwd + nodes
+    xe = q(r(F, E, scale=2, off=3, gen=gen), 1 / 16)
+    Ps, Pt = q(r(4 * F, NS, gen=gen), 1 / 256), q(r(4 * F, NT, gen=gen), 1 / 256)
+    W1, W2 = q(r(4 * F, 4 * F, scale=0.3, gen=gen), 1 / 64), r(F, 4 * F, scale=0.3, gen=gen)
+    g_tot = r(F, E, gen=gen)
+    alpha, gam0, gam1 = r(F, gen=gen), r(F, gen=gen) * 0.1, r(F, gen=gen) * 0.1
+    gh = [torch.zeros(4 * F, 4 * F, device="cuda"), torch.zeros(F, 4 * F, device="cuda"), torch.zeros(F, device="cuda")]
+    ge = [torch.zeros(4 * F, 4 * F, dtype=torch.float64), torch.zeros(F, 4 * F, dtype=torch.float64), torch.zeros(F, dtype=torch.float64)]
+    nxs_e, nxt_e = r(F, NS, gen=gen), r(F, NT, gen=gen)
+    nxs_h, nxt_h = cuda(nxs_e), cuda(nxt_e)
+    oh = hb.edge_mlp_bwd(d, cuda(g_tot), cuda(alpha), cuda(gam0), cuda(gam1), cuda(y), cuda(xe), None, None,
+                         cuda(Ps), cuda(Pt), cuda(W1), cuda(W2), *gh, want_gxe=False, nodes=(nxs_h, nxt_h))
+    oe = emu.edge_mlp_bwd(de, g_tot, alpha, gam0, gam1, y, xe, None, None, Ps, Pt, W1, W2, *ge, want_gxe=False,
+                          nodes=(nxs_e, nxt_e))
+    torch.cuda.synchronize()
+    for a, b, nm in zip(oh[1:], oe[1:], ["GzEs", "GzEt", "Vu"]):
+        close(a, b, rtol=5e-4, name=nm)
+    close(nxs_h, nxs_e, rtol=5e-4, name="g_xs(E)"); close(nxt_h, nxt_e, rtol=5e-4, name="g_xt(E)")

@@ -1,4 +1,2 @@
-for wb in 256 128 64 32; do
-  PFSGNN_WG_BLOCKS=$wb timeout -k 10 120 python bench.py --no-cpu-baseline --steps 100 > gpurun_out/wb$wb.log 2>&1 || exit 1
-  echo "wb=$wb $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/wb$wb.log)"
-done
+bash tools/gpu_run.sh \
+ "gputests:700:python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k 'epilogues or global_fused'"
