@@ -40,7 +40,10 @@ PRECISION = {
     "valu": "fp32 fmaf chains on the vector ALU; weight gradients bf16x3 MFMA",
     "bf16y": "mfma32 arithmetic with the edge state rounded to bf16",
     "bf16m": "every per-edge contraction a single bf16 MFMA, fp32 accumulation and edge state",
-    "bf16": "single-bf16 MFMA contractions and bf16 edge state (BASELINE configs[4])",
+    "bf16": "single-bf16 MFMA contractions and bf16 edge state",
+    "bf16x3": "every per-edge contraction (forward, backward recompute, gradient chains, weight "
+              "gradients) on bf16 MFMAs with split hi+lo operands (bf16x3, ~2^-16 relative per "
+              "product); fp32 accumulation, edge state, node level and loss (BASELINE configs[4])",
 }
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense fp32-input MFMA (= fp32 vector peak)

@@ -53,7 +53,11 @@ size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F);
  *       bf16 where it is stored (the numerics of bf16 edge-state storage);
  *   PFSGNN_EDGE_BF16 -- every per-edge contraction a single bf16 MFMA (fp32
  *       accumulation) + bf16 edge state (BASELINE configs[4]; Fdim 10);
- *   PFSGNN_EDGE_BF16_MFMA -- the bf16 contractions with the fp32 edge state.
+ *   PFSGNN_EDGE_BF16_MFMA -- the bf16 contractions with the fp32 edge state;
+ *   PFSGNN_EDGE_BF16X3 -- every per-edge contraction, the forward ones and
+ *       their backward recompute included, on v_mfma_f32_16x16x32_bf16 with
+ *       split operands (bf16 hi + lo, ~2^-16 relative per product, fp32
+ *       accumulation and edge state; BASELINE configs[4] at fp32 tolerance).
  * The fp32-class paths (MFMA, MFMA_F32, VALU) produce the same outputs to the
  * parity tolerance; the bf16 paths' deviation is measured, not bounded
  * (DESIGN.md §Numerics).  Node-level ops, reductions and the loss are shared. */
@@ -63,6 +67,7 @@ size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F);
 #define PFSGNN_EDGE_BF16Y 3
 #define PFSGNN_EDGE_BF16 4
 #define PFSGNN_EDGE_BF16_MFMA 5
+#define PFSGNN_EDGE_BF16X3 6
 int pfsgnn_set_edge_path(int path);
 int pfsgnn_get_edge_path(void);
 /* Grid the current edge path launches for a batch (host-only query, for tests

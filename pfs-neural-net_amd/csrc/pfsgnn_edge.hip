@@ -1323,9 +1323,18 @@ int columns_lin(const float* part, int G, int BPG, int NC, int C, float* out, co
 int g_path = PFSGNN_EDGE_MFMA;
 bool use_mfma() { return g_path != PFSGNN_EDGE_VALU; }
 // precision of the MFMA kernels' contractions (pfsgnn_mfma.h) and bf16 edge state
-int mf_prec() {
+// `model`: 0 the EdgeModel kernels, 1 the SModel / TModel ones (a model's
+// forward kernel and its backward recompute always share one precision).
+// Diagnostic knob PFSGNN_X3_MASK (bit per model, default both): which models
+// the bf16x3 path runs bf16x3 forward contractions in (the others as MFMA).
+int mf_prec(int model) {
+  static const int x3mask = [] {
+    const char* e = getenv("PFSGNN_X3_MASK");
+    return e ? atoi(e) : 3;
+  }();
   return g_path == PFSGNN_EDGE_MFMA ? 1
-         : (g_path == PFSGNN_EDGE_BF16 || g_path == PFSGNN_EDGE_BF16_MFMA) ? 2 : 0;
+         : (g_path == PFSGNN_EDGE_BF16 || g_path == PFSGNN_EDGE_BF16_MFMA) ? 2
+         : g_path == PFSGNN_EDGE_BF16X3 ? ((x3mask >> model) & 1 ? 3 : 1) : 0;
 }
 int mf_bfy() { return g_path == PFSGNN_EDGE_BF16Y || g_path == PFSGNN_EDGE_BF16 ? 1 : 0; }
 // MFMA blocks stage their class-table rows in LDS: at most MAX_CPS classes each
@@ -1367,9 +1376,10 @@ EdgeGeo geo_for(int G, int NF, int NC) {
 }  // namespace
 
 extern "C" int pfsgnn_set_edge_path(int path) {
-  if (path < PFSGNN_EDGE_VALU || path > PFSGNN_EDGE_BF16_MFMA)
+  if (path < PFSGNN_EDGE_VALU || path > PFSGNN_EDGE_BF16X3)
     return pf::fail("pfsgnn_set_edge_path",
-                    "path must be PFSGNN_EDGE_VALU, _MFMA, _MFMA_F32, _BF16Y, _BF16 or _BF16_MFMA");
+                    "path must be PFSGNN_EDGE_VALU, _MFMA, _MFMA_F32, _BF16Y, _BF16, _BF16_MFMA "
+                    "or _BF16X3");
   g_path = path;
   return 0;
 }
@@ -1426,7 +1436,7 @@ static int edge_mlp_fwd_impl(int G, int NF, int NC, int F, const float* xe, cons
   if (use_mfma()) {
     PF_REQUIRE(part, "pfsgnn_edge_mlp_fwd", "workspace too small");
     { pf::Timer tm_("edge_mlp_fwd", st);
-    if (int rc = pfm::edge_mlp_fwd(geo, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part, mf_prec(), mf_bfy(), st)) return rc;
+    if (int rc = pfm::edge_mlp_fwd(geo, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part, mf_prec(0), mf_bfy(), st)) return rc;
     tm_.end(); }
     hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(256), 0, st, part, geo.nblocks, F, geo.E,
                        mu, var, bn);
@@ -1482,7 +1492,7 @@ extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, c
   if (use_mfma()) {
     PF_REQUIRE(partS, "pfsgnn_source_fwd", "workspace too small");
     pf::Timer tm_("source_fwd", st);
-    if (int rc = pfm::source_fwd(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, partS, mf_prec(), st)) return rc;
+    if (int rc = pfm::source_fwd(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, partS, mf_prec(1), st)) return rc;
     tm_.end();
   } else {
   const float* QtT = class_rows(Qt, C, geo, w, st);
@@ -1512,7 +1522,7 @@ extern "C" int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, c
   hipStream_t st = as_stream(stream);
   { pf::Timer tm_("target_fwd", st);
   if (use_mfma()) {
-    if (int rc = pfm::target_fwd(geo, F, y, sc, sh, Rs, Wt1, part, mf_prec(), st)) return rc;
+    if (int rc = pfm::target_fwd(geo, F, y, sc, sh, Rs, Wt1, part, mf_prec(1), st)) return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
                                    sc, sh, Rs, Wt1, part));
@@ -1545,7 +1555,7 @@ extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, c
   PF_REQUIRE(part && gz && ghT, "pfsgnn_target_bwd", "workspace too small");
   { pf::Timer tm_("target_bwd", st);
   if (use_mfma()) {
-    if (int rc = pfm::target_bwd(geo, F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part, mf_prec(), st)) return rc;
+    if (int rc = pfm::target_bwd(geo, F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part, mf_prec(1), st)) return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
                                    sc, sh, Rs, Wt1, ghT, gz, gxe, part));
@@ -1674,7 +1684,7 @@ static int source_bwd_impl(int G, int NF, int NC, int F, const float* y, const f
   { pf::Timer tm_("source_bwd", st);
   if (mfma) {
     if (int rc = pfm::source_bwd(geo, F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT,
-                                 g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, mf_prec(), st))
+                                 g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, mf_prec(1), st))
       return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_source_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
@@ -1760,7 +1770,7 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
     PF_REQUIRE(pW2 && pW1 && pCol && gs, "pfsgnn_edge_mlp_bwd", "workspace too small");
     pf::Timer tm_("edge_mlp_bwd", st);
     if (int rc = pfm::edge_mlp_bwd(geo, F, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1,
-                                   W2, gxe, gs, pW2, pW1, pCol, mf_prec(), st))
+                                   W2, gxe, gs, pW2, pW1, pCol, mf_prec(0), st))
       return rc;
     tm_.end();
   } else {

@@ -1,18 +1,20 @@
 // pfsgnn_mfma.hip -- the per-edge kernels of the message-passing block on the
 // matrix cores (the default edge path; pfsgnn_edge.hip holds the fp32 VALU one).
 //
-// Arithmetic.  Every layer-to-layer contraction of gnn.py's per-edge MLPs
-// (EdgeModel gnn.py:86-101, SModel / TModel message MLPs gnn.py:136, 188) and
-// of their backward runs on v_mfma_f32_16x16x4_f32: exact fp32 products, fp32
-// accumulation -- the numerics of an fmaf chain, i.e. of the fp32 VALU path.
-// (bf16 operands, even split hi+lo "bf16x3", are not accurate enough there:
-// SModel's skew / kurtosis features divide by std^3 / std^4 of the message
-// over a fiber's classes and amplify message rounding; measured 6 % gradient
-// deviation against fp64 on small graphs)  The weight
-// gradients -- sums over all edges of outer products -- use
-// v_mfma_f32_16x16x16_bf16 on split operands (v = bf16 hi + bf16 lo, products
-// hi*hi + hi*lo + lo*hi, fp32 accumulate): a product carries ~2^-16 relative
-// error with random sign, which averages out over the edge sum.
+// Arithmetic (PREC, per edge path; include/pfsgnn.h).  The layer-to-layer
+// contractions of gnn.py's per-edge MLPs (EdgeModel gnn.py:86-101, SModel /
+// TModel message MLPs gnn.py:136, 188) and of their backward run either on
+// v_mfma_f32_16x16x4_f32 -- exact fp32 products, fp32 accumulation, the
+// numerics of an fmaf chain (LayerF) -- or on v_mfma_f32_16x16x32_bf16 with
+// split operands v = bf16 hi + bf16 lo and products hi*hi + hi*lo + lo*hi
+// ("bf16x3", ~2^-16 relative per product, fp32 accumulation; LayerB3), at
+// about 5x the fp32 form's K per cycle.  SModel's skew / kurtosis features
+// divide by std^3 / std^4 of a fiber's messages and amplify message rounding,
+// so the precision of every path is measured against the fp64 oracle at the
+// metric shape (tests/test_gpu_precision_table.py).  The
+// weight gradients -- sums over all edges of outer products -- are bf16x3 on
+// every path: a product's ~2^-16 relative error has a random sign and
+// averages out over the edge sum.
 //
 // Tile geometry.  Canonical edge order is class-major, e = (g*NC + c)*NF + f
 // (channel-major [C][E] tensors), as in pfsgnn_edge.hip.  A 256-thread block
@@ -137,18 +139,11 @@ __device__ __forceinline__ Fr split(const floatx4& v) {
                    (__bf16)(v[2] - bf_f(hs[2])), (__bf16)(v[3] - bf_f(hs[3]))};
   return {hs, __builtin_bit_cast(s16x4, l)};
 }
-__device__ __forceinline__ floatx4 mf(s16x4 a, s16x4 b, floatx4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
-}
-// c += A B with A = Ah + Al, B = Bh + Bl (Al*Bl dropped); small terms first
-__device__ __forceinline__ floatx4 mma3(const Fr& a, const Fr& b, floatx4 c) {
-  c = mf(a.l, b.h, c);
-  c = mf(a.h, b.l, c);
-  return mf(a.h, b.h, c);
-}
 // the 16x16x32 form: lane (g, i) holds A[i][k = 8g + q], B[k = 8g + q][i], q = 0..7;
-// slot q of a K-tile pair is slot q & 3 of tile q >> 2, so a pair of 16x16x16
-// operands concatenates into one 16x16x32 operand with the same k <-> slot map
+// element q of an 8-wide operand is slot q & 3 of half q >> 2, and a product
+// sums over every (lane group, element) position, so two 4-slot halves (two
+// K-tiles, or the hi and lo planes of one) concatenate into one operand as
+// long as A and B put matching halves in the same place
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 b16x8 __attribute__((ext_vector_type(8)));
 struct Fr8 {
@@ -167,29 +162,28 @@ __device__ __forceinline__ floatx4 mma3w(const Fr8& a, const Fr8& b, floatx4 c) 
   c = mf8(a.h, b.l, c);
   return mf8(a.h, b.h, c);
 }
-// bf16 1.0 in every element: B operand that sums an A image over its 16 edges
-__device__ __forceinline__ s16x4 ones16() {
-  return s16x4{(short)0x3F80, (short)0x3F80, (short)0x3F80, (short)0x3F80};
-}
-
 // ------------------------------------------------------------ bf16x3 layer
-// y (+)= W x for the GRADIENT chains of the backward kernels (PFSGNN_EDGE_MFMA):
-// v_mfma_f32_16x16x16_bf16 on split operands, ~2^-16 relative per product
-// (the forward values and their recompute stay exact fp32: LayerF).  K-step
-// u of v_mfma_f32_16x16x16 takes the 4 slots 4u..4u+3 of every lane group, so
-// a D-row input costs GM<D>::NT steps (20 -> 2, 40 -> 3) instead of
-// GM<D>::RPG fp32 steps (5, 10); the input is the lane's own floatx4 tiles,
-// split once (the same splits feed the weight-gradient images).
+// y (+)= W x with split operands (W = Wh + Wl, x = xh + xl, products
+// Wh xh + Wh xl + Wl xh, ~2^-16 relative each, fp32 accumulation) on
+// v_mfma_f32_16x16x32_bf16: the backward's gradient chains (PREC 1), and every
+// per-edge contraction, forward and recompute included (PREC 3).  K-step u of
+// a 16-deep bf16 operand takes the 4 slots 4u..4u+3 of every lane group, so a
+// D-row input is GM<D>::NT K-tiles (10 -> 1, 20 -> 2, 40 -> 3) where the fp32
+// form takes GM<D>::RPG steps (3, 5, 10).  The 3 partial products of a K-tile
+// are 3 halves of a 16x16x32 MFMA (twice the K of 16x16x16 in the same cycles:
+// tools/mfma_cycles.hip); they are packed so that KT K-tiles cost
+// ceil(3 KT / 2) MFMAs:
+//   * a pair of K-tiles (2p, 2p+1): A = [Wh_2p | Wh_2p+1] and [Wl_2p | Wl_2p+1]
+//     against B = [xh | xh] and [xl | xl]: 3 MFMAs for 6 halves;
+//   * an odd last K-tile u: A = [Wh_u | Wl_u] against B = [xl_u | xh_u]
+//     (Wh xl + Wl xh) and against [xh_u | 0] (Wh xh): 2 MFMAs for 3 halves.
+// Every MFMA of a chain is the one 16x16x32 form (DESIGN.md §MFMA form mixing).
 template <int M, int K>
 struct LayerB3 {
-  static constexpr int MT = GM<M>::NT, KT = GM<K>::NT, KP = (KT + 1) / 2;
-  // K-tile pairs on v_mfma_f32_16x16x32_bf16 (twice the K of the 16x16x16 form
-  // in the same cycles: tools/mfma_cycles.hip; pairing checked bitwise by
-  // tools/mfma_pair_check.hip); an odd last K-tile is paired with zeros.  (A
-  // 16x16x16 finishing a chain of 16x16x32s on the same accumulator gave wrong
-  // sums on gfx950 -- the edge op tests at F = 10, K = 40 -- so a chain stays
-  // on the one MFMA form.)
-  Fr8 ap[MT][KP];
+  static constexpr int MT = GM<M>::NT, KT = GM<K>::NT, KP = KT / 2;
+  static constexpr bool ODD = (KT & 1) != 0;
+  Fr8 ap[MT][KP > 0 ? KP : 1];   // K-tile pairs
+  s16x8 ao[MT];                  // odd last K-tile: [Wh | Wl]
   template <class Fn>
   __device__ __forceinline__ void load(Fn fn, int lane) {
     const int g = lane >> 4, i = lane & 15;
@@ -207,18 +201,47 @@ struct LayerB3 {
         a[u] = split(v);
       }
 #pragma unroll
-      for (int p = 0; p < KP; ++p) ap[t][p] = cat(a[2 * p], 2 * p + 1 < KT ? a[2 * p + 1] : Fr{});
+      for (int p = 0; p < KP; ++p) ap[t][p] = cat(a[2 * p], a[2 * p + 1]);
+      if constexpr (ODD) ao[t] = cat8(a[KT - 1].h, a[KT - 1].l);
     }
   }
   __device__ __forceinline__ void apply(const Fr (&x)[KT], floatx4 (&y)[MT]) const {
 #pragma unroll
     for (int p = 0; p < KP; ++p) {
-      const Fr8 xp = cat(x[2 * p], 2 * p + 1 < KT ? x[2 * p + 1] : Fr{});
+      const Fr8 xp = cat(x[2 * p], x[2 * p + 1]);
 #pragma unroll
       for (int t = 0; t < MT; ++t) y[t] = mma3w(ap[t][p], xp, y[t]);
     }
+    if constexpr (ODD) {
+      const s16x8 xlh = cat8(x[KT - 1].l, x[KT - 1].h), xh0 = cat8(x[KT - 1].h, s16x4{});
+#pragma unroll
+      for (int t = 0; t < MT; ++t) y[t] = mf8(ao[t], xh0, mf8(ao[t], xlh, y[t]));
+    }
+  }
+  // fp32 input tiles, split here (PREC 3 forward / recompute)
+  __device__ __forceinline__ void apply(const floatx4 (&x)[KT], floatx4 (&y)[MT]) const {
+    Fr s[KT];
+#pragma unroll
+    for (int u = 0; u < KT; ++u) s[u] = split(x[u]);
+    apply(s, y);
   }
 };
+
+// ------------------------------------------------------------ weight gradients
+// acc += A B^T summed over a tile's 16 edges (edge = MFMA K), A and B read from
+// wave-private bf16 images (hi and lo planes), as 2 v_mfma_f32_16x16x32_bf16:
+// [Ah | Al] . [Bl | Bh] (Ah Bl + Al Bh) and [Ah | Al] . [Bh | 0] (Ah Bh).
+// The A tuple [Ah | Al] against ones gives A's sums over the 16 edges (hi + lo).
+__device__ __forceinline__ s16x8 ones8() {
+  const short o = (short)0x3F80;
+  return s16x8{o, o, o, o, o, o, o, o};
+}
+struct WgB {
+  s16x8 lh, h0;   // [Bl | Bh], [Bh | 0]
+};
+__device__ __forceinline__ floatx4 mma3g(s16x8 a_hl, const WgB& b, floatx4 c) {
+  return mf8(a_hl, b.h0, mf8(a_hl, b.lh, c));
+}
 
 // ------------------------------------------------------------ bf16 layer
 // y (+)= W x with every product a single v_mfma_f32_16x16x16_bf16 on bf16
@@ -274,12 +297,18 @@ struct LayerB1 {
 // Precision of the per-edge contractions (PREC, per edge path):
 //   0 exact fp32 everywhere (PFSGNN_EDGE_MFMA_F32, _BF16Y);
 //   1 forward fp32, backward gradient chains bf16x3 (PFSGNN_EDGE_MFMA);
-//   2 every contraction single bf16 (PFSGNN_EDGE_BF16).
+//   2 every contraction single bf16 (PFSGNN_EDGE_BF16);
+//   3 every contraction bf16x3, forward and recompute included (PFSGNN_EDGE_BF16X3).
+// The forward layers of a backward kernel (its recompute) use FwdLayer<FP(PREC)>,
+// exactly the arithmetic of the forward kernel, so the recomputed activations
+// and LeakyReLU masks are bitwise those of the forward pass.
+__host__ __device__ constexpr int FP(int prec) { return prec == 2 ? 2 : prec == 3 ? 3 : 0; }
 template <int PREC, int M, int K>
-using FwdLayer = std::conditional_t<PREC == 2, LayerB1<M, K>, LayerF<M, K>>;
+using FwdLayer = std::conditional_t<
+    PREC == 2, LayerB1<M, K>, std::conditional_t<PREC == 3, LayerB3<M, K>, LayerF<M, K>>>;
 template <int PREC, int M, int K>
-using GradLayer = std::conditional_t<PREC == 0, LayerF<M, K>,
-                                     std::conditional_t<PREC == 1, LayerB3<M, K>, LayerB1<M, K>>>;
+using GradLayer = std::conditional_t<
+    PREC == 0, LayerF<M, K>, std::conditional_t<PREC == 2, LayerB1<M, K>, LayerB3<M, K>>>;
 
 // Wave-private image of one 16x16 bf16 block, [16 edges][16 slots] (32-byte
 // rows, the four 8-byte chunks of row e XOR-swizzled by e>>2: conflict-free b64
@@ -303,6 +332,15 @@ __device__ __forceinline__ void img_put2(short* img, int lane, const Fr& v) {
 }
 __device__ __forceinline__ Fr img_tr2(const short* img, int lane) {
   return {img_tr(img, lane), img_tr(img + IMG_SHORTS, lane)};
+}
+// weight-gradient operands from an image (mma3g): A side [hi | lo]; B side
+// [lo | hi] and [hi | 0]
+__device__ __forceinline__ s16x8 img_trA(const short* img, int lane) {
+  return cat8(img_tr(img, lane), img_tr(img + IMG_SHORTS, lane));
+}
+__device__ __forceinline__ WgB img_trB(const short* img, int lane) {
+  const s16x4 h = img_tr(img, lane);
+  return {cat8(img_tr(img + IMG_SHORTS, lane), h), cat8(h, s16x4{})};
 }
 // compiler-only ordering point between a wave's image writes and its reads
 // (one wave's LDS operations execute in order)
@@ -591,7 +629,7 @@ __global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float*
     st_frows<F>(y, eo, RB, g4, fvalid, yo[0]);
     if (fvalid) {
       cnt += 1.f;
-      const float rc = 1.0f / cnt;
+      const float rc = __builtin_amdgcn_rcpf(cnt);   // v_rcp_f32 (<= 1 ulp): a Welford weight
 #pragma unroll
       for (int r = 0; r < GM<F>::RPG; ++r) {
         const float d = yo[0][r] - mean[r];
@@ -694,7 +732,7 @@ __global__ __launch_bounds__(256) void km_source_fwd(EdgeGeo geo, const float* _
     L2.apply(a, m);
     const float nold = cnt;
     cnt += 1.f;
-    const float inv = 1.f / cnt, a3 = cnt - 2.f, a4 = cnt * cnt - 3.f * cnt + 3.f;
+    const float inv = __builtin_amdgcn_rcpf(cnt), a3 = cnt - 2.f, a4 = cnt * cnt - 3.f * cnt + 3.f;
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
@@ -796,7 +834,7 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
   __shared__ __attribute__((aligned(16))) float ghl[MF_MAX_CPS * ClassRows<C>::CP];
   ClassRows<C>::stage(ghl, ghS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
   short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
-  FwdLayer<PREC == 2 ? 2 : 0, C, F> L1;
+  FwdLayer<FP(PREC), C, F> L1;
   L1.load([&](int h, int k) { return Wt1[h * 2 * F + F + k]; }, lane);
   GradLayer<PREC, F, C> LT;
   LT.load([&](int k, int h) { return gxe ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
@@ -844,10 +882,10 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
     for (int tt = 0; tt < NT; ++tt) img_put2(img + tt * 2 * IMG_SHORTS, lane, sgz[tt]);
     img_put2(img + NT * 2 * IMG_SHORTS, lane, split(x[0]));
     lds_order();
-    const Fr tx = img_tr2(img + NT * 2 * IMG_SHORTS, lane);
+    const WgB tx = img_trB(img + NT * 2 * IMG_SHORTS, lane);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt)
-      accW[tt] = mma3(img_tr2(img + tt * 2 * IMG_SHORTS, lane), tx, accW[tt]);
+      accW[tt] = mma3g(img_trA(img + tt * 2 * IMG_SHORTS, lane), tx, accW[tt]);
   });
   if (fvalid) {
 #pragma unroll
@@ -899,10 +937,10 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   const long long CNS = (long long)C * NS;
   const bool tpart = Rs != nullptr;
 
-  FwdLayer<PREC == 2 ? 2 : 0, C, F> L1s, L1t;
+  FwdLayer<FP(PREC), C, F> L1s, L1t;
   L1s.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
   L1t.load([&](int h, int k) { return tpart ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
-  FwdLayer<PREC == 2 ? 2 : 0, C, C> L2;
+  FwdLayer<FP(PREC), C, C> L2;
   L2.load([&](int o, int h) { return Ws2[o * C + h]; }, lane);
   // gradient chains: exact fp32, bf16x3 or bf16 by PREC
   GradLayer<PREC, C, C> L2T;
@@ -1028,19 +1066,19 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     }
     // ---- weight gradients (edge = K) through the transposed images
     lds_order();
-    const Fr tx = img_tr2(im_x, lane);
-    Fr ta[NT];
+    const WgB tx = img_trB(im_x, lane);
+    WgB ta[NT];
 #pragma unroll
-    for (int nb = 0; nb < NT; ++nb) ta[nb] = img_tr2(im_a + nb * 2 * IMG_SHORTS, lane);
+    for (int nb = 0; nb < NT; ++nb) ta[nb] = img_trB(im_a + nb * 2 * IMG_SHORTS, lane);
     const int cl = c - cbase;
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      const Fr tgm = img_tr2(im_gm + tt * 2 * IMG_SHORTS, lane);
+      const s16x8 tgm = img_trA(im_gm + tt * 2 * IMG_SHORTS, lane);
 #pragma unroll
-      for (int nb = 0; nb < NT; ++nb) accW2[tt * NT + nb] = mma3(tgm, ta[nb], accW2[tt * NT + nb]);
-      const Fr tgz = img_tr2(im_gz + tt * 2 * IMG_SHORTS, lane);
-      accW1[tt] = mma3(tgz, tx, accW1[tt]);
-      const floatx4 cs = mf(tgz.h, ones16(), mf(tgz.l, ones16(), zero4()));
+      for (int nb = 0; nb < NT; ++nb) accW2[tt * NT + nb] = mma3g(tgm, ta[nb], accW2[tt * NT + nb]);
+      const s16x8 tgz = img_trA(im_gz + tt * 2 * IMG_SHORTS, lane);
+      accW1[tt] = mma3g(tgz, tx, accW1[tt]);
+      const floatx4 cs = mf8(tgz, ones8(), zero4());
       if (j16 == 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1125,7 +1163,7 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
   short* im_gz = im_a + NT * 2 * IMG_SHORTS;
   short* im_x = im_gz + NT * 2 * IMG_SHORTS;
 
-  FwdLayer<PREC == 2 ? 2 : 0, H, F> L1;
+  FwdLayer<FP(PREC), H, F> L1;
   L1.load([&](int h, int k) { return W1[h * 4 * F + 2 * F + k]; }, lane);
   // gradient chains: exact fp32, bf16x3 or bf16 by PREC
   GradLayer<PREC, H, F> L2T;
@@ -1198,17 +1236,17 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
       if constexpr (PREC >= 1) L1T.apply(sgz, gx); else L1T.apply(gz, gx);
       st_frows<F>(gxe, eo, RB, g4, fvalid, gx[0]);
     }
-    const Fr tgy = img_tr2(im_gy, lane);
+    const s16x8 tgy = img_trA(im_gy, lane);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt)
-      accW2[tt] = mma3(tgy, img_tr2(im_a + tt * 2 * IMG_SHORTS, lane), accW2[tt]);
-    const Fr tx = img_tr2(im_x, lane);
+      accW2[tt] = mma3g(tgy, img_trB(im_a + tt * 2 * IMG_SHORTS, lane), accW2[tt]);
+    const WgB tx = img_trB(im_x, lane);
     const int cl = c - cbase;
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      const Fr tgz = img_tr2(im_gz + tt * 2 * IMG_SHORTS, lane);
-      accW1[tt] = mma3(tgz, tx, accW1[tt]);
-      const floatx4 cs = mf(tgz.h, ones16(), mf(tgz.l, ones16(), zero4()));
+      const s16x8 tgz = img_trA(im_gz + tt * 2 * IMG_SHORTS, lane);
+      accW1[tt] = mma3g(tgz, tx, accW1[tt]);
+      const floatx4 cs = mf8(tgz, ones8(), zero4());
       if (j16 == 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1271,15 +1309,15 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
   switch ((F) * 4 + (P)) {                                                        \
     MF_CASE(8, 0, K, __VA_ARGS__) MF_CASE(8, 1, K, __VA_ARGS__)                  \
     MF_CASE(10, 0, K, __VA_ARGS__) MF_CASE(10, 1, K, __VA_ARGS__)                \
-    MF_CASE(10, 2, K, __VA_ARGS__)                                                \
+    MF_CASE(10, 2, K, __VA_ARGS__) MF_CASE(10, 3, K, __VA_ARGS__)                \
     MF_CASE(16, 0, K, __VA_ARGS__) MF_CASE(16, 1, K, __VA_ARGS__)                \
     default: return pf::fail("pfsgnn mfma", "unsupported Fdim for this edge path"); \
   }
 
 namespace pfm {
 
-// forward kernels only distinguish single-bf16 (2) from fp32 (0, 1)
-static inline int fwd_prec(int prec) { return prec == 2 ? 2 : 0; }
+// forward kernels only distinguish fp32 (0, 1), single bf16 (2) and bf16x3 (3)
+static inline int fwd_prec(int prec) { return FP(prec); }
 
 int edge_mlp_fwd(const EdgeGeo& geo, int F, const float* xe, const float* xsc, const float* xsh,
                  const float* Ps, const float* PtS, const float* W1, const float* W2,

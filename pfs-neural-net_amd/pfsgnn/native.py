@@ -183,7 +183,7 @@ def lib():
     return _lib
 
 
-EDGE_PATHS = {"valu": 0, "mfma": 1, "mfma32": 2, "bf16y": 3, "bf16": 4, "bf16m": 5}
+EDGE_PATHS = {"valu": 0, "mfma": 1, "mfma32": 2, "bf16y": 3, "bf16": 4, "bf16m": 5, "bf16x3": 6}
 
 
 def set_edge_path(path):
@@ -191,8 +191,10 @@ def set_edge_path(path):
     exact fp32 forward products, bf16x3 gradient chains), "mfma32" (matrix
     cores, every layer product exact fp32), "valu" (fp32 fmaf chains), "bf16y"
     (mfma32 with the edge state rounded to bf16), "bf16m" (single-bf16 MFMA
-    contractions) or "bf16" (bf16m + bf16 edge state; BASELINE configs[4],
-    Fdim 10).
+    contractions), "bf16" (bf16m + bf16 edge state) or "bf16x3" (every
+    per-edge contraction on bf16 MFMAs with split hi + lo operands, forward and
+    recompute included; BASELINE configs[4] at fp32 tolerance).  The bf16
+    paths are built for Fdim 10.
     Read at launch time; env PFSGNN_EDGE_PATH sets it when the library loads."""
     if path not in EDGE_PATHS:
         raise ValueError(f"edge path must be one of {sorted(EDGE_PATHS)}, got {path!r}")

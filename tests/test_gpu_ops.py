@@ -44,7 +44,7 @@ def dims(G, NF, NC, F=10):
     return Dims(G, NF, NC, F), EDims(G, NF, NC, F)
 
 
-@pytest.fixture(params=["mfma", "mfma32", "valu"])
+@pytest.fixture(params=["mfma", "mfma32", "valu", "bf16x3"])
 def prec(request):
     import pfsgnn
     pfsgnn.set_edge_path(request.param)
@@ -58,11 +58,15 @@ EDGE_CASES = [(G, NF, NC, 10) for G, NF, NC in GEOMS] + [(2, 50, 16, 8), (1, 33,
 
 @pytest.mark.parametrize("G,NF,NC,F", EDGE_CASES)
 def test_edge_ops(hb, prec, G, NF, NC, F):
-    """Every per-edge kernel on both paths (fp32 VALU, MFMA)
-    against the float64 emulation, at every supported Fdim."""
+    """Every per-edge kernel on every fp32-class path (fp32 VALU, MFMA, the
+    bf16x3 contractions) against the float64 emulation, at every supported
+    Fdim (the bf16 paths are built for Fdim 10)."""
+    if prec == "bf16x3" and F != 10:
+        pytest.skip("bf16 edge paths are instantiated for Fdim 10")
     gen = torch.Generator().manual_seed(G * 1000 + NF * 10 + NC + F)
     # Inputs on a grid on which every FIRST-layer pre-activation is computed exactly
-    # by all three paths (fp64 emulation, fp32 fmaf chains, fp32 MFMA): weights
+    # by every path (fp64 emulation, fp32 fmaf chains, fp32 MFMA, and bf16x3,
+    # whose hi + lo split holds a 16-bit significand exactly): weights
     # bf16-exact (multiples of 1/64, |w| < 2), edge inputs with <= 16 significant
     # bits, node parts on a 1/256 grid, sums below 2^24 grid units.  LeakyReLU's
     # slope then switches on the same edges in every path; on random data an edge

@@ -9,6 +9,8 @@ oracle, for every edge path:
   bf16y   mfma32 arithmetic, edge state y rounded to bf16 (bf16 storage numerics)
   bf16m   single-bf16 MFMA for every per-edge contraction, fp32 edge state
   bf16    single-bf16 MFMA contractions + bf16 edge state
+  bf16x3  every per-edge contraction (forward, recompute, gradient chains)
+          on bf16 MFMAs with split hi + lo operands, fp32 edge state
 
 For each path and compared tensor it records max|ours - oracle64| / scale and /
 max|oracle32 - oracle64|; the worst over all tensors is the path's line.  The
@@ -55,7 +57,7 @@ def _tensors(m, out, loss):
 TABLE = {}
 
 
-@pytest.mark.parametrize("path", ["mfma32", "mfma", "valu", "bf16y", "bf16m", "bf16"])
+@pytest.mark.parametrize("path", ["mfma32", "mfma", "valu", "bf16x3", "bf16y", "bf16m", "bf16"])
 def test_precision_line(oracle, path):
     import pfsgnn
     model, graph, seed, r64, r32 = oracle
