@@ -243,10 +243,10 @@ def main():
         return loss
 
     def step():
+        sync_buffers(gnn)          # DDP broadcast_buffers, before the forward (no-op at N=1)
         loss = fwd_bwd()
         allreduce_gradients(gnn)
         opt.step()
-        sync_buffers(gnn)          # DDP broadcast_buffers semantics (no-op at N=1)
         return loss
 
     for i in range(args.warmup):
@@ -271,11 +271,12 @@ def main():
         torch.cuda.synchronize()
 
         def step():  # noqa: F811
+            if world > 1:
+                sync_buffers(gnn)
             graph.replay()
             if world > 1:
                 allreduce_gradients(gnn)
                 opt.step()
-                sync_buffers(gnn)
             return static_loss
 
         step()
@@ -297,6 +298,21 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     assert torch.isfinite(loss).item(), "non-finite loss"
+    consistency = None
+    if world > 1:
+        # every rank must end the K steps with bitwise the same parameters
+        # (one all-reduce, the same Adam) and, after the buffer broadcast that
+        # opens the next step, the same BatchNorm buffers
+        sync_buffers(gnn)
+        flat = gnn.flat_parameters()[0]
+        bufs = torch.cat([b.detach().double().reshape(-1) for b in gnn.buffers()])
+        consistency = {}
+        for name, t in (("parameters", flat.double()), ("buffers", bufs)):
+            hi, lo = t.clone(), t.clone()
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+            consistency[name + "_bitwise_equal"] = bool(torch.equal(hi, lo))
+        assert all(consistency.values()), consistency
 
     # ---- per-kernel device times: HIP events around each main kernel, on its
     # launch stream, over a few eager steps of the same workload right after
@@ -373,6 +389,8 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if consistency is not None:
+            line["rank_consistency"] = consistency
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

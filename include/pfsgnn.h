@@ -430,14 +430,21 @@ int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, const float*
 int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                       const float* sh, const float* Rs, const float* Wt1, float* hsum,
                       const float* Wt2, const float* bt2, float bscale, float* agg,
-                      void* ws, size_t ws_bytes, void* stream);
+                      unsigned char* tmask, void* ws, size_t ws_bytes, void* stream);
+/* Bytes of the TModel mask the current edge path keeps between the forward
+ * and the backward (0: it keeps none, recomputes).  When non-zero and `tmask`
+ * (this many bytes) is given to pfsgnn_target_fwd, the forward writes the
+ * sign pattern of TModel's per-edge pre-activation (gnn.py:188, the LeakyReLU
+ * of node_mlp_1) and pfsgnn_target_bwd / pfsgnn_source_bwd(_bn) given the
+ * same buffer read it in place of recomputing that layer. */
+size_t pfsgnn_tmask_bytes(int G, int NF, int NC, int F);
 /* TModel edge backward: GzT[:,f] = sum_c g_z; dWt1[:,F:2F] += sum g_z x^T;
  * optional gxe = Wt1[:,F:2F]^T g_z (standalone TModel only); optional g_xs
  * += Wt1[:,0:F]^T GzT (the x_s[src] input gradient, in the reduction epilogue). */
 int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                       const float* sh, const float* Rs, const float* Wt1, const float* g_hsum,
-                      float* GzT, float* dWt1, float* gxe, float* g_xs, void* ws,
-                      size_t ws_bytes, void* stream);
+                      float* GzT, float* dWt1, float* gxe, float* g_xs,
+                      const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream);
 /* SModel edge backward fused with TModel's per-edge input gradient, the
  * downstream edge gradient and the edge BatchNorm's two gradient sums:
  * g_tot = Ws1e^T g_zs + [Wt1e^T g_zt] + [g_next]; GzS per class;
@@ -450,7 +457,8 @@ int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, const float*
                       const float* Wt1, const float* g_hsum, const float* g_next,
                       const float* mu1, const float* inv1, float* g_tot, float* GzS,
                       float* dWs1, float* dWs2, float* dbs2, float* Sg, float* Sgx,
-                      float* g_xt, void* ws, size_t ws_bytes, void* stream);
+                      float* g_xt, const unsigned char* tmask, void* ws, size_t ws_bytes,
+                      void* stream);
 /* the same with the edge BatchNorm's backward finished in the same call: in
  * place of Sg / Sgx it writes pfsgnn_bn2_bwd_coef's alpha, gam0, gam1 and
  * accumulates dgamma / dbeta (gamma, var1: that BatchNorm's weight and batch
@@ -462,8 +470,8 @@ int pfsgnn_source_bwd_bn(int G, int NF, int NC, int F, const float* y, const flo
                          const float* mu1, const float* inv1, const float* var1,
                          const float* gamma, long long n, float eps, float* g_tot, float* GzS,
                          float* dWs1, float* dWs2, float* dbs2, float* alpha, float* gam0,
-                         float* gam1, float* dgamma, float* dbeta, float* g_xt, void* ws,
-                         size_t ws_bytes, void* stream);
+                         float* gam1, float* dgamma, float* dbeta, float* g_xt,
+                         const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream);
 /* Sg = sum g, Sgx = sum g*(y-mu1)*inv1 (standalone EdgeModel backward). */
 int pfsgnn_edge_bn_grad_sums(int G, int NF, int NC, int F, const float* g, const float* y,
                              const float* mu1, const float* inv1, float* Sg, float* Sgx,

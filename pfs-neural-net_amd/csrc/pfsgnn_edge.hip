@@ -323,6 +323,7 @@ struct Bn2Args {
 };
 
 #define MF_PB 16  // partials per thread (nb <= 4096 in one round: the edge grids)
+static_assert(256 * MF_PB == 4096, "MF_PB: one round of the partial loop covers 4096 blocks");
 __global__ __launch_bounds__(256) void k_moments_finalize(const float* __restrict__ part, int nb,
                                                           int F, long long n,
                                                           float* __restrict__ mu,
@@ -331,7 +332,7 @@ __global__ __launch_bounds__(256) void k_moments_finalize(const float* __restric
   __shared__ double red[256];
   float pc[MF_PB], pm[MF_PB], pq[MF_PB];
   double S = 0.0, Q = 0.0;
-  for (int b0 = 0; b0 < nb; b0 += 256 * MF_PB) {   // one round for nb <= 2048
+  for (int b0 = 0; b0 < nb; b0 += 256 * MF_PB) {   // one round for nb <= 256 * MF_PB = 4096
 #pragma unroll
     for (int i = 0; i < MF_PB; ++i) {
       const int b = b0 + t + 256 * i;
@@ -1509,10 +1510,15 @@ extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, c
   return pf::check_launch("pfsgnn_source_fwd");
 }
 
+extern "C" size_t pfsgnn_tmask_bytes(int G, int NF, int NC, int F) {
+  if (G <= 0 || NF <= 0 || NC <= 0 || F <= 0 || 2 * F > 32 || !use_mfma()) return 0;
+  return (size_t)G * NF * NC * 4;   // one byte per (edge, lane group), pfsgnn_mfma.hip mask_bits
+}
+
 extern "C" int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                                  const float* sh, const float* Rs, const float* Wt1, float* hsum,
                                  const float* Wt2, const float* bt2, float bscale, float* agg,
-                                 void* ws, size_t ws_bytes, void* stream) {
+                                 unsigned char* tmask, void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_target_fwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(y && Rs && Wt1 && hsum, "pfsgnn_target_fwd", "null");
   const EdgeGeo geo = geo_for(G, NF, NC);
@@ -1522,7 +1528,7 @@ extern "C" int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, c
   hipStream_t st = as_stream(stream);
   { pf::Timer tm_("target_fwd", st);
   if (use_mfma()) {
-    if (int rc = pfm::target_fwd(geo, F, y, sc, sh, Rs, Wt1, part, mf_prec(1), st)) return rc;
+    if (int rc = pfm::target_fwd(geo, F, y, sc, sh, Rs, Wt1, part, tmask, mf_prec(1), st)) return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
                                    sc, sh, Rs, Wt1, part));
@@ -1539,7 +1545,8 @@ extern "C" int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, c
 extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                                  const float* sh, const float* Rs, const float* Wt1,
                                  const float* g_hsum, float* GzT, float* dWt1, float* gxe,
-                                 float* g_xs, void* ws, size_t ws_bytes, void* stream) {
+                                 float* g_xs, const unsigned char* tmask, void* ws,
+                                 size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_target_bwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(y && Rs && Wt1 && g_hsum && GzT && dWt1, "pfsgnn_target_bwd", "null");
   const EdgeGeo geo = geo_for(G, NF, NC);
@@ -1555,7 +1562,9 @@ extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, c
   PF_REQUIRE(part && gz && ghT, "pfsgnn_target_bwd", "workspace too small");
   { pf::Timer tm_("target_bwd", st);
   if (use_mfma()) {
-    if (int rc = pfm::target_bwd(geo, F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part, mf_prec(1), st)) return rc;
+    if (int rc = pfm::target_bwd(geo, F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part, tmask,
+                                 mf_prec(1), st))
+      return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
                                    sc, sh, Rs, Wt1, ghT, gz, gxe, part));
@@ -1618,7 +1627,8 @@ static int source_bwd_impl(int G, int NF, int NC, int F, const float* y, const f
                            const float* Wt1, const float* g_hsum, const float* g_next,
                            const float* mu1, const float* inv1, float* g_tot, float* GzS,
                            float* dWs1, float* dWs2, float* dbs2, float* Sg, float* Sgx,
-                           const Bn2Bwd* bb, float* g_xt, void* ws, size_t ws_bytes, void* stream);
+                           const Bn2Bwd* bb, float* g_xt, const unsigned char* tmask, void* ws,
+                           size_t ws_bytes, void* stream);
 
 extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                                  const float* sh, const float* Qt, const float* Ws1,
@@ -1627,10 +1637,11 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
                                  const float* g_hsum, const float* g_next, const float* mu1,
                                  const float* inv1, float* g_tot, float* GzS, float* dWs1,
                                  float* dWs2, float* dbs2, float* Sg, float* Sgx, float* g_xt,
-                                 void* ws, size_t ws_bytes, void* stream) {
+                                 const unsigned char* tmask, void* ws, size_t ws_bytes,
+                                 void* stream) {
   return source_bwd_impl(G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, g_hsum,
                          g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, Sg, Sgx, nullptr, g_xt,
-                         ws, ws_bytes, stream);
+                         tmask, ws, ws_bytes, stream);
 }
 
 extern "C" int pfsgnn_source_bwd_bn(int G, int NF, int NC, int F, const float* y, const float* sc,
@@ -1642,13 +1653,14 @@ extern "C" int pfsgnn_source_bwd_bn(int G, int NF, int NC, int F, const float* y
                                     long long n, float eps, float* g_tot, float* GzS, float* dWs1,
                                     float* dWs2, float* dbs2, float* alpha, float* gam0,
                                     float* gam1, float* dgamma, float* dbeta, float* g_xt,
-                                    void* ws, size_t ws_bytes, void* stream) {
+                                    const unsigned char* tmask, void* ws, size_t ws_bytes,
+                                    void* stream) {
   PF_REQUIRE(mu1 && inv1 && var1 && gamma && n > 0 && alpha && gam0 && gam1 && dgamma && dbeta,
              "pfsgnn_source_bwd_bn", "null");
   const Bn2Bwd bb{gamma, mu1, var1, n, eps, alpha, gam0, gam1, dgamma, dbeta};
   return source_bwd_impl(G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, g_hsum,
                          g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, nullptr, nullptr, &bb,
-                         g_xt, ws, ws_bytes, stream);
+                         g_xt, tmask, ws, ws_bytes, stream);
 }
 
 static int source_bwd_impl(int G, int NF, int NC, int F, const float* y, const float* sc,
@@ -1657,7 +1669,8 @@ static int source_bwd_impl(int G, int NF, int NC, int F, const float* y, const f
                            const float* Wt1, const float* g_hsum, const float* g_next,
                            const float* mu1, const float* inv1, float* g_tot, float* GzS,
                            float* dWs1, float* dWs2, float* dbs2, float* Sg, float* Sgx,
-                           const Bn2Bwd* bb, float* g_xt, void* ws, size_t ws_bytes, void* stream) {
+                           const Bn2Bwd* bb, float* g_xt, const unsigned char* tmask, void* ws,
+                           size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_source_bwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(y && Qt && Ws1 && Ws2 && bs2 && mean && coef && g_tot && GzS && dWs1 && dWs2 && dbs2,
              "pfsgnn_source_bwd", "null");
@@ -1684,7 +1697,8 @@ static int source_bwd_impl(int G, int NF, int NC, int F, const float* y, const f
   { pf::Timer tm_("source_bwd", st);
   if (mfma) {
     if (int rc = pfm::source_bwd(geo, F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT,
-                                 g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, mf_prec(1), st))
+                                 g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask,
+                                 mf_prec(1), st))
       return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_source_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,

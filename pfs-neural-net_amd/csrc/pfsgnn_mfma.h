@@ -25,17 +25,21 @@ int edge_mlp_fwd(const EdgeGeo& geo, int F, const float* xe, const float* xsc, c
 int source_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
                float* partS, int prec, hipStream_t st);
+// TModel's LeakyReLU mask (pfsgnn_mfma.hip mask_bits): target_fwd writes it
+// when `tmask` is non-null (4 bytes per edge), target_bwd / source_bwd read
+// it in place of recomputing that layer when non-null
 int target_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
-               const float* Rs, const float* Wt1, float* part, int prec, hipStream_t st);
+               const float* Rs, const float* Wt1, float* part, uint8_t* tmask, int prec,
+               hipStream_t st);
 int target_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* Rs, const float* Wt1, const float* ghS, float* gz, float* gxe,
-               float* part, int prec, hipStream_t st);
+               float* part, const uint8_t* tmask, int prec, hipStream_t st);
 int source_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
                const float* mean, const float* coef, const float* Rs, const float* Wt1,
                const float* ghS, const float* g_next, const float* mu1, const float* inv1,
-               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN, int prec,
-               hipStream_t st);
+               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN,
+               const uint8_t* tmask, int prec, hipStream_t st);
 int edge_mlp_bwd(const EdgeGeo& geo, int F, const float* g_tot, const float* alpha,
                  const float* gam0, const float* gam1, const float* y, const float* xe,
                  const float* xsc, const float* xsh, const float* Ps, const float* PtS,

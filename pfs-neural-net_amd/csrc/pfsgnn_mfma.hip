@@ -536,7 +536,27 @@ __device__ __forceinline__ void class_stream(int c0, int c1, Load load, Body bod
 template <int NA>
 struct Rows {
   floatx4 v[NA];
+  uint32_t m;   // the edge's TModel LeakyReLU mask byte (RowsM loads only)
 };
+
+// TModel's LeakyReLU mask of a message MLP pre-activation, one byte per
+// (edge, lane group): bit s set iff slot s of the lane's rows is > 0.
+// target_fwd writes it at byte eo + g (eo: the edge's byte offset in a
+// channel-major [C][E] fp32 tensor, i.e. 4 bytes per edge, one per lane
+// group), so a wave's tile is one coalesced 64-byte store; target_bwd and
+// source_bwd read it instead of recomputing the layer (tmask_bytes()).
+template <int C>
+__device__ __forceinline__ uint32_t mask_bits(const floatx4 (&z)[GM<C>::NT]) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int tt = 0; tt < GM<C>::NT; ++tt)
+#pragma unroll
+    for (int r = 0; r < GM<C>::nreg(tt); ++r) m |= (z[tt][r] > 0.f ? 1u : 0u) << (4 * tt + r);
+  return m;
+}
+__device__ __forceinline__ float mask_slope(uint32_t m, int s) {
+  return (m >> s) & 1u ? 1.f : PF_LEAKY;
+}
 
 #define MF_GEO                                                                        \
   const int t = threadIdx.x, lane = t & 63;                                           \
@@ -771,7 +791,8 @@ __global__ __launch_bounds__(256) void km_target_fwd(EdgeGeo geo, const float* _
                                                      const float* __restrict__ sh,
                                                      const float* __restrict__ Rs,
                                                      const float* __restrict__ Wt1,
-                                                     float* __restrict__ part) {
+                                                     float* __restrict__ part,
+                                                     uint8_t* __restrict__ tmask) {
   constexpr int C = 2 * F, NT = GM<C>::NT;
   MF_GEO
   __shared__ float colbuf[COL_CH * 4 * C];
@@ -795,6 +816,7 @@ __global__ __launch_bounds__(256) void km_target_fwd(EdgeGeo geo, const float* _
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) z[tt] = rs[tt];
     L1.apply(x, z);
+    if (tmask && fvalid) tmask[eo0 + (uint32_t)c * eoc + g4] = (uint8_t)mask_bits<C>(z);
     const int cl = c - cbase;
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt)
@@ -816,7 +838,7 @@ __global__ __launch_bounds__(256) void km_target_fwd(EdgeGeo geo, const float* _
 // ============================================================ TModel bwd
 // g_z = g_hsum[c] * lrelu'(z) per edge; per-fiber sums of g_z (-> g_Rs), the
 // edge-input gradient Wt1[:, F:2F]^T g_z (optional) and dWt1[:, F:2F] += g_z x^T.
-template <int F, int PREC>
+template <int F, int PREC, bool TM>
 __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* __restrict__ y,
                                                      const float* __restrict__ sc,
                                                      const float* __restrict__ sh,
@@ -825,7 +847,8 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
                                                      const float* __restrict__ ghS,
                                                      float* __restrict__ GzT,
                                                      float* __restrict__ gxe,
-                                                     float* __restrict__ partW) {
+                                                     float* __restrict__ partW,
+                                                     const uint8_t* __restrict__ tmask) {
   constexpr int C = 2 * F, NT = GM<C>::NT;
   constexpr int NIMG = NT + 1;  // g_z tiles | x
   MF_GEO
@@ -834,14 +857,16 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
   __shared__ __attribute__((aligned(16))) float ghl[MF_MAX_CPS * ClassRows<C>::CP];
   ClassRows<C>::stage(ghl, ghS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
   short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
+  // the pre-activation z = Rs[f] + Wt1[:, F:2F] x is recomputed, or (TM) only
+  // its LeakyReLU mask is read back from target_fwd
   FwdLayer<FP(PREC), C, F> L1;
-  L1.load([&](int h, int k) { return Wt1[h * 2 * F + F + k]; }, lane);
+  if constexpr (!TM) L1.load([&](int h, int k) { return Wt1[h * 2 * F + F + k]; }, lane);
   GradLayer<PREC, F, C> LT;
   LT.load([&](int k, int h) { return gxe ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
   floatx4 rs[NT], accF[NT], accW[NT];
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt) {
-    rs[tt] = ld_node<C>(Rs, tt, g4, NS, n, fvalid);
+    if constexpr (!TM) rs[tt] = ld_node<C>(Rs, tt, g4, NS, n, fvalid);
     accF[tt] = zero4();
     accW[tt] = zero4();
   }
@@ -851,22 +876,29 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
 
   auto load = [&](int c) {
     Rows<1> r;
-    r.v[0] = ld_frows<F>(y, eo0 + (uint32_t)c * eoc, RB, g4);
+    const uint32_t eo = eo0 + (uint32_t)c * eoc;
+    r.v[0] = ld_frows<F>(y, eo, RB, g4);
+    if constexpr (TM) r.m = tmask[eo + g4];
     return r;
   };
   class_stream<MF_DEPTH_BWD>(c0, c1, load, [&](const Rows<1>& rows, int c) {
     const uint32_t eo = eo0 + (uint32_t)c * eoc;
     const floatx4 x[1] = {edge_in<F>(rows.v[0], fm, sc, scv, shv)};
     floatx4 z[NT], gz[NT];
+    if constexpr (!TM) {
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) z[tt] = rs[tt];
-    L1.apply(x, z);
+      for (int tt = 0; tt < NT; ++tt) z[tt] = rs[tt];
+      L1.apply(x, z);
+    }
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
       const floatx4 gh = ClassRows<C>::get(ghl, c - c0, tt, g4);
       gz[tt] = zero4();
 #pragma unroll
-      for (int r = 0; r < GM<C>::nreg(tt); ++r) gz[tt][r] = fvalid ? gh[r] * dlrelu(z[tt][r]) : 0.f;
+      for (int r = 0; r < GM<C>::nreg(tt); ++r) {
+        const float sl = TM ? mask_slope(rows.m, 4 * tt + r) : dlrelu(z[tt][r]);
+        gz[tt][r] = fvalid ? gh[r] * sl : 0.f;
+      }
       accF[tt] += gz[tt];
     }
     Fr sgz[NT];
@@ -908,7 +940,7 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
 // message MLP; plus TModel's recomputed input gradient, the downstream edge
 // gradient and the edge BatchNorm's two gradient sums.  dWs2 += g_m a^T,
 // dbs2 += g_m, dWs1[:, F:2F] += g_zs x^T, per-class sums of g_zs (-> g_Qt).
-template <int F, int PREC>
+template <int F, int PREC, bool TM>
 __global__ __launch_bounds__(256, 2) void km_source_bwd(
     EdgeGeo geo, const float* __restrict__ y, const float* __restrict__ sc,
     const float* __restrict__ sh, const float* __restrict__ QtS, const float* __restrict__ Ws1,
@@ -917,7 +949,7 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     const float* __restrict__ ghS, const float* __restrict__ g_next,
     const float* __restrict__ mu1, const float* __restrict__ inv1, float* __restrict__ g_tot,
     float* __restrict__ partW2, float* __restrict__ partW1, float* __restrict__ partCol,
-    float* __restrict__ partBN) {
+    float* __restrict__ partBN, const uint8_t* __restrict__ tmask) {
   constexpr int C = 2 * F, NT = GM<C>::NT;
   constexpr int NIMG = 3 * NT + 1;          // g_m | a | g_zs | x
   constexpr int SCR = C * (C + 1) > C * F ? C * (C + 1) : C * F;
@@ -937,9 +969,9 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   const long long CNS = (long long)C * NS;
   const bool tpart = Rs != nullptr;
 
-  FwdLayer<FP(PREC), C, F> L1s, L1t;
+  FwdLayer<FP(PREC), C, F> L1s, L1t;   // L1t: TModel's layer, recomputed unless TM
   L1s.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
-  L1t.load([&](int h, int k) { return tpart ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
+  if constexpr (!TM) L1t.load([&](int h, int k) { return tpart ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
   FwdLayer<FP(PREC), C, C> L2;
   L2.load([&](int o, int h) { return Ws2[o * C + h]; }, lane);
   // gradient chains: exact fp32, bf16x3 or bf16 by PREC
@@ -951,7 +983,7 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   floatx4 rs[NT], bias[NT], mn[NT], q0[NT], q1[NT], q2[NT], q3[NT];
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt) {
-    rs[tt] = ld_node<C>(Rs, tt, g4, NS, n, fvalid);
+    if constexpr (!TM) rs[tt] = ld_node<C>(Rs, tt, g4, NS, n, fvalid);
     bias[tt] = ld_vec<C>(bs2, tt, g4);
     mn[tt] = ld_node<C>(mean, tt, g4, NS, n, fvalid);
     q0[tt] = ld_node<C>(coef, tt, g4, NS, n, fvalid);
@@ -980,6 +1012,7 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     const uint32_t eo = eo0 + (uint32_t)c * eoc;
     r.v[0] = ld_frows<F>(y, eo, RB, g4);
     r.v[1] = g_next ? ld_frows<F>(g_next, eo, RB, g4) : zero4();
+    if constexpr (TM) r.m = tpart ? tmask[eo + g4] : 0u;
     return r;
   };
   class_stream<MF_DEPTH_BWD>(c0, c1, load, [&](const Rows<2>& rows, int c) {
@@ -1034,16 +1067,21 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     lds_order();
     floatx4 g[1] = {zero4()};
     if constexpr (PREC >= 1) L1sT.apply(sgz, g); else L1sT.apply(gz, g);
-    if (tpart) {  // TModel's per-edge input gradient, recomputed (gnn.py:188-190)
+    if (tpart) {  // TModel's per-edge input gradient (gnn.py:188-190)
       floatx4 zt[NT];
+      if constexpr (!TM) {   // its pre-activation recomputed
 #pragma unroll
-      for (int tt = 0; tt < NT; ++tt) zt[tt] = rs[tt];
-      L1t.apply(x, zt);
+        for (int tt = 0; tt < NT; ++tt) zt[tt] = rs[tt];
+        L1t.apply(x, zt);
+      }
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
         const floatx4 gh = ClassRows<C>::get(ghl, c - c0, tt, g4);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) zt[tt][r] = (fvalid && r < GM<C>::nreg(tt)) ? gh[r] * dlrelu(zt[tt][r]) : 0.f;
+        for (int r = 0; r < 4; ++r) {
+          const float sl = TM ? mask_slope(rows.m, 4 * tt + r) : dlrelu(zt[tt][r]);
+          zt[tt][r] = (fvalid && r < GM<C>::nreg(tt)) ? gh[r] * sl : 0.f;
+        }
       }
       if constexpr (PREC >= 1) {
         Fr szt[NT];
@@ -1314,6 +1352,21 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
     default: return pf::fail("pfsgnn mfma", "unsupported Fdim for this edge path"); \
   }
 
+// kernels with a third template flag (TM: the TModel mask is read, not recomputed)
+#define MF_CASE3(FF, PP, TT, K, ...)                                              \
+  case FF * 4 + PP: {                                                             \
+    hipLaunchKernelGGL((K<FF, PP, TT>), dim3(geo.nblocks), dim3(256), 0, st, geo, \
+                       __VA_ARGS__);                                              \
+  } break;
+#define MF_LAUNCH3(F, P, TT, K, ...)                                              \
+  switch ((F) * 4 + (P)) {                                                        \
+    MF_CASE3(8, 0, TT, K, __VA_ARGS__) MF_CASE3(8, 1, TT, K, __VA_ARGS__)        \
+    MF_CASE3(10, 0, TT, K, __VA_ARGS__) MF_CASE3(10, 1, TT, K, __VA_ARGS__)      \
+    MF_CASE3(10, 2, TT, K, __VA_ARGS__) MF_CASE3(10, 3, TT, K, __VA_ARGS__)      \
+    MF_CASE3(16, 0, TT, K, __VA_ARGS__) MF_CASE3(16, 1, TT, K, __VA_ARGS__)      \
+    default: return pf::fail("pfsgnn mfma", "unsupported Fdim for this edge path"); \
+  }
+
 namespace pfm {
 
 // forward kernels only distinguish fp32 (0, 1), single bf16 (2) and bf16x3 (3)
@@ -1334,15 +1387,20 @@ int source_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const
 }
 
 int target_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
-               const float* Rs, const float* Wt1, float* part, int prec, hipStream_t st) {
-  MF_LAUNCH(F, fwd_prec(prec), km_target_fwd, y, sc, sh, Rs, Wt1, part)
+               const float* Rs, const float* Wt1, float* part, uint8_t* tmask, int prec,
+               hipStream_t st) {
+  MF_LAUNCH(F, fwd_prec(prec), km_target_fwd, y, sc, sh, Rs, Wt1, part, tmask)
   return 0;
 }
 
 int target_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* Rs, const float* Wt1, const float* ghS, float* gz, float* gxe,
-               float* part, int prec, hipStream_t st) {
-  MF_LAUNCH(F, prec, km_target_bwd, y, sc, sh, Rs, Wt1, ghS, gz, gxe, part)
+               float* part, const uint8_t* tmask, int prec, hipStream_t st) {
+  if (tmask) {
+    MF_LAUNCH3(F, prec, true, km_target_bwd, y, sc, sh, Rs, Wt1, ghS, gz, gxe, part, tmask)
+  } else {
+    MF_LAUNCH3(F, prec, false, km_target_bwd, y, sc, sh, Rs, Wt1, ghS, gz, gxe, part, tmask)
+  }
   return 0;
 }
 
@@ -1350,10 +1408,15 @@ int source_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
                const float* mean, const float* coef, const float* Rs, const float* Wt1,
                const float* ghS, const float* g_next, const float* mu1, const float* inv1,
-               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN, int prec,
-               hipStream_t st) {
-  MF_LAUNCH(F, prec, km_source_bwd, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghS,
-            g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN)
+               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN,
+               const uint8_t* tmask, int prec, hipStream_t st) {
+  if (tmask && Rs) {
+    MF_LAUNCH3(F, prec, true, km_source_bwd, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+               ghS, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask)
+  } else {
+    MF_LAUNCH3(F, prec, false, km_source_bwd, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+               ghS, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask)
+  }
   return 0;
 }
 

@@ -9,10 +9,11 @@ bucket is the right size.
 
 BatchNorm: the batch statistics a forward normalises with are per rank (no
 SyncBN), as under torch DDP.  The running statistics (and
-num_batches_tracked) follow DDP's default ``broadcast_buffers=True``: rank
-0's buffers are broadcast to every rank once per step (``sync_buffers``, one
-collective on a packed buffer), so eval-mode inference and checkpoints do not
-depend on the rank.
+num_batches_tracked) follow DDP's default ``broadcast_buffers=True``: at the
+start of every step, before the forward (where DDP does it), rank 0's buffers
+are broadcast to every rank (``sync_buffers``: the float buffers live in one
+packed tensor, so it is one collective plus one for the int64 counters), so
+eval-mode inference and checkpoints do not depend on the rank.
 """
 import os
 
@@ -48,26 +49,49 @@ def broadcast_parameters(model, src=0):
         dist.broadcast(b, src)
 
 
+def _packed(model, names, dtype):
+    """One tensor holding every `dtype` buffer of `model` in `names` order, the
+    module buffers re-pointed at views of it (kept while they stay views)."""
+    key = "_pf_bufpack_" + str(dtype).split(".")[-1]
+    bufs = dict(model.named_buffers())
+    cache = model.__dict__.get(key)
+    if cache is not None and cache[0] == names:
+        flat, offs = cache[1], cache[2]
+        if all(bufs[n].data_ptr() == flat.data_ptr() + flat.element_size() * o
+               and bufs[n].device == flat.device for n, o in zip(names, offs)):
+            return flat
+    # int64 counters of pfsgnn.GNN are already one tensor (GNN._bump_batches)
+    nbt = model.__dict__.get("_pf_nbt")
+    if dtype == torch.int64 and nbt is not None:
+        flat = nbt[1]
+        offs = [(bufs[n].data_ptr() - flat.data_ptr()) // 8 for n in names]
+        if all(0 <= o < flat.numel() for o in offs) and len(set(offs)) == len(offs) == flat.numel():
+            model.__dict__[key] = (names, flat, offs)
+            return flat
+    flat = torch.cat([bufs[n].detach().reshape(-1) for n in names]).contiguous()
+    offs, o = [], 0
+    for n in names:
+        b = bufs[n]
+        mod = model.get_submodule(n.rsplit(".", 1)[0]) if "." in n else model
+        mod._buffers[n.rsplit(".", 1)[-1]] = flat[o:o + b.numel()].view_as(b)
+        offs.append(o)
+        o += b.numel()
+    model.__dict__[key] = (names, flat, offs)
+    return flat
+
+
 def sync_buffers(model, src=0):
     """DDP's broadcast_buffers=True: every rank takes rank `src`'s BatchNorm
-    running statistics and batch counters (one broadcast of a packed buffer)."""
+    running statistics and batch counters.  Call it at the start of a step,
+    before the forward, as DDP does (the forward then reads and updates the
+    same buffers on every rank)."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return
-    bufs = [b for b in model.buffers()]
-    if not bufs:
-        return
-    fl = [b for b in bufs if b.dtype == torch.float32]
-    it = [b for b in bufs if b.dtype != torch.float32]
-    for group in (fl, it):
-        if not group:
-            continue
-        packed = torch.cat([b.reshape(-1) for b in group])
-        dist.broadcast(packed, src)
-        off = 0
-        for b in group:
-            n = b.numel()
-            b.copy_(packed[off:off + n].view_as(b))
-            off += n
+    groups = {}
+    for n, b in model.named_buffers():
+        groups.setdefault(b.dtype, []).append(n)
+    for dtype, names in groups.items():
+        dist.broadcast(_packed(model, tuple(names), dtype), src)
 
 
 def allreduce_gradients(model):

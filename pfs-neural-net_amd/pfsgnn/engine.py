@@ -318,10 +318,11 @@ class Engine:
         return be.moment_coef(st["mom"], gst, d.NC if d.sp is None else d.sp.fib_ptr)
 
     def source_edge_bwd(self, P, Gr, d, pre, st, coef, tpart, g_next, bnstat, g_xt, se=None,
-                        epre=None):
+                        epre=None, tmask=None):
         """SModel edge backward; with the upstream EdgeModel's state ``se`` (and
         its prefix) the edge BatchNorm's backward coefficients come out of the
-        same call -> (g_tot, (alpha, gam0, gam1)); else -> (g_tot, Sg, Sgx)."""
+        same call -> (g_tot, (alpha, gam0, gam1)); else -> (g_tot, Sg, Sgx).
+        ``tmask``: the TModel forward's mask for ``tpart`` (target_fwd)."""
         be, F = self.be, self.F
         Ws1, Ws2 = P[pre + "node_mlp_1.0.weight"], P[pre + "node_mlp_1.2.weight"]
         y, sc, sh = st["xe3"]
@@ -333,7 +334,8 @@ class Engine:
         out = be.source_bwd(
             d, y, sc, sh, st["Qt"], Ws1, Ws2, P[pre + "node_mlp_1.2.bias"], st["mom"][0], coef,
             tpart, g_next, bnstat, Gr[pre + "node_mlp_1.0.weight"], Gr[pre + "node_mlp_1.2.weight"],
-            Gr[pre + "node_mlp_1.2.bias"], bn2=bn2, g_xt=g_xt)  # + g_xt += Ws1x^T GzS
+            Gr[pre + "node_mlp_1.2.bias"], bn2=bn2, g_xt=g_xt,  # + g_xt += Ws1x^T GzS
+            **({"tmask": tmask} if tmask is not None and tpart is not None else {}))
         g_tot, GzS = out[0], out[1]
         be.wgrad(GzS, st["xt"], Gr[pre + "node_mlp_1.0.weight"], col0=0,
                  db=Gr[pre + "node_mlp_1.0.bias"])
@@ -347,10 +349,14 @@ class Engine:
         Wt1, bt1 = P[pre + "node_mlp_1.0.weight"], P[pre + "node_mlp_1.0.bias"]
         Wt2, bt2 = P[pre + "node_mlp_1.2.weight"], P[pre + "node_mlp_1.2.bias"]
         Rs = be.lin(Wt1, 0, F, xs, b=bt1)
+        # the LeakyReLU mask of the per-edge layer, kept for the backward (MFMA
+        # path; None where the backward recomputes it)
+        tmask = be.tmask(d) if self.training and hasattr(be, "tmask") else None
         if d.sp is None:
             # the second Linear after the per-class sum, in the op's reduction epilogue
             hsum, agg = be.target_fwd(d, xe3[0], xe3[1], xe3[2], Rs, Wt1,
-                                      agg=(Wt2, bt2, float(d.NF)))
+                                      agg=(Wt2, bt2, float(d.NF)),
+                                      **({"tmask": tmask} if tmask is not None else {}))
         else:
             hsum = be.target_fwd(d, xe3[0], xe3[1], xe3[2], Rs, Wt1)
             # the bias of the summed messages is deg(c) * b2 (gnn.py:190)
@@ -359,7 +365,8 @@ class Engine:
         # node_mlp_2 input [x, agg, u[batch]] (gnn.py:191), in place, + BatchNorm1d
         hT = [(xt, 0, False), (agg, F, False), (u, 3 * F, True)]
         xt_new, sT = self.mlp_fwd(P, pre + "node_mlp_2.", hT, pre + "norm.", BN)
-        return dict(xs=xs, xt=xt, xe3=xe3, u=u, Rs=Rs, hsum=hsum, sT=sT, xt_new=xt_new)
+        return dict(xs=xs, xt=xt, xe3=xe3, u=u, Rs=Rs, hsum=hsum, sT=sT, xt_new=xt_new,
+                    tmask=tmask)
 
     def target_node_bwd(self, P, Gr, d, pre, st, g_xt_new, g_xt, g_u):
         be, F, G = self.be, self.F, d.G
@@ -381,9 +388,10 @@ class Engine:
         be, F = self.be, self.F
         Wt1 = P[pre + "node_mlp_1.0.weight"]
         y, sc, sh = st["xe3"]
+        kw = {"tmask": st["tmask"]} if st.get("tmask") is not None else {}
         GzT, gxe = be.target_bwd(d, y, sc, sh, st["Rs"], Wt1, g_hsum,
                                  Gr[pre + "node_mlp_1.0.weight"], want_gxe=want_gxe,
-                                 g_xs=g_xs)          # + g_xs += Wt1s^T GzT
+                                 g_xs=g_xs, **kw)          # + g_xs += Wt1s^T GzT
         be.wgrad(GzT, st["xs"], Gr[pre + "node_mlp_1.0.weight"], col0=0,
                  db=Gr[pre + "node_mlp_1.0.bias"])
         return gxe
@@ -512,7 +520,8 @@ class Engine:
                 coef = self.source_node_bwd(P, Gr, d, p + "s_model.", ss, g_xs_new, g_xs_in, g_u_in)
                 g_tot, *bnc = self.source_edge_bwd(P, Gr, d, p + "s_model.", ss, coef, tpart,
                                                    g_xe, bnstat, g_xt_in, se=se,
-                                                   epre=p + "edge_model.")
+                                                   epre=p + "edge_model.",
+                                                   tmask=stt.get("tmask") if live_t else None)
                 bnc = bnc[0] if self.normed else None
             else:
                 g_tot = be.zeros(F, d.E) if g_xe is None else g_xe

@@ -269,6 +269,20 @@ class _ParamMixin:
     def _bn_buffers(self):
         return {n: b for n, b in self.named_buffers() if "running" in n}
 
+    def _recording_grads(self):
+        """The gradient dict a backward writes through, recording which
+        parameters it wrote (``_mark_live`` after the backward)."""
+        return _GradRecorder(self._flat_grads())
+
+    def _mark_live(self, names):
+        """Parameters a backward wrote (the ones the reference's autograd would
+        give a .grad); FusedAdam skips the others (weight decay, step counts)."""
+        params = dict(self.named_parameters())
+        for n in names:
+            p = params.get(n)
+            if p is not None:
+                p._pf_live = True
+
     def _bump_batches(self, edge_keys=(), node_keys=()):
         bufs = dict(self.named_buffers())
         for k in edge_keys:
@@ -332,9 +346,6 @@ class _FlatMixin(_ParamMixin):
                     p.grad = sl.view(p.shape)
         return {n: p.grad for n, p in self.named_parameters()}
 
-    def _recording_grads(self):
-        return _GradRecorder(self._flat_grads())
-
     def _bump_batches(self, edge_keys=(), node_keys=()):
         """num_batches_tracked += 2 (edge BatchNorms, applied twice) / += 1 for
         every BatchNorm of a forward, as ONE device add: the counters are
@@ -363,15 +374,6 @@ class _FlatMixin(_ParamMixin):
             cache = (key, flat, inc)
             self.__dict__["_pf_nbt"] = cache
         cache[1].add_(cache[2])
-
-    def _mark_live(self, names):
-        """Parameters a backward wrote (the ones the reference's autograd would
-        give a .grad); FusedAdam skips the others when weight_decay != 0."""
-        params = dict(self.named_parameters())
-        for n in names:
-            p = params.get(n)
-            if p is not None:
-                p._pf_live = True
 
     def zero_grad(self, set_to_none=True):
         """Zero the flat gradient buffer in one kernel and keep every ``p.grad``
@@ -435,11 +437,12 @@ class _MLPFn(torch.autograd.Function):
         module = ctx.module
         eng = _engine_for(module[0].out_features, True)
         P = module._flat_params()
-        Gr = module._flat_grads()
+        Gr = module._recording_grads()
         be = backend()
         K = module[0].in_features
         dx = be.empty(K, gy.shape[0])
         eng.mlp_bwd(P, Gr, "", gy.t().contiguous(), ctx.saved_pf, outs=[(dx, K, False)])
+        module._mark_live(Gr.used)
         return dx.t(), None, None
 
 
@@ -478,7 +481,7 @@ class _EdgeFn(torch.autograd.Function):
         module, d, lay, st = ctx.pf
         be, F = backend(), module.Fdim
         eng = _engine_for(F, module.normed)
-        P, Gr = module._flat_params(), module._flat_grads()
+        P, Gr = module._flat_params(), module._recording_grads()
         gc = grad_edges_in(g, lay)
         gc = be.zeros(F, d.E) if gc is None else gc.contiguous()
         bnc = None
@@ -487,6 +490,7 @@ class _EdgeFn(torch.autograd.Function):
             bnc = eng.edge_bn_coef(P, Gr, d, "", st, Sg, Sgx)
         g_xs, g_xt, g_u = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
         g_xe = eng.edge_bwd(P, Gr, d, "", st, gc, bnc, True, g_xs, g_xt, g_u)
+        module._mark_live(Gr.used)
         return g_xs.t(), g_xt.t(), grad_edges_out(g_xe, lay), g_u.t(), None, None, None
 
 
@@ -524,10 +528,11 @@ class _SourceFn(torch.autograd.Function):
         module, d, lay, st = ctx.pf
         be, F = backend(), module.Fdim
         eng = _engine_for(F, module.normed)
-        P, Gr = module._flat_params(), module._flat_grads()
+        P, Gr = module._flat_params(), module._recording_grads()
         g_xs, g_xt, g_u = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
         coef = eng.source_node_bwd(P, Gr, d, "", st, g.t().contiguous(), g_xs, g_u)
         g_tot = eng.source_edge_bwd(P, Gr, d, "", st, coef, None, None, None, g_xt)[0]
+        module._mark_live(Gr.used)
         return g_xs.t(), g_xt.t(), grad_edges_out(g_tot, lay), g_u.t(), None, None, None
 
 
@@ -568,10 +573,11 @@ class _TargetFn(torch.autograd.Function):
         module, d, lay, st = ctx.pf
         be, F = backend(), module.Fdim
         eng = _engine_for(F, module.normed)
-        P, Gr = module._flat_params(), module._flat_grads()
+        P, Gr = module._flat_params(), module._recording_grads()
         g_xs, g_xt, g_u = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
         g_hsum = eng.target_node_bwd(P, Gr, d, "", st, g.t().contiguous(), g_xt, g_u)
         gxe = eng.target_edge_bwd(P, Gr, d, "", st, g_hsum, True, g_xs)
+        module._mark_live(Gr.used)
         return g_xs.t(), g_xt.t(), grad_edges_out(gxe, lay), g_u.t(), None, None, None
 
 
@@ -610,9 +616,10 @@ class _GlobalFn(torch.autograd.Function):
         module, d, st = ctx.pf
         be, F = backend(), module.Fdim
         eng = _engine_for(F, module.normed)
-        P, Gr = module._flat_params(), module._flat_grads()
+        P, Gr = module._flat_params(), module._recording_grads()
         g_xs, g_xt, g_u = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
         eng.global_bwd(P, Gr, d, "", st, g.t().contiguous(), g_xs, g_xt, g_u)
+        module._mark_live(Gr.used)
         return g_xs.t(), g_xt.t(), g_u.t(), None, None
 
 

@@ -146,10 +146,11 @@ _SIGS = {
     "pfsgnn_edge_mlp_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_edge_mlp_fwd_bn": ([I, I, I, I] + [P] * 15 + [FL, FL, P, P, P, P, P, SZ, P], I),
     "pfsgnn_source_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
-    "pfsgnn_target_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, P, P, SZ, P], I),
-    "pfsgnn_target_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
-    "pfsgnn_source_bwd": ([I, I, I, I] + [P] * 23 + [P, SZ, P], I),
-    "pfsgnn_source_bwd_bn": ([I, I, I, I] + [P] * 17 + [LL, FL] + [P] * 11 + [P, SZ, P], I),
+    "pfsgnn_target_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, P, P, P, SZ, P], I),
+    "pfsgnn_tmask_bytes": ([I, I, I, I], SZ),
+    "pfsgnn_target_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_source_bwd": ([I, I, I, I] + [P] * 24 + [P, SZ, P], I),
+    "pfsgnn_source_bwd_bn": ([I, I, I, I] + [P] * 17 + [LL, FL] + [P] * 12 + [P, SZ, P], I),
     "pfsgnn_edge_bn_grad_sums": ([I, I, I, I, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_edge_mlp_bwd": ([I, I, I, I] + [P] * 21 + [P, SZ, P], I),
     "pfsgnn_loss_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, FL, FL, ULL, P, P, P, P, P, P, P, SZ, P], I),
@@ -770,9 +771,18 @@ class HipBackend:
               hs_out.data_ptr(), ws, wsb, _stream())
         return mom
 
-    def target_fwd(self, d, y, sc, sh, Rs, Wt1, agg=None):
+    def tmask(self, d):
+        """A buffer for TModel's LeakyReLU mask (pfsgnn_tmask_bytes), or None
+        when the current edge path recomputes that layer in the backward."""
+        if d.sp is not None:
+            return None
+        n = lib().pfsgnn_tmask_bytes(d.G, d.NF, d.NC, d.F)
+        return torch.empty(n, dtype=torch.uint8, device=config.device) if n else None
+
+    def target_fwd(self, d, y, sc, sh, Rs, Wt1, agg=None, tmask=None):
         """-> hsum; with ``agg`` = (Wt2, bt2, bscale) -> (hsum, Wt2 hsum + bscale bt2),
-        the second Linear done in the class reduction's epilogue."""
+        the second Linear done in the class reduction's epilogue.  ``tmask``
+        (from ``tmask(d)``) receives TModel's LeakyReLU mask for the backward."""
         if d.sp is not None:
             hsum = self._sp.target_fwd(d, y, sc, sh, Rs, Wt1)
             if agg is None:
@@ -790,11 +800,13 @@ class HipBackend:
         ws, wsb = self._wsargs(d)
         _call("pfsgnn_target_fwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
               Rs.data_ptr(), Wt1.data_ptr(), hsum.data_ptr(), _ptr(Wt2), _ptr(bt2),
-              float(bscale), _ptr(A), ws, wsb, _stream())
+              float(bscale), _ptr(A), _ptr(tmask), ws, wsb, _stream())
         return hsum if agg is None else (hsum, A)
 
-    def target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False, g_xs=None):
-        """-> (GzT, gxe); with ``g_xs``: g_xs += Wt1[:, :F]^T GzT as well."""
+    def target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False, g_xs=None,
+                   tmask=None):
+        """-> (GzT, gxe); with ``g_xs``: g_xs += Wt1[:, :F]^T GzT as well;
+        ``tmask``: the forward's mask (target_fwd), read instead of recomputed."""
         if d.sp is not None:
             out = self._sp.target_bwd(d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=want_gxe)
             if g_xs is not None:
@@ -807,11 +819,11 @@ class HipBackend:
         ws, wsb = self._wsargs(d)
         _call("pfsgnn_target_bwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
               Rs.data_ptr(), Wt1.data_ptr(), g_hsum.data_ptr(), GzT.data_ptr(), dWt1.data_ptr(),
-              _ptr(gxe), _ptr(g_xs), ws, wsb, _stream())
+              _ptr(gxe), _ptr(g_xs), _ptr(tmask), ws, wsb, _stream())
         return GzT, gxe
 
     def source_bwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next, bnstat,
-                   dWs1, dWs2, dbs2, bn2=None, g_xt=None):
+                   dWs1, dWs2, dbs2, bn2=None, g_xt=None, tmask=None):
         """-> (g_tot, GzS, Sg, Sgx).  With ``bn2`` = (gamma, var1, n, eps, dgamma,
         dbeta) (and ``bnstat``) the edge BatchNorm's backward is finished in the
         same call: -> (g_tot, GzS, None, None, (alpha, gam0, gam1)).  With
@@ -851,11 +863,11 @@ class HipBackend:
             _call("pfsgnn_source_bwd_bn", *head, var1.data_ptr(), gamma.data_ptr(), int(n),
                   float(eps), g_tot.data_ptr(), GzS.data_ptr(), dWs1.data_ptr(), dWs2.data_ptr(),
                   dbs2.data_ptr(), a.data_ptr(), g0.data_ptr(), g1.data_ptr(), dg.data_ptr(),
-                  db.data_ptr(), _ptr(g_xt), ws, wsb, _stream())
+                  db.data_ptr(), _ptr(g_xt), _ptr(tmask), ws, wsb, _stream())
             return g_tot, GzS, None, None, (a, g0, g1)
         _call("pfsgnn_source_bwd", *head, g_tot.data_ptr(), GzS.data_ptr(), dWs1.data_ptr(),
-              dWs2.data_ptr(), dbs2.data_ptr(), _ptr(Sg), _ptr(Sgx), _ptr(g_xt), ws, wsb,
-              _stream())
+              dWs2.data_ptr(), dbs2.data_ptr(), _ptr(Sg), _ptr(Sgx), _ptr(g_xt), _ptr(tmask), ws,
+              wsb, _stream())
         return g_tot, GzS, Sg, Sgx
 
     def edge_bn_grad_sums(self, d, g, y, mu1, inv1):

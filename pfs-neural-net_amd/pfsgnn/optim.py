@@ -28,11 +28,26 @@ def _flat_base(tensors):
     return base, [o - lo for o in offs]
 
 
+def _is_live(p):
+    """Whether this step's backward gave p a gradient, as torch.optim.Adam sees
+    it (``p.grad is not None``).  pfsgnn's fused backward keeps every
+    ``p.grad`` attached to the flat gradient buffer (graph capture) and marks
+    the parameters it wrote with ``p._pf_live`` instead (gnn._GradRecorder)."""
+    live = getattr(p, "_pf_live", None)
+    return (p.grad is not None) if live is None else bool(live)
+
+
 class FusedAdam(torch.optim.Optimizer):
     """``capturable=True`` keeps the step count on the device (as torch's
     capturable Adam does), so ``step()`` issues no host sync and can be
     captured in a HIP graph: each replay increments the count and the kernel
-    derives the bias corrections from it."""
+    derives the bias corrections from it.  That count is one per group, so a
+    capturable optimizer requires the set of parameters with gradients to stay
+    the one of its first step (it raises otherwise).  Without ``capturable``
+    every parameter keeps its own step count, as torch.optim.Adam does: a
+    parameter without a gradient is skipped (no moment decay, no weight decay,
+    no step), and the flat one-launch update runs whenever the live parameters
+    share one count (per-parameter launches otherwise)."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
                  capturable=False):
@@ -41,18 +56,19 @@ class FusedAdam(torch.optim.Optimizer):
         super().__init__(params, defaults)
         self._flat = {}
         self._masks = {}
+        self._live0 = {}
 
-    def _live_mask(self, gi, group, n):
-        """None if every parameter of the group got a gradient this step, else a
-        device uint8 mask over the flat buffer: torch.optim.Adam skips the
-        parameters whose .grad the reference leaves None (p._pf_live False,
-        set by pfsgnn.GNN's backward) -- which only changes the update when
-        weight_decay != 0 (zero grads with zero moments leave p unchanged)."""
-        if group["weight_decay"] == 0.0:
-            return None
-        live = tuple(bool(getattr(p, "_pf_live", True)) for p in group["params"])
-        if all(live):
-            return None
+    def zero_grad(self, set_to_none=True):
+        """torch's zero_grad, and every pfsgnn parameter back to 'no gradient
+        this step' until a backward writes it (``_pf_live``)."""
+        for group in self.param_groups:
+            for p in group["params"]:
+                if hasattr(p, "_pf_live"):
+                    p._pf_live = False
+        super().zero_grad(set_to_none=set_to_none)
+
+    def _live_mask(self, gi, group, n, live):
+        """Device uint8 mask over the flat buffer, 1 on the parameters in `live`."""
         key = (gi, live)
         m = self._masks.get(key)
         if m is None:
@@ -90,7 +106,9 @@ class FusedAdam(torch.optim.Optimizer):
             else:
                 step_t = None
             for p, off in zip(ps, pb[1]):
-                self.state[p] = {"step": step_t if step_t is not None else torch.tensor(float(step)),
+                st = self.state.get(p)
+                own = float(st["step"]) if st and "step" in st else 0.0
+                self.state[p] = {"step": step_t if step_t is not None else torch.tensor(own),
                                  "exp_avg": m[off:off + p.numel()].view(p.shape),
                                  "exp_avg_sq": v[off:off + p.numel()].view(p.shape)}
             cache = (m, v)
@@ -106,26 +124,45 @@ class FusedAdam(torch.optim.Optimizer):
         be = backend()
         for gi, group in enumerate(self.param_groups):
             beta1, beta2 = group["betas"]
+            ps = group["params"]
             flat = self._group_flat(gi, group)
+            live = tuple(_is_live(q) for q in ps)
+            if flat is not None and group.get("capturable", False):
+                p, g, m, v = flat
+                first = self._live0.setdefault(gi, live)
+                if live != first:
+                    raise RuntimeError("FusedAdam(capturable=True) keeps one device step count per "
+                                       "group: the set of parameters with gradients must stay the "
+                                       "one of the first step")
+                # the dead parameters of a fixed live set never had a gradient:
+                # zero moments, so a zero-gradient update leaves them unchanged
+                # unless weight decay applies
+                mask = (None if all(live) or group["weight_decay"] == 0.0
+                        else self._live_mask(gi, group, p.numel(), live))
+                step_t = self.state[ps[0]]["step"]          # one device tensor shared by the group
+                step_t.add_(1.0)
+                be.adam(p, g, m, v, step_t, group["lr"], beta1, beta2, group["eps"],
+                        group["weight_decay"], live=mask)
+                continue
             if flat is not None:
                 p, g, m, v = flat
-                live = self._live_mask(gi, group, p.numel())
-                st0 = self.state[group["params"][0]]
-                if group.get("capturable", False):
-                    step_t = st0["step"]          # one device tensor shared by the group
-                    step_t.add_(1.0)
-                    be.adam(p, g, m, v, step_t, group["lr"], beta1, beta2, group["eps"],
-                            group["weight_decay"], live=live)
+                steps = [int(self.state[q]["step"]) for q in ps]     # host tensors: no sync
+                counts = {c for c, on in zip(steps, live) if on}
+                if len(counts) <= 1:
+                    step = (counts.pop() if counts else 0) + 1
+                    # a dead parameter is left exactly as it is (torch skips it)
+                    # unless its moments are zero and no weight decay applies
+                    need = any(not on and (group["weight_decay"] != 0.0 or c > 0)
+                               for c, on in zip(steps, live))
+                    mask = self._live_mask(gi, group, p.numel(), live) if need else None
+                    be.adam(p, g, m, v, step, group["lr"], beta1, beta2, group["eps"],
+                            group["weight_decay"], live=mask)
+                    for q, on in zip(ps, live):
+                        if on:
+                            self.state[q]["step"] = torch.tensor(float(step))
                     continue
-                step = int(st0["step"]) + 1
-                be.adam(p, g, m, v, step, group["lr"], beta1, beta2, group["eps"],
-                        group["weight_decay"], live=live)
-                for q in group["params"]:
-                    self.state[q]["step"].fill_(float(step))
-                continue
-            for q in group["params"]:
-                if q.grad is None or (group["weight_decay"] != 0.0
-                                      and not getattr(q, "_pf_live", True)):
+            for q in ps:
+                if q.grad is None or not _is_live(q):
                     continue
                 st = self.state[q]
                 if "exp_avg" not in st:

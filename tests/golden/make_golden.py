@@ -16,6 +16,11 @@ source is copied and nothing in a reference file is executed:
 * params/model_gnn_0.pth and models/model_gnn_0.pth -- loaded with
   ``torch.load(weights_only=True)`` (accepted).  -> ckpt_params.npz,
   ckpt_models.npz (model state only).
+* params/model_gnn_0.pth's ``optim_state`` (train.py:154-165 saves
+  ``optimizer.state_dict()`` of torch.optim.Adam beside the model): the Adam
+  step count, the indices of the parameters that have state (the ones the
+  reference's backward ever gave a gradient) and their ``exp_avg`` /
+  ``exp_avg_sq``, plus the param group's hyper-parameters.  -> ckpt_adam.npz
 * params/*.txt -- class tables (T_i hours per visit, N_i galaxies).  -> classes.npz
 """
 import os
@@ -51,6 +56,18 @@ def checkpoints():
     ck = torch.load(os.path.join(REF, "params/model_gnn_0.pth"), weights_only=True, map_location="cpu")
     arrs = {k: v.numpy() for k, v in ck["model_state"].items()}
     np.savez_compressed(os.path.join(HERE, "ckpt_params.npz"), epoch=np.int64(ck["epoch"]), **arrs)
+    st = ck["optim_state"]["state"]
+    grp = ck["optim_state"]["param_groups"][0]
+    idx = sorted(st.keys())
+    adam = {"indices": np.array(idx, dtype=np.int64),
+            "step": np.array([float(st[i]["step"]) for i in idx]),
+            "n_params": np.int64(len(grp["params"])), "lr": np.float64(grp["lr"]),
+            "betas": np.array(grp["betas"], dtype=np.float64), "eps": np.float64(grp["eps"]),
+            "weight_decay": np.float64(grp["weight_decay"])}
+    for i in idx:
+        adam[f"exp_avg_{i}"] = st[i]["exp_avg"].numpy()
+        adam[f"exp_avg_sq_{i}"] = st[i]["exp_avg_sq"].numpy()
+    np.savez_compressed(os.path.join(HERE, "ckpt_adam.npz"), **adam)
     sd = torch.load(os.path.join(REF, "models/model_gnn_0.pth"), weights_only=True, map_location="cpu")
     np.savez_compressed(os.path.join(HERE, "ckpt_models.npz"), **{k: v.numpy() for k, v in sd.items()})
 

@@ -1,0 +1,67 @@
+"""Oracle parity at the benchmarked geometry: the normed training step of the
+bench batch (G=16 complete 2394x128 graphs, B=8 blocks; bench.py's workload)
+against the float64 oracle, with test_gpu_parity's ``check`` bar (error
+within 16x the float32 oracle's own error, or TOL_REL of the tensor's scale).
+
+The oracle at this size needs ~130 GB of host memory and minutes of CPU, so
+its outputs are a committed fixture (tests/golden/g16_oracle.npz, made by
+tools/make_g16_fixture.py on the GPU box's host from the same seeded
+make_problem inputs): the loss, every parameter gradient, the BatchNorm
+running statistics, x_t and x_u whole, x_s / x_e on seeded row samples, and
+x_e's per-channel sums and sums of squares over all 4.9 M edges.
+
+The default edge path must reach the bench's grid here: KS = 5 class splits,
+3040 blocks per edge kernel (pfsgnn_edge_grid).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from harness import make_problem  # noqa: E402
+from test_gpu_parity import check, ours_step  # noqa: E402
+
+FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "g16_oracle.npz")
+
+
+@pytest.fixture(params=["mfma", "mfma32"])
+def path(request):
+    import pfsgnn
+    pfsgnn.set_edge_path(request.param)
+    yield request.param
+    pfsgnn.set_edge_path("mfma")
+
+
+def test_bench_geometry_training_step_matches_oracle(path):
+    from pfsgnn import native
+    z = np.load(FIX)
+    G, NF, NC, B = (int(z[k]) for k in ("G", "NF", "NC", "B"))
+    grid = native.edge_grid(G, NF, NC)
+    assert (G, NF, NC, B) == (16, 2394, 128, 8)
+    if path == "mfma":
+        assert grid["KS"] == 5 and grid["nblocks"] == 3040, grid
+    model, graph = make_problem(G, NF, NC, B=B, seed=int(z["model_seed"]))
+    gnn, out, loss = ours_step(model, graph, G, NF, NC, B, int(z["noise_seed"]), float(z["sharp"]))
+
+    def ref(k):
+        return torch.as_tensor(z["f64:" + k]), torch.as_tensor(z["f32:" + k])
+
+    check("loss", loss.reshape(1), *ref("loss"))
+    ixs, ixe = torch.as_tensor(z["ix_s"]), torch.as_tensor(z["ix_e"])
+    xe = out.x_e.detach()
+    check("x_t", out.x_t, *ref("x_t"))
+    check("x_u", out.x_u, *ref("x_u"))
+    check("x_s (sample)", out.x_s.detach()[ixs.cuda()], *ref("x_s_sample"))
+    check("x_e (sample)", xe[ixe.cuda()], *ref("x_e_sample"))
+    check("x_e channel sums", xe.double().sum(0), *ref("x_e_sum"))
+    check("x_e channel sums of squares", (xe.double() ** 2).sum(0), *ref("x_e_sumsq"))
+    for name, p in gnn.named_parameters():
+        check("grad " + name, p.grad, *ref("grad " + name))
+    for k, v in gnn.state_dict().items():
+        if "running" in k:
+            check(k, v.double(), *ref(k))
+        elif "num_batches" in k:
+            assert int(v) == int(z["f64:" + k]), k

@@ -151,3 +151,48 @@ def test_completeness_min_propagates_nan():
     assert torch.isnan(utils).all().item() and torch.isnan(loss).all().item()
     comp = n_prime.cpu() / (ci[1].cpu() / 10.0)
     assert torch.isnan(torch.min(comp))
+
+
+def test_fused_adam_tracks_live_sets_like_torch_adam():
+    """GNN.node_prediction / edge_prediction run decoder_s /
+    decoder_e through the module-level MLP autograd function, whose backward
+    must mark the decoder parameters live, and a parameter whose gradient
+    comes and goes keeps torch.optim.Adam's per-parameter step count and is
+    left untouched (no moment decay, no weight decay) on steps without one.
+    Steps alternate between the fused train.py loss and a loss on
+    node_prediction(out.x_s) + the unfused edge_prediction(out.x_e), so the
+    live set changes every step; weight decay on."""
+    import pfsgnn
+    from pfsgnn.train import loss_function
+    model, graph = make_problem(1, 48, 12, B=2, seed=6)
+    gnn = _hip_model(model, 2)
+    data = pfsgnn.BipartiteData(graph.edge_index, graph.x_s.float(), graph.x_t.float(),
+                                graph.x_e.float(), graph.x_u.float())
+    ci = graph.x_t.float().cuda()
+    opt = pfsgnn.FusedAdam(gnn.parameters(), lr=1e-2, weight_decay=0.05)
+    ref_params = {n: p.detach().cpu().clone().requires_grad_(True) for n, p in gnn.named_parameters()}
+    ropt = torch.optim.Adam(list(ref_params.values()), lr=1e-2, weight_decay=0.05)
+    for it in range(4):
+        opt.zero_grad()
+        gnn.zero_grad()
+        out = gnn(data)
+        if it % 2 == 0:
+            loss, _ = loss_function(out, ci, pclass=0.1, pfiber=0.1, sharpness=10.0, seed=20 + it)
+        else:
+            pred = gnn.node_prediction(out.x_s)
+            loss = (pred * torch.linspace(-1, 1, pred.shape[1], device="cuda")).sum() \
+                + 1e-3 * gnn.edge_prediction(out.x_e).sum()
+        loss.backward()
+        torch.cuda.synchronize()
+        live = {n for n, p in gnn.named_parameters() if p._pf_live}
+        if it % 2 == 0:
+            assert "decoder_s.0.weight" not in live and "decoder_e.0.weight" in live
+        else:
+            assert "decoder_s.0.weight" in live and "decoder_e.2.bias" in live
+        for n, p in gnn.named_parameters():
+            ref_params[n].grad = p.grad.detach().cpu().clone() if n in live else None
+        opt.step()
+        ropt.step()
+    for n, p in gnn.named_parameters():
+        torch.testing.assert_close(p.detach().cpu(), ref_params[n].detach(), rtol=1e-5, atol=1e-6,
+                                   msg=n)

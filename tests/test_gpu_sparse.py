@@ -176,3 +176,37 @@ def test_sparse_step_is_bitwise_reproducible():
     assert torch.equal(o1.x_e, o2.x_e) and torch.equal(o1.x_s, o2.x_s)
     for (n, a), (_, b) in zip(g1.named_parameters(), g2.named_parameters()):
         assert torch.equal(a.grad, b.grad), n
+
+
+def test_segment_moments_track_fp64_where_the_reference_formula_cancels():
+    """gnn.py:141 computes var = leaky_relu(E[m^2] - mean^2), which
+    cancels in fp32 when a fiber's messages have a large mean and a small
+    spread (it can even round negative, where the leaky_relu branch fires).
+    pfsgnn computes the central moments directly (two passes here, Pebay's
+    update on the complete path); both equal the reference's var in exact
+    arithmetic, and the parity tests compare against float64.  In this regime
+    ours stays within 1e-3 of the float64 moments, while the reference's
+    formula evaluated in fp32 is off by more than 100 % of the variance."""
+    hb, em = _hb(), EmuBackend()
+    gen = torch.Generator().manual_seed(5)
+    G, NF, NC, C = 1, 64, 40, 20
+    ei = sparse_edges(G, NF, NC, 0.7, gen)
+    sa, sb = hb.sparse_layout(ei.cuda(), G, NF, NC), em.sparse_layout(ei, G, NF, NC)
+    E = sb.E
+    X = 1000.0 + 1e-2 * torch.randn(C, E, generator=gen, dtype=torch.float64)
+    X32 = X.float()
+    hs = hb.empty(4 * C, G * NF)
+    mom = hb.segment_moments(X32.cuda(), sa.fib_ptr, G * NF, hs)
+    ref = em.segment_moments(X32.double(), sb.fib_ptr, G * NF,
+                             torch.empty(4 * C, G * NF, dtype=torch.float64))
+    ptr = sb.fib_ptr.long()
+    cnt = (ptr[1:] - ptr[:-1]).clamp(min=1).double()
+    seg = torch.repeat_interleave(torch.arange(G * NF), ptr[1:] - ptr[:-1])
+    m1 = torch.zeros(C, G * NF).index_add_(1, seg, X32) / cnt.float()
+    m2 = torch.zeros(C, G * NF).index_add_(1, seg, X32 * X32) / cnt.float()
+    var_ref32 = m2 - m1 * m1                       # gnn.py:141 in fp32 (before leaky_relu)
+    c2 = ref[1]
+    live = c2 > 0
+    ours = mom[1].double().cpu()
+    assert ((ours - c2).abs()[live] / c2[live]).max().item() < 1e-3
+    assert ((var_ref32.double() - c2).abs()[live] / c2[live]).max().item() > 1.0
