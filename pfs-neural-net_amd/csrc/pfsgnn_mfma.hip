@@ -354,26 +354,60 @@ __device__ __forceinline__ void stE(float* p, uint32_t off, float v) {
   *reinterpret_cast<float*>(reinterpret_cast<char*>(p) + off) = v;
 }
 
-// the lane's rows of an F-wide edge tensor at edge byte offset eo (slots with
-// no feature load row 0 again -- same 64-B segment -- and are masked later)
+// Per-lane byte offsets of the lane's F rows of a channel-major edge tensor
+// at class 0 of its wave (slots with no feature point at row 0 again -- same
+// 64-B segment -- and are masked later).  Every edge tensor of a kernel has
+// the same geometry, so one set serves them all: a class's rows are then
+// `(char*)p + c*eoc` (wave-uniform, scalar registers) + these offsets, a
+// global_load with an SGPR base and no per-load address arithmetic.
 template <int F>
-__device__ __forceinline__ floatx4 ld_frows(const float* p, uint32_t eo, uint32_t RB, int g) {
+struct RowOff {
+  uint32_t o[GM<F>::RPG];
+  __device__ __forceinline__ RowOff(uint32_t eo0, uint32_t RB, int g) {
+#pragma unroll
+    for (int r = 0; r < GM<F>::RPG; ++r) {
+      const int k = GM<F>::row(g, r);
+      o[r] = eo0 + (uint32_t)(k < 0 ? 0 : k) * RB;
+    }
+  }
+};
+
+// An edge tensor's rows of class c.  Loads: the tensor as a buffer resource,
+// the lane's byte offset (RowOff) in the VGPR offset and the wave-uniform
+// class offset c*eoc in the SGPR soffset -- buffer_load ... offen, no address
+// arithmetic per row (an access past `bytes` reads 0).  Stores: the SGPR-base
+// global form, (char*)p + c*eoc plus the 32-bit lane offset, which goes
+// through an empty asm so that hipcc keeps it 32-bit at the access rather than
+// hoisting a 64-bit copy.  (buffer_store with exec-masked rows was miscompiled
+// here: one row's value stored to all three rows; DESIGN.md §MFMA edge path.)
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes,
+                                           0x00020000);
+}
+__device__ __forceinline__ uint32_t opaque(uint32_t v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// the lane's rows of an F-wide edge tensor at class byte offset co = c*eoc
+template <int F>
+__device__ __forceinline__ floatx4 ld_frows(Rsrc p, uint32_t co, const RowOff<F>& ro) {
   floatx4 v = zero4();
 #pragma unroll
-  for (int r = 0; r < GM<F>::RPG; ++r) {
-    const int k = GM<F>::row(g, r);
-    v[r] = ldE(p, eo + (uint32_t)(k < 0 ? 0 : k) * RB);
-  }
+  for (int r = 0; r < GM<F>::RPG; ++r)
+    v[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(p, ro.o[r], co, 0));
   return v;
 }
 
 template <int F>
-__device__ __forceinline__ void st_frows(float* p, uint32_t eo, uint32_t RB, int g, bool valid,
-                                         const floatx4& v) {
+__device__ __forceinline__ void st_frows(float* p, uint32_t co, const RowOff<F>& ro, int g,
+                                         bool valid, const floatx4& v) {
+  char* base = reinterpret_cast<char*>(p) + co;
 #pragma unroll
   for (int r = 0; r < GM<F>::RPG; ++r) {
     const int k = GM<F>::row(g, r);
-    if (valid && k >= 0) stE(p, eo + (uint32_t)k * RB, v[r]);
+    if (valid && k >= 0) *reinterpret_cast<float*>(base + opaque(ro.o[r])) = v[r];
   }
 }
 
@@ -435,6 +469,8 @@ __device__ __forceinline__ floatx4 ld_vec(const float* p, int t, int g) {
   return v;
 }
 
+// (the max(x, 0.1 x) form is no cheaper here: hipcc canonicalizes an MFMA
+// result before a v_max_f32 in IEEE mode, 3 VALU either way)
 __device__ __forceinline__ float lrelu(float x) { return x > 0.f ? x : PF_LEAKY * x; }
 __device__ __forceinline__ float dlrelu(float z) { return z > 0.f ? 1.f : PF_LEAKY; }
 template <int D>
@@ -574,8 +610,9 @@ __device__ __forceinline__ float mask_slope(uint32_t m, int s) {
   const uint32_t eo0 =                                                                \
       (uint32_t)((((long long)gg * geo.NC) * geo.NF + (fvalid ? f : 0)) * 4);         \
   const uint32_t eoc = (uint32_t)geo.NF * 4u;                                         \
+  const uint32_t EB = (uint32_t)geo.E * 4u; /* bytes per channel row and of the mask */ \
   const long long colbase = ((long long)gg * geo.NFG + fg) * geo.NC;                  \
-  (void)t; (void)n; (void)NS; (void)RB; (void)colbase; (void)j16;
+  (void)t; (void)n; (void)NS; (void)RB; (void)colbase; (void)j16; (void)EB;
 
 // x = valid ? (sc*raw + sh) : 0 on the lane's F slots
 template <int F>
@@ -590,7 +627,8 @@ __device__ __forceinline__ floatx4 edge_in(const floatx4& raw, const bool (&fm)[
 
 #define MF_FMASK(F)                                                                   \
   bool fm[4];                                                                         \
-  _Pragma("unroll") for (int r = 0; r < 4; ++r) fm[r] = fvalid && GM<F>::row(g4, r) >= 0;
+  _Pragma("unroll") for (int r = 0; r < 4; ++r) fm[r] = fvalid && GM<F>::row(g4, r) >= 0; \
+  const RowOff<F> ro(eo0, RB, g4);
 
 // ============================================================ EdgeModel fwd
 // y = W2 lrelu(Ps[f] + Pt[c] + W1[:, 2F:3F] x) + b2 per edge (gnn.py:86-101 with
@@ -621,17 +659,17 @@ __global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float*
   const floatx4 bb = ld_fconst<F>(b2, g4, 0.f);
   const floatx4 scv = ld_fconst<F>(xsc, g4, 1.f), shv = ld_fconst<F>(xsh, g4, 0.f);
   MF_FMASK(F)
+  const Rsrc rxe = rsrc(xe, EB * F);
 
   float cnt = 0.f;
   floatx4 mean = zero4(), m2 = zero4();
   __syncthreads();   // ptl
   auto load = [&](int c) {
     Rows<1> r;
-    r.v[0] = ld_frows<F>(xe, eo0 + (uint32_t)c * eoc, RB, g4);
+    r.v[0] = ld_frows<F>(rxe, (uint32_t)c * eoc, ro);
     return r;
   };
   class_stream<MF_DEPTH_FWD>(c0, c1, load, [&](const Rows<1>& rows, int c) {
-    const uint32_t eo = eo0 + (uint32_t)c * eoc;
     const floatx4 x[1] = {edge_in<F>(rows.v[0], fm, xsc, scv, shv)};
     floatx4 z[NT], a[NT];
 #pragma unroll
@@ -646,7 +684,7 @@ __global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float*
 #pragma unroll
       for (int r = 0; r < 4; ++r) yo[0][r] = bf_f(h[r]);
     }
-    st_frows<F>(y, eo, RB, g4, fvalid, yo[0]);
+    st_frows<F>(y, (uint32_t)c * eoc, ro, g4, fvalid, yo[0]);
     if (fvalid) {
       cnt += 1.f;
       const float rc = __builtin_amdgcn_rcpf(cnt);   // v_rcp_f32 (<= 1 ulp): a Welford weight
@@ -729,15 +767,33 @@ __global__ __launch_bounds__(256) void km_source_fwd(EdgeGeo geo, const float* _
   for (int tt = 0; tt < NT; ++tt) bias[tt] = ld_vec<C>(bs2, tt, g4);
   const floatx4 scv = ld_fconst<F>(sc, g4, 1.f), shv = ld_fconst<F>(sh, g4, 0.f);
   MF_FMASK(F)
+  const Rsrc ry = rsrc(y, EB * F);
 
   floatx4 S1[NT], S2[NT], S3[NT], S4[NT];  // mean | M2 | M3 | M4
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt) S1[tt] = S2[tt] = S3[tt] = S4[tt] = zero4();
-  float cnt = 0.f;
-  __syncthreads();   // qtl
+  // Pebay's one-pass update of the central sums after the n-th message, with
+  // its count-only coefficients per class (uniform over the wave) from a table:
+  //   d = m - mean;  M4 += d^4 A4 + 6 d^2 M2 / n^2 - 4 d M3 / n;
+  //   M3 += d^3 A3 - 3 d M2 / n;  M2 += d^2 A2;  mean += d / n
+  // A2 = (n-1)/n, A3 = (n-1)(n-2)/n^2, A4 = (n-1)(n^2-3n+3)/n^3 (12 VALU per
+  // element, the M2 / M3 of the previous count on the right-hand sides)
+  __shared__ __attribute__((aligned(16))) float pco[MF_MAX_CPS][8];
+  if (t < c1 - c0) {
+    const double nn = t + 1, r = 1.0 / nn;
+    pco[t][0] = (float)((nn - 1) * r);                            // A2
+    pco[t][1] = (float)((nn - 1) * (nn - 2) * r * r);             // A3
+    pco[t][2] = (float)((nn - 1) * (nn * nn - 3 * nn + 3) * r * r * r);  // A4
+    pco[t][3] = (float)r;                                         // 1/n
+    pco[t][4] = (float)(6 * r * r);                               // 6/n^2
+    pco[t][5] = (float)(-4 * r);                                  // -4/n
+    pco[t][6] = (float)(-3 * r);                                  // -3/n
+    pco[t][7] = 0.f;
+  }
+  __syncthreads();   // qtl, pco
   auto load = [&](int c) {
     Rows<1> r;
-    r.v[0] = ld_frows<F>(y, eo0 + (uint32_t)c * eoc, RB, g4);
+    r.v[0] = ld_frows<F>(ry, (uint32_t)c * eoc, ro);
     return r;
   };
   class_stream<MF_DEPTH_FWD>(c0, c1, load, [&](const Rows<1>& rows, int c) {
@@ -750,19 +806,18 @@ __global__ __launch_bounds__(256) void km_source_fwd(EdgeGeo geo, const float* _
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) m[tt] = bias[tt];
     L2.apply(a, m);
-    const float nold = cnt;
-    cnt += 1.f;
-    const float inv = __builtin_amdgcn_rcpf(cnt), a3 = cnt - 2.f, a4 = cnt * cnt - 3.f * cnt + 3.f;
+    const floatx4 ca = *reinterpret_cast<const floatx4*>(&pco[c - c0][0]);
+    const floatx4 cb = *reinterpret_cast<const floatx4*>(&pco[c - c0][4]);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
       for (int r = 0; r < GM<C>::nreg(tt); ++r) {
-        const float delta = m[tt][r] - S1[tt][r];
-        const float dn = delta * inv, dn2 = dn * dn, t1 = delta * dn * nold;
-        S4[tt][r] = fmaf(t1 * dn2, a4, fmaf(6.f * dn2, S2[tt][r], fmaf(-4.f * dn, S3[tt][r], S4[tt][r])));
-        S3[tt][r] = fmaf(t1 * dn, a3, fmaf(-3.f * dn, S2[tt][r], S3[tt][r]));
-        S2[tt][r] += t1;
-        S1[tt][r] += dn;
+        const float d = m[tt][r] - S1[tt][r], d2 = d * d;
+        const float m2 = S2[tt][r], m3 = S3[tt][r];
+        S4[tt][r] = fmaf(d, m3 * cb[1], fmaf(d2, fmaf(d2, ca[2], m2 * cb[0]), S4[tt][r]));
+        S3[tt][r] = fmaf(d, fmaf(d2, ca[1], m2 * cb[2]), m3);
+        S2[tt][r] = fmaf(d2, ca[0], m2);
+        S1[tt][r] = fmaf(d, ca[3], S1[tt][r]);
       }
   });
   if (fvalid) {
@@ -803,11 +858,12 @@ __global__ __launch_bounds__(256) void km_target_fwd(EdgeGeo geo, const float* _
   for (int tt = 0; tt < NT; ++tt) rs[tt] = ld_node<C>(Rs, tt, g4, NS, n, fvalid);
   const floatx4 scv = ld_fconst<F>(sc, g4, 1.f), shv = ld_fconst<F>(sh, g4, 0.f);
   MF_FMASK(F)
+  const Rsrc ry = rsrc(y, EB * F);
 
   int cbase = c0;
   auto load = [&](int c) {
     Rows<1> r;
-    r.v[0] = ld_frows<F>(y, eo0 + (uint32_t)c * eoc, RB, g4);
+    r.v[0] = ld_frows<F>(ry, (uint32_t)c * eoc, ro);
     return r;
   };
   class_stream<MF_DEPTH_FWD>(c0, c1, load, [&](const Rows<1>& rows, int c) {
@@ -816,7 +872,8 @@ __global__ __launch_bounds__(256) void km_target_fwd(EdgeGeo geo, const float* _
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) z[tt] = rs[tt];
     L1.apply(x, z);
-    if (tmask && fvalid) tmask[eo0 + (uint32_t)c * eoc + g4] = (uint8_t)mask_bits<C>(z);
+    if (tmask && fvalid)
+      (tmask + (uint32_t)c * eoc)[opaque(eo0 + g4)] = (uint8_t)mask_bits<C>(z);
     const int cl = c - cbase;
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt)
@@ -872,17 +929,17 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
   }
   const floatx4 scv = ld_fconst<F>(sc, g4, 1.f), shv = ld_fconst<F>(sh, g4, 0.f);
   MF_FMASK(F)
+  const Rsrc ry = rsrc(y, EB * F), rtm = rsrc(tmask, EB);
   __syncthreads();   // ghl
 
   auto load = [&](int c) {
     Rows<1> r;
-    const uint32_t eo = eo0 + (uint32_t)c * eoc;
-    r.v[0] = ld_frows<F>(y, eo, RB, g4);
-    if constexpr (TM) r.m = tmask[eo + g4];
+    const uint32_t co = (uint32_t)c * eoc;
+    r.v[0] = ld_frows<F>(ry, co, ro);
+    if constexpr (TM) r.m = __builtin_amdgcn_raw_buffer_load_b8(rtm, eo0 + g4, co, 0);
     return r;
   };
   class_stream<MF_DEPTH_BWD>(c0, c1, load, [&](const Rows<1>& rows, int c) {
-    const uint32_t eo = eo0 + (uint32_t)c * eoc;
     const floatx4 x[1] = {edge_in<F>(rows.v[0], fm, sc, scv, shv)};
     floatx4 z[NT], gz[NT];
     if constexpr (!TM) {
@@ -907,7 +964,7 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
     if (gxe) {
       floatx4 gx[1] = {zero4()};
       if constexpr (PREC >= 1) LT.apply(sgz, gx); else LT.apply(gz, gx);
-      st_frows<F>(gxe, eo, RB, g4, fvalid, gx[0]);
+      st_frows<F>(gxe, (uint32_t)c * eoc, ro, g4, fvalid, gx[0]);
     }
     lds_order();
 #pragma unroll
@@ -994,6 +1051,7 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   const floatx4 scv = ld_fconst<F>(sc, g4, 1.f), shv = ld_fconst<F>(sh, g4, 0.f);
   const floatx4 m1v = ld_fconst<F>(mu1, g4, 0.f), i1v = ld_fconst<F>(inv1, g4, 0.f);
   MF_FMASK(F)
+  const Rsrc ry = rsrc(y, EB * F), rgn = rsrc(g_next, EB * F), rtm = rsrc(tmask, EB);
 
   floatx4 accW2[NT * NT], accW1[NT], accB[NT];
 #pragma unroll
@@ -1009,14 +1067,13 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   int cbase = c0;
   auto load = [&](int c) {
     Rows<2> r;
-    const uint32_t eo = eo0 + (uint32_t)c * eoc;
-    r.v[0] = ld_frows<F>(y, eo, RB, g4);
-    r.v[1] = g_next ? ld_frows<F>(g_next, eo, RB, g4) : zero4();
-    if constexpr (TM) r.m = tpart ? tmask[eo + g4] : 0u;
+    const uint32_t co = (uint32_t)c * eoc;
+    r.v[0] = ld_frows<F>(ry, co, ro);
+    r.v[1] = g_next ? ld_frows<F>(rgn, co, ro) : zero4();
+    if constexpr (TM) r.m = tpart ? __builtin_amdgcn_raw_buffer_load_b8(rtm, eo0 + g4, co, 0) : 0u;
     return r;
   };
   class_stream<MF_DEPTH_BWD>(c0, c1, load, [&](const Rows<2>& rows, int c) {
-    const uint32_t eo = eo0 + (uint32_t)c * eoc;
     const floatx4 yr = rows.v[0], gnr = rows.v[1];
     const floatx4 x[1] = {edge_in<F>(yr, fm, sc, scv, shv)};
     // ---- forward recompute: z_s, a_s, m
@@ -1094,7 +1151,7 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) g[0][r] = fm[r] ? g[0][r] + (g_next ? gnr[r] : 0.f) : 0.f;
-    st_frows<F>(g_tot, eo, RB, g4, fvalid, g[0]);
+    st_frows<F>(g_tot, (uint32_t)c * eoc, ro, g4, fvalid, g[0]);
     if (mu1) {
 #pragma unroll
       for (int r = 0; r < GM<F>::RPG; ++r) {
@@ -1221,19 +1278,19 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
                 g1v = ld_fconst<F>(gam1, g4, 0.f);
   const floatx4 scv = ld_fconst<F>(xsc, g4, 1.f), shv = ld_fconst<F>(xsh, g4, 0.f);
   MF_FMASK(F)
+  const Rsrc rgt = rsrc(g_tot, EB * F), ry = rsrc(y, EB * F), rxe = rsrc(xe, EB * F);
   __syncthreads();   // ptl
 
   int cbase = c0;
   auto load = [&](int c) {
     Rows<3> r;
-    const uint32_t eo = eo0 + (uint32_t)c * eoc;
-    r.v[0] = ld_frows<F>(g_tot, eo, RB, g4);
-    r.v[1] = ld_frows<F>(y, eo, RB, g4);
-    r.v[2] = ld_frows<F>(xe, eo, RB, g4);
+    const uint32_t co = (uint32_t)c * eoc;
+    r.v[0] = ld_frows<F>(rgt, co, ro);
+    r.v[1] = ld_frows<F>(ry, co, ro);
+    r.v[2] = ld_frows<F>(rxe, co, ro);
     return r;
   };
   class_stream<MF_DEPTH_BWD>(c0, c1, load, [&](const Rows<3>& rows, int c) {
-    const uint32_t eo = eo0 + (uint32_t)c * eoc;
     floatx4 gy[1] = {zero4()};
 #pragma unroll
     for (int r = 0; r < GM<F>::RPG; ++r)
@@ -1272,7 +1329,7 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
     if (gxe) {
       floatx4 gx[1] = {zero4()};
       if constexpr (PREC >= 1) L1T.apply(sgz, gx); else L1T.apply(gz, gx);
-      st_frows<F>(gxe, eo, RB, g4, fvalid, gx[0]);
+      st_frows<F>(gxe, (uint32_t)c * eoc, ro, g4, fvalid, gx[0]);
     }
     const s16x8 tgy = img_trA(im_gy, lane);
 #pragma unroll

@@ -777,7 +777,7 @@ class HipBackend:
         if d.sp is not None:
             return None
         n = lib().pfsgnn_tmask_bytes(d.G, d.NF, d.NC, d.F)
-        return torch.empty(n, dtype=torch.uint8, device=config.device) if n else None
+        return torch.empty(n, dtype=torch.uint8, device=self.device) if n else None
 
     def target_fwd(self, d, y, sc, sh, Rs, Wt1, agg=None, tmask=None):
         """-> hsum; with ``agg`` = (Wt2, bt2, bscale) -> (hsum, Wt2 hsum + bscale bt2),
