@@ -64,7 +64,10 @@ def parse():
                     help="launch every kernel from Python instead of replaying a captured HIP graph")
     ap.add_argument("--edge-path", default=os.environ.get("PFSGNN_EDGE_PATH", "mfma"),
                     help="per-edge kernel precision: mfma (default: fp32 forward, bf16x3 "
-                         "gradient chains), mfma32, valu, bf16y, bf16m, bf16 (configs[4])")
+                         "gradient chains), mfma32, valu, bf16y, bf16m, bf16, bf16x3 (configs[4])")
+    ap.add_argument("--alt-paths", default="bf16x3,mfma32",
+                    help="other edge paths whose step rate is measured after the headline "
+                         "one (N=1, graph replay; reported in alt_paths; '' for none)")
     return ap.parse_args()
 
 
@@ -87,12 +90,13 @@ def make_batch(G, rank, device):
 # per-edge algorithmic HBM bytes of each main kernel
 def kernel_bytes_per_edge(F, first_block_excluded=False):
     f = 4 * F
+    m = 4 if 2 * F <= 32 else 0   # TModel's LeakyReLU mask, 1 byte per (edge, lane group)
     return {
         "edge_mlp_fwd": 2 * f,   # read xe, write y
         "source_fwd": f,         # read y
-        "target_fwd": f,         # read y
-        "target_bwd": f,         # read y
-        "source_bwd": 3 * f,     # read y, g_next; write g_tot
+        "target_fwd": f + m,     # read y; write the TModel mask
+        "target_bwd": f + m,     # read y, the mask
+        "source_bwd": 3 * f + m,  # read y, g_next, the mask; write g_tot
         "edge_mlp_bwd": 4 * f,   # read g_tot, y, xe; write g_xe (blocks > 0)
         "loss_fwd": f,
         "loss_bwd": 2 * f,
@@ -314,6 +318,33 @@ def main():
             consistency[name + "_bitwise_equal"] = bool(torch.equal(hi, lo))
         assert all(consistency.values()), consistency
 
+    # ---- the same step on the other edge paths (BASELINE configs[4]: the
+    # bf16x3 contractions; the exact-fp32 one), each captured and replayed like
+    # the headline path, N=1 only; the parameters keep training (synthetic data)
+    alt = {}
+    if world == 1 and use_graph and args.alt_paths:
+        for pth in [p for p in args.alt_paths.split(",") if p and p != args.edge_path]:
+            native.set_edge_path(pth)
+            for i in range(2):
+                fwd_bwd()
+                opt.step()
+            torch.cuda.synchronize()
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2):
+                fwd_bwd()
+                opt.step()
+            g2.replay()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(args.steps):
+                g2.replay()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            alt[pth] = {"value": E * args.steps / el, "ms_per_step": el / args.steps * 1e3,
+                        "precision": PRECISION[pth]}
+            del g2
+        native.set_edge_path(args.edge_path)
+
     # ---- per-kernel device times: HIP events around each main kernel, on its
     # launch stream, over a few eager steps of the same workload right after
     # the timed region (a replayed graph has no per-kernel host hook)
@@ -391,6 +422,8 @@ def main():
         }
         if consistency is not None:
             line["rank_consistency"] = consistency
+        if alt:
+            line["alt_paths"] = alt
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

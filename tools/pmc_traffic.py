@@ -11,7 +11,7 @@ tools/calib_pmc.sh on known byte counts past the Infinity Cache):
     runs of different channel rows): reads are corrected by 1/0.625 = 1.6;
     the guide's 2.0 (upper bound) is reported beside it.
 
-    python tools/pmc_traffic.py gpurun_out/pmc_xxx r02b128 [E F B]
+    python tools/pmc_traffic.py gpurun_out/pmc_xxx r02b128 [E F B [pass-dir prefix]]
 """
 import collections
 import csv
@@ -30,8 +30,16 @@ read_cal = cal["edge_read_correction"]
 
 
 def kname(full):
-    """'void (anonymous namespace)::km_source_bwd<10>(EdgeGeo, ...)' -> 'km_source_bwd<10>'"""
-    return full.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+    """'void (anonymous namespace)::km_source_bwd<10, 1, true>(EdgeGeo, ...)' ->
+    'km_source_bwd<10>' (the Fdim only: the precision / mask template flags of
+    one edge path are one kernel per step)"""
+    k = full.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+    if k.startswith(("km_", "k_")) and "<" in k:
+        k = k.split("<")[0] + "<" + k.split("<")[1].split(",")[0].rstrip(">") + ">"
+    return k
+
+
+PREC = os.environ.get("PFSGNN_PMC_PREC", "1")   # the default edge path's MFMA kernels
 
 
 def per_dispatch(path, counter):
@@ -39,6 +47,15 @@ def per_dispatch(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
+        full = r["Kernel_Name"]
+        if "km_" in full and "forward" not in full:
+            # only the headline path's kernels (bench.py also times other
+            # paths): <F, PREC[, TM]>, the forward kernels' PREC being 0 for it
+            tmpl = full.split("<")[1].split(">")[0].split(",")
+            want = ("0" if PREC == "1" else PREC) if kname(full).split("<")[0] in (
+                "km_edge_mlp_fwd", "km_source_fwd", "km_target_fwd") else PREC
+            if tmpl[1].strip() != want:
+                continue
         k = kname(r["Kernel_Name"])
         agg[k] += float(r["Counter_Value"])
         n[k].add(r["Dispatch_Id"])
@@ -57,8 +74,9 @@ def algorithmic(kernel):
     return per[base] * E
 
 
-fetch = per_dispatch(os.path.join(d, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-write = per_dispatch(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+pre = sys.argv[6] if len(sys.argv) > 6 else ""     # pass directories <d>/<pre>fetch, <pre>write
+fetch = per_dispatch(os.path.join(d, pre + "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+write = per_dispatch(os.path.join(d, pre + "write", "run_counter_collection.csv"), "WRITE_SIZE")
 out = {"E": E, "F": F, "read_calibration": read_cal,
        "calibration": "profiles/r02_fetch_calibration.json (rdrows pattern)",
        "note": "traffic_bytes = FETCH_SIZE*read_calibration + WRITE_SIZE per launch; "
