@@ -41,6 +41,9 @@ PRECISION = {
     "bf16y": "mfma32 arithmetic with the edge state rounded to bf16",
     "bf16m": "every per-edge contraction a single bf16 MFMA, fp32 accumulation and edge state",
     "bf16": "single-bf16 MFMA contractions and bf16 edge state",
+    "bf16x6": "forward contractions and their backward recompute on bf16 MFMAs with three-way "
+              "split operands (hi+mid+lo, six products: fp32-class, ~2^-24 relative); backward "
+              "gradient chains and weight gradients bf16x3; fp32 accumulation and edge state",
     "bf16x3": "every per-edge contraction (forward, backward recompute, gradient chains, weight "
               "gradients) on bf16 MFMAs with split hi+lo operands (bf16x3, ~2^-16 relative per "
               "product); fp32 accumulation, edge state, node level and loss (BASELINE configs[4])",
@@ -65,7 +68,7 @@ def parse():
     ap.add_argument("--edge-path", default=os.environ.get("PFSGNN_EDGE_PATH", "mfma"),
                     help="per-edge kernel precision: mfma (default: fp32 forward, bf16x3 "
                          "gradient chains), mfma32, valu, bf16y, bf16m, bf16, bf16x3 (configs[4])")
-    ap.add_argument("--alt-paths", default="bf16x3,mfma32",
+    ap.add_argument("--alt-paths", default="bf16x3,bf16x6,mfma32",
                     help="other edge paths whose step rate is measured after the headline "
                          "one (N=1, graph replay; reported in alt_paths; '' for none)")
     return ap.parse_args()
@@ -105,16 +108,17 @@ def kernel_bytes_per_edge(F, first_block_excluded=False):
 
 # per-edge algorithmic FLOPs (2 per real multiply-add of the unpadded layer
 # shapes); H = 4F hidden units of the EdgeModel MLP,
-# C = 2F of the S/T message MLPs.  source_bwd includes TModel's recomputed
-# input gradient; edge_mlp_bwd's input-gradient product is absent in block 0.
+# C = 2F of the S/T message MLPs.  source_bwd includes TModel's input-gradient
+# chain (its pre-activation comes from target_fwd's mask, not recomputed);
+# edge_mlp_bwd's input-gradient product is absent in block 0.
 def kernel_flops_per_edge(F, B):
     H, C = 4 * F, 2 * F
     return {
         "edge_mlp_fwd": 2 * (H * F + F * H) + 4 * H,
-        "source_fwd": 2 * (C * F + C * C) + 4 * C + 14 * C,
+        "source_fwd": 2 * (C * F + C * C) + 4 * C + 12 * C,
         "target_fwd": 2 * C * F + 4 * C,
-        "target_bwd": 2 * (C * F + C * F) + 3 * C,
-        "source_bwd": 2 * (C * F + C * C + C * C + F * C + C * F + F * C + C * C + C * F) + 12 * C,
+        "target_bwd": 2 * C * F + 3 * C,
+        "source_bwd": 2 * (C * F + C * C + C * C + F * C + F * C + C * C + C * F) + 12 * C,
         "edge_mlp_bwd": 2 * (H * F + H * F + H * F + F * H) + 2 * (F * H) * (B - 1) / B + 8 * H,
     }
 

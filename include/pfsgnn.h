@@ -57,7 +57,11 @@ size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F);
  *   PFSGNN_EDGE_BF16X3 -- every per-edge contraction, the forward ones and
  *       their backward recompute included, on v_mfma_f32_16x16x32_bf16 with
  *       split operands (bf16 hi + lo, ~2^-16 relative per product, fp32
- *       accumulation and edge state; BASELINE configs[4] at fp32 tolerance).
+ *       accumulation and edge state; BASELINE configs[4] at fp32 tolerance);
+ *   PFSGNN_EDGE_BF16X6 -- the forward contractions and their backward
+ *       recompute on v_mfma_f32_16x16x32_bf16 with three-way split operands
+ *       (hi + mid + lo, the six products down to ~2^-18: fp32-class
+ *       products), the gradient chains and weight gradients as PFSGNN_EDGE_MFMA.
  * The fp32-class paths (MFMA, MFMA_F32, VALU) produce the same outputs to the
  * parity tolerance; the bf16 paths' deviation is measured, not bounded
  * (DESIGN.md §Numerics).  Node-level ops, reductions and the loss are shared. */
@@ -68,6 +72,7 @@ size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F);
 #define PFSGNN_EDGE_BF16 4
 #define PFSGNN_EDGE_BF16_MFMA 5
 #define PFSGNN_EDGE_BF16X3 6
+#define PFSGNN_EDGE_BF16X6 7
 int pfsgnn_set_edge_path(int path);
 int pfsgnn_get_edge_path(void);
 /* Grid the current edge path launches for a batch (host-only query, for tests

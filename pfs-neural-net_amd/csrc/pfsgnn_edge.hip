@@ -1335,7 +1335,8 @@ int mf_prec(int model) {
   }();
   return g_path == PFSGNN_EDGE_MFMA ? 1
          : (g_path == PFSGNN_EDGE_BF16 || g_path == PFSGNN_EDGE_BF16_MFMA) ? 2
-         : g_path == PFSGNN_EDGE_BF16X3 ? ((x3mask >> model) & 1 ? 3 : 1) : 0;
+         : g_path == PFSGNN_EDGE_BF16X3 ? ((x3mask >> model) & 1 ? 3 : 1)
+         : g_path == PFSGNN_EDGE_BF16X6 ? 4 : 0;
 }
 int mf_bfy() { return g_path == PFSGNN_EDGE_BF16Y || g_path == PFSGNN_EDGE_BF16 ? 1 : 0; }
 // MFMA blocks stage their class-table rows in LDS: at most MAX_CPS classes each
@@ -1377,10 +1378,10 @@ EdgeGeo geo_for(int G, int NF, int NC) {
 }  // namespace
 
 extern "C" int pfsgnn_set_edge_path(int path) {
-  if (path < PFSGNN_EDGE_VALU || path > PFSGNN_EDGE_BF16X3)
+  if (path < PFSGNN_EDGE_VALU || path > PFSGNN_EDGE_BF16X6)
     return pf::fail("pfsgnn_set_edge_path",
-                    "path must be PFSGNN_EDGE_VALU, _MFMA, _MFMA_F32, _BF16Y, _BF16, _BF16_MFMA "
-                    "or _BF16X3");
+                    "path must be PFSGNN_EDGE_VALU, _MFMA, _MFMA_F32, _BF16Y, _BF16, _BF16_MFMA, "
+                    "_BF16X3 or _BF16X6");
   g_path = path;
   return 0;
 }

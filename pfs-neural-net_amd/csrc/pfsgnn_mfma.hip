@@ -131,6 +131,11 @@ struct Fr {
 __device__ __forceinline__ float bf_f(short s) {
   return __builtin_bit_cast(float, ((uint32_t)(uint16_t)s) << 16);
 }
+// bf16_rne of four values (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ s16x4 hi4(const floatx4& v) {
+  const b16x4 h = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  return __builtin_bit_cast(s16x4, h);
+}
 // v = hi + lo (+ ~2^-17 |v|): hi = bf16_rne(v), lo = bf16_rne(v - hi)
 __device__ __forceinline__ Fr split(const floatx4& v) {
   const b16x4 h = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
@@ -227,6 +232,67 @@ struct LayerB3 {
   }
 };
 
+// ------------------------------------------------------------ bf16x6 layer
+// y (+)= W x with three-way split operands v = vh + vm + vl (each bf16 RNE,
+// |v - vh - vm - vl| <= ~2^-27 |v|) and the six products whose order is at most
+// 2^-18: Wh xh, Wh xm, Wm xh, Wh xl, Wl xh, Wm xm -- the dropped ones are
+// <= ~2^-26 relative, so a product is as exact as fp32's own rounding and the
+// contraction has the numerics of an fp32 one (PREC 4: the forward
+// contractions and their recompute).  Per K-tile three v_mfma_f32_16x16x32_bf16,
+// small terms first: [Wh | Wm].[xl | xm] (hl + mm), [Wh | Wl].[xm | xh]
+// (hm + lh), [Wh | Wm].[xh | xh] (hh + mh): 48 cycles per 16 K-slots where
+// v_mfma_f32_16x16x4_f32 takes 128.
+struct Fr3 {
+  s16x4 h, m, l;
+};
+__device__ __forceinline__ Fr3 split3(const floatx4& v) {
+  const s16x4 h = hi4(v);
+  floatx4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = v[j] - bf_f(h[j]);
+  const s16x4 m = hi4(r);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = r[j] - bf_f(m[j]);
+  return {h, m, hi4(r)};
+}
+template <int M, int K>
+struct LayerB6 {
+  static constexpr int MT = GM<M>::NT, KT = GM<K>::NT;
+  s16x8 ahm[MT][KT], ahl[MT][KT];   // [Wh | Wm], [Wh | Wl]
+  template <class Fn>
+  __device__ __forceinline__ void load(Fn fn, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+        floatx4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ro = GM<M>::mrow(t, i), ri = GM<K>::row(g, 4 * u + j);
+          v[j] = (ro >= 0 && ri >= 0) ? fn(ro, ri) : 0.f;
+        }
+        const Fr3 a = split3(v);
+        ahm[t][u] = cat8(a.h, a.m);
+        ahl[t][u] = cat8(a.h, a.l);
+      }
+  }
+  __device__ __forceinline__ void apply(const Fr3 (&x)[KT], floatx4 (&y)[MT]) const {
+#pragma unroll
+    for (int u = 0; u < KT; ++u) {
+      const s16x8 b1 = cat8(x[u].l, x[u].m), b2 = cat8(x[u].m, x[u].h), b3 = cat8(x[u].h, x[u].h);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) y[t] = mf8(ahm[t][u], b3, mf8(ahl[t][u], b2, mf8(ahm[t][u], b1, y[t])));
+    }
+  }
+  __device__ __forceinline__ void apply(const floatx4 (&x)[KT], floatx4 (&y)[MT]) const {
+    Fr3 s[KT];
+#pragma unroll
+    for (int u = 0; u < KT; ++u) s[u] = split3(x[u]);
+    apply(s, y);
+  }
+};
+
 // ------------------------------------------------------------ weight gradients
 // acc += A B^T summed over a tile's 16 edges (edge = MFMA K), A and B read from
 // wave-private bf16 images (hi and lo planes), as 2 v_mfma_f32_16x16x32_bf16:
@@ -247,10 +313,6 @@ __device__ __forceinline__ floatx4 mma3g(s16x8 a_hl, const WgB& b, floatx4 c) {
 // y (+)= W x with every product a single v_mfma_f32_16x16x16_bf16 on bf16
 // operands (RNE), fp32 accumulation: the "bf16" edge path (BASELINE configs[4],
 // PFSGNN_EDGE_BF16) -- one MFMA per K-tile where LayerF issues GM<K>::RPG.
-__device__ __forceinline__ s16x4 hi4(const floatx4& v) {
-  const b16x4 h = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-  return __builtin_bit_cast(s16x4, h);
-}
 template <int M, int K>
 struct LayerB1 {
   static constexpr int MT = GM<M>::NT, KT = GM<K>::NT, KP = (KT + 1) / 2;
@@ -298,14 +360,23 @@ struct LayerB1 {
 //   0 exact fp32 everywhere (PFSGNN_EDGE_MFMA_F32, _BF16Y);
 //   1 forward fp32, backward gradient chains bf16x3 (PFSGNN_EDGE_MFMA);
 //   2 every contraction single bf16 (PFSGNN_EDGE_BF16);
-//   3 every contraction bf16x3, forward and recompute included (PFSGNN_EDGE_BF16X3).
+//   3 every contraction bf16x3, forward and recompute included (PFSGNN_EDGE_BF16X3);
+//   4 forward contractions and recompute bf16x6 (fp32-class), backward gradient
+//     chains bf16x3 (PFSGNN_EDGE_BF16X6).
 // The forward layers of a backward kernel (its recompute) use FwdLayer<FP(PREC)>,
 // exactly the arithmetic of the forward kernel, so the recomputed activations
 // and LeakyReLU masks are bitwise those of the forward pass.
-__host__ __device__ constexpr int FP(int prec) { return prec == 2 ? 2 : prec == 3 ? 3 : 0; }
+__host__ __device__ constexpr int FP(int prec) { return prec >= 2 ? prec : 0; }
+// source_bwd's recompute at PREC 4 stays exact fp32 (LayerF): the bf16x6 weight
+// tuples would push that kernel past 256 VGPRs (spills).  Its activations then
+// differ from the forward's by fp32 rounding only, the level at which the fp32
+// reference differs from the float64 oracle.
+__host__ __device__ constexpr int FPS(int prec) { return prec == 4 ? 0 : FP(prec); }
 template <int PREC, int M, int K>
 using FwdLayer = std::conditional_t<
-    PREC == 2, LayerB1<M, K>, std::conditional_t<PREC == 3, LayerB3<M, K>, LayerF<M, K>>>;
+    PREC == 2, LayerB1<M, K>,
+    std::conditional_t<PREC == 3, LayerB3<M, K>,
+                       std::conditional_t<PREC == 4, LayerB6<M, K>, LayerF<M, K>>>>;
 template <int PREC, int M, int K>
 using GradLayer = std::conditional_t<
     PREC == 0, LayerF<M, K>, std::conditional_t<PREC == 2, LayerB1<M, K>, LayerB3<M, K>>>;
@@ -502,7 +573,9 @@ __device__ __forceinline__ float row_sum16(float v) {
 // Per-class column partials of the block, chunked: each wave parks its 16-fiber
 // sums of COL_CH classes in buf[COL_CH][4][CW]; the block then writes the 4-wave
 // sums (fixed order) to part[(rowbase + c) * CW + h] ([G][NFG][NC][CW] layout).
+#ifndef COL_CH
 #define COL_CH 8
+#endif
 template <int CW>
 __device__ __forceinline__ void col_flush(const float* buf, int nch, int cbase, float* part,
                                           long long rowbase) {
@@ -1026,10 +1099,10 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   const long long CNS = (long long)C * NS;
   const bool tpart = Rs != nullptr;
 
-  FwdLayer<FP(PREC), C, F> L1s, L1t;   // L1t: TModel's layer, recomputed unless TM
+  FwdLayer<FPS(PREC), C, F> L1s, L1t;   // L1t: TModel's layer, recomputed unless TM
   L1s.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
   if constexpr (!TM) L1t.load([&](int h, int k) { return tpart ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
-  FwdLayer<FP(PREC), C, C> L2;
+  FwdLayer<FPS(PREC), C, C> L2;
   L2.load([&](int o, int h) { return Ws2[o * C + h]; }, lane);
   // gradient chains: exact fp32, bf16x3 or bf16 by PREC
   GradLayer<PREC, C, C> L2T;
@@ -1396,30 +1469,32 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
 // Instantiations: Fdim 8, 10, 16 for the fp32 / bf16x3 precisions (PREC 0, 1);
 // the single-bf16 path (PREC 2, BASELINE configs[4]) at Fdim 10.
 #define MF_CASE(FF, PP, K, ...)                                                   \
-  case FF * 4 + PP: {                                                             \
+  case FF * 8 + PP: {                                                             \
     hipLaunchKernelGGL((K<FF, PP>), dim3(geo.nblocks), dim3(256), 0, st, geo,     \
                        __VA_ARGS__);                                              \
   } break;
 #define MF_LAUNCH(F, P, K, ...)                                                   \
-  switch ((F) * 4 + (P)) {                                                        \
+  switch ((F) * 8 + (P)) {                                                        \
     MF_CASE(8, 0, K, __VA_ARGS__) MF_CASE(8, 1, K, __VA_ARGS__)                  \
     MF_CASE(10, 0, K, __VA_ARGS__) MF_CASE(10, 1, K, __VA_ARGS__)                \
     MF_CASE(10, 2, K, __VA_ARGS__) MF_CASE(10, 3, K, __VA_ARGS__)                \
+    MF_CASE(10, 4, K, __VA_ARGS__)                                                \
     MF_CASE(16, 0, K, __VA_ARGS__) MF_CASE(16, 1, K, __VA_ARGS__)                \
     default: return pf::fail("pfsgnn mfma", "unsupported Fdim for this edge path"); \
   }
 
 // kernels with a third template flag (TM: the TModel mask is read, not recomputed)
 #define MF_CASE3(FF, PP, TT, K, ...)                                              \
-  case FF * 4 + PP: {                                                             \
+  case FF * 8 + PP: {                                                             \
     hipLaunchKernelGGL((K<FF, PP, TT>), dim3(geo.nblocks), dim3(256), 0, st, geo, \
                        __VA_ARGS__);                                              \
   } break;
 #define MF_LAUNCH3(F, P, TT, K, ...)                                              \
-  switch ((F) * 4 + (P)) {                                                        \
+  switch ((F) * 8 + (P)) {                                                        \
     MF_CASE3(8, 0, TT, K, __VA_ARGS__) MF_CASE3(8, 1, TT, K, __VA_ARGS__)        \
     MF_CASE3(10, 0, TT, K, __VA_ARGS__) MF_CASE3(10, 1, TT, K, __VA_ARGS__)      \
     MF_CASE3(10, 2, TT, K, __VA_ARGS__) MF_CASE3(10, 3, TT, K, __VA_ARGS__)      \
+    MF_CASE3(10, 4, TT, K, __VA_ARGS__)                                           \
     MF_CASE3(16, 0, TT, K, __VA_ARGS__) MF_CASE3(16, 1, TT, K, __VA_ARGS__)      \
     default: return pf::fail("pfsgnn mfma", "unsupported Fdim for this edge path"); \
   }

@@ -16,6 +16,12 @@ import torch
 from .sparse import SparseEdgeOps, SparseGeo
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpfsgnn.so")
+# tuning builds (tools/variants.sh): PFSGNN_LIB_VARIANT=<name> loads
+# pfsgnn/libpfsgnn_<name>.so, an in-tree build of the same sources with other
+# compile-time knobs
+if os.environ.get("PFSGNN_LIB_VARIANT"):
+    _LIB_PATH = os.path.join(os.path.dirname(_LIB_PATH),
+                             "libpfsgnn_" + os.environ["PFSGNN_LIB_VARIANT"] + ".so")
 
 
 class NativeUnavailable(RuntimeError):
@@ -184,7 +190,8 @@ def lib():
     return _lib
 
 
-EDGE_PATHS = {"valu": 0, "mfma": 1, "mfma32": 2, "bf16y": 3, "bf16": 4, "bf16m": 5, "bf16x3": 6}
+EDGE_PATHS = {"valu": 0, "mfma": 1, "mfma32": 2, "bf16y": 3, "bf16": 4, "bf16m": 5, "bf16x3": 6,
+              "bf16x6": 7}
 
 
 def set_edge_path(path):
@@ -194,7 +201,9 @@ def set_edge_path(path):
     (mfma32 with the edge state rounded to bf16), "bf16m" (single-bf16 MFMA
     contractions), "bf16" (bf16m + bf16 edge state) or "bf16x3" (every
     per-edge contraction on bf16 MFMAs with split hi + lo operands, forward and
-    recompute included; BASELINE configs[4] at fp32 tolerance).  The bf16
+    recompute included; BASELINE configs[4] at fp32 tolerance) or "bf16x6"
+    (the forward contractions and recompute on bf16 MFMAs with three-way split
+    operands, fp32-class products; gradient chains as "mfma").  The bf16
     paths are built for Fdim 10.
     Read at launch time; env PFSGNN_EDGE_PATH sets it when the library loads."""
     if path not in EDGE_PATHS:

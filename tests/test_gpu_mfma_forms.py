@@ -1,13 +1,19 @@
 """MFMA form mixing on gfx950 (DESIGN.md §MFMA form mixing).
 
-An accumulation chain of v_mfma_f32_16x16x32_bf16 finished on the SAME
-accumulator by a v_mfma_f32_16x16x16_bf16 gave wrong sums in round 2's edge
-kernels; since round 3 every bf16 chain of pfsgnn_mfma.hip is on the one
-16x16x32 form.  This test runs the mixed chain (tests/native/mfma_mix.hip) as
-hipcc schedules it, with 16 wait states forced between the two forms, and in
-the other order, against a float64 reference of the same products (bf16
-products are exact in fp32; the sums of 48 of them per element are compared at
-1e-6 of their scale), and pins which of them is right.
+Round 2 recorded that an accumulation chain of v_mfma_f32_16x16x32_bf16
+finished on the SAME accumulator by a v_mfma_f32_16x16x16_bf16 gave wrong sums
+in its edge kernels, and kept every chain on one form.  This test isolates the
+transition (tests/native/mfma_mix.hip): the mixed chain as hipcc schedules it
+(no wait states between the two forms; hipcc even writes the first MFMA's
+result over its own A operand registers), the same with 16 wait states forced
+between the forms, and the other order, each against a float64 reference of
+the same products (bf16 products are exact in fp32; sums of 48 of them per
+element, compared at 1e-6 of their scale).  All three are exact on gfx950
+(measured: 8e-8, 8e-8, 1e-7 of scale), so the hardware and hipcc's hazard
+handling of the form change are not the cause; the round-2 failure lay in that
+round's own operand construction for the unpaired K-tile (code that no longer
+exists: every bf16 chain of pfsgnn_mfma.hip is now on the 16x16x32 form by
+construction, LayerB3 / LayerB6).  The test pins that finding.
 """
 import ctypes
 import os
@@ -71,8 +77,6 @@ def test_mfma_form_mixing():
     scale = np.abs(ref).max()
     errs = {v: np.abs(run(A, B, A2, B2, v) - ref).max() / scale for v in (0, 1, 2)}
     print("MFMA form mixing: max |err| / scale per variant", errs)
-    # with the wait states in place the mixed chain is exact to fp32 rounding
-    assert errs[1] < 1e-6, errs
-    # the pinned finding: recorded per variant; the product
-    # kernels never mix forms, so this asserts nothing about them
-    pytest.mfma_form_errs = errs
+    # every variant -- as scheduled, with forced wait states, other order --
+    # is exact to fp32 rounding
+    assert all(e < 1e-6 for e in errs.values()), errs

@@ -44,7 +44,7 @@ def dims(G, NF, NC, F=10):
     return Dims(G, NF, NC, F), EDims(G, NF, NC, F)
 
 
-@pytest.fixture(params=["mfma", "mfma32", "valu", "bf16x3"])
+@pytest.fixture(params=["mfma", "mfma32", "valu", "bf16x3", "bf16x6"])
 def prec(request):
     import pfsgnn
     pfsgnn.set_edge_path(request.param)
@@ -61,7 +61,7 @@ def test_edge_ops(hb, prec, G, NF, NC, F):
     """Every per-edge kernel on every fp32-class path (fp32 VALU, MFMA, the
     bf16x3 contractions) against the float64 emulation, at every supported
     Fdim (the bf16 paths are built for Fdim 10)."""
-    if prec == "bf16x3" and F != 10:
+    if prec in ("bf16x3", "bf16x6") and F != 10:
         pytest.skip("bf16 edge paths are instantiated for Fdim 10")
     gen = torch.Generator().manual_seed(G * 1000 + NF * 10 + NC + F)
     # Inputs on a grid on which every FIRST-layer pre-activation is computed exactly

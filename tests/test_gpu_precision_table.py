@@ -11,6 +11,8 @@ oracle, for every edge path:
   bf16    single-bf16 MFMA contractions + bf16 edge state
   bf16x3  every per-edge contraction (forward, recompute, gradient chains)
           on bf16 MFMAs with split hi + lo operands, fp32 edge state
+  bf16x6  forward contractions + recompute on bf16 MFMAs with three-way
+          split operands (fp32-class products), gradient chains as mfma
 
 For each path and compared tensor it records max|ours - oracle64| / scale and /
 max|oracle32 - oracle64|; the worst over all tensors is the path's line.  The
@@ -57,7 +59,8 @@ def _tensors(m, out, loss):
 TABLE = {}
 
 
-@pytest.mark.parametrize("path", ["mfma32", "mfma", "valu", "bf16x3", "bf16y", "bf16m", "bf16"])
+@pytest.mark.parametrize("path", ["mfma32", "mfma", "valu", "bf16x6", "bf16x3", "bf16y", "bf16m",
+                                  "bf16"])
 def test_precision_line(oracle, path):
     import pfsgnn
     model, graph, seed, r64, r32 = oracle
