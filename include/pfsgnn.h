@@ -221,6 +221,45 @@ int pfsgnn_mlp_fwd(const pfsgnn_seg* segs, int nseg, int N, const float* W1, int
                    const float* gamma, const float* beta, float* rm, float* rv, float momentum,
                    float eps, float* Y, float* mu, float* var, void* ws, size_t ws_bytes,
                    void* stream);
+/* A linear map of a node table written where the table is produced:
+ * out[k][n] = sum_o W[k*ldw + col0 + o] * Y[o][n] + b[k] (b may be NULL), k < nk. */
+typedef struct {
+  const float* W;
+  int ldw;
+  int col0;
+  int nk;
+  const float* b;
+  float* out;
+} pfsgnn_linmap;
+/* pfsgnn_mlp_fwd with up to 2 such maps of the normalised output Y (BatchNorm
+ * required; nk <= 64) done in the normalising pass: SModel's x_s' feeds TModel's
+ * Rs = Wt1[:, :F] x_s' + bt1 (gnn.py:188) and the next block's EdgeModel
+ * Ps = W1[:, :F] x_s' (gnn.py:100), which then need no launch of their own. */
+int pfsgnn_mlp_fwd_epi(const pfsgnn_seg* segs, int nseg, int N, const float* W1, int ldw1,
+                       int H, const float* b1, const float* W2, int O, const float* b2, float* Z,
+                       float* Yp, const float* gamma, const float* beta, float* rm, float* rv,
+                       float momentum, float eps, float* Y, float* mu, float* var,
+                       const pfsgnn_linmap* epi, int nepi, void* ws, size_t ws_bytes, void* stream);
+/* The tail of a message-passing block (gnn.py:191-192 + 218-223) in two launches:
+ * TModel's node_mlp_2 over the G*NC classes (as pfsgnn_mlp_fwd: Z, Yp, W2 [F][H])
+ * and its training BatchNorm1d -> xt [F][G*NC], mu/var [F], running stats rm/rv;
+ * then one workgroup per graph applies the norm to its classes and runs the
+ * GlobalModel as pfsgnn_global_fwd on the new x_s (xs [F][G*NF]) and x_t:
+ * means [2F][G], gZ [gH][G], gV [F][G], unew [F][G] (RMSNorm with weight gw, eps
+ * reps, y1/r1/r2 saved; gw NULL: unew = gV); and, with We != NULL, the next
+ * block's per-class first-Linear parts from the new x_t and u:
+ * Pt = We[:, F:2F] xt + We[:, 3F:4F] unew[g] + be  ([4F][G*NC], EdgeModel, gnn.py:100)
+ * Qt = Ws[:, 0:F] xt + bs                          ([2F][G*NC], SModel, gnn.py:136).
+ * F <= 16; 3F, gH <= 192; ws >= pfsgnn_mlp_ws_bytes(G*NC). */
+int pfsgnn_target_global_fwd(
+    const pfsgnn_seg* segs, int nseg, int G, int NC, const float* W1, int ldw1, int H,
+    const float* b1, const float* W2, int F, const float* b2, float* Z, float* Yp,
+    const float* gamma, const float* beta, float* rm, float* rv, float momentum, float eps,
+    float* xt, float* mu, float* var, const float* xs, int NF, const float* u, const float* gW1,
+    int gH, const float* gb1, const float* gW2, const float* gb2, const float* gw, float reps,
+    float* means, float* gZ, float* gV, float* unew, float* y1, float* r1, float* r2,
+    const float* We, const float* be, const float* Ws, const float* bs, float* Pt, float* Qt,
+    void* ws, size_t ws_bytes, void* stream);
 /* One row block of an input-gradient output: rows `rows` of dX go to x
  * ([rows][N], overwritten, or accumulated when add != 0); x == NULL drops them. */
 typedef struct {

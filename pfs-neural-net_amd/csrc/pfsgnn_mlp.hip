@@ -274,21 +274,18 @@ __global__ __launch_bounds__(256, (M <= 3 ? 2 : 1)) void k_mlp_fwd(InSegs S, int
   }
 }
 
-// BatchNorm1d training forward from the MLP's per-block partials: every block
-// merges them in the same fixed order (double), block 0 writes mu / var and
-// updates the running statistics (unbiased variance), all apply the norm.
-__global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__ part, int nb,
-                                                       int O, int N, const float* __restrict__ Yp,
-                                                       const float* __restrict__ gamma,
-                                                       const float* __restrict__ beta, float eps,
-                                                       float* __restrict__ rm,
-                                                       float* __restrict__ rv, float momentum,
-                                                       float* __restrict__ Y,
-                                                       float* __restrict__ mu,
-                                                       float* __restrict__ var) {
+// BatchNorm1d training statistics from the MLP's per-block partials, in every
+// block of the calling kernel: the partials merged in the same fixed order
+// (double); `write` (one block) stores mu / var and updates the running
+// statistics (unbiased variance).  -> cf[0][o] = mean, cf[1][o] = 1/sqrt(var +
+// eps), cf[2] = gamma, cf[3] = beta (256 threads; nb <= 512).
+__device__ void bn_stats_part(const float* __restrict__ part, int nb, int O, int N,
+                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                              float eps, float* __restrict__ rm, float* __restrict__ rv,
+                              float momentum, float* __restrict__ mu, float* __restrict__ var,
+                              bool write, float (*cf)[16]) {
   __shared__ double acc[16][16][2];
   __shared__ double mean_s[16];
-  __shared__ float cf[4][16];
   const int t = threadIdx.x, c = t & 15, u = t >> 4;
   constexpr int PB = 32;  // partials per thread: nb <= 512 (the MLP grid)
   float pc[PB], pm[PB], pq[PB];
@@ -333,7 +330,7 @@ __global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__
     cf[1][t] = 1.0f / sqrtf(vf + eps);
     cf[2][t] = live ? gamma[t] : 0.f;
     cf[3][t] = live ? beta[t] : 0.f;
-    if (blockIdx.x == 0 && live) {
+    if (write && live) {
       mu[t] = muf;
       var[t] = vf;
       if (rm) {
@@ -344,11 +341,227 @@ __global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__
     }
   }
   __syncthreads();
-  for (int o = 0; o < O; ++o) {
-    const float m = cf[0][o], a = cf[1][o] * cf[2][o], b = cf[3][o];
-    const float* yp = Yp + (size_t)o * N;
-    float* y = Y + (size_t)o * N;
-    for (int n = blockIdx.x * 256 + t; n < N; n += gridDim.x * 256) y[n] = (yp[n] - m) * a + b;
+}
+
+// Linear maps of the normalised output, done where it is written (the node
+// parts the next consumers need: TModel's Rs = Wt1[:, :F] x_s' + bt1 and the
+// next block's EdgeModel Ps = W1[:, :F] x_s', gnn.py:100/188):
+// out_e[k][n] = sum_o W_e[k][col0_e + o] Y[o][n] + b_e[k]
+constexpr int EPI_MAXK = 64;
+struct BnEpi {
+  const float* W[2];
+  int ldw[2], col0[2], nk[2];
+  const float* b[2];
+  float* out[2];
+};
+
+// BatchNorm1d training forward from the MLP's per-block partials: every block
+// merges them (bn_stats_part), block 0 writes mu / var and the running
+// statistics, all apply the norm (+ the epilogues, thread per node).
+__global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__ part, int nb,
+                                                       int O, int N, const float* __restrict__ Yp,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float eps,
+                                                       float* __restrict__ rm,
+                                                       float* __restrict__ rv, float momentum,
+                                                       float* __restrict__ Y,
+                                                       float* __restrict__ mu,
+                                                       float* __restrict__ var, BnEpi E) {
+  __shared__ float cf[4][16];
+  __shared__ float ew[2][EPI_MAXK * 16], eb[2][EPI_MAXK];
+  const int t = threadIdx.x;
+  const bool epi = E.W[0] || E.W[1];
+  if (epi) {  // weight blocks staged before the statistics (latency overlapped)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      if (!E.W[e]) continue;
+      for (int i = t; i < E.nk[e] * 16; i += 256) {
+        const int k = i >> 4, o = i & 15;
+        ew[e][i] = o < O ? E.W[e][(size_t)k * E.ldw[e] + E.col0[e] + o] : 0.f;
+      }
+      for (int k = t; k < E.nk[e]; k += 256) eb[e][k] = E.b[e] ? E.b[e][k] : 0.f;
+    }
+  }
+  bn_stats_part(part, nb, O, N, gamma, beta, eps, rm, rv, momentum, mu, var, blockIdx.x == 0, cf);
+  if (!epi) {
+    for (int o = 0; o < O; ++o) {
+      const float m = cf[0][o], a = cf[1][o] * cf[2][o], b = cf[3][o];
+      const float* yp = Yp + (size_t)o * N;
+      float* y = Y + (size_t)o * N;
+      for (int n = blockIdx.x * 256 + t; n < N; n += gridDim.x * 256) y[n] = (yp[n] - m) * a + b;
+    }
+    return;
+  }
+  for (int n = blockIdx.x * 256 + t; n < N; n += gridDim.x * 256) {
+    float y[16];
+#pragma unroll
+    for (int o = 0; o < 16; ++o) {
+      y[o] = 0.f;
+      if (o < O) {
+        y[o] = (Yp[(size_t)o * N + n] - cf[0][o]) * (cf[1][o] * cf[2][o]) + cf[3][o];
+        Y[(size_t)o * N + n] = y[o];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      if (!E.W[e]) continue;
+      for (int k = 0; k < E.nk[e]; ++k) {
+        float a = eb[e][k];
+#pragma unroll
+        for (int o = 0; o < 16; ++o) a = fmaf(ew[e][k * 16 + o], y[o], a);
+        E.out[e][(size_t)k * N + n] = a;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- class side + GlobalModel
+// The block's tail after TModel's node_mlp_2 (k_mlp_fwd: Yp and BatchNorm
+// partials), one workgroup per graph: TModel's BatchNorm1d (gnn.py:192; the
+// statistics merged in every workgroup in the same order, workgroup 0 writes
+// mu / var / running stats) applied to the graph's classes; GlobalModel
+// (gnn.py:218-223: the x_s / x_t means, MLP(3F -> H -> F), RMSNorm twice, the
+// arithmetic of k_global_fwd); then the next block's class parts from the new
+// x_t and u: Pt = We[:, F:2F] x_t + We[:, 3F:4F] u[g] + be (EdgeModel,
+// gnn.py:100) and Qt = Ws[:, :F] x_t + bs (SModel, gnn.py:136).  One launch for
+// what was bn_apply + graph_mean2 + global_fwd + the next block's class GEMMs.
+constexpr int CG_MAXF = 16, CG_MAXH = 192;
+struct ClassGlobalArgs {
+  const float* part;  // TModel node_mlp_2's BatchNorm partials (k_mlp_fwd), nb of them
+  int nb, F, NC, G, NF;
+  const float* Yp;    // [F][G*NC] pre-norm node_mlp_2 output
+  const float *gamma, *beta;
+  float eps, momentum;
+  float *rm, *rv, *xt, *mu, *var;    // xt [F][G*NC]: the new x_t
+  const float* xs;    // [F][G*NF] the new x_s
+  const float* u;     // [F][G]
+  const float *W1, *b1, *W2, *b2, *w;  // GlobalModel MLP (W1 [H][3F]) and RMSNorm weight (or null)
+  int H;
+  float reps;
+  float *means, *Z, *V, *Y, *y1, *r1, *r2;  // as k_global_fwd
+  const float *We, *be, *Ws, *bs;           // next block (We null: none)
+  float *Pt, *Qt;                           // [4F][G*NC], [2F][G*NC]
+};
+
+__global__ __launch_bounds__(256) void k_class_global_fwd(ClassGlobalArgs A) {
+  __shared__ float cf[4][16];
+  __shared__ float h[CG_MAXH], z[CG_MAXH], vv[CG_MAXH];
+  __shared__ float scratch[4 * 2 * CG_MAXF];
+  __shared__ float wt[4 * CG_MAXF * CG_MAXF], ws2[2 * CG_MAXF * CG_MAXF], cu[4 * CG_MAXF],
+      bq[2 * CG_MAXF];
+  const int g = blockIdx.x, t = threadIdx.x, F = A.F, NC = A.NC;
+  const long long NT = (long long)A.G * NC, NS = (long long)A.G * A.NF;
+  if (A.We) {  // next block's weight blocks staged early
+    for (int i = t; i < 4 * F * F; i += 256) {
+      const int k = i / F, o = i - k * F;
+      wt[i] = A.We[(size_t)k * 4 * F + F + o];
+    }
+    for (int i = t; i < 2 * F * F; i += 256) {
+      const int k = i / F, o = i - k * F;
+      ws2[i] = A.Ws[(size_t)k * 2 * F + o];
+    }
+  }
+  bn_stats_part(A.part, A.nb, F, (int)NT, A.gamma, A.beta, A.eps, A.rm, A.rv, A.momentum, A.mu,
+                A.var, g == 0, cf);
+  // the graph's classes: x_t = BN(Yp), and the per-channel sums for its mean
+  float sm[2 * CG_MAXF];
+#pragma unroll
+  for (int o = 0; o < 2 * CG_MAXF; ++o) sm[o] = 0.f;
+  for (int c = t; c < NC; c += 256) {
+    const long long n = (long long)g * NC + c;
+#pragma unroll
+    for (int o = 0; o < CG_MAXF; ++o) {
+      if (o < F) {
+        const float v = (A.Yp[(size_t)o * NT + n] - cf[0][o]) * (cf[1][o] * cf[2][o]) + cf[3][o];
+        A.xt[(size_t)o * NT + n] = v;
+        sm[CG_MAXF + o] += v;
+      }
+    }
+  }
+  for (int f = t; f < A.NF; f += 256) {
+    const long long n = (long long)g * A.NF + f;
+#pragma unroll
+    for (int o = 0; o < CG_MAXF; ++o)
+      if (o < F) sm[o] += A.xs[(size_t)o * NS + n];
+  }
+  block_sum<2 * CG_MAXF>(sm, scratch);
+  const int K = 3 * F;
+  if (t < F) {
+    h[t] = A.u[(size_t)t * A.G + g];
+    const float ms = sm[t] / (float)A.NF, mt = sm[CG_MAXF + t] / (float)NC;
+    h[F + t] = ms;
+    h[2 * F + t] = mt;
+    A.means[(size_t)t * A.G + g] = ms;
+    A.means[(size_t)(F + t) * A.G + g] = mt;
+  }
+  __syncthreads();
+  for (int j = t; j < A.H; j += 256) {
+    float acc = A.b1[j];
+    for (int k = 0; k < K; ++k) acc = fmaf(A.W1[(size_t)j * K + k], h[k], acc);
+    z[j] = acc;
+    A.Z[(size_t)j * A.G + g] = acc;
+  }
+  __syncthreads();
+  for (int o = t; o < F; o += 256) {
+    float acc = A.b2[o];
+    for (int j = 0; j < A.H; ++j) acc = fmaf(A.W2[(size_t)o * A.H + j], lrelu(z[j]), acc);
+    vv[o] = acc;
+    A.V[(size_t)o * A.G + g] = acc;
+  }
+  __syncthreads();
+  if (t == 0) {
+    if (!A.w) {
+      for (int c = 0; c < F; ++c) h[c] = vv[c];
+    } else {
+      float s = 0.f;
+      for (int c = 0; c < F; ++c) s += vv[c] * vv[c];
+      const float a = rsqrtf(s / F + A.reps);
+      float s2 = 0.f;
+      for (int c = 0; c < F; ++c) {
+        const float q = vv[c] * a * A.w[c];
+        z[c] = q;
+        A.y1[(size_t)c * A.G + g] = q;
+        s2 += q * q;
+      }
+      const float b = rsqrtf(s2 / F + A.reps);
+      for (int c = 0; c < F; ++c) h[c] = z[c] * b * A.w[c];
+      A.r1[g] = a;
+      A.r2[g] = b;
+    }
+  }
+  __syncthreads();
+  if (t < F) A.Y[(size_t)t * A.G + g] = h[t];   // u_new
+  if (!A.We) return;
+  // next block: per-graph constant of Pt (u term + bias), then per class
+  if (t < 4 * F) {
+    float acc = A.be[t];
+    for (int o = 0; o < F; ++o) acc = fmaf(A.We[(size_t)t * 4 * F + 3 * F + o], h[o], acc);
+    cu[t] = acc;
+  } else if (t >= 128 && t - 128 < 2 * F) {
+    bq[t - 128] = A.bs[t - 128];
+  }
+  __syncthreads();
+  for (int c = t; c < NC; c += 256) {
+    const long long n = (long long)g * NC + c;
+    float x[CG_MAXF];
+#pragma unroll
+    for (int o = 0; o < CG_MAXF; ++o)
+      x[o] = o < F ? (A.Yp[(size_t)o * NT + n] - cf[0][o]) * (cf[1][o] * cf[2][o]) + cf[3][o]
+                   : 0.f;
+    for (int k = 0; k < 4 * F; ++k) {
+      float acc = cu[k];
+#pragma unroll
+      for (int o = 0; o < CG_MAXF; ++o)
+        if (o < F) acc = fmaf(wt[k * F + o], x[o], acc);
+      A.Pt[(size_t)k * NT + n] = acc;
+    }
+    for (int k = 0; k < 2 * F; ++k) {
+      float acc = bq[k];
+#pragma unroll
+      for (int o = 0; o < CG_MAXF; ++o)
+        if (o < F) acc = fmaf(ws2[k * F + o], x[o], acc);
+      A.Qt[(size_t)k * NT + n] = acc;
+    }
   }
 }
 
@@ -657,28 +870,17 @@ extern "C" size_t pfsgnn_mlp_ws_bytes(int N) {
          align256((size_t)256 * SUM_LEN * sizeof(float)) + (N > 0 ? 0 : 0);
 }
 
-extern "C" int pfsgnn_mlp_fwd(const pfsgnn_seg* segs, int nseg, int N, const float* W1, int ldw1,
-                              int H, const float* b1, const float* W2, int O, const float* b2,
-                              float* Z, float* Yp, const float* gamma, const float* beta,
-                              float* rm, float* rv, float momentum, float eps, float* Y,
-                              float* mu, float* var, void* ws, size_t ws_bytes, void* stream) {
-  const char* where = "pfsgnn_mlp_fwd";
-  PF_REQUIRE(W1 && b1 && W2 && b2 && Yp && N > 0 && H > 0 && O > 0 && O <= 16, where,
-             "bad arguments");
-  InSegs S;
-  const int K = make_in(segs, nseg, N, S);
-  PF_REQUIRE(K > 0, where, "bad segment list (blocks must cover weight columns 0..K in order)");
+namespace {
+// the MLP launch of pfsgnn_mlp_fwd (BatchNorm partials into `part` when given)
+int mlp_fwd_launch(const InSegs& S, int K, int N, const float* W1, int ldw1, int H,
+                   const float* b1, const float* W2, int O, const float* b2, float* Z, float* Yp,
+                   float* part, int* grid_out, hipStream_t st) {
   const int m = tiles_for(K, H);
-  PF_REQUIRE(m > 0, where, "K, H > 112 not supported");
-  const bool bn = gamma != nullptr;
-  PF_REQUIRE(!bn || (beta && Y && mu && var && N > 1), where,
-             "BatchNorm needs beta, Y, mu, var and more than one node");
-  PF_REQUIRE(ws && ws_bytes >= pfsgnn_mlp_ws_bytes(N), where, "workspace too small");
-  hipStream_t st = as_stream(stream);
+  if (m <= 0) return -2;
   const size_t lds = fwd_lds(m);
   const int grid = grid_for(N, m, lds);
-  float* part = bn ? reinterpret_cast<float*>(ws) : nullptr;
-  const int rc = with_tiles(m, [&](auto mc) {
+  *grid_out = grid;
+  return with_tiles(m, [&](auto mc) {
     constexpr int MM = decltype(mc)::value;
     static size_t attr = 0;  // dynamic LDS above the 64 KB default must be opted into
     if (lds > 65536 && attr < lds) {
@@ -691,13 +893,100 @@ extern "C" int pfsgnn_mlp_fwd(const pfsgnn_seg* segs, int nseg, int N, const flo
                        W2, O, b2, Z, Yp, part);
     return 0;
   });
+}
+}  // namespace
+
+extern "C" int pfsgnn_mlp_fwd(const pfsgnn_seg* segs, int nseg, int N, const float* W1, int ldw1,
+                              int H, const float* b1, const float* W2, int O, const float* b2,
+                              float* Z, float* Yp, const float* gamma, const float* beta,
+                              float* rm, float* rv, float momentum, float eps, float* Y,
+                              float* mu, float* var, void* ws, size_t ws_bytes, void* stream) {
+  return pfsgnn_mlp_fwd_epi(segs, nseg, N, W1, ldw1, H, b1, W2, O, b2, Z, Yp, gamma, beta, rm, rv,
+                            momentum, eps, Y, mu, var, nullptr, 0, ws, ws_bytes, stream);
+}
+
+extern "C" int pfsgnn_mlp_fwd_epi(const pfsgnn_seg* segs, int nseg, int N, const float* W1,
+                                  int ldw1, int H, const float* b1, const float* W2, int O,
+                                  const float* b2, float* Z, float* Yp, const float* gamma,
+                                  const float* beta, float* rm, float* rv, float momentum,
+                                  float eps, float* Y, float* mu, float* var,
+                                  const pfsgnn_linmap* epi, int nepi, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  const char* where = "pfsgnn_mlp_fwd";
+  PF_REQUIRE(W1 && b1 && W2 && b2 && Yp && N > 0 && H > 0 && O > 0 && O <= 16, where,
+             "bad arguments");
+  InSegs S;
+  const int K = make_in(segs, nseg, N, S);
+  PF_REQUIRE(K > 0, where, "bad segment list (blocks must cover weight columns 0..K in order)");
+  PF_REQUIRE(tiles_for(K, H) > 0, where, "K, H > 112 not supported");
+  const bool bn = gamma != nullptr;
+  PF_REQUIRE(!bn || (beta && Y && mu && var && N > 1), where,
+             "BatchNorm needs beta, Y, mu, var and more than one node");
+  PF_REQUIRE(ws && ws_bytes >= pfsgnn_mlp_ws_bytes(N), where, "workspace too small");
+  PF_REQUIRE(nepi >= 0 && nepi <= 2 && (nepi == 0 || (epi && bn)), where,
+             "epilogues (at most 2) need the BatchNorm");
+  BnEpi E{};
+  for (int e = 0; e < nepi; ++e) {
+    PF_REQUIRE(epi[e].W && epi[e].out && epi[e].nk > 0 && epi[e].nk <= EPI_MAXK &&
+                   epi[e].col0 >= 0 && epi[e].col0 + O <= epi[e].ldw,
+               where, "bad epilogue (nk <= 64, columns col0..col0+O inside ldw)");
+    E.W[e] = epi[e].W;
+    E.ldw[e] = epi[e].ldw;
+    E.col0[e] = epi[e].col0;
+    E.nk[e] = epi[e].nk;
+    E.b[e] = epi[e].b;
+    E.out[e] = epi[e].out;
+  }
+  hipStream_t st = as_stream(stream);
+  float* part = bn ? reinterpret_cast<float*>(ws) : nullptr;
+  int grid = 0;
+  const int rc = mlp_fwd_launch(S, K, N, W1, ldw1, H, b1, W2, O, b2, Z, Yp, part, &grid, st);
   PF_REQUIRE(rc != -3, where, "hipFuncSetAttribute (dynamic LDS) failed");
   PF_REQUIRE(rc == 0, where, "no kernel for this width");
   if (bn) {
     const int ag = std::max(1, std::min(256, (int)(((size_t)O * N + 1023) / 1024)));
     hipLaunchKernelGGL(k_bn_apply_part, dim3(ag), dim3(256), 0, st, part, grid, O, N, Yp, gamma,
-                       beta, eps, rm, rv, momentum, Y, mu, var);
+                       beta, eps, rm, rv, momentum, Y, mu, var, E);
   }
+  return pf::check_launch(where);
+}
+
+extern "C" int pfsgnn_target_global_fwd(
+    const pfsgnn_seg* segs, int nseg, int G, int NC, const float* W1, int ldw1, int H,
+    const float* b1, const float* W2, int F, const float* b2, float* Z, float* Yp,
+    const float* gamma, const float* beta, float* rm, float* rv, float momentum, float eps,
+    float* xt, float* mu, float* var, const float* xs, int NF, const float* u, const float* gW1,
+    int gH, const float* gb1, const float* gW2, const float* gb2, const float* gw, float reps,
+    float* means, float* gZ, float* gV, float* unew, float* y1, float* r1, float* r2,
+    const float* We, const float* be, const float* Ws, const float* bs, float* Pt, float* Qt,
+    void* ws, size_t ws_bytes, void* stream) {
+  const char* where = "pfsgnn_target_global_fwd";
+  PF_REQUIRE(G > 0 && NC > 0 && NF > 0 && F > 0 && F <= CG_MAXF && W1 && b1 && W2 && b2 && Z &&
+                 Yp && gamma && beta && xt && mu && var && xs && u && gW1 && gb1 && gW2 && gb2 &&
+                 means && gZ && gV && unew && gH > 0 && gH <= CG_MAXH && 3 * F <= CG_MAXH,
+             where, "bad arguments (F <= 16, GlobalModel widths <= 192)");
+  PF_REQUIRE(!gw || (y1 && r1 && r2), where, "RMSNorm needs y1, r1, r2");
+  PF_REQUIRE(!We || (be && Ws && bs && Pt && Qt), where, "next-block parts need be, Ws, bs, Pt, Qt");
+  const int N = G * NC;
+  PF_REQUIRE(N > 1, where, "BatchNorm needs more than one node");
+  InSegs S;
+  const int K = make_in(segs, nseg, N, S);
+  PF_REQUIRE(K > 0, where, "bad segment list (blocks must cover weight columns 0..K in order)");
+  PF_REQUIRE(ws && ws_bytes >= pfsgnn_mlp_ws_bytes(N), where, "workspace too small");
+  hipStream_t st = as_stream(stream);
+  float* part = reinterpret_cast<float*>(ws);
+  int grid = 0;
+  const int rc = mlp_fwd_launch(S, K, N, W1, ldw1, H, b1, W2, F, b2, Z, Yp, part, &grid, st);
+  PF_REQUIRE(rc != -3, where, "hipFuncSetAttribute (dynamic LDS) failed");
+  PF_REQUIRE(rc == 0, where, "no kernel for this width (K, H <= 112)");
+  ClassGlobalArgs A{};
+  A.part = part; A.nb = grid; A.F = F; A.NC = NC; A.G = G; A.NF = NF;
+  A.Yp = Yp; A.gamma = gamma; A.beta = beta; A.eps = eps; A.momentum = momentum;
+  A.rm = rm; A.rv = rv; A.xt = xt; A.mu = mu; A.var = var;
+  A.xs = xs; A.u = u; A.W1 = gW1; A.b1 = gb1; A.W2 = gW2; A.b2 = gb2; A.w = gw; A.H = gH;
+  A.reps = reps; A.means = means; A.Z = gZ; A.V = gV; A.Y = unew; A.y1 = y1; A.r1 = r1; A.r2 = r2;
+  A.We = We; A.be = be; A.Ws = Ws; A.bs = bs; A.Pt = Pt; A.Qt = Qt;
+  hipLaunchKernelGGL(k_class_global_fwd, dim3(G), dim3(256), 0, st, A);
   return pf::check_launch(where);
 }
 

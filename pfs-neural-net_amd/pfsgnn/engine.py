@@ -109,24 +109,45 @@ class Engine:
         self.training = True
 
     # ================================================================= MLP
-    def mlp_fwd(self, P, pre, X, bnkey=None, BN=None):
+    def _bn_args(self, P, BN, bnkey):
+        return (P[bnkey + "weight"], P[bnkey + "bias"], BN.get(bnkey + "running_mean"),
+                BN.get(bnkey + "running_var"), self.bn_momentum, self.bn_eps)
+
+    def _fused_tail_ok(self, P, d, pre_s, pre_t, pre_g):
+        """The fused block tail (mlp_fwd_epi on SModel's node_mlp_2,
+        target_global_fwd for TModel's node_mlp_2 + the GlobalModel): training
+        with normalisation, on the HIP ops' shapes."""
+        be, F = self.be, self.F
+        if not (self.training and self.normed and hasattr(be, "target_global_fwd") and F <= 16):
+            return False
+        def mlp_ok(pre):
+            W1, W2 = P[pre + "0.weight"], P[pre + "2.weight"]
+            return max(W1.shape) <= 112 and W2.shape[0] <= 16
+        return (mlp_ok(pre_s + "node_mlp_2.") and mlp_ok(pre_t + "node_mlp_2.")
+                and max(P[pre_g + "0.weight"].shape) <= 192)
+
+    def mlp_fwd(self, P, pre, X, bnkey=None, BN=None, epi=None):
         """MLP (gnn.py:65): Linear -> LeakyReLU(0.1) -> Linear on [K, N], as ONE
         fused op, optionally followed by the module's BatchNorm1d (``bnkey``,
         gnn.py:154/192).  X is a tensor or, for the concatenated inputs of
         gnn.py:153/191/220, a list of row blocks ``(tensor, weight column,
         per_graph)`` read in place (a per_graph block is [rows, G], broadcast
-        over each graph's nodes).  Returns (Y, saved)."""
+        over each graph's nodes).  Returns (Y, saved); with ``epi`` (training
+        BatchNorm only: [(W, col0, nk, b)]) -> (Y, saved, [W[:, col0:col0+O] Y + b])."""
         be = self.be
         W1, b1, W2, b2 = P[pre + "0.weight"], P[pre + "0.bias"], P[pre + "2.weight"], P[pre + "2.bias"]
         segs = X if isinstance(X, list) else [(X, 0, False)]
         N = _seg_n(segs)
         norm = bnkey is not None and self.normed
+        if epi:
+            assert norm and self.training and _fused_mlp_ok(W1, W2, segs)
+            Y, Z, Yp, mu, var, outs = be.mlp_fwd_epi(segs, N, W1, b1, W2, b2,
+                                                     self._bn_args(P, BN, bnkey), epi)
+            return Y, (segs, Z, (Yp, mu, var, bnkey)), outs
         if not _fused_mlp_ok(W1, W2, segs):
             return self._mlp_fwd_ops(P, BN, pre, segs, N, bnkey if norm else None)
         if norm and self.training:
-            bn = (P[bnkey + "weight"], P[bnkey + "bias"], BN.get(bnkey + "running_mean"),
-                  BN.get(bnkey + "running_var"), self.bn_momentum, self.bn_eps)
-            Y, Z, Yp, mu, var = be.mlp_fwd(segs, N, W1, b1, W2, b2, bn=bn)
+            Y, Z, Yp, mu, var = be.mlp_fwd(segs, N, W1, b1, W2, b2, bn=self._bn_args(P, BN, bnkey))
             return Y, (segs, Z, (Yp, mu, var, bnkey))
         Y, Z, _, _, _ = be.mlp_fwd(segs, N, W1, b1, W2, b2, save_z=self.training)
         if norm:
@@ -292,7 +313,9 @@ class Engine:
         return g_xe
 
     # --- SModel (gnn.py:123-154)
-    def source_fwd(self, P, BN, d, pre, xs, xt, xe3, u, Qt=None):
+    def source_fwd(self, P, BN, d, pre, xs, xt, xe3, u, Qt=None, epi=None):
+        """``epi`` (fused block tail): {name: (W, col0, nk, b)} linear maps of
+        the new x_s done in its normalising pass, returned under their names."""
         be, F = self.be, self.F
         Ws1, bs1 = P[pre + "node_mlp_1.0.weight"], P[pre + "node_mlp_1.0.bias"]
         Ws2, bs2 = P[pre + "node_mlp_1.2.weight"], P[pre + "node_mlp_1.2.bias"]
@@ -303,8 +326,16 @@ class Engine:
         # node_mlp_2 input [x, mean, std, skew, kurt, u[batch]] (gnn.py:153), in place,
         # + its BatchNorm1d (gnn.py:154) in the same fused op
         hS = [(xs, 0, False), (hmom, F, False), (u, 9 * F, True)]
-        xs_new, sS = self.mlp_fwd(P, pre + "node_mlp_2.", hS, pre + "norm.", BN)
-        return dict(xs=xs, xt=xt, xe3=xe3, u=u, Qt=Qt, mom=mom, sS=sS, xs_new=xs_new)
+        st = dict(xs=xs, xt=xt, xe3=xe3, u=u, Qt=Qt, mom=mom)
+        if epi:
+            names = list(epi)
+            xs_new, sS, outs = self.mlp_fwd(P, pre + "node_mlp_2.", hS, pre + "norm.", BN,
+                                            epi=[epi[k] for k in names])
+            st.update(zip(names, outs))
+        else:
+            xs_new, sS = self.mlp_fwd(P, pre + "node_mlp_2.", hS, pre + "norm.", BN)
+        st.update(sS=sS, xs_new=xs_new)
+        return st
 
     def source_node_bwd(self, P, Gr, d, pre, st, g_xs_new, g_xs, g_u):
         """Node half of the SModel backward; returns the per-fiber moment coefficients."""
@@ -344,11 +375,16 @@ class Engine:
         return g_tot, out[2], out[3]
 
     # --- TModel (gnn.py:175-192)
-    def target_fwd(self, P, BN, d, pre, xs, xt, xe3, u):
+    def target_fwd(self, P, BN, d, pre, xs, xt, xe3, u, Rs=None, glob=None):
+        """``glob`` (fused block tail) = (GlobalModel prefix, next block's prefix
+        or None): TModel's node_mlp_2 + BatchNorm and the GlobalModel run as one
+        op (target_global_fwd); the GlobalModel's state comes back as ["su"] and
+        the next block's class parts (Pt, Qt) as ["parts_t"]."""
         be, F = self.be, self.F
         Wt1, bt1 = P[pre + "node_mlp_1.0.weight"], P[pre + "node_mlp_1.0.bias"]
         Wt2, bt2 = P[pre + "node_mlp_1.2.weight"], P[pre + "node_mlp_1.2.bias"]
-        Rs = be.lin(Wt1, 0, F, xs, b=bt1)
+        if Rs is None:
+            Rs = be.lin(Wt1, 0, F, xs, b=bt1)
         # the LeakyReLU mask of the per-edge layer, kept for the backward (MFMA
         # path; None where the backward recomputes it)
         tmask = be.tmask(d) if self.training and hasattr(be, "tmask") else None
@@ -364,9 +400,29 @@ class Engine:
             be.lin(bt2.view(-1, 1), 0, 1, d.sp.deg_t, out=agg, add=True)
         # node_mlp_2 input [x, agg, u[batch]] (gnn.py:191), in place, + BatchNorm1d
         hT = [(xt, 0, False), (agg, F, False), (u, 3 * F, True)]
-        xt_new, sT = self.mlp_fwd(P, pre + "node_mlp_2.", hT, pre + "norm.", BN)
-        return dict(xs=xs, xt=xt, xe3=xe3, u=u, Rs=Rs, hsum=hsum, sT=sT, xt_new=xt_new,
-                    tmask=tmask)
+        st = dict(xs=xs, xt=xt, xe3=xe3, u=u, Rs=Rs, hsum=hsum, tmask=tmask)
+        if glob is None:
+            xt_new, sT = self.mlp_fwd(P, pre + "node_mlp_2.", hT, pre + "norm.", BN)
+            st.update(sT=sT, xt_new=xt_new)
+            return st
+        pg, pnext = glob
+        m2 = pre + "node_mlp_2."
+        w = P[pg + "norm.weight"]
+        nxt = None
+        if pnext is not None:
+            pe, ps = pnext + "edge_model.", pnext + "s_model."
+            nxt = (P[pe + "0.weight"], P[pe + "0.bias"], P[ps + "node_mlp_1.0.weight"],
+                   P[ps + "node_mlp_1.0.bias"])
+        r = be.target_global_fwd(hT, d.G, d.NC, P[m2 + "0.weight"], P[m2 + "0.bias"],
+                                 P[m2 + "2.weight"], P[m2 + "2.bias"],
+                                 self._bn_args(P, BN, pre + "norm."), xs, d.NF, u,
+                                 P[pg + "0.weight"], P[pg + "0.bias"], P[pg + "2.weight"],
+                                 P[pg + "2.bias"], w, self._rms_eps(u), nxt)
+        st.update(sT=(hT, r["Z"], (r["Yp"], r["mu"], r["var"], pre + "norm.")), xt_new=r["xt"])
+        st["su"] = dict(sU=([(u, 0, False), (r["means"], F, False)], r["gZ"], None), v=r["gV"],
+                        rms=r["rms"], u_new=r["u"], fused=True)
+        st["parts_t"] = (r["Pt"], r["Qt"])
+        return st
 
     def target_node_bwd(self, P, Gr, d, pre, st, g_xt_new, g_xt, g_u):
         be, F, G = self.be, self.F, d.G
@@ -451,16 +507,38 @@ class Engine:
         ctx = {"d": d, "enc": (s_enc, t_enc), "blocks": [], "training": training}
         xe3 = (xe_in, None, None)
         u = u_in
+        parts = None
         for b in range(self.B):
             p = f"mpb.{b}."
-            parts = self.node_parts(P, d, p + "edge_model.", p + "s_model.", xs, xt, u)
+            pn = f"mpb.{b + 1}." if b + 1 < self.B else None
+            if parts is None:
+                parts = self.node_parts(P, d, p + "edge_model.", p + "s_model.", xs, xt, u)
             se = self.edge_fwd(P, BN, d, p + "edge_model.", xs, xt, xe3, u,
                                parts=None if parts is None else parts[:2])
             xe3n = (se["y"], se["sc"], se["sh"])
+            # fused block tail: x_s' is mapped to TModel's Rs (and the next block's
+            # EdgeModel Ps) where it is normalised; TModel's node MLP, the
+            # GlobalModel and the next block's class parts run as one op
+            fused = self._fused_tail_ok(P, d, p + "s_model.", p + "t_model.", p + "global_model.")
+            epi = None
+            if fused:
+                F = self.F
+                pt1 = p + "t_model.node_mlp_1.0."
+                epi = {"Rs": (P[pt1 + "weight"], 0, 2 * F, P[pt1 + "bias"])}
+                if pn is not None:
+                    epi["Ps_next"] = (P[pn + "edge_model.0.weight"], 0, 4 * F, None)
             ss = self.source_fwd(P, BN, d, p + "s_model.", xs, xt, xe3n, u,
-                                 Qt=None if parts is None else parts[2])
-            stt = self.target_fwd(P, BN, d, p + "t_model.", ss["xs_new"], xt, xe3n, u)
-            su = self.global_fwd(P, d, p + "global_model.", ss["xs_new"], stt["xt_new"], u)
+                                 Qt=None if parts is None else parts[2], epi=epi)
+            stt = self.target_fwd(P, BN, d, p + "t_model.", ss["xs_new"], xt, xe3n, u,
+                                  Rs=ss.get("Rs"),
+                                  glob=(p + "global_model.", pn) if fused else None)
+            if fused:
+                su = stt.pop("su")
+                pt = stt.pop("parts_t")
+                parts = (ss["Ps_next"],) + tuple(pt) if pn is not None else None
+            else:
+                su = self.global_fwd(P, d, p + "global_model.", ss["xs_new"], stt["xt_new"], u)
+                parts = None
             ctx["blocks"].append((se, ss, stt, su))
             xs, xt, xe3, u = ss["xs_new"], stt["xt_new"], xe3n, su["u_new"]
         ctx["out"] = (xs, xt, xe3, u)

@@ -87,6 +87,15 @@ class GemmJob(ctypes.Structure):
 
 GMJP = ctypes.POINTER(GemmJob)
 
+
+class LinMap(ctypes.Structure):
+    """pfsgnn_linmap (include/pfsgnn.h): out = W[:, col0:col0+O] . Y + b."""
+    _fields_ = [("W", ctypes.c_void_p), ("ldw", ctypes.c_int), ("col0", ctypes.c_int),
+                ("nk", ctypes.c_int), ("b", ctypes.c_void_p), ("out", ctypes.c_void_p)]
+
+
+LINMP = ctypes.POINTER(LinMap)
+
 _SIGS = {
     "pfsgnn_version": ([], ctypes.c_char_p),
     "pfsgnn_last_error": ([], ctypes.c_char_p),
@@ -119,6 +128,11 @@ _SIGS = {
     "pfsgnn_mlp_ws_bytes": ([I], SZ),
     "pfsgnn_mlp_fwd": ([SEGP, I, I, P, I, I, P, P, I, P, P, P, P, P, P, P, FL, FL, P, P, P, P,
                         SZ, P], I),
+    "pfsgnn_mlp_fwd_epi": ([SEGP, I, I, P, I, I, P, P, I, P, P, P, P, P, P, P, FL, FL, P, P, P,
+                            LINMP, I, P, SZ, P], I),
+    "pfsgnn_target_global_fwd": ([SEGP, I, I, I, P, I, I, P, P, I, P, P, P, P, P, P, P, FL, FL,
+                                  P, P, P, P, I, P, P, I, P, P, P, P, FL] + [P] * 7
+                                 + [P] * 6 + [P, SZ, P], I),
     "pfsgnn_mlp_bwd": ([P, I, P, P, P, P, FL, P, P, P, P, I, I, I, P, I, P, P, OSEGP, I, P, SZ,
                         P], I),
     "pfsgnn_build_complete": ([I, I, I, I, P, P], I),
@@ -515,6 +529,69 @@ class HipBackend:
               W2.data_ptr(), O, b2.data_ptr(), _ptr(Z), Yp.data_ptr(), _ptr(g), _ptr(bt), _ptr(rm),
               _ptr(rv), float(mom), float(eps), _ptr(Y), _ptr(mu), _ptr(var), ws, wsb, _stream())
         return (Yp if Y is None else Y), Z, Yp, mu, var
+
+    def mlp_fwd_epi(self, segs, N, W1, b1, W2, b2, bn, epi):
+        """mlp_fwd with BatchNorm + up to two linear maps of the normalised output
+        done in the normalising pass: ``epi`` = [(W, col0, nk, b)] ->
+        W[:, col0:col0+O] . Y + b ([nk, N] each, returned as a 6th item)."""
+        H, ldw1 = W1.shape
+        O = W2.shape[0]
+        self._chk(W1, b1, W2, b2)
+        arr = self._segs(segs, N)
+        Z, Yp = self.empty(H, N), self.empty(O, N)
+        g, bt, rm, rv, mom, eps = bn
+        self._chk(g, bt, rm, rv)
+        Y, mu, var = self.empty(O, N), self.empty(O), self.empty(O)
+        em = (LinMap * len(epi))()
+        outs = []
+        for i, (W, col0, nk, b) in enumerate(epi):
+            self._chk(W, b)
+            assert col0 + O <= W.shape[1] and nk <= W.shape[0]
+            o = self.empty(nk, N)
+            em[i] = LinMap(W.data_ptr(), W.shape[1], int(col0), int(nk), _ptr(b), o.data_ptr())
+            outs.append(o)
+        ws, wsb = self._wsargs(getattr(self, "_dims", None))
+        _call("pfsgnn_mlp_fwd_epi", arr, len(segs), N, W1.data_ptr(), ldw1, H, b1.data_ptr(),
+              W2.data_ptr(), O, b2.data_ptr(), Z.data_ptr(), Yp.data_ptr(), g.data_ptr(),
+              bt.data_ptr(), _ptr(rm), _ptr(rv), float(mom), float(eps), Y.data_ptr(),
+              mu.data_ptr(), var.data_ptr(), em, len(epi), ws, wsb, _stream())
+        return Y, Z, Yp, mu, var, outs
+
+    def target_global_fwd(self, segs, G, NC, W1, b1, W2, b2, bn, xs, NF, u, gW1, gb1, gW2, gb2,
+                          gw, reps, nxt=None):
+        """TModel's node_mlp_2 + BatchNorm1d (gnn.py:191-192) and the GlobalModel
+        (gnn.py:218-223), + with ``nxt`` = (We, be, Ws, bs) the next block's
+        per-class parts Pt, Qt (pfsgnn_target_global_fwd).  -> dict."""
+        H, ldw1 = W1.shape
+        F = W2.shape[0]
+        N = G * NC
+        gH = gW1.shape[0]
+        self._chk(W1, b1, W2, b2, xs, u, gW1, gb1, gW2, gb2, gw)
+        arr = self._segs(segs, N)
+        g, bt, rm, rv, mom, eps = bn
+        self._chk(g, bt, rm, rv)
+        r = dict(Z=self.empty(H, N), Yp=self.empty(F, N), xt=self.empty(F, N), mu=self.empty(F),
+                 var=self.empty(F), means=self.empty(2 * F, G), gZ=self.empty(gH, G),
+                 gV=self.empty(F, G), u=self.empty(F, G))
+        rms = (self.empty(F, G), self.empty(G), self.empty(G)) if gw is not None else None
+        y1, r1, r2 = rms if rms is not None else (None, None, None)
+        We = be = Ws = bs = Pt = Qt = None
+        if nxt is not None:
+            We, be, Ws, bs = nxt
+            self._chk(We, be, Ws, bs)
+            assert We.shape == (4 * F, 4 * F) and Ws.shape == (2 * F, 2 * F)
+            Pt, Qt = self.empty(4 * F, N), self.empty(2 * F, N)
+        ws, wsb = self._wsargs(getattr(self, "_dims", None))
+        _call("pfsgnn_target_global_fwd", arr, len(segs), G, NC, W1.data_ptr(), ldw1, H,
+              b1.data_ptr(), W2.data_ptr(), F, b2.data_ptr(), r["Z"].data_ptr(),
+              r["Yp"].data_ptr(), g.data_ptr(), bt.data_ptr(), _ptr(rm), _ptr(rv), float(mom),
+              float(eps), r["xt"].data_ptr(), r["mu"].data_ptr(), r["var"].data_ptr(),
+              xs.data_ptr(), NF, u.data_ptr(), gW1.data_ptr(), gH, gb1.data_ptr(), gW2.data_ptr(),
+              gb2.data_ptr(), _ptr(gw), float(reps), r["means"].data_ptr(), r["gZ"].data_ptr(),
+              r["gV"].data_ptr(), r["u"].data_ptr(), _ptr(y1), _ptr(r1), _ptr(r2), _ptr(We),
+              _ptr(be), _ptr(Ws), _ptr(bs), _ptr(Pt), _ptr(Qt), ws, wsb, _stream())
+        r["rms"], r["Pt"], r["Qt"] = rms, Pt, Qt
+        return r
 
     def mlp_bwd(self, dY, Z, W1, W2, K, bn=None, outs=()):
         """Input side of the MLP(+BN) backward.  ``bn`` = (Yp, mu, var, gamma, eps,

@@ -172,6 +172,26 @@ class EmuBackend:
         Y, mu, var = self.bn_fwd(Yp, g, bt, rm, rv, mom, eps)
         return Y, Z, Yp, mu, var
 
+    def mlp_fwd_epi(self, segs, N, W1, b1, W2, b2, bn, epi):
+        Y, Z, Yp, mu, var = self.mlp_fwd(segs, N, W1, b1, W2, b2, bn=bn)
+        O = W2.shape[0]
+        outs = [W[:nk, col0:col0 + O] @ Y + (0 if b is None else b[:nk, None])
+                for W, col0, nk, b in epi]
+        return Y, Z, Yp, mu, var, outs
+
+    def target_global_fwd(self, segs, G, NC, W1, b1, W2, b2, bn, xs, NF, u, gW1, gb1, gW2, gb2,
+                          gw, reps, nxt=None):
+        xt, Z, Yp, mu, var = self.mlp_fwd(segs, G * NC, W1, b1, W2, b2, bn=bn)
+        un, means, gZ, gV, rms = self.global_fwd(xs, xt, u, gW1, gb1, gW2, gb2, gw, reps, G)
+        r = dict(Z=Z, Yp=Yp, xt=xt, mu=mu, var=var, means=means, gZ=gZ, gV=gV, u=un, rms=rms,
+                 Pt=None, Qt=None)
+        if nxt is not None:
+            We, be, Ws, bs = nxt
+            F = xt.shape[0]
+            r["Pt"] = self.lin_cat(We, [(xt, F, False), (un, 3 * F, True)], G * NC, b=be)
+            r["Qt"] = self.lin(Ws, 0, F, xt, b=bs)
+        return r
+
     def mlp_bwd(self, dY, Z, W1, W2, K, bn=None, outs=()):
         dYp = dY
         if bn is not None:

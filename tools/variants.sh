@@ -6,7 +6,7 @@
 set -e
 cd "$(dirname "$0")/../pfs-neural-net_amd"
 make -j8 >/dev/null
-objs=$(ls build/*.o | grep -v pfsgnn_mfma.o)
+objs=$(ls build/*.o | grep -v -e pfsgnn_mfma.o -e var_)
 flags=$(make -s -f - print <<'MK'
 include Makefile
 print:
