@@ -75,6 +75,14 @@ size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F);
 #define PFSGNN_EDGE_BF16X6 7
 int pfsgnn_set_edge_path(int path);
 int pfsgnn_get_edge_path(void);
+/* Sync buffer of the in-launch reductions: a device buffer of
+ * pfsgnn_sync_bytes() bytes, ZEROED by the caller before it is set and then
+ * owned by the library (every launch leaves it zeroed again; one stream at a
+ * time).  With it, kernels whose blocks write partials of a group (the
+ * SModel moments' class splits, ...) finish the group's reduction in the
+ * group's last block instead of a separate reduce launch.  NULL unsets it. */
+size_t pfsgnn_sync_bytes(void);
+int pfsgnn_set_sync_buffer(void* buf, size_t bytes);
 /* Grid the current edge path launches for a batch (host-only query, for tests
  * and diagnostics): info[0] = KS class splits, [1] = classes per split,
  * [2] = blocks per edge kernel, [3] = 64-fiber groups per graph. */

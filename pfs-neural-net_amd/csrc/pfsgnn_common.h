@@ -51,6 +51,15 @@ class Timer {
 __device__ __forceinline__ float lrelu(float x) { return x > 0.f ? x : PF_LEAKY * x; }
 __device__ __forceinline__ float dlrelu(float z) { return z > 0.f ? 1.f : PF_LEAKY; }
 
+// agent-scope relaxed atomic store / load of a float: global_store / load ... sc1
+// (write-through / L1-bypassing; the in-launch hand-off below)
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ------------------------------------------------------------ double BatchNorm
 // EdgeModel's BatchNorm applied twice (gnn.py:101) from the batch moments
 // (m, v) of channel c: xe_new = sc*y + sh, and both running-stat updates.
@@ -164,6 +173,8 @@ __device__ __forceinline__ void pebay_merge(T na, T& ma, T& M2a, T& M3a, T& M4a,
 // Pebay partials partS [KS][4][C][NS] (merged in k order, in double), written
 // as mom [4][C][NS] = (mean, M2/n, M3/n, M4/n) and hs [4C][NS] = (mean, std,
 // skew, kurt) with gnn.py:140-151's leaky variance and eps
+// (SC1: the partials are read with sc1 loads -- the in-launch hand-off)
+template <bool SC1 = false>
 __device__ __forceinline__ void source_finalize_one(const float* __restrict__ partS, int KS,
                                                     int CPS, int C, long long NS, int NC,
                                                     long long idx, float* __restrict__ mom,
@@ -174,10 +185,13 @@ __device__ __forceinline__ void source_finalize_one(const float* __restrict__ pa
     const float* p = partS + (size_t)k * 4 * CNS + idx;
     const double nb = (double)(min(NC, (k + 1) * CPS) - k * CPS);
     if (nb <= 0) break;
+    const float p0 = SC1 ? ld_sc1(p) : p[0], p1 = SC1 ? ld_sc1(p + CNS) : p[CNS];
+    const float p2 = SC1 ? ld_sc1(p + 2 * CNS) : p[2 * CNS];
+    const float p3 = SC1 ? ld_sc1(p + 3 * CNS) : p[3 * CNS];
     if (na == 0) {
-      mean = p[0]; M2 = p[CNS]; M3 = p[2 * CNS]; M4 = p[3 * CNS];
+      mean = p0; M2 = p1; M3 = p2; M4 = p3;
     } else {
-      pebay_merge<double>(na, mean, M2, M3, M4, nb, p[0], p[CNS], p[2 * CNS], p[3 * CNS]);
+      pebay_merge<double>(na, mean, M2, M3, M4, nb, p0, p1, p2, p3);
     }
     na += nb;
   }
@@ -346,3 +360,35 @@ void launch_reduce_columns(const float* part, int G, int BPG, int NC, int C, flo
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 static inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// ------------------------------------------------------------ in-launch hand-off
+// A kernel whose blocks each write a partial of a group (the KS class splits of
+// a fiber group, ...) can finish the group's reduction in the block that
+// arrives last, instead of a separate reduce launch.  Protocol (gfx950, the
+// sc1 form of MI355X_MICROARCH.md's hand-off table, row 1): every partial byte
+// is stored with an agent-scope relaxed atomic store (global_store ... sc1,
+// written through to the memory side), every storing wave waits for its
+// stores, a workgroup barrier, then ONE lane adds 1 to the group's counter
+// (agent-scope atomic, returning); the block that draws expect-1 reads every
+// partial with sc1 loads (agent-scope relaxed atomic loads) after another
+// barrier, and resets the counter for the next launch.  No release fence
+// (no L2 write-back) is needed: no partial is ever held in a non-coherent L2.
+// The counters live in the library's zero-initialised sync buffer
+// (pfsgnn_set_sync_buffer); without one the callers keep their reduce launch.
+namespace pf {
+unsigned* sync_counters(size_t n);   // n counters, or nullptr
+}  // namespace pf
+// true in every thread of the block that arrives last of `expect` at *cnt
+// (the caller's stores of its partial must all be st_sc1); flag: an LDS word
+__device__ __forceinline__ bool last_arrival(unsigned* cnt, unsigned expect, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old + 1u == expect ? 1 : 0;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}

@@ -1493,9 +1493,15 @@ extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, c
   float* partS = w.take((size_t)geo.KS * 4 * C * geo.NS);
   if (use_mfma()) {
     PF_REQUIRE(partS, "pfsgnn_source_fwd", "workspace too small");
+    // the class splits of a fiber group are merged by its last block (the
+    // in-launch hand-off) when the library has a sync buffer
+    unsigned* cnt = pf::sync_counters((size_t)G * geo.NFG);
     pf::Timer tm_("source_fwd", st);
-    if (int rc = pfm::source_fwd(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, partS, mf_prec(1), st)) return rc;
+    if (int rc = pfm::source_fwd(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, partS, cnt, mom, hs,
+                                 mf_prec(1), st))
+      return rc;
     tm_.end();
+    if (cnt) return pf::check_launch("pfsgnn_source_fwd");
   } else {
   const float* QtT = class_rows(Qt, C, geo, w, st);
   const float* Ws2T = transposed(Ws2, C, C, w, st);

@@ -24,7 +24,7 @@ int edge_mlp_fwd(const EdgeGeo& geo, int F, const float* xe, const float* xsc, c
                  const float* b2, float* y, float* part, int prec, int bfy, hipStream_t st);
 int source_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
-               float* partS, int prec, hipStream_t st);
+               float* partS, unsigned* cnt, float* mom, float* hs, int prec, hipStream_t st);
 // TModel's LeakyReLU mask (pfsgnn_mfma.hip mask_bits): target_fwd writes it
 // when `tmask` is non-null (4 bytes per edge), target_bwd / source_bwd read
 // it in place of recomputing that layer when non-null

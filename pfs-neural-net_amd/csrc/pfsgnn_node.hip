@@ -1141,7 +1141,24 @@ float* defer_take(size_t nfloats) {
 }
 
 void defer_push(const RedDesc* d, int n) { g_defer.q.insert(g_defer.q.end(), d, d + n); }
+
+// the in-launch hand-off counters (pfsgnn_common.h): a caller-owned, zeroed
+// device buffer; every launch leaves its counters at zero again
+namespace {
+unsigned* g_sync = nullptr;
+size_t g_sync_n = 0;
+}  // namespace
+unsigned* sync_counters(size_t n) { return (g_sync && n <= g_sync_n) ? g_sync : nullptr; }
 }  // namespace pf
+
+extern "C" size_t pfsgnn_sync_bytes(void) { return (size_t)1 << 20; }
+
+extern "C" int pfsgnn_set_sync_buffer(void* buf, size_t bytes) {
+  PF_REQUIRE(!buf || bytes >= sizeof(unsigned), "pfsgnn_set_sync_buffer", "buffer too small");
+  pf::g_sync = static_cast<unsigned*>(buf);
+  pf::g_sync_n = buf ? bytes / sizeof(unsigned) : 0;
+  return 0;
+}
 
 extern "C" int pfsgnn_defer_begin(void* arena, size_t bytes) {
   pf::DeferCtx& D = pf::g_defer;

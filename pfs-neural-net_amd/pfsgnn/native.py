@@ -101,6 +101,8 @@ _SIGS = {
     "pfsgnn_last_error": ([], ctypes.c_char_p),
     "pfsgnn_workspace_bytes": ([I, I, I, I], SZ),
     "pfsgnn_set_edge_path": ([I], I),
+    "pfsgnn_sync_bytes": ([], SZ),
+    "pfsgnn_set_sync_buffer": ([P, SZ], I),
     "pfsgnn_get_edge_path": ([], I),
     "pfsgnn_edge_grid": ([I, I, I, ctypes.POINTER(ctypes.c_int)], I),
     "pfsgnn_timing_enable": ([I], I),
@@ -281,6 +283,22 @@ def _call(name, *args):
     _check(getattr(lib(), name)(*args), name)
 
 
+_SYNC = None
+
+
+def _ensure_sync(device):
+    """The library's in-launch reduction counters (pfsgnn_set_sync_buffer): one
+    zeroed device buffer per process, set once.  PFSGNN_NO_HANDOFF=1 leaves it
+    unset (the kernels then keep their separate reduce launches: an A/B knob)."""
+    global _SYNC
+    if _SYNC is not None or os.environ.get("PFSGNN_NO_HANDOFF", "0") == "1":
+        return
+    n = lib().pfsgnn_sync_bytes()
+    _SYNC = torch.zeros(n, dtype=torch.uint8, device=device)
+    torch.cuda.synchronize(device)
+    _call("pfsgnn_set_sync_buffer", _SYNC.data_ptr(), n)
+
+
 class HipBackend:
     """The op set of pfsgnn.engine on libpfsgnn.so (fp32, channel-major)."""
 
@@ -300,6 +318,7 @@ class HipBackend:
         # must never write into memory the allocator has handed out again
         self._retired = []
         self._sp = SparseEdgeOps(self)
+        _ensure_sync(self.device)
 
     # ------------------------------------------------------------ memory
     def empty(self, *shape):
