@@ -1338,6 +1338,17 @@ int mf_prec(int model) {
          : g_path == PFSGNN_EDGE_BF16X3 ? ((x3mask >> model) & 1 ? 3 : 1)
          : g_path == PFSGNN_EDGE_BF16X6 ? 4 : 0;
 }
+// SModel forward on the fiber-tile grid (km_source_fwd_ft, no class-split
+// partials) with PFSGNN_SFWD_TILES=1 (A/B knob; the class-split grid's blocks
+// fill the chip's slots better at the bench shape: 3040 blocks = 2.97 rounds of
+// 1024 vs 2400 = 2.34)
+bool sfwd_tiles() {
+  static const bool on = [] {
+    const char* e = getenv("PFSGNN_SFWD_TILES");
+    return e && atoi(e) == 1;
+  }();
+  return on;
+}
 int mf_bfy() { return g_path == PFSGNN_EDGE_BF16Y || g_path == PFSGNN_EDGE_BF16 ? 1 : 0; }
 // MFMA blocks stage their class-table rows in LDS: at most MAX_CPS classes each
 EdgeGeo geo_mfma(int G, int NF, int NC) {
@@ -1490,6 +1501,14 @@ extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, c
   const int C = 2 * F;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
   hipStream_t st = as_stream(stream);
+  if (use_mfma() && NC <= 256 && sfwd_tiles()) {
+    pf::Timer tm_("source_fwd", st);
+    if (int rc = pfm::source_fwd_tiles(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs, mf_prec(1),
+                                       st))
+      return rc;
+    tm_.end();
+    return pf::check_launch("pfsgnn_source_fwd");
+  }
   float* partS = w.take((size_t)geo.KS * 4 * C * geo.NS);
   if (use_mfma()) {
     PF_REQUIRE(partS, "pfsgnn_source_fwd", "workspace too small");

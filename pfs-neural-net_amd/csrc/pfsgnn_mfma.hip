@@ -933,6 +933,153 @@ __global__ __launch_bounds__(256) void km_source_fwd(EdgeGeo geo, const float* _
   }
 }
 
+// ------------------------------------------------------------ SModel fwd, fiber tiles
+// The same message and Pebay update on a fiber-tile grid: a block owns 16
+// fibers of one graph and ALL its classes, wave w the classes w, w+4, ...; the
+// 4 waves' states are merged in the block (Pebay's pairwise formula, double,
+// fixed order 0 <- 1 <- 2 <- 3) and the moments written straight to mom / hs
+// (k_source_finalize's arithmetic): no class-split partials, no finalize
+// launch.  Blocks are mapped XCD-aware: the 8 XCDs take blocks round-robin,
+// so block b runs tile (b % 8) * ceil(nb / 8) + b / 8 -- neighbouring tiles,
+// whose 64-byte rows share 128-byte lines, sit in one XCD's L2.
+#define MF_SFT_MAXNC 256
+template <int F, int PREC>
+__global__ __launch_bounds__(256) void km_source_fwd_ft(
+    EdgeGeo geo, int ntiles, const float* __restrict__ y, const float* __restrict__ sc,
+    const float* __restrict__ sh, const float* __restrict__ QtS, const float* __restrict__ Ws1,
+    const float* __restrict__ Ws2, const float* __restrict__ bs2, float* __restrict__ mom,
+    float* __restrict__ hs) {
+  constexpr int C = 2 * F, NT = GM<C>::NT, CP = ClassRows<C>::CP;
+  constexpr int MS = 4 * 4 * NT;   // a lane's merge state: 4 sums x NT tiles x 4 slots
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int g4 = lane >> 4, j16 = lane & 15;
+  const int per = (ntiles + 7) >> 3, bx = blockIdx.x;
+  const int tile = (bx & 7) * per + (bx >> 3);
+  const int TPG = (geo.NF + 15) >> 4;            // tiles per graph
+  if (tile >= ntiles) return;   // (block-uniform: the grid is rounded up to 8 * per)
+  const bool tvalid = true;
+  const int gg = tile / TPG, ft = tile - gg * TPG;
+  const int f = ft * 16 + j16;
+  const bool fvalid = tvalid && f < geo.NF;
+  const long long NS = geo.NS, n = (long long)gg * geo.NF + (fvalid ? f : 0);
+  const int NC = geo.NC;
+  const uint32_t RB = (uint32_t)geo.E * 4u;
+  const uint32_t eo0 = (uint32_t)((((long long)gg * NC) * geo.NF + (fvalid ? f : 0)) * 4);
+  const uint32_t eoc = (uint32_t)geo.NF * 4u, EB = (uint32_t)geo.E * 4u;
+  __shared__ __attribute__((aligned(16))) float qtl[MF_SFT_MAXNC * CP];
+  __shared__ __attribute__((aligned(16))) float pco[MF_SFT_MAXNC / 4 + 1][8];
+  ClassRows<C>::stage(qtl, QtS, geo.NT, (long long)gg * NC, NC);
+  FwdLayer<PREC, C, F> L1;
+  L1.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
+  FwdLayer<PREC, C, C> L2;
+  L2.load([&](int o, int h) { return Ws2[o * C + h]; }, lane);
+  floatx4 bias[NT];
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt) bias[tt] = ld_vec<C>(bs2, tt, g4);
+  const floatx4 scv = ld_fconst<F>(sc, g4, 1.f), shv = ld_fconst<F>(sh, g4, 0.f);
+  MF_FMASK(F)
+  const Rsrc ry = rsrc(y, EB * F);
+  floatx4 S1[NT], S2[NT], S3[NT], S4[NT];
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt) S1[tt] = S2[tt] = S3[tt] = S4[tt] = zero4();
+  // Pebay coefficients of the k-th message of a wave (count k + 1), as km_source_fwd
+  const int nk = (NC + 3) >> 2;
+  if (t < nk) {
+    const double nn = t + 1, r = 1.0 / nn;
+    pco[t][0] = (float)((nn - 1) * r);
+    pco[t][1] = (float)((nn - 1) * (nn - 2) * r * r);
+    pco[t][2] = (float)((nn - 1) * (nn * nn - 3 * nn + 3) * r * r * r);
+    pco[t][3] = (float)r;
+    pco[t][4] = (float)(6 * r * r);
+    pco[t][5] = (float)(-4 * r);
+    pco[t][6] = (float)(-3 * r);
+    pco[t][7] = 0.f;
+  }
+  __syncthreads();   // qtl, pco
+  // wave w: classes w + 4k, k = 0 .. (its count) - 1, streamed as k
+  const int kw = (NC - wave + 3) >> 2;
+  auto load = [&](int k) {
+    Rows<1> r;
+    r.v[0] = ld_frows<F>(ry, (uint32_t)(wave + 4 * k) * eoc, ro);
+    return r;
+  };
+  class_stream<MF_DEPTH_FWD>(0, kw, load, [&](const Rows<1>& rows, int k) {
+    const int c = wave + 4 * k;
+    const floatx4 x[1] = {edge_in<F>(rows.v[0], fm, sc, scv, shv)};
+    floatx4 z[NT], a[NT], m[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) z[tt] = ClassRows<C>::get(qtl, c, tt, g4);
+    L1.apply(x, z);
+    lrelu_act<C>(z, a);
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) m[tt] = bias[tt];
+    L2.apply(a, m);
+    const floatx4 ca = *reinterpret_cast<const floatx4*>(&pco[k][0]);
+    const floatx4 cb = *reinterpret_cast<const floatx4*>(&pco[k][4]);
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+      for (int r = 0; r < GM<C>::nreg(tt); ++r) {
+        const float d = m[tt][r] - S1[tt][r], d2 = d * d;
+        const float m2 = S2[tt][r], m3 = S3[tt][r];
+        S4[tt][r] = fmaf(d, m3 * cb[1], fmaf(d2, fmaf(d2, ca[2], m2 * cb[0]), S4[tt][r]));
+        S3[tt][r] = fmaf(d, fmaf(d2, ca[1], m2 * cb[2]), m3);
+        S2[tt][r] = fmaf(d2, ca[0], m2);
+        S1[tt][r] = fmaf(d, ca[3], S1[tt][r]);
+      }
+  });
+  // merge: waves 1..3 park their states in LDS (qtl is free once every wave is past its loop)
+  __syncthreads();
+  float* ms = qtl;   // [3][MS][64]
+  static_assert(3 * MS * 64 <= MF_SFT_MAXNC * CP, "merge scratch exceeds the class table");
+  if (wave > 0) {
+    float* p = ms + (size_t)(wave - 1) * MS * 64 + lane;
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        p[((0 * NT + tt) * 4 + r) * 64] = S1[tt][r];
+        p[((1 * NT + tt) * 4 + r) * 64] = S2[tt][r];
+        p[((2 * NT + tt) * 4 + r) * 64] = S3[tt][r];
+        p[((3 * NT + tt) * 4 + r) * 64] = S4[tt][r];
+      }
+  }
+  __syncthreads();
+  if (wave != 0 || !fvalid) return;
+  const double invn = 1.0 / (double)NC;
+#pragma unroll
+  for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+    for (int r = 0; r < GM<C>::nreg(tt); ++r) {
+      const int o = GM<C>::row(g4, 4 * tt + r);
+      if (o < 0) continue;
+      double na = (double)kw, mean = S1[tt][r], M2 = S2[tt][r], M3 = S3[tt][r], M4 = S4[tt][r];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        const double nb = (double)((NC - w + 3) >> 2);
+        if (nb <= 0) continue;
+        const float* p = ms + (size_t)(w - 1) * MS * 64 + lane;
+        pebay_merge<double>(na, mean, M2, M3, M4, nb, p[((0 * NT + tt) * 4 + r) * 64],
+                            p[((1 * NT + tt) * 4 + r) * 64], p[((2 * NT + tt) * 4 + r) * 64],
+                            p[((3 * NT + tt) * 4 + r) * 64]);
+        na += nb;
+      }
+      const long long idx = (long long)o * NS + n, CNS = (long long)C * NS;
+      const float c2 = (float)(M2 * invn), c3 = (float)(M3 * invn), c4 = (float)(M4 * invn);
+      mom[idx] = (float)mean;
+      mom[CNS + idx] = c2;
+      mom[2 * CNS + idx] = c3;
+      mom[3 * CNS + idx] = c4;
+      const float var = c2 > 0.f ? c2 : 0.01f * c2;  // F.leaky_relu (slope 0.01), gnn.py:141
+      const float sd = sqrtf(var + 1e-6f);
+      hs[idx] = (float)mean;
+      hs[CNS + idx] = sd;
+      hs[2 * CNS + idx] = c3 / (sd * sd * sd);
+      hs[3 * CNS + idx] = c4 / ((sd * sd) * (sd * sd));
+    }
+}
+
 // ============================================================ TModel fwd
 // a = lrelu(Rs[f] + Wt1[:, F:2F] x) per edge and its per-class sum over fibers
 // (gnn.py:188-190; the second Linear runs after the sum, on the node side).
@@ -1538,6 +1685,26 @@ int source_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
                float* partS, unsigned* cnt, float* mom, float* hs, int prec, hipStream_t st) {
   MF_LAUNCH(F, fwd_prec(prec), km_source_fwd, y, sc, sh, QtS, Ws1, Ws2, bs2, partS, cnt, mom, hs)
+  return 0;
+}
+
+int source_fwd_tiles(const EdgeGeo& geo, int F, const float* y, const float* sc,
+                     const float* sh, const float* QtS, const float* Ws1, const float* Ws2,
+                     const float* bs2, float* mom, float* hs, int prec, hipStream_t st) {
+  if (geo.NC > MF_SFT_MAXNC) return pf::fail("pfsgnn mfma", "source_fwd_tiles: NC > 256");
+  const int ntiles = geo.G * ((geo.NF + 15) / 16);
+  const int nb = 8 * ((ntiles + 7) / 8);
+#define MF_SFT(FF, PP)                                                                    \
+  case FF * 8 + PP:                                                                       \
+    hipLaunchKernelGGL((km_source_fwd_ft<FF, PP>), dim3(nb), dim3(256), 0, st, geo, ntiles, \
+                       y, sc, sh, QtS, Ws1, Ws2, bs2, mom, hs);                           \
+    break;
+  switch (F * 8 + fwd_prec(prec)) {
+    MF_SFT(8, 0) MF_SFT(8, 1) MF_SFT(10, 0) MF_SFT(10, 1) MF_SFT(10, 2) MF_SFT(10, 3)
+    MF_SFT(10, 4) MF_SFT(16, 0) MF_SFT(16, 1)
+    default: return pf::fail("pfsgnn mfma", "unsupported Fdim for this edge path");
+  }
+#undef MF_SFT
   return 0;
 }
 

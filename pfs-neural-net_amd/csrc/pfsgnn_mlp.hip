@@ -286,12 +286,13 @@ __device__ void bn_stats_part(const float* __restrict__ part, int nb, int O, int
                               bool write, float (*cf)[16]) {
   __shared__ double acc[16][16][2];
   __shared__ double mean_s[16];
-  const int t = threadIdx.x, c = t & 15, u = t >> 4;
+  const int t = threadIdx.x, c = t & 15, u = (t >> 4) & 15;
+  const bool act = t < 256;   // (blocks wider than 256 threads: the first 256 merge)
   constexpr int PB = 32;  // partials per thread: nb <= 512 (the MLP grid)
   float pc[PB], pm[PB], pq[PB];
 #pragma unroll
   for (int i = 0; i < PB; ++i) {  // every load in flight before the sums
-    const int b = u + 16 * i;
+    const int b = act ? u + 16 * i : nb;
     const float* p = part + (size_t)(b < nb ? b : 0) * PART_LEN;
     pc[i] = b < nb ? p[0] : 0.f;
     pm[i] = b < nb ? p[1 + c] : 0.f;
@@ -302,7 +303,7 @@ __device__ void bn_stats_part(const float* __restrict__ part, int nb, int O, int
   double S = 0.0;
 #pragma unroll
   for (int i = 0; i < PB; ++i) S += (double)pc[i] * (double)pm[i];
-  acc[u][c][0] = S;
+  if (act) acc[u][c][0] = S;
   __syncthreads();
   if (t < 16) {
     double St = 0.0;
@@ -317,7 +318,7 @@ __device__ void bn_stats_part(const float* __restrict__ part, int nb, int O, int
     const double d = (double)pm[i] - mean;
     Q += (double)pq[i] + (double)pc[i] * d * d;
   }
-  acc[u][c][1] = Q;
+  if (act) acc[u][c][1] = Q;
   __syncthreads();
   if (t < 16) {
     double Qc = 0.0;
@@ -443,20 +444,21 @@ struct ClassGlobalArgs {
   float *Pt, *Qt;                           // [4F][G*NC], [2F][G*NC]
 };
 
-__global__ __launch_bounds__(256) void k_class_global_fwd(ClassGlobalArgs A) {
+constexpr int CG_THREADS = 512;
+__global__ __launch_bounds__(CG_THREADS) void k_class_global_fwd(ClassGlobalArgs A) {
   __shared__ float cf[4][16];
   __shared__ float h[CG_MAXH], z[CG_MAXH], vv[CG_MAXH];
-  __shared__ float scratch[4 * 2 * CG_MAXF];
+  __shared__ float scratch[CG_THREADS / 64][2 * CG_MAXF];
   __shared__ float wt[4 * CG_MAXF * CG_MAXF], ws2[2 * CG_MAXF * CG_MAXF], cu[4 * CG_MAXF],
       bq[2 * CG_MAXF];
   const int g = blockIdx.x, t = threadIdx.x, F = A.F, NC = A.NC;
   const long long NT = (long long)A.G * NC, NS = (long long)A.G * A.NF;
   if (A.We) {  // next block's weight blocks staged early
-    for (int i = t; i < 4 * F * F; i += 256) {
+    for (int i = t; i < 4 * F * F; i += CG_THREADS) {
       const int k = i / F, o = i - k * F;
       wt[i] = A.We[(size_t)k * 4 * F + F + o];
     }
-    for (int i = t; i < 2 * F * F; i += 256) {
+    for (int i = t; i < 2 * F * F; i += CG_THREADS) {
       const int k = i / F, o = i - k * F;
       ws2[i] = A.Ws[(size_t)k * 2 * F + o];
     }
@@ -467,7 +469,7 @@ __global__ __launch_bounds__(256) void k_class_global_fwd(ClassGlobalArgs A) {
   float sm[2 * CG_MAXF];
 #pragma unroll
   for (int o = 0; o < 2 * CG_MAXF; ++o) sm[o] = 0.f;
-  for (int c = t; c < NC; c += 256) {
+  for (int c = t; c < NC; c += CG_THREADS) {
     const long long n = (long long)g * NC + c;
 #pragma unroll
     for (int o = 0; o < CG_MAXF; ++o) {
@@ -478,13 +480,38 @@ __global__ __launch_bounds__(256) void k_class_global_fwd(ClassGlobalArgs A) {
       }
     }
   }
-  for (int f = t; f < A.NF; f += 256) {
-    const long long n = (long long)g * A.NF + f;
+  // the graph's x_s: U fibers x F channels of loads in flight per thread (a
+  // serial loop over the 2394 fibers is latency-bound: round 2 measured 39 us)
+  constexpr int U = 4;
+  for (int f0 = 0; f0 < A.NF; f0 += CG_THREADS * U) {
+    float v[U][CG_MAXF];
 #pragma unroll
-    for (int o = 0; o < CG_MAXF; ++o)
-      if (o < F) sm[o] += A.xs[(size_t)o * NS + n];
+    for (int q = 0; q < U; ++q) {
+      const int f = f0 + q * CG_THREADS + t;
+      const long long n = (long long)g * A.NF + (f < A.NF ? f : 0);
+#pragma unroll
+      for (int o = 0; o < CG_MAXF; ++o) v[q][o] = (o < F && f < A.NF) ? A.xs[(size_t)o * NS + n] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q)
+#pragma unroll
+      for (int o = 0; o < CG_MAXF; ++o) sm[o] += v[q][o];
   }
-  block_sum<2 * CG_MAXF>(sm, scratch);
+  {  // block sums, fixed order: DPP within each wave, then the waves in order
+    const int wv = t >> 6, ln = t & 63;
+#pragma unroll
+    for (int i = 0; i < 2 * CG_MAXF; ++i) {
+      const float x = wave_sum(sm[i]);
+      if (ln == 0) scratch[wv][i] = x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2 * CG_MAXF; ++i) {
+      float x = 0.f;
+      for (int w = 0; w < CG_THREADS / 64; ++w) x += scratch[w][i];
+      sm[i] = x;
+    }
+  }
   const int K = 3 * F;
   if (t < F) {
     h[t] = A.u[(size_t)t * A.G + g];
@@ -495,14 +522,14 @@ __global__ __launch_bounds__(256) void k_class_global_fwd(ClassGlobalArgs A) {
     A.means[(size_t)(F + t) * A.G + g] = mt;
   }
   __syncthreads();
-  for (int j = t; j < A.H; j += 256) {
+  for (int j = t; j < A.H; j += CG_THREADS) {
     float acc = A.b1[j];
     for (int k = 0; k < K; ++k) acc = fmaf(A.W1[(size_t)j * K + k], h[k], acc);
     z[j] = acc;
     A.Z[(size_t)j * A.G + g] = acc;
   }
   __syncthreads();
-  for (int o = t; o < F; o += 256) {
+  for (int o = t; o < F; o += CG_THREADS) {
     float acc = A.b2[o];
     for (int j = 0; j < A.H; ++j) acc = fmaf(A.W2[(size_t)o * A.H + j], lrelu(z[j]), acc);
     vv[o] = acc;
@@ -541,7 +568,7 @@ __global__ __launch_bounds__(256) void k_class_global_fwd(ClassGlobalArgs A) {
     bq[t - 128] = A.bs[t - 128];
   }
   __syncthreads();
-  for (int c = t; c < NC; c += 256) {
+  for (int c = t; c < NC; c += CG_THREADS) {
     const long long n = (long long)g * NC + c;
     float x[CG_MAXF];
 #pragma unroll
@@ -986,7 +1013,7 @@ extern "C" int pfsgnn_target_global_fwd(
   A.xs = xs; A.u = u; A.W1 = gW1; A.b1 = gb1; A.W2 = gW2; A.b2 = gb2; A.w = gw; A.H = gH;
   A.reps = reps; A.means = means; A.Z = gZ; A.V = gV; A.Y = unew; A.y1 = y1; A.r1 = r1; A.r2 = r2;
   A.We = We; A.be = be; A.Ws = Ws; A.bs = bs; A.Pt = Pt; A.Qt = Qt;
-  hipLaunchKernelGGL(k_class_global_fwd, dim3(G), dim3(256), 0, st, A);
+  hipLaunchKernelGGL(k_class_global_fwd, dim3(G), dim3(CG_THREADS), 0, st, A);
   return pf::check_launch(where);
 }
 
