@@ -1338,14 +1338,14 @@ int mf_prec(int model) {
          : g_path == PFSGNN_EDGE_BF16X3 ? ((x3mask >> model) & 1 ? 3 : 1)
          : g_path == PFSGNN_EDGE_BF16X6 ? 4 : 0;
 }
-// SModel forward on the fiber-tile grid (km_source_fwd_ft, no class-split
-// partials) with PFSGNN_SFWD_TILES=1 (A/B knob; the class-split grid's blocks
-// fill the chip's slots better at the bench shape: 3040 blocks = 2.97 rounds of
-// 1024 vs 2400 = 2.34)
+// SModel forward on the fiber-tile grid (km_source_fwd_ft: no class-split
+// partials, no finalize launch); PFSGNN_SFWD_TILES=0 keeps the class-split
+// kernel + k_source_finalize (A/B knob: 136 + 16 us vs 149 us per launch at the
+// bench shape, where the class-split grid fills the chip's block slots better)
 bool sfwd_tiles() {
   static const bool on = [] {
     const char* e = getenv("PFSGNN_SFWD_TILES");
-    return e && atoi(e) == 1;
+    return !(e && atoi(e) == 0);
   }();
   return on;
 }
@@ -1512,15 +1512,10 @@ extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, c
   float* partS = w.take((size_t)geo.KS * 4 * C * geo.NS);
   if (use_mfma()) {
     PF_REQUIRE(partS, "pfsgnn_source_fwd", "workspace too small");
-    // the class splits of a fiber group are merged by its last block (the
-    // in-launch hand-off) when the library has a sync buffer
-    unsigned* cnt = pf::sync_counters((size_t)G * geo.NFG);
     pf::Timer tm_("source_fwd", st);
-    if (int rc = pfm::source_fwd(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, partS, cnt, mom, hs,
-                                 mf_prec(1), st))
+    if (int rc = pfm::source_fwd(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, partS, mf_prec(1), st))
       return rc;
     tm_.end();
-    if (cnt) return pf::check_launch("pfsgnn_source_fwd");
   } else {
   const float* QtT = class_rows(Qt, C, geo, w, st);
   const float* Ws2T = transposed(Ws2, C, C, w, st);

@@ -24,7 +24,7 @@ int edge_mlp_fwd(const EdgeGeo& geo, int F, const float* xe, const float* xsc, c
                  const float* b2, float* y, float* part, int prec, int bfy, hipStream_t st);
 int source_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
-               float* partS, unsigned* cnt, float* mom, float* hs, int prec, hipStream_t st);
+               float* partS, int prec, hipStream_t st);
 // the fiber-tile form (pfsgnn_mfma.hip km_source_fwd_ft): moments straight to
 // mom / hs, no partials; NC <= 256
 int source_fwd_tiles(const EdgeGeo& geo, int F, const float* y, const float* sc,

@@ -826,10 +826,7 @@ __global__ __launch_bounds__(256) void km_source_fwd(EdgeGeo geo, const float* _
                                                      const float* __restrict__ Ws1,
                                                      const float* __restrict__ Ws2,
                                                      const float* __restrict__ bs2,
-                                                     float* __restrict__ partS,
-                                                     unsigned* __restrict__ cnt,
-                                                     float* __restrict__ mom,
-                                                     float* __restrict__ hs) {
+                                                     float* __restrict__ partS) {
   constexpr int C = 2 * F, NT = GM<C>::NT;
   MF_GEO
   __shared__ __attribute__((aligned(16))) float qtl[MF_MAX_CPS * ClassRows<C>::CP];
@@ -904,32 +901,12 @@ __global__ __launch_bounds__(256) void km_source_fwd(EdgeGeo geo, const float* _
       for (int r = 0; r < GM<C>::nreg(tt); ++r) {
         const int o = GM<C>::row(g4, 4 * tt + r);
         if (o >= 0) {
-          if (cnt) {   // the hand-off form (pfsgnn_common.h)
-            st_sc1(dst + (size_t)o * NS, S1[tt][r]);
-            st_sc1(dst + (size_t)(C + o) * NS, S2[tt][r]);
-            st_sc1(dst + (size_t)(2 * C + o) * NS, S3[tt][r]);
-            st_sc1(dst + (size_t)(3 * C + o) * NS, S4[tt][r]);
-          } else {
-            dst[(size_t)o * NS] = S1[tt][r];
-            dst[(size_t)(C + o) * NS] = S2[tt][r];
-            dst[(size_t)(2 * C + o) * NS] = S3[tt][r];
-            dst[(size_t)(3 * C + o) * NS] = S4[tt][r];
-          }
+          dst[(size_t)o * NS] = S1[tt][r];
+          dst[(size_t)(C + o) * NS] = S2[tt][r];
+          dst[(size_t)(2 * C + o) * NS] = S3[tt][r];
+          dst[(size_t)(3 * C + o) * NS] = S4[tt][r];
         }
       }
-  }
-  if (!cnt) return;
-  // the fiber group's last class split merges the KS partials (k_source_finalize's
-  // arithmetic, fixed order) into mom / hs: no finalize launch
-  __shared__ int lastf;
-  if (!last_arrival(cnt + grp, (unsigned)geo.KS, &lastf)) return;
-  const int nf = min(64, geo.NF - fg * 64);
-  const long long nb0 = (long long)gg * geo.NF + fg * 64;
-  for (int e = t; e < C * 64; e += PF_BLOCK) {
-    const int o = e >> 6, fl = e & 63;
-    if (fl < nf)
-      source_finalize_one<true>(partS, geo.KS, geo.CPS, C, NS, geo.NC, (long long)o * NS + nb0 + fl,
-                                mom, hs);
   }
 }
 
@@ -1683,8 +1660,8 @@ int edge_mlp_fwd(const EdgeGeo& geo, int F, const float* xe, const float* xsc, c
 
 int source_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
-               float* partS, unsigned* cnt, float* mom, float* hs, int prec, hipStream_t st) {
-  MF_LAUNCH(F, fwd_prec(prec), km_source_fwd, y, sc, sh, QtS, Ws1, Ws2, bs2, partS, cnt, mom, hs)
+               float* partS, int prec, hipStream_t st) {
+  MF_LAUNCH(F, fwd_prec(prec), km_source_fwd, y, sc, sh, QtS, Ws1, Ws2, bs2, partS)
   return 0;
 }
 

@@ -33,6 +33,8 @@ Algebra used to cut per-edge work (all exact in real arithmetic):
   SModel edge pass, which also adds the downstream edge gradient and takes the
   edge BatchNorm's two gradient sums -- one pass instead of four.
 """
+import os
+
 import torch
 
 
@@ -118,6 +120,8 @@ class Engine:
         target_global_fwd for TModel's node_mlp_2 + the GlobalModel): training
         with normalisation, on the HIP ops' shapes."""
         be, F = self.be, self.F
+        if os.environ.get("PFSGNN_FUSED_TAIL", "1") == "0":   # A/B knob
+            return False
         if not (self.training and self.normed and hasattr(be, "target_global_fwd") and F <= 16):
             return False
         def mlp_ok(pre):
