@@ -288,21 +288,29 @@ __device__ void bn_stats_part(const float* __restrict__ part, int nb, int O, int
   __shared__ double mean_s[16];
   const int t = threadIdx.x, c = t & 15, u = (t >> 4) & 15;
   const bool act = t < 256;   // (blocks wider than 256 threads: the first 256 merge)
-  constexpr int PB = 32;  // partials per thread: nb <= 512 (the MLP grid)
+  // partials per thread per round: 16 (one round for nb <= 256, the MLP grids
+  // of <= 256 blocks; two for <= 512, re-read for the second pass)
+  constexpr int PB = 16;
+  const int rounds = (nb + 255) >> 8;
   float pc[PB], pm[PB], pq[PB];
+  auto fetch = [&](int r) {
 #pragma unroll
-  for (int i = 0; i < PB; ++i) {  // every load in flight before the sums
-    const int b = act ? u + 16 * i : nb;
-    const float* p = part + (size_t)(b < nb ? b : 0) * PART_LEN;
-    pc[i] = b < nb ? p[0] : 0.f;
-    pm[i] = b < nb ? p[1 + c] : 0.f;
-    pq[i] = b < nb ? p[17 + c] : 0.f;
-  }
+    for (int i = 0; i < PB; ++i) {  // every load of the round in flight before the sums
+      const int b = act ? r * 256 + u + 16 * i : nb;
+      const float* p = part + (size_t)(b < nb ? b : 0) * PART_LEN;
+      pc[i] = b < nb ? p[0] : 0.f;
+      pm[i] = b < nb ? p[1 + c] : 0.f;
+      pq[i] = b < nb ? p[17 + c] : 0.f;
+    }
+  };
   // the partials combined in closed form (fixed order, no serial chain of
   // divisions): mean = sum c_b m_b / N, M2 = sum (q_b + c_b (m_b - mean)^2)
   double S = 0.0;
+  for (int r = 0; r < rounds; ++r) {
+    fetch(r);
 #pragma unroll
-  for (int i = 0; i < PB; ++i) S += (double)pc[i] * (double)pm[i];
+    for (int i = 0; i < PB; ++i) S += (double)pc[i] * (double)pm[i];
+  }
   if (act) acc[u][c][0] = S;
   __syncthreads();
   if (t < 16) {
@@ -313,10 +321,13 @@ __device__ void bn_stats_part(const float* __restrict__ part, int nb, int O, int
   __syncthreads();
   const double mean = mean_s[c];
   double Q = 0.0;
+  for (int r = 0; r < rounds; ++r) {
+    if (rounds > 1) fetch(r);
 #pragma unroll
-  for (int i = 0; i < PB; ++i) {
-    const double d = (double)pm[i] - mean;
-    Q += (double)pq[i] + (double)pc[i] * d * d;
+    for (int i = 0; i < PB; ++i) {
+      const double d = (double)pm[i] - mean;
+      Q += (double)pq[i] + (double)pc[i] * d * d;
+    }
   }
   if (act) acc[u][c][1] = Q;
   __syncthreads();
@@ -369,18 +380,20 @@ __global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__
                                                        float* __restrict__ mu,
                                                        float* __restrict__ var, BnEpi E) {
   __shared__ float cf[4][16];
-  __shared__ float ew[2][EPI_MAXK * 16], eb[2][EPI_MAXK];
+  __shared__ __attribute__((aligned(16))) float ew[2][EPI_MAXK * 16];
+  __shared__ float eb[2][EPI_MAXK];
   const int t = threadIdx.x;
   const bool epi = E.W[0] || E.W[1];
   if (epi) {  // weight blocks staged before the statistics (latency overlapped)
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       if (!E.W[e]) continue;
-      for (int i = t; i < E.nk[e] * 16; i += 256) {
+      const int nk4 = (E.nk[e] + 3) & ~3;   // rows past nk are zero (4-row groups below)
+      for (int i = t; i < nk4 * 16; i += 256) {
         const int k = i >> 4, o = i & 15;
-        ew[e][i] = o < O ? E.W[e][(size_t)k * E.ldw[e] + E.col0[e] + o] : 0.f;
+        ew[e][i] = (o < O && k < E.nk[e]) ? E.W[e][(size_t)k * E.ldw[e] + E.col0[e] + o] : 0.f;
       }
-      for (int k = t; k < E.nk[e]; k += 256) eb[e][k] = E.b[e] ? E.b[e][k] : 0.f;
+      for (int k = t; k < nk4; k += 256) eb[e][k] = (E.b[e] && k < E.nk[e]) ? E.b[e][k] : 0.f;
     }
   }
   bn_stats_part(part, nb, O, N, gamma, beta, eps, rm, rv, momentum, mu, var, blockIdx.x == 0, cf);
@@ -406,11 +419,21 @@ __global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       if (!E.W[e]) continue;
-      for (int k = 0; k < E.nk[e]; ++k) {
-        float a = eb[e][k];
+      for (int k0 = 0; k0 < E.nk[e]; k0 += 4) {   // 4 independent rows per step
+        float a[4];
 #pragma unroll
-        for (int o = 0; o < 16; ++o) a = fmaf(ew[e][k * 16 + o], y[o], a);
-        E.out[e][(size_t)k * N + n] = a;
+        for (int j = 0; j < 4; ++j) a[j] = eb[e][k0 + j];
+#pragma unroll
+        for (int o4 = 0; o4 < 16; o4 += 4)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const floatx4 w = *reinterpret_cast<const floatx4*>(&ew[e][(k0 + j) * 16 + o4]);
+            a[j] = fmaf(w[0], y[o4], fmaf(w[1], y[o4 + 1], fmaf(w[2], y[o4 + 2],
+                        fmaf(w[3], y[o4 + 3], a[j]))));
+          }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (k0 + j < E.nk[e]) E.out[e][(size_t)(k0 + j) * N + n] = a[j];
       }
     }
   }
@@ -426,7 +449,7 @@ __global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__
 // x_t and u: Pt = We[:, F:2F] x_t + We[:, 3F:4F] u[g] + be (EdgeModel,
 // gnn.py:100) and Qt = Ws[:, :F] x_t + bs (SModel, gnn.py:136).  One launch for
 // what was bn_apply + graph_mean2 + global_fwd + the next block's class GEMMs.
-constexpr int CG_MAXF = 16, CG_MAXH = 192;
+constexpr int CG_MAXF = 16, CG_MAXH = 192, CG_GW1 = 4096;
 struct ClassGlobalArgs {
   const float* part;  // TModel node_mlp_2's BatchNorm partials (k_mlp_fwd), nb of them
   int nb, F, NC, G, NF;
@@ -445,123 +468,133 @@ struct ClassGlobalArgs {
 };
 
 constexpr int CG_THREADS = 512;
+// (templated on F: every per-channel loop has an exact trip count -- with 16
+// guarded iterations the straight-line code of this 16-block kernel grew past
+// 5000 instructions and it ran at 43 us)
+template <int F>
 __global__ __launch_bounds__(CG_THREADS) void k_class_global_fwd(ClassGlobalArgs A) {
   __shared__ float cf[4][16];
   __shared__ float h[CG_MAXH], z[CG_MAXH], vv[CG_MAXH];
-  __shared__ float scratch[CG_THREADS / 64][2 * CG_MAXF];
-  __shared__ float wt[4 * CG_MAXF * CG_MAXF], ws2[2 * CG_MAXF * CG_MAXF], cu[4 * CG_MAXF],
-      bq[2 * CG_MAXF];
-  const int g = blockIdx.x, t = threadIdx.x, F = A.F, NC = A.NC;
+  __shared__ float scratch[CG_THREADS / 64][2 * F];
+  __shared__ float wt[4 * F * F], ws2[2 * F * F], cu[4 * F], bq[2 * F], rw[F], rs[2];
+  __shared__ float gw1[CG_GW1], gw2[F * CG_MAXH];
+  const int g = blockIdx.x, t = threadIdx.x, NC = A.NC, K = 3 * F;
   const long long NT = (long long)A.G * NC, NS = (long long)A.G * A.NF;
-  if (A.We) {  // next block's weight blocks staged early
-    for (int i = t; i < 4 * F * F; i += CG_THREADS) {
-      const int k = i / F, o = i - k * F;
-      wt[i] = A.We[(size_t)k * 4 * F + F + o];
-    }
-    for (int i = t; i < 2 * F * F; i += CG_THREADS) {
-      const int k = i / F, o = i - k * F;
-      ws2[i] = A.Ws[(size_t)k * 2 * F + o];
-    }
+  const bool gws = A.H * K <= CG_GW1;   // GlobalModel weights staged in LDS (F = 10: 900 + 300)
+  if (gws) {
+    for (int i = t; i < A.H * K; i += CG_THREADS) gw1[i] = A.W1[i];
+    for (int i = t; i < F * A.H; i += CG_THREADS) gw2[i] = A.W2[i];
+  }
+  if (t < F) rw[t] = A.w ? A.w[t] : 1.f;
+  if (A.We) {  // next block's weight blocks
+    for (int i = t; i < 4 * F * F; i += CG_THREADS) wt[i] = A.We[(size_t)(i / F) * 4 * F + F + i % F];
+    for (int i = t; i < 2 * F * F; i += CG_THREADS) ws2[i] = A.Ws[(size_t)(i / F) * 2 * F + i % F];
   }
   bn_stats_part(A.part, A.nb, F, (int)NT, A.gamma, A.beta, A.eps, A.rm, A.rv, A.momentum, A.mu,
                 A.var, g == 0, cf);
-  // the graph's classes: x_t = BN(Yp), and the per-channel sums for its mean
-  float sm[2 * CG_MAXF];
+  float sm[2 * F];
 #pragma unroll
-  for (int o = 0; o < 2 * CG_MAXF; ++o) sm[o] = 0.f;
+  for (int o = 0; o < 2 * F; ++o) sm[o] = 0.f;
+  // the graph's classes: x_t = BN(Yp), and their sum for the x_t mean
   for (int c = t; c < NC; c += CG_THREADS) {
     const long long n = (long long)g * NC + c;
+    float v[F];
 #pragma unroll
-    for (int o = 0; o < CG_MAXF; ++o) {
-      if (o < F) {
-        const float v = (A.Yp[(size_t)o * NT + n] - cf[0][o]) * (cf[1][o] * cf[2][o]) + cf[3][o];
-        A.xt[(size_t)o * NT + n] = v;
-        sm[CG_MAXF + o] += v;
-      }
+    for (int o = 0; o < F; ++o) v[o] = A.Yp[(size_t)o * NT + n];
+#pragma unroll
+    for (int o = 0; o < F; ++o) {
+      v[o] = (v[o] - cf[0][o]) * (cf[1][o] * cf[2][o]) + cf[3][o];
+      A.xt[(size_t)o * NT + n] = v[o];
+      sm[F + o] += v[o];
     }
   }
-  // the graph's x_s: U fibers x F channels of loads in flight per thread (a
-  // serial loop over the 2394 fibers is latency-bound: round 2 measured 39 us)
+  // the graph's x_s: U fibers x F channels of loads in flight per thread
   constexpr int U = 4;
   for (int f0 = 0; f0 < A.NF; f0 += CG_THREADS * U) {
-    float v[U][CG_MAXF];
+    float v[U][F];
 #pragma unroll
     for (int q = 0; q < U; ++q) {
       const int f = f0 + q * CG_THREADS + t;
       const long long n = (long long)g * A.NF + (f < A.NF ? f : 0);
 #pragma unroll
-      for (int o = 0; o < CG_MAXF; ++o) v[q][o] = (o < F && f < A.NF) ? A.xs[(size_t)o * NS + n] : 0.f;
+      for (int o = 0; o < F; ++o) v[q][o] = f < A.NF ? A.xs[(size_t)o * NS + n] : 0.f;
     }
 #pragma unroll
     for (int q = 0; q < U; ++q)
 #pragma unroll
-      for (int o = 0; o < CG_MAXF; ++o) sm[o] += v[q][o];
+      for (int o = 0; o < F; ++o) sm[o] += v[q][o];
   }
   {  // block sums, fixed order: DPP within each wave, then the waves in order
     const int wv = t >> 6, ln = t & 63;
 #pragma unroll
-    for (int i = 0; i < 2 * CG_MAXF; ++i) {
+    for (int i = 0; i < 2 * F; ++i) {
       const float x = wave_sum(sm[i]);
       if (ln == 0) scratch[wv][i] = x;
     }
     __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 2 * CG_MAXF; ++i) {
+    if (t < 2 * F) {
       float x = 0.f;
-      for (int w = 0; w < CG_THREADS / 64; ++w) x += scratch[w][i];
-      sm[i] = x;
+      for (int w = 0; w < CG_THREADS / 64; ++w) x += scratch[w][t];
+      const float m = x / (float)(t < F ? A.NF : NC);
+      h[F + t] = m;   // [u, mean x_s, mean x_t] (gnn.py:220-222)
+      A.means[(size_t)t * A.G + g] = m;
+    } else if (t >= 64 && t < 64 + F) {
+      h[t - 64] = A.u[(size_t)(t - 64) * A.G + g];
     }
-  }
-  const int K = 3 * F;
-  if (t < F) {
-    h[t] = A.u[(size_t)t * A.G + g];
-    const float ms = sm[t] / (float)A.NF, mt = sm[CG_MAXF + t] / (float)NC;
-    h[F + t] = ms;
-    h[2 * F + t] = mt;
-    A.means[(size_t)t * A.G + g] = ms;
-    A.means[(size_t)(F + t) * A.G + g] = mt;
   }
   __syncthreads();
   for (int j = t; j < A.H; j += CG_THREADS) {
     float acc = A.b1[j];
-    for (int k = 0; k < K; ++k) acc = fmaf(A.W1[(size_t)j * K + k], h[k], acc);
+    for (int k = 0; k < K; ++k) acc = fmaf(gws ? gw1[j * K + k] : A.W1[(size_t)j * K + k], h[k], acc);
     z[j] = acc;
     A.Z[(size_t)j * A.G + g] = acc;
   }
   __syncthreads();
-  for (int o = t; o < F; o += CG_THREADS) {
-    float acc = A.b2[o];
-    for (int j = 0; j < A.H; ++j) acc = fmaf(A.W2[(size_t)o * A.H + j], lrelu(z[j]), acc);
-    vv[o] = acc;
-    A.V[(size_t)o * A.G + g] = acc;
+  if (t < F) {
+    float acc = A.b2[t];
+    for (int j = 0; j < A.H; ++j)
+      acc = fmaf(gws ? gw2[t * A.H + j] : A.W2[(size_t)t * A.H + j], lrelu(z[j]), acc);
+    vv[t] = acc;
+    A.V[(size_t)t * A.G + g] = acc;
   }
   __syncthreads();
-  if (t == 0) {
+  if (t == 0) {   // RMSNorm twice (k_rms2_fwd's arithmetic), LDS operands only
     if (!A.w) {
+#pragma unroll
       for (int c = 0; c < F; ++c) h[c] = vv[c];
     } else {
       float s = 0.f;
+#pragma unroll
       for (int c = 0; c < F; ++c) s += vv[c] * vv[c];
       const float a = rsqrtf(s / F + A.reps);
       float s2 = 0.f;
+#pragma unroll
       for (int c = 0; c < F; ++c) {
-        const float q = vv[c] * a * A.w[c];
+        const float q = vv[c] * a * rw[c];
         z[c] = q;
-        A.y1[(size_t)c * A.G + g] = q;
         s2 += q * q;
       }
       const float b = rsqrtf(s2 / F + A.reps);
-      for (int c = 0; c < F; ++c) h[c] = z[c] * b * A.w[c];
-      A.r1[g] = a;
-      A.r2[g] = b;
+#pragma unroll
+      for (int c = 0; c < F; ++c) h[c] = z[c] * b * rw[c];
+      rs[0] = a;
+      rs[1] = b;
     }
   }
   __syncthreads();
-  if (t < F) A.Y[(size_t)t * A.G + g] = h[t];   // u_new
+  if (t < F) {
+    A.Y[(size_t)t * A.G + g] = h[t];   // u_new
+    if (A.w) A.y1[(size_t)t * A.G + g] = z[t];
+  }
+  if (A.w && t == 0) {
+    A.r1[g] = rs[0];
+    A.r2[g] = rs[1];
+  }
   if (!A.We) return;
   // next block: per-graph constant of Pt (u term + bias), then per class
   if (t < 4 * F) {
     float acc = A.be[t];
+#pragma unroll
     for (int o = 0; o < F; ++o) acc = fmaf(A.We[(size_t)t * 4 * F + 3 * F + o], h[o], acc);
     cu[t] = acc;
   } else if (t >= 128 && t - 128 < 2 * F) {
@@ -570,23 +603,21 @@ __global__ __launch_bounds__(CG_THREADS) void k_class_global_fwd(ClassGlobalArgs
   __syncthreads();
   for (int c = t; c < NC; c += CG_THREADS) {
     const long long n = (long long)g * NC + c;
-    float x[CG_MAXF];
+    float x[F];
 #pragma unroll
-    for (int o = 0; o < CG_MAXF; ++o)
-      x[o] = o < F ? (A.Yp[(size_t)o * NT + n] - cf[0][o]) * (cf[1][o] * cf[2][o]) + cf[3][o]
-                   : 0.f;
+    for (int o = 0; o < F; ++o) x[o] = A.Yp[(size_t)o * NT + n];
+#pragma unroll
+    for (int o = 0; o < F; ++o) x[o] = (x[o] - cf[0][o]) * (cf[1][o] * cf[2][o]) + cf[3][o];
     for (int k = 0; k < 4 * F; ++k) {
       float acc = cu[k];
 #pragma unroll
-      for (int o = 0; o < CG_MAXF; ++o)
-        if (o < F) acc = fmaf(wt[k * F + o], x[o], acc);
+      for (int o = 0; o < F; ++o) acc = fmaf(wt[k * F + o], x[o], acc);
       A.Pt[(size_t)k * NT + n] = acc;
     }
     for (int k = 0; k < 2 * F; ++k) {
       float acc = bq[k];
 #pragma unroll
-      for (int o = 0; o < CG_MAXF; ++o)
-        if (o < F) acc = fmaf(ws2[k * F + o], x[o], acc);
+      for (int o = 0; o < F; ++o) acc = fmaf(ws2[k * F + o], x[o], acc);
       A.Qt[(size_t)k * NT + n] = acc;
     }
   }
@@ -1013,7 +1044,12 @@ extern "C" int pfsgnn_target_global_fwd(
   A.xs = xs; A.u = u; A.W1 = gW1; A.b1 = gb1; A.W2 = gW2; A.b2 = gb2; A.w = gw; A.H = gH;
   A.reps = reps; A.means = means; A.Z = gZ; A.V = gV; A.Y = unew; A.y1 = y1; A.r1 = r1; A.r2 = r2;
   A.We = We; A.be = be; A.Ws = Ws; A.bs = bs; A.Pt = Pt; A.Qt = Qt;
-  hipLaunchKernelGGL(k_class_global_fwd, dim3(G), dim3(CG_THREADS), 0, st, A);
+  switch (F) {
+    case 8: hipLaunchKernelGGL(k_class_global_fwd<8>, dim3(G), dim3(CG_THREADS), 0, st, A); break;
+    case 10: hipLaunchKernelGGL(k_class_global_fwd<10>, dim3(G), dim3(CG_THREADS), 0, st, A); break;
+    case 16: hipLaunchKernelGGL(k_class_global_fwd<16>, dim3(G), dim3(CG_THREADS), 0, st, A); break;
+    default: return pf::fail(where, "Fdim must be 8, 10 or 16");
+  }
   return pf::check_launch(where);
 }
 
