@@ -33,6 +33,9 @@ struct InSegs {
   int k0[NM_SEG + 1];  // first row of each block; INT_MAX past the last
   int pg[NM_SEG];      // 1: per-graph block [rows][Gc], node n reads column n / npg
   int npg, Gc;
+  // the same blocks in a K index padded to whole K-steps of 4 (k_mlp_fwd RS):
+  // block s at [kp0[s], kp0[s] + rows[s]), kp0 a multiple of 4, Kp the padded K
+  int kp0[NM_SEG + 1], rows[NM_SEG], Kp;
 };
 
 // gradient output rows: block s covers rows [k0[s], k0[s+1]); p == nullptr drops them
@@ -84,8 +87,14 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 constexpr int PART_LEN = 33;  // BN forward partial: count, mean[16], M2[16]
 
 // ============================================================ forward
-template <int M>
-__global__ __launch_bounds__(256, (M <= 3 ? 2 : 1)) void k_mlp_fwd(InSegs S, int K, int N,
+// RS (the wide MLPs, M >= 5): the chunk's inputs go straight to registers
+// (each lane loads its 4M rows, prefetched one chunk ahead) instead of through
+// the double-buffered LDS copy, so the LDS holds only the weight images
+// (57 KB at M = 7) and two blocks fit a CU: two waves per SIMD to hide the
+// loads and the MFMA dependency latency (one block per CU ran the 100x100
+// SModel MLP at 28 % MFMA utilisation).
+template <int M, bool RS>
+__global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_fwd(InSegs S, int K, int N,
                                                     const float* __restrict__ W1, int ldw1, int H,
                                                     const float* __restrict__ b1,
                                                     const float* __restrict__ W2, int O,
@@ -113,8 +122,31 @@ __global__ __launch_bounds__(256, (M <= 3 ? 2 : 1)) void k_mlp_fwd(InSegs S, int
     float* dst = Xs0 + buf * XSZ;
     for (int k = wu; k < K; k += 4) glds4(in_ptr(S, k, nc, ng, N), dst + k * XS_LD);
   };
-  if ((int)blockIdx.x < nch) issue(blockIdx.x, 0);
-  for (int i = K * XS_LD + t; i < XSZ; i += 256) Xs0[i] = Xs0[XSZ + i] = 0.f;
+  // RS: lane (col, kq) holds rows 4s + kq of its node (the B operand of K-step s)
+  float xq[RS ? 4 * M : 1];
+  // (RS uses the padded K index: every K-step's 4 rows lie in one block, so
+  // the block and its base pointer are wave-uniform scalars per step)
+  auto fetch = [&](int ch) {
+    const int n = ch * 64 + wave * 16 + col;
+    const int nc = n < N ? n : N - 1;
+    const int ng = S.npg ? nc / S.npg : 0;
+#pragma unroll
+    for (int s = 0; s < (RS ? 4 * M : 0); ++s) {
+      int kk = 4 * s;
+      asm volatile("" : "+s"(kk));   // (per fetch: 28 hoisted scalar bases spill)
+      const int sg = (kk >= S.kp0[1]) + (kk >= S.kp0[2]) + (kk >= S.kp0[3]);
+      const int r = kk - S.kp0[sg] + kq;
+      const bool pgs = S.pg[sg] != 0;
+      const float* src = S.p[sg] + (size_t)r * (pgs ? S.Gc : N) + (pgs ? ng : nc);
+      xq[s] = (kk < S.Kp && r < S.rows[sg]) ? *src : 0.f;
+    }
+  };
+  if (RS) {
+    if ((int)blockIdx.x < nch) fetch(blockIdx.x);
+  } else {
+    if ((int)blockIdx.x < nch) issue(blockIdx.x, 0);
+    for (int i = K * XS_LD + t; i < XSZ; i += 256) Xs0[i] = Xs0[XSZ + i] = 0.f;
+  }
   {  // weight images: every load of the thread in flight at once (a load ->
      // store loop would pay one L2 round trip per element)
     float v[M * M], w[M];
@@ -122,8 +154,16 @@ __global__ __launch_bounds__(256, (M <= 3 ? 2 : 1)) void k_mlp_fwd(InSegs S, int
     for (int i = 0; i < M * M; ++i) {
       const int idx = t + 256 * i;
       const int j = idx & 3, l = (idx >> 2) & 63, q = (idx >> 8) % M, mt = (idx >> 8) / M;
-      const int row = 16 * mt + (l & 15), k = 4 * (4 * q + j) + (l >> 4);
-      v[i] = (row < H && k < K) ? W1[(size_t)row * ldw1 + k] : 0.f;
+      const int row = 16 * mt + (l & 15);
+      int k = 4 * (4 * q + j) + (l >> 4);
+      bool kv = k < K;
+      if (RS) {   // padded K index -> weight column (pad rows: 0)
+        const int sg = (k >= S.kp0[1]) + (k >= S.kp0[2]) + (k >= S.kp0[3]);
+        const int r = k - S.kp0[sg];
+        kv = k < S.Kp && r < S.rows[sg];
+        k = S.k0[sg] + r;
+      }
+      v[i] = (row < H && kv) ? W1[(size_t)row * ldw1 + k] : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < M; ++i) {
@@ -142,11 +182,14 @@ __global__ __launch_bounds__(256, (M <= 3 ? 2 : 1)) void k_mlp_fwd(InSegs S, int
 
   float cnt = 0.f, mean[4] = {0.f, 0.f, 0.f, 0.f}, m2[4] = {0.f, 0.f, 0.f, 0.f};
   int it = 0;
+  if (RS) __syncthreads();   // weight images
   for (int ch = blockIdx.x; ch < nch; ch += gridDim.x, ++it) {
     const int buf = it & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of chunk ch landed
-    __syncthreads();                                    // ... and every other wave's
-    if (ch + (int)gridDim.x < nch) issue(ch + gridDim.x, buf ^ 1);
+    if (!RS) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of chunk ch landed
+      __syncthreads();                                    // ... and every other wave's
+      if (ch + (int)gridDim.x < nch) issue(ch + gridDim.x, buf ^ 1);
+    }
     const float* Xs = Xs0 + buf * XSZ;
     const int n = ch * 64 + wave * 16 + col;
     const bool nv = n < N;
@@ -157,59 +200,83 @@ __global__ __launch_bounds__(256, (M <= 3 ? 2 : 1)) void k_mlp_fwd(InSegs S, int
     const floatx4* A1c = A1 + lo;
     const floatx4* A2c = A2 + lo;
     const float* xr = Xs + lo + kq * XS_LD + wave * 16 + col;
-    floatx4 acc[M];
-#pragma unroll
-    for (int mt = 0; mt < M; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
-    // K-step group q: its M weight float4s and 4 input values are read first
-    // (the next group's reads are issued before this group's MFMAs), and the
-    // MFMAs run across the M independent accumulators (no dependent back-to-back)
-    floatx4 an[M];
-    float xn[4];
-#pragma unroll
-    for (int mt = 0; mt < M; ++mt) an[mt] = A1c[mt * M * 64 + lane];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) xn[j] = xr[(4 * j) * XS_LD];
-#pragma unroll
-    for (int q = 0; q < M; ++q) {
-      floatx4 a[M];
-      float x[4];
-#pragma unroll
-      for (int mt = 0; mt < M; ++mt) a[mt] = an[mt];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) x[j] = xn[j];
-      if (q + 1 < M) {
-#pragma unroll
-        for (int mt = 0; mt < M; ++mt) an[mt] = A1c[(mt * M + q + 1) * 64 + lane];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) xn[j] = xr[(4 * (4 * (q + 1) + j)) * XS_LD];
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int mt = 0; mt < M; ++mt) acc[mt] = mfma4(a[mt][j], x[j], acc[mt]);
-    }
+    // the hidden tiles in groups of MG (RS: fewer live accumulators), each
+    // group's layer 1 over all K-steps, then its share of layer 2: the same
+    // per-accumulator order as one group of M
+    constexpr int MG = RS ? 4 : M;
     floatx4 ye = floatx4{0.f, 0.f, 0.f, 0.f}, yo = ye;
-    floatx4 act[M], w2[M];
 #pragma unroll
-    for (int mt = 0; mt < M; ++mt) {
-      w2[mt] = A2c[mt * 64 + lane];
-      const floatx4 bb = *reinterpret_cast<const floatx4*>(B1 + 16 * mt + 4 * kq);
-      const floatx4 z = acc[mt] + bb;
+    for (int g0 = 0; g0 < M; g0 += MG) {
+      constexpr int dummy = 0;
+      (void)dummy;
+      const int GN = (M - g0) < MG ? (M - g0) : MG;   // (compile-time after unrolling)
+      floatx4 acc[MG];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int h = 16 * mt + 4 * kq + r;
-        if (Z && nv && h < H) Z[(size_t)h * N + n] = z[r];
-        act[mt][r] = lrelu(z[r]);
+      for (int i = 0; i < MG; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+      // K-step group q: its weight float4s and 4 input values are read first
+      // (the next group's reads are issued before this group's MFMAs), and the
+      // MFMAs run across the independent accumulators (no dependent back-to-back)
+      floatx4 an[MG];
+      float xn[4];
+#pragma unroll
+      for (int i = 0; i < MG; ++i)
+        if (i < GN) an[i] = A1c[(g0 + i) * M * 64 + lane];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xn[j] = RS ? xq[j] : xr[(4 * j) * XS_LD];
+#pragma unroll
+      for (int q = 0; q < M; ++q) {
+        floatx4 av[MG];
+        float x[4];
+#pragma unroll
+        for (int i = 0; i < MG; ++i) av[i] = an[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[j] = xn[j];
+        if (q + 1 < M) {
+#pragma unroll
+          for (int i = 0; i < MG; ++i)
+            if (i < GN) an[i] = A1c[((g0 + i) * M + q + 1) * 64 + lane];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            xn[j] = RS ? xq[4 * (q + 1) + j] : xr[(4 * (4 * (q + 1) + j)) * XS_LD];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < MG; ++i)
+            if (i < GN) acc[i] = mfma4(av[i][j], x[j], acc[i]);
+      }
+      // RS: the next chunk's rows load while this one finishes (its layer 2 and
+      // epilogue, and the other block's waves on the SIMD)
+      if (RS && g0 + MG >= M && ch + (int)gridDim.x < nch) fetch(ch + gridDim.x);
+      floatx4 act[MG], w2[MG];
+#pragma unroll
+      for (int i = 0; i < MG; ++i) {
+        if (i >= GN) continue;
+        const int mt = g0 + i;
+        w2[i] = A2c[mt * 64 + lane];
+        const floatx4 bb = *reinterpret_cast<const floatx4*>(B1 + 16 * mt + 4 * kq);
+        const floatx4 z = acc[i] + bb;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int h = 16 * mt + 4 * kq + r;
+          if (Z && nv && h < H) Z[(size_t)h * N + n] = z[r];
+          act[i][r] = lrelu(z[r]);
+        }
+      }
+      // two accumulators (even / odd hidden tiles), each in K order
+#pragma unroll
+      for (int i = 0; i < MG; ++i) {
+        if (i >= GN) continue;
+        const int mt = g0 + i;
+        if ((mt & 1) == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            ye = mfma4(w2[i][r], act[i][r], ye);
+            if (i + 1 < GN) yo = mfma4(w2[i + 1][r], act[i + 1][r], yo);
+          }
+        }
       }
     }
-    // two accumulators (even / odd hidden tiles), each in K order
-#pragma unroll
-    for (int mt = 0; mt < M; mt += 2)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        ye = mfma4(w2[mt][r], act[mt][r], ye);
-        if (mt + 1 < M) yo = mfma4(w2[mt + 1][r], act[mt + 1][r], yo);
-      }
     const floatx4 bo = *reinterpret_cast<const floatx4*>(B2 + 4 * kq);
     const floatx4 y = ye + yo + bo;
     if (nv) {
@@ -672,8 +739,25 @@ __global__ __launch_bounds__(256) void k_bn_sums_part(const float* __restrict__ 
         ((scratch[t] + scratch[32 + t]) + scratch[64 + t]) + scratch[96 + t];
 }
 
-template <int M>
-__global__ __launch_bounds__(256, (M <= 3 ? 2 : 1)) void k_mlp_bwd(
+// Row k of the input gradient at one lane's node n (k per lane: the block
+// and its add flag are selected per lane)
+__device__ __forceinline__ void out_row_lane(const OutSegs& S, int k, int n, int N, float v) {
+  float* p = S.p[0];
+  int kb = 0, add = S.add[0];
+  if (k >= S.k0[1]) { p = S.p[1]; kb = S.k0[1]; add = S.add[1]; }
+  if (k >= S.k0[2]) { p = S.p[2]; kb = S.k0[2]; add = S.add[2]; }
+  if (k >= S.k0[3]) { p = S.p[3]; kb = S.k0[3]; add = S.add[3]; }
+  if (!p) return;
+  float* q = p + (size_t)(k - kb) * N + n;
+  *q = add ? *q + v : v;
+}
+
+// RS (the wide MLPs, M >= 5): no LDS staging of the input gradient -- each
+// lane writes its rows straight from the MFMA output layout (64-byte row
+// segments) -- the output tiles in groups of 4 and no prefetch of Z, so the
+// kernel fits 256 registers and 2 blocks per CU (LDS: the weight images only).
+template <int M, bool RS>
+__global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_bwd(
     int K, int N, int H, int O, const float* __restrict__ dY, const float* __restrict__ Yp,
     const float* __restrict__ spart, int nsp, const float* __restrict__ mu,
     const float* __restrict__ var, const float* __restrict__ gamma, float eps,
@@ -778,11 +862,12 @@ __global__ __launch_bounds__(256, (M <= 3 ? 2 : 1)) void k_mlp_bwd(
   if (ch < nch) load(ch);
   for (; ch < nch; ch += gridDim.x) {
     float g[4], y[4], z[4 * M];
+    if (RS && ch != (int)blockIdx.x) load(ch);   // (RS: no prefetch, one set of z registers)
 #pragma unroll
     for (int r = 0; r < 4; ++r) { g[r] = gv[r]; y[r] = yv[r]; }
 #pragma unroll
     for (int s = 0; s < 4 * M; ++s) z[s] = zv[s];
-    if (ch + (int)gridDim.x < nch) load(ch + gridDim.x);
+    if (!RS && ch + (int)gridDim.x < nch) load(ch + gridDim.x);
     const int n = ch * 64 + wave * 16 + col;
     const bool nv = n < N;
     int lo = 0;  // opaque: weight images re-read from LDS per chunk (see k_mlp_fwd)
@@ -793,7 +878,12 @@ __global__ __launch_bounds__(256, (M <= 3 ? 2 : 1)) void k_mlp_bwd(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int o = 4 * kq + r;
-      gp[r] = bn ? gi[r] * (g[r] - k0[r] - (y[r] - mm[r]) * iv[r] * k1[r]) : g[r];
+      if (RS) {   // (the coefficients re-read from LDS: registers are the limit here)
+        gp[r] = bn ? BC[o] * (g[r] - BC[16 + o] - (y[r] - BC[48 + o]) * BC[64 + o] * BC[32 + o])
+                   : g[r];
+      } else {
+        gp[r] = bn ? gi[r] * (g[r] - k0[r] - (y[r] - mm[r]) * iv[r] * k1[r]) : g[r];
+      }
       if (o >= O) gp[r] = 0.f;
       if (bn && dYp && nv && o < O) dYp[(size_t)o * N + n] = gp[r];
     }
@@ -818,7 +908,46 @@ __global__ __launch_bounds__(256, (M <= 3 ? 2 : 1)) void k_mlp_bwd(
         dz[mt][r] *= dlrelu(z[4 * mt + r]);
         if (nv && h < H) dZ[(size_t)h * N + n] = dz[mt][r];
       }
-    if (want_dx) {
+    if (RS && want_dx) {
+      // dX = W1^T dZ by output-tile groups of 4: each group's 64 rows staged in
+      // a 64-row LDS buffer, then written as coalesced 256-byte rows (the
+      // block and add flag wave-uniform per row), as below
+      constexpr int MG = 4;
+#pragma unroll
+      for (int g0 = 0; g0 < M; g0 += MG) {
+        const int GN = (M - g0) < MG ? (M - g0) : MG;
+        floatx4 dx[MG];
+#pragma unroll
+        for (int i = 0; i < MG; ++i) dx[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int mt = 0; mt < M; ++mt) {
+          floatx4 w[MG];   // (no read-ahead: the other block's waves cover the LDS latency)
+#pragma unroll
+          for (int i = 0; i < MG; ++i)
+            if (i < GN) w[i] = T1c[((g0 + i) * M + mt) * 64 + lane];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int i = 0; i < MG; ++i)
+              if (i < GN) dx[i] = mfma4(w[i][r], dz[mt][r], dx[i]);
+        }
+        __syncthreads();                           // the previous group's rows are stored
+#pragma unroll
+        for (int i = 0; i < MG; ++i) {
+          if (i >= GN) continue;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            DXs[(16 * i + 4 * kq + r) * XS_LD + wave * 16 + col] = dx[i][r];
+        }
+        __syncthreads();
+        const int n2 = ch * 64 + lane;
+        const int kend = min(K, 16 * (g0 + GN));
+        if (n2 < N) {
+          for (int k = 16 * g0 + wu; k < kend; k += 4)
+            out_row(outs, k, n2, N, DXs[(k - 16 * g0) * XS_LD + lane]);
+        }
+      }
+    } else if (want_dx) {
       __syncthreads();                             // previous chunk's stores from DXs done
       // dX = W1^T dZ: K-step group mt (hidden tile) over the M output tiles, its
       // weight float4s read one group ahead, independent accumulators back to back
@@ -882,18 +1011,21 @@ int with_tiles(int m, Fn fn) {
   return -1;
 }
 
+// the wide MLPs (M >= 5) stage their inputs in registers (k_mlp_fwd RS)
+bool fwd_rs(int m) { return m >= 5; }
 size_t fwd_lds(int m) {
-  return ((size_t)m * m * 256 + (size_t)m * 256 + 16 * m + 16 + (size_t)2 * 16 * m * XS_LD) * 4;
+  return ((size_t)m * m * 256 + (size_t)m * 256 + 16 * m + 16 +
+          (fwd_rs(m) ? 0 : (size_t)2 * 16 * m * XS_LD)) * 4;
 }
-size_t bwd_lds(int m) {
-  return ((size_t)m * 256 + (size_t)m * m * 256 + 80 + (size_t)16 * m * XS_LD) * 4;
+size_t bwd_lds(int m) {   // (RS: a 64-row input-gradient buffer, one output-tile group)
+  return ((size_t)m * 256 + (size_t)m * m * 256 + 80 + (size_t)16 * (fwd_rs(m) ? 4 : m) * XS_LD) * 4;
 }
 
 // blocks per CU: the M <= 3 kernels fit 2 (registers, LDS), the wider ones
 // run one 4-wave block per CU with up to 512 registers per lane
 int grid_for(int N, int m, size_t lds) {
   const int nch = (N + 63) / 64;
-  const int per_cu = (m <= 3 && lds <= 72 * 1024) ? 2 : 1;
+  const int per_cu = (lds <= 80 * 1024) ? 2 : 1;   // (160 KB of LDS per CU)
   return std::max(1, std::min(nch, 256 * per_cu));
 }
 
@@ -912,8 +1044,13 @@ int make_in(const pfsgnn_seg* segs, int nseg, int N, InSegs& S) {
     S.p[i] = g.x;
     S.k0[i] = k;
     S.pg[i] = g.per_graph ? 1 : 0;
+    S.rows[i] = g.rows;
+    S.kp0[i] = i == 0 ? 0 : S.kp0[i - 1] + ((S.rows[i - 1] + 3) & ~3);
     k += g.rows;
   }
+  S.Kp = S.kp0[nseg - 1] + ((S.rows[nseg - 1] + 3) & ~3);
+  for (int i = nseg; i <= NM_SEG; ++i) S.kp0[i] = INT_MAX;
+  for (int i = nseg; i < NM_SEG; ++i) S.rows[i] = 0;
   for (int i = nseg; i <= NM_SEG; ++i) S.k0[i] = INT_MAX;
   for (int i = nseg; i < NM_SEG; ++i) S.p[i] = S.p[0];
   S.npg = npg;
@@ -933,22 +1070,24 @@ namespace {
 int mlp_fwd_launch(const InSegs& S, int K, int N, const float* W1, int ldw1, int H,
                    const float* b1, const float* W2, int O, const float* b2, float* Z, float* Yp,
                    float* part, int* grid_out, hipStream_t st) {
-  const int m = tiles_for(K, H);
-  if (m <= 0) return -2;
+  int m = tiles_for(K, H);
+  if (m > 0 && fwd_rs(m)) m = tiles_for(S.Kp, H);   // (RS: the padded K must fit the tiles)
+  if (m <= 0 || (fwd_rs(m) && 16 * m < S.Kp)) return -2;
   const size_t lds = fwd_lds(m);
   const int grid = grid_for(N, m, lds);
   *grid_out = grid;
   return with_tiles(m, [&](auto mc) {
     constexpr int MM = decltype(mc)::value;
+    constexpr bool RS = MM >= 5;
     static size_t attr = 0;  // dynamic LDS above the 64 KB default must be opted into
     if (lds > 65536 && attr < lds) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mlp_fwd<MM>),
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mlp_fwd<MM, RS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return -3;
       attr = lds;
     }
-    hipLaunchKernelGGL(k_mlp_fwd<MM>, dim3(grid), dim3(256), lds, st, S, K, N, W1, ldw1, H, b1,
-                       W2, O, b2, Z, Yp, part);
+    hipLaunchKernelGGL((k_mlp_fwd<MM, RS>), dim3(grid), dim3(256), lds, st, S, K, N, W1, ldw1, H,
+                       b1, W2, O, b2, Z, Yp, part);
     return 0;
   });
 }
@@ -1097,12 +1236,12 @@ extern "C" int pfsgnn_mlp_bwd(const float* dY, int N, const float* Yp, const flo
     constexpr int MM = decltype(mc)::value;
     static size_t attr = 0;  // dynamic LDS above the 64 KB default must be opted into
     if (lds > 65536 && attr < lds) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mlp_bwd<MM>),
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mlp_bwd<MM, MM >= 5>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return -3;
       attr = lds;
     }
-    hipLaunchKernelGGL(k_mlp_bwd<MM>, dim3(grid), dim3(256), lds, st, K, N, H, O, dY, Yp, spart,
+    hipLaunchKernelGGL((k_mlp_bwd<MM, MM >= 5>), dim3(grid), dim3(256), lds, st, K, N, H, O, dY, Yp, spart,
                        nsp, mu, var, gamma, eps, dgamma, dbeta, Z, W1, ldw1, W2, dYp, dZ, OS,
                        want_dx);
     return 0;
