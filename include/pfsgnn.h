@@ -451,6 +451,51 @@ int pfsgnn_rows_bn_sums(const float* g, const float* y, int C, long long N, cons
 int pfsgnn_rows_axpby(const float* g, const float* y, int C, long long N, const float* alpha,
                       const float* gam1, const float* gam0, float* out, void* stream);
 
+/* ------------------------------------------------ sliced general graphs
+ * The FUSED edge kernels for general batches (pfsgnn_sliced.hip): the fiber
+ * CSR of pfsgnn_sparse_layout is re-cut into slices of 16 fibers of one graph
+ * (each graph's fibers sorted by degree, descending, stable), the k-th edge of
+ * slice lane j at position base[s] + 16 k + j for k < len[s] (the slice's
+ * largest degree); a fiber with fewer edges leaves padding positions.  Edge
+ * tensors are channel-major [C][EP] over these positions and hold 0 at padding.
+ * Slice s = 4 b + w is wave w of block b = g * ceil(NF/64) + (its 64-fiber
+ * group), so the pfsgnn_sl_* edge ops below run the complete path's grid with
+ * one class split and share its reductions; they take the same arguments and
+ * give the same outputs as the complete-graph op of the same name (G, NF, NC:
+ * the batch's graphs and per-graph node counts), plus the layout.  NC <= 128
+ * classes per graph; Fdim 8, 10, 16.  (Replaces torch_scatter.scatter, x[src],
+ * x[tgt] of gnn.py:100, 136-144, 188-190 for such graphs, fused.) */
+typedef struct {
+  const int* fib;            /* [G*ceil(NF/64)*4*16] global fiber of each slice lane, -1: none */
+  const int* base;           /* [G*ceil(NF/64)*4] first position of each slice */
+  const int* len;            /* [G*ceil(NF/64)*4] steps of each slice (its largest degree) */
+  const unsigned char* cls;  /* [EP] class within its graph of each position, 0xFF: padding */
+  const float* pco;          /* [maxdeg][8] Pebay coefficients (pfsgnn_sliced_fill) */
+  long long EP;              /* positions = edge-tensor columns, padding included */
+  long long E;               /* edges */
+  int maxdeg;                /* largest fiber degree */
+} pfsgnn_sliced_t;
+size_t pfsgnn_sliced_plan_ws_bytes(int G, int NF);
+/* From fib_ptr [G*NF+1] (pfsgnn_sparse_layout): the slice lanes `fib`, lengths
+ * `len`, first positions `base`, slot_of [G*NF] (the slice lane 16 s + j of
+ * each fiber) and, in info (device int64[2]), EP and maxdeg. */
+int pfsgnn_sliced_plan(const int* fib_ptr, int G, int NF, int* fib, int* base, int* len,
+                       int* slot_of, long long* info, void* ws, size_t ws_bytes, void* stream);
+/* From the sparse layout (src_p, tgt_p, user_of, fib_ptr) and the plan: cls [EP]
+ * and pos_user [EP] (the caller's edge at each position, -1 at padding), pco
+ * [maxdeg*8].  NC < 255. */
+int pfsgnn_sliced_fill(const int* src_p, const int* tgt_p, const int* user_of, const int* fib_ptr,
+                       long long E, int NF, int NC, const int* slot_of, const int* base,
+                       long long EP, int maxdeg, unsigned char* cls, int* pos_user, float* pco,
+                       void* stream);
+/* caller-order edge rows [E][F] -> a slot tensor [F][EP] (0 at padding), and
+ * back (dst [E][F] if rowmajor else [F][E]; with sc/sh the lazy affine first) */
+int pfsgnn_edges_to_slots(const float* src, long long E, long long EP, int F, const int* pos_user,
+                          float* dst, void* stream);
+int pfsgnn_edges_from_slots(const float* y, const float* sc, const float* sh, long long E,
+                            long long EP, int F, const int* pos_user, int rowmajor, float* dst,
+                            void* stream);
+
 /* ---------------------------------------------------------------- edge ops */
 
 /* EdgeModel per-edge MLP (gnn.py:99-101 with the first Linear split):
@@ -540,6 +585,61 @@ int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_tot, const 
                         const float* W1, const float* W2, float* dW1, float* dW2, float* db2,
                         float* gxe, float* GzEs, float* GzEt, float* g_xs, float* g_xt,
                         float* Vu, void* ws, size_t ws_bytes, void* stream);
+
+/* The edge ops above on a sliced general batch (pfsgnn_sliced_t): arguments
+ * and outputs as the op of the same name; edge tensors are [C][sl->EP]; the
+ * EdgeModel BatchNorm counts sl->E edges; `tmask` has pfsgnn_sl_tmask_bytes. */
+int pfsgnn_sl_edge_mlp_fwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                           const float* xe, const float* xsc, const float* xsh, const float* Ps,
+                           const float* Pt, const float* W1, const float* W2, const float* b2,
+                           float* y, float* mu, float* var, void* ws, size_t ws_bytes,
+                           void* stream);
+int pfsgnn_sl_edge_mlp_fwd_bn(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                              const float* xe, const float* xsc, const float* xsh,
+                              const float* Ps, const float* Pt, const float* W1, const float* W2,
+                              const float* b2, float* y, float* mu, float* var,
+                              const float* gamma, const float* beta, float* rm, float* rv,
+                              float momentum, float eps, float* sc, float* sh, float* inv1,
+                              float* inv2, void* ws, size_t ws_bytes, void* stream);
+int pfsgnn_sl_source_fwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F, const float* y,
+                         const float* sc, const float* sh, const float* Qt, const float* Ws1,
+                         const float* Ws2, const float* bs2, float* mom, float* hs, void* ws,
+                         size_t ws_bytes, void* stream);
+size_t pfsgnn_sl_tmask_bytes(const pfsgnn_sliced_t* sl, int F);
+int pfsgnn_sl_target_fwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F, const float* y,
+                         const float* sc, const float* sh, const float* Rs, const float* Wt1,
+                         float* hsum, const float* Wt2, const float* bt2, float bscale,
+                         float* agg, unsigned char* tmask, void* ws, size_t ws_bytes,
+                         void* stream);
+int pfsgnn_sl_target_bwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F, const float* y,
+                         const float* sc, const float* sh, const float* Rs, const float* Wt1,
+                         const float* g_hsum, float* GzT, float* dWt1, float* gxe, float* g_xs,
+                         const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream);
+int pfsgnn_sl_source_bwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F, const float* y,
+                         const float* sc, const float* sh, const float* Qt, const float* Ws1,
+                         const float* Ws2, const float* bs2, const float* mean,
+                         const float* coef, const float* Rs, const float* Wt1,
+                         const float* g_hsum, const float* g_next, const float* mu1,
+                         const float* inv1, float* g_tot, float* GzS, float* dWs1, float* dWs2,
+                         float* dbs2, float* Sg, float* Sgx, float* g_xt,
+                         const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream);
+int pfsgnn_sl_source_bwd_bn(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                            const float* y, const float* sc, const float* sh, const float* Qt,
+                            const float* Ws1, const float* Ws2, const float* bs2,
+                            const float* mean, const float* coef, const float* Rs,
+                            const float* Wt1, const float* g_hsum, const float* g_next,
+                            const float* mu1, const float* inv1, const float* var1,
+                            const float* gamma, long long n, float eps, float* g_tot, float* GzS,
+                            float* dWs1, float* dWs2, float* dbs2, float* alpha, float* gam0,
+                            float* gam1, float* dgamma, float* dbeta, float* g_xt,
+                            const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream);
+int pfsgnn_sl_edge_mlp_bwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                           const float* g_tot, const float* alpha, const float* gam0,
+                           const float* gam1, const float* y, const float* xe, const float* xsc,
+                           const float* xsh, const float* Ps, const float* Pt, const float* W1,
+                           const float* W2, float* dW1, float* dW2, float* db2, float* gxe,
+                           float* GzEs, float* GzEt, float* g_xs, float* g_xt, float* Vu,
+                           void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- loss
  * train.py:29-80: decoder_e (gnn.py:307) + softplus + softfloor (train.py:21)

@@ -1385,6 +1385,24 @@ EdgeGeo geo_mfma(int G, int NF, int NC) {
 EdgeGeo geo_for(int G, int NF, int NC) {
   return use_mfma() ? geo_mfma(G, NF, NC) : make_geo(G, NF, NC);
 }
+// a sliced general batch (include/pfsgnn.h pfsgnn_sliced_t): its kernel view
+pfm::SlGeo sl_of(const pfsgnn_sliced_t& s) {
+  return pfm::SlGeo{s.fib, s.base, s.len, s.cls, s.pco, s.EP, s.E, s.maxdeg};
+}
+int check_sliced(const char* where, const pfsgnn_sliced_t* sl, int NC, int F) {
+  if (!sl) return 0;
+  if (sl->EP * F * 4 >= (1ll << 32)) return pf::fail(where, "edge tensor exceeds 4 GiB (split the batch)");
+  if (!sl->fib || !sl->base || !sl->len || !sl->cls || !sl->pco || sl->EP <= 0 || sl->E <= 0 ||
+      sl->EP < sl->E)
+    return pf::fail(where, "bad sliced layout");
+  if (NC > pfm::SL_MAX_NC) return pf::fail(where, "sliced layout: NC > 128 classes per graph");
+  if (mf_bfy()) return pf::fail(where, "sliced layout: bf16 edge-state paths are not supported");
+  return 0;
+}
+// the grid of an edge op: the complete path's, or the sliced batch's (KS = 1)
+EdgeGeo geo_of(int G, int NF, int NC, const pfsgnn_sliced_t* sl) {
+  return sl ? pfm::sl_geo(G, NF, NC, sl_of(*sl)) : geo_for(G, NF, NC);
+}
 
 }  // namespace
 
@@ -1436,16 +1454,29 @@ extern "C" size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F) {
   return (std::max(std::max(edge, node), lay) + 64 * 16) * sizeof(float) + 16 * 256;
 }
 
-static int edge_mlp_fwd_impl(int G, int NF, int NC, int F, const float* xe, const float* xsc,
-                             const float* xsh, const float* Ps, const float* Pt, const float* W1,
-                             const float* W2, const float* b2, float* y, float* mu, float* var,
-                             Bn2Args bn, void* ws, size_t ws_bytes, void* stream) {
+static int edge_mlp_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                             const float* xe, const float* xsc, const float* xsh, const float* Ps,
+                             const float* Pt, const float* W1, const float* W2, const float* b2,
+                             float* y, float* mu, float* var, Bn2Args bn, void* ws,
+                             size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_edge_mlp_fwd", G, NF, NC, F)) return rc;
+  if (int rc = check_sliced("pfsgnn_edge_mlp_fwd", sl, NC, F)) return rc;
   PF_REQUIRE(xe && Ps && Pt && W1 && W2 && b2 && y && mu && var, "pfsgnn_edge_mlp_fwd", "null");
-  const EdgeGeo geo = geo_for(G, NF, NC);
+  const EdgeGeo geo = geo_of(G, NF, NC, sl);
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
   hipStream_t st = as_stream(stream);
   float* part = w.take((size_t)geo.nblocks * (1 + 2 * F));
+  if (sl) {
+    PF_REQUIRE(part, "pfsgnn_edge_mlp_fwd", "workspace too small");
+    { pf::Timer tm_("edge_mlp_fwd", st);
+    if (int rc = pfm::sl_edge_mlp_fwd(geo, sl_of(*sl), F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part,
+                                      mf_prec(0), st))
+      return rc;
+    tm_.end(); }
+    hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(256), 0, st, part, geo.nblocks, F, sl->E,
+                       mu, var, bn);
+    return pf::check_launch("pfsgnn_edge_mlp_fwd");
+  }
   if (use_mfma()) {
     PF_REQUIRE(part, "pfsgnn_edge_mlp_fwd", "workspace too small");
     { pf::Timer tm_("edge_mlp_fwd", st);
@@ -1472,8 +1503,8 @@ extern "C" int pfsgnn_edge_mlp_fwd(int G, int NF, int NC, int F, const float* xe
                                    const float* Pt, const float* W1, const float* W2,
                                    const float* b2, float* y, float* mu, float* var, void* ws,
                                    size_t ws_bytes, void* stream) {
-  return edge_mlp_fwd_impl(G, NF, NC, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, mu, var, Bn2Args{},
-                           ws, ws_bytes, stream);
+  return edge_mlp_fwd_impl(nullptr, G, NF, NC, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, mu, var,
+                           Bn2Args{}, ws, ws_bytes, stream);
 }
 
 extern "C" int pfsgnn_edge_mlp_fwd_bn(int G, int NF, int NC, int F, const float* xe,
@@ -1486,21 +1517,55 @@ extern "C" int pfsgnn_edge_mlp_fwd_bn(int G, int NF, int NC, int F, const float*
                                       void* stream) {
   PF_REQUIRE(gamma && beta && sc && sh && inv1 && inv2 && (!rm == !rv),
              "pfsgnn_edge_mlp_fwd_bn", "null");
-  return edge_mlp_fwd_impl(G, NF, NC, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, mu, var,
+  return edge_mlp_fwd_impl(nullptr, G, NF, NC, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, mu, var,
                            Bn2Args{gamma, beta, rm, rv, momentum, eps, sc, sh, inv1, inv2}, ws,
                            ws_bytes, stream);
 }
 
-extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
-                                 const float* sh, const float* Qt, const float* Ws1,
-                                 const float* Ws2, const float* bs2, float* mom, float* hs,
-                                 void* ws, size_t ws_bytes, void* stream) {
+extern "C" int pfsgnn_sl_edge_mlp_fwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                                      const float* xe, const float* xsc, const float* xsh,
+                                      const float* Ps, const float* Pt, const float* W1,
+                                      const float* W2, const float* b2, float* y, float* mu,
+                                      float* var, void* ws, size_t ws_bytes, void* stream) {
+  PF_REQUIRE(sl, "pfsgnn_sl_edge_mlp_fwd", "null layout");
+  return edge_mlp_fwd_impl(sl, G, NF, NC, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, mu, var,
+                           Bn2Args{}, ws, ws_bytes, stream);
+}
+
+extern "C" int pfsgnn_sl_edge_mlp_fwd_bn(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                                         const float* xe, const float* xsc, const float* xsh,
+                                         const float* Ps, const float* Pt, const float* W1,
+                                         const float* W2, const float* b2, float* y, float* mu,
+                                         float* var, const float* gamma, const float* beta,
+                                         float* rm, float* rv, float momentum, float eps,
+                                         float* sc, float* sh, float* inv1, float* inv2, void* ws,
+                                         size_t ws_bytes, void* stream) {
+  PF_REQUIRE(sl && gamma && beta && sc && sh && inv1 && inv2 && (!rm == !rv),
+             "pfsgnn_sl_edge_mlp_fwd_bn", "null");
+  return edge_mlp_fwd_impl(sl, G, NF, NC, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, mu, var,
+                           Bn2Args{gamma, beta, rm, rv, momentum, eps, sc, sh, inv1, inv2}, ws,
+                           ws_bytes, stream);
+}
+
+static int source_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                           const float* y, const float* sc, const float* sh, const float* Qt,
+                           const float* Ws1, const float* Ws2, const float* bs2, float* mom,
+                           float* hs, void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_source_fwd", G, NF, NC, F)) return rc;
+  if (int rc = check_sliced("pfsgnn_source_fwd", sl, NC, F)) return rc;
   PF_REQUIRE(y && Qt && Ws1 && Ws2 && bs2 && mom && hs, "pfsgnn_source_fwd", "null");
-  const EdgeGeo geo = geo_for(G, NF, NC);
+  const EdgeGeo geo = geo_of(G, NF, NC, sl);
   const int C = 2 * F;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
   hipStream_t st = as_stream(stream);
+  if (sl) {   // moments straight to mom / hs (per-fiber counts: the degrees)
+    pf::Timer tm_("source_fwd", st);
+    if (int rc = pfm::sl_source_fwd(geo, sl_of(*sl), F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs,
+                                    mf_prec(1), st))
+      return rc;
+    tm_.end();
+    return pf::check_launch("pfsgnn_source_fwd");
+  }
   if (use_mfma() && NC <= 256 && sfwd_tiles()) {
     pf::Timer tm_("source_fwd", st);
     if (int rc = pfm::source_fwd_tiles(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs, mf_prec(1),
@@ -1531,24 +1596,53 @@ extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, c
   return pf::check_launch("pfsgnn_source_fwd");
 }
 
+extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
+                                 const float* sh, const float* Qt, const float* Ws1,
+                                 const float* Ws2, const float* bs2, float* mom, float* hs,
+                                 void* ws, size_t ws_bytes, void* stream) {
+  return source_fwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs, ws,
+                         ws_bytes, stream);
+}
+
+extern "C" int pfsgnn_sl_source_fwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                                    const float* y, const float* sc, const float* sh,
+                                    const float* Qt, const float* Ws1, const float* Ws2,
+                                    const float* bs2, float* mom, float* hs, void* ws,
+                                    size_t ws_bytes, void* stream) {
+  PF_REQUIRE(sl, "pfsgnn_sl_source_fwd", "null layout");
+  return source_fwd_impl(sl, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs, ws, ws_bytes,
+                         stream);
+}
+
 extern "C" size_t pfsgnn_tmask_bytes(int G, int NF, int NC, int F) {
   if (G <= 0 || NF <= 0 || NC <= 0 || F <= 0 || 2 * F > 32 || !use_mfma()) return 0;
   return (size_t)G * NF * NC * 4;   // one byte per (edge, lane group), pfsgnn_mfma.hip mask_bits
 }
 
-extern "C" int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
-                                 const float* sh, const float* Rs, const float* Wt1, float* hsum,
-                                 const float* Wt2, const float* bt2, float bscale, float* agg,
-                                 unsigned char* tmask, void* ws, size_t ws_bytes, void* stream) {
+extern "C" size_t pfsgnn_sl_tmask_bytes(const pfsgnn_sliced_t* sl, int F) {
+  if (!sl || sl->EP <= 0 || F <= 0 || 2 * F > 32) return 0;
+  return (size_t)sl->EP * 4;   // per position, as pfsgnn_tmask_bytes per edge
+}
+
+static int target_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                           const float* y, const float* sc, const float* sh, const float* Rs,
+                           const float* Wt1, float* hsum, const float* Wt2, const float* bt2,
+                           float bscale, float* agg, unsigned char* tmask, void* ws,
+                           size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_target_fwd", G, NF, NC, F)) return rc;
+  if (int rc = check_sliced("pfsgnn_target_fwd", sl, NC, F)) return rc;
   PF_REQUIRE(y && Rs && Wt1 && hsum, "pfsgnn_target_fwd", "null");
-  const EdgeGeo geo = geo_for(G, NF, NC);
+  const EdgeGeo geo = geo_of(G, NF, NC, sl);
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
   float* part = w.take((size_t)G * geo.NFG * NC * 2 * F);
   PF_REQUIRE(part, "pfsgnn_target_fwd", "workspace too small");
   hipStream_t st = as_stream(stream);
   { pf::Timer tm_("target_fwd", st);
-  if (use_mfma()) {
+  if (sl) {
+    if (int rc = pfm::sl_target_fwd(geo, sl_of(*sl), F, y, sc, sh, Rs, Wt1, part, tmask,
+                                    mf_prec(1), st))
+      return rc;
+  } else if (use_mfma()) {
     if (int rc = pfm::target_fwd(geo, F, y, sc, sh, Rs, Wt1, part, tmask, mf_prec(1), st)) return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
@@ -1563,14 +1657,34 @@ extern "C" int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, c
   return pf::check_launch("pfsgnn_target_fwd");
 }
 
-extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
-                                 const float* sh, const float* Rs, const float* Wt1,
-                                 const float* g_hsum, float* GzT, float* dWt1, float* gxe,
-                                 float* g_xs, const unsigned char* tmask, void* ws,
-                                 size_t ws_bytes, void* stream) {
+extern "C" int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, const float* sc,
+                                 const float* sh, const float* Rs, const float* Wt1, float* hsum,
+                                 const float* Wt2, const float* bt2, float bscale, float* agg,
+                                 unsigned char* tmask, void* ws, size_t ws_bytes, void* stream) {
+  return target_fwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Rs, Wt1, hsum, Wt2, bt2, bscale, agg,
+                         tmask, ws, ws_bytes, stream);
+}
+
+extern "C" int pfsgnn_sl_target_fwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                                    const float* y, const float* sc, const float* sh,
+                                    const float* Rs, const float* Wt1, float* hsum,
+                                    const float* Wt2, const float* bt2, float bscale, float* agg,
+                                    unsigned char* tmask, void* ws, size_t ws_bytes,
+                                    void* stream) {
+  PF_REQUIRE(sl, "pfsgnn_sl_target_fwd", "null layout");
+  return target_fwd_impl(sl, G, NF, NC, F, y, sc, sh, Rs, Wt1, hsum, Wt2, bt2, bscale, agg, tmask,
+                         ws, ws_bytes, stream);
+}
+
+static int target_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                           const float* y, const float* sc, const float* sh, const float* Rs,
+                           const float* Wt1, const float* g_hsum, float* GzT, float* dWt1,
+                           float* gxe, float* g_xs, const unsigned char* tmask, void* ws,
+                           size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_target_bwd", G, NF, NC, F)) return rc;
+  if (int rc = check_sliced("pfsgnn_target_bwd", sl, NC, F)) return rc;
   PF_REQUIRE(y && Rs && Wt1 && g_hsum && GzT && dWt1, "pfsgnn_target_bwd", "null");
-  const EdgeGeo geo = geo_for(G, NF, NC);
+  const EdgeGeo geo = geo_of(G, NF, NC, sl);
   const int C = 2 * F;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
   hipStream_t st = as_stream(stream);
@@ -1578,11 +1692,15 @@ extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, c
   const bool defer = part != nullptr;
   if (!defer) part = w.take((size_t)geo.nblocks * C * F);
   float* gz = fiber_dst(geo, C, GzT, w);
-  const float* ghT = use_mfma() ? g_hsum
-                                : class_rows(g_hsum, C, geo, w, st);
+  const float* ghT = (sl || use_mfma()) ? g_hsum
+                                       : class_rows(g_hsum, C, geo, w, st);
   PF_REQUIRE(part && gz && ghT, "pfsgnn_target_bwd", "workspace too small");
   { pf::Timer tm_("target_bwd", st);
-  if (use_mfma()) {
+  if (sl) {
+    if (int rc = pfm::sl_target_bwd(geo, sl_of(*sl), F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part,
+                                    tmask, mf_prec(1), st))
+      return rc;
+  } else if (use_mfma()) {
     if (int rc = pfm::target_bwd(geo, F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part, tmask,
                                  mf_prec(1), st))
       return rc;
@@ -1600,6 +1718,26 @@ extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, c
   if (defer) pf::defer_push(&rd, 1);
   else launch_reduce_multi(&rd, 1, st);
   return pf::check_launch("pfsgnn_target_bwd");
+}
+
+extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
+                                 const float* sh, const float* Rs, const float* Wt1,
+                                 const float* g_hsum, float* GzT, float* dWt1, float* gxe,
+                                 float* g_xs, const unsigned char* tmask, void* ws,
+                                 size_t ws_bytes, void* stream) {
+  return target_bwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Rs, Wt1, g_hsum, GzT, dWt1, gxe, g_xs,
+                         tmask, ws, ws_bytes, stream);
+}
+
+extern "C" int pfsgnn_sl_target_bwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                                    const float* y, const float* sc, const float* sh,
+                                    const float* Rs, const float* Wt1, const float* g_hsum,
+                                    float* GzT, float* dWt1, float* gxe, float* g_xs,
+                                    const unsigned char* tmask, void* ws, size_t ws_bytes,
+                                    void* stream) {
+  PF_REQUIRE(sl, "pfsgnn_sl_target_bwd", "null layout");
+  return target_bwd_impl(sl, G, NF, NC, F, y, sc, sh, Rs, Wt1, g_hsum, GzT, dWt1, gxe, g_xs, tmask,
+                         ws, ws_bytes, stream);
 }
 
 // The edge BatchNorm's two gradient sums straight from source_bwd's block
@@ -1642,14 +1780,14 @@ __global__ __launch_bounds__(256) void k_bn2_coef_part(const float* __restrict__
   }
 }
 
-static int source_bwd_impl(int G, int NF, int NC, int F, const float* y, const float* sc,
-                           const float* sh, const float* Qt, const float* Ws1, const float* Ws2,
-                           const float* bs2, const float* mean, const float* coef, const float* Rs,
-                           const float* Wt1, const float* g_hsum, const float* g_next,
-                           const float* mu1, const float* inv1, float* g_tot, float* GzS,
-                           float* dWs1, float* dWs2, float* dbs2, float* Sg, float* Sgx,
-                           const Bn2Bwd* bb, float* g_xt, const unsigned char* tmask, void* ws,
-                           size_t ws_bytes, void* stream);
+static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                           const float* y, const float* sc, const float* sh, const float* Qt,
+                           const float* Ws1, const float* Ws2, const float* bs2, const float* mean,
+                           const float* coef, const float* Rs, const float* Wt1,
+                           const float* g_hsum, const float* g_next, const float* mu1,
+                           const float* inv1, float* g_tot, float* GzS, float* dWs1, float* dWs2,
+                           float* dbs2, float* Sg, float* Sgx, const Bn2Bwd* bb, float* g_xt,
+                           const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream);
 
 extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                                  const float* sh, const float* Qt, const float* Ws1,
@@ -1660,9 +1798,9 @@ extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, c
                                  float* dWs2, float* dbs2, float* Sg, float* Sgx, float* g_xt,
                                  const unsigned char* tmask, void* ws, size_t ws_bytes,
                                  void* stream) {
-  return source_bwd_impl(G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, g_hsum,
-                         g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, Sg, Sgx, nullptr, g_xt,
-                         tmask, ws, ws_bytes, stream);
+  return source_bwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+                         g_hsum, g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, Sg, Sgx, nullptr,
+                         g_xt, tmask, ws, ws_bytes, stream);
 }
 
 extern "C" int pfsgnn_source_bwd_bn(int G, int NF, int NC, int F, const float* y, const float* sc,
@@ -1679,27 +1817,61 @@ extern "C" int pfsgnn_source_bwd_bn(int G, int NF, int NC, int F, const float* y
   PF_REQUIRE(mu1 && inv1 && var1 && gamma && n > 0 && alpha && gam0 && gam1 && dgamma && dbeta,
              "pfsgnn_source_bwd_bn", "null");
   const Bn2Bwd bb{gamma, mu1, var1, n, eps, alpha, gam0, gam1, dgamma, dbeta};
-  return source_bwd_impl(G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, g_hsum,
-                         g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, nullptr, nullptr, &bb,
+  return source_bwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+                         g_hsum, g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, nullptr, nullptr,
+                         &bb, g_xt, tmask, ws, ws_bytes, stream);
+}
+
+extern "C" int pfsgnn_sl_source_bwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                                    const float* y, const float* sc, const float* sh,
+                                    const float* Qt, const float* Ws1, const float* Ws2,
+                                    const float* bs2, const float* mean, const float* coef,
+                                    const float* Rs, const float* Wt1, const float* g_hsum,
+                                    const float* g_next, const float* mu1, const float* inv1,
+                                    float* g_tot, float* GzS, float* dWs1, float* dWs2,
+                                    float* dbs2, float* Sg, float* Sgx, float* g_xt,
+                                    const unsigned char* tmask, void* ws, size_t ws_bytes,
+                                    void* stream) {
+  PF_REQUIRE(sl, "pfsgnn_sl_source_bwd", "null layout");
+  return source_bwd_impl(sl, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+                         g_hsum, g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, Sg, Sgx, nullptr,
                          g_xt, tmask, ws, ws_bytes, stream);
 }
 
-static int source_bwd_impl(int G, int NF, int NC, int F, const float* y, const float* sc,
-                           const float* sh, const float* Qt, const float* Ws1, const float* Ws2,
-                           const float* bs2, const float* mean, const float* coef, const float* Rs,
-                           const float* Wt1, const float* g_hsum, const float* g_next,
-                           const float* mu1, const float* inv1, float* g_tot, float* GzS,
-                           float* dWs1, float* dWs2, float* dbs2, float* Sg, float* Sgx,
-                           const Bn2Bwd* bb, float* g_xt, const unsigned char* tmask, void* ws,
-                           size_t ws_bytes, void* stream) {
+extern "C" int pfsgnn_sl_source_bwd_bn(
+    const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F, const float* y, const float* sc,
+    const float* sh, const float* Qt, const float* Ws1, const float* Ws2, const float* bs2,
+    const float* mean, const float* coef, const float* Rs, const float* Wt1, const float* g_hsum,
+    const float* g_next, const float* mu1, const float* inv1, const float* var1,
+    const float* gamma, long long n, float eps, float* g_tot, float* GzS, float* dWs1,
+    float* dWs2, float* dbs2, float* alpha, float* gam0, float* gam1, float* dgamma, float* dbeta,
+    float* g_xt, const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream) {
+  PF_REQUIRE(sl && mu1 && inv1 && var1 && gamma && n > 0 && alpha && gam0 && gam1 && dgamma &&
+                 dbeta,
+             "pfsgnn_sl_source_bwd_bn", "null");
+  const Bn2Bwd bb{gamma, mu1, var1, n, eps, alpha, gam0, gam1, dgamma, dbeta};
+  return source_bwd_impl(sl, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+                         g_hsum, g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, nullptr, nullptr,
+                         &bb, g_xt, tmask, ws, ws_bytes, stream);
+}
+
+static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                           const float* y, const float* sc, const float* sh, const float* Qt,
+                           const float* Ws1, const float* Ws2, const float* bs2, const float* mean,
+                           const float* coef, const float* Rs, const float* Wt1,
+                           const float* g_hsum, const float* g_next, const float* mu1,
+                           const float* inv1, float* g_tot, float* GzS, float* dWs1, float* dWs2,
+                           float* dbs2, float* Sg, float* Sgx, const Bn2Bwd* bb, float* g_xt,
+                           const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_source_bwd", G, NF, NC, F)) return rc;
+  if (int rc = check_sliced("pfsgnn_source_bwd", sl, NC, F)) return rc;
   PF_REQUIRE(y && Qt && Ws1 && Ws2 && bs2 && mean && coef && g_tot && GzS && dWs1 && dWs2 && dbs2,
              "pfsgnn_source_bwd", "null");
   PF_REQUIRE((Rs == nullptr) == (Wt1 == nullptr) && (Rs == nullptr) == (g_hsum == nullptr),
              "pfsgnn_source_bwd", "Rs, Wt1, g_hsum must be given together");
   PF_REQUIRE(!mu1 || (inv1 && ((Sg && Sgx) || bb)), "pfsgnn_source_bwd",
              "mu1 needs inv1, Sg, Sgx");
-  const EdgeGeo geo = geo_for(G, NF, NC);
+  const EdgeGeo geo = geo_of(G, NF, NC, sl);
   const int C = 2 * F;
   const size_t nb = geo.nblocks;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
@@ -1710,13 +1882,18 @@ static int source_bwd_impl(int G, int NF, int NC, int F, const float* y, const f
   float* pCol = w.take((size_t)G * geo.NFG * NC * C);
   float* pBN = w.take(nb * 2 * F);
   hipStream_t st = as_stream(stream);
-  const bool mfma = use_mfma();
+  const bool mfma = sl || use_mfma();
   const float* QtT = mfma ? Qt : class_rows(Qt, C, geo, w, st);
   const float* ghT = mfma ? g_hsum : class_rows(g_hsum, C, geo, w, st);
   PF_REQUIRE(pW2 && pW1 && pCol && pBN && QtT && (ghT || !g_hsum), "pfsgnn_source_bwd",
              "workspace too small");
   { pf::Timer tm_("source_bwd", st);
-  if (mfma) {
+  if (sl) {
+    if (int rc = pfm::sl_source_bwd(geo, sl_of(*sl), F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef,
+                                    Rs, Wt1, ghT, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN,
+                                    tmask, mf_prec(1), st))
+      return rc;
+  } else if (mfma) {
     if (int rc = pfm::source_bwd(geo, F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT,
                                  g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask,
                                  mf_prec(1), st))
@@ -1778,19 +1955,19 @@ extern "C" int pfsgnn_edge_bn_grad_sums(int G, int NF, int NC, int F, const floa
   return pf::check_launch("pfsgnn_edge_bn_grad_sums");
 }
 
-extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_tot,
-                                   const float* alpha, const float* gam0, const float* gam1,
-                                   const float* y, const float* xe, const float* xsc,
-                                   const float* xsh, const float* Ps, const float* Pt,
-                                   const float* W1, const float* W2, float* dW1, float* dW2,
-                                   float* db2, float* gxe, float* GzEs, float* GzEt,
-                                   float* g_xs, float* g_xt, float* Vu, void* ws,
-                                   size_t ws_bytes, void* stream) {
+static int edge_mlp_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                             const float* g_tot, const float* alpha, const float* gam0,
+                             const float* gam1, const float* y, const float* xe, const float* xsc,
+                             const float* xsh, const float* Ps, const float* Pt, const float* W1,
+                             const float* W2, float* dW1, float* dW2, float* db2, float* gxe,
+                             float* GzEs, float* GzEt, float* g_xs, float* g_xt, float* Vu,
+                             void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_edge_mlp_bwd", G, NF, NC, F)) return rc;
+  if (int rc = check_sliced("pfsgnn_edge_mlp_bwd", sl, NC, F)) return rc;
   PF_REQUIRE(g_tot && alpha && gam0 && gam1 && y && xe && Ps && Pt && W1 && W2 && dW1 && dW2 &&
                  db2 && GzEs && GzEt,
              "pfsgnn_edge_mlp_bwd", "null");
-  const EdgeGeo geo = geo_for(G, NF, NC);
+  const EdgeGeo geo = geo_of(G, NF, NC, sl);
   const int H = 4 * F;
   const size_t nb = geo.nblocks;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
@@ -1801,7 +1978,15 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
   float* pCol = w.take((size_t)G * geo.NFG * NC * H);
   float* gs = fiber_dst(geo, H, GzEs, w);
   hipStream_t st = as_stream(stream);
-  if (use_mfma()) {
+  if (sl) {
+    PF_REQUIRE(pW2 && pW1 && pCol && gs, "pfsgnn_edge_mlp_bwd", "workspace too small");
+    pf::Timer tm_("edge_mlp_bwd", st);
+    if (int rc = pfm::sl_edge_mlp_bwd(geo, sl_of(*sl), F, g_tot, alpha, gam0, gam1, y, xe, xsc,
+                                      xsh, Ps, Pt, W1, W2, gxe, gs, pW2, pW1, pCol, mf_prec(0),
+                                      st))
+      return rc;
+    tm_.end();
+  } else if (use_mfma()) {
     PF_REQUIRE(pW2 && pW1 && pCol && gs, "pfsgnn_edge_mlp_bwd", "workspace too small");
     pf::Timer tm_("edge_mlp_bwd", st);
     if (int rc = pfm::edge_mlp_bwd(geo, F, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1,
@@ -1838,4 +2023,31 @@ extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_
                            lin_t_add(g_xt ? W1 : nullptr, 4 * F, F, F, g_xt, geo.NT), Lu, st))
     return rc;
   return pf::check_launch("pfsgnn_edge_mlp_bwd");
+}
+
+extern "C" int pfsgnn_edge_mlp_bwd(int G, int NF, int NC, int F, const float* g_tot,
+                                   const float* alpha, const float* gam0, const float* gam1,
+                                   const float* y, const float* xe, const float* xsc,
+                                   const float* xsh, const float* Ps, const float* Pt,
+                                   const float* W1, const float* W2, float* dW1, float* dW2,
+                                   float* db2, float* gxe, float* GzEs, float* GzEt,
+                                   float* g_xs, float* g_xt, float* Vu, void* ws,
+                                   size_t ws_bytes, void* stream) {
+  return edge_mlp_bwd_impl(nullptr, G, NF, NC, F, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps,
+                           Pt, W1, W2, dW1, dW2, db2, gxe, GzEs, GzEt, g_xs, g_xt, Vu, ws,
+                           ws_bytes, stream);
+}
+
+extern "C" int pfsgnn_sl_edge_mlp_bwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
+                                      const float* g_tot, const float* alpha, const float* gam0,
+                                      const float* gam1, const float* y, const float* xe,
+                                      const float* xsc, const float* xsh, const float* Ps,
+                                      const float* Pt, const float* W1, const float* W2,
+                                      float* dW1, float* dW2, float* db2, float* gxe, float* GzEs,
+                                      float* GzEt, float* g_xs, float* g_xt, float* Vu, void* ws,
+                                      size_t ws_bytes, void* stream) {
+  PF_REQUIRE(sl, "pfsgnn_sl_edge_mlp_bwd", "null layout");
+  return edge_mlp_bwd_impl(sl, G, NF, NC, F, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1,
+                           W2, dW1, dW2, db2, gxe, GzEs, GzEt, g_xs, g_xt, Vu, ws, ws_bytes,
+                           stream);
 }

@@ -51,4 +51,49 @@ int edge_mlp_bwd(const EdgeGeo& geo, int F, const float* g_tot, const float* alp
                  const float* W1, const float* W2, float* gxe, float* gs, float* pW2, float* pW1,
                  float* pCol, int prec, hipStream_t st);
 
+// ------------------------------------------------------------ sliced general graphs
+// A general (non-complete) batch laid out in slices (pfsgnn_sliced.hip,
+// include/pfsgnn.h pfsgnn_sliced_t): slice s = 16 fibers of one graph, the k-th
+// edge of lane j at position base[s] + 16 k + j for k < len[s]; cls[p] the class
+// within its graph of position p (0xFF: padding).  The kernels take the
+// complete path's EdgeGeo with KS = 1, NFG = ceil(NF / 64) blocks per graph
+// (4 slices per block) and E = EP (edge-tensor columns), and write the same
+// per-block partials, so every finishing reduction is shared.
+struct SlGeo {
+  const int* fib;        // [nslices * 16] global fiber of each lane, -1: none
+  const int* base;       // [nslices]
+  const int* len;        // [nslices]
+  const uint8_t* cls;    // [EP]
+  const float* pco;      // [maxdeg][8] Pebay coefficients of counts 1..maxdeg
+  long long EP, E;       // positions (padding included), real edges
+  int maxdeg;
+};
+static constexpr int SL_MAX_NC = 128;   // classes per graph (LDS class rows + accumulators)
+EdgeGeo sl_geo(int G, int NF, int NC, const SlGeo& sl);
+int sl_edge_mlp_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* xe, const float* xsc,
+                    const float* xsh, const float* Ps, const float* PtS, const float* W1,
+                    const float* W2, const float* b2, float* y, float* part, int prec,
+                    hipStream_t st);
+// moments straight to mom / hs (per-fiber counts: the fiber degrees)
+int sl_source_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, const float* sc,
+                  const float* sh, const float* QtS, const float* Ws1, const float* Ws2,
+                  const float* bs2, float* mom, float* hs, int prec, hipStream_t st);
+int sl_target_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, const float* sc,
+                  const float* sh, const float* Rs, const float* Wt1, float* part, uint8_t* tmask,
+                  int prec, hipStream_t st);
+int sl_target_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, const float* sc,
+                  const float* sh, const float* Rs, const float* Wt1, const float* ghS, float* gz,
+                  float* gxe, float* part, const uint8_t* tmask, int prec, hipStream_t st);
+int sl_source_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, const float* sc,
+                  const float* sh, const float* QtS, const float* Ws1, const float* Ws2,
+                  const float* bs2, const float* mean, const float* coef, const float* Rs,
+                  const float* Wt1, const float* ghS, const float* g_next, const float* mu1,
+                  const float* inv1, float* g_tot, float* pW2, float* pW1, float* pCol,
+                  float* pBN, const uint8_t* tmask, int prec, hipStream_t st);
+int sl_edge_mlp_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* g_tot,
+                    const float* alpha, const float* gam0, const float* gam1, const float* y,
+                    const float* xe, const float* xsc, const float* xsh, const float* Ps,
+                    const float* PtS, const float* W1, const float* W2, float* gxe, float* gs,
+                    float* pW2, float* pW1, float* pCol, int prec, hipStream_t st);
+
 }  // namespace pfm

@@ -61,6 +61,112 @@ __global__ void k_sp_ptr(const int* __restrict__ keys, long long E, int n, int* 
   ptr[k] = (int)lo;
 }
 
+// ------------------------------------------------------------ sliced layout
+// (pfsgnn_sliced.hip) key per fiber: its graph in the high word, 2^32-1 minus its
+// degree in the low one -- one stable ascending sort orders the fibers by
+// graph, then by degree descending, ties in fiber order
+__global__ void k_sl_keys(const int* __restrict__ fib_ptr, int NS, int NF,
+                          unsigned long long* __restrict__ key, int* __restrict__ val) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= NS) return;
+  const unsigned deg = (unsigned)(fib_ptr[n + 1] - fib_ptr[n]);
+  key[n] = ((unsigned long long)(unsigned)(n / NF) << 32) | (0xFFFFFFFFu - deg);
+  val[n] = n;
+}
+
+// thread per slice: lane j of slice q of graph g takes the (16 q + j)-th fiber
+// of g in degree order; the slice runs for its largest degree (lane 0's)
+__global__ void k_sl_slices(const int* __restrict__ sorted, const int* __restrict__ fib_ptr,
+                            int G, int NF, int SPG, int* __restrict__ fib, int* __restrict__ len,
+                            long long* __restrict__ cnt, int* __restrict__ slot_of) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= G * SPG) return;
+  const int g = s / SPG, q = s - g * SPG;
+  int L = 0;
+  for (int j = 0; j < 16; ++j) {
+    const int i = 16 * q + j;
+    const int f = i < NF ? sorted[(long long)g * NF + i] : -1;
+    fib[s * 16 + j] = f;
+    if (f >= 0) {
+      slot_of[f] = s * 16 + j;
+      L = max(L, fib_ptr[f + 1] - fib_ptr[f]);
+    }
+  }
+  len[s] = L;
+  cnt[s] = 16ll * L;
+}
+
+__global__ void k_sl_info(const long long* __restrict__ base64, const long long* __restrict__ cnt,
+                          int nsl, const int* __restrict__ maxd, int* __restrict__ base,
+                          long long* __restrict__ info) {
+  for (int s = blockIdx.x * 256 + threadIdx.x; s < nsl; s += gridDim.x * 256)
+    base[s] = (int)base64[s];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    info[0] = base64[nsl - 1] + cnt[nsl - 1];
+    info[1] = maxd[0];
+  }
+}
+
+// thread per fiber-sorted position p: its slot position base + 16 k + lane
+__global__ void k_sl_fill(const int* __restrict__ src_p, const int* __restrict__ tgt_p,
+                          const int* __restrict__ user_of, const int* __restrict__ fib_ptr,
+                          long long E, int NF, int NC, const int* __restrict__ slot_of,
+                          const int* __restrict__ base, unsigned char* __restrict__ cls,
+                          int* __restrict__ pos_user) {
+  for (long long p = (long long)blockIdx.x * 256 + threadIdx.x; p < E;
+       p += (long long)gridDim.x * 256) {
+    const int n = src_p[p];
+    const int k = (int)(p - fib_ptr[n]);
+    const int sl = slot_of[n];
+    const long long q = (long long)base[sl >> 4] + 16ll * k + (sl & 15);
+    cls[q] = (unsigned char)(tgt_p[p] - (n / NF) * NC);
+    pos_user[q] = user_of[p];
+  }
+}
+
+// Pebay's count-only coefficients of the n-th message (pfsgnn_mfma.hip
+// km_source_fwd's table), n = k + 1
+__global__ void k_sl_pco(int maxdeg, float* __restrict__ pco) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= maxdeg) return;
+  const double nn = k + 1, r = 1.0 / nn;
+  float* p = pco + 8 * k;
+  p[0] = (float)((nn - 1) * r);
+  p[1] = (float)((nn - 1) * (nn - 2) * r * r);
+  p[2] = (float)((nn - 1) * (nn * nn - 3 * nn + 3) * r * r * r);
+  p[3] = (float)r;
+  p[4] = (float)(6 * r * r);
+  p[5] = (float)(-4 * r);
+  p[6] = (float)(-3 * r);
+  p[7] = 0.f;
+}
+
+// caller-order rows [E][F] <-> slot tensors [F][EP] (0 at padding)
+__global__ void k_to_slots(const float* __restrict__ src, long long EP, int F,
+                           const int* __restrict__ pos_user, float* __restrict__ dst) {
+  for (long long p = (long long)blockIdx.x * 256 + threadIdx.x; p < EP;
+       p += (long long)gridDim.x * 256) {
+    const int u = pos_user[p];
+    for (int j = 0; j < F; ++j) dst[(long long)j * EP + p] = u >= 0 ? src[(long long)u * F + j] : 0.f;
+  }
+}
+__global__ void k_from_slots(const float* __restrict__ y, const float* __restrict__ sc,
+                             const float* __restrict__ sh, long long E, long long EP, int F,
+                             const int* __restrict__ pos_user, int rowmajor,
+                             float* __restrict__ dst) {
+  for (long long p = (long long)blockIdx.x * 256 + threadIdx.x; p < EP;
+       p += (long long)gridDim.x * 256) {
+    const int u = pos_user[p];
+    if (u < 0) continue;
+    for (int j = 0; j < F; ++j) {
+      float v = y[(long long)j * EP + p];
+      if (sc) v = fmaf(v, sc[j], sh[j]);
+      if (rowmajor) dst[(long long)u * F + j] = v;
+      else dst[(long long)j * E + u] = v;
+    }
+  }
+}
+
 // ------------------------------------------------------------ gathers
 // thread per position e (idx[e] read once), every channel: coalesced writes
 // out[c][e]; mode 0: = X[c][idx[e]], 1: += X[c][idx[e]], 2: = X[c][idx[e]] *
@@ -463,4 +569,109 @@ extern "C" int pfsgnn_rows_axpby(const float* g, const float* y, int C, long lon
   hipLaunchKernelGGL(k_rows_axpby, dim3(grid_of(N)), dim3(256), 0, as_stream(stream), g, y, C, N,
                      alpha, gam1, gam0, out);
   return pf::check_launch("pfsgnn_rows_axpby");
+}
+
+// ---------------------------------------------------------------- sliced layout
+namespace {
+struct SlPlanWs {
+  size_t keys, vals, cnt, tmp, total;
+};
+SlPlanWs sl_plan_ws(int G, int NF) {
+  const int NS = G * NF, nsl = G * ((NF + 63) / 64) * 4;
+  size_t ts = 0, tc = 0, tr = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, ts, (const unsigned long long*)nullptr,
+                                           (unsigned long long*)nullptr, (const int*)nullptr,
+                                           (int*)nullptr, NS);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tc, (const long long*)nullptr,
+                                         (long long*)nullptr, nsl);
+  (void)hipcub::DeviceReduce::Max(nullptr, tr, (const int*)nullptr, (int*)nullptr, nsl);
+  SlPlanWs w;
+  w.keys = 2 * align256((size_t)NS * 8);
+  w.vals = 2 * align256((size_t)NS * 4);
+  w.cnt = 2 * align256((size_t)nsl * 8) + 256;
+  w.tmp = align256(std::max(ts, std::max(tc, tr)));
+  w.total = w.keys + w.vals + w.cnt + w.tmp;
+  return w;
+}
+}  // namespace
+
+extern "C" size_t pfsgnn_sliced_plan_ws_bytes(int G, int NF) {
+  if (G <= 0 || NF <= 0) return 256;
+  return sl_plan_ws(G, NF).total;
+}
+
+extern "C" int pfsgnn_sliced_plan(const int* fib_ptr, int G, int NF, int* fib, int* base, int* len,
+                                  int* slot_of, long long* info, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  const char* where = "pfsgnn_sliced_plan";
+  PF_REQUIRE(fib_ptr && G > 0 && NF > 0 && fib && base && len && slot_of && info, where,
+             "bad arguments");
+  PF_REQUIRE((long long)G * NF < INT32_MAX, where, "too many fibers for int32 indices");
+  const SlPlanWs p = sl_plan_ws(G, NF);
+  PF_REQUIRE(ws && ws_bytes >= p.total, where, "workspace too small");
+  hipStream_t st = as_stream(stream);
+  const int NS = G * NF, SPG = ((NF + 63) / 64) * 4, nsl = G * SPG;
+  char* w = static_cast<char*>(ws);
+  auto* key = reinterpret_cast<unsigned long long*>(w);
+  auto* key2 = reinterpret_cast<unsigned long long*>(w + p.keys / 2);
+  int* val = reinterpret_cast<int*>(w + p.keys);
+  int* sorted = reinterpret_cast<int*>(w + p.keys + p.vals / 2);
+  auto* cnt = reinterpret_cast<long long*>(w + p.keys + p.vals);
+  auto* base64 = reinterpret_cast<long long*>(w + p.keys + p.vals + (p.cnt - 256) / 2);
+  int* maxd = reinterpret_cast<int*>(w + p.keys + p.vals + p.cnt - 256);
+  void* tmp = w + p.keys + p.vals + p.cnt;
+  size_t tmpb = p.tmp;
+  hipLaunchKernelGGL(k_sl_keys, dim3((NS + 255) / 256), dim3(256), 0, st, fib_ptr, NS, NF, key, val);
+  if (hipcub::DeviceRadixSort::SortPairs(tmp, tmpb, key, key2, val, sorted, NS, 0,
+                                         32 + key_bits(G), st) != hipSuccess)
+    return pf::fail(where, "radix sort (fiber degrees)");
+  hipLaunchKernelGGL(k_sl_slices, dim3((nsl + 255) / 256), dim3(256), 0, st, sorted, fib_ptr, G,
+                     NF, SPG, fib, len, cnt, slot_of);
+  tmpb = p.tmp;
+  if (hipcub::DeviceScan::ExclusiveSum(tmp, tmpb, cnt, base64, nsl, st) != hipSuccess)
+    return pf::fail(where, "scan (slice bases)");
+  tmpb = p.tmp;
+  if (hipcub::DeviceReduce::Max(tmp, tmpb, len, maxd, nsl, st) != hipSuccess)
+    return pf::fail(where, "reduce (largest degree)");
+  hipLaunchKernelGGL(k_sl_info, dim3((nsl + 255) / 256), dim3(256), 0, st, base64, cnt, nsl, maxd,
+                     base, info);
+  return pf::check_launch(where);
+}
+
+extern "C" int pfsgnn_sliced_fill(const int* src_p, const int* tgt_p, const int* user_of,
+                                  const int* fib_ptr, long long E, int NF, int NC,
+                                  const int* slot_of, const int* base, long long EP, int maxdeg,
+                                  unsigned char* cls, int* pos_user, float* pco, void* stream) {
+  const char* where = "pfsgnn_sliced_fill";
+  PF_REQUIRE(src_p && tgt_p && user_of && fib_ptr && slot_of && base && cls && pos_user && pco &&
+                 E > 0 && EP >= E && NF > 0 && NC > 0 && NC < 255 && maxdeg >= 0,
+             where, "bad arguments (NC < 255)");
+  hipStream_t st = as_stream(stream);
+  if (hipMemsetAsync(cls, 0xFF, (size_t)EP, st) != hipSuccess ||
+      hipMemsetAsync(pos_user, 0xFF, (size_t)EP * sizeof(int), st) != hipSuccess)
+    return pf::fail(where, "memset");
+  hipLaunchKernelGGL(k_sl_fill, dim3(grid_of(E)), dim3(256), 0, st, src_p, tgt_p, user_of, fib_ptr,
+                     E, NF, NC, slot_of, base, cls, pos_user);
+  if (maxdeg > 0)
+    hipLaunchKernelGGL(k_sl_pco, dim3((maxdeg + 255) / 256), dim3(256), 0, st, maxdeg, pco);
+  return pf::check_launch(where);
+}
+
+extern "C" int pfsgnn_edges_to_slots(const float* src, long long E, long long EP, int F,
+                                     const int* pos_user, float* dst, void* stream) {
+  PF_REQUIRE(src && pos_user && dst && E > 0 && EP >= E && F > 0, "pfsgnn_edges_to_slots",
+             "bad arguments");
+  hipLaunchKernelGGL(k_to_slots, dim3(grid_of(EP)), dim3(256), 0, as_stream(stream), src, EP, F,
+                     pos_user, dst);
+  return pf::check_launch("pfsgnn_edges_to_slots");
+}
+
+extern "C" int pfsgnn_edges_from_slots(const float* y, const float* sc, const float* sh,
+                                       long long E, long long EP, int F, const int* pos_user,
+                                       int rowmajor, float* dst, void* stream) {
+  PF_REQUIRE(y && pos_user && dst && E > 0 && EP >= E && F > 0 && (!sc == !sh),
+             "pfsgnn_edges_from_slots", "bad arguments");
+  hipLaunchKernelGGL(k_from_slots, dim3(grid_of(EP)), dim3(256), 0, as_stream(stream), y, sc, sh,
+                     E, EP, F, pos_user, rowmajor, dst);
+  return pf::check_launch("pfsgnn_edges_from_slots");
 }

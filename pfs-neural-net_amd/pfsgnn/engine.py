@@ -47,6 +47,8 @@ class Dims:
         self.G, self.NF, self.NC, self.F = int(G), int(NF), int(NC), int(F)
         self.sp = sp
         self.E = self.G * self.NF * self.NC if sp is None else sp.E
+        # columns of an edge tensor (a sliced general batch pads its fibers' runs)
+        self.EP = self.E if sp is None else sp.EP
         self.NS = self.G * self.NF
         self.NT = self.G * self.NC
 
@@ -398,7 +400,8 @@ class Engine:
                                       agg=(Wt2, bt2, float(d.NF)),
                                       **({"tmask": tmask} if tmask is not None else {}))
         else:
-            hsum = be.target_fwd(d, xe3[0], xe3[1], xe3[2], Rs, Wt1)
+            hsum = be.target_fwd(d, xe3[0], xe3[1], xe3[2], Rs, Wt1,
+                                 **({"tmask": tmask} if tmask is not None else {}))
             # the bias of the summed messages is deg(c) * b2 (gnn.py:190)
             agg = be.lin(Wt2, 0, 2 * F, hsum)
             be.lin(bt2.view(-1, 1), 0, 1, d.sp.deg_t, out=agg, add=True)
@@ -606,7 +609,7 @@ class Engine:
                                                    tmask=stt.get("tmask") if live_t else None)
                 bnc = bnc[0] if self.normed else None
             else:
-                g_tot = be.zeros(F, d.E) if g_xe is None else g_xe
+                g_tot = be.zeros(F, d.EP) if g_xe is None else g_xe
                 bnc = None
                 if self.normed:
                     Sg, Sgx = be.edge_bn_grad_sums(d, g_tot, se["y"], *bnstat)

@@ -26,6 +26,7 @@ from ``BipartiteData.__inc__``) with ``x_u`` of shape [G, F]; ``u[g]`` is
 broadcast to the edges / nodes of graph g and the GlobalModel means are
 per graph.  With G == 1 this is exactly the reference.
 """
+import os
 import weakref
 
 import torch
@@ -153,12 +154,21 @@ class Layout:
     (``sp`` set) is a PERM layout over its E positions (G=1, NF=E, NC=1 in the
     ABI's terms) whose permutation is the position -> caller-edge map."""
     PERM, FIBER_MAJOR, CANONICAL = 0, 1, 2
+    SLOTS = 3   # a sliced general batch: positions of native.SlicedLayout (pos_user)
 
     def __init__(self, G, NF, NC, mode, perm=None, fiber_major=False, sp=None):
         self.G, self.NF, self.NC, self.mode = G, NF, NC, mode
         self.perm = perm if mode == Layout.PERM else None
         self.fiber_major = fiber_major    # caller order == train.py's positional order
         self.sp = sp
+
+
+def sliced_ok(NC, F):
+    """General batches run on the fused sliced kernels (pfsgnn_sliced.hip) when
+    their class tables fit the LDS (NC <= 128 classes per graph) and Fdim is
+    8, 10 or 16, unless PFSGNN_SLICED=0 (the composed ops of pfsgnn.sparse)."""
+    return (os.environ.get("PFSGNN_SLICED", "1") != "0" and NC <= 128 and F in (8, 10, 16)
+            and hasattr(backend(), "sliced_layout"))
 
 
 def geometry(x_s, x_t, x_u, edge_index, F):
@@ -184,7 +194,12 @@ def geometry(x_s, x_t, x_u, edge_index, F):
             hit = Layout(G, NF, NC, mode, perm, fiber_major=fm)
         else:
             sp = backend().sparse_layout(edge_index, G, NF, NC)
-            hit = Layout(1, E, 1, Layout.PERM, sp.user_of, sp=sp)
+            if sliced_ok(NC, F):
+                # the fused general-graph kernels (pfsgnn_sliced.hip)
+                sp.sl = backend().sliced_layout(sp, G, NF, NC)
+                hit = Layout(1, E, 1, Layout.SLOTS, sp.sl.pos_user, sp=sp)
+            else:
+                hit = Layout(1, E, 1, Layout.PERM, sp.user_of, sp=sp)
         _LAYOUT_CACHE.put(edge_index, key, hit)
     return Dims(G, NF, NC, F, sp=hit.sp), hit
 
@@ -483,7 +498,7 @@ class _EdgeFn(torch.autograd.Function):
         eng = _engine_for(F, module.normed)
         P, Gr = module._flat_params(), module._recording_grads()
         gc = grad_edges_in(g, lay)
-        gc = be.zeros(F, d.E) if gc is None else gc.contiguous()
+        gc = be.zeros(F, d.EP) if gc is None else gc.contiguous()
         bnc = None
         if module.normed:
             Sg, Sgx = be.edge_bn_grad_sums(d, gc, st["y"], st["mu1"], st["inv1"])

@@ -58,6 +58,17 @@ class Red(ctypes.Structure):
 REDP = ctypes.POINTER(Red)
 
 
+class Sliced(ctypes.Structure):
+    """pfsgnn_sliced_t (include/pfsgnn.h): a general batch cut into slices of 16
+    fibers for the fused edge kernels (pfsgnn_sliced.hip)."""
+    _fields_ = [("fib", ctypes.c_void_p), ("base", ctypes.c_void_p), ("len", ctypes.c_void_p),
+                ("cls", ctypes.c_void_p), ("pco", ctypes.c_void_p), ("EP", ctypes.c_longlong),
+                ("E", ctypes.c_longlong), ("maxdeg", ctypes.c_int)]
+
+
+SLP = ctypes.POINTER(Sliced)
+
+
 class OSeg(ctypes.Structure):
     """pfsgnn_oseg (include/pfsgnn.h): one row block of an input-gradient output."""
     _fields_ = [("x", ctypes.c_void_p), ("rows", ctypes.c_int), ("add", ctypes.c_int)]
@@ -183,7 +194,17 @@ _SIGS = {
     "pfsgnn_edges_to_canonical": ([P, I, I, I, I, I, P, P, P], I),
     "pfsgnn_edges_from_canonical": ([P, P, P, I, I, I, I, I, P, I, P, P], I),
     "pfsgnn_adam": ([P, P, P, P, LL, I, P, FL, FL, FL, FL, FL, P, P], I),
+    "pfsgnn_sliced_plan_ws_bytes": ([I, I], SZ),
+    "pfsgnn_sliced_plan": ([P, I, I, P, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_sliced_fill": ([P, P, P, P, LL, I, I, P, P, LL, I, P, P, P, P], I),
+    "pfsgnn_edges_to_slots": ([P, LL, LL, I, P, P, P], I),
+    "pfsgnn_edges_from_slots": ([P, P, P, LL, LL, I, P, I, P, P], I),
+    "pfsgnn_sl_tmask_bytes": ([SLP, I], SZ),
 }
+# the edge ops on a sliced general batch: the complete op's arguments after the layout
+for _op in ("edge_mlp_fwd", "edge_mlp_fwd_bn", "source_fwd", "target_fwd", "target_bwd",
+            "source_bwd", "source_bwd_bn", "edge_mlp_bwd"):
+    _SIGS["pfsgnn_sl_" + _op] = ([SLP] + _SIGS["pfsgnn_" + _op][0], I)
 
 
 def lib():
@@ -297,6 +318,23 @@ def _ensure_sync(device):
     _SYNC = torch.zeros(n, dtype=torch.uint8, device=device)
     torch.cuda.synchronize(device)
     _call("pfsgnn_set_sync_buffer", _SYNC.data_ptr(), n)
+
+
+SLOTS = 3   # pfsgnn.gnn.Layout.SLOTS: the positions of a sliced general batch
+
+
+class SlicedLayout:
+    """A sliced general batch's device tensors (pfsgnn_sliced_plan / _fill) and
+    the pfsgnn_sliced_t pointing at them, kept alive together.  pos_user [EP]:
+    the caller's edge at each position (-1: padding)."""
+
+    def __init__(self, fib, base, ln, slot_of, cls, pos_user, pco, EP, E, maxdeg):
+        self.fib, self.base, self.len, self.slot_of = fib, base, ln, slot_of
+        self.cls, self.pos_user, self.pco = cls, pos_user, pco
+        self.EP, self.E, self.maxdeg = int(EP), int(E), int(maxdeg)
+        self.c = Sliced(fib.data_ptr(), base.data_ptr(), ln.data_ptr(), cls.data_ptr(),
+                        pco.data_ptr(), self.EP, self.E, self.maxdeg)
+        self.ref = ctypes.pointer(self.c)
 
 
 class HipBackend:
@@ -832,14 +870,29 @@ class HipBackend:
     def _set_dims(self, d):
         self._dims = d
 
+    @staticmethod
+    def _composed(d):
+        """A general batch without a sliced layout: the composed ops (pfsgnn.sparse)."""
+        return d.sp is not None and d.sp.sl is None
+
+    @staticmethod
+    def _ecall(op, d, *args):
+        """Edge op `op` of the C ABI: pfsgnn_<op> on complete graphs,
+        pfsgnn_sl_<op> (same arguments after the layout) on a sliced batch."""
+        sl = d.sp.sl if d.sp is not None else None
+        if sl is None:
+            _call("pfsgnn_" + op, *args)
+        else:
+            _call("pfsgnn_sl_" + op, sl.ref, *args)
+
     def edge_mlp_fwd(self, d, xe, xsc, xsh, Ps, Pt, W1, W2, b2):
-        if d.sp is not None:
+        if self._composed(d):
             return self._sp.edge_mlp_fwd(d, xe, xsc, xsh, Ps, Pt, W1, W2, b2)
         self._set_dims(d)
-        y, mu, var = self.empty(d.F, d.E), self.empty(d.F), self.empty(d.F)
+        y, mu, var = self.empty(d.F, d.EP), self.empty(d.F), self.empty(d.F)
         self._chk(xe, Ps, Pt, W1, W2, b2)
         ws, wsb = self._wsargs(d)
-        _call("pfsgnn_edge_mlp_fwd", d.G, d.NF, d.NC, d.F, xe.data_ptr(), _ptr(xsc), _ptr(xsh),
+        self._ecall("edge_mlp_fwd", d, d.G, d.NF, d.NC, d.F, xe.data_ptr(), _ptr(xsc), _ptr(xsh),
               Ps.data_ptr(), Pt.data_ptr(), W1.data_ptr(), W2.data_ptr(), b2.data_ptr(),
               y.data_ptr(), mu.data_ptr(), var.data_ptr(), ws, wsb, _stream())
         return y, mu, var
@@ -848,17 +901,17 @@ class HipBackend:
         """edge_mlp_fwd + bn2_finalize in one call; ``bn`` = (gamma, beta,
         running_mean, running_var, momentum, eps).  -> y, mu1, var1, sc, sh, inv1."""
         gamma, beta, rm, rv, momentum, eps = bn
-        if d.sp is not None:
+        if self._composed(d):
             y, mu, var = self._sp.edge_mlp_fwd(d, xe, xsc, xsh, Ps, Pt, W1, W2, b2)
             sc, sh, inv1, _ = self.bn2_finalize(mu, var, gamma, beta, rm, rv, d.E, momentum, eps)
             return y, mu, var, sc, sh, inv1
         self._set_dims(d)
         F = d.F
-        y, mu, var = self.empty(F, d.E), self.empty(F), self.empty(F)
+        y, mu, var = self.empty(F, d.EP), self.empty(F), self.empty(F)
         sc, sh, inv1, inv2 = self.empty(F), self.empty(F), self.empty(F), self.empty(F)
         self._chk(xe, Ps, Pt, W1, W2, b2, gamma, beta, rm, rv)
         ws, wsb = self._wsargs(d)
-        _call("pfsgnn_edge_mlp_fwd_bn", d.G, d.NF, d.NC, F, xe.data_ptr(), _ptr(xsc), _ptr(xsh),
+        self._ecall("edge_mlp_fwd_bn", d, d.G, d.NF, d.NC, F, xe.data_ptr(), _ptr(xsc), _ptr(xsh),
               Ps.data_ptr(), Pt.data_ptr(), W1.data_ptr(), W2.data_ptr(), b2.data_ptr(),
               y.data_ptr(), mu.data_ptr(), var.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
               _ptr(rm), _ptr(rv), float(momentum), float(eps), sc.data_ptr(), sh.data_ptr(),
@@ -866,12 +919,12 @@ class HipBackend:
         return y, mu, var, sc, sh, inv1
 
     def source_fwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, hs_out):
-        if d.sp is not None:
+        if self._composed(d):
             return self._sp.source_fwd(d, y, sc, sh, Qt, Ws1, Ws2, bs2, hs_out)
         mom = self.empty(4, 2 * d.F, d.NS)
         self._chk(y, Qt, Ws1, Ws2, bs2, hs_out)
         ws, wsb = self._wsargs(d)
-        _call("pfsgnn_source_fwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
+        self._ecall("source_fwd", d, d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
               Qt.data_ptr(), Ws1.data_ptr(), Ws2.data_ptr(), bs2.data_ptr(), mom.data_ptr(),
               hs_out.data_ptr(), ws, wsb, _stream())
         return mom
@@ -879,8 +932,11 @@ class HipBackend:
     def tmask(self, d):
         """A buffer for TModel's LeakyReLU mask (pfsgnn_tmask_bytes), or None
         when the current edge path recomputes that layer in the backward."""
-        if d.sp is not None:
+        if self._composed(d):
             return None
+        if d.sp is not None:
+            n = lib().pfsgnn_sl_tmask_bytes(d.sp.sl.ref, d.F)
+            return torch.empty(n, dtype=torch.uint8, device=self.device) if n else None
         n = lib().pfsgnn_tmask_bytes(d.G, d.NF, d.NC, d.F)
         return torch.empty(n, dtype=torch.uint8, device=self.device) if n else None
 
@@ -888,7 +944,7 @@ class HipBackend:
         """-> hsum; with ``agg`` = (Wt2, bt2, bscale) -> (hsum, Wt2 hsum + bscale bt2),
         the second Linear done in the class reduction's epilogue.  ``tmask``
         (from ``tmask(d)``) receives TModel's LeakyReLU mask for the backward."""
-        if d.sp is not None:
+        if self._composed(d):
             hsum = self._sp.target_fwd(d, y, sc, sh, Rs, Wt1)
             if agg is None:
                 return hsum
@@ -903,7 +959,7 @@ class HipBackend:
             assert Wt2.shape == (2 * d.F, 2 * d.F)
             A = self.empty(2 * d.F, d.NT)
         ws, wsb = self._wsargs(d)
-        _call("pfsgnn_target_fwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
+        self._ecall("target_fwd", d, d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
               Rs.data_ptr(), Wt1.data_ptr(), hsum.data_ptr(), _ptr(Wt2), _ptr(bt2),
               float(bscale), _ptr(A), _ptr(tmask), ws, wsb, _stream())
         return hsum if agg is None else (hsum, A)
@@ -912,17 +968,17 @@ class HipBackend:
                    tmask=None):
         """-> (GzT, gxe); with ``g_xs``: g_xs += Wt1[:, :F]^T GzT as well;
         ``tmask``: the forward's mask (target_fwd), read instead of recomputed."""
-        if d.sp is not None:
+        if self._composed(d):
             out = self._sp.target_bwd(d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=want_gxe)
             if g_xs is not None:
                 self.lin_t(Wt1, 0, d.F, out[0], out=g_xs, add=True)
             return out
         self._chk(g_xs)
         GzT = self.empty(2 * d.F, d.NS)
-        gxe = self.empty(d.F, d.E) if want_gxe else None
+        gxe = self.empty(d.F, d.EP) if want_gxe else None
         g_hsum = g_hsum.contiguous()
         ws, wsb = self._wsargs(d)
-        _call("pfsgnn_target_bwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
+        self._ecall("target_bwd", d, d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
               Rs.data_ptr(), Wt1.data_ptr(), g_hsum.data_ptr(), GzT.data_ptr(), dWt1.data_ptr(),
               _ptr(gxe), _ptr(g_xs), _ptr(tmask), ws, wsb, _stream())
         return GzT, gxe
@@ -933,7 +989,7 @@ class HipBackend:
         dbeta) (and ``bnstat``) the edge BatchNorm's backward is finished in the
         same call: -> (g_tot, GzS, None, None, (alpha, gam0, gam1)).  With
         ``g_xt``: g_xt += Ws1[:, :F]^T GzS as well."""
-        if d.sp is not None:
+        if self._composed(d):
             out = self._sp.source_bwd(d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next,
                                       bnstat, dWs1, dWs2, dbs2)
             if g_xt is not None:
@@ -943,7 +999,7 @@ class HipBackend:
             gamma, var1, n, eps, dg, db = bn2
             cf = self.bn2_bwd_coef(out[2], out[3], bnstat[0], var1, gamma, n, eps, dg, db)
             return out[0], out[1], None, None, cf
-        g_tot = self.empty(d.F, d.E)
+        g_tot = self.empty(d.F, d.EP)
         GzS = self.empty(2 * d.F, d.NT)
         Rs = Wt1 = g_hsum = None
         if tpart is not None:
@@ -965,18 +1021,18 @@ class HipBackend:
             assert bnstat is not None
             gamma, var1, n, eps, dg, db = bn2
             a, g0, g1 = self.empty(d.F), self.empty(d.F), self.empty(d.F)
-            _call("pfsgnn_source_bwd_bn", *head, var1.data_ptr(), gamma.data_ptr(), int(n),
+            self._ecall("source_bwd_bn", d, *head, var1.data_ptr(), gamma.data_ptr(), int(n),
                   float(eps), g_tot.data_ptr(), GzS.data_ptr(), dWs1.data_ptr(), dWs2.data_ptr(),
                   dbs2.data_ptr(), a.data_ptr(), g0.data_ptr(), g1.data_ptr(), dg.data_ptr(),
                   db.data_ptr(), _ptr(g_xt), _ptr(tmask), ws, wsb, _stream())
             return g_tot, GzS, None, None, (a, g0, g1)
-        _call("pfsgnn_source_bwd", *head, g_tot.data_ptr(), GzS.data_ptr(), dWs1.data_ptr(),
+        self._ecall("source_bwd", d, *head, g_tot.data_ptr(), GzS.data_ptr(), dWs1.data_ptr(),
               dWs2.data_ptr(), dbs2.data_ptr(), _ptr(Sg), _ptr(Sgx), _ptr(g_xt), _ptr(tmask), ws,
               wsb, _stream())
         return g_tot, GzS, Sg, Sgx
 
     def edge_bn_grad_sums(self, d, g, y, mu1, inv1):
-        if d.sp is not None:
+        if d.sp is not None:   # (slot tensors hold 0 at padding: the column sums hold)
             return self._sp.edge_bn_grad_sums(d, g, y, mu1, inv1)
         Sg, Sgx = self.empty(d.F), self.empty(d.F)
         ws, wsb = self._wsargs(d)
@@ -989,7 +1045,7 @@ class HipBackend:
         """-> (gxe, GzEs, GzEt); with ``nodes`` = (g_xs, g_xt) the first Linear's
         node-input gradients are added in the reductions' epilogues and the
         result is (gxe, GzEs, GzEt, Vu), Vu = W1[:, 3F:4F]^T GzEt per class."""
-        if d.sp is not None:
+        if self._composed(d):
             out = self._sp.edge_mlp_bwd(d, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1,
                                         W2, dW1, dW2, db2, want_gxe=want_gxe)
             if nodes is None:
@@ -998,7 +1054,7 @@ class HipBackend:
             self.lin_t(W1, 0, F, out[1], out=nodes[0], add=True)
             self.lin_t(W1, F, F, out[2], out=nodes[1], add=True)
             return out + (self.lin_t(W1, 3 * F, F, out[2]),)
-        gxe = self.empty(d.F, d.E) if want_gxe else None
+        gxe = self.empty(d.F, d.EP) if want_gxe else None
         GzEs, GzEt = self.empty(4 * d.F, d.NS), self.empty(4 * d.F, d.NT)
         g_xs = g_xt = Vu = None
         if nodes is not None:
@@ -1006,7 +1062,7 @@ class HipBackend:
             self._chk(g_xs, g_xt)
             Vu = self.empty(d.F, d.NT)
         ws, wsb = self._wsargs(d)
-        _call("pfsgnn_edge_mlp_bwd", d.G, d.NF, d.NC, d.F, g_tot.data_ptr(), alpha.data_ptr(),
+        self._ecall("edge_mlp_bwd", d, d.G, d.NF, d.NC, d.F, g_tot.data_ptr(), alpha.data_ptr(),
               gam0.data_ptr(), gam1.data_ptr(), y.data_ptr(), xe.data_ptr(), _ptr(xsc), _ptr(xsh),
               Ps.data_ptr(), Pt.data_ptr(), W1.data_ptr(), W2.data_ptr(), dW1.data_ptr(),
               dW2.data_ptr(), db2.data_ptr(), _ptr(gxe), GzEs.data_ptr(), GzEt.data_ptr(),
@@ -1105,6 +1161,30 @@ class HipBackend:
         deg_t = (cls_ptr[1:] - cls_ptr[:-1]).to(torch.float32).reshape(1, -1).contiguous()
         return SparseGeo(E, src_p, tgt_p, user_of, fib_ptr, cls_ord, cls_ptr, deg_t)
 
+    def sliced_layout(self, sp, G, NF, NC):
+        """Slices of 16 fibers over a sparse layout (pfsgnn_sliced_plan / _fill):
+        the fused general-graph edge kernels' layout (pfsgnn_sliced.hip).  One
+        host read (the position count EP) per edge_index."""
+        i32 = dict(dtype=torch.int32, device=self.device)
+        nsl = G * ((NF + 63) // 64) * 4
+        fib, base, ln = torch.empty(nsl * 16, **i32), torch.empty(nsl, **i32), torch.empty(nsl, **i32)
+        slot_of = torch.empty(G * NF, **i32)
+        info = torch.empty(2, dtype=torch.int64, device=self.device)
+        ws = torch.empty(lib().pfsgnn_sliced_plan_ws_bytes(int(G), int(NF)), dtype=torch.uint8,
+                         device=self.device)
+        _call("pfsgnn_sliced_plan", sp.fib_ptr.data_ptr(), int(G), int(NF), fib.data_ptr(),
+              base.data_ptr(), ln.data_ptr(), slot_of.data_ptr(), info.data_ptr(), ws.data_ptr(),
+              ws.numel(), _stream())
+        EP, maxdeg = (int(v) for v in info.tolist())
+        cls = torch.empty(EP, dtype=torch.uint8, device=self.device)
+        pos_user = torch.empty(EP, **i32)
+        pco = torch.empty(8 * max(maxdeg, 1), dtype=torch.float32, device=self.device)
+        _call("pfsgnn_sliced_fill", sp.src_p.data_ptr(), sp.tgt_p.data_ptr(),
+              sp.user_of.data_ptr(), sp.fib_ptr.data_ptr(), sp.E, int(NF), int(NC),
+              slot_of.data_ptr(), base.data_ptr(), EP, maxdeg, cls.data_ptr(), pos_user.data_ptr(),
+              pco.data_ptr(), _stream())
+        return SlicedLayout(fib, base, ln, slot_of, cls, pos_user, pco, EP, sp.E, maxdeg)
+
     def gather_cols(self, X, idx, mode=0, out=None, Z=None):
         """out[c][e] (=, +=) X[c][idx[e]]; mode 2: X[c][idx[e]] * lrelu'(Z[c][e])."""
         C, N = X.shape
@@ -1199,6 +1279,12 @@ class HipBackend:
         (G, NF, NC, mode, perm) (pfsgnn.gnn.Layout)."""
         E, F = x.shape
         x = x.to(device=self.device, dtype=torch.float32).contiguous()
+        if lay.mode == SLOTS:
+            sl = lay.sp.sl
+            out = self.empty(F, sl.EP)
+            _call("pfsgnn_edges_to_slots", x.data_ptr(), E, sl.EP, F, sl.pos_user.data_ptr(),
+                  out.data_ptr(), _stream())
+            return out
         out = self.empty(F, E)
         _call("pfsgnn_edges_to_canonical", x.data_ptr(), lay.G, lay.NF, lay.NC, F, lay.mode,
               _ptr(lay.perm), out.data_ptr(), _stream())
@@ -1206,6 +1292,13 @@ class HipBackend:
 
     def edges_from_canonical(self, y, sc, sh, lay, rowmajor=True):
         F, E = y.shape
+        if lay.mode == SLOTS:
+            sl = lay.sp.sl
+            E = sl.E
+            out = self.empty(E, F) if rowmajor else self.empty(F, E)
+            _call("pfsgnn_edges_from_slots", y.data_ptr(), _ptr(sc), _ptr(sh), E, sl.EP, F,
+                  sl.pos_user.data_ptr(), int(rowmajor), out.data_ptr(), _stream())
+            return out
         out = self.empty(E, F) if rowmajor else self.empty(F, E)
         _call("pfsgnn_edges_from_canonical", y.data_ptr(), _ptr(sc), _ptr(sh), lay.G, lay.NF,
               lay.NC, F, lay.mode, _ptr(lay.perm), int(rowmajor), out.data_ptr(), _stream())

@@ -43,6 +43,12 @@ class SparseGeo:
         self.src_p, self.tgt_p, self.user_of = src_p, tgt_p, user_of
         self.fib_ptr, self.cls_ord, self.cls_ptr = fib_ptr, cls_ord, cls_ptr
         self.deg_t = deg_t
+        self.sl = None   # native.SlicedLayout when the fused sliced kernels run the batch
+
+    @property
+    def EP(self):
+        """Edge-tensor columns: E positions, or the sliced layout's (padding included)."""
+        return self.E if self.sl is None else self.sl.EP
 
 
 class SparseEdgeOps:

@@ -76,4 +76,5 @@ def run(density, label):
 dens = [float(x) for x in os.environ.get("SPARSE_DENSITIES", "1.0,0.999,0.3,0.05").split(",")]
 for dd in dens:
     run(dd, "complete (fused edge kernels)" if dd >= 1.0 else
-        f"{100 * dd:g}% dense (general path)")
+        f"{100 * dd:g}% dense (general, " +
+        ("composed)" if os.environ.get("PFSGNN_SLICED") == "0" else "sliced)"))
