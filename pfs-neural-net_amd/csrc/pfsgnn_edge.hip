@@ -1399,9 +1399,15 @@ int check_sliced(const char* where, const pfsgnn_sliced_t* sl, int NC, int F) {
   if (mf_bfy()) return pf::fail(where, "sliced layout: bf16 edge-state paths are not supported");
   return 0;
 }
-// the grid of an edge op: the complete path's, or the sliced batch's (KS = 1)
+// the grid of an edge op: the complete path's, or the sliced batch's
 EdgeGeo geo_of(int G, int NF, int NC, const pfsgnn_sliced_t* sl) {
   return sl ? pfm::sl_geo(G, NF, NC, sl_of(*sl)) : geo_for(G, NF, NC);
+}
+// blocks per graph of the per-class column partials [G][BPG][NC][D]: the
+// complete path's KS class splits own disjoint classes (one row per 64-fiber
+// group), a sliced batch's KS step splits each hold every class
+int col_bpg(const EdgeGeo& geo, const pfsgnn_sliced_t* sl) {
+  return sl ? geo.NFG * geo.KS : geo.NFG;
 }
 
 }  // namespace
@@ -1445,10 +1451,18 @@ size_t edge_ws_floats(const EdgeGeo& geo, int G, int NC, int F) {
 }  // namespace
 
 extern "C" size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F) {
-  // the larger of the two edge paths' partials (either may be selected later)
+  // the larger of the edge paths' partials (any may be selected later; a
+  // general batch's sliced grid at its largest step-split count, its class
+  // partials one row per split)
   const EdgeGeo geo = make_geo(G, NF, NC);
-  const size_t edge = std::max(edge_ws_floats(geo, G, NC, F),
-                               edge_ws_floats(geo_mfma(G, NF, NC), G, NC, F));
+  pfm::SlGeo sg{};
+  sg.maxdeg = 1 << 30;
+  EdgeGeo gs = pfm::sl_geo(G, NF, NC, sg);
+  gs.NFG *= gs.KS;
+  gs.nblocks = G * gs.NFG;
+  const size_t edge = std::max(std::max(edge_ws_floats(geo, G, NC, F),
+                                        edge_ws_floats(geo_mfma(G, NF, NC), G, NC, F)),
+                               edge_ws_floats(gs, G, NC, F));
   size_t node = (size_t)512 * 161 * 161 + 4096;                                     // wgrad splits
   size_t lay = (size_t)geo.E + 1024;                                                // layout counts
   return (std::max(std::max(edge, node), lay) + 64 * 16) * sizeof(float) + 16 * 256;
@@ -1634,7 +1648,7 @@ static int target_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
   PF_REQUIRE(y && Rs && Wt1 && hsum, "pfsgnn_target_fwd", "null");
   const EdgeGeo geo = geo_of(G, NF, NC, sl);
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
-  float* part = w.take((size_t)G * geo.NFG * NC * 2 * F);
+  float* part = w.take((size_t)G * col_bpg(geo, sl) * NC * 2 * F);
   PF_REQUIRE(part, "pfsgnn_target_fwd", "workspace too small");
   hipStream_t st = as_stream(stream);
   { pf::Timer tm_("target_fwd", st);
@@ -1653,7 +1667,7 @@ static int target_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
   // agg = Wt2 hsum + bscale bt2 (gnn.py:188-190, the second Linear after the sum)
   const NodeLin La = Wt2 ? NodeLin{Wt2, 2 * F, 0, 2 * F, 0, bt2, bscale, agg, (long long)G * NC}
                          : no_lin();
-  if (int rc = columns_lin(part, G, geo.NFG, NC, 2 * F, hsum, La, no_lin(), st)) return rc;
+  if (int rc = columns_lin(part, G, col_bpg(geo, sl), NC, 2 * F, hsum, La, no_lin(), st)) return rc;
   return pf::check_launch("pfsgnn_target_fwd");
 }
 
@@ -1879,7 +1893,7 @@ static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
   const bool defer = pW2 != nullptr;
   if (!defer) pW2 = w.take(nb * C * (C + 1) + nb * C * F);
   float* pW1 = pW2 ? pW2 + nb * C * (C + 1) : nullptr;
-  float* pCol = w.take((size_t)G * geo.NFG * NC * C);
+  float* pCol = w.take((size_t)G * col_bpg(geo, sl) * NC * C);
   float* pBN = w.take(nb * 2 * F);
   hipStream_t st = as_stream(stream);
   const bool mfma = sl || use_mfma();
@@ -1925,7 +1939,7 @@ static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
                          Sgx);
   }
   // g_xt += Ws1[:, 0:F]^T GzS (gnn.py:136, the x_t[tgt] input gradient)
-  if (int rc = columns_lin(pCol, G, geo.NFG, NC, C, GzS,
+  if (int rc = columns_lin(pCol, G, col_bpg(geo, sl), NC, C, GzS,
                            lin_t_add(g_xt ? Ws1 : nullptr, 2 * F, 0, F, g_xt, geo.NT), no_lin(),
                            st))
     return rc;
@@ -1975,7 +1989,7 @@ static int edge_mlp_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, i
   const bool defer = pW2 != nullptr;
   if (!defer) pW2 = w.take(nb * F * (H + 1) + nb * H * F);
   float* pW1 = pW2 ? pW2 + nb * F * (H + 1) : nullptr;
-  float* pCol = w.take((size_t)G * geo.NFG * NC * H);
+  float* pCol = w.take((size_t)G * col_bpg(geo, sl) * NC * H);
   float* gs = fiber_dst(geo, H, GzEs, w);
   hipStream_t st = as_stream(stream);
   if (sl) {
@@ -2019,7 +2033,7 @@ static int edge_mlp_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, i
   }
   NodeLin Lu = lin_t_add(Vu ? W1 : nullptr, 4 * F, 3 * F, F, Vu, geo.NT);
   Lu.add = 0;
-  if (int rc = columns_lin(pCol, G, geo.NFG, NC, H, GzEt,
+  if (int rc = columns_lin(pCol, G, col_bpg(geo, sl), NC, H, GzEt,
                            lin_t_add(g_xt ? W1 : nullptr, 4 * F, F, F, g_xt, geo.NT), Lu, st))
     return rc;
   return pf::check_launch("pfsgnn_edge_mlp_bwd");

@@ -22,6 +22,8 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -1011,14 +1013,30 @@ int with_tiles(int m, Fn fn) {
   return -1;
 }
 
-// the wide MLPs (M >= 5) stage their inputs in registers (k_mlp_fwd RS)
-bool fwd_rs(int m) { return m >= 5; }
+// the wide MLPs (M >= 5) stage their inputs in registers (k_mlp_fwd RS) and
+// run their backward with a 64-row input-gradient buffer (k_mlp_bwd RS);
+// A/B knobs PFSGNN_MLP_FWD_RS / PFSGNN_MLP_BWD_RS = 0: the LDS-staged forms
+static bool env_on(const char* name) {
+  const char* e = getenv(name);
+  return !(e && atoi(e) == 0);
+}
+bool fwd_rs(int m) {   // (default off: the LDS-staged forward is 0.38 ms/step faster at the bench shape)
+  static const bool on = [] {
+    const char* e = getenv("PFSGNN_MLP_FWD_RS");
+    return e && atoi(e) != 0;
+  }();
+  return m >= 5 && on;
+}
+bool bwd_rs(int m) {
+  static const bool on = env_on("PFSGNN_MLP_BWD_RS");
+  return m >= 5 && on;
+}
 size_t fwd_lds(int m) {
   return ((size_t)m * m * 256 + (size_t)m * 256 + 16 * m + 16 +
           (fwd_rs(m) ? 0 : (size_t)2 * 16 * m * XS_LD)) * 4;
 }
 size_t bwd_lds(int m) {   // (RS: a 64-row input-gradient buffer, one output-tile group)
-  return ((size_t)m * 256 + (size_t)m * m * 256 + 80 + (size_t)16 * (fwd_rs(m) ? 4 : m) * XS_LD) * 4;
+  return ((size_t)m * 256 + (size_t)m * m * 256 + 80 + (size_t)16 * (bwd_rs(m) ? 4 : m) * XS_LD) * 4;
 }
 
 // blocks per CU: the M <= 3 kernels fit 2 (registers, LDS), the wider ones
@@ -1076,19 +1094,23 @@ int mlp_fwd_launch(const InSegs& S, int K, int N, const float* W1, int ldw1, int
   const size_t lds = fwd_lds(m);
   const int grid = grid_for(N, m, lds);
   *grid_out = grid;
+  const bool rs = fwd_rs(m);
   return with_tiles(m, [&](auto mc) {
     constexpr int MM = decltype(mc)::value;
-    constexpr bool RS = MM >= 5;
-    static size_t attr = 0;  // dynamic LDS above the 64 KB default must be opted into
-    if (lds > 65536 && attr < lds) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mlp_fwd<MM, RS>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-        return -3;
-      attr = lds;
-    }
-    hipLaunchKernelGGL((k_mlp_fwd<MM, RS>), dim3(grid), dim3(256), lds, st, S, K, N, W1, ldw1, H,
-                       b1, W2, O, b2, Z, Yp, part);
-    return 0;
+    auto launch = [&](auto rsc) {
+      constexpr bool RS = decltype(rsc)::value && MM >= 5;
+      static size_t attr = 0;  // dynamic LDS above the 64 KB default must be opted into
+      if (lds > 65536 && attr < lds) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mlp_fwd<MM, RS>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+          return -3;
+        attr = lds;
+      }
+      hipLaunchKernelGGL((k_mlp_fwd<MM, RS>), dim3(grid), dim3(256), lds, st, S, K, N, W1, ldw1, H,
+                         b1, W2, O, b2, Z, Yp, part);
+      return 0;
+    };
+    return rs ? launch(std::true_type{}) : launch(std::false_type{});
   });
 }
 }  // namespace
@@ -1232,19 +1254,24 @@ extern "C" int pfsgnn_mlp_bwd(const float* dY, int N, const float* Yp, const flo
   const size_t lds = bwd_lds(m);
   const int grid = grid_for(N, m, lds);
   const int want_dx = nout > 0 ? 1 : 0;
+  const bool rs = bwd_rs(m);
   const int rc = with_tiles(m, [&](auto mc) {
     constexpr int MM = decltype(mc)::value;
-    static size_t attr = 0;  // dynamic LDS above the 64 KB default must be opted into
-    if (lds > 65536 && attr < lds) {
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mlp_bwd<MM, MM >= 5>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-        return -3;
-      attr = lds;
-    }
-    hipLaunchKernelGGL((k_mlp_bwd<MM, MM >= 5>), dim3(grid), dim3(256), lds, st, K, N, H, O, dY, Yp, spart,
-                       nsp, mu, var, gamma, eps, dgamma, dbeta, Z, W1, ldw1, W2, dYp, dZ, OS,
-                       want_dx);
-    return 0;
+    auto launch = [&](auto rsc) {
+      constexpr bool RS = decltype(rsc)::value && MM >= 5;
+      static size_t attr = 0;  // dynamic LDS above the 64 KB default must be opted into
+      if (lds > 65536 && attr < lds) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mlp_bwd<MM, RS>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+          return -3;
+        attr = lds;
+      }
+      hipLaunchKernelGGL((k_mlp_bwd<MM, RS>), dim3(grid), dim3(256), lds, st, K, N, H, O, dY, Yp,
+                         spart, nsp, mu, var, gamma, eps, dgamma, dbeta, Z, W1, ldw1, W2, dYp, dZ,
+                         OS, want_dx);
+      return 0;
+    };
+    return rs ? launch(std::true_type{}) : launch(std::false_type{});
   });
   PF_REQUIRE(rc != -3, where, "hipFuncSetAttribute (dynamic LDS) failed");
   PF_REQUIRE(rc == 0, where, "no kernel for this width");

@@ -20,15 +20,19 @@
 //     class-table rows (Pt, Qt, g_hsum) of the whole graph are staged in LDS and
 //     read per lane;
 //   * per-class sums (TModel's scatter-sum, gnn.py:190; the class-side
-//     gradients) go to a wave-private LDS accumulator [NC][D] by LDS float
-//     atomics -- one wave's adds to one address execute in program order and,
-//     inside one instruction, in the hardware's fixed lane order, so the sums are
-//     reproducible -- then the 4 waves' accumulators are merged in fixed order
-//     into the complete path's per-block column partials [G][NFG][NC][D].
+//     gradients) go to a wave-private LDS accumulator [NC][D + 1] (acc_add: a
+//     DPP row sum when the tile's edges share one class, else plain
+//     read-add-writes in conflict-free rounds -- one wave's updates of one
+//     row happen in a fixed order, so the sums are reproducible), then the
+//     4 waves' accumulators are merged in fixed order into the complete path's
+//     per-block column partials [G][NFG][NC][D].
 // The grid is the complete path's with KS = 1 (block = 4 slices = 64 fibers of
 // one graph, NFG blocks per graph), so every finishing reduction, BatchNorm
 // finalize and deferred weight-gradient flush of pfsgnn_edge.hip is shared.
 #include "pfsgnn_mfma_core.h"
+
+#include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -48,22 +52,27 @@ struct SRows {
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);                             \
   const int g4 = lane >> 4, j16 = lane & 15;                                           \
   const int bx = blockIdx.x;                                                           \
-  const int fg = bx % geo.NFG, gg = bx / geo.NFG;                                      \
-  const int slc = 4 * bx + wave;                                                       \
+  const int ks = bx % geo.KS, grp = bx / geo.KS;                                       \
+  const int fg = grp % geo.NFG, gg = grp / geo.NFG;                                    \
+  const int slc = 4 * grp + wave;                                                      \
   const int fib = sl.fib[slc * 16 + j16];                                              \
   const bool fvalid = fib >= 0;                                                        \
   const long long n = fvalid ? fib : 0;                                                \
   const int pb = __builtin_amdgcn_readfirstlane(sl.base[slc]);                         \
-  const int L = __builtin_amdgcn_readfirstlane(sl.len[slc]);                           \
+  const int Ls = __builtin_amdgcn_readfirstlane(sl.len[slc]);                          \
+  /* split ks of KS: steps [k0, k1) of the slice */                                    \
+  const int k0 = (int)(((long long)Ls * ks) / geo.KS);                                 \
+  const int k1 = (int)(((long long)Ls * (ks + 1)) / geo.KS);                           \
   const int NC = geo.NC;                                                               \
   const long long NS = geo.NS;                                                         \
   const uint32_t RB = (uint32_t)geo.E * 4u; /* channel-row bytes of an edge tensor */  \
   const uint32_t EB = RB;                                                              \
   const uint32_t eo0 = (uint32_t)(pb + j16) * 4u;                                      \
   constexpr uint32_t eoc = 64u; /* one step = 16 positions */                          \
-  const long long colbase = ((long long)gg * geo.NFG + fg) * NC;                       \
+  /* class partials [G][NFG * KS][NC][D] (columns_lin with NFG * KS blocks per graph) */ \
+  const long long colbase = ((long long)grp * geo.KS + ks) * NC;                       \
   const Rsrc rcl = rsrc(sl.cls, (uint32_t)geo.E);                                      \
-  (void)t; (void)n; (void)NS; (void)colbase; (void)EB; (void)fg;
+  (void)t; (void)n; (void)NS; (void)colbase; (void)EB; (void)fg; (void)k0; (void)k1;
 
 // the class byte of step k of the lane's fiber
 #define SL_CLS(k) \
@@ -79,33 +88,99 @@ struct SRows {
 
 extern __shared__ __attribute__((aligned(16))) float sl_dyn[];
 
-// zero the 4 waves' class accumulators [4][NC][D]
+// The graph's class-table rows (Pt, Qt, g_hsum) in LDS, ClassRows' slot order
+// with a row stride of CP + 4 floats: the lanes of a tile read 16 different
+// classes' rows, and a stride of CP = 32 / 48 words would put them all on the
+// same banks.
+template <int D>
+struct SlRows {
+  static constexpr int CP = ClassRows<D>::CP, S = CP + 4;
+  __device__ __forceinline__ static void stage(float* buf, const float* P, long long NT,
+                                               long long cn0, int ncl) {
+    for (int i = threadIdx.x; i < ncl * CP; i += PF_BLOCK) {
+      const int cl = i / CP, q = i - cl * CP;
+      const int h = GM<D>::row((q >> 2) & 3, 4 * (q >> 4) + (q & 3));
+      buf[cl * S + q] = h >= 0 ? P[(long long)h * NT + cn0 + cl] : 0.f;
+    }
+  }
+  __device__ __forceinline__ static floatx4 get(const float* buf, int cl, int t, int g) {
+    return *reinterpret_cast<const floatx4*>(buf + cl * S + 16 * t + 4 * g);
+  }
+};
+
+// A wave's class accumulator is [NC][D + 1]: the odd row stride spreads the
+// rows of different classes over the LDS banks (a stride of 20 or 40 words maps
+// every class row onto 16 / 8 bank offsets).
+template <int D>
+struct Acc {
+  static constexpr int S = D + 1;
+};
+// zero the 4 waves' class accumulators [4][NC][D + 1]
 __device__ __forceinline__ void acc_zero(float* acc, int len4) {
   for (int i = threadIdx.x; i < len4; i += PF_BLOCK) acc[i] = 0.f;
 }
-// the lane's edge vector (channels of its lane group, compact row map) into
-// its class's row of the wave's accumulator
+// The step's edge vectors (lane (g, j): the channels of lane group g of edge j,
+// compact row map) into their classes' rows of the wave's accumulator.  When
+// every valid edge of the tile has one class (complete-like slices) the 16
+// edges are summed across lanes first (DPP row sums, as km_target_fwd) and one
+// lane per group adds.  Otherwise the lanes add their own rows with plain LDS
+// read-add-writes, in rounds: each pending lane writes its edge index to its
+// class's owner slot; the lanes that read their own index back -- one edge per
+// class, the hardware's fixed choice among the writers -- add, the others wait
+// for the next round.  One wave's updates of a row thus happen in a fixed
+// order.  (Measured on the 30 % bench batch: LDS float atomics instead,
+// ~1 lane per 4 cycles on gfx950, 4-8x slower; ranks from DPP row rotations
+// instead of the owner slots, +7 %.)  `own`: the wave's [NC] owner table.
 template <int D>
-__device__ __forceinline__ void acc_add(float* wacc, int cl, bool ev, int g,
+__device__ __forceinline__ void acc_add(float* wacc, int* own, int cl, bool ev, int g, int j,
                                         const floatx4 (&v)[GM<D>::NT]) {
-  if (!ev) return;
-  float* a = wacc + cl * D;
+#ifdef SL_NO_ACC   // (timing experiment only: class sums dropped)
+  return;
+#endif
+  const uint64_t vm = __ballot(ev);
+  if (vm == 0) return;
+  const int c0 = __builtin_amdgcn_readlane(cl, (int)__builtin_ctzll(vm));
+  if (__ballot(ev && cl != c0) == 0) {
+    float* a = wacc + c0 * Acc<D>::S;
 #pragma unroll
-  for (int tt = 0; tt < GM<D>::NT; ++tt)
+    for (int tt = 0; tt < GM<D>::NT; ++tt)
 #pragma unroll
-    for (int r = 0; r < GM<D>::nreg(tt); ++r) {
-      const int h = GM<D>::row(g, 4 * tt + r);
-      if (h >= 0) atomicAdd(a + h, v[tt][r]);
+      for (int r = 0; r < GM<D>::nreg(tt); ++r) {
+        const float sum = row_sum16(ev ? v[tt][r] : 0.f);
+        const int h = GM<D>::row(g, 4 * tt + r);
+        if (j == 15 && h >= 0) a[h] += sum;
+      }
+    return;
+  }
+  float* a = wacc + cl * Acc<D>::S;
+  bool pend = ev;
+  while (__ballot(pend) != 0) {
+    if (pend) own[cl] = j;
+    lds_order();
+    const bool win = pend && own[cl] == j;
+    if (win) {
+#pragma unroll
+      for (int tt = 0; tt < GM<D>::NT; ++tt)
+#pragma unroll
+        for (int r = 0; r < GM<D>::nreg(tt); ++r) {
+          const int h = GM<D>::row(g, 4 * tt + r);
+          if (h >= 0) a[h] += v[tt][r];
+        }
     }
+    lds_order();
+    pend = pend && !win;
+  }
 }
 // the block's column partial of every class of its graph: 4-wave sums, fixed order
 template <int D>
 __device__ __forceinline__ void acc_flush(const float* acc, int NC, float* part, long long colbase) {
   __syncthreads();
-  const int len = NC * D;
+  const int len = NC * Acc<D>::S;
   float* p = part + colbase * D;
-  for (int i = threadIdx.x; i < len; i += PF_BLOCK)
-    p[i] = ((acc[i] + acc[len + i]) + acc[2 * len + i]) + acc[3 * len + i];
+  for (int i = threadIdx.x; i < NC * D; i += PF_BLOCK) {
+    const int c = i / D, q = c * Acc<D>::S + (i - c * D);
+    p[i] = ((acc[q] + acc[len + q]) + acc[2 * len + q]) + acc[3 * len + q];
+  }
 }
 
 // ============================================================ EdgeModel fwd
@@ -120,7 +195,7 @@ __global__ __launch_bounds__(256) void ksl_edge_mlp_fwd(
   constexpr int H = 4 * F, NT = GM<H>::NT;
   SL_GEO
   float* ptl = sl_dyn;   // [NC][CP]
-  ClassRows<H>::stage(ptl, PtS, geo.NT, (long long)gg * NC, NC);
+  SlRows<H>::stage(ptl, PtS, geo.NT, (long long)gg * NC, NC);
   FwdLayer<PREC, H, F> L1;
   L1.load([&](int h, int k) { return W1[h * 4 * F + 2 * F + k]; }, lane);
   FwdLayer<PREC, F, H> L2;
@@ -141,12 +216,12 @@ __global__ __launch_bounds__(256) void ksl_edge_mlp_fwd(
     r.c = SL_CLS(k);
     return r;
   };
-  class_stream<MF_DEPTH_FWD>(0, L, load, [&](const SRows<1>& rows, int k) {
+  class_stream<MF_DEPTH_FWD>(k0, k1, load, [&](const SRows<1>& rows, int k) {
     SL_STEP(rows)
     const floatx4 x[1] = {edge_in<F>(rows.v[0], fe, xsc, scv, shv)};
     floatx4 z[NT], a[NT];
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) z[tt] = ps[tt] + ClassRows<H>::get(ptl, cl, tt, g4);
+    for (int tt = 0; tt < NT; ++tt) z[tt] = ps[tt] + SlRows<H>::get(ptl, cl, tt, g4);
     L1.apply(x, z);
     lrelu_act<H>(z, a);
     floatx4 yo[1] = {bb};
@@ -212,10 +287,14 @@ __global__ __launch_bounds__(256) void ksl_edge_mlp_fwd(
 
 // ============================================================ SModel fwd
 // message m = Ws2 lrelu(Qt[c] + Ws1[:, F:2F] x) + bs2 (gnn.py:136-137) and the
-// fiber's centred moments by Pebay's one-pass update over its edges (count k + 1
-// at step k); the moments and SModel's features go straight to mom / hs with
-// the fiber's degree as count (gnn.py:140-151; an empty fiber: mean 0, var 0 as
-// scatter-mean's clamped count gives)
+// fiber's centred moments (gnn.py:140-151).  A block owns ONE slice; wave w
+// walks its steps k = w, w + 4, ... with Pebay's one-pass update (the i-th step
+// of a wave has count i + 1 in every lane whose fiber reaches it: a fiber's
+// edges are a prefix of the steps), then the 4 waves' states are merged per
+// fiber (Pebay's pairwise formula in double, fixed order 0 <- 1 <- 2 <- 3, the
+// per-lane counts) and the moments and SModel's features go straight to mom /
+// hs with the fiber's degree as count (an empty fiber: mean 0, var 0, as
+// scatter-mean's clamped count gives).
 template <int F, int PREC>
 __global__ __launch_bounds__(256) void ksl_source_fwd(
     EdgeGeo geo, SlGeo sl, const float* __restrict__ y, const float* __restrict__ sc,
@@ -223,9 +302,26 @@ __global__ __launch_bounds__(256) void ksl_source_fwd(
     const float* __restrict__ Ws2, const float* __restrict__ bs2, float* __restrict__ mom,
     float* __restrict__ hs) {
   constexpr int C = 2 * F, NT = GM<C>::NT;
-  SL_GEO
+  constexpr int MS = 4 * 4 * NT;   // a lane's merge state: 4 sums x NT tiles x 4 slots
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int g4 = lane >> 4, j16 = lane & 15;
+  const int slc = blockIdx.x;                    // one slice per block
+  const int gg = slc / (4 * geo.NFG);
+  const int fib = sl.fib[slc * 16 + j16];
+  const bool fvalid = fib >= 0;
+  const long long n = fvalid ? fib : 0;
+  const int pb = __builtin_amdgcn_readfirstlane(sl.base[slc]);
+  const int Ls = __builtin_amdgcn_readfirstlane(sl.len[slc]);
+  const int nw = (Ls - wave + 3) >> 2;           // this wave's steps
+  const int NC = geo.NC;
+  const long long NS = geo.NS;
+  const uint32_t RB = (uint32_t)geo.E * 4u, EB = RB;
+  const uint32_t eo0 = (uint32_t)(pb + j16) * 4u;
+  constexpr uint32_t eoc = 64u;
+  const Rsrc rcl = rsrc(sl.cls, (uint32_t)geo.E);
   float* qtl = sl_dyn;   // [NC][CP]
-  ClassRows<C>::stage(qtl, QtS, geo.NT, (long long)gg * NC, NC);
+  SlRows<C>::stage(qtl, QtS, geo.NT, (long long)gg * NC, NC);
   FwdLayer<PREC, C, F> L1;
   L1.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
   FwdLayer<PREC, C, C> L2;
@@ -241,26 +337,27 @@ __global__ __launch_bounds__(256) void ksl_source_fwd(
   for (int tt = 0; tt < NT; ++tt) S1[tt] = S2[tt] = S3[tt] = S4[tt] = zero4();
   float cnt = 0.f;
   __syncthreads();   // qtl
-  auto load = [&](int k) {
+  auto load = [&](int i) {
+    const int k = wave + 4 * i;
     SRows<1> r;
     r.v[0] = ld_frows<F>(ry, (uint32_t)k * eoc, ro);
     r.c = SL_CLS(k);
     return r;
   };
-  class_stream<MF_DEPTH_FWD>(0, L, load, [&](const SRows<1>& rows, int k) {
+  class_stream<MF_DEPTH_FWD>(0, nw, load, [&](const SRows<1>& rows, int i) {
     SL_STEP(rows)
     const floatx4 x[1] = {edge_in<F>(rows.v[0], fe, sc, scv, shv)};
     floatx4 z[NT], a[NT], m[NT];
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) z[tt] = ClassRows<C>::get(qtl, cl, tt, g4);
+    for (int tt = 0; tt < NT; ++tt) z[tt] = SlRows<C>::get(qtl, cl, tt, g4);
     L1.apply(x, z);
     lrelu_act<C>(z, a);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) m[tt] = bias[tt];
     L2.apply(a, m);
-    // Pebay's update (km_source_fwd), coefficients of count k + 1
-    const floatx4 ca = *reinterpret_cast<const floatx4*>(sl.pco + 8 * k);
-    const floatx4 cb = *reinterpret_cast<const floatx4*>(sl.pco + 8 * k + 4);
+    // Pebay's update (km_source_fwd), coefficients of count i + 1
+    const floatx4 ca = *reinterpret_cast<const floatx4*>(sl.pco + 8 * i);
+    const floatx4 cb = *reinterpret_cast<const floatx4*>(sl.pco + 8 * i + 4);
     if (ev) {
       cnt += 1.f;
 #pragma unroll
@@ -276,8 +373,26 @@ __global__ __launch_bounds__(256) void ksl_source_fwd(
         }
     }
   });
-  if (!fvalid) return;
-  const double invn = cnt > 0.f ? 1.0 / (double)cnt : 0.0;
+  // merge: waves 1..3 park their states and counts in LDS
+  __shared__ float ms[3][MS + 1][64];
+  if (wave > 0) {
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ms[wave - 1][(0 * NT + tt) * 4 + r][lane] = S1[tt][r];
+        ms[wave - 1][(1 * NT + tt) * 4 + r][lane] = S2[tt][r];
+        ms[wave - 1][(2 * NT + tt) * 4 + r][lane] = S3[tt][r];
+        ms[wave - 1][(3 * NT + tt) * 4 + r][lane] = S4[tt][r];
+      }
+    ms[wave - 1][MS][lane] = cnt;
+  }
+  __syncthreads();
+  if (wave != 0 || !fvalid) return;
+  double ntot = cnt;
+#pragma unroll
+  for (int w = 1; w < 4; ++w) ntot += ms[w - 1][MS][lane];
+  const double invn = ntot > 0 ? 1.0 / ntot : 0.0;
   const long long CNS = (long long)C * NS;
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt)
@@ -285,16 +400,26 @@ __global__ __launch_bounds__(256) void ksl_source_fwd(
     for (int r = 0; r < GM<C>::nreg(tt); ++r) {
       const int o = GM<C>::row(g4, 4 * tt + r);
       if (o < 0) continue;
+      double na = cnt, mean = S1[tt][r], M2 = S2[tt][r], M3 = S3[tt][r], M4 = S4[tt][r];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        const double nb = ms[w - 1][MS][lane];
+        if (nb <= 0) continue;
+        pebay_merge<double>(na, mean, M2, M3, M4, nb, ms[w - 1][(0 * NT + tt) * 4 + r][lane],
+                            ms[w - 1][(1 * NT + tt) * 4 + r][lane],
+                            ms[w - 1][(2 * NT + tt) * 4 + r][lane],
+                            ms[w - 1][(3 * NT + tt) * 4 + r][lane]);
+        na += nb;
+      }
       const long long idx = (long long)o * NS + n;
-      const float c2 = (float)(S2[tt][r] * invn), c3 = (float)(S3[tt][r] * invn),
-                  c4 = (float)(S4[tt][r] * invn);
-      mom[idx] = S1[tt][r];
+      const float c2 = (float)(M2 * invn), c3 = (float)(M3 * invn), c4 = (float)(M4 * invn);
+      mom[idx] = (float)mean;
       mom[CNS + idx] = c2;
       mom[2 * CNS + idx] = c3;
       mom[3 * CNS + idx] = c4;
       const float var = c2 > 0.f ? c2 : 0.01f * c2;  // F.leaky_relu (slope 0.01), gnn.py:141
       const float sd = sqrtf(var + 1e-6f);
-      hs[idx] = S1[tt][r];
+      hs[idx] = (float)mean;
       hs[CNS + idx] = sd;
       hs[2 * CNS + idx] = c3 / (sd * sd * sd);
       hs[3 * CNS + idx] = c4 / ((sd * sd) * (sd * sd));
@@ -311,9 +436,11 @@ __global__ __launch_bounds__(256) void ksl_target_fwd(
     float* __restrict__ part, uint8_t* __restrict__ tmask) {
   constexpr int C = 2 * F, NT = GM<C>::NT;
   SL_GEO
-  float* acc = sl_dyn;   // [4][NC][C]
-  acc_zero(acc, 4 * NC * C);
-  float* wacc = acc + wave * NC * C;
+  float* acc = sl_dyn;   // [4][NC][C + 1]
+  acc_zero(acc, 4 * NC * Acc<C>::S);
+  float* wacc = acc + wave * NC * Acc<C>::S;
+  __shared__ int owners[4][pfm::SL_MAX_NC];
+  int* own = owners[wave];
   FwdLayer<PREC, C, F> L1;
   L1.load([&](int h, int k) { return Wt1[h * 2 * F + F + k]; }, lane);
   floatx4 rs[NT];
@@ -329,7 +456,7 @@ __global__ __launch_bounds__(256) void ksl_target_fwd(
     r.c = SL_CLS(k);
     return r;
   };
-  class_stream<MF_DEPTH_FWD>(0, L, load, [&](const SRows<1>& rows, int k) {
+  class_stream<MF_DEPTH_FWD>(k0, k1, load, [&](const SRows<1>& rows, int k) {
     SL_STEP(rows)
     const floatx4 x[1] = {edge_in<F>(rows.v[0], fe, sc, scv, shv)};
     floatx4 z[NT], a[NT];
@@ -338,7 +465,7 @@ __global__ __launch_bounds__(256) void ksl_target_fwd(
     L1.apply(x, z);
     if (tmask) (tmask + (uint32_t)k * eoc)[opaque(eo0 + g4)] = (uint8_t)mask_bits<C>(z);
     lrelu_act<C>(z, a);
-    acc_add<C>(wacc, cl, ev, g4, a);
+    acc_add<C>(wacc, own, cl, ev, g4, j16, a);
   });
   acc_flush<C>(acc, NC, part, colbase);
 }
@@ -358,7 +485,7 @@ __global__ __launch_bounds__(256) void ksl_target_bwd(
   __shared__ short imgs[4 * NIMG * 2 * IMG_SHORTS];
   __shared__ float scratch[4 * C * F];
   float* ghl = sl_dyn;   // [NC][CP]
-  ClassRows<C>::stage(ghl, ghS, geo.NT, (long long)gg * NC, NC);
+  SlRows<C>::stage(ghl, ghS, geo.NT, (long long)gg * NC, NC);
   short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
   FwdLayer<FP(PREC), C, F> L1;
   if constexpr (!TM) L1.load([&](int h, int k) { return Wt1[h * 2 * F + F + k]; }, lane);
@@ -383,7 +510,7 @@ __global__ __launch_bounds__(256) void ksl_target_bwd(
     if constexpr (TM) r.m = __builtin_amdgcn_raw_buffer_load_b8(rtm, eo0 + g4, co, 0);
     return r;
   };
-  class_stream<MF_DEPTH_BWD>(0, L, load, [&](const SRows<1>& rows, int k) {
+  class_stream<MF_DEPTH_BWD>(k0, k1, load, [&](const SRows<1>& rows, int k) {
     SL_STEP(rows)
     const floatx4 x[1] = {edge_in<F>(rows.v[0], fe, sc, scv, shv)};
     floatx4 z[NT], gz[NT];
@@ -394,7 +521,7 @@ __global__ __launch_bounds__(256) void ksl_target_bwd(
     }
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      const floatx4 gh = ClassRows<C>::get(ghl, cl, tt, g4);
+      const floatx4 gh = SlRows<C>::get(ghl, cl, tt, g4);
       gz[tt] = zero4();
 #pragma unroll
       for (int r = 0; r < GM<C>::nreg(tt); ++r) {
@@ -427,7 +554,7 @@ __global__ __launch_bounds__(256) void ksl_target_bwd(
 #pragma unroll
       for (int r = 0; r < GM<C>::nreg(tt); ++r) {
         const int h = GM<C>::row(g4, 4 * tt + r);
-        if (h >= 0) GzT[(size_t)h * NS + n] = accF[tt][r];
+        if (h >= 0) GzT[(size_t)ks * C * NS + (size_t)h * NS + n] = accF[tt][r];
       }
   }
   block_partial(accW, scratch, C * F, [&](int a, int s, int jj) {
@@ -451,7 +578,7 @@ __global__ __launch_bounds__(256, 2) void ksl_source_bwd(
     const float* __restrict__ mu1, const float* __restrict__ inv1, float* __restrict__ g_tot,
     float* __restrict__ partW2, float* __restrict__ partW1, float* __restrict__ partCol,
     float* __restrict__ partBN, const uint8_t* __restrict__ tmask) {
-  constexpr int C = 2 * F, NT = GM<C>::NT, CP = ClassRows<C>::CP;
+  constexpr int C = 2 * F, NT = GM<C>::NT, CP = SlRows<C>::S;
   constexpr int NIMG = 3 * NT + 1;          // g_m | a | g_zs | x
   constexpr int SCR = C * (C + 1) > C * F ? C * (C + 1) : C * F;
   SL_GEO
@@ -459,11 +586,13 @@ __global__ __launch_bounds__(256, 2) void ksl_source_bwd(
   __shared__ float scratch[4 * SCR];
   float* qtl = sl_dyn;                  // [NC][CP]
   float* ghl = qtl + NC * CP;           // [NC][CP]
-  float* acc = ghl + NC * CP;           // [4][NC][C]
-  ClassRows<C>::stage(qtl, QtS, geo.NT, (long long)gg * NC, NC);
-  if (ghS) ClassRows<C>::stage(ghl, ghS, geo.NT, (long long)gg * NC, NC);
-  acc_zero(acc, 4 * NC * C);
-  float* wacc = acc + wave * NC * C;
+  float* acc = ghl + NC * CP;           // [4][NC][C + 1]
+  SlRows<C>::stage(qtl, QtS, geo.NT, (long long)gg * NC, NC);
+  if (ghS) SlRows<C>::stage(ghl, ghS, geo.NT, (long long)gg * NC, NC);
+  acc_zero(acc, 4 * NC * Acc<C>::S);
+  float* wacc = acc + wave * NC * Acc<C>::S;
+  __shared__ int owners[4][pfm::SL_MAX_NC];
+  int* own = owners[wave];
   short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
   short* im_gm = img;
   short* im_a = img + NT * 2 * IMG_SHORTS;
@@ -518,13 +647,13 @@ __global__ __launch_bounds__(256, 2) void ksl_source_bwd(
     if constexpr (TM) r.m = tpart ? __builtin_amdgcn_raw_buffer_load_b8(rtm, eo0 + g4, co, 0) : 0u;
     return r;
   };
-  class_stream<MF_DEPTH_BWD>(0, L, load, [&](const SRows<2>& rows, int k) {
+  class_stream<MF_DEPTH_BWD>(k0, k1, load, [&](const SRows<2>& rows, int k) {
     SL_STEP(rows)
     const floatx4 yr = rows.v[0], gnr = rows.v[1];
     const floatx4 x[1] = {edge_in<F>(yr, fe, sc, scv, shv)};
     floatx4 zs[NT], as[NT], m[NT];
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) zs[tt] = ClassRows<C>::get(qtl, cl, tt, g4);
+    for (int tt = 0; tt < NT; ++tt) zs[tt] = SlRows<C>::get(qtl, cl, tt, g4);
     L1s.apply(x, zs);
     lrelu_act<C>(zs, as);
 #pragma unroll
@@ -574,7 +703,7 @@ __global__ __launch_bounds__(256, 2) void ksl_source_bwd(
       }
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
-        const floatx4 gh = ClassRows<C>::get(ghl, cl, tt, g4);
+        const floatx4 gh = SlRows<C>::get(ghl, cl, tt, g4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float slp = TM ? mask_slope(rows.m, 4 * tt + r) : dlrelu(zt[tt][r]);
@@ -601,7 +730,7 @@ __global__ __launch_bounds__(256, 2) void ksl_source_bwd(
       }
     }
     // per-class sums of g_zs (the lane's own edge)
-    acc_add<C>(wacc, cl, ev, g4, gz);
+    acc_add<C>(wacc, own, cl, ev, g4, j16, gz);
     // weight gradients (edge = K) through the transposed images
     lds_order();
     const WgB tx = img_trB(im_x, lane);
@@ -667,17 +796,19 @@ __global__ __launch_bounds__(256, 2) void ksl_edge_mlp_bwd(
     const float* __restrict__ Ps, const float* __restrict__ PtS, const float* __restrict__ W1,
     const float* __restrict__ W2, float* __restrict__ gxe, float* __restrict__ GzEs,
     float* __restrict__ partW2, float* __restrict__ partW1, float* __restrict__ partCol) {
-  constexpr int H = 4 * F, NT = GM<H>::NT, CP = ClassRows<H>::CP;
+  constexpr int H = 4 * F, NT = GM<H>::NT, CP = SlRows<H>::S;
   constexpr int NIMG = 1 + NT + NT + 1;          // g_y | a | g_z | x
   constexpr int SCR = F * (H + 1) > H * F ? F * (H + 1) : H * F;
   SL_GEO
   __shared__ short imgs[4 * NIMG * 2 * IMG_SHORTS];
   __shared__ float scratch[4 * SCR];
   float* ptl = sl_dyn;              // [NC][CP]
-  float* acc = ptl + NC * CP;       // [4][NC][H]
-  ClassRows<H>::stage(ptl, PtS, geo.NT, (long long)gg * NC, NC);
-  acc_zero(acc, 4 * NC * H);
-  float* wacc = acc + wave * NC * H;
+  float* acc = ptl + NC * CP;       // [4][NC][H + 1]
+  SlRows<H>::stage(ptl, PtS, geo.NT, (long long)gg * NC, NC);
+  acc_zero(acc, 4 * NC * Acc<H>::S);
+  float* wacc = acc + wave * NC * Acc<H>::S;
+  __shared__ int owners[4][pfm::SL_MAX_NC];
+  int* own = owners[wave];
   short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
   short* im_gy = img;
   short* im_a = img + 2 * IMG_SHORTS;
@@ -715,7 +846,7 @@ __global__ __launch_bounds__(256, 2) void ksl_edge_mlp_bwd(
     r.c = SL_CLS(k);
     return r;
   };
-  class_stream<MF_DEPTH_BWD>(0, L, load, [&](const SRows<3>& rows, int k) {
+  class_stream<MF_DEPTH_BWD>(k0, k1, load, [&](const SRows<3>& rows, int k) {
     SL_STEP(rows)
     floatx4 gy[1] = {zero4()};
 #pragma unroll
@@ -726,7 +857,7 @@ __global__ __launch_bounds__(256, 2) void ksl_edge_mlp_bwd(
     floatx4 z[NT], a[NT], gz[NT];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      z[tt] = ps[tt] + ClassRows<H>::get(ptl, cl, tt, g4);
+      z[tt] = ps[tt] + SlRows<H>::get(ptl, cl, tt, g4);
       gz[tt] = zero4();
     }
     L1.apply(x, z);
@@ -755,7 +886,7 @@ __global__ __launch_bounds__(256, 2) void ksl_edge_mlp_bwd(
       if constexpr (PREC >= 1) L1T.apply(sgz, gx); else L1T.apply(gz, gx);
       st_frows<F>(gxe, (uint32_t)k * eoc, ro, g4, true, gx[0]);
     }
-    acc_add<H>(wacc, cl, ev, g4, gz);
+    acc_add<H>(wacc, own, cl, ev, g4, j16, gz);
     const s16x8 tgy = img_trA(im_gy, lane);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt)
@@ -771,7 +902,7 @@ __global__ __launch_bounds__(256, 2) void ksl_edge_mlp_bwd(
 #pragma unroll
       for (int r = 0; r < GM<H>::nreg(tt); ++r) {
         const int h = GM<H>::row(g4, 4 * tt + r);
-        if (h >= 0) GzEs[(size_t)h * NS + n] = accF[tt][r];
+        if (h >= 0) GzEs[(size_t)ks * H * NS + (size_t)h * NS + n] = accF[tt][r];
       }
   }
   acc_flush<H>(acc, NC, partCol, colbase);
@@ -803,13 +934,22 @@ __global__ __launch_bounds__(256, 2) void ksl_edge_mlp_bwd(
 // ============================================================ host launchers
 namespace pfm {
 
+// KS step splits per slice bring the grid near TARGET_BLOCKS (the backward
+// kernels hold one or two blocks per CU: their LDS class tables)
 EdgeGeo sl_geo(int G, int NF, int NC, const SlGeo& sl) {
   EdgeGeo g;
   g.G = G; g.NF = NF; g.NC = NC;
   g.NFG = (NF + 63) / 64;
-  g.KS = 1;
+  const long long groups = (long long)G * g.NFG;
+  static const int ks_env = [] {   // tuning knob: PFSGNN_SL_KS (step splits)
+    const char* e = getenv("PFSGNN_SL_KS");
+    return e ? atoi(e) : 0;
+  }();
+  long long ks = ks_env > 0 ? ks_env : (TARGET_BLOCKS / 2 + groups - 1) / groups;
+  ks = std::max<long long>(1, std::min<long long>(ks, std::min(8, std::max(1, sl.maxdeg / 8))));
+  g.KS = (int)ks;
   g.CPS = NC;
-  g.nblocks = G * g.NFG;
+  g.nblocks = (int)(groups * g.KS);
   g.E = sl.EP;
   g.NS = (long long)G * NF;
   g.NT = (long long)G * NC;
@@ -838,7 +978,7 @@ int sl_launch(K kernel, const EdgeGeo& geo, size_t lds, hipStream_t st, A... arg
   return 0;
 }
 
-constexpr int cp_of(int D) { return 16 * ((((D + 3) / 4) + 3) / 4); }   // ClassRows<D>::CP
+constexpr int cp_of(int D) { return 16 * ((((D + 3) / 4) + 3) / 4) + 4; }   // SlRows<D>::S
 
 }  // namespace
 
@@ -868,9 +1008,12 @@ int sl_source_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, co
                   const float* sh, const float* QtS, const float* Ws1, const float* Ws2,
                   const float* bs2, float* mom, float* hs, int prec, hipStream_t st) {
   const size_t lds = (size_t)geo.NC * cp_of(2 * F) * sizeof(float);
+  EdgeGeo g1 = geo;   // one block per slice (its 4 waves interleave the steps)
+  g1.KS = 1;
+  g1.nblocks = geo.G * geo.NFG * 4;
 #define SL_C(FF, PP)                                                                        \
   case FF * 8 + PP:                                                                         \
-    return sl_launch(ksl_source_fwd<FF, PP>, geo, lds, st, geo, sl, y, sc, sh, QtS, Ws1, Ws2, \
+    return sl_launch(ksl_source_fwd<FF, PP>, g1, lds, st, g1, sl, y, sc, sh, QtS, Ws1, Ws2, \
                      bs2, mom, hs);
   SL_SWITCH(F, FP(prec), SL_C)
 #undef SL_C
@@ -879,7 +1022,7 @@ int sl_source_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, co
 int sl_target_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, const float* sc,
                   const float* sh, const float* Rs, const float* Wt1, float* part, uint8_t* tmask,
                   int prec, hipStream_t st) {
-  const size_t lds = (size_t)4 * geo.NC * 2 * F * sizeof(float);
+  const size_t lds = (size_t)4 * geo.NC * (2 * F + 1) * sizeof(float);
 #define SL_C(FF, PP)                                                                        \
   case FF * 8 + PP:                                                                         \
     return sl_launch(ksl_target_fwd<FF, PP>, geo, lds, st, geo, sl, y, sc, sh, Rs, Wt1, part, \
@@ -908,7 +1051,7 @@ int sl_source_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, co
                   const float* Wt1, const float* ghS, const float* g_next, const float* mu1,
                   const float* inv1, float* g_tot, float* pW2, float* pW1, float* pCol,
                   float* pBN, const uint8_t* tmask, int prec, hipStream_t st) {
-  const size_t lds = (size_t)geo.NC * (2 * cp_of(2 * F) + 4 * 2 * F) * sizeof(float);
+  const size_t lds = (size_t)geo.NC * (2 * cp_of(2 * F) + 4 * (2 * F + 1)) * sizeof(float);
   const bool tm = tmask && Rs;
 #define SL_C(FF, PP)                                                                        \
   case FF * 8 + PP:                                                                         \
@@ -927,7 +1070,7 @@ int sl_edge_mlp_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* g_t
                     const float* xe, const float* xsc, const float* xsh, const float* Ps,
                     const float* PtS, const float* W1, const float* W2, float* gxe, float* gs,
                     float* pW2, float* pW1, float* pCol, int prec, hipStream_t st) {
-  const size_t lds = (size_t)geo.NC * (cp_of(4 * F) + 4 * 4 * F) * sizeof(float);
+  const size_t lds = (size_t)geo.NC * (cp_of(4 * F) + 4 * (4 * F + 1)) * sizeof(float);
 #define SL_C(FF, PP)                                                                         \
   case FF * 8 + PP:                                                                          \
     return sl_launch(ksl_edge_mlp_bwd<FF, PP>, geo, lds, st, geo, sl, g_tot, alpha, gam0, gam1, \

@@ -70,7 +70,13 @@ def run(density, label):
         step()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t) / STEPS * 1e3
-    print(f"{label:34s} E={E:9d}  {ms:8.2f} ms/step  {E / ms / 1e3:8.1f} M edges/s", flush=True)
+    from pfsgnn import gnn as gmod
+    pad = ""
+    for e in gmod._LAYOUT_CACHE.d.values():
+        if e[0]() is data.edge_index and e[3].sp is not None and e[3].sp.sl is not None:
+            pad = f"  EP/E {e[3].sp.sl.EP / E:.3f}"
+    print(f"{label:34s} E={E:9d}  {ms:8.2f} ms/step  {E / ms / 1e3:8.1f} M edges/s{pad}",
+          flush=True)
 
 
 dens = [float(x) for x in os.environ.get("SPARSE_DENSITIES", "1.0,0.999,0.3,0.05").split(",")]
