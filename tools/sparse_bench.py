@@ -24,7 +24,7 @@ G = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 NF = int(sys.argv[2]) if len(sys.argv) > 2 else 2394
 NC = int(sys.argv[3]) if len(sys.argv) > 3 else 128
 B = int(sys.argv[4]) if len(sys.argv) > 4 else 8
-STEPS = int(sys.argv[5]) if len(sys.argv) > 5 else 10
+STEPS = int(sys.argv[5]) if len(sys.argv) > 5 else 20
 F = 10
 config.device = torch.device("cuda")
 gen = torch.Generator().manual_seed(0)
@@ -62,14 +62,19 @@ def run(density, label):
         loss.backward()
         opt.step()
 
+    for _ in range(5):
+        step()
+    # median of 3 timed runs of STEPS steps (one short run swings by +-30 % on a
+    # shared box)
+    runs = []
     for _ in range(3):
-        step()
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(STEPS):
-        step()
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t) / STEPS * 1e3
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(STEPS):
+            step()
+        torch.cuda.synchronize()
+        runs.append((time.perf_counter() - t) / STEPS * 1e3)
+    ms = sorted(runs)[1]
     from pfsgnn import gnn as gmod
     pad = ""
     for e in gmod._LAYOUT_CACHE.d.values():
