@@ -56,9 +56,10 @@ int edge_mlp_bwd(const EdgeGeo& geo, int F, const float* g_tot, const float* alp
 // include/pfsgnn.h pfsgnn_sliced_t): slice s = 16 fibers of one graph, the k-th
 // edge of lane j at position base[s] + 16 k + j for k < len[s]; cls[p] the class
 // within its graph of position p (0xFF: padding).  The kernels take the
-// complete path's EdgeGeo with KS = 1, NFG = ceil(NF / 64) blocks per graph
-// (4 slices per block) and E = EP (edge-tensor columns), and write the same
-// per-block partials, so every finishing reduction is shared.
+// complete path's EdgeGeo with NFG = ceil(NF / 64) 4-slice groups per graph,
+// KS step splits per slice (sl_geo) and E = EP (edge-tensor columns), and write
+// the same per-block partials (class partials: one row per split), so every
+// finishing reduction is shared.
 struct SlGeo {
   const int* fib;        // [nslices * 16] global fiber of each lane, -1: none
   const int* base;       // [nslices]
@@ -89,7 +90,11 @@ int sl_source_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, co
                   const float* bs2, const float* mean, const float* coef, const float* Rs,
                   const float* Wt1, const float* ghS, const float* g_next, const float* mu1,
                   const float* inv1, float* g_tot, float* pW2, float* pW1, float* pCol,
-                  float* pBN, const uint8_t* tmask, int prec, hipStream_t st);
+                  float* pBN, const uint8_t* tmask, float* tabs, int prec, hipStream_t st);
+// (tabs: workspace for the two class tables in global memory, sl_tab_floats)
+static inline long long sl_tab_floats(const EdgeGeo& geo, int F) {
+  return 2 * geo.NT * 16 * ((((2 * F + 3) / 4) + 3) / 4);
+}
 int sl_edge_mlp_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* g_tot,
                     const float* alpha, const float* gam0, const float* gam1, const float* y,
                     const float* xe, const float* xsc, const float* xsh, const float* Ps,

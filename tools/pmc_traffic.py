@@ -53,7 +53,7 @@ def per_dispatch(path, counter):
             # paths): <F, PREC[, TM]>, the forward kernels' PREC being 0 for it
             tmpl = full.split("<")[1].split(">")[0].split(",")
             want = ("0" if PREC == "1" else PREC) if kname(full).split("<")[0] in (
-                "km_edge_mlp_fwd", "km_source_fwd", "km_target_fwd") else PREC
+                "km_edge_mlp_fwd", "km_source_fwd", "km_source_fwd_ft", "km_target_fwd") else PREC
             if tmpl[1].strip() != want:
                 continue
         k = kname(r["Kernel_Name"])
@@ -67,6 +67,7 @@ def algorithmic(kernel):
     import bench
     per = bench.kernel_bytes_per_edge(F)
     base = kernel.split("<")[0].replace("km_", "").replace("k_", "")
+    base = {"source_fwd_ft": "source_fwd"}.get(base, base)   # (the fiber-tile grid: same bytes)
     if base not in per:
         return None
     if base == "edge_mlp_bwd":          # block 0 writes no input gradient
