@@ -123,6 +123,14 @@ def kernel_flops_per_edge(F, B):
     }
 
 
+# the part of kernel_flops_per_edge that recomputes forward activations (the
+# backward kernels keep no per-edge hidden state): EdgeModel's first Linear in
+# edge_mlp_bwd, SModel's message MLP in source_bwd
+def recompute_flops_per_edge(F):
+    H, C = 4 * F, 2 * F
+    return {"edge_mlp_bwd": 2 * H * F, "source_bwd": 2 * (C * F + C * C)}
+
+
 def pmc_traffic(kernel, E, F):
     """HBM bytes per launch of `kernel` from the latest committed PMC pass
     (profiles/<round>_traffic.json, made by tools/prof_pmc.sh +
@@ -386,8 +394,11 @@ def main():
     mfma = None
     if flops is not None:
         tfs = flops * E / avg_s / 1e12
+        rc = recompute_flops_per_edge(FDIM).get(dom, 0)
         mfma = {"achieved": round(tfs, 2), "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                "frac": round(tfs / F32_MFMA_PEAK_TFS, 4), "flops_per_launch": int(flops * E)}
+                "frac": round(tfs / F32_MFMA_PEAK_TFS, 4), "flops_per_launch": int(flops * E),
+                # the same without the forward recompute's flops
+                "frac_excl_recompute": round(tfs * (flops - rc) / flops / F32_MFMA_PEAK_TFS, 4)}
     top = mfma if mfma is not None and mfma["frac"] > hbm["frac"] else hbm
     roofline = {"bound": "mfma" if top is mfma else "hbm", "kernel": dom,
                 "achieved": top["achieved"], "peak": top["peak"], "unit": top["unit"],
