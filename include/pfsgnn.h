@@ -458,13 +458,15 @@ int pfsgnn_rows_axpby(const float* g, const float* y, int C, long long N, const 
  * slice lane j at position base[s] + 16 k + j for k < len[s] (the slice's
  * largest degree); a fiber with fewer edges leaves padding positions.  Edge
  * tensors are channel-major [C][EP] over these positions and hold 0 at padding.
- * Slice s = 4 b + w is wave w of block b = g * ceil(NF/64) + (its 64-fiber
- * group), so the pfsgnn_sl_* edge ops below run the complete path's grid with
- * one class split and share its reductions; they take the same arguments and
- * give the same outputs as the complete-graph op of the same name (G, NF, NC:
- * the batch's graphs and per-graph node counts), plus the layout.  NC <= 128
- * classes per graph; Fdim 8, 10, 16.  (Replaces torch_scatter.scatter, x[src],
- * x[tgt] of gnn.py:100, 136-144, 188-190 for such graphs, fused.) */
+ * Slices 4 q .. 4 q + 3 are the 4 waves of the blocks of 64-fiber group q =
+ * g * ceil(NF/64) + (its group in graph g), each block taking one of KS step
+ * splits, so the pfsgnn_sl_* edge ops below run the complete path's grid
+ * shape and share its reductions; they take the same arguments and give the
+ * same outputs as the complete-graph op of the same name (G, NF, NC: the
+ * batch's graphs and per-graph node counts), plus the layout.  NC <= 128
+ * classes per graph; Fdim 8, 10, 16; the workspace of pfsgnn_workspace_bytes.
+ * (Replaces torch_scatter.scatter, x[src], x[tgt] of gnn.py:100, 136-144,
+ * 188-190 for such graphs, fused.) */
 typedef struct {
   const int* fib;            /* [G*ceil(NF/64)*4*16] global fiber of each slice lane, -1: none */
   const int* base;           /* [G*ceil(NF/64)*4] first position of each slice */

@@ -1483,8 +1483,10 @@ static int edge_mlp_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, i
   if (sl) {
     PF_REQUIRE(part, "pfsgnn_edge_mlp_fwd", "workspace too small");
     { pf::Timer tm_("edge_mlp_fwd", st);
+    float* tabs = w.take((size_t)pfm::sl_tab_floats(geo, F));
+    PF_REQUIRE(tabs, "pfsgnn_edge_mlp_fwd", "workspace too small");
     if (int rc = pfm::sl_edge_mlp_fwd(geo, sl_of(*sl), F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part,
-                                      mf_prec(0), st))
+                                      tabs, mf_prec(0), st))
       return rc;
     tm_.end(); }
     hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(256), 0, st, part, geo.nblocks, F, sl->E,
@@ -1574,7 +1576,9 @@ static int source_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
   hipStream_t st = as_stream(stream);
   if (sl) {   // moments straight to mom / hs (per-fiber counts: the degrees)
     pf::Timer tm_("source_fwd", st);
-    if (int rc = pfm::sl_source_fwd(geo, sl_of(*sl), F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs,
+    float* tabs = w.take((size_t)pfm::sl_tab_floats(geo, F));
+    PF_REQUIRE(tabs, "pfsgnn_source_fwd", "workspace too small");
+    if (int rc = pfm::sl_source_fwd(geo, sl_of(*sl), F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs, tabs,
                                     mf_prec(1), st))
       return rc;
     tm_.end();
@@ -1711,8 +1715,10 @@ static int target_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
   PF_REQUIRE(part && gz && ghT, "pfsgnn_target_bwd", "workspace too small");
   { pf::Timer tm_("target_bwd", st);
   if (sl) {
+    float* tabs = w.take((size_t)pfm::sl_tab_floats(geo, F));
+    PF_REQUIRE(tabs, "pfsgnn_target_bwd", "workspace too small");
     if (int rc = pfm::sl_target_bwd(geo, sl_of(*sl), F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part,
-                                    tmask, mf_prec(1), st))
+                                    tmask, tabs, mf_prec(1), st))
       return rc;
   } else if (use_mfma()) {
     if (int rc = pfm::target_bwd(geo, F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part, tmask,
@@ -1903,9 +1909,11 @@ static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
              "workspace too small");
   { pf::Timer tm_("source_bwd", st);
   if (sl) {
+    float* tabs = w.take((size_t)pfm::sl_tab_floats(geo, F));
+    PF_REQUIRE(tabs, "pfsgnn_source_bwd", "workspace too small");
     if (int rc = pfm::sl_source_bwd(geo, sl_of(*sl), F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef,
                                     Rs, Wt1, ghT, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN,
-                                    tmask, mf_prec(1), st))
+                                    tmask, tabs, mf_prec(1), st))
       return rc;
   } else if (mfma) {
     if (int rc = pfm::source_bwd(geo, F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT,
@@ -1995,9 +2003,11 @@ static int edge_mlp_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, i
   if (sl) {
     PF_REQUIRE(pW2 && pW1 && pCol && gs, "pfsgnn_edge_mlp_bwd", "workspace too small");
     pf::Timer tm_("edge_mlp_bwd", st);
+    float* tabs = w.take((size_t)pfm::sl_tab_floats(geo, F));
+    PF_REQUIRE(tabs, "pfsgnn_edge_mlp_bwd", "workspace too small");
     if (int rc = pfm::sl_edge_mlp_bwd(geo, sl_of(*sl), F, g_tot, alpha, gam0, gam1, y, xe, xsc,
-                                      xsh, Ps, Pt, W1, W2, gxe, gs, pW2, pW1, pCol, mf_prec(0),
-                                      st))
+                                      xsh, Ps, Pt, W1, W2, gxe, gs, pW2, pW1, pCol, tabs,
+                                      mf_prec(0), st))
       return rc;
     tm_.end();
   } else if (use_mfma()) {

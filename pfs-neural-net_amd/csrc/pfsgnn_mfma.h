@@ -73,32 +73,36 @@ static constexpr int SL_MAX_NC = 128;   // classes per graph (LDS class rows + a
 EdgeGeo sl_geo(int G, int NF, int NC, const SlGeo& sl);
 int sl_edge_mlp_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* xe, const float* xsc,
                     const float* xsh, const float* Ps, const float* PtS, const float* W1,
-                    const float* W2, const float* b2, float* y, float* part, int prec,
-                    hipStream_t st);
+                    const float* W2, const float* b2, float* y, float* part, float* tabs,
+                    int prec, hipStream_t st);
 // moments straight to mom / hs (per-fiber counts: the fiber degrees)
 int sl_source_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, const float* sc,
                   const float* sh, const float* QtS, const float* Ws1, const float* Ws2,
-                  const float* bs2, float* mom, float* hs, int prec, hipStream_t st);
+                  const float* bs2, float* mom, float* hs, float* tabs, int prec,
+                  hipStream_t st);
 int sl_target_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, const float* sc,
                   const float* sh, const float* Rs, const float* Wt1, float* part, uint8_t* tmask,
                   int prec, hipStream_t st);
 int sl_target_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, const float* sc,
                   const float* sh, const float* Rs, const float* Wt1, const float* ghS, float* gz,
-                  float* gxe, float* part, const uint8_t* tmask, int prec, hipStream_t st);
+                  float* gxe, float* part, const uint8_t* tmask, float* tabs, int prec,
+                  hipStream_t st);
 int sl_source_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, const float* sc,
                   const float* sh, const float* QtS, const float* Ws1, const float* Ws2,
                   const float* bs2, const float* mean, const float* coef, const float* Rs,
                   const float* Wt1, const float* ghS, const float* g_next, const float* mu1,
                   const float* inv1, float* g_tot, float* pW2, float* pW1, float* pCol,
                   float* pBN, const uint8_t* tmask, float* tabs, int prec, hipStream_t st);
-// (tabs: workspace for the two class tables in global memory, sl_tab_floats)
+// (tabs: workspace for the class tables in global memory, sl_tab_floats
+// floats: source_bwd's two C-wide ones, or one H-wide one)
 static inline long long sl_tab_floats(const EdgeGeo& geo, int F) {
-  return 2 * geo.NT * 16 * ((((2 * F + 3) / 4) + 3) / 4);
+  const long long c = 16 * ((((2 * F + 3) / 4) + 3) / 4), h = 16 * ((((4 * F + 3) / 4) + 3) / 4);
+  return geo.NT * (2 * c > h ? 2 * c : h);
 }
 int sl_edge_mlp_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* g_tot,
                     const float* alpha, const float* gam0, const float* gam1, const float* y,
                     const float* xe, const float* xsc, const float* xsh, const float* Ps,
                     const float* PtS, const float* W1, const float* W2, float* gxe, float* gs,
-                    float* pW2, float* pW1, float* pCol, int prec, hipStream_t st);
+                    float* pW2, float* pW1, float* pCol, float* tabs, int prec, hipStream_t st);
 
 }  // namespace pfm

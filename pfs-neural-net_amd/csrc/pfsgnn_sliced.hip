@@ -72,7 +72,7 @@ struct SRows {
   /* class partials [G][NFG * KS][NC][D] (columns_lin with NFG * KS blocks per graph) */ \
   const long long colbase = ((long long)grp * geo.KS + ks) * NC;                       \
   const Rsrc rcl = rsrc(sl.cls, (uint32_t)geo.E);                                      \
-  (void)t; (void)n; (void)NS; (void)colbase; (void)EB; (void)fg; (void)k0; (void)k1;
+  (void)t; (void)n; (void)NS; (void)colbase; (void)EB; (void)fg; (void)gg; (void)k0; (void)k1;
 
 // the class byte of step k of the lane's fiber
 #define SL_CLS(k) \
@@ -115,6 +115,45 @@ template <int D>
 struct Acc {
   static constexpr int S = D + 1;
 };
+// The class rows of every graph in ClassRows' slot order in global memory,
+// [G*NC][CP] (k_sl_rows_table): ksl_source_bwd reads its two tables from there
+// (L2-resident, 16 B per lane and tile) instead of LDS, which leaves it room
+// for two blocks per CU.
+template <int D>
+__global__ __launch_bounds__(256) void k_sl_rows_table(const float* __restrict__ P, long long NT,
+                                                       float* __restrict__ out) {
+  constexpr int CP = ClassRows<D>::CP;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= NT * CP) return;
+  const long long c = i / CP;
+  const int q = (int)(i - c * CP);
+  const int h = GM<D>::row((q >> 2) & 3, 4 * (q >> 4) + (q & 3));
+  out[i] = h >= 0 ? P[(long long)h * NT + c] : 0.f;
+}
+template <int D>
+__device__ __forceinline__ floatx4 tab_get(const float* tab, long long c, int t, int g) {
+  return *reinterpret_cast<const floatx4*>(tab + c * ClassRows<D>::CP + 16 * t + 4 * g);
+}
+
+// Class rows of the edge kernels: staged in LDS per block (default), or read
+// from the permuted global tables (SL_GLOBAL_TABLES, the A/B variant: no
+// per-block staging, but an L2 round trip per tile; measured on the 30 % /
+// 99.9 % bench batches: 3 % / 9 % slower; ksl_source_bwd always reads its two
+// tables from global memory, which leaves it LDS for two blocks per CU).
+// CROWS_DECL(buf, P) prepares, CROW(buf, P, cl, t) reads tile t of class cl
+// (within the block's graph gg).
+#ifndef SL_GLOBAL_TABLES
+#define CROWS_DECL(D, buf, P, base)                                  \
+  float* buf = base;                                                 \
+  SlRows<D>::stage(buf, P, geo.NT, (long long)gg * NC, NC);
+#define CROW(D, buf, P, cl, t) SlRows<D>::get(buf, cl, t, g4)
+#define CROWS_FLOATS(D) (SlRows<D>::S)
+#else
+#define CROWS_DECL(D, buf, P, base) const long long buf = (long long)gg * NC; (void)base;
+#define CROW(D, buf, P, cl, t) tab_get<D>(P, buf + (cl), t, g4)
+#define CROWS_FLOATS(D) 0
+#endif
+
 // zero the 4 waves' class accumulators [4][NC][D + 1]
 __device__ __forceinline__ void acc_zero(float* acc, int len4) {
   for (int i = threadIdx.x; i < len4; i += PF_BLOCK) acc[i] = 0.f;
@@ -194,8 +233,7 @@ __global__ __launch_bounds__(256) void ksl_edge_mlp_fwd(
     float* __restrict__ y, float* __restrict__ part) {
   constexpr int H = 4 * F, NT = GM<H>::NT;
   SL_GEO
-  float* ptl = sl_dyn;   // [NC][CP]
-  SlRows<H>::stage(ptl, PtS, geo.NT, (long long)gg * NC, NC);
+  CROWS_DECL(H, ptl, PtS, sl_dyn)   // [NC][CP]
   FwdLayer<PREC, H, F> L1;
   L1.load([&](int h, int k) { return W1[h * 4 * F + 2 * F + k]; }, lane);
   FwdLayer<PREC, F, H> L2;
@@ -221,7 +259,7 @@ __global__ __launch_bounds__(256) void ksl_edge_mlp_fwd(
     const floatx4 x[1] = {edge_in<F>(rows.v[0], fe, xsc, scv, shv)};
     floatx4 z[NT], a[NT];
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) z[tt] = ps[tt] + SlRows<H>::get(ptl, cl, tt, g4);
+    for (int tt = 0; tt < NT; ++tt) z[tt] = ps[tt] + CROW(H, ptl, PtS, cl, tt);
     L1.apply(x, z);
     lrelu_act<H>(z, a);
     floatx4 yo[1] = {bb};
@@ -320,8 +358,7 @@ __global__ __launch_bounds__(256) void ksl_source_fwd(
   const uint32_t eo0 = (uint32_t)(pb + j16) * 4u;
   constexpr uint32_t eoc = 64u;
   const Rsrc rcl = rsrc(sl.cls, (uint32_t)geo.E);
-  float* qtl = sl_dyn;   // [NC][CP]
-  SlRows<C>::stage(qtl, QtS, geo.NT, (long long)gg * NC, NC);
+  CROWS_DECL(C, qtl, QtS, sl_dyn)   // [NC][CP]
   FwdLayer<PREC, C, F> L1;
   L1.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
   FwdLayer<PREC, C, C> L2;
@@ -349,7 +386,7 @@ __global__ __launch_bounds__(256) void ksl_source_fwd(
     const floatx4 x[1] = {edge_in<F>(rows.v[0], fe, sc, scv, shv)};
     floatx4 z[NT], a[NT], m[NT];
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) z[tt] = SlRows<C>::get(qtl, cl, tt, g4);
+    for (int tt = 0; tt < NT; ++tt) z[tt] = CROW(C, qtl, QtS, cl, tt);
     L1.apply(x, z);
     lrelu_act<C>(z, a);
 #pragma unroll
@@ -484,8 +521,7 @@ __global__ __launch_bounds__(256) void ksl_target_bwd(
   SL_GEO
   __shared__ short imgs[4 * NIMG * 2 * IMG_SHORTS];
   __shared__ float scratch[4 * C * F];
-  float* ghl = sl_dyn;   // [NC][CP]
-  SlRows<C>::stage(ghl, ghS, geo.NT, (long long)gg * NC, NC);
+  CROWS_DECL(C, ghl, ghS, sl_dyn)   // [NC][CP]
   short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
   FwdLayer<FP(PREC), C, F> L1;
   if constexpr (!TM) L1.load([&](int h, int k) { return Wt1[h * 2 * F + F + k]; }, lane);
@@ -521,7 +557,7 @@ __global__ __launch_bounds__(256) void ksl_target_bwd(
     }
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      const floatx4 gh = SlRows<C>::get(ghl, cl, tt, g4);
+      const floatx4 gh = CROW(C, ghl, ghS, cl, tt);
       gz[tt] = zero4();
 #pragma unroll
       for (int r = 0; r < GM<C>::nreg(tt); ++r) {
@@ -578,17 +614,15 @@ __global__ __launch_bounds__(256, 2) void ksl_source_bwd(
     const float* __restrict__ mu1, const float* __restrict__ inv1, float* __restrict__ g_tot,
     float* __restrict__ partW2, float* __restrict__ partW1, float* __restrict__ partCol,
     float* __restrict__ partBN, const uint8_t* __restrict__ tmask) {
-  constexpr int C = 2 * F, NT = GM<C>::NT, CP = SlRows<C>::S;
+  constexpr int C = 2 * F, NT = GM<C>::NT;
   constexpr int NIMG = 3 * NT + 1;          // g_m | a | g_zs | x
   constexpr int SCR = C * (C + 1) > C * F ? C * (C + 1) : C * F;
   SL_GEO
   __shared__ short imgs[4 * NIMG * 2 * IMG_SHORTS];
   __shared__ float scratch[4 * SCR];
-  float* qtl = sl_dyn;                  // [NC][CP]
-  float* ghl = qtl + NC * CP;           // [NC][CP]
-  float* acc = ghl + NC * CP;           // [4][NC][C + 1]
-  SlRows<C>::stage(qtl, QtS, geo.NT, (long long)gg * NC, NC);
-  if (ghS) SlRows<C>::stage(ghl, ghS, geo.NT, (long long)gg * NC, NC);
+  // QtS / ghS: the class tables in k_sl_rows_table's layout [G*NC][CP]
+  float* acc = sl_dyn;                  // [4][NC][C + 1]
+  const long long gc0 = (long long)gg * NC;
   acc_zero(acc, 4 * NC * Acc<C>::S);
   float* wacc = acc + wave * NC * Acc<C>::S;
   __shared__ int owners[4][pfm::SL_MAX_NC];
@@ -653,7 +687,7 @@ __global__ __launch_bounds__(256, 2) void ksl_source_bwd(
     const floatx4 x[1] = {edge_in<F>(yr, fe, sc, scv, shv)};
     floatx4 zs[NT], as[NT], m[NT];
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) zs[tt] = SlRows<C>::get(qtl, cl, tt, g4);
+    for (int tt = 0; tt < NT; ++tt) zs[tt] = tab_get<C>(QtS, gc0 + cl, tt, g4);
     L1s.apply(x, zs);
     lrelu_act<C>(zs, as);
 #pragma unroll
@@ -703,7 +737,7 @@ __global__ __launch_bounds__(256, 2) void ksl_source_bwd(
       }
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
-        const floatx4 gh = SlRows<C>::get(ghl, cl, tt, g4);
+        const floatx4 gh = tab_get<C>(ghS, gc0 + cl, tt, g4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float slp = TM ? mask_slope(rows.m, 4 * tt + r) : dlrelu(zt[tt][r]);
@@ -796,15 +830,14 @@ __global__ __launch_bounds__(256, 2) void ksl_edge_mlp_bwd(
     const float* __restrict__ Ps, const float* __restrict__ PtS, const float* __restrict__ W1,
     const float* __restrict__ W2, float* __restrict__ gxe, float* __restrict__ GzEs,
     float* __restrict__ partW2, float* __restrict__ partW1, float* __restrict__ partCol) {
-  constexpr int H = 4 * F, NT = GM<H>::NT, CP = SlRows<H>::S;
+  constexpr int H = 4 * F, NT = GM<H>::NT;
   constexpr int NIMG = 1 + NT + NT + 1;          // g_y | a | g_z | x
   constexpr int SCR = F * (H + 1) > H * F ? F * (H + 1) : H * F;
   SL_GEO
   __shared__ short imgs[4 * NIMG * 2 * IMG_SHORTS];
   __shared__ float scratch[4 * SCR];
-  float* ptl = sl_dyn;              // [NC][CP]
-  float* acc = ptl + NC * CP;       // [4][NC][H + 1]
-  SlRows<H>::stage(ptl, PtS, geo.NT, (long long)gg * NC, NC);
+  CROWS_DECL(H, ptl, PtS, sl_dyn)             // [NC][CP]
+  float* acc = sl_dyn + NC * CROWS_FLOATS(H);  // [4][NC][H + 1]
   acc_zero(acc, 4 * NC * Acc<H>::S);
   float* wacc = acc + wave * NC * Acc<H>::S;
   __shared__ int owners[4][pfm::SL_MAX_NC];
@@ -857,7 +890,7 @@ __global__ __launch_bounds__(256, 2) void ksl_edge_mlp_bwd(
     floatx4 z[NT], a[NT], gz[NT];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      z[tt] = ps[tt] + SlRows<H>::get(ptl, cl, tt, g4);
+      z[tt] = ps[tt] + CROW(H, ptl, PtS, cl, tt);
       gz[tt] = zero4();
     }
     L1.apply(x, z);
@@ -979,6 +1012,29 @@ int sl_launch(K kernel, const EdgeGeo& geo, size_t lds, hipStream_t st, A... arg
 }
 
 constexpr int cp_of(int D) { return 16 * ((((D + 3) / 4) + 3) / 4) + 4; }   // SlRows<D>::S
+constexpr int cpg_of(int D) { return 16 * ((((D + 3) / 4) + 3) / 4); }      // ClassRows<D>::CP
+
+// P [D][NT] -> the permuted global table [NT][CP] (k_sl_rows_table)
+int rows_table(int D, const float* P, long long NT, float* out, hipStream_t st) {
+  const unsigned nb = (unsigned)((NT * cpg_of(D) + 255) / 256);
+  switch (D) {
+#define RT(DD) case DD: hipLaunchKernelGGL(k_sl_rows_table<DD>, dim3(nb), dim3(256), 0, st, P, NT, out); break;
+    RT(16) RT(20) RT(32) RT(40) RT(64)
+#undef RT
+    default: return pf::fail("pfsgnn sliced", "unsupported class-table width");
+  }
+  return 0;
+}
+#ifndef SL_GLOBAL_TABLES
+constexpr bool kGTab = false;
+#else
+constexpr bool kGTab = true;
+#endif
+// the lds bytes of a kernel's class table, and the table it reads (staged from
+// P in LDS, or P permuted into `tabs`)
+inline size_t tab_lds(const EdgeGeo& geo, int D) {
+  return kGTab ? 0 : (size_t)geo.NC * cp_of(D) * sizeof(float);
+}
 
 }  // namespace
 
@@ -993,9 +1049,13 @@ constexpr int cp_of(int D) { return 16 * ((((D + 3) / 4) + 3) / 4) + 4; }   // S
 
 int sl_edge_mlp_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* xe, const float* xsc,
                     const float* xsh, const float* Ps, const float* PtS, const float* W1,
-                    const float* W2, const float* b2, float* y, float* part, int prec,
-                    hipStream_t st) {
-  const size_t lds = (size_t)geo.NC * cp_of(4 * F) * sizeof(float);
+                    const float* W2, const float* b2, float* y, float* part, float* tabs,
+                    int prec, hipStream_t st) {
+  const size_t lds = tab_lds(geo, 4 * F);
+  if (kGTab) {
+    if (int rc = rows_table(4 * F, PtS, geo.NT, tabs, st)) return rc;
+    PtS = tabs;
+  }
 #define SL_C(FF, PP)                                                                       \
   case FF * 8 + PP:                                                                        \
     return sl_launch(ksl_edge_mlp_fwd<FF, PP>, geo, lds, st, geo, sl, xe, xsc, xsh, Ps, PtS, W1, \
@@ -1006,8 +1066,13 @@ int sl_edge_mlp_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* xe,
 
 int sl_source_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, const float* sc,
                   const float* sh, const float* QtS, const float* Ws1, const float* Ws2,
-                  const float* bs2, float* mom, float* hs, int prec, hipStream_t st) {
-  const size_t lds = (size_t)geo.NC * cp_of(2 * F) * sizeof(float);
+                  const float* bs2, float* mom, float* hs, float* tabs, int prec,
+                  hipStream_t st) {
+  const size_t lds = tab_lds(geo, 2 * F);
+  if (kGTab) {
+    if (int rc = rows_table(2 * F, QtS, geo.NT, tabs, st)) return rc;
+    QtS = tabs;
+  }
   EdgeGeo g1 = geo;   // one block per slice (its 4 waves interleave the steps)
   g1.KS = 1;
   g1.nblocks = geo.G * geo.NFG * 4;
@@ -1033,8 +1098,13 @@ int sl_target_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, co
 
 int sl_target_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, const float* sc,
                   const float* sh, const float* Rs, const float* Wt1, const float* ghS, float* gz,
-                  float* gxe, float* part, const uint8_t* tmask, int prec, hipStream_t st) {
-  const size_t lds = (size_t)geo.NC * cp_of(2 * F) * sizeof(float);
+                  float* gxe, float* part, const uint8_t* tmask, float* tabs, int prec,
+                  hipStream_t st) {
+  const size_t lds = tab_lds(geo, 2 * F);
+  if (kGTab) {
+    if (int rc = rows_table(2 * F, ghS, geo.NT, tabs, st)) return rc;
+    ghS = tabs;
+  }
 #define SL_C(FF, PP)                                                                        \
   case FF * 8 + PP:                                                                         \
     return tmask ? sl_launch(ksl_target_bwd<FF, PP, true>, geo, lds, st, geo, sl, y, sc, sh, Rs, \
@@ -1050,9 +1120,18 @@ int sl_source_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, co
                   const float* bs2, const float* mean, const float* coef, const float* Rs,
                   const float* Wt1, const float* ghS, const float* g_next, const float* mu1,
                   const float* inv1, float* g_tot, float* pW2, float* pW1, float* pCol,
-                  float* pBN, const uint8_t* tmask, int prec, hipStream_t st) {
-  const size_t lds = (size_t)geo.NC * (2 * cp_of(2 * F) + 4 * (2 * F + 1)) * sizeof(float);
+                  float* pBN, const uint8_t* tmask, float* tabs, int prec, hipStream_t st) {
+  const size_t lds = (size_t)geo.NC * 4 * (2 * F + 1) * sizeof(float);
   const bool tm = tmask && Rs;
+  // the two class tables in global memory (tabs: 2 * NT * CP floats of workspace)
+  const long long tlen = geo.NT * cpg_of(2 * F);
+  float* tq = tabs;
+  float* tg = ghS ? tabs + tlen : nullptr;
+  if (int rc = rows_table(2 * F, QtS, geo.NT, tq, st)) return rc;
+  if (tg)
+    if (int rc = rows_table(2 * F, ghS, geo.NT, tg, st)) return rc;
+  QtS = tq;
+  ghS = tg;
 #define SL_C(FF, PP)                                                                        \
   case FF * 8 + PP:                                                                         \
     return tm ? sl_launch(ksl_source_bwd<FF, PP, true>, geo, lds, st, geo, sl, y, sc, sh, QtS, \
@@ -1069,8 +1148,12 @@ int sl_edge_mlp_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* g_t
                     const float* alpha, const float* gam0, const float* gam1, const float* y,
                     const float* xe, const float* xsc, const float* xsh, const float* Ps,
                     const float* PtS, const float* W1, const float* W2, float* gxe, float* gs,
-                    float* pW2, float* pW1, float* pCol, int prec, hipStream_t st) {
-  const size_t lds = (size_t)geo.NC * (cp_of(4 * F) + 4 * (4 * F + 1)) * sizeof(float);
+                    float* pW2, float* pW1, float* pCol, float* tabs, int prec, hipStream_t st) {
+  const size_t lds = tab_lds(geo, 4 * F) + (size_t)geo.NC * 4 * (4 * F + 1) * sizeof(float);
+  if (kGTab) {
+    if (int rc = rows_table(4 * F, PtS, geo.NT, tabs, st)) return rc;
+    PtS = tabs;
+  }
 #define SL_C(FF, PP)                                                                         \
   case FF * 8 + PP:                                                                          \
     return sl_launch(ksl_edge_mlp_bwd<FF, PP>, geo, lds, st, geo, sl, g_tot, alpha, gam0, gam1, \
