@@ -48,6 +48,11 @@ PRECISION = {
               "gradients) on bf16 MFMAs with split hi+lo operands (bf16x3, ~2^-16 relative per "
               "product); fp32 accumulation, edge state, node level and loss (BASELINE configs[4])",
 }
+# the arithmetic each edge path computes in (`precision` spells it out): the
+# default path's backward products are split-bf16 (bf16x3), its forward fp32
+DTYPE = {"mfma": "f32 (bf16x3 backward products)", "mfma32": "f32", "valu": "f32",
+         "bf16y": "f32 (bf16 edge state)", "bf16m": "bf16", "bf16": "bf16",
+         "bf16x6": "f32-class split bf16 (bf16x6 forward, bf16x3 backward)", "bf16x3": "bf16x3"}
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense fp32-input MFMA (= fp32 vector peak)
 
@@ -423,7 +428,7 @@ def main():
             "value": value, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16" if args.edge_path in ("bf16", "bf16m") else "f32",
+            "dtype": DTYPE[args.edge_path],
             "data": "synthetic",
             "precision": PRECISION[args.edge_path],
             "config": {"workload": f"{G} complete bipartite {NF}x{NC} graphs per GPU, {B} "
