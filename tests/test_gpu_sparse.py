@@ -137,9 +137,9 @@ def _oracle(model, graph, w, dtype, reverse=False):
     return m, out
 
 
-def _ours(model, graph, w, B, normed=True):
+def _ours(model, graph, w, B, normed=True, F=10):
     import pfsgnn
-    gnn = pfsgnn.GNN(B=B, Fdim=10, T=12, F_s=1, F_t=2, normed=normed).cuda()
+    gnn = pfsgnn.GNN(B=B, Fdim=F, T=12, F_s=1, F_t=2, normed=normed).cuda()
     gnn.load_state_dict({k: v.float() for k, v in model.state_dict().items()})
     gnn.train()
     data = pfsgnn.BipartiteData(graph.edge_index, graph.x_s.float(), graph.x_t.float(),
@@ -162,12 +162,13 @@ def _weights(graph, G, NF, NC, gen, F=10):
 @pytest.mark.parametrize("G,NF,NC,density,B,dup,normed", [
     (1, 40, 12, 0.5, 2, 3, True), (2, 24, 16, 0.3, 2, 0, True), (3, 10, 7, 0.7, 3, 4, True),
     (1, 300, 64, 0.08, 2, 0, True), (2, 24, 16, 0.4, 2, 2, False)])
-def test_sparse_gnn_matches_oracle(G, NF, NC, density, B, dup, normed, sliced):
-    model, graph, gen = sparse_problem(G, NF, NC, density, B=B, seed=G + NF, dup=dup, normed=normed)
-    w = _weights(graph, G, NF, NC, gen)
+def test_sparse_gnn_matches_oracle(G, NF, NC, density, B, dup, normed, sliced, F=10):
+    model, graph, gen = sparse_problem(G, NF, NC, density, F=F, B=B, seed=G + NF, dup=dup,
+                                       normed=normed)
+    w = _weights(graph, G, NF, NC, gen, F=F)
     m64, o64 = _oracle(model, graph, w, torch.float64)
     r32 = [_oracle(model, graph, w, torch.float32, reverse=rv) for rv in (False, True)]
-    gnn, out = _ours(model, graph, w, B, normed=normed)
+    gnn, out = _ours(model, graph, w, B, normed=normed, F=F)
     from pfsgnn import gnn as gmod
     lays = [e[3] for e in gmod._LAYOUT_CACHE.d.values()]   # (the fixture cleared the cache)
     assert lays and all((lay.sp.sl is not None) == sliced for lay in lays)
@@ -185,6 +186,13 @@ def test_sparse_gnn_matches_oracle(G, NF, NC, density, B, dup, normed, sliced):
         if "running" in k or "num_batches" in k:
             check(k, v.double(), b64[k].double(), [r[0].state_dict()[k].double() for r in r32],
                   tol)
+
+
+@pytest.mark.parametrize("F", [8, 16])
+def test_sparse_gnn_other_fdim(F, sliced):
+    """Fdim 8 and 16 (the other instantiations of the edge kernels, sliced
+    and composed) on a ragged batch with repeated pairs"""
+    test_sparse_gnn_matches_oracle(2, 40, 12, 0.4, 2, 3, True, sliced, F=F)
 
 
 def sliced_plan_ref(fib_ptr, src_p, tgt_p, user_of, G, NF, NC):
