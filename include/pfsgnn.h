@@ -491,7 +491,8 @@ int pfsgnn_sliced_fill(const int* src_p, const int* tgt_p, const int* user_of, c
                        long long EP, int maxdeg, unsigned char* cls, int* pos_user, float* pco,
                        void* stream);
 /* caller-order edge rows [E][F] -> a slot tensor [F][EP] (0 at padding), and
- * back (dst [E][F] if rowmajor else [F][E]; with sc/sh the lazy affine first) */
+ * back (dst [E][F] if rowmajor else [F][E]; with sc/sh the lazy affine first);
+ * F = 8, 10 or 16 */
 int pfsgnn_edges_to_slots(const float* src, long long E, long long EP, int F, const int* pos_user,
                           float* dst, void* stream);
 int pfsgnn_edges_from_slots(const float* y, const float* sc, const float* sh, long long E,

@@ -828,7 +828,7 @@ __global__ __launch_bounds__(512) void k_wgrad(const float* __restrict__ dY, int
 // Several independent weight gradients in one launch (pfsgnn_wgrad_multi):
 // job j owns blocks [blk0_j, blk0_j + nblk_j); the table rides in the kernel
 // arguments and a block selects its job with constant indices (uniform).
-#define WG_MULTI 8
+#define WG_MULTI 24   // (24 jobs x 144 B: the table stays under the 4 KB kernel-argument limit)
 struct WgJob {
   const float* dY;
   XSegs S;
@@ -839,6 +839,7 @@ struct WgTable {
   WgJob j[WG_MULTI];
   int njob;
 };
+static_assert(sizeof(WgTable) <= 4096, "k_wgrad_multi's job table must fit the kernel arguments");
 
 template <int TMAX, int PER>
 __global__ __launch_bounds__(512) void k_wgrad_multi(WgTable T) {

@@ -141,28 +141,57 @@ __global__ void k_sl_pco(int maxdeg, float* __restrict__ pco) {
   p[7] = 0.f;
 }
 
-// caller-order rows [E][F] <-> slot tensors [F][EP] (0 at padding)
-__global__ void k_to_slots(const float* __restrict__ src, long long EP, int F,
+// caller-order rows [E][F] <-> slot tensors [F][EP] (0 at padding): thread per
+// position, the slot side coalesced; the caller's row (F floats at a random
+// row: 8-byte aligned for even F) moves as F/2 float2 accesses
+template <int F>
+__global__ void k_to_slots(const float* __restrict__ src, long long EP,
                            const int* __restrict__ pos_user, float* __restrict__ dst) {
   for (long long p = (long long)blockIdx.x * 256 + threadIdx.x; p < EP;
        p += (long long)gridDim.x * 256) {
     const int u = pos_user[p];
-    for (int j = 0; j < F; ++j) dst[(long long)j * EP + p] = u >= 0 ? src[(long long)u * F + j] : 0.f;
+    float v[F];
+    if (F % 2 == 0) {
+      const float2* r = reinterpret_cast<const float2*>(src + (long long)(u >= 0 ? u : 0) * F);
+#pragma unroll
+      for (int j = 0; j < F / 2; ++j) {
+        const float2 q = r[j];
+        v[2 * j] = q.x;
+        v[2 * j + 1] = q.y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < F; ++j) v[j] = src[(long long)(u >= 0 ? u : 0) * F + j];
+    }
+#pragma unroll
+    for (int j = 0; j < F; ++j) dst[(long long)j * EP + p] = u >= 0 ? v[j] : 0.f;
   }
 }
+template <int F>
 __global__ void k_from_slots(const float* __restrict__ y, const float* __restrict__ sc,
-                             const float* __restrict__ sh, long long E, long long EP, int F,
+                             const float* __restrict__ sh, long long E, long long EP,
                              const int* __restrict__ pos_user, int rowmajor,
                              float* __restrict__ dst) {
   for (long long p = (long long)blockIdx.x * 256 + threadIdx.x; p < EP;
        p += (long long)gridDim.x * 256) {
     const int u = pos_user[p];
     if (u < 0) continue;
+    float v[F];
+#pragma unroll
     for (int j = 0; j < F; ++j) {
-      float v = y[(long long)j * EP + p];
-      if (sc) v = fmaf(v, sc[j], sh[j]);
-      if (rowmajor) dst[(long long)u * F + j] = v;
-      else dst[(long long)j * E + u] = v;
+      v[j] = y[(long long)j * EP + p];
+      if (sc) v[j] = fmaf(v[j], sc[j], sh[j]);
+    }
+    if (rowmajor && F % 2 == 0) {
+      float2* r = reinterpret_cast<float2*>(dst + (long long)u * F);
+#pragma unroll
+      for (int j = 0; j < F / 2; ++j) r[j] = make_float2(v[2 * j], v[2 * j + 1]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < F; ++j) {
+        if (rowmajor) dst[(long long)u * F + j] = v[j];
+        else dst[(long long)j * E + u] = v[j];
+      }
     }
   }
 }
@@ -661,8 +690,13 @@ extern "C" int pfsgnn_edges_to_slots(const float* src, long long E, long long EP
                                      const int* pos_user, float* dst, void* stream) {
   PF_REQUIRE(src && pos_user && dst && E > 0 && EP >= E && F > 0, "pfsgnn_edges_to_slots",
              "bad arguments");
-  hipLaunchKernelGGL(k_to_slots, dim3(grid_of(EP)), dim3(256), 0, as_stream(stream), src, EP, F,
-                     pos_user, dst);
+  hipStream_t st = as_stream(stream);
+  switch (F) {
+#define TS(FF) case FF: hipLaunchKernelGGL(k_to_slots<FF>, dim3(grid_of(EP)), dim3(256), 0, st, src, EP, pos_user, dst); break;
+    TS(8) TS(10) TS(16)
+#undef TS
+    default: return pf::fail("pfsgnn_edges_to_slots", "F must be 8, 10 or 16");
+  }
   return pf::check_launch("pfsgnn_edges_to_slots");
 }
 
@@ -671,7 +705,12 @@ extern "C" int pfsgnn_edges_from_slots(const float* y, const float* sc, const fl
                                        int rowmajor, float* dst, void* stream) {
   PF_REQUIRE(y && pos_user && dst && E > 0 && EP >= E && F > 0 && (!sc == !sh),
              "pfsgnn_edges_from_slots", "bad arguments");
-  hipLaunchKernelGGL(k_from_slots, dim3(grid_of(EP)), dim3(256), 0, as_stream(stream), y, sc, sh,
-                     E, EP, F, pos_user, rowmajor, dst);
+  hipStream_t st = as_stream(stream);
+  switch (F) {
+#define FS(FF) case FF: hipLaunchKernelGGL(k_from_slots<FF>, dim3(grid_of(EP)), dim3(256), 0, st, y, sc, sh, E, EP, pos_user, rowmajor, dst); break;
+    FS(8) FS(10) FS(16)
+#undef FS
+    default: return pf::fail("pfsgnn_edges_from_slots", "F must be 8, 10 or 16");
+  }
   return pf::check_launch("pfsgnn_edges_from_slots");
 }

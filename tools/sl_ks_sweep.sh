@@ -1,1 +1,7 @@
-for ks in 1 2 4; do PFSGNN_SL_KS=$ks SPARSE_DENSITIES=0.3,0.999 python tools/sparse_bench.py 2>&1 | grep edges | sed "s/^/KS=$ks /"; done
+#!/bin/bash
+# step-split count of the sliced kernels (PFSGNN_SL_KS) on tools/sparse_bench.py
+for ks in 1 2 3 4; do
+  for d in 0.3 0.999; do
+    PFSGNN_SL_KS=$ks SPARSE_DENSITIES=$d python tools/sparse_bench.py 2>/dev/null | sed "s/^/KS=$ks /"
+  done
+done
