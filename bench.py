@@ -52,7 +52,7 @@ PRECISION = {
 # default path's backward products are split-bf16 (bf16x3), its forward fp32
 DTYPE = {"mfma": "f32 (bf16x3 backward products)", "mfma32": "f32", "valu": "f32",
          "bf16y": "f32 (bf16 edge state)", "bf16m": "bf16", "bf16": "bf16",
-         "bf16x6": "f32-class split bf16 (bf16x6 forward, bf16x3 backward)", "bf16x3": "bf16x3"}
+         "bf16x6": "f32 (split-bf16 products: bf16x6 forward, bf16x3 backward)", "bf16x3": "bf16x3"}
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense fp32-input MFMA (= fp32 vector peak)
 
@@ -151,7 +151,9 @@ def pmc_traffic(kernel, E, F):
         from pfsgnn import native
         pre = "k_" if native.get_edge_path() == "valu" else "km_"
         key = f"{pre}{kernel}<{F}>"
-        if d.get("E") == E and d.get("F") == F and key in d.get("kernels", {}):
+        # (passes without an edge_path field were taken on the mfma path)
+        if (d.get("E") == E and d.get("F") == F and key in d.get("kernels", {})
+                and d.get("edge_path", "mfma") == native.get_edge_path()):
             return d["kernels"][key]["traffic_bytes"], os.path.basename(path)
     return None
 

@@ -58,10 +58,12 @@ size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F);
  *       their backward recompute included, on v_mfma_f32_16x16x32_bf16 with
  *       split operands (bf16 hi + lo, ~2^-16 relative per product, fp32
  *       accumulation and edge state; BASELINE configs[4] at fp32 tolerance);
- *   PFSGNN_EDGE_BF16X6 -- the forward contractions and their backward
- *       recompute on v_mfma_f32_16x16x32_bf16 with three-way split operands
- *       (hi + mid + lo, the six products down to ~2^-18: fp32-class
- *       products), the gradient chains and weight gradients as PFSGNN_EDGE_MFMA.
+ *   PFSGNN_EDGE_BF16X6 -- the forward contractions and their
+ *       backward recompute on v_mfma_f32_16x16x32_bf16 with three-way split
+ *       operands (hi + mid + lo, the six products down to ~2^-18: fp32-class
+ *       products), the gradient chains and weight gradients as
+ *       PFSGNN_EDGE_MFMA.  Built for Fdim 10; at other Fdims this path runs
+ *       the PFSGNN_EDGE_MFMA arithmetic.
  * The fp32-class paths (MFMA, MFMA_F32, VALU) produce the same outputs to the
  * parity tolerance; the bf16 paths' deviation is measured, not bounded
  * (DESIGN.md §Numerics).  Node-level ops, reductions and the loss are shared. */

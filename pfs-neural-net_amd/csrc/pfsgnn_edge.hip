@@ -1327,8 +1327,11 @@ bool use_mfma() { return g_path != PFSGNN_EDGE_VALU; }
 // `model`: 0 the EdgeModel kernels, 1 the SModel / TModel ones (a model's
 // forward kernel and its backward recompute always share one precision).
 // Diagnostic knob PFSGNN_X3_MASK (bit per model, default both): which models
-// the bf16x3 path runs bf16x3 forward contractions in (the others as MFMA).
-int mf_prec(int model) {
+// the bf16x3 / bf16x6 paths run their split-bf16 forward contractions in (the
+// others as MFMA).
+// The bf16x6 kernels (PREC 4) are built for Fdim 10; at other Fdims that path
+// runs the MFMA arithmetic (PREC 1).
+int mf_prec(int model, int F) {
   static const int x3mask = [] {
     const char* e = getenv("PFSGNN_X3_MASK");
     return e ? atoi(e) : 3;
@@ -1336,7 +1339,7 @@ int mf_prec(int model) {
   return g_path == PFSGNN_EDGE_MFMA ? 1
          : (g_path == PFSGNN_EDGE_BF16 || g_path == PFSGNN_EDGE_BF16_MFMA) ? 2
          : g_path == PFSGNN_EDGE_BF16X3 ? ((x3mask >> model) & 1 ? 3 : 1)
-         : g_path == PFSGNN_EDGE_BF16X6 ? 4 : 0;
+         : g_path == PFSGNN_EDGE_BF16X6 ? (F == 10 && ((x3mask >> model) & 1) ? 4 : 1) : 0;
 }
 // SModel forward on the fiber-tile grid (km_source_fwd_ft: no class-split
 // partials, no finalize launch); PFSGNN_SFWD_TILES=0 keeps the class-split
@@ -1486,7 +1489,7 @@ static int edge_mlp_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, i
     float* tabs = w.take((size_t)pfm::sl_tab_floats(geo, F));
     PF_REQUIRE(tabs, "pfsgnn_edge_mlp_fwd", "workspace too small");
     if (int rc = pfm::sl_edge_mlp_fwd(geo, sl_of(*sl), F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part,
-                                      tabs, mf_prec(0), st))
+                                      tabs, mf_prec(0, F), st))
       return rc;
     tm_.end(); }
     hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(256), 0, st, part, geo.nblocks, F, sl->E,
@@ -1496,7 +1499,7 @@ static int edge_mlp_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, i
   if (use_mfma()) {
     PF_REQUIRE(part, "pfsgnn_edge_mlp_fwd", "workspace too small");
     { pf::Timer tm_("edge_mlp_fwd", st);
-    if (int rc = pfm::edge_mlp_fwd(geo, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part, mf_prec(0), mf_bfy(), st)) return rc;
+    if (int rc = pfm::edge_mlp_fwd(geo, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part, mf_prec(0, F), mf_bfy(), st)) return rc;
     tm_.end(); }
     hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(256), 0, st, part, geo.nblocks, F, geo.E,
                        mu, var, bn);
@@ -1579,14 +1582,14 @@ static int source_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
     float* tabs = w.take((size_t)pfm::sl_tab_floats(geo, F));
     PF_REQUIRE(tabs, "pfsgnn_source_fwd", "workspace too small");
     if (int rc = pfm::sl_source_fwd(geo, sl_of(*sl), F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs, tabs,
-                                    mf_prec(1), st))
+                                    mf_prec(1, F), st))
       return rc;
     tm_.end();
     return pf::check_launch("pfsgnn_source_fwd");
   }
   if (use_mfma() && NC <= 256 && sfwd_tiles()) {
     pf::Timer tm_("source_fwd", st);
-    if (int rc = pfm::source_fwd_tiles(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs, mf_prec(1),
+    if (int rc = pfm::source_fwd_tiles(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs, mf_prec(1, F),
                                        st))
       return rc;
     tm_.end();
@@ -1596,7 +1599,7 @@ static int source_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
   if (use_mfma()) {
     PF_REQUIRE(partS, "pfsgnn_source_fwd", "workspace too small");
     pf::Timer tm_("source_fwd", st);
-    if (int rc = pfm::source_fwd(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, partS, mf_prec(1), st))
+    if (int rc = pfm::source_fwd(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, partS, mf_prec(1, F), st))
       return rc;
     tm_.end();
   } else {
@@ -1658,10 +1661,10 @@ static int target_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
   { pf::Timer tm_("target_fwd", st);
   if (sl) {
     if (int rc = pfm::sl_target_fwd(geo, sl_of(*sl), F, y, sc, sh, Rs, Wt1, part, tmask,
-                                    mf_prec(1), st))
+                                    mf_prec(1, F), st))
       return rc;
   } else if (use_mfma()) {
-    if (int rc = pfm::target_fwd(geo, F, y, sc, sh, Rs, Wt1, part, tmask, mf_prec(1), st)) return rc;
+    if (int rc = pfm::target_fwd(geo, F, y, sc, sh, Rs, Wt1, part, tmask, mf_prec(1, F), st)) return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
                                    sc, sh, Rs, Wt1, part));
@@ -1718,11 +1721,11 @@ static int target_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
     float* tabs = w.take((size_t)pfm::sl_tab_floats(geo, F));
     PF_REQUIRE(tabs, "pfsgnn_target_bwd", "workspace too small");
     if (int rc = pfm::sl_target_bwd(geo, sl_of(*sl), F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part,
-                                    tmask, tabs, mf_prec(1), st))
+                                    tmask, tabs, mf_prec(1, F), st))
       return rc;
   } else if (use_mfma()) {
     if (int rc = pfm::target_bwd(geo, F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part, tmask,
-                                 mf_prec(1), st))
+                                 mf_prec(1, F), st))
       return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
@@ -1913,12 +1916,12 @@ static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
     PF_REQUIRE(tabs, "pfsgnn_source_bwd", "workspace too small");
     if (int rc = pfm::sl_source_bwd(geo, sl_of(*sl), F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef,
                                     Rs, Wt1, ghT, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN,
-                                    tmask, tabs, mf_prec(1), st))
+                                    tmask, tabs, mf_prec(1, F), st))
       return rc;
   } else if (mfma) {
     if (int rc = pfm::source_bwd(geo, F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT,
                                  g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask,
-                                 mf_prec(1), st))
+                                 mf_prec(1, F), st))
       return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_source_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
@@ -2007,14 +2010,14 @@ static int edge_mlp_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, i
     PF_REQUIRE(tabs, "pfsgnn_edge_mlp_bwd", "workspace too small");
     if (int rc = pfm::sl_edge_mlp_bwd(geo, sl_of(*sl), F, g_tot, alpha, gam0, gam1, y, xe, xsc,
                                       xsh, Ps, Pt, W1, W2, gxe, gs, pW2, pW1, pCol, tabs,
-                                      mf_prec(0), st))
+                                      mf_prec(0, F), st))
       return rc;
     tm_.end();
   } else if (use_mfma()) {
     PF_REQUIRE(pW2 && pW1 && pCol && gs, "pfsgnn_edge_mlp_bwd", "workspace too small");
     pf::Timer tm_("edge_mlp_bwd", st);
     if (int rc = pfm::edge_mlp_bwd(geo, F, g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, Pt, W1,
-                                   W2, gxe, gs, pW2, pW1, pCol, mf_prec(0), st))
+                                   W2, gxe, gs, pW2, pW1, pCol, mf_prec(0, F), st))
       return rc;
     tm_.end();
   } else {

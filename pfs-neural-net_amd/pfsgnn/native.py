@@ -241,7 +241,8 @@ def set_edge_path(path):
     recompute included; BASELINE configs[4] at fp32 tolerance) or "bf16x6"
     (the forward contractions and recompute on bf16 MFMAs with three-way split
     operands, fp32-class products; gradient chains as "mfma").  The bf16
-    paths are built for Fdim 10.
+    paths are built for Fdim 10; at other Fdims "bf16x6" runs the "mfma"
+    arithmetic.
     Read at launch time; env PFSGNN_EDGE_PATH sets it when the library loads."""
     if path not in EDGE_PATHS:
         raise ValueError(f"edge path must be one of {sorted(EDGE_PATHS)}, got {path!r}")

@@ -37,9 +37,10 @@ NF = 2394
 @pytest.fixture(params=["mfma", "mfma32", "valu"])
 def prec(request):
     import pfsgnn
+    prev = pfsgnn.get_edge_path()
     pfsgnn.set_edge_path(request.param)
     yield request.param
-    pfsgnn.set_edge_path("mfma")
+    pfsgnn.set_edge_path(prev)
 
 
 def _grid(G, NC):

@@ -30,9 +30,10 @@ FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "g16_or
 @pytest.fixture(params=["mfma", "mfma32"])
 def path(request):
     import pfsgnn
+    prev = pfsgnn.get_edge_path()
     pfsgnn.set_edge_path(request.param)
     yield request.param
-    pfsgnn.set_edge_path("mfma")
+    pfsgnn.set_edge_path(prev)
 
 
 def test_bench_geometry_training_step_matches_oracle(path):

@@ -39,7 +39,10 @@ def kname(full):
     return k
 
 
-PREC = os.environ.get("PFSGNN_PMC_PREC", "1")   # the default edge path's MFMA kernels
+# the profiled edge path's MFMA kernels: 1 = mfma (the default path; its
+# forward kernels at PREC 0), 4 = bf16x6
+PREC = os.environ.get("PFSGNN_PMC_PREC", "1")
+PATH_OF = {"4": "bf16x6", "1": "mfma", "0": "mfma32", "3": "bf16x3"}
 
 
 def per_dispatch(path, counter):
@@ -78,7 +81,7 @@ def algorithmic(kernel):
 pre = sys.argv[6] if len(sys.argv) > 6 else ""     # pass directories <d>/<pre>fetch, <pre>write
 fetch = per_dispatch(os.path.join(d, pre + "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
 write = per_dispatch(os.path.join(d, pre + "write", "run_counter_collection.csv"), "WRITE_SIZE")
-out = {"E": E, "F": F, "read_calibration": read_cal,
+out = {"E": E, "F": F, "edge_path": PATH_OF.get(PREC, PREC), "read_calibration": read_cal,
        "calibration": "profiles/r02_fetch_calibration.json (rdrows pattern)",
        "note": "traffic_bytes = FETCH_SIZE*read_calibration + WRITE_SIZE per launch; "
                "traffic_bytes_guide2x uses the guide's 2.0 read correction (upper bound)",

@@ -2,7 +2,7 @@
 # PMC passes over a short bench run (one rocprofv3 process per counter group).
 # Usage (on the GPU box, from the repo root): bash tools/prof_pmc.sh <outdir> [bench args]
 out=$1; shift
-args=${@:-"--steps 3 --warmup 1 --no-cpu-baseline"}
+args=${@:-"--steps 3 --warmup 1 --no-cpu-baseline --alt-paths ,"}
 root=$(pwd)
 cd /tmp && export TMPDIR=/tmp
 run() {
