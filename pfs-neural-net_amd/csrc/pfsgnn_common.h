@@ -342,7 +342,7 @@ struct RedDesc {
   int ldo, add;
   float scale;
 };
-#define PF_MAX_RED 32
+#define PF_MAX_RED 48   // (48 x 64 B: the descriptor pack stays under the 4 KB kernel-argument limit)
 void launch_reduce_multi(const RedDesc* d, int n, hipStream_t st);
 // Deferred weight-gradient reductions (pfsgnn_defer_begin / _end): while a
 // pass is open, the edge backward kernels put their weight partials in the

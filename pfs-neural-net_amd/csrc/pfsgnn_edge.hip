@@ -1102,15 +1102,21 @@ __device__ __forceinline__ void stage_lin(const NodeLin& L0, const NodeLin& L1, 
 // wave w sums channels w, w+4, ...; the epilogues read the block's sums and
 // the staged weights from LDS.
 template <int C>
-__global__ __launch_bounds__(256) void k_reduce_fiber_lin(const float* __restrict__ part, int KS,
-                                                          long long NS, float* __restrict__ out,
-                                                          NodeLin L0, NodeLin L1) {
+struct FiberLinLds {
+  float res[C][65];
+  float ws[2 * NL_MAXK * C];
+};
+template <int C>
+__device__ __forceinline__ void reduce_fiber_lin_block(FiberLinLds<C>& S, int bx,
+                                                       const float* __restrict__ part, int KS,
+                                                       long long NS, float* __restrict__ out,
+                                                       const NodeLin& L0, const NodeLin& L1) {
   static_assert(C % 4 == 0, "C must be a multiple of 4");
   constexpr int CPW = C / 4;
-  __shared__ float res[C][65];
-  __shared__ float ws[2 * NL_MAXK * C];
+  auto& res = S.res;
+  float* ws = S.ws;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const long long n0 = (long long)blockIdx.x * 64, n = n0 + lane;
+  const long long n0 = (long long)bx * 64, n = n0 + lane;
   const bool v = n < NS;
   const long long nc = v ? n : NS - 1;   // clamped: every load unconditional
   const long long len = (long long)C * NS;
@@ -1154,17 +1160,24 @@ __global__ __launch_bounds__(256) void k_reduce_fiber_lin(const float* __restric
 // 16 partial lanes per output, two accumulators each, fixed-order combine), for
 // 4 whole classes per block, + up to two epilogues on those classes' columns
 template <int C>
-__global__ __launch_bounds__(256) void k_reduce_columns_lin(const float* __restrict__ part, int G,
-                                                            int BPG, int NC,
-                                                            float* __restrict__ out, NodeLin L0,
-                                                            NodeLin L1) {
-  constexpr int CPB = 4, NO = CPB * C, NP = NO / 16;   // outputs, 16-output passes
+struct ColLinLds {
+  static constexpr int CPB = 4, NO = CPB * C, NP = NO / 16;   // outputs, 16-output passes
+  float sh[NP][16][17];
+  float res[NO];
+  float ws[2 * NL_MAXK * C];
+};
+template <int C>
+__device__ __forceinline__ void reduce_columns_lin_block(ColLinLds<C>& S, int bx,
+                                                         const float* __restrict__ part, int G,
+                                                         int BPG, int NC, float* __restrict__ out,
+                                                         const NodeLin& L0, const NodeLin& L1) {
+  constexpr int CPB = ColLinLds<C>::CPB, NO = ColLinLds<C>::NO, NP = ColLinLds<C>::NP;
   static_assert(NO % 16 == 0, "4C must be a multiple of 16");
-  __shared__ float sh[NP][16][17];
-  __shared__ float res[NO];
-  __shared__ float ws[2 * NL_MAXK * C];
+  auto& sh = S.sh;
+  float* res = S.res;
+  float* ws = S.ws;
   const int t = threadIdx.x, o = t & 15, pl = t >> 4;
-  const long long NT = (long long)G * NC, q0 = (long long)blockIdx.x * CPB;
+  const long long NT = (long long)G * NC, q0 = (long long)bx * CPB;
   stage_lin<C>(L0, L1, ws);
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
@@ -1208,6 +1221,50 @@ __global__ __launch_bounds__(256) void k_reduce_columns_lin(const float* __restr
       *op = L.add ? *op + acc : acc;
     }
   }
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void k_reduce_fiber_lin(const float* __restrict__ part, int KS,
+                                                          long long NS, float* __restrict__ out,
+                                                          NodeLin L0, NodeLin L1) {
+  __shared__ FiberLinLds<C> S;
+  reduce_fiber_lin_block<C>(S, blockIdx.x, part, KS, NS, out, L0, L1);
+}
+template <int C>
+__global__ __launch_bounds__(256) void k_reduce_columns_lin(const float* __restrict__ part, int G,
+                                                            int BPG, int NC,
+                                                            float* __restrict__ out, NodeLin L0,
+                                                            NodeLin L1) {
+  __shared__ ColLinLds<C> S;
+  reduce_columns_lin_block<C>(S, blockIdx.x, part, G, BPG, NC, out, L0, L1);
+}
+// both of an edge kernel's node-side reductions in one launch (they are
+// independent): blocks [0, nbf) reduce the fiber partials, the rest the class
+// columns; the two LDS layouts share one allocation
+struct FiberRed {
+  const float* part;
+  int KS;
+  long long NS;
+  float* out;
+  NodeLin L0, L1;
+};
+struct ColRed {
+  const float* part;
+  int G, BPG, NC;
+  float* out;
+  NodeLin L0, L1;
+};
+template <int C>
+__global__ __launch_bounds__(256) void k_reduce_fiber_columns_lin(FiberRed fr, ColRed cr, int nbf) {
+  __shared__ union {
+    FiberLinLds<C> f;
+    ColLinLds<C> c;
+  } S;
+  const int bx = blockIdx.x;
+  if (bx < nbf)
+    reduce_fiber_lin_block<C>(S.f, bx, fr.part, fr.KS, fr.NS, fr.out, fr.L0, fr.L1);
+  else
+    reduce_columns_lin_block<C>(S.c, bx - nbf, cr.part, cr.G, cr.BPG, cr.NC, cr.out, cr.L0, cr.L1);
 }
 
 #define DISPATCH_C(C, ...)                                            \
@@ -1318,6 +1375,25 @@ int columns_lin(const float* part, int G, int BPG, int NC, int C, float* out, co
   DISPATCH_C(C, hipLaunchKernelGGL(k_reduce_columns_lin<CC>,
                                    dim3((unsigned)(((long long)G * NC + 3) / 4)), dim3(256), 0,
                                    st, part, G, BPG, NC, out, L0, L1));
+  return 0;
+}
+// fiber_finish_lin + columns_lin in one launch when both have an epilogue
+// (and the fiber partials need a reduction); otherwise the two calls
+int fiber_columns_lin(const EdgeGeo& geo, int C, const float* dst, float* fout, const NodeLin& F0,
+                      const NodeLin& F1, const float* part, int BPG, float* cout,
+                      const NodeLin& C0, const NodeLin& C1, hipStream_t st) {
+  if (!(F0.W || F1.W) || !(C0.W || C1.W)) {
+    if (int rc = fiber_finish_lin(geo, C, dst, fout, F0, F1, st)) return rc;
+    return columns_lin(part, geo.G, BPG, geo.NC, C, cout, C0, C1, st);
+  }
+  if (F0.nk > NL_MAXK || F1.nk > NL_MAXK || C0.nk > NL_MAXK || C1.nk > NL_MAXK)
+    return pf::fail("fiber_columns_lin", "nk > 32");
+  const FiberRed fr{geo.KS == 1 ? fout : dst, geo.KS, geo.NS, fout, F0, F1};
+  const ColRed cr{part, geo.G, BPG, geo.NC, cout, C0, C1};
+  const int nbf = (int)((geo.NS + 63) / 64);
+  const int nbc = (int)(((long long)geo.G * geo.NC + 3) / 4);
+  DISPATCH_C(C, hipLaunchKernelGGL(k_reduce_fiber_columns_lin<CC>, dim3(nbf + nbc), dim3(256), 0,
+                                   st, fr, cr, nbf));
   return 0;
 }
 
@@ -1775,10 +1851,10 @@ struct Bn2Bwd {
   float *alpha, *gam0, *gam1, *dgamma, *dbeta;
 };
 
-__global__ __launch_bounds__(256) void k_bn2_coef_part(const float* __restrict__ part, int nb,
-                                                       int F, Bn2Bwd bb, float* __restrict__ Sg,
-                                                       float* __restrict__ Sgx) {
-  const int k = blockIdx.x, t = threadIdx.x;
+__device__ __forceinline__ void bn2_coef_block(int k, const float* __restrict__ part, int nb, int F,
+                                               const Bn2Bwd& bb, float* __restrict__ Sg,
+                                               float* __restrict__ Sgx) {
+  const int t = threadIdx.x;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
   int b = t;
   for (; b + 768 < nb; b += 1024) {  // 4 partials in flight per thread and sum
@@ -1801,6 +1877,25 @@ __global__ __launch_bounds__(256) void k_bn2_coef_part(const float* __restrict__
     bn2_bwd_coef_one(k, v[0], v[1], bb.mu1, bb.var1, bb.gamma, bb.n, bb.eps, bb.alpha, bb.gam0,
                      bb.gam1, bb.dgamma, bb.dbeta);
   }
+}
+__global__ __launch_bounds__(256) void k_bn2_coef_part(const float* __restrict__ part, int nb,
+                                                       int F, Bn2Bwd bb, float* __restrict__ Sg,
+                                                       float* __restrict__ Sgx) {
+  bn2_coef_block(blockIdx.x, part, nb, F, bb, Sg, Sgx);
+}
+// k_bn2_coef_part (blocks [0, F)) and source_bwd's class-column reduction (the
+// rest) in one launch: independent, both read only source_bwd's partials
+template <int C>
+__global__ __launch_bounds__(256) void k_bn2_coef_columns_lin(const float* __restrict__ part,
+                                                              int nb, int F, Bn2Bwd bb,
+                                                              float* __restrict__ Sg,
+                                                              float* __restrict__ Sgx, ColRed cr) {
+  __shared__ ColLinLds<C> S;
+  const int bx = blockIdx.x;
+  if (bx < F)
+    bn2_coef_block(bx, part, nb, F, bb, Sg, Sgx);
+  else
+    reduce_columns_lin_block<C>(S, bx - F, cr.part, cr.G, cr.BPG, cr.NC, cr.out, cr.L0, cr.L1);
 }
 
 static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
@@ -1945,15 +2040,21 @@ static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
       nnow -= 3;
     }
     if (nnow) launch_reduce_multi(now, nnow, st);
+  }
+  // g_xt += Ws1[:, 0:F]^T GzS (gnn.py:136, the x_t[tgt] input gradient), with
+  // the BatchNorm backward coefficients in the same launch when both are due
+  const NodeLin Lx = lin_t_add(g_xt ? Ws1 : nullptr, 2 * F, 0, F, g_xt, geo.NT);
+  if (bb && Lx.W) {
+    const ColRed cr{pCol, G, col_bpg(geo, sl), NC, GzS, Lx, no_lin()};
+    const int nbc = (int)(((long long)G * NC + 3) / 4);
+    DISPATCH_C(C, hipLaunchKernelGGL(k_bn2_coef_columns_lin<CC>, dim3(F + nbc), dim3(256), 0, st,
+                                     pBN, (int)nb, F, *bb, Sg, Sgx, cr));
+  } else {
     if (bb)
       hipLaunchKernelGGL(k_bn2_coef_part, dim3(F), dim3(256), 0, st, pBN, (int)nb, F, *bb, Sg,
                          Sgx);
+    if (int rc = columns_lin(pCol, G, col_bpg(geo, sl), NC, C, GzS, Lx, no_lin(), st)) return rc;
   }
-  // g_xt += Ws1[:, 0:F]^T GzS (gnn.py:136, the x_t[tgt] input gradient)
-  if (int rc = columns_lin(pCol, G, col_bpg(geo, sl), NC, C, GzS,
-                           lin_t_add(g_xt ? Ws1 : nullptr, 2 * F, 0, F, g_xt, geo.NT), no_lin(),
-                           st))
-    return rc;
   return pf::check_launch("pfsgnn_source_bwd");
 }
 
@@ -2033,10 +2134,6 @@ static int edge_mlp_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, i
   // node-input gradients of the first Linear (gnn.py:100): g_xs += W1[:, 0:F]^T GzEs,
   // g_xt += W1[:, F:2F]^T GzEt, and Vu = W1[:, 3F:4F]^T GzEt per class (the
   // caller sums it per graph into g_u)
-  if (int rc = fiber_finish_lin(geo, H, gs, GzEs,
-                                lin_t_add(g_xs ? W1 : nullptr, 4 * F, 0, F, g_xs, geo.NS),
-                                no_lin(), st))
-    return rc;
   {
     RedDesc rd[3] = {{pW2, (int)nb, (size_t)F * (H + 1), H + 1, F, H, dW2, H, 1, 1.f},
                      {pW2 + H, (int)nb, (size_t)F * (H + 1), H + 1, F, 1, db2, 1, 1, 1.f},
@@ -2046,8 +2143,10 @@ static int edge_mlp_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, i
   }
   NodeLin Lu = lin_t_add(Vu ? W1 : nullptr, 4 * F, 3 * F, F, Vu, geo.NT);
   Lu.add = 0;
-  if (int rc = columns_lin(pCol, G, col_bpg(geo, sl), NC, H, GzEt,
-                           lin_t_add(g_xt ? W1 : nullptr, 4 * F, F, F, g_xt, geo.NT), Lu, st))
+  if (int rc = fiber_columns_lin(geo, H, gs, GzEs,
+                                 lin_t_add(g_xs ? W1 : nullptr, 4 * F, 0, F, g_xs, geo.NS),
+                                 no_lin(), pCol, col_bpg(geo, sl), GzEt,
+                                 lin_t_add(g_xt ? W1 : nullptr, 4 * F, F, F, g_xt, geo.NT), Lu, st))
     return rc;
   return pf::check_launch("pfsgnn_edge_mlp_bwd");
 }

@@ -77,6 +77,29 @@ struct EdgeLoss {
   }
 };
 
+// decoder_e's weights staged in LDS (read as broadcasts inside the edge loop):
+// held in SGPRs they overflowed the scalar file (119 / 139 SGPR spills, each
+// use a v_readlane in the loop)
+template <int F>
+struct DecW {
+  static constexpr int N = F * F + 2 * F + 1;
+  float w[N];   // Wd1 [F][F] | bd1 [F] | Wd2 [F] | bd2
+  __device__ __forceinline__ void load(const float* __restrict__ Wd1, const float* __restrict__ bd1,
+                                       const float* __restrict__ Wd2, const float* __restrict__ bd2) {
+    for (int i = threadIdx.x; i < N; i += blockDim.x)
+      w[i] = i < F * F ? Wd1[i] : i < F * F + F ? bd1[i - F * F]
+                                : i < F * F + 2 * F ? Wd2[i - F * F - F] : bd2[0];
+  }
+};
+// the weights' base as an opaque value per loop iteration: the compiler would
+// otherwise hoist all F*F + 2F + 1 loop-invariant reads into VGPRs (occupancy 7 -> 3)
+template <int F>
+__device__ __forceinline__ const float* dec_base(const DecW<F>& d) {
+  int lo = 0;
+  asm volatile("" : "+v"(lo));
+  return d.w + lo;
+}
+
 template <int F>
 __global__ __launch_bounds__(256) void k_loss_fwd(EdgeGeo geo, const float* __restrict__ y,
                                                   const float* __restrict__ sc,
@@ -94,6 +117,9 @@ __global__ __launch_bounds__(256) void k_loss_fwd(EdgeGeo geo, const float* __re
   EDGE_PROLOGUE
   const uint64_t key = seed_dev ? pf_noise_key(*seed_dev) : key0;
   __shared__ float scratch[4 * 64];
+  __shared__ __attribute__((aligned(16))) DecW<F> dw;
+  dw.load(Wd1, bd1, Wd2, bd2);
+  __syncthreads();
   float ft = 0.f;
   const float nw = (float)nvalid;
   CLASS_LOOP_BEGIN
@@ -105,7 +131,8 @@ __global__ __launch_bounds__(256) void k_loss_fwd(EdgeGeo geo, const float* __re
     }
     const float noise = noiselevel * (pf_uniform(key, (uint64_t)eu) - 0.5f);
     EdgeLoss<F> L;
-    L.run(x, Wd1, bd1, Wd2, bd2, scale, ci[cn], noise, sf);
+    const float* dwp = dec_base(dw);
+    L.run(x, dwp, dwp + F * F, dwp + F * F + F, dwp + F * F + 2 * F, scale, ci[cn], noise, sf);
     const float tt = fvalid ? L.tt : 0.f;
     ft += tt;
     if (tt_out && fvalid) tt_out[eu] = L.tt;
@@ -241,6 +268,9 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
   constexpr int LDS_N = (4 * WG::LDS_FLOATS > 4 * F * (F + 1)) ? 4 * WG::LDS_FLOATS
                                                                 : 4 * F * (F + 1);
   __shared__ float lds[LDS_N + 4 * (F + 1)];
+  __shared__ __attribute__((aligned(16))) DecW<F> dw;
+  dw.load(Wd1, bd1, Wd2, bd2);
+  __syncthreads();
   float* region = lds + wave * WG::LDS_FLOATS;
   WG wg;
   wg.zero();
@@ -263,7 +293,8 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
     float xf[F];
 #pragma unroll
     for (int k = 0; k < F; ++k) xf[k] = x[k];
-    L.run(xf, Wd1, bd1, Wd2, bd2, scale, Ti, noise, sf);
+    const float* dwp = dec_base(dw);
+    L.run(xf, dwp, dwp + F * F, dwp + F * F + F, dwp + F * F + 2 * F, scale, Ti, noise, sf);
     const float g_tt = Gf_f + Gv_c * (L.tt - tm_c);
     const float g_gal = Gn_c + Ti * g_tt;
     const float mask = L.graw > 0.f ? 1.f : (L.graw == 0.f ? 0.5f : 0.f);
@@ -276,7 +307,7 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
 #pragma unroll
     for (int j = 0; j < F; ++j) {
       acc[j] = fmaf(g_pred, L.ad[j], acc[j]);
-      gz[j] = Wd2[j] * g_pred * dlrelu(L.zd[j]);
+      gz[j] = dwp[F * F + F + j] * g_pred * dlrelu(L.zd[j]);
     }
     acc[F] += g_pred;
     if (fvalid) {
@@ -284,7 +315,7 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
       for (int k = 0; k < F; ++k) {
         float s = 0.f;
 #pragma unroll
-        for (int j = 0; j < F; ++j) s = fmaf(Wd1[j * F + k], gz[j], s);
+        for (int j = 0; j < F; ++j) s = fmaf(dwp[j * F + k], gz[j], s);
         gxe[(long long)k * E + e] = s;
       }
     }

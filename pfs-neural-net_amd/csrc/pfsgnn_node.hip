@@ -127,6 +127,7 @@ extern "C" const char* pfsgnn_version(void) { return "pfsgnn 0.1 gfx950"; }
 struct RedPack {
   RedDesc d[PF_MAX_RED];
 };
+static_assert(sizeof(RedPack) <= 4096, "k_reduce_rows' descriptor pack must fit the kernel arguments");
 
 __global__ __launch_bounds__(256) void k_reduce_rows(RedPack pk) {
   const RedDesc& D = pk.d[blockIdx.z];
