@@ -29,6 +29,21 @@
 
 #define CLASS_LOOP_END }
 
+// the next class's edge rows of this wave prefetched one iteration ahead
+// (register ring; the loop body is one long dependent chain per class)
+#define Y_PREFETCH_DECL(F)                                                    \
+  float yq[F];                                                              \
+  auto yload = [&](int cc) {                                                \
+    const long long ee = ((long long)gg * geo.NC + cc) * geo.NF + (fvalid ? f : 0); \
+    _Pragma("unroll") for (int k = 0; k < F; ++k)                           \
+      yq[k] = (fvalid && cc < c1) ? y[(long long)k * E + ee] : 0.f;         \
+  };                                                                        \
+  yload(c0 + wave);
+#define Y_TAKE(F, x)                                                          \
+  _Pragma("unroll") for (int k = 0; k < F; ++k)                             \
+    x[k] = sc ? fmaf(yq[k], sc[k], sh[k]) : yq[k];                          \
+  yload(c + 4);
+
 __device__ __forceinline__ void wave_lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
@@ -122,13 +137,11 @@ __global__ __launch_bounds__(256) void k_loss_fwd(EdgeGeo geo, const float* __re
   __syncthreads();
   float ft = 0.f;
   const float nw = (float)nvalid;
+  Y_PREFETCH_DECL(F)
   CLASS_LOOP_BEGIN
+    (void)e;
     float x[F];
-#pragma unroll
-    for (int k = 0; k < F; ++k) {
-      const float v = fvalid ? y[(long long)k * E + e] : 0.f;
-      x[k] = sc ? fmaf(v, sc[k], sh[k]) : v;
-    }
+    Y_TAKE(F, x)
     const float noise = noiselevel * (pf_uniform(key, (uint64_t)eu) - 0.5f);
     EdgeLoss<F> L;
     const float* dwp = dec_base(dw);
@@ -154,28 +167,49 @@ __global__ __launch_bounds__(256) void k_loss_fwd(EdgeGeo geo, const float* __re
         ((scratch[t] + scratch[64 + t]) + scratch[128 + t]) + scratch[192 + t];
 }
 
-__global__ void k_loss_class_reduce(const float* __restrict__ part, int G, int NFG, int NC,
-                                    int NF, float* __restrict__ n_prime, float* __restrict__ tmean,
-                                    float* __restrict__ tvar) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over G*NC
+__device__ __forceinline__ double wave_dsum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// one wave per class: lane l takes the fiber groups l, l + 64, ... and the
+// moments merge in closed form (mean = sum c_b m_b / sum c_b, M2 = sum (q_b +
+// c_b (m_b - mean)^2), in double; fixed lane and butterfly order): the loads
+// are independent, where a per-thread Chan chain ran NFG dependent divisions
+__global__ __launch_bounds__(256) void k_loss_class_reduce(const float* __restrict__ part, int G,
+                                                           int NFG, int NC, int NF,
+                                                           float* __restrict__ n_prime,
+                                                           float* __restrict__ tmean,
+                                                           float* __restrict__ tvar) {
+  const int idx = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;  // over G*NC
   if (idx >= G * NC) return;
   const int g = idx / NC, c = idx - g * NC;
-  double P = 0, C0 = 0, M0 = 0, Q0 = 0;
-  for (int b = 0; b < NFG; ++b) {
-    const float* q = part + (((size_t)g * NFG + b) * NC + c) * 4;
+  const float* q0 = part + ((size_t)g * NFG * NC + c) * 4;
+  const size_t stride = (size_t)NC * 4;
+  double P = 0, C = 0, S = 0;
+  for (int b = lane; b < NFG; b += 64) {
+    const float* q = q0 + (size_t)b * stride;
     P += q[0];
-    const double cb = q[1], mb = q[2], qb = q[3];
-    const double tot = C0 + cb;
-    if (tot > 0) {
-      const double d = mb - M0;
-      M0 += d * (cb / tot);
-      Q0 += qb + d * d * (C0 * cb / tot);
-    }
-    C0 = tot;
+    C += q[1];
+    S += (double)q[1] * (double)q[2];
   }
-  n_prime[idx] = (float)P;
-  tmean[idx] = (float)M0;
-  tvar[idx] = NF > 1 ? (float)(Q0 / (double)(NF - 1)) : NAN;  // torch.var, correction=1
+  P = wave_dsum(P);
+  C = wave_dsum(C);
+  S = wave_dsum(S);
+  const double M = C > 0 ? S / C : 0.0;
+  double Q = 0;
+  for (int b = lane; b < NFG; b += 64) {
+    const float* q = q0 + (size_t)b * stride;
+    const double d = (double)q[2] - M;
+    Q += (double)q[3] + (double)q[1] * d * d;
+  }
+  Q = wave_dsum(Q);
+  if (lane == 0) {
+    n_prime[idx] = (float)P;
+    tmean[idx] = (float)M;
+    tvar[idx] = NF > 1 ? (float)(Q / (double)(NF - 1)) : NAN;  // torch.var, correction=1
+  }
 }
 
 // torch.min propagates NaN (train.py:53: a class with N_i = 0 gives 0/0);
@@ -279,14 +313,11 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
   for (int j = 0; j <= F; ++j) acc[j] = 0.f;
   const float gs = gscale ? gscale[0] : 1.f;
   const float Gf_f = fvalid ? Gf[n] : 0.f;
+  Y_PREFETCH_DECL(F)
   CLASS_LOOP_BEGIN
     const float Ti = ci[cn], Gn_c = Gn[cn], Gv_c = Gv[cn], tm_c = tmean[cn];
     float x[F + 1];
-#pragma unroll
-    for (int k = 0; k < F; ++k) {
-      const float v = fvalid ? y[(long long)k * E + e] : 0.f;
-      x[k] = sc ? fmaf(v, sc[k], sh[k]) : v;
-    }
+    Y_TAKE(F, x)
     x[F] = 1.f;
     const float noise = noiselevel * (pf_uniform(key, (uint64_t)eu) - 0.5f);
     EdgeLoss<F> L;
@@ -507,7 +538,7 @@ extern "C" int pfsgnn_loss_fwd(int G, int NF, int NC, int F, const float* y, con
   if (geo.KS > 1)
     hipLaunchKernelGGL(k_fiber_partial_sum, dim3((unsigned)((geo.NS + 255) / 256)), dim3(256), 0,
                        st, ftp, geo.KS, geo.NS, fiber_time);
-  hipLaunchKernelGGL(k_loss_class_reduce, dim3((G * NC + 255) / 256), dim3(256), 0, st, part, G,
+  hipLaunchKernelGGL(k_loss_class_reduce, dim3((G * NC + 3) / 4), dim3(256), 0, st, part, G,
                      geo.NFG, NC, NF, n_prime, tmean, tvar);
   return pf::check_launch("pfsgnn_loss_fwd");
 }
