@@ -777,6 +777,7 @@ __global__ __launch_bounds__(256) void k_edge_bn_sums(EdgeGeo geo, const float* 
   float v[2 * F];
 #pragma unroll
   for (int k = 0; k < 2 * F; ++k) v[k] = 0.f;
+  // (a one-class prefetch ring, as the loss kernels', measured 87 -> 93 us: not kept)
   CLASS_LOOP_BEGIN
     pf_cptr m1 = pf_fresh(mu1), i1 = pf_fresh(inv1);
 #pragma unroll
