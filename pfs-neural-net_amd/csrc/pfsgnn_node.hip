@@ -112,15 +112,9 @@ extern "C" const char* pfsgnn_last_error(void) { return pf::g_err.c_str(); }
 extern "C" const char* pfsgnn_version(void) { return "pfsgnn 0.1 gfx950"; }
 
 // ---------------------------------------------------------------- reduce
-// One 64-lane wave per output element: lane l sums partials l, l+64, ... in
-// order, then a fixed butterfly -- deterministic, and every lane's loads are
-// independent (no serial chain over the blocks).
 // Partial reductions out[r][c] (+)= scale * sum_b part[b*plen + r*ldp + c],
-// up to PF_MAX_RED independent ones per launch (blockIdx.z picks one).  A block
-// owns 16 consecutive outputs x 16 partial lanes: thread (o, pl) sums partials
-// b = pl, pl+16, ... with 4 independent accumulators (4 loads in flight); the
-// 16 lanes are combined in a fixed order -- deterministic for a given nb.
-// Long lists (nb > 256) first take an in-place stage: segment s of RED_SEG
+// up to PF_MAX_RED independent ones per launch (blockIdx.z picks one; block
+// layout below).  Long lists (nb > 256) first take an in-place stage: segment s of RED_SEG
 // partials is summed into the segment's first row (each block touches only its
 // own cells; the descriptors of one launch never share cells).
 #define RED_SEG 128
@@ -129,6 +123,16 @@ struct RedPack {
 };
 static_assert(sizeof(RedPack) <= 4096, "k_reduce_rows' descriptor pack must fit the kernel arguments");
 
+// k_reduce_rows: a block owns 16 consecutive outputs x 16 partial lanes; lane
+// (o, pl) sums partials b = pl, pl + 16, ... with 4 independent accumulators
+// (4 loads in flight), the 16 lanes combined in a fixed order -- deterministic
+// for a given nb.  k_reduce_seg (a segment of RED_SEG partials per block): RED_O
+// consecutive outputs x RED_P lanes, so a wave reads 256 contiguous bytes of a
+// partial row per load (16 x 16 read 64-byte runs: the deferred flush's 48-way
+// segment stage took 55 us; measured 74 -> 57 us per step.  The same layout in
+// k_reduce_rows, whose lists are short, was slower: 82 -> 109 us).
+#define RED_O 64
+#define RED_P 4
 __global__ __launch_bounds__(256) void k_reduce_rows(RedPack pk) {
   const RedDesc& D = pk.d[blockIdx.z];
   const int t = threadIdx.x, o = t & 15, pl = t >> 4;
@@ -160,28 +164,30 @@ __global__ __launch_bounds__(256) void k_reduce_rows(RedPack pk) {
 
 __global__ __launch_bounds__(256) void k_reduce_seg(RedPack pk) {
   const RedDesc& D = pk.d[blockIdx.z];
-  const int t = threadIdx.x, o = t & 15, pl = t >> 4;
-  const int idx = blockIdx.x * 16 + o;
+  const int t = threadIdx.x, o = t & (RED_O - 1), pl = t / RED_O;
+  const int idx = blockIdx.x * RED_O + o;
   const int b0 = blockIdx.y * RED_SEG;
-  if (blockIdx.x * 16 >= D.rows * D.cols || b0 >= D.nb || D.nb <= 2 * RED_SEG) return;
+  if (blockIdx.x * RED_O >= D.rows * D.cols || b0 >= D.nb || D.nb <= 2 * RED_SEG) return;
   const bool v = idx < D.rows * D.cols;
   const int r = v ? idx / D.cols : 0, c = v ? idx - r * D.cols : 0;
   const int b1 = min(D.nb, b0 + RED_SEG);
   float* p = const_cast<float*>(D.part) + (size_t)r * D.ldp + c;
-  float s0 = 0.f, s1 = 0.f;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   int b = b0 + pl;
-  for (; b + 16 < b1; b += 32) {
+  for (; b + 3 * RED_P < b1; b += 4 * RED_P) {
     s0 += p[(size_t)b * D.plen];
-    s1 += p[(size_t)(b + 16) * D.plen];
+    s1 += p[(size_t)(b + RED_P) * D.plen];
+    s2 += p[(size_t)(b + 2 * RED_P) * D.plen];
+    s3 += p[(size_t)(b + 3 * RED_P) * D.plen];
   }
-  if (b < b1) s0 += p[(size_t)b * D.plen];
-  __shared__ float sh[16][17];
-  sh[pl][o] = s0 + s1;
+  for (; b < b1; b += RED_P) s0 += p[(size_t)b * D.plen];
+  __shared__ float sh[RED_P][RED_O];
+  sh[pl][o] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (t < 16 && v) {
+  if (t < RED_O && v) {
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) s += sh[i][t];
+    for (int i = 0; i < RED_P; ++i) s += sh[i][t];
     p[(size_t)b0 * D.plen] = s;
   }
 }
@@ -190,18 +196,19 @@ void launch_reduce_multi(const RedDesc* d, int n, hipStream_t st) {
   for (int i0 = 0; i0 < n; i0 += PF_MAX_RED) {
     const int m = std::min(PF_MAX_RED, n - i0);
     RedPack pk{};
-    int gx = 1, gy = 1;
+    int gx = 1, gxs = 1, gy = 1;
     bool seg = false;
     for (int i = 0; i < m; ++i) {
       pk.d[i] = d[i0 + i];
       gx = std::max(gx, (pk.d[i].rows * pk.d[i].cols + 15) / 16);
+      gxs = std::max(gxs, (pk.d[i].rows * pk.d[i].cols + RED_O - 1) / RED_O);
       if (pk.d[i].nb > 2 * RED_SEG) {
         seg = true;
         gy = std::max(gy, (pk.d[i].nb + RED_SEG - 1) / RED_SEG);
       }
     }
     if (seg) {
-      hipLaunchKernelGGL(k_reduce_seg, dim3(gx, gy, m), dim3(256), 0, st, pk);
+      hipLaunchKernelGGL(k_reduce_seg, dim3(gxs, gy, m), dim3(256), 0, st, pk);
       for (int i = 0; i < m; ++i)
         if (pk.d[i].nb > 2 * RED_SEG) {
           pk.d[i].nb = (pk.d[i].nb + RED_SEG - 1) / RED_SEG;
