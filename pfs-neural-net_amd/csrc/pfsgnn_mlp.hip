@@ -1041,10 +1041,21 @@ size_t bwd_lds(int m) {   // (RS: a 64-row input-gradient buffer, one output-til
 
 // blocks per CU: the M <= 3 kernels fit 2 (registers, LDS), the wider ones
 // run one 4-wave block per CU with up to 512 registers per lane
+// The grid is balanced over the rounds the chunks need anyway (599 chunks at
+// 512 slots: 300 blocks of 2 chunks, not 512 of which 87 run a second one),
+// so fewer blocks stage the weight images for the same number of chunk rounds
+// (opt-in knob PFSGNN_MLP_BALANCE=1, default off: one block per slot).
 int grid_for(int N, int m, size_t lds) {
+  static const bool bal = [] {
+    const char* e = getenv("PFSGNN_MLP_BALANCE");
+    return e && atoi(e) != 0;
+  }();
   const int nch = (N + 63) / 64;
   const int per_cu = (lds <= 80 * 1024) ? 2 : 1;   // (160 KB of LDS per CU)
-  return std::max(1, std::min(nch, 256 * per_cu));
+  const int slots = 256 * per_cu;
+  if (!bal) return std::max(1, std::min(nch, slots));
+  const int rounds = (nch + slots - 1) / slots;
+  return std::max(1, (nch + rounds - 1) / rounds);
 }
 
 // pfsgnn_seg list -> InSegs (blocks must be contiguous in the weight columns)
