@@ -479,6 +479,14 @@ typedef struct {
   long long E;               /* edges */
   int maxdeg;                /* largest fiber degree */
 } pfsgnn_sliced_t;
+/* The most classes per graph (NC) the sliced kernels of the CURRENT edge path
+ * take at Fdim F: every kernel's static LDS plus its per-class tables must fit
+ * the CU's 160 KB (e.g. 124 at Fdim 16 on the default path), and at most 128.
+ * 0: no sliced kernels for this (F, path) -- the bf16 edge-state paths and
+ * Fdims other than 8 / 10 / 16.  A batch above the limit runs the composed
+ * general-graph ops (pfsgnn.sparse); the pfsgnn_sl_* ops refuse it.
+ * (Host-side query; it reads the kernels' attributes from the HIP runtime.) */
+int pfsgnn_sliced_max_nc(int F, int* nc);
 size_t pfsgnn_sliced_plan_ws_bytes(int G, int NF);
 /* From fib_ptr [G*NF+1] (pfsgnn_sparse_layout): the slice lanes `fib`, lengths
  * `len`, first positions `base`, slot_of [G*NF] (the slice lane 16 s + j of
@@ -702,10 +710,15 @@ int pfsgnn_edges_from_canonical(const float* y, const float* sc, const float* sh
  * float) overrides `step` (capturable form).  live (optional, device byte
  * per element): elements with live[i] == 0 belong to parameters whose .grad
  * the reference leaves None (unused by the loss); torch.optim.Adam skips
- * those, so they are left untouched (matters when weight_decay != 0). */
+ * those, so they are left untouched (matters when weight_decay != 0).
+ * The hyper-parameters are the Python floats (doubles) torch's Adam holds:
+ * its scalars 1 - beta1, 1 - beta2 and lr / (1 - beta1^t) are formed in
+ * double and rounded to fp32 once, as torch does (torch/optim/adam.py
+ * _single_tensor_adam), so the update is torch's bit for bit up to the
+ * order of the last division (CUDA's addcdiv: value * (m / denom)). */
 int pfsgnn_adam(float* p, const float* g, float* m, float* v, long long n, int step,
-                const float* step_dev, float lr, float beta1, float beta2, float eps,
-                float weight_decay, const unsigned char* live, void* stream);
+                const float* step_dev, double lr, double beta1, double beta2, double eps,
+                double weight_decay, const unsigned char* live, void* stream);
 
 #ifdef __cplusplus
 }

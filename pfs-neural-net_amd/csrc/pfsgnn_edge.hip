@@ -22,6 +22,8 @@
 #include "pfsgnn_mfma.h"
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 
 #define EDGE_PROLOGUE                                                       \
   const int t = threadIdx.x, lane = t & 63;                                 \
@@ -1469,14 +1471,29 @@ EdgeGeo geo_for(int G, int NF, int NC) {
 pfm::SlGeo sl_of(const pfsgnn_sliced_t& s) {
   return pfm::SlGeo{s.fib, s.base, s.len, s.cls, s.pco, s.EP, s.E, s.maxdeg};
 }
+// classes per graph the sliced kernels of the current edge path take at Fdim F
+// (both models' precisions; cached per (F, path): hipFuncGetAttributes per kernel)
+int sliced_max_nc(int F) {
+  if (mf_bfy()) return 0;
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, int> memo;
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_pair(F, g_path);
+  auto it = memo.find(key);
+  if (it != memo.end()) return it->second;
+  const int p0 = mf_prec(0, F), p1 = mf_prec(1, F);
+  const int m = std::min(pfm::sl_max_nc(F, p0), p1 == p0 ? pfm::SL_MAX_NC : pfm::sl_max_nc(F, p1));
+  memo[key] = m;
+  return m;
+}
 int check_sliced(const char* where, const pfsgnn_sliced_t* sl, int NC, int F) {
   if (!sl) return 0;
   if (sl->EP * F * 4 >= (1ll << 32)) return pf::fail(where, "edge tensor exceeds 4 GiB (split the batch)");
   if (!sl->fib || !sl->base || !sl->len || !sl->cls || !sl->pco || sl->EP <= 0 || sl->E <= 0 ||
       sl->EP < sl->E)
     return pf::fail(where, "bad sliced layout");
-  if (NC > pfm::SL_MAX_NC) return pf::fail(where, "sliced layout: NC > 128 classes per graph");
   if (mf_bfy()) return pf::fail(where, "sliced layout: bf16 edge-state paths are not supported");
+  if (NC > sliced_max_nc(F)) return pf::fail(where, "sliced layout: too many classes per graph for the LDS (pfsgnn_sliced_max_nc)");
   return 0;
 }
 // the grid of an edge op: the complete path's, or the sliced batch's
@@ -1501,6 +1518,12 @@ extern "C" int pfsgnn_set_edge_path(int path) {
   return 0;
 }
 extern "C" int pfsgnn_get_edge_path(void) { return g_path; }
+
+extern "C" int pfsgnn_sliced_max_nc(int F, int* nc) {
+  PF_REQUIRE(nc, "pfsgnn_sliced_max_nc", "null");
+  *nc = sliced_max_nc(F);
+  return 0;
+}
 
 extern "C" int pfsgnn_edge_grid(int G, int NF, int NC, int* info) {
   PF_REQUIRE(G > 0 && NF > 0 && NC > 0 && info, "pfsgnn_edge_grid", "bad arguments");

@@ -70,6 +70,9 @@ struct SlGeo {
   int maxdeg;
 };
 static constexpr int SL_MAX_NC = 128;   // classes per graph (LDS class rows + accumulators)
+// the most classes per graph that every sliced kernel of (F, prec) fits in the
+// LDS (static + dynamic <= 160 KB), <= SL_MAX_NC; 0: (F, prec) not built
+int sl_max_nc(int F, int prec);
 EdgeGeo sl_geo(int G, int NF, int NC, const SlGeo& sl);
 int sl_edge_mlp_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* xe, const float* xsc,
                     const float* xsh, const float* Ps, const float* PtS, const float* W1,

@@ -590,10 +590,15 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   const long long CNS = (long long)C * NS;
   const bool tpart = Rs != nullptr;
 
-  FwdLayer<FPS(PREC), C, F> L1s, L1t;   // L1t: TModel's layer, recomputed unless TM
+  RecLayer<PREC, C, F> L1s, L1t;   // L1t: TModel's layer, recomputed unless TM
+  RecLayer<PREC, C, C> L2;
+  constexpr int R1 = RecLds<RecLayer<PREC, C, F>>::n, R2 = RecLds<RecLayer<PREC, C, C>>::n;
+  __shared__ s16x8 recw[(R1 * (TM ? 1 : 2) + R2) > 0 ? R1 * (TM ? 1 : 2) + R2 : 1];
+  rec_bind(L1s, recw);
+  rec_bind(L2, recw + R1);
+  rec_bind(L1t, recw + R1 + R2);
   L1s.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
   if constexpr (!TM) L1t.load([&](int h, int k) { return tpart ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
-  FwdLayer<FPS(PREC), C, C> L2;
   L2.load([&](int o, int h) { return Ws2[o * C + h]; }, lane);
   // gradient chains: exact fp32, bf16x3 or bf16 by PREC
   GradLayer<PREC, C, C> L2T;

@@ -255,6 +255,61 @@ struct LayerB6 {
   }
 };
 
+// The same bf16x6 layer with its weight tuples staged in LDS instead of held
+// in registers: [2 (t * KT + u) + {0: Wh|Wm, 1: Wh|Wl}][64 lanes] x 16 bytes, one
+// conflict-free ds_read_b128 per MFMA operand.  For a backward kernel's
+// recompute whose registers are already full (km_source_bwd at PREC 4: the
+// register-resident tuples cost 32 more VGPRs and spill), so that the recompute
+// runs exactly the forward kernel's arithmetic -- same operands, same MFMA
+// order, bitwise the same messages.  bind() gives the LDS block; load() is
+// executed by every wave, wave 0 writes (the kernel's __syncthreads after its
+// staging publishes the tuples).  The reads sit behind the loop's lds_order()
+// points, so the compiler cannot hoist them back into registers.
+template <int M, int K>
+struct LayerB6S {
+  static constexpr int MT = GM<M>::NT, KT = GM<K>::NT, NOP = 2 * MT * KT;
+  const s16x8* w = nullptr;   // this lane's operand 0; operand o at w[64 o]
+  s16x8* base = nullptr;
+  __device__ __forceinline__ void bind(s16x8* lds) { base = lds; }
+  template <class Fn>
+  __device__ __forceinline__ void load(Fn fn, int lane) {
+    w = base + lane;
+    if ((threadIdx.x >> 6) != 0) return;
+    const int g = lane >> 4, i = lane & 15;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+        floatx4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ro = GM<M>::mrow(t, i), ri = GM<K>::row(g, 4 * u + j);
+          v[j] = (ro >= 0 && ri >= 0) ? fn(ro, ri) : 0.f;
+        }
+        const Fr3 a = split3(v);
+        base[(2 * (t * KT + u)) * 64 + lane] = cat8(a.h, a.m);
+        base[(2 * (t * KT + u) + 1) * 64 + lane] = cat8(a.h, a.l);
+      }
+  }
+  __device__ __forceinline__ void apply(const Fr3 (&x)[KT], floatx4 (&y)[MT]) const {
+#pragma unroll
+    for (int u = 0; u < KT; ++u) {
+      const s16x8 b1 = cat8(x[u].l, x[u].m), b2 = cat8(x[u].m, x[u].h), b3 = cat8(x[u].h, x[u].h);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const s16x8 ahm = w[(2 * (t * KT + u)) * 64], ahl = w[(2 * (t * KT + u) + 1) * 64];
+        y[t] = mf8(ahm, b3, mf8(ahl, b2, mf8(ahm, b1, y[t])));
+      }
+    }
+  }
+  __device__ __forceinline__ void apply(const floatx4 (&x)[KT], floatx4 (&y)[MT]) const {
+    Fr3 s[KT];
+#pragma unroll
+    for (int u = 0; u < KT; ++u) s[u] = split3(x[u]);
+    apply(s, y);
+  }
+};
+
 // ------------------------------------------------------------ weight gradients
 // acc += A B^T summed over a tile's 16 edges (edge = MFMA K), A and B read from
 // wave-private bf16 images (hi and lo planes), as 2 v_mfma_f32_16x16x32_bf16:
@@ -329,16 +384,31 @@ struct LayerB1 {
 // exactly the arithmetic of the forward kernel, so the recomputed activations
 // and LeakyReLU masks are bitwise those of the forward pass.
 __host__ __device__ constexpr int FP(int prec) { return prec >= 2 ? prec : 0; }
-// source_bwd's recompute at PREC 4 stays exact fp32 (LayerF): the bf16x6 weight
-// tuples would push that kernel past 256 VGPRs (spills).  Its activations then
-// differ from the forward's by fp32 rounding only, the level at which the fp32
-// reference differs from the float64 oracle.
-__host__ __device__ constexpr int FPS(int prec) { return prec == 4 ? 0 : FP(prec); }
 template <int PREC, int M, int K>
 using FwdLayer = std::conditional_t<
     PREC == 2, LayerB1<M, K>,
     std::conditional_t<PREC == 3, LayerB3<M, K>,
                        std::conditional_t<PREC == 4, LayerB6<M, K>, LayerF<M, K>>>>;
+// The recompute layers of source_bwd: the forward's arithmetic (FwdLayer<FP>),
+// with the bf16x6 tuples staged in LDS (LayerB6S) -- held in registers they
+// push that kernel past 256 VGPRs.  Round 3 ran this recompute in exact fp32
+// instead; the moments' backward then combined forward statistics with
+// messages of another rounding, which 1/std^3 and 1/std^4 amplify on fibers
+// of nearly constant messages (22x the parity bar on a 24x16 graph).
+template <int PREC, int M, int K>
+using RecLayer = std::conditional_t<FP(PREC) == 4, LayerB6S<M, K>, FwdLayer<FP(PREC), M, K>>;
+template <class L>
+struct RecLds {   // s16x8 operands of L's LDS image (0: a register layer)
+  static constexpr int n = 0;
+};
+template <int M, int K>
+struct RecLds<LayerB6S<M, K>> {
+  static constexpr int n = LayerB6S<M, K>::NOP * 64;
+};
+template <class L>
+__device__ __forceinline__ void rec_bind(L&, s16x8*) {}
+template <int M, int K>
+__device__ __forceinline__ void rec_bind(LayerB6S<M, K>& l, s16x8* p) { l.bind(p); }
 template <int PREC, int M, int K>
 using GradLayer = std::conditional_t<
     PREC == 0, LayerF<M, K>, std::conditional_t<PREC == 2, LayerB1<M, K>, LayerB3<M, K>>>;

@@ -1949,48 +1949,71 @@ extern "C" int pfsgnn_moment_coef_seg(const float* mom, const float* gst, int C,
 }
 
 // ---------------------------------------------------------------- adam
-// torch.optim.Adam single-tensor semantics (torch/optim/adam.py
-// _single_tensor_adam, amsgrad=False): bias corrections on the host in double.
+// torch.optim.Adam as the reference runs it on a GPU (torch/optim/adam.py
+// _multi_tensor_adam, the default for device tensors; amsgrad=False): the
+// scalars torch forms in double (1 - beta1, 1 - beta2, lr / bias_correction1,
+// sqrt(bias_correction2)) are formed in double here too and rounded to fp32
+// once, and the element arithmetic is fp32 in the order of torch's device
+// kernels, fused multiply-adds where they contract:
+//   exp_avg.lerp_(g, 1 - beta1)          m = fma(1 - beta1, g - m, m)
+//   exp_avg_sq.mul_(beta2)               v = v * beta2
+//   .addcmul_(g, g, 1 - beta2)           v = fma(1 - beta2, g * g, v)
+//   denom = sqrt(v) / sqrt(bc2) + eps    (three roundings)
+//   p.addcdiv_(m, denom, -step_size)     p = fma(-step_size, m / denom, p)
+struct AdamK {
+  float omb1, omb2, b2, eps, wd;   // fp32 scalars as torch rounds them
+  float neg_step, bc2_sqrt;        // host step
+  double beta1, beta2, lr;         // capturable: bias corrections on the device
+};
 __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                       float* __restrict__ v, long long n, float neg_step0, float beta1, float beta2,
-                       float bc2_sqrt0, float eps, float wd, float lr,
+                       float* __restrict__ v, long long n, AdamK k,
                        const float* __restrict__ step_dev, const unsigned char* __restrict__ live) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   // a parameter whose .grad the reference leaves None is skipped by
   // torch.optim.Adam: no decay, moments and value untouched
   if (live && !live[i]) return;
-  float neg_step = neg_step0, bc2_sqrt = bc2_sqrt0;
+  float neg_step = k.neg_step, bc2_sqrt = k.bc2_sqrt;
   if (step_dev) {  // capturable form: the step count lives on the device
     const double st = (double)*step_dev;
-    const double bc1 = 1.0 - pow((double)beta1, st);
-    const double bc2 = 1.0 - pow((double)beta2, st);
-    neg_step = (float)(-(double)lr / bc1);
+    const double bc1 = 1.0 - pow(k.beta1, st);
+    const double bc2 = 1.0 - pow(k.beta2, st);
+    neg_step = (float)(-(k.lr / bc1));
     bc2_sqrt = (float)sqrt(bc2);
   }
   float gi = g[i];
-  if (wd != 0.f) gi = gi + wd * p[i];
+  if (k.wd != 0.f) gi = fmaf(k.wd, p[i], gi);              // grad.add(param, alpha=wd)
   const float mo = m[i];
-  const float mi = mo + (1.f - beta1) * (gi - mo);        // exp_avg.lerp_(grad, 1-beta1)
-  const float vi = v[i] * beta2 + (1.f - beta2) * gi * gi; // mul_(beta2).addcmul_(g, g, 1-beta2)
+  const float mi = fmaf(k.omb1, gi - mo, mo);              // exp_avg.lerp_(grad, 1-beta1)
+  const float vb = __fmul_rn(v[i], k.b2);                  // exp_avg_sq.mul_(beta2)
+  const float vi = fmaf(k.omb2, __fmul_rn(gi, gi), vb);    // .addcmul_(g, g, 1-beta2)
   m[i] = mi;
   v[i] = vi;
-  const float denom = sqrtf(vi) / bc2_sqrt + eps;          // (sqrt(v)/sqrt(bc2)).add_(eps)
-  p[i] = p[i] + neg_step * (mi / denom);                   // addcdiv_(m, denom, -lr/bc1)
+  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vi), bc2_sqrt), k.eps);  // sqrt(v)/sqrt(bc2) + eps
+  p[i] = fmaf(neg_step, __fdiv_rn(mi, denom), p[i]);       // addcdiv_(m, denom, -lr/bc1)
 }
 
 extern "C" int pfsgnn_adam(float* p, const float* g, float* m, float* v, long long n, int step,
-                           const float* step_dev, float lr, float beta1, float beta2, float eps,
-                           float weight_decay, const unsigned char* live, void* stream) {
+                           const float* step_dev, double lr, double beta1, double beta2,
+                           double eps, double weight_decay, const unsigned char* live,
+                           void* stream) {
   PF_REQUIRE(p && g && m && v && n > 0 && (step >= 1 || step_dev), "pfsgnn_adam",
              "bad arguments");
   const int st = step >= 1 ? step : 1;
-  const double bc1 = 1.0 - std::pow((double)beta1, st);
-  const double bc2 = 1.0 - std::pow((double)beta2, st);
-  const float neg_step = (float)(-(double)lr / bc1);
-  const float bc2_sqrt = (float)std::sqrt(bc2);
+  const double bc1 = 1.0 - std::pow(beta1, st);
+  const double bc2 = 1.0 - std::pow(beta2, st);
+  AdamK k;
+  k.omb1 = (float)(1.0 - beta1);
+  k.omb2 = (float)(1.0 - beta2);
+  k.b2 = (float)beta2;
+  k.eps = (float)eps;
+  k.wd = (float)weight_decay;
+  k.neg_step = (float)(-(lr / bc1));
+  k.bc2_sqrt = (float)std::sqrt(bc2);
+  k.beta1 = beta1;
+  k.beta2 = beta2;
+  k.lr = lr;
   hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream),
-                     p, g, m, v, n, neg_step, beta1, beta2, bc2_sqrt, eps, weight_decay, lr,
-                     step_dev, live);
+                     p, g, m, v, n, k, step_dev, live);
   return pf::check_launch("pfsgnn_adam");
 }

@@ -635,10 +635,15 @@ __global__ __launch_bounds__(256, 2) void ksl_source_bwd(
   const long long CNS = (long long)C * NS;
   const bool tpart = Rs != nullptr;
 
-  FwdLayer<FPS(PREC), C, F> L1s, L1t;
+  RecLayer<PREC, C, F> L1s, L1t;   // the forward's arithmetic (pfsgnn_mfma_core.h RecLayer)
+  RecLayer<PREC, C, C> L2;
+  constexpr int R1 = RecLds<RecLayer<PREC, C, F>>::n, R2 = RecLds<RecLayer<PREC, C, C>>::n;
+  __shared__ s16x8 recw[(R1 * (TM ? 1 : 2) + R2) > 0 ? R1 * (TM ? 1 : 2) + R2 : 1];
+  rec_bind(L1s, recw);
+  rec_bind(L2, recw + R1);
+  rec_bind(L1t, recw + R1 + R2);
   L1s.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
   if constexpr (!TM) L1t.load([&](int h, int k) { return tpart ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
-  FwdLayer<FPS(PREC), C, C> L2;
   L2.load([&](int o, int h) { return Ws2[o * C + h]; }, lane);
   GradLayer<PREC, C, C> L2T;
   L2T.load([&](int h, int o) { return Ws2[o * C + h]; }, lane);
@@ -991,11 +996,20 @@ EdgeGeo sl_geo(int G, int NF, int NC, const SlGeo& sl) {
 
 namespace {
 
+// static LDS of a kernel instantiation (its __shared__ arrays)
+template <class K>
+size_t static_lds(K kernel) {
+  hipFuncAttributes a{};
+  if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(kernel)) != hipSuccess) return 0;
+  return a.sharedSizeBytes;
+}
+constexpr size_t LDS_CU = 160 * 1024;
 // dynamic LDS of a kernel (class rows + accumulators), opted in above 64 KB once
-// per kernel instantiation
+// per kernel instantiation; static + dynamic must fit the CU's 160 KB
 template <class K>
 int dyn_lds(K kernel, size_t bytes) {
-  if (bytes > 160 * 1024) return pf::fail("pfsgnn sliced", "class tables exceed the LDS (NC too large)");
+  if (bytes + static_lds(kernel) > LDS_CU)
+    return pf::fail("pfsgnn sliced", "class tables exceed the LDS (NC too large)");
   if (bytes > 64 * 1024) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
@@ -1160,6 +1174,47 @@ int sl_edge_mlp_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* g_t
                      y, xe, xsc, xsh, Ps, PtS, W1, W2, gxe, gs, pW2, pW1, pCol);
   SL_SWITCH(F, prec, SL_C)
 #undef SL_C
+}
+
+// The most classes per graph every sliced kernel of (F, prec) fits in the LDS:
+// static LDS + the per-class bytes of its dynamic tables (the launchers'
+// formulas above) <= 160 KB, and <= SL_MAX_NC.  0: no sliced kernels for (F, prec).
+int sl_max_nc(int F, int prec) {
+  auto cap = [](size_t stat, size_t per_class) {
+    if (stat >= LDS_CU) return 0;
+    const size_t n = per_class ? (LDS_CU - stat) / per_class : (size_t)SL_MAX_NC;
+    return (int)std::min<size_t>(n, SL_MAX_NC);
+  };
+  const size_t tc = kGTab ? 0 : (size_t)cp_of(2 * F) * 4, th = kGTab ? 0 : (size_t)cp_of(4 * F) * 4;
+  const size_t ac = (size_t)4 * (2 * F + 1) * 4, ah = (size_t)4 * (4 * F + 1) * 4;
+  int m = SL_MAX_NC;
+  const int fp = FP(prec);
+#define SL_M(FF, PP)                                                                               \
+  case FF * 8 + PP:                                                                                \
+    m = std::min(m, cap(static_lds(ksl_target_bwd<FF, PP, true>), tc));                            \
+    m = std::min(m, cap(static_lds(ksl_target_bwd<FF, PP, false>), tc));                           \
+    m = std::min(m, cap(static_lds(ksl_source_bwd<FF, PP, true>), ac));                            \
+    m = std::min(m, cap(static_lds(ksl_source_bwd<FF, PP, false>), ac));                           \
+    m = std::min(m, cap(static_lds(ksl_edge_mlp_bwd<FF, PP>), th + ah));                           \
+    break;
+  switch (F * 8 + prec) {
+    SL_M(8, 0) SL_M(8, 1) SL_M(10, 0) SL_M(10, 1) SL_M(10, 2) SL_M(10, 3) SL_M(10, 4)
+    SL_M(16, 0) SL_M(16, 1)
+    default: return 0;
+  }
+#undef SL_M
+#define SL_MF(FF, PP)                                                                              \
+  case FF * 8 + PP:                                                                                \
+    m = std::min(m, cap(static_lds(ksl_edge_mlp_fwd<FF, PP>), th));                                \
+    m = std::min(m, cap(static_lds(ksl_source_fwd<FF, PP>), tc));                                  \
+    m = std::min(m, cap(static_lds(ksl_target_fwd<FF, PP>), ac));                                  \
+    break;
+  switch (F * 8 + fp) {
+    SL_MF(8, 0) SL_MF(10, 0) SL_MF(10, 2) SL_MF(10, 3) SL_MF(10, 4) SL_MF(16, 0)
+    default: return 0;
+  }
+#undef SL_MF
+  return m;
 }
 
 }  // namespace pfm

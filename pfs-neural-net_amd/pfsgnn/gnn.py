@@ -163,12 +163,20 @@ class Layout:
         self.sp = sp
 
 
+def sliced_on():
+    return os.environ.get("PFSGNN_SLICED", "1") != "0"
+
+
 def sliced_ok(NC, F):
     """General batches run on the fused sliced kernels (pfsgnn_sliced.hip) when
-    their class tables fit the LDS (NC <= 128 classes per graph) and Fdim is
-    8, 10 or 16, unless PFSGNN_SLICED=0 (the composed ops of pfsgnn.sparse)."""
-    return (os.environ.get("PFSGNN_SLICED", "1") != "0" and NC <= 128 and F in (8, 10, 16)
-            and hasattr(backend(), "sliced_layout"))
+    the current edge path has them at this Fdim and their class tables fit the
+    LDS (``pfsgnn_sliced_max_nc``: at most 128 classes per graph, 124 at Fdim
+    16; none on the bf16 edge-state paths), unless PFSGNN_SLICED=0 (the
+    composed ops of pfsgnn.sparse)."""
+    be = backend()
+    if not (sliced_on() and F in (8, 10, 16) and hasattr(be, "sliced_layout")):
+        return False
+    return NC <= be.sliced_max_nc(F)
 
 
 def geometry(x_s, x_t, x_u, edge_index, F):
@@ -183,7 +191,11 @@ def geometry(x_s, x_t, x_u, edge_index, F):
     E = int(edge_index.size(1))
     if E == 0:
         raise ValueError("edge_index has no edges")
-    key = (E, G, NF, NC)
+    # the layout depends on the sliced/composed choice, which depends on Fdim
+    # and the edge path (sliced_ok), so they are part of the key
+    be = backend()
+    path = be.edge_path() if hasattr(be, "edge_path") else None
+    key = (E, G, NF, NC, F, path, sliced_on())
     hit = _LAYOUT_CACHE.get(edge_index, key)
     if hit is None:
         complete = False

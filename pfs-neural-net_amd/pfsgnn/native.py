@@ -193,7 +193,9 @@ _SIGS = {
     "pfsgnn_layout_analyze": ([P, LL, I, I, I, P, P, P, SZ, P], I),
     "pfsgnn_edges_to_canonical": ([P, I, I, I, I, I, P, P, P], I),
     "pfsgnn_edges_from_canonical": ([P, P, P, I, I, I, I, I, P, I, P, P], I),
-    "pfsgnn_adam": ([P, P, P, P, LL, I, P, FL, FL, FL, FL, FL, P, P], I),
+    "pfsgnn_adam": ([P, P, P, P, LL, I, P, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                     ctypes.c_double, ctypes.c_double, P, P], I),
+    "pfsgnn_sliced_max_nc": ([I, ctypes.POINTER(ctypes.c_int)], I),
     "pfsgnn_sliced_plan_ws_bytes": ([I, I], SZ),
     "pfsgnn_sliced_plan": ([P, I, I, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_sliced_fill": ([P, P, P, P, LL, I, I, P, P, LL, I, P, P, P, P], I),
@@ -311,9 +313,22 @@ _SYNC = None
 def _ensure_sync(device):
     """The library's in-launch reduction counters (pfsgnn_set_sync_buffer): one
     zeroed device buffer per process, set once.  PFSGNN_NO_HANDOFF=1 leaves it
-    unset (the kernels then keep their separate reduce launches: an A/B knob)."""
+    unset (the kernels then keep their separate reduce launches: an A/B knob).
+
+    The counters are process-wide, so pfsgnn ops run on ONE device per process
+    (the one-process-per-GPU model of torch.distributed) and on one stream at a
+    time; a backend on a second device is refused rather than pointed at
+    another device's counters."""
     global _SYNC
-    if _SYNC is not None or os.environ.get("PFSGNN_NO_HANDOFF", "0") == "1":
+    if os.environ.get("PFSGNN_NO_HANDOFF", "0") == "1":
+        return
+    if _SYNC is not None:
+        dev = torch.device(device)
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        if _SYNC.device.index != idx:
+            raise RuntimeError(
+                f"pfsgnn runs on one device per process: its sync buffer lives on "
+                f"{_SYNC.device}, a backend on {dev} was requested (one process per GPU)")
         return
     n = lib().pfsgnn_sync_bytes()
     _SYNC = torch.zeros(n, dtype=torch.uint8, device=device)
@@ -358,6 +373,10 @@ class HipBackend:
         self._retired = []
         self._sp = SparseEdgeOps(self)
         _ensure_sync(self.device)
+
+    def edge_path(self):
+        """The current edge path's code (pfsgnn_get_edge_path)."""
+        return lib().pfsgnn_get_edge_path()
 
     # ------------------------------------------------------------ memory
     def empty(self, *shape):
@@ -1161,6 +1180,14 @@ class HipBackend:
                              f"graphs (G={G}, NF={NF}, NC={NC}; gnn.py:32-47 batching)")
         deg_t = (cls_ptr[1:] - cls_ptr[:-1]).to(torch.float32).reshape(1, -1).contiguous()
         return SparseGeo(E, src_p, tgt_p, user_of, fib_ptr, cls_ord, cls_ptr, deg_t)
+
+    def sliced_max_nc(self, F):
+        """Classes per graph the fused sliced kernels of the current edge path
+        take at Fdim F (pfsgnn_sliced_max_nc: static + per-class LDS <= 160 KB);
+        0 when that path has no sliced kernels (the bf16 edge-state paths)."""
+        nc = ctypes.c_int(0)
+        _call("pfsgnn_sliced_max_nc", int(F), ctypes.byref(nc))
+        return nc.value
 
     def sliced_layout(self, sp, G, NF, NC):
         """Slices of 16 fibers over a sparse layout (pfsgnn_sliced_plan / _fill):

@@ -733,6 +733,35 @@ class EmuBackend:
         out.copy_(r)
         return out
 
+    # ------------------------------------------------------------ optimizer
+    def adam(self, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, live=None):
+        """pfsgnn_adam (pfsgnn_node.hip k_adam) restated: torch.optim.Adam's
+        device update in the tensors' dtype (its fused multiply-adds as one
+        rounding each), bias corrections in double
+        (from the host int ``step``, or the already incremented count in a
+        0-d tensor: the capturable form), elements with live == 0 untouched."""
+        st = float(step) if isinstance(step, torch.Tensor) else float(int(step))
+        bc1 = 1.0 - beta1 ** st
+        bc2 = 1.0 - beta2 ** st
+        dt = p.dtype
+
+        def sc(x):   # a double scalar rounded once to the tensors' dtype
+            return torch.tensor(x, dtype=torch.float64).to(dt)
+
+        def fma(a, b, c):   # a*b + c rounded once (exact product in float64)
+            return (a.double() * b.double() + c.double()).to(dt)
+
+        gi = g if weight_decay == 0.0 else fma(sc(weight_decay), p, g)
+        mi = fma(sc(1.0 - beta1), gi - m, m)
+        vi = fma(sc(1.0 - beta2), gi * gi, v * sc(beta2))
+        pi = fma(sc(-(lr / bc1)), mi / (torch.sqrt(vi) / sc(math.sqrt(bc2)) + sc(eps)), p)
+        if live is not None:
+            keep = live.reshape(p.shape) != 0
+            mi, vi, pi = (torch.where(keep, a, b) for a, b in ((mi, m), (vi, v), (pi, p)))
+        m.copy_(mi)
+        v.copy_(vi)
+        p.copy_(pi)
+
     # ------------------------------------------------------------ misc
     def noise_uniform(self, seed, E):
         from noise_ref import uniform_numpy

@@ -27,7 +27,7 @@ from test_gpu_parity import check, ours_step  # noqa: E402
 FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "g16_oracle.npz")
 
 
-@pytest.fixture(params=["mfma", "mfma32"])
+@pytest.fixture(params=["mfma", "mfma32", "bf16x6"])
 def path(request):
     import pfsgnn
     prev = pfsgnn.get_edge_path()
@@ -42,7 +42,7 @@ def test_bench_geometry_training_step_matches_oracle(path):
     G, NF, NC, B = (int(z[k]) for k in ("G", "NF", "NC", "B"))
     grid = native.edge_grid(G, NF, NC)
     assert (G, NF, NC, B) == (16, 2394, 128, 8)
-    if path == "mfma":
+    if path in ("mfma", "bf16x6"):
         assert grid["KS"] == 5 and grid["nblocks"] == 3040, grid
     model, graph = make_problem(G, NF, NC, B=B, seed=int(z["model_seed"]))
     gnn, out, loss = ours_step(model, graph, G, NF, NC, B, int(z["noise_seed"]), float(z["sharp"]))

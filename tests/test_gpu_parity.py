@@ -3,8 +3,10 @@
 Every test runs on each fp32-class implementation of the per-edge kernels
 (pfsgnn.set_edge_path): "mfma" (the default: matrix cores, exact fp32 forward
 products, split-bf16 gradient chains and weight gradients), "mfma32" (every
-layer product exact fp32) and "valu" (fp32 fmaf chains).  PFSGNN_PARITY_PATHS
-selects others (bf16x6: passes with PFSGNN_X3_MASK=1).
+layer product exact fp32), "valu" (fp32 fmaf chains) and "bf16x6" (BASELINE
+configs[4]: the forward contractions and their backward recompute on bf16
+MFMAs with three-way split operands, gradient chains as "mfma").
+PFSGNN_PARITY_PATHS selects others (e.g. bf16x3 with PFSGNN_TOL_REPORT=1).
 
 Tolerance vs the float64 oracle: for every compared tensor,
     max|ours - oracle64| <= max(TOL_K * max|oracle32 - oracle64|, TOL_REL[mode] * max|oracle64|)
@@ -39,7 +41,7 @@ REPORT = os.environ.get("PFSGNN_TOL_REPORT") == "1"   # print error ratios, neve
 
 # PFSGNN_PARITY_PATHS=a,b: run the parity cases on other edge paths (with
 # PFSGNN_TOL_REPORT=1, to measure a path that is not held to the bar)
-PATHS = os.environ.get("PFSGNN_PARITY_PATHS", "mfma,mfma32,valu").split(",")
+PATHS = os.environ.get("PFSGNN_PARITY_PATHS", "mfma,mfma32,valu,bf16x6").split(",")
 
 
 @pytest.fixture(params=PATHS, autouse=True)
@@ -110,7 +112,10 @@ def ours_step(model, graph, G, NF, NC, B, seed, sharp, normed=True):
     (1, 40, 12, 2, 12.0, True), (2, 24, 16, 2, 5.0, True), (1, 16, 128, 1, 20.0, True),
     (3, 10, 7, 3, 0.0, True),
     # GNN(normed=False): every norm is the identity (gnn.py:84/121/173/206)
-    (2, 24, 16, 2, 5.0, False), (1, 70, 16, 3, 10.0, False)])
+    (2, 24, 16, 2, 5.0, False), (1, 70, 16, 3, 10.0, False),
+    # train.py's own workload: one graph of 2000 fibers x 12 classes, B = 3
+    # (config.py:16-17, train.py:94-104)
+    (1, 2000, 12, 3, 10.0, True)])
 def test_gnn_training_step_matches_oracle(G, NF, NC, B, sharp, normed):
     model, graph = make_problem(G, NF, NC, B=B, seed=G + NF + NC, normed=normed)
     seed = 777 + NC

@@ -195,6 +195,76 @@ def test_sparse_gnn_other_fdim(F, sliced):
     test_sparse_gnn_matches_oracle(2, 40, 12, 0.4, 2, 3, True, sliced, F=F)
 
 
+@pytest.fixture
+def edge_path():
+    """Set an edge path for one test, restore the previous one after it."""
+    import pfsgnn
+    prev = pfsgnn.get_edge_path()
+    yield pfsgnn.set_edge_path
+    pfsgnn.set_edge_path(prev)
+
+
+@pytest.mark.parametrize("case", [(1, 40, 12, 0.5, 2, 3, True), (2, 24, 16, 0.3, 2, 0, True)])
+def test_sparse_gnn_bf16x6_path(case, sliced, edge_path):
+    """BASELINE configs[4]'s path on general graphs: the sliced kernels at PREC 4
+    (bf16x6 forward + recompute, bf16x3 chains: the default path's bar)."""
+    edge_path("bf16x6")
+    test_sparse_gnn_matches_oracle(*case, sliced)
+
+
+def test_sparse_gnn_bf16_state_paths_fall_back_to_composed(edge_path, monkeypatch):
+    """the bf16 edge-state paths have no sliced kernels
+    (pfsgnn_sliced_max_nc = 0), so a general batch takes the composed ops
+    (exact fp32 here) instead of failing in check_sliced."""
+    from pfsgnn import gnn as gmod
+    monkeypatch.setenv("PFSGNN_SLICED", "1")
+    gmod._LAYOUT_CACHE.clear()
+    model, graph, gen = sparse_problem(2, 24, 16, 0.4, B=2, seed=26, dup=2)
+    w = _weights(graph, 2, 24, 16, gen)
+    gnn, out = _ours(model, graph, w, 2)        # default path: sliced
+    assert all(e[3].sp.sl is not None for e in gmod._LAYOUT_CACHE.d.values())
+    for path in ("bf16", "bf16y"):
+        edge_path(path)
+        assert _hb().sliced_max_nc(10) == 0
+        assert not gmod.sliced_ok(16, 10)
+        gmod._LAYOUT_CACHE.clear()
+        test_sparse_gnn_matches_oracle(2, 24, 16, 0.4, 2, 2, True, False)
+    gmod._LAYOUT_CACHE.clear()
+
+
+def test_sliced_class_limit_at_fdim16(edge_path, monkeypatch):
+    """at Fdim 16 the sliced edge_mlp_bwd's LDS (static + class
+    tables) caps the classes per graph below 128.  At the limit the batch runs
+    sliced, one class above it the composed ops -- both at the oracle bar."""
+    from pfsgnn import gnn as gmod
+    edge_path("mfma")
+    monkeypatch.setenv("PFSGNN_SLICED", "1")
+    lim = _hb().sliced_max_nc(16)
+    assert 64 <= lim < 128, lim
+    assert _hb().sliced_max_nc(10) == 128 and _hb().sliced_max_nc(8) == 128
+    for NC, want in ((lim, True), (lim + 1, False)):
+        gmod._LAYOUT_CACHE.clear()
+        model, graph, gen = sparse_problem(1, 20, NC, 0.5, F=16, B=1, seed=NC, dup=3)
+        w = _weights(graph, 1, 20, NC, gen, F=16)
+        m64, o64 = _oracle(model, graph, w, torch.float64)
+        r32 = [_oracle(model, graph, w, torch.float32, reverse=rv) for rv in (False, True)]
+        gnn, out = _ours(model, graph, w, 1, F=16)
+        lays = [e[3] for e in gmod._LAYOUT_CACHE.d.values()]
+        assert lays and all((lay.sp.sl is not None) == want for lay in lays), (NC, want)
+        for nm in ("x_e", "x_s", "x_t", "x_u"):
+            check(f"{nm} NC={NC}", getattr(out, nm), getattr(o64, nm),
+                  [getattr(r[1], nm) for r in r32], TOL_REL[want])
+        p64 = dict(m64.named_parameters())
+        p32 = [dict(r[0].named_parameters()) for r in r32]
+        for name, p in gnn.named_parameters():
+            z = torch.zeros_like(p64[name])
+            check(f"grad {name} NC={NC}", p.grad,
+                  p64[name].grad if p64[name].grad is not None else z,
+                  [q[name].grad if q[name].grad is not None else z.float() for q in p32],
+                  TOL_REL[want])
+    gmod._LAYOUT_CACHE.clear()
+
+
 def sliced_plan_ref(fib_ptr, src_p, tgt_p, user_of, G, NF, NC):
     """The sliced layout (include/pfsgnn.h pfsgnn_sliced_t) restated in torch:
     each graph's fibers by degree (descending, stable), slices of 16, the k-th
