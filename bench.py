@@ -36,8 +36,10 @@ NF, NC, FDIM = 2394, 128, 10      # overridden by --fibers / --classes
 PRECISION = {
     "mfma": "fp32 MFMA forward contractions and recompute; backward gradient chains and weight "
             "gradients bf16x3 (~2^-16 relative per product); fp32 accumulation and edge state",
-    "mfma32": "every per-edge contraction exact fp32 MFMA; weight gradients bf16x3",
-    "valu": "fp32 fmaf chains on the vector ALU; weight gradients bf16x3 MFMA",
+    "mfma32": "every per-edge contraction exact fp32 MFMA (v_mfma_f32_16x16x4_f32), the weight "
+              "gradients' outer products included; fp32 accumulation and edge state",
+    "valu": "fp32 fmaf chains on the vector ALU; weight gradients exact fp32 MFMA "
+            "(v_mfma_f32_16x16x4_f32)",
     "bf16y": "mfma32 arithmetic with the edge state rounded to bf16",
     "bf16m": "every per-edge contraction a single bf16 MFMA, fp32 accumulation and edge state",
     "bf16": "single-bf16 MFMA contractions and bf16 edge state",

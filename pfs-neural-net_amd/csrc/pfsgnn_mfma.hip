@@ -472,12 +472,13 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
                                                      const uint8_t* __restrict__ tmask) {
   constexpr int C = 2 * F, NT = GM<C>::NT;
   constexpr int NIMG = NT + 1;  // g_z tiles | x
+  using WI = WgImg<PREC>;       // weight-gradient images: bf16x3, or exact fp32 at PREC 0
   MF_GEO
-  __shared__ short imgs[4 * NIMG * 2 * IMG_SHORTS];
+  __shared__ __attribute__((aligned(16))) short imgs[4 * NIMG * WI::U];
   __shared__ float scratch[4 * C * F];
   __shared__ __attribute__((aligned(16))) float ghl[MF_MAX_CPS * ClassRows<C>::CP];
   ClassRows<C>::stage(ghl, ghS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
-  short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
+  short* img = imgs + wave * NIMG * WI::U;
   // the pre-activation z = Rs[f] + Wt1[:, F:2F] x is recomputed, or (TM) only
   // its LeakyReLU mask is read back from target_fwd
   FwdLayer<FP(PREC), C, F> L1;
@@ -532,13 +533,13 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
     }
     lds_order();
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) img_put2(img + tt * 2 * IMG_SHORTS, lane, sgz[tt]);
-    img_put2(img + NT * 2 * IMG_SHORTS, lane, split(x[0]));
+    for (int tt = 0; tt < NT; ++tt) WI::put(img + tt * WI::U, lane, gz[tt], sgz[tt]);
+    WI::put(img + NT * WI::U, lane, x[0], split(x[0]));
     lds_order();
-    const WgB tx = img_trB(img + NT * 2 * IMG_SHORTS, lane);
+    const typename WI::TB tx = WI::B(img + NT * WI::U, lane);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt)
-      accW[tt] = mma3g(img_trA(img + tt * 2 * IMG_SHORTS, lane), tx, accW[tt]);
+      accW[tt] = WI::mma(WI::A(img + tt * WI::U, lane), tx, accW[tt]);
   });
   if (fvalid) {
 #pragma unroll
@@ -574,19 +575,20 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   constexpr int C = 2 * F, NT = GM<C>::NT;
   constexpr int NIMG = 3 * NT + 1;          // g_m | a | g_zs | x
   constexpr int SCR = C * (C + 1) > C * F ? C * (C + 1) : C * F;
+  using WI = WgImg<PREC>;
   MF_GEO
-  __shared__ short imgs[4 * NIMG * 2 * IMG_SHORTS];
+  __shared__ __attribute__((aligned(16))) short imgs[4 * NIMG * WI::U];
   __shared__ float colbuf[COL_CH * 4 * C];
   __shared__ float scratch[4 * SCR];
   __shared__ __attribute__((aligned(16))) float qtl[MF_MAX_CPS * ClassRows<C>::CP];
   __shared__ __attribute__((aligned(16))) float ghl[MF_MAX_CPS * ClassRows<C>::CP];
   ClassRows<C>::stage(qtl, QtS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
   if (ghS) ClassRows<C>::stage(ghl, ghS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
-  short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
+  short* img = imgs + wave * NIMG * WI::U;
   short* im_gm = img;
-  short* im_a = img + NT * 2 * IMG_SHORTS;
-  short* im_gz = im_a + NT * 2 * IMG_SHORTS;
-  short* im_x = im_gz + NT * 2 * IMG_SHORTS;
+  short* im_a = img + NT * WI::U;
+  short* im_gz = im_a + NT * WI::U;
+  short* im_x = im_gz + NT * WI::U;
   const long long CNS = (long long)C * NS;
   const bool tpart = Rs != nullptr;
 
@@ -685,11 +687,11 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     lds_order();
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      img_put2(im_gm + tt * 2 * IMG_SHORTS, lane, sgm[tt]);
-      img_put2(im_a + tt * 2 * IMG_SHORTS, lane, split(as[tt]));
-      img_put2(im_gz + tt * 2 * IMG_SHORTS, lane, sgz[tt]);
+      WI::put(im_gm + tt * WI::U, lane, gm[tt], sgm[tt]);
+      WI::put(im_a + tt * WI::U, lane, as[tt], split(as[tt]));
+      WI::put(im_gz + tt * WI::U, lane, gz[tt], sgz[tt]);
     }
-    img_put2(im_x, lane, split(x[0]));
+    WI::put(im_x, lane, x[0], split(x[0]));
     lds_order();
     floatx4 g[1] = {zero4()};
     if constexpr (PREC >= 1) L1sT.apply(sgz, g); else L1sT.apply(gz, g);
@@ -730,20 +732,20 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     }
     // ---- weight gradients (edge = K) through the transposed images
     lds_order();
-    const WgB tx = img_trB(im_x, lane);
-    WgB ta[NT];
+    const typename WI::TB tx = WI::B(im_x, lane);
+    typename WI::TB ta[NT];
 #pragma unroll
-    for (int nb = 0; nb < NT; ++nb) ta[nb] = img_trB(im_a + nb * 2 * IMG_SHORTS, lane);
+    for (int nb = 0; nb < NT; ++nb) ta[nb] = WI::B(im_a + nb * WI::U, lane);
     const int cl = c - cbase;
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      const s16x8 tgm = img_trA(im_gm + tt * 2 * IMG_SHORTS, lane);
+      const typename WI::TA tgm = WI::A(im_gm + tt * WI::U, lane);
 #pragma unroll
-      for (int nb = 0; nb < NT; ++nb) accW2[tt * NT + nb] = mma3g(tgm, ta[nb], accW2[tt * NT + nb]);
-      const s16x8 tgz = img_trA(im_gz + tt * 2 * IMG_SHORTS, lane);
-      accW1[tt] = mma3g(tgz, tx, accW1[tt]);
-      const floatx4 cs = mf8(tgz, ones8(), zero4());
-      if (j16 == 0) {
+      for (int nb = 0; nb < NT; ++nb) accW2[tt * NT + nb] = WI::mma(tgm, ta[nb], accW2[tt * NT + nb]);
+      const typename WI::TA tgz = WI::A(im_gz + tt * WI::U, lane);
+      accW1[tt] = WI::mma(tgz, tx, accW1[tt]);
+      const floatx4 cs = WI::colsum(tgz, gz[tt]);
+      if (j16 == WI::CS_LANE) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int h = GM<C>::mrow(tt, 4 * g4 + r);
@@ -815,17 +817,18 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
   constexpr int H = 4 * F, NT = GM<H>::NT;
   constexpr int NIMG = 1 + NT + NT + 1;          // g_y | a | g_z | x
   constexpr int SCR = F * (H + 1) > H * F ? F * (H + 1) : H * F;
+  using WI = WgImg<PREC>;
   MF_GEO
-  __shared__ short imgs[4 * NIMG * 2 * IMG_SHORTS];
+  __shared__ __attribute__((aligned(16))) short imgs[4 * NIMG * WI::U];
   __shared__ float colbuf[COL_CH * 4 * H];
   __shared__ float scratch[4 * SCR];
   __shared__ __attribute__((aligned(16))) float ptl[MF_MAX_CPS * ClassRows<H>::CP];
   ClassRows<H>::stage(ptl, PtS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
-  short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
+  short* img = imgs + wave * NIMG * WI::U;
   short* im_gy = img;
-  short* im_a = img + 2 * IMG_SHORTS;
-  short* im_gz = im_a + NT * 2 * IMG_SHORTS;
-  short* im_x = im_gz + NT * 2 * IMG_SHORTS;
+  short* im_a = img + WI::U;
+  short* im_gz = im_a + NT * WI::U;
+  short* im_x = im_gz + NT * WI::U;
 
   FwdLayer<FP(PREC), H, F> L1;
   L1.load([&](int h, int k) { return W1[h * 4 * F + 2 * F + k]; }, lane);
@@ -887,31 +890,31 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
     // the weight-gradient images are written first: their LDS latency hides
     // behind the edge-input gradient chain below
     lds_order();
-    img_put2(im_gy, lane, sgy[0]);
+    WI::put(im_gy, lane, gy[0], sgy[0]);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      img_put2(im_a + tt * 2 * IMG_SHORTS, lane, split(a[tt]));
-      img_put2(im_gz + tt * 2 * IMG_SHORTS, lane, sgz[tt]);
+      WI::put(im_a + tt * WI::U, lane, a[tt], split(a[tt]));
+      WI::put(im_gz + tt * WI::U, lane, gz[tt], sgz[tt]);
     }
-    img_put2(im_x, lane, split(x[0]));
+    WI::put(im_x, lane, x[0], split(x[0]));
     lds_order();
     if (gxe) {
       floatx4 gx[1] = {zero4()};
       if constexpr (PREC >= 1) L1T.apply(sgz, gx); else L1T.apply(gz, gx);
       st_frows<F>(gxe, (uint32_t)c * eoc, ro, g4, fvalid, gx[0]);
     }
-    const s16x8 tgy = img_trA(im_gy, lane);
+    const typename WI::TA tgy = WI::A(im_gy, lane);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt)
-      accW2[tt] = mma3g(tgy, img_trB(im_a + tt * 2 * IMG_SHORTS, lane), accW2[tt]);
-    const WgB tx = img_trB(im_x, lane);
+      accW2[tt] = WI::mma(tgy, WI::B(im_a + tt * WI::U, lane), accW2[tt]);
+    const typename WI::TB tx = WI::B(im_x, lane);
     const int cl = c - cbase;
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      const s16x8 tgz = img_trA(im_gz + tt * 2 * IMG_SHORTS, lane);
-      accW1[tt] = mma3g(tgz, tx, accW1[tt]);
-      const floatx4 cs = mf8(tgz, ones8(), zero4());
-      if (j16 == 0) {
+      const typename WI::TA tgz = WI::A(im_gz + tt * WI::U, lane);
+      accW1[tt] = WI::mma(tgz, tx, accW1[tt]);
+      const floatx4 cs = WI::colsum(tgz, gz[tt]);
+      if (j16 == WI::CS_LANE) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int h = GM<H>::mrow(tt, 4 * g4 + r);

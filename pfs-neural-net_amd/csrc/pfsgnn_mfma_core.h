@@ -449,6 +449,76 @@ __device__ __forceinline__ WgB img_trB(const short* img, int lane) {
 // (one wave's LDS operations execute in order)
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 
+// ------------------------------------------------------------ fp32 weight gradients
+// The exact-fp32 form of the weight-gradient outer products (PREC 0: the
+// "mfma32" edge path): a wave-private fp32 image [16 slots][IMGF_STRIDE] of a
+// tile, edge e of slot i at i * IMGF_STRIDE + 4 (e & 3) + (e >> 2), so that one
+// ds_read_b128 hands lane (g, i) slot i of edges g, g + 4, g + 8, g + 12 --
+// the A[i][k = g] / B[k = g][j = i] operands of the four
+// v_mfma_f32_16x16x4_f32 K-steps over the tile's 16 edges (exact fp32
+// products, fp32 accumulation).  Stride 20: conflict-free b128 reads, 2-way
+// b32 writes.
+#define IMGF_STRIDE 20
+#define IMGF_FLOATS (16 * IMGF_STRIDE)
+__device__ __forceinline__ void imgf_put(float* img, int lane, const floatx4& v) {
+  const int g = lane >> 4, j = lane & 15;
+  const int c = 4 * (j & 3) + (j >> 2);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) img[(4 * g + r) * IMGF_STRIDE + c] = v[r];
+}
+__device__ __forceinline__ floatx4 imgf_tr(const float* img, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  return *reinterpret_cast<const floatx4*>(img + i * IMGF_STRIDE + 4 * g);
+}
+__device__ __forceinline__ floatx4 mmaf(const floatx4& a, const floatx4& b, floatx4 c) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], c, 0, 0, 0);
+  return c;
+}
+
+// The weight-gradient images of a backward kernel by precision: bf16x3 (the
+// hi / lo planes, mma3g; every path but PREC 0) or exact fp32 (PREC 0).
+// U: shorts per image; put() takes the tile both as fp32 and as its split;
+// A() / B(): the operands of mma(); colsum(): per-slot sums of a tile over its
+// 16 edges (bf16x3: the A tuple against ones; fp32: DPP row sums in fp32),
+// valid in lane CS_LANE of each lane group.
+template <int PREC>
+struct WgImg {
+  static constexpr int U = 2 * IMG_SHORTS;
+  static constexpr int CS_LANE = 0;
+  using TA = s16x8;
+  using TB = WgB;
+  static __device__ __forceinline__ void put(short* im, int lane, const floatx4&, const Fr& s) {
+    img_put2(im, lane, s);
+  }
+  static __device__ __forceinline__ TA A(const short* im, int lane) { return img_trA(im, lane); }
+  static __device__ __forceinline__ TB B(const short* im, int lane) { return img_trB(im, lane); }
+  static __device__ __forceinline__ floatx4 mma(const TA& a, const TB& b, floatx4 c) {
+    return mma3g(a, b, c);
+  }
+  static __device__ __forceinline__ floatx4 colsum(const TA& a, const floatx4&) {
+    return mf8(a, ones8(), zero4());
+  }
+};
+template <>
+struct WgImg<0> {
+  static constexpr int U = 2 * IMGF_FLOATS;
+  static constexpr int CS_LANE = 15;
+  using TA = floatx4;
+  using TB = floatx4;
+  static __device__ __forceinline__ void put(short* im, int lane, const floatx4& v, const Fr&) {
+    imgf_put(reinterpret_cast<float*>(im), lane, v);
+  }
+  static __device__ __forceinline__ TA A(const short* im, int lane) {
+    return imgf_tr(reinterpret_cast<const float*>(im), lane);
+  }
+  static __device__ __forceinline__ TB B(const short* im, int lane) { return A(im, lane); }
+  static __device__ __forceinline__ floatx4 mma(const TA& a, const TB& b, floatx4 c) {
+    return mmaf(a, b, c);
+  }
+  static __device__ __forceinline__ floatx4 colsum(const TA&, const floatx4& v);
+};
+
 // ------------------------------------------------------------ memory
 __device__ __forceinline__ float ldE(const float* p, uint32_t off) {
   return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(p) + off);
@@ -481,8 +551,12 @@ struct RowOff {
 // arithmetic per row (an access past `bytes` reads 0).  Stores: the SGPR-base
 // global form, (char*)p + c*eoc plus the 32-bit lane offset, which goes
 // through an empty asm so that hipcc keeps it 32-bit at the access rather than
-// hoisting a 64-bit copy.  (buffer_store with exec-masked rows was miscompiled
-// here: one row's value stored to all three rows; DESIGN.md §MFMA edge path.)
+// hoisting a 64-bit copy.  (Round 3's buffer-store form stored one row's value
+// to all of a lane's rows.  The cause is a hipcc defect in
+// __builtin_bit_cast(unsigned int, v[r]) of a vector ELEMENT -- it reads
+// element 0 for every r -- not the buffer stores: bit-cast a float copy of
+// the element instead.  tests/test_bitcast_vector_element.py,
+// tests/test_gpu_buffer_store.py; DESIGN.md §Edge-row stores.)
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 __device__ __forceinline__ Rsrc rsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes,
@@ -600,6 +674,13 @@ __device__ __forceinline__ float row_sum16(float v) {
   v += dpp0<0x114>(v);
   v += dpp0<0x118>(v);
   return v;
+}
+// exact fp32 per-slot sums of a tile over its 16 edges (lane 15 of each group)
+__device__ __forceinline__ floatx4 WgImg<0>::colsum(const TA&, const floatx4& v) {
+  floatx4 s;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) s[r] = row_sum16(v[r]);
+  return s;
 }
 
 // Per-class column partials of the block, chunked: each wave parks its 16-fiber

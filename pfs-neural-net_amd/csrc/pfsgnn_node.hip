@@ -1989,7 +1989,13 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
   const float vi = fmaf(k.omb2, __fmul_rn(gi, gi), vb);    // .addcmul_(g, g, 1-beta2)
   m[i] = mi;
   v[i] = vi;
-  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vi), bc2_sqrt), k.eps);  // sqrt(v)/sqrt(bc2) + eps
+  // sqrt(v)/sqrt(bc2) + eps.  The square root is taken in double and rounded
+  // once: correctly rounded (53 >= 2*24 + 2), as torch's is, where the fp32
+  // hardware square root (v_sqrt_f32, which __fsqrt_rn lowers to here) is
+  // 1-ulp accurate and changed 2 of 10000 updates of a checkpoint resume by
+  // one ulp (tests/test_gpu_adam_resume.py)
+  const float sq = (float)sqrt((double)vi);
+  const float denom = __fadd_rn(__fdiv_rn(sq, bc2_sqrt), k.eps);
   p[i] = fmaf(neg_step, __fdiv_rn(mi, denom), p[i]);       // addcdiv_(m, denom, -lr/bc1)
 }
 

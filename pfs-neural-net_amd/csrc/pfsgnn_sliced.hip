@@ -518,11 +518,12 @@ __global__ __launch_bounds__(256) void ksl_target_bwd(
     float* __restrict__ partW, const uint8_t* __restrict__ tmask) {
   constexpr int C = 2 * F, NT = GM<C>::NT;
   constexpr int NIMG = NT + 1;  // g_z tiles | x
+  using WI = WgImg<PREC>;       // weight-gradient images: bf16x3, or exact fp32 at PREC 0
   SL_GEO
-  __shared__ short imgs[4 * NIMG * 2 * IMG_SHORTS];
+  __shared__ __attribute__((aligned(16))) short imgs[4 * NIMG * WI::U];
   __shared__ float scratch[4 * C * F];
   CROWS_DECL(C, ghl, ghS, sl_dyn)   // [NC][CP]
-  short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
+  short* img = imgs + wave * NIMG * WI::U;
   FwdLayer<FP(PREC), C, F> L1;
   if constexpr (!TM) L1.load([&](int h, int k) { return Wt1[h * 2 * F + F + k]; }, lane);
   GradLayer<PREC, F, C> LT;
@@ -576,13 +577,13 @@ __global__ __launch_bounds__(256) void ksl_target_bwd(
     }
     lds_order();
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) img_put2(img + tt * 2 * IMG_SHORTS, lane, sgz[tt]);
-    img_put2(img + NT * 2 * IMG_SHORTS, lane, split(x[0]));
+    for (int tt = 0; tt < NT; ++tt) WI::put(img + tt * WI::U, lane, gz[tt], sgz[tt]);
+    WI::put(img + NT * WI::U, lane, x[0], split(x[0]));
     lds_order();
-    const WgB tx = img_trB(img + NT * 2 * IMG_SHORTS, lane);
+    const typename WI::TB tx = WI::B(img + NT * WI::U, lane);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt)
-      accW[tt] = mma3g(img_trA(img + tt * 2 * IMG_SHORTS, lane), tx, accW[tt]);
+      accW[tt] = WI::mma(WI::A(img + tt * WI::U, lane), tx, accW[tt]);
   });
   if (fvalid) {
 #pragma unroll
@@ -617,8 +618,9 @@ __global__ __launch_bounds__(256, 2) void ksl_source_bwd(
   constexpr int C = 2 * F, NT = GM<C>::NT;
   constexpr int NIMG = 3 * NT + 1;          // g_m | a | g_zs | x
   constexpr int SCR = C * (C + 1) > C * F ? C * (C + 1) : C * F;
+  using WI = WgImg<PREC>;
   SL_GEO
-  __shared__ short imgs[4 * NIMG * 2 * IMG_SHORTS];
+  __shared__ __attribute__((aligned(16))) short imgs[4 * NIMG * WI::U];
   __shared__ float scratch[4 * SCR];
   // QtS / ghS: the class tables in k_sl_rows_table's layout [G*NC][CP]
   float* acc = sl_dyn;                  // [4][NC][C + 1]
@@ -627,11 +629,11 @@ __global__ __launch_bounds__(256, 2) void ksl_source_bwd(
   float* wacc = acc + wave * NC * Acc<C>::S;
   __shared__ int owners[4][pfm::SL_MAX_NC];
   int* own = owners[wave];
-  short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
+  short* img = imgs + wave * NIMG * WI::U;
   short* im_gm = img;
-  short* im_a = img + NT * 2 * IMG_SHORTS;
-  short* im_gz = im_a + NT * 2 * IMG_SHORTS;
-  short* im_x = im_gz + NT * 2 * IMG_SHORTS;
+  short* im_a = img + NT * WI::U;
+  short* im_gz = im_a + NT * WI::U;
+  short* im_x = im_gz + NT * WI::U;
   const long long CNS = (long long)C * NS;
   const bool tpart = Rs != nullptr;
 
@@ -725,11 +727,11 @@ __global__ __launch_bounds__(256, 2) void ksl_source_bwd(
     lds_order();
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      img_put2(im_gm + tt * 2 * IMG_SHORTS, lane, sgm[tt]);
-      img_put2(im_a + tt * 2 * IMG_SHORTS, lane, split(as[tt]));
-      img_put2(im_gz + tt * 2 * IMG_SHORTS, lane, sgz[tt]);
+      WI::put(im_gm + tt * WI::U, lane, gm[tt], sgm[tt]);
+      WI::put(im_a + tt * WI::U, lane, as[tt], split(as[tt]));
+      WI::put(im_gz + tt * WI::U, lane, gz[tt], sgz[tt]);
     }
-    img_put2(im_x, lane, split(x[0]));
+    WI::put(im_x, lane, x[0], split(x[0]));
     lds_order();
     floatx4 g[1] = {zero4()};
     if constexpr (PREC >= 1) L1sT.apply(sgz, g); else L1sT.apply(gz, g);
@@ -772,16 +774,16 @@ __global__ __launch_bounds__(256, 2) void ksl_source_bwd(
     acc_add<C>(wacc, own, cl, ev, g4, j16, gz);
     // weight gradients (edge = K) through the transposed images
     lds_order();
-    const WgB tx = img_trB(im_x, lane);
-    WgB ta[NT];
+    const typename WI::TB tx = WI::B(im_x, lane);
+    typename WI::TB ta[NT];
 #pragma unroll
-    for (int nb = 0; nb < NT; ++nb) ta[nb] = img_trB(im_a + nb * 2 * IMG_SHORTS, lane);
+    for (int nb = 0; nb < NT; ++nb) ta[nb] = WI::B(im_a + nb * WI::U, lane);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      const s16x8 tgm = img_trA(im_gm + tt * 2 * IMG_SHORTS, lane);
+      const typename WI::TA tgm = WI::A(im_gm + tt * WI::U, lane);
 #pragma unroll
-      for (int nb = 0; nb < NT; ++nb) accW2[tt * NT + nb] = mma3g(tgm, ta[nb], accW2[tt * NT + nb]);
-      accW1[tt] = mma3g(img_trA(im_gz + tt * 2 * IMG_SHORTS, lane), tx, accW1[tt]);
+      for (int nb = 0; nb < NT; ++nb) accW2[tt * NT + nb] = WI::mma(tgm, ta[nb], accW2[tt * NT + nb]);
+      accW1[tt] = WI::mma(WI::A(im_gz + tt * WI::U, lane), tx, accW1[tt]);
     }
   });
   acc_flush<C>(acc, NC, partCol, colbase);
@@ -838,8 +840,9 @@ __global__ __launch_bounds__(256, 2) void ksl_edge_mlp_bwd(
   constexpr int H = 4 * F, NT = GM<H>::NT;
   constexpr int NIMG = 1 + NT + NT + 1;          // g_y | a | g_z | x
   constexpr int SCR = F * (H + 1) > H * F ? F * (H + 1) : H * F;
+  using WI = WgImg<PREC>;
   SL_GEO
-  __shared__ short imgs[4 * NIMG * 2 * IMG_SHORTS];
+  __shared__ __attribute__((aligned(16))) short imgs[4 * NIMG * WI::U];
   __shared__ float scratch[4 * SCR];
   CROWS_DECL(H, ptl, PtS, sl_dyn)             // [NC][CP]
   float* acc = sl_dyn + NC * CROWS_FLOATS(H);  // [4][NC][H + 1]
@@ -847,11 +850,11 @@ __global__ __launch_bounds__(256, 2) void ksl_edge_mlp_bwd(
   float* wacc = acc + wave * NC * Acc<H>::S;
   __shared__ int owners[4][pfm::SL_MAX_NC];
   int* own = owners[wave];
-  short* img = imgs + wave * NIMG * 2 * IMG_SHORTS;
+  short* img = imgs + wave * NIMG * WI::U;
   short* im_gy = img;
-  short* im_a = img + 2 * IMG_SHORTS;
-  short* im_gz = im_a + NT * 2 * IMG_SHORTS;
-  short* im_x = im_gz + NT * 2 * IMG_SHORTS;
+  short* im_a = img + WI::U;
+  short* im_gz = im_a + NT * WI::U;
+  short* im_x = im_gz + NT * WI::U;
 
   FwdLayer<FP(PREC), H, F> L1;
   L1.load([&](int h, int k) { return W1[h * 4 * F + 2 * F + k]; }, lane);
@@ -911,13 +914,13 @@ __global__ __launch_bounds__(256, 2) void ksl_edge_mlp_bwd(
       sgz[tt] = split(gz[tt]);
     }
     lds_order();
-    img_put2(im_gy, lane, sgy[0]);
+    WI::put(im_gy, lane, gy[0], sgy[0]);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      img_put2(im_a + tt * 2 * IMG_SHORTS, lane, split(a[tt]));
-      img_put2(im_gz + tt * 2 * IMG_SHORTS, lane, sgz[tt]);
+      WI::put(im_a + tt * WI::U, lane, a[tt], split(a[tt]));
+      WI::put(im_gz + tt * WI::U, lane, gz[tt], sgz[tt]);
     }
-    img_put2(im_x, lane, split(x[0]));
+    WI::put(im_x, lane, x[0], split(x[0]));
     lds_order();
     if (gxe) {
       floatx4 gx[1] = {zero4()};
@@ -925,14 +928,14 @@ __global__ __launch_bounds__(256, 2) void ksl_edge_mlp_bwd(
       st_frows<F>(gxe, (uint32_t)k * eoc, ro, g4, true, gx[0]);
     }
     acc_add<H>(wacc, own, cl, ev, g4, j16, gz);
-    const s16x8 tgy = img_trA(im_gy, lane);
+    const typename WI::TA tgy = WI::A(im_gy, lane);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt)
-      accW2[tt] = mma3g(tgy, img_trB(im_a + tt * 2 * IMG_SHORTS, lane), accW2[tt]);
-    const WgB tx = img_trB(im_x, lane);
+      accW2[tt] = WI::mma(tgy, WI::B(im_a + tt * WI::U, lane), accW2[tt]);
+    const typename WI::TB tx = WI::B(im_x, lane);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt)
-      accW1[tt] = mma3g(img_trA(im_gz + tt * 2 * IMG_SHORTS, lane), tx, accW1[tt]);
+      accW1[tt] = WI::mma(WI::A(im_gz + tt * WI::U, lane), tx, accW1[tt]);
   });
   if (fvalid) {
 #pragma unroll

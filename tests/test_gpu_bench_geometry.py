@@ -48,7 +48,12 @@ def test_bench_geometry_training_step_matches_oracle(path):
     gnn, out, loss = ours_step(model, graph, G, NF, NC, B, int(z["noise_seed"]), float(z["sharp"]))
 
     def ref(k):
-        return torch.as_tensor(z["f64:" + k]), torch.as_tensor(z["f32:" + k])
+        # the fp32 error level from two fp32 orders (as given, reversed) when the
+        # fixture holds both (test_gpu_parity's two-sample bar)
+        r32 = [torch.as_tensor(z["f32:" + k])]
+        if "f32r:" + k in z.files:
+            r32.append(torch.as_tensor(z["f32r:" + k]))
+        return torch.as_tensor(z["f64:" + k]), r32
 
     check("loss", loss.reshape(1), *ref("loss"))
     ixs, ixe = torch.as_tensor(z["ix_s"]), torch.as_tensor(z["ix_e"])
