@@ -118,6 +118,13 @@ __device__ __forceinline__ void bn2_bwd_coef_one(int c, float Sg, float Sgx, con
 struct EdgeGeo {
   int G, NF, NC, NFG, KS, CPS, nblocks;
   long long E, NS, NT;
+  // XCD-aware block order of the MFMA edge kernels (pfsgnn_mfma_core.h
+  // MF_GEO): 0 = blockIdx order; else the launch has 8 * xcdper blocks and
+  // hardware block b (dispatched to XCD b % 8) runs logical block
+  // (b % 8) * xcdper + b / 8, so each XCD works a contiguous range of logical
+  // blocks -- neighbouring 64-fiber groups, whose edge rows share 128-byte
+  // lines, read them through one L2
+  int xcdper = 0;
 };
 
 // Blocks of 4 waves on 64 fibers; KS class splits bring the grid to about

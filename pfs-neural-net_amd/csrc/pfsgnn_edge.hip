@@ -1464,8 +1464,20 @@ EdgeGeo geo_mfma(int G, int NF, int NC) {
   }
   return best;
 }
+// XCD-aware block order for the MFMA edge kernels (EdgeGeo::xcdper);
+// PFSGNN_XCD_ORDER=0 keeps blockIdx order (A/B knob)
+bool xcd_order() {
+  static const bool on = [] {
+    const char* e = getenv("PFSGNN_XCD_ORDER");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
 EdgeGeo geo_for(int G, int NF, int NC) {
-  return use_mfma() ? geo_mfma(G, NF, NC) : make_geo(G, NF, NC);
+  if (!use_mfma()) return make_geo(G, NF, NC);
+  EdgeGeo g = geo_mfma(G, NF, NC);
+  if (xcd_order()) g.xcdper = (g.nblocks + 7) / 8;
+  return g;
 }
 // a sliced general batch (include/pfsgnn.h pfsgnn_sliced_t): its kernel view
 pfm::SlGeo sl_of(const pfsgnn_sliced_t& s) {
