@@ -127,6 +127,15 @@ struct EdgeGeo {
   int xcdper = 0;
 };
 
+// the launch grid of an edge kernel (EdgeGeo::xcdper: rounded to 8 blocks)
+static inline unsigned edge_grid(const EdgeGeo& geo) {
+  return geo.xcdper ? 8u * (unsigned)geo.xcdper : (unsigned)geo.nblocks;
+}
+// the logical block of this hardware block (XCD order), >= nblocks: none
+#define PF_LOGICAL_BLOCK(geo)                                                          \
+  ((geo).xcdper ? (int)(blockIdx.x & 7u) * (geo).xcdper + (int)(blockIdx.x >> 3)       \
+                : (int)blockIdx.x)
+
 // Blocks of 4 waves on 64 fibers; KS class splits bring the grid to about
 // `target` blocks (2048 = 8 blocks of 4 waves per CU on 256 CUs: enough
 // resident waves to hide the scalar-weight and HBM latencies).

@@ -28,7 +28,8 @@
 #define EDGE_PROLOGUE                                                       \
   const int t = threadIdx.x, lane = t & 63;                                 \
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);                  \
-  const int bx = blockIdx.x;                                                \
+  const int bx = PF_LOGICAL_BLOCK(geo);                                     \
+  if (bx >= geo.nblocks) return;                                            \
   const int ks = bx % geo.KS, grp = bx / geo.KS;                            \
   const int fg = grp % geo.NFG, gg = grp / geo.NFG;                         \
   const int f = fg * 64 + lane;                                             \
@@ -1621,7 +1622,7 @@ static int edge_mlp_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, i
   const float* W2T = transposed(W2, F, 4 * F, w, st);
   PF_REQUIRE(part && PtT && W2T, "pfsgnn_edge_mlp_fwd", "workspace too small");
   { pf::Timer tm_("edge_mlp_fwd", st);
-  DISPATCH_F(F, hipLaunchKernelGGL(k_edge_mlp_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
+  DISPATCH_F(F, hipLaunchKernelGGL(k_edge_mlp_fwd<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo,
                                    xe, xsc, xsh, Ps, PtT, W1, W2T, b2, y, part));
   tm_.end(); }
   hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(256), 0, st, part, geo.nblocks, F, geo.E,
@@ -1719,7 +1720,7 @@ static int source_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
   const float* Ws2T = transposed(Ws2, C, C, w, st);
   PF_REQUIRE(partS && QtT && Ws2T, "pfsgnn_source_fwd", "workspace too small");
   { pf::Timer tm_("source_fwd", st);
-  DISPATCH_F(F, hipLaunchKernelGGL(k_source_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
+  DISPATCH_F(F, hipLaunchKernelGGL(k_source_fwd<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo, y,
                                    sc, sh, QtT, Ws1, Ws2T, bs2, partS));
   tm_.end(); }
   }
@@ -1778,7 +1779,7 @@ static int target_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
   } else if (use_mfma()) {
     if (int rc = pfm::target_fwd(geo, F, y, sc, sh, Rs, Wt1, part, tmask, mf_prec(1, F), st)) return rc;
   } else {
-  DISPATCH_F(F, hipLaunchKernelGGL(k_target_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
+  DISPATCH_F(F, hipLaunchKernelGGL(k_target_fwd<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo, y,
                                    sc, sh, Rs, Wt1, part));
   }
   tm_.end(); }
@@ -1840,7 +1841,7 @@ static int target_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
                                  mf_prec(1, F), st))
       return rc;
   } else {
-  DISPATCH_F(F, hipLaunchKernelGGL(k_target_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
+  DISPATCH_F(F, hipLaunchKernelGGL(k_target_bwd<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo, y,
                                    sc, sh, Rs, Wt1, ghT, gz, gxe, part));
   }
   tm_.end(); }
@@ -2055,7 +2056,7 @@ static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
                                  mf_prec(1, F), st))
       return rc;
   } else {
-  DISPATCH_F(F, hipLaunchKernelGGL(k_source_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
+  DISPATCH_F(F, hipLaunchKernelGGL(k_source_bwd<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo, y,
                                    sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT, g_next,
                                    mu1, inv1, g_tot, pW2, pW1, pCol, pBN));
   }
@@ -2106,7 +2107,7 @@ extern "C" int pfsgnn_edge_bn_grad_sums(int G, int NF, int NC, int F, const floa
   PF_REQUIRE(pBN, "pfsgnn_edge_bn_grad_sums", "workspace too small");
   hipStream_t st = as_stream(stream);
   { pf::Timer tm_("edge_bn_sums", st);
-  DISPATCH_F(F, hipLaunchKernelGGL(k_edge_bn_sums<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, g,
+  DISPATCH_F(F, hipLaunchKernelGGL(k_edge_bn_sums<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo, g,
                                    y, mu1, inv1, pBN));
   tm_.end(); }
   {
@@ -2162,7 +2163,7 @@ static int edge_mlp_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, i
   const float* W2T = transposed(W2, F, H, w, st);
   PF_REQUIRE(pW2 && pW1 && pCol && gs && PtT && W2T, "pfsgnn_edge_mlp_bwd", "workspace too small");
   { pf::Timer tm_("edge_mlp_bwd", st);
-  DISPATCH_F(F, hipLaunchKernelGGL(k_edge_mlp_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo,
+  DISPATCH_F(F, hipLaunchKernelGGL(k_edge_mlp_bwd<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo,
                                    g_tot, alpha, gam0, gam1, y, xe, xsc, xsh, Ps, PtT, W1, W2T, gxe,
                                    gs, pW2, pW1, pCol));
   tm_.end(); }

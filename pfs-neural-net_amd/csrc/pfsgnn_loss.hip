@@ -9,7 +9,8 @@
 #define EDGE_PROLOGUE                                                       \
   const int t = threadIdx.x, lane = t & 63;                                 \
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);                  \
-  const int bx = blockIdx.x;                                                \
+  const int bx = PF_LOGICAL_BLOCK(geo);                                     \
+  if (bx >= geo.nblocks) return;                                            \
   const int ks = bx % geo.KS, grp = bx / geo.KS;                            \
   const int fg = grp % geo.NFG, gg = grp / geo.NFG;                         \
   const int f = fg * 64 + lane;                                             \
@@ -531,7 +532,7 @@ extern "C" int pfsgnn_loss_fwd(int G, int NF, int NC, int F, const float* y, con
   const SoftFloor sf = make_softfloor(sharpness);
   const uint64_t key = pf_noise_key((uint64_t)seed);
   { pf::Timer tm_("loss_fwd", st);
-  DISPATCH_F(F, hipLaunchKernelGGL(k_loss_fwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y,
+  DISPATCH_F(F, hipLaunchKernelGGL(k_loss_fwd<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo, y,
                                    sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sf, noiselevel, key, seed_dev,
                                    ftp, tt, part));
   tm_.end(); }
@@ -581,7 +582,7 @@ extern "C" int pfsgnn_loss_bwd(int G, int NF, int NC, int F, const float* y, con
   const SoftFloor sf = make_softfloor(sharpness);
   const uint64_t key = pf_noise_key((uint64_t)seed);
   { pf::Timer tm_("loss_bwd", st);
-  DISPATCH_F(F, hipLaunchKernelGGL(k_loss_bwd<FF>, dim3(geo.nblocks), dim3(256), 0, st, geo, y, sc,
+  DISPATCH_F(F, hipLaunchKernelGGL(k_loss_bwd<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo, y, sc,
                                    sh, Wd1, bd1, Wd2, bd2, ci, scale, sf, noiselevel, key, seed_dev, Gn, Gf,
                                    Gv, tmean, gscale, gxe, pW, pV));
   tm_.end(); }

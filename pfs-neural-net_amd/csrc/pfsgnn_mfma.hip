@@ -965,16 +965,12 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
 }  // namespace
 
 // ============================================================ host launchers
-// the launch grid of an MF_GEO kernel: nblocks, or 8 * xcdper with the XCD order
-static inline unsigned mf_grid(const EdgeGeo& geo) {
-  return geo.xcdper ? 8u * (unsigned)geo.xcdper : (unsigned)geo.nblocks;
-}
 
 // Instantiations: Fdim 8, 10, 16 for the fp32 / bf16x3 precisions (PREC 0, 1);
 // the single-bf16 path (PREC 2, BASELINE configs[4]) at Fdim 10.
 #define MF_CASE(FF, PP, K, ...)                                                   \
   case FF * 8 + PP: {                                                             \
-    hipLaunchKernelGGL((K<FF, PP>), dim3(mf_grid(geo)), dim3(256), 0, st, geo,    \
+    hipLaunchKernelGGL((K<FF, PP>), dim3(edge_grid(geo)), dim3(256), 0, st, geo,    \
                        __VA_ARGS__);                                              \
   } break;
 #define MF_LAUNCH(F, P, K, ...)                                                   \
@@ -990,7 +986,7 @@ static inline unsigned mf_grid(const EdgeGeo& geo) {
 // kernels with a third template flag (TM: the TModel mask is read, not recomputed)
 #define MF_CASE3(FF, PP, TT, K, ...)                                              \
   case FF * 8 + PP: {                                                             \
-    hipLaunchKernelGGL((K<FF, PP, TT>), dim3(mf_grid(geo)), dim3(256), 0, st, geo, \
+    hipLaunchKernelGGL((K<FF, PP, TT>), dim3(edge_grid(geo)), dim3(256), 0, st, geo, \
                        __VA_ARGS__);                                              \
   } break;
 #define MF_LAUNCH3(F, P, TT, K, ...)                                              \

@@ -784,8 +784,7 @@ __device__ __forceinline__ float mask_slope(uint32_t m, int s) {
   const int t = threadIdx.x, lane = t & 63;                                           \
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);                            \
   const int g4 = lane >> 4, j16 = lane & 15;                                          \
-  const int bx = geo.xcdper ? (int)(blockIdx.x & 7u) * geo.xcdper + (int)(blockIdx.x >> 3) \
-                            : (int)blockIdx.x;                                        \
+  const int bx = PF_LOGICAL_BLOCK(geo);                                               \
   if (bx >= geo.nblocks) return; /* (block-uniform: the XCD grid is rounded to 8) */  \
   const int ks = bx % geo.KS, grp = bx / geo.KS;                                      \
   const int fg = grp % geo.NFG, gg = grp / geo.NFG;                                   \
