@@ -92,9 +92,21 @@ int pfsgnn_edge_grid(int G, int NF, int NC, int* info);
 
 /* Per-kernel HIP-event timing of the main edge/loss kernels (diagnostics for
  * bench.py; off by default, must stay off while a stream is captured).
- * Names: edge_mlp_fwd, source_fwd, target_fwd, target_bwd, source_bwd,
- * edge_bn_sums, edge_mlp_bwd, loss_fwd, loss_bwd.  query() synchronises. */
+ * on = 1: events recorded around each launch; on = 2: the same behind a
+ * ~0.1 ms single-wave spin kernel enqueued before the start event, so that
+ * the interval holds the kernel alone and not the host's launch latency of
+ * an eager step (the GPU reaches the start event only once the kernel is
+ * enqueued).  Names: edge_mlp_fwd, source_fwd, target_fwd, target_bwd,
+ * source_bwd, edge_bn_sums, edge_mlp_bwd, loss_fwd, loss_bwd.  query()
+ * synchronises. */
 int pfsgnn_timing_enable(int on);
+/* Launch the named main kernel 1 + extra times back to back (0: once, the
+ * default).  Diagnostics for bench.py's roofline: the kernel only overwrites
+ * its outputs, so a captured step with extra = 1 computes the same results,
+ * and the difference between its replay time and the plain step's, per
+ * launch, is the kernel's duration inside the replayed step.  Supported:
+ * edge_mlp_bwd (complete graphs, MFMA edge paths). */
+int pfsgnn_timing_repeat(const char* name, int extra);
 int pfsgnn_timing_reset(void);
 int pfsgnn_timing_query(const char* name, double* total_ms, long long* count);
 

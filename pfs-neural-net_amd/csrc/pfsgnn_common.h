@@ -29,6 +29,9 @@ void set_error(const std::string& msg);
 int fail(const char* where, const char* what);
 int check_launch(const char* where);
 // brackets one kernel launch with HIP events when pfsgnn_timing_enable(1)
+// extra back-to-back launches of a named main kernel (pfsgnn_timing_repeat;
+// 0 unless bench.py measures that kernel's in-graph duration)
+int repeats(const char* name);
 class Timer {
  public:
   Timer(const char* name, hipStream_t st);

@@ -41,7 +41,7 @@ namespace pf {
 struct TimerRec {
   hipEvent_t a, b;
 };
-static bool g_timing = false;
+static int g_timing = 0;   // 0 off, 1 events around each launch, 2 + a lead-in spin
 static std::map<std::string, std::vector<TimerRec>> g_pending;
 static std::map<std::string, std::pair<double, long long>> g_done;
 static std::vector<hipEvent_t> g_pool;
@@ -57,10 +57,29 @@ static hipEvent_t take_event() {
   return e;
 }
 
+// Mode 2: a ~0.1 ms single-wave spin kernel goes on the stream before the
+// start event.  In eager launching the GPU otherwise idles between kernels
+// while the host enqueues the next one, and the start event would time-stamp
+// that idle gap (host launch latency) into the kernel's interval; behind the
+// spin the start event, the kernel and the end event are all enqueued before
+// the GPU reaches them, so the interval is the kernel's own, as in a replayed
+// graph (bench.py; rocprofv3's kernel trace of the same command agrees).
+__global__ void k_timing_spin(float* sink, int iters) {
+  float a = (float)threadIdx.x, b = 1.0000001f;
+  for (int i = 0; i < iters; ++i) a = fmaf(a, b, 1e-7f);
+  if (a == -1.f) sink[threadIdx.x] = a;   // (never true: keeps the loop)
+}
+static float* g_sink = nullptr;
+
 Timer::Timer(const char* name, hipStream_t st) : name_(name), st_(st), a_(nullptr) {
   if (!g_timing) return;
   a_ = take_event();
-  if (a_) (void)hipEventRecord(a_, st_);
+  if (!a_) return;
+  if (g_timing == 2) {
+    if (!g_sink && hipMalloc(&g_sink, 256) != hipSuccess) g_sink = nullptr;
+    if (g_sink) hipLaunchKernelGGL(k_timing_spin, dim3(1), dim3(64), 0, st_, g_sink, 50000);
+  }
+  (void)hipEventRecord(a_, st_);
 }
 
 void Timer::end() {
@@ -89,8 +108,26 @@ static void resolve(const std::string& name) {
 }
 }  // namespace pf
 
+namespace pf {
+static std::map<std::string, int> g_repeat;
+int repeats(const char* name) {
+  if (g_repeat.empty()) return 0;
+  auto it = g_repeat.find(name);
+  return it == g_repeat.end() ? 0 : it->second;
+}
+}  // namespace pf
+
+extern "C" int pfsgnn_timing_repeat(const char* name, int extra) {
+  PF_REQUIRE(name && extra >= 0 && extra <= 16, "pfsgnn_timing_repeat", "bad arguments");
+  if (extra == 0)
+    pf::g_repeat.erase(name);
+  else
+    pf::g_repeat[name] = extra;
+  return 0;
+}
+
 extern "C" int pfsgnn_timing_enable(int on) {
-  pf::g_timing = on != 0;
+  pf::g_timing = on == 2 ? 2 : (on != 0 ? 1 : 0);
   return 0;
 }
 

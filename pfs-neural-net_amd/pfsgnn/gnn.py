@@ -191,12 +191,12 @@ def geometry(x_s, x_t, x_u, edge_index, F):
     E = int(edge_index.size(1))
     if E == 0:
         raise ValueError("edge_index has no edges")
-    # the layout depends on the sliced/composed choice, which depends on Fdim
-    # and the edge path (sliced_ok), so they are part of the key
-    be = backend()
-    path = be.edge_path() if hasattr(be, "edge_path") else None
-    key = (E, G, NF, NC, F, path, sliced_on())
+    key = (E, G, NF, NC)
     hit = _LAYOUT_CACHE.get(edge_index, key)
+    if hit is not None and hit.sp is not None and (hit.sp.sl is not None) != sliced_ok(NC, F):
+        # a general batch's sliced / composed choice follows Fdim and the edge
+        # path (sliced_ok): a layout made under another choice is remade
+        hit = None
     if hit is None:
         complete = False
         if E == G * NF * NC:

@@ -118,6 +118,7 @@ _SIGS = {
     "pfsgnn_edge_grid": ([I, I, I, ctypes.POINTER(ctypes.c_int)], I),
     "pfsgnn_timing_enable": ([I], I),
     "pfsgnn_timing_reset": ([], I),
+    "pfsgnn_timing_repeat": ([ctypes.c_char_p, I], I),
     "pfsgnn_timing_query": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_longlong)], I),
     "pfsgnn_lin": ([P, I, I, I, P, I, P, FL, I, P, I, P], I),
@@ -272,7 +273,14 @@ KERNELS = ["edge_mlp_fwd", "source_fwd", "target_fwd", "target_bwd", "source_bwd
 
 
 def timing_enable(on=True):
-    lib().pfsgnn_timing_enable(1 if on else 0)
+    """on: False / True (events around each launch) / "spin" (the same behind
+    a lead-in spin kernel: the kernel's own time in an eager step)."""
+    lib().pfsgnn_timing_enable(2 if on == "spin" else (1 if on else 0))
+
+
+def timing_repeat(name, extra):
+    """Launch kernel `name` 1 + extra times back to back (pfsgnn_timing_repeat)."""
+    _check(lib().pfsgnn_timing_repeat(name.encode(), int(extra)), "pfsgnn_timing_repeat")
 
 
 def timing_reset():
