@@ -322,7 +322,9 @@ def main():
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    assert torch.isfinite(loss).item(), "non-finite loss"
+    # (PFSGNN_BENCH_ANY_LOSS=1: timing studies of ablation builds, tools/variants.sh)
+    assert torch.isfinite(loss).item() or os.environ.get("PFSGNN_BENCH_ANY_LOSS") == "1", \
+        "non-finite loss"
     consistency = None
     if world > 1:
         # every rank must end the K steps with bitwise the same parameters

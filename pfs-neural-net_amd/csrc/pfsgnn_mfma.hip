@@ -91,18 +91,39 @@ __global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float*
     floatx4 z[NT], a[NT];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) z[tt] = ps[tt] + ClassRows<H>::get(ptl, c - c0, tt, g4);
+#ifndef MF_ABL_NOL1   // (MF_ABL_*: ablation builds for timing studies only, tools/variants.sh)
     L1.apply(x, z);
+#else
+    z[0] += x[0];
+#endif
+#ifndef MF_ABL_NOLRELU
     lrelu_act<H>(z, a);
+#else
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) a[tt] = z[tt];
+#endif
     floatx4 yo[1] = {bb};
+#ifndef MF_ABL_NOL2
     L2.apply(a, yo);
+#else
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) yo[0] += a[tt];
+#endif
     if (bfy) {  // the edge state at bf16 (PFSGNN_EDGE_BF16Y / _BF16): every consumer
                 // reads exactly what a bf16 store would hold
       const s16x4 h = hi4(yo[0]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) yo[0][r] = bf_f(h[r]);
     }
-    st_frows<F>(y, (uint32_t)c * eoc, ro, g4, fvalid, yo[0]);
+#ifndef MF_ABL_NOSTORE
+    st_frows<F>(y, EB * F, (uint32_t)c * eoc, ro, g4, fvalid, yo[0]);
+#endif
+#ifdef MF_ABL_NOSTATS
+    if (fvalid) { cnt += 1.f; mean += yo[0]; }
+    if (false) {
+#else
     if (fvalid) {
+#endif
       cnt += 1.f;
       const float rc = __builtin_amdgcn_rcpf(cnt);   // v_rcp_f32 (<= 1 ulp): a Welford weight
 #pragma unroll
@@ -529,7 +550,7 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
     if (gxe) {
       floatx4 gx[1] = {zero4()};
       if constexpr (PREC >= 1) LT.apply(sgz, gx); else LT.apply(gz, gx);
-      st_frows<F>(gxe, (uint32_t)c * eoc, ro, g4, fvalid, gx[0]);
+      st_frows<F>(gxe, EB * F, (uint32_t)c * eoc, ro, g4, fvalid, gx[0]);
     }
     lds_order();
 #pragma unroll
@@ -722,7 +743,7 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) g[0][r] = fm[r] ? g[0][r] + (g_next ? gnr[r] : 0.f) : 0.f;
-    st_frows<F>(g_tot, (uint32_t)c * eoc, ro, g4, fvalid, g[0]);
+    st_frows<F>(g_tot, EB * F, (uint32_t)c * eoc, ro, g4, fvalid, g[0]);
     if (mu1) {
 #pragma unroll
       for (int r = 0; r < GM<F>::RPG; ++r) {
@@ -901,7 +922,7 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
     if (gxe) {
       floatx4 gx[1] = {zero4()};
       if constexpr (PREC >= 1) L1T.apply(sgz, gx); else L1T.apply(gz, gx);
-      st_frows<F>(gxe, (uint32_t)c * eoc, ro, g4, fvalid, gx[0]);
+      st_frows<F>(gxe, EB * F, (uint32_t)c * eoc, ro, g4, fvalid, gx[0]);
     }
     const typename WI::TA tgy = WI::A(im_gy, lane);
 #pragma unroll

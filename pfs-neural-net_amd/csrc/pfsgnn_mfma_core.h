@@ -577,15 +577,39 @@ __device__ __forceinline__ floatx4 ld_frows(Rsrc p, uint32_t co, const RowOff<F>
   return v;
 }
 
+// The lane's rows of an F-wide edge tensor of `bytes` bytes at class offset co:
+// global stores under per-row exec masks (default), or (MF_BUF_STORE=1)
+// branch-free buffer stores, a row the lane does not own (invalid fiber,
+// padding slot) given a voffset past the buffer's range and dropped by the
+// range check -- measured equal on the bench step (profiles/r04k_ab.txt;
+// target_bwd 4 % slower), so not the default.  The buffer form passes the
+// row's value through a float temporary before its bit-cast: hipcc's
+// __builtin_bit_cast of a vector ELEMENT reads element 0 (DESIGN.md
+// §Edge-row stores; tests/test_bitcast_vector_element.py).
+#ifndef MF_BUF_STORE
+#define MF_BUF_STORE 0
+#endif
 template <int F>
-__device__ __forceinline__ void st_frows(float* p, uint32_t co, const RowOff<F>& ro, int g,
-                                         bool valid, const floatx4& v) {
+__device__ __forceinline__ void st_frows(float* p, uint32_t bytes, uint32_t co, const RowOff<F>& ro,
+                                         int g, bool valid, const floatx4& v) {
+#if MF_BUF_STORE
+  const Rsrc rp = rsrc(p, bytes);
+#pragma unroll
+  for (int r = 0; r < GM<F>::RPG; ++r) {
+    const int k = GM<F>::row(g, r);
+    const float e = v[r];
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, e), rp,
+                                          (valid && k >= 0) ? ro.o[r] : bytes, co, 0);
+  }
+#else
+  (void)bytes;
   char* base = reinterpret_cast<char*>(p) + co;
 #pragma unroll
   for (int r = 0; r < GM<F>::RPG; ++r) {
     const int k = GM<F>::row(g, r);
     if (valid && k >= 0) *reinterpret_cast<float*>(base + opaque(ro.o[r])) = v[r];
   }
+#endif
 }
 
 // per-feature constants of an F-wide block in the lane's slot order

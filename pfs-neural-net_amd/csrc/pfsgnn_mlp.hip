@@ -1040,22 +1040,26 @@ size_t bwd_lds(int m) {   // (RS: a 64-row input-gradient buffer, one output-til
 }
 
 // blocks per CU: the M <= 3 kernels fit 2 (registers, LDS), the wider ones
-// run one 4-wave block per CU with up to 512 registers per lane
-// The grid is balanced over the rounds the chunks need anyway (599 chunks at
-// 512 slots: 300 blocks of 2 chunks, not 512 of which 87 run a second one),
-// so fewer blocks stage the weight images for the same number of chunk rounds
-// (opt-in knob PFSGNN_MLP_BALANCE=1, default off: one block per slot).
-int grid_for(int N, int m, size_t lds) {
-  static const bool bal = [] {
-    const char* e = getenv("PFSGNN_MLP_BALANCE");
-    return e && atoi(e) != 0;
+// run one 4-wave block per CU with up to 512 registers per lane; one block per
+// slot of the device's CUs (persistent grid-stride over the 64-node chunks).
+// (Balancing the grid over the chunk rounds -- 300 blocks of 2 chunks instead
+// of 512 with 87 running a second one -- measured no different at either
+// bench shape, profiles/r04l_ab.txt, and was removed.)
+int cu_count() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      return 256;
+    return v;
   }();
+  return n;
+}
+int grid_for(int N, int m, size_t lds) {
+  (void)m;
   const int nch = (N + 63) / 64;
   const int per_cu = (lds <= 80 * 1024) ? 2 : 1;   // (160 KB of LDS per CU)
-  const int slots = 256 * per_cu;
-  if (!bal) return std::max(1, std::min(nch, slots));
-  const int rounds = (nch + slots - 1) / slots;
-  return std::max(1, (nch + rounds - 1) / rounds);
+  return std::max(1, std::min(nch, cu_count() * per_cu));
 }
 
 // pfsgnn_seg list -> InSegs (blocks must be contiguous in the weight columns)

@@ -266,7 +266,7 @@ __global__ __launch_bounds__(256) void ksl_edge_mlp_fwd(
     L2.apply(a, yo);
 #pragma unroll
     for (int r = 0; r < 4; ++r) yo[0][r] = ev ? yo[0][r] : 0.f;
-    st_frows<F>(y, (uint32_t)k * eoc, ro, g4, true, yo[0]);
+    st_frows<F>(y, EB * F, (uint32_t)k * eoc, ro, g4, true, yo[0]);
     if (ev) {
       cnt += 1.f;
       const float rc = __builtin_amdgcn_rcpf(cnt);
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(256) void ksl_target_bwd(
     if (gxe) {
       floatx4 gx[1] = {zero4()};
       if constexpr (PREC >= 1) LT.apply(sgz, gx); else LT.apply(gz, gx);
-      st_frows<F>(gxe, (uint32_t)k * eoc, ro, g4, true, gx[0]);
+      st_frows<F>(gxe, EB * F, (uint32_t)k * eoc, ro, g4, true, gx[0]);
     }
     lds_order();
 #pragma unroll
@@ -762,7 +762,7 @@ __global__ __launch_bounds__(256, 2) void ksl_source_bwd(
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) g[0][r] = fe[r] ? g[0][r] + (g_next ? gnr[r] : 0.f) : 0.f;
-    st_frows<F>(g_tot, (uint32_t)k * eoc, ro, g4, true, g[0]);
+    st_frows<F>(g_tot, EB * F, (uint32_t)k * eoc, ro, g4, true, g[0]);
     if (mu1) {
 #pragma unroll
       for (int r = 0; r < GM<F>::RPG; ++r) {
@@ -925,7 +925,7 @@ __global__ __launch_bounds__(256, 2) void ksl_edge_mlp_bwd(
     if (gxe) {
       floatx4 gx[1] = {zero4()};
       if constexpr (PREC >= 1) L1T.apply(sgz, gx); else L1T.apply(gz, gx);
-      st_frows<F>(gxe, (uint32_t)k * eoc, ro, g4, true, gx[0]);
+      st_frows<F>(gxe, EB * F, (uint32_t)k * eoc, ro, g4, true, gx[0]);
     }
     acc_add<H>(wacc, own, cl, ev, g4, j16, gz);
     const typename WI::TA tgy = WI::A(im_gy, lane);

@@ -318,6 +318,10 @@ class _ParamMixin:
             bufs[k + "num_batches_tracked"].add_(1)
 
 
+def _mark_live_hook(p):
+    p._pf_live = True
+
+
 class _FlatMixin(_ParamMixin):
     """Top-level modules keep all parameters (and grads) as views of one flat
     fp32 buffer in the reference's state_dict order: the optimiser (FusedAdam)
@@ -350,6 +354,13 @@ class _FlatMixin(_ParamMixin):
             if isinstance(mod, torch.nn.BatchNorm1d):
                 mod.to(dev)
         self._pf_flat, self._pf_gflat, self._pf_off = flat, gflat, offs
+        # a gradient that reaches a parameter through plain torch autograd (a
+        # regulariser on the weights, ...) marks it live too, as p.grad is not
+        # None would for torch.optim.Adam (FusedAdam reads _pf_live)
+        for _, p in params:
+            if not getattr(p, "_pf_hooked", False):
+                p.register_post_accumulate_grad_hook(_mark_live_hook)
+                p._pf_hooked = True
 
     def _flat_grads(self):
         """Attach every p.grad as a view of the flat grad buffer (zeroing the

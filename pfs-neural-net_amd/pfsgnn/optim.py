@@ -32,7 +32,9 @@ def _is_live(p):
     """Whether this step's backward gave p a gradient, as torch.optim.Adam sees
     it (``p.grad is not None``).  pfsgnn's fused backward keeps every
     ``p.grad`` attached to the flat gradient buffer (graph capture) and marks
-    the parameters it wrote with ``p._pf_live`` instead (gnn._GradRecorder)."""
+    the parameters it wrote with ``p._pf_live`` instead (gnn._GradRecorder);
+    a gradient accumulated by plain torch autograd (a torch-side term of the
+    loss on the weights) sets it too (gnn._mark_live_hook)."""
     live = getattr(p, "_pf_live", None)
     return (p.grad is not None) if live is None else bool(live)
 

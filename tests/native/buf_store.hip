@@ -9,10 +9,12 @@
 //   variant 1: buffer_store per row, unconditional, the offset of an invalid
 //              row moved past the buffer's range (discarded by the bounds
 //              check): the branch-free form DESIGN.md §Performance tried;
-//   variant 2: st_frows, the global stores the kernels use;
+//   variant 2: global stores under per-row exec masks (the kernels' form
+//              until round 4);
 //   variants 3 / 4: variants 0 / 1 with the row's value first copied out of
 //              the vector into a float (`const float e = v[r]`) and THAT
 //              bit-cast to the builtin's unsigned data operand.
+//   variant 5: the product's st_frows (pfsgnn_mfma_core.h: variant 4's form).
 // Variants 0 / 1 bit-cast the vector element itself,
 // __builtin_bit_cast(unsigned int, v[r]) -- the only way to hand a float
 // element to __builtin_amdgcn_raw_buffer_store_b32 without a temporary.
@@ -58,8 +60,15 @@ __global__ __launch_bounds__(256) void kstore(const float* __restrict__ x, float
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v[r]), ry, off,
                                               co, 0);
       }
-    } else if constexpr (V == 2) {
-      st_frows<F>(y, co, ro, g4, fvalid, v);
+    } else if constexpr (V == 2) {   // global stores under per-row exec masks
+      char* base = reinterpret_cast<char*>(y) + co;
+#pragma unroll
+      for (int r = 0; r < GM<F>::RPG; ++r) {
+        const int k = GM<F>::row(g4, r);
+        if (fvalid && k >= 0) *reinterpret_cast<float*>(base + opaque(ro.o[r])) = v[r];
+      }
+    } else if constexpr (V == 5) {   // the product's st_frows
+      st_frows<F>(y, RB * F, co, ro, g4, fvalid, v);
     } else {
 #pragma unroll
       for (int r = 0; r < GM<F>::RPG; ++r) {
@@ -79,7 +88,7 @@ __global__ __launch_bounds__(256) void kstore(const float* __restrict__ x, float
 extern "C" int buf_store_run(const float* hx, float* hy, int NF, int NC, int variant) {
   const size_t n = (size_t)F * NF * NC;
   float *x, *y;
-  if (variant < 0 || variant > 4) return 2;
+  if (variant < 0 || variant > 5) return 2;
   if (hipMalloc(&x, n * 4) || hipMalloc(&y, n * 4)) return 1;
   int rc = 0;
   rc |= hipMemcpy(x, hx, n * 4, hipMemcpyHostToDevice) != hipSuccess;
@@ -89,7 +98,8 @@ extern "C" int buf_store_run(const float* hx, float* hy, int NF, int NC, int var
   else if (variant == 1) hipLaunchKernelGGL(kstore<1>, grid, block, 0, 0, x, y, NF, NC);
   else if (variant == 2) hipLaunchKernelGGL(kstore<2>, grid, block, 0, 0, x, y, NF, NC);
   else if (variant == 3) hipLaunchKernelGGL(kstore<3>, grid, block, 0, 0, x, y, NF, NC);
-  else hipLaunchKernelGGL(kstore<4>, grid, block, 0, 0, x, y, NF, NC);
+  else if (variant == 4) hipLaunchKernelGGL(kstore<4>, grid, block, 0, 0, x, y, NF, NC);
+  else hipLaunchKernelGGL(kstore<5>, grid, block, 0, 0, x, y, NF, NC);
   rc |= hipDeviceSynchronize() != hipSuccess;
   rc |= hipMemcpy(hy, y, n * 4, hipMemcpyDeviceToHost) != hipSuccess;
   rc |= hipFree(x) != hipSuccess;

@@ -149,3 +149,39 @@ def test_resume_from_reference_adam_state(emu_pfsgnn, capturable):
     wp, wm = check_resume(*run_resume(emu_pfsgnn, "cpu", capturable), max_ulp=2)
     print(f"capturable={capturable}: worst difference vs torch CPU Adam: parameters "
           f"{wp:.2f} ulp, moments {wm:.2f} ulp")
+
+
+def test_torch_side_gradient_marks_a_parameter_live(emu_pfsgnn):
+    """a parameter the fused backward leaves dead (decoder_s under
+    train.py's loss) but that a torch-side term of the loss reaches (here an
+    L2 penalty on its weights) must be updated by FusedAdam as torch.optim.Adam
+    updates it (its .grad is not None there)."""
+    from pfsgnn.optim import FusedAdam, _is_live
+    from pfsgnn.train import loss_function
+    from oracle.ref_graph import train_graph
+    pfsgnn = emu_pfsgnn
+    classes = np.load(os.path.join(GOLD, "classes.npz"))["increasing"]
+    ei, xs, xt, xe, u = train_graph(classes, 200, 10, generator=torch.Generator().manual_seed(3))
+    gnn = pfsgnn.GNN(B=2, Fdim=10, T=12, F_s=1, F_t=2)
+    gnn.train()
+    names = [n for n, _ in gnn.named_parameters()]
+    params = list(gnn.parameters())
+    opt = FusedAdam(params, lr=1e-2)
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in params]
+    ropt = torch.optim.Adam(ref, lr=1e-2)
+    gnn.zero_grad()
+    out = gnn(pfsgnn.BipartiteData(ei, xs, xt, xe, u))
+    loss, _ = loss_function(out, xt, pclass=0.1, pfiber=0.1, sharpness=10.0, seed=3)
+    pen = gnn.decoder_s[0].weight
+    (loss + 1e-3 * (pen * pen).sum()).backward()
+    live = {n for n, p in zip(names, params) if _is_live(p)}
+    assert "decoder_s.0.weight" in live and "decoder_s.2.weight" not in live
+    for r, p in zip(ref, params):
+        r.grad = p.grad.detach().clone() if _is_live(p) else None
+    i = names.index("decoder_s.0.weight")
+    before = params[i].detach().clone()
+    opt.step()
+    ropt.step()
+    for n, p, r in zip(names, params, ref):
+        assert torch.allclose(p.detach(), r.detach(), rtol=1e-6, atol=1e-7), n
+    assert not torch.equal(params[i].detach(), before)       # the penalised weight moved

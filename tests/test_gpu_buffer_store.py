@@ -3,10 +3,11 @@ own row map, offsets and loads from pfsgnn_mfma_core.h; 100 fibers x 7 classes
 at Fdim 10, so lane group 3 holds one row and two masked slots, and 28 lanes
 of the second block have no fiber).
 
-* variants 2 (st_frows: the global stores the edge kernels use), 3 and 4
-  (buffer stores, masked or with invalid offsets moved past the range, the
-  row value copied to a float before its bit-cast) store every row exactly
-  and nothing else;
+* variants 2 (global stores under per-row exec masks), 3 and 4 (buffer
+  stores, masked or with invalid offsets moved past the range, the row value
+  copied to a float before its bit-cast) and 5 (the product's st_frows, the
+  edge kernels' stores since round 4: variant 4's form) store every row
+  exactly and nothing else;
 * variants 0 and 1 (the same buffer stores with
   __builtin_bit_cast(unsigned int, v[r]) of the vector element itself) store
   row 0's value to all of a lane's rows: the compiler defect pinned on the
@@ -45,7 +46,7 @@ def test_edge_row_store_forms():
     rng = np.random.default_rng(11)
     x = rng.standard_normal((F, NC * NF)).astype(np.float32)      # [F][E], e = c*NF + f
     want = (x.astype(np.float64) * 2 + 1).astype(np.float32)   # = fmaf(x, 2, 1): 2x is exact
-    for v in (2, 3, 4):
+    for v in (2, 3, 4, 5):
         y = run(x, v)
         assert np.array_equal(y, want), f"variant {v}"
     # the defect's signature: every row of a lane holds its first row's value
