@@ -325,6 +325,41 @@ def main():
     # (PFSGNN_BENCH_ANY_LOSS=1: timing studies of ablation builds, tools/variants.sh)
     assert torch.isfinite(loss).item() or os.environ.get("PFSGNN_BENCH_ANY_LOSS") == "1", \
         "non-finite loss"
+    # ---- N > 1: the eager tail of a step (outside the captured graph): the
+    # buffer broadcast before the replay, the gradient all-reduce and Adam
+    # after it, each timed alone (synchronised) over a few extra steps
+    tail = None
+    if world > 1 and use_graph:
+        t_sync, t_red, t_adam = [], [], []
+        for i in range(min(args.steps, 10)):
+            torch.cuda.synchronize()
+            ta = time.perf_counter()
+            sync_buffers(gnn)
+            torch.cuda.synchronize()
+            tb = time.perf_counter()
+            graph.replay()
+            torch.cuda.synchronize()
+            tc = time.perf_counter()
+            allreduce_gradients(gnn)
+            torch.cuda.synchronize()
+            td = time.perf_counter()
+            opt.step()
+            torch.cuda.synchronize()
+            te = time.perf_counter()
+            t_sync.append(tb - ta)
+            t_red.append(td - tc)
+            t_adam.append(te - td)
+        med = lambda v: sorted(v)[len(v) // 2] * 1e3  # noqa: E731
+        tail = {"sync_buffers_ms": round(med(t_sync), 4), "allreduce_ms": round(med(t_red), 4),
+                "adam_ms": round(med(t_adam), 4),
+                "note": "per step, each part synchronised alone (median of %d steps after the "
+                        "timed region); in the timed steps they run unsynchronised around the "
+                        "graph replay" % len(t_sync)}
+        t = torch.tensor([tail["sync_buffers_ms"], tail["allreduce_ms"], tail["adam_ms"]],
+                         device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tail.update(sync_buffers_ms=round(float(t[0]), 4), allreduce_ms=round(float(t[1]), 4),
+                    adam_ms=round(float(t[2]), 4), over_ranks="max")
     consistency = None
     if world > 1:
         # every rank must end the K steps with bitwise the same parameters
@@ -506,6 +541,8 @@ def main():
         }
         if consistency is not None:
             line["rank_consistency"] = consistency
+        if tail is not None:
+            line["eager_tail"] = tail
         if alt:
             line["alt_paths"] = alt
         print(json.dumps(line), flush=True)

@@ -3,8 +3,11 @@ complete-graph path, on the bench geometry (GPU box).
 
 The objective is a fixed random linear functional of the GNN outputs (x_s,
 x_t, x_e, u) -- train.py's loss needs complete fiber-major graphs -- and the
-step is zero_grad + GNN forward + objective + backward + FusedAdam, eager,
-synchronised around the timed steps.
+step is zero_grad + GNN forward + objective + backward + FusedAdam, captured
+as a HIP graph and replayed (as bench.py times the headline; SPARSE_GRAPH=0:
+eager launches), synchronised around the timed steps; the median of
+SPARSE_RUNS (default 5) timed runs is reported, with the spread.  The edge
+kernels' eager per-step times (pfsgnn timing) follow each line.
 
     python tools/sparse_bench.py [G] [NF] [NC] [B] [steps]
 """
@@ -51,7 +54,8 @@ def run(density, label):
     data = pfsgnn.BipartiteData(ei, xs, xt, xe, torch.zeros(G, F))
     gnn = pfsgnn.GNN(B=B, Fdim=F, T=NC, F_s=1, F_t=2).cuda()
     gnn.train()
-    opt = pfsgnn.FusedAdam(gnn.parameters(), lr=1e-4)
+    use_graph = os.environ.get("SPARSE_GRAPH", "1") != "0"
+    opt = pfsgnn.FusedAdam(gnn.parameters(), lr=1e-4, capturable=use_graph)
     w = [torch.randn(n, F, device="cuda") * 1e-3 for n in (G * NF, G * NC, E, G)]
 
     def step():
@@ -64,24 +68,49 @@ def run(density, label):
 
     for _ in range(5):
         step()
-    # median of 3 timed runs of STEPS steps (one short run swings by +-30 % on a
+    torch.cuda.synchronize()
+    from pfsgnn import native
+    native.timing_enable("spin")
+    native.timing_reset()
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    native.timing_enable(False)
+    kt = {k: round(native.timing_query(k)[0] / 3, 3) for k in native.KERNELS}
+    kt = {k: v for k, v in kt.items() if v}
+    run_step = step
+    if use_graph:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            step()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step()
+        run_step = g.replay
+    # median of SPARSE_RUNS timed runs of STEPS steps (one short run swings on a
     # shared box)
     runs = []
-    for _ in range(3):
+    for _ in range(int(os.environ.get("SPARSE_RUNS", "5"))):
         torch.cuda.synchronize()
         t = time.perf_counter()
         for _ in range(STEPS):
-            step()
+            run_step()
         torch.cuda.synchronize()
         runs.append((time.perf_counter() - t) / STEPS * 1e3)
-    ms = sorted(runs)[1]
+    runs.sort()
+    ms = runs[len(runs) // 2]
     from pfsgnn import gnn as gmod
     pad = ""
     for e in gmod._LAYOUT_CACHE.d.values():
         if e[0]() is data.edge_index and e[3].sp is not None and e[3].sp.sl is not None:
             pad = f"  EP/E {e[3].sp.sl.EP / E:.3f}"
-    print(f"{label:34s} E={E:9d}  {ms:8.2f} ms/step  {E / ms / 1e3:8.1f} M edges/s{pad}",
+    print(f"{label:34s} E={E:9d}  {ms:8.2f} ms/step  {E / ms / 1e3:8.1f} M edges/s{pad}"
+          f"  (runs {runs[0]:.2f}..{runs[-1]:.2f} ms; {'graph' if use_graph else 'eager'})",
           flush=True)
+    print(f"{'':34s} edge kernels, ms per eager step: {kt}", flush=True)
 
 
 dens = [float(x) for x in os.environ.get("SPARSE_DENSITIES", "1.0,0.999,0.3,0.05").split(",")]

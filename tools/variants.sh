@@ -1,12 +1,12 @@
 #!/bin/bash
 # Tuning builds of the MFMA edge kernels: libpfsgnn_<name>.so = the normal
-# objects with pfsgnn_mfma.o rebuilt under extra -D flags; select one at run
-# time with PFSGNN_LIB_VARIANT=<name> (pfsgnn/native.py).
+# objects with pfsgnn_mfma.o and pfsgnn_sliced.o rebuilt under extra -D flags;
+# select one at run time with PFSGNN_LIB_VARIANT=<name> (pfsgnn/native.py).
 #   bash tools/variants.sh name1 "-DMF_DEPTH_BWD=3" name2 "-DCOL_CH=16" ...
 set -e
 cd "$(dirname "$0")/../pfs-neural-net_amd"
 make -j8 >/dev/null
-objs=$(ls build/*.o | grep -v -e pfsgnn_mfma.o -e var_)
+objs=$(ls build/*.o | grep -v -e pfsgnn_mfma.o -e pfsgnn_sliced.o -e var_)
 flags=$(make -s -f - print <<'MK'
 include Makefile
 print:
@@ -17,7 +17,8 @@ pids=()
 while [ $# -gt 0 ]; do
   name=$1; def=$2; shift 2
   ( /opt/rocm/bin/hipcc $flags $def -c csrc/pfsgnn_mfma.hip -o build/var_$name.o &&
-    /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o pfsgnn/libpfsgnn_$name.so $objs build/var_$name.o &&
+    /opt/rocm/bin/hipcc $flags $def -c csrc/pfsgnn_sliced.hip -o build/var_sl_$name.o &&
+    /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o pfsgnn/libpfsgnn_$name.so $objs build/var_$name.o build/var_sl_$name.o &&
     echo "built libpfsgnn_$name.so ($def)" ) &
   pids+=($!)
 done
