@@ -282,6 +282,41 @@ int pfsgnn_target_global_fwd(
     float* means, float* gZ, float* gV, float* unew, float* y1, float* r1, float* r2,
     const float* We, const float* be, const float* Ws, const float* bs, float* Pt, float* Qt,
     void* ws, size_t ws_bytes, void* stream);
+/* A whole block tail on a COMPLETE batch (gnn.py:188-192 + 218-223) in two
+ * launches: TModel's per-edge layer (as pfsgnn_target_fwd: hsum, agg = Wt2 hsum +
+ * NF bt2, tmask), then ONE launch for the class side -- the per-class sums of
+ * the edge kernel's partials, node_mlp_2 + BatchNorm1d, the GlobalModel and the
+ * next block's Pt / Qt -- with every output of pfsgnn_target_global_fwd.  The
+ * class launch runs G * ceil(NC / 32) units of 32 classes on at most one
+ * workgroup per CU with one device-wide barrier between node_mlp_2 (and its
+ * BatchNorm partials) and the norm (pfsgnn_sync_faults counts barrier
+ * time-outs; 0 in a healthy run).  node_mlp_2's weights: W1 [4F][4F], W2
+ * [F][4F] (its input [x_t, agg, u[batch]], gnn.py:191).  Replaces
+ * pfsgnn_target_fwd + pfsgnn_target_global_fwd (4 launches) on complete graphs. */
+typedef struct {
+  int G, NF, NC, F;
+  /* TModel per-edge layer (pfsgnn_target_fwd) */
+  const float *y, *sc, *sh, *Rs, *Wt1, *Wt2, *bt2;
+  unsigned char* tmask;
+  float *hsum, *agg;                              /* [2F][G*NC] each */
+  /* node_mlp_2 + BatchNorm1d (pfsgnn_target_global_fwd) */
+  const float *xt, *u, *W1, *b1, *W2, *b2, *gamma, *beta;
+  float *Z, *Yp, *rm, *rv, *xt_new, *mu, *var;
+  float momentum, eps;
+  /* GlobalModel */
+  const float *xs, *gW1, *gb1, *gW2, *gb2, *gw;
+  int gH;
+  float reps;
+  float *means, *gZ, *gV, *unew, *y1, *r1, *r2;
+  /* next block's class parts (We NULL: none) */
+  const float *We, *be, *Ws, *bs;
+  float *Pt, *Qt;
+} pfsgnn_block_tail;
+int pfsgnn_target_block_fwd(const pfsgnn_block_tail* a, void* ws, size_t ws_bytes, void* stream);
+/* sizeof(pfsgnn_block_tail), for bindings to check their struct layout */
+size_t pfsgnn_block_tail_bytes(void);
+/* device-wide barrier time-outs since load (a diagnostic; *n = count) */
+int pfsgnn_sync_faults(unsigned* n);
 /* One row block of an input-gradient output: rows `rows` of dX go to x
  * ([rows][N], overwritten, or accumulated when add != 0); x == NULL drops them. */
 typedef struct {

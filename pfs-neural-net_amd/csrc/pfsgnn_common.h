@@ -27,6 +27,9 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 namespace pf {
 void set_error(const std::string& msg);
 int fail(const char* where, const char* what);
+// the class launch of pfsgnn_target_block_fwd (pfsgnn_mlp.hip) and its
+// workspace in floats
+size_t tail_ws_floats(int G, int NC, int F);
 int check_launch(const char* where);
 // brackets one kernel launch with HIP events when pfsgnn_timing_enable(1)
 // extra back-to-back launches of a named main kernel (pfsgnn_timing_repeat;

@@ -1758,6 +1758,29 @@ extern "C" size_t pfsgnn_sl_tmask_bytes(const pfsgnn_sliced_t* sl, int F) {
   return (size_t)sl->EP * 4;   // per position, as pfsgnn_tmask_bytes per edge
 }
 
+namespace pf {
+int class_tail_fwd(const pfsgnn_block_tail& a, const float* cpart, int BPG, float bscale,
+                   float* scratch, hipStream_t st);
+}
+// TModel's per-edge layer into the per-block column partials `part`
+static int target_fwd_edges(const pfsgnn_sliced_t* sl, const EdgeGeo& geo, int F, const float* y,
+                            const float* sc, const float* sh, const float* Rs, const float* Wt1,
+                            float* part, unsigned char* tmask, hipStream_t st) {
+  pf::Timer tm_("target_fwd", st);
+  if (sl) {
+    if (int rc = pfm::sl_target_fwd(geo, sl_of(*sl), F, y, sc, sh, Rs, Wt1, part, tmask,
+                                    mf_prec(1, F), st))
+      return rc;
+  } else if (use_mfma()) {
+    if (int rc = pfm::target_fwd(geo, F, y, sc, sh, Rs, Wt1, part, tmask, mf_prec(1, F), st)) return rc;
+  } else {
+    DISPATCH_F(F, hipLaunchKernelGGL(k_target_fwd<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo,
+                                     y, sc, sh, Rs, Wt1, part));
+  }
+  tm_.end();
+  return 0;
+}
+
 static int target_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
                            const float* y, const float* sc, const float* sh, const float* Rs,
                            const float* Wt1, float* hsum, const float* Wt2, const float* bt2,
@@ -1771,18 +1794,7 @@ static int target_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
   float* part = w.take((size_t)G * col_bpg(geo, sl) * NC * 2 * F);
   PF_REQUIRE(part, "pfsgnn_target_fwd", "workspace too small");
   hipStream_t st = as_stream(stream);
-  { pf::Timer tm_("target_fwd", st);
-  if (sl) {
-    if (int rc = pfm::sl_target_fwd(geo, sl_of(*sl), F, y, sc, sh, Rs, Wt1, part, tmask,
-                                    mf_prec(1, F), st))
-      return rc;
-  } else if (use_mfma()) {
-    if (int rc = pfm::target_fwd(geo, F, y, sc, sh, Rs, Wt1, part, tmask, mf_prec(1, F), st)) return rc;
-  } else {
-  DISPATCH_F(F, hipLaunchKernelGGL(k_target_fwd<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo, y,
-                                   sc, sh, Rs, Wt1, part));
-  }
-  tm_.end(); }
+  if (int rc = target_fwd_edges(sl, geo, F, y, sc, sh, Rs, Wt1, part, tmask, st)) return rc;
   PF_REQUIRE(!Wt2 || agg, "pfsgnn_target_fwd", "Wt2 needs agg");
   // agg = Wt2 hsum + bscale bt2 (gnn.py:188-190, the second Linear after the sum)
   const NodeLin La = Wt2 ? NodeLin{Wt2, 2 * F, 0, 2 * F, 0, bt2, bscale, agg, (long long)G * NC}
@@ -1797,6 +1809,37 @@ extern "C" int pfsgnn_target_fwd(int G, int NF, int NC, int F, const float* y, c
                                  unsigned char* tmask, void* ws, size_t ws_bytes, void* stream) {
   return target_fwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Rs, Wt1, hsum, Wt2, bt2, bscale, agg,
                          tmask, ws, ws_bytes, stream);
+}
+
+extern "C" size_t pfsgnn_block_tail_bytes(void) { return sizeof(pfsgnn_block_tail); }
+
+extern "C" int pfsgnn_target_block_fwd(const pfsgnn_block_tail* a, void* ws, size_t ws_bytes,
+                                       void* stream) {
+  const char* where = "pfsgnn_target_block_fwd";
+  PF_REQUIRE(a, where, "null");
+  const int G = a->G, NF = a->NF, NC = a->NC, F = a->F;
+  if (int rc = check_dims(where, G, NF, NC, F)) return rc;
+  PF_REQUIRE(a->y && a->Rs && a->Wt1 && a->Wt2 && a->bt2 && a->hsum && a->agg && a->xt && a->u &&
+                 a->W1 && a->b1 && a->W2 && a->b2 && a->gamma && a->beta && a->Z && a->Yp &&
+                 a->xt_new && a->mu && a->var && a->xs && a->gW1 && a->gb1 && a->gW2 && a->gb2 &&
+                 a->means && a->gZ && a->gV && a->unew,
+             where, "null");
+  PF_REQUIRE(a->gH > 0 && a->gH <= 192, where, "GlobalModel width must be <= 192");
+  PF_REQUIRE(!a->gw || (a->y1 && a->r1 && a->r2), where, "RMSNorm needs y1, r1, r2");
+  PF_REQUIRE(!a->We || (a->be && a->Ws && a->bs && a->Pt && a->Qt), where,
+             "next-block parts need be, Ws, bs, Pt, Qt");
+  PF_REQUIRE((long long)G * NC > 1, where, "BatchNorm needs more than one class");
+  const EdgeGeo geo = geo_of(G, NF, NC, nullptr);
+  Ws w{reinterpret_cast<char*>(ws), ws_bytes};
+  float* part = w.take((size_t)G * col_bpg(geo, nullptr) * NC * 2 * F);
+  float* scratch = w.take(pf::tail_ws_floats(G, NC, F));
+  PF_REQUIRE(part && scratch, where, "workspace too small");
+  hipStream_t st = as_stream(stream);
+  if (int rc = target_fwd_edges(nullptr, geo, F, a->y, a->sc, a->sh, a->Rs, a->Wt1, part, a->tmask,
+                                st))
+    return rc;
+  if (int rc = pf::class_tail_fwd(*a, part, col_bpg(geo, nullptr), (float)NF, scratch, st)) return rc;
+  return pf::check_launch(where);
 }
 
 extern "C" int pfsgnn_sl_target_fwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,

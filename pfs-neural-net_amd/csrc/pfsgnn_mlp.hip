@@ -47,17 +47,6 @@ struct OutSegs {
   int add[NM_SEG];
 };
 
-// Address of row k of the concatenated input at node n (k wave-uniform: the
-// block selection is scalar, the node offset per lane)
-__device__ __forceinline__ const float* in_ptr(const InSegs& S, int k, int n, int ng, int N) {
-  const float* p = S.p[0];
-  int kb = 0, pg = S.pg[0];
-  if (k >= S.k0[1]) { p = S.p[1]; kb = S.k0[1]; pg = S.pg[1]; }
-  if (k >= S.k0[2]) { p = S.p[2]; kb = S.k0[2]; pg = S.pg[2]; }
-  if (k >= S.k0[3]) { p = S.p[3]; kb = S.k0[3]; pg = S.pg[3]; }
-  return pg ? p + (size_t)(k - kb) * S.Gc + ng : p + (size_t)(k - kb) * N + n;
-}
-
 // async global -> LDS copy of one float per lane: LDS row base (wave-uniform)
 // + 4*lane, no VGPR destination (global_load_lds_dword)
 __device__ __forceinline__ void glds4(const float* src, float* lds_row) {
@@ -65,16 +54,40 @@ __device__ __forceinline__ void glds4(const float* src, float* lds_row) {
                                    (__attribute__((address_space(3))) void*)lds_row, 4, 0, 0);
 }
 
-// Row k of the input gradient for the 64 nodes of a chunk (k wave-uniform)
-__device__ __forceinline__ void out_row(const OutSegs& S, int k, int n, int N, float v) {
+// Row descriptors of a concatenated input (RowIn: row k's base at node 0 --
+// column 0 for a per-graph block -- and the per-graph flag) or of the gradient
+// outputs (RowOut: row k's base, null when dropped, and the add flag), built
+// once per block in LDS by threads k < K.  The row loops then read a ready
+// base pointer: selecting the block from the kernel arguments per row cost a
+// dependent scalar load and wait per row (25 rows per wave and chunk of the
+// 100-wide SModel MLP), in series with the copies and the stores.
+struct RowIn {
+  const float* p;
+  int pg, pad;
+};
+struct RowOut {
+  float* p;
+  int add, pad;
+};
+__device__ __forceinline__ void build_in_rows(const InSegs& S, int K, int N, RowIn* tab) {
+  const int k = threadIdx.x;
+  if (k >= K) return;
+  const float* p = S.p[0];
+  int kb = 0, pg = S.pg[0];
+  if (k >= S.k0[1]) { p = S.p[1]; kb = S.k0[1]; pg = S.pg[1]; }
+  if (k >= S.k0[2]) { p = S.p[2]; kb = S.k0[2]; pg = S.pg[2]; }
+  if (k >= S.k0[3]) { p = S.p[3]; kb = S.k0[3]; pg = S.pg[3]; }
+  tab[k] = RowIn{p + (size_t)(k - kb) * (pg ? S.Gc : N), pg, 0};
+}
+__device__ __forceinline__ void build_out_rows(const OutSegs& S, int K, int N, RowOut* tab) {
+  const int k = threadIdx.x;
+  if (k >= K) return;
   float* p = S.p[0];
   int kb = 0, add = S.add[0];
   if (k >= S.k0[1]) { p = S.p[1]; kb = S.k0[1]; add = S.add[1]; }
   if (k >= S.k0[2]) { p = S.p[2]; kb = S.k0[2]; add = S.add[2]; }
   if (k >= S.k0[3]) { p = S.p[3]; kb = S.k0[3]; add = S.add[3]; }
-  if (!p) return;
-  float* q = p + (size_t)(k - kb) * N + n;
-  *q = add ? *q + v : v;
+  tab[k] = RowOut{p ? p + (size_t)(k - kb) * N : nullptr, add, 0};
 }
 
 // node tables of a chunk staged in LDS as [row][XS_LD]: a wave's 16-node
@@ -117,12 +130,31 @@ __global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_fwd(InSeg
   constexpr int XSZ = 16 * M * XS_LD;
   const int nch = (N + 63) / 64;
   const int wu = __builtin_amdgcn_readfirstlane(wave);
+  // this wave's input rows k = wu + 4 i (LDS-staged form): bases in registers
+  __shared__ RowIn rin[RS ? 1 : 16 * M];
+  const float* rp[RS ? 1 : 4 * M];
+  uint32_t pgm = 0;
+  if (!RS) {
+    build_in_rows(S, K, N, rin);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < (RS ? 0 : 4 * M); ++i) {
+      const int k = wu + 4 * i;
+      const RowIn r = rin[k < K ? k : 0];
+      rp[i] = r.p;
+      pgm |= (uint32_t)(r.pg != 0) << i;
+    }
+  }
   auto issue = [&](int ch, int buf) {
     const int n = ch * 64 + lane;
     const int nc = n < N ? n : N - 1;
     const int ng = S.npg ? nc / S.npg : 0;
     float* dst = Xs0 + buf * XSZ;
-    for (int k = wu; k < K; k += 4) glds4(in_ptr(S, k, nc, ng, N), dst + k * XS_LD);
+#pragma unroll
+    for (int i = 0; i < (RS ? 0 : 4 * M); ++i) {
+      const int k = wu + 4 * i;
+      if (k < K) glds4(rp[i] + (((pgm >> i) & 1u) ? ng : nc), dst + k * XS_LD);
+    }
   };
   // RS: lane (col, kq) holds rows 4s + kq of its node (the B operand of K-step s)
   float xq[RS ? 4 * M : 1];
@@ -692,6 +724,360 @@ __global__ __launch_bounds__(CG_THREADS) void k_class_global_fwd(ClassGlobalArgs
   }
 }
 
+// ---------------------------------------------------------------- fused block tail
+// A block's whole class side on a complete batch in ONE launch
+// (pfsgnn_target_block_fwd): units of 32 classes of one graph, one workgroup
+// per CU at most (persistent over the units), in two phases around one
+// device-wide barrier:
+//   1. TModel's per-class sum of the edge kernel's column partials (hsum, its
+//      second Linear agg = Wt2 hsum + bscale bt2, gnn.py:188-190), node_mlp_2
+//      over [x_t, agg, u[g]] (gnn.py:191; fp32 FMA chains in k order), its
+//      Welford partials, and the unit's share of the graph sums of x_s and of
+//      the pre-norm output;
+//   2. every workgroup merges the partials in one fixed order (bn_stats_part;
+//      workgroup 0 writes mu / var / running statistics), normalises its
+//      classes (gnn.py:192), runs the GlobalModel of its graph (gnn.py:218-223;
+//      the mean of x_t from the pre-norm sums -- the norm is affine per
+//      channel) and the next block's Pt / Qt (gnn.py:100, 136) of its classes.
+// One launch for what were reduce_columns_lin + mlp_fwd + class_global_fwd.
+constexpr int CT_CLS = 32;                  // most classes per unit (8, 16 or 32: the
+                                            // smallest that keeps the units <= 512)
+__device__ unsigned pf_tail_bar[2];         // device-wide barrier: arrivals, generation
+__device__ unsigned pf_sync_fault_count;    // barrier time-outs (diagnostic)
+
+// every workgroup of the grid (all resident: the grid is at most one per CU)
+// waits here; the arrivals publish their global writes (agent-scope release)
+// and the waiters acquire them.  A wait that outlives ~2^24 sleeps is counted
+// and abandoned, so no wave can hang on it.
+__device__ void grid_sync(unsigned nb) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned gen = __hip_atomic_load(&pf_tail_bar[1], __ATOMIC_ACQUIRE,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned a = __hip_atomic_fetch_add(&pf_tail_bar[0], 1u, __ATOMIC_ACQ_REL,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    if (a == nb - 1) {
+      __hip_atomic_store(&pf_tail_bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&pf_tail_bar[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      unsigned spins = 0;
+      while (__hip_atomic_load(&pf_tail_bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        __builtin_amdgcn_s_sleep(4);
+        if (++spins > (1u << 24)) {
+          __hip_atomic_fetch_add(&pf_sync_fault_count, 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+#ifdef PF_TAIL_STAMPS   // (diagnostic build: per-workgroup phase clocks, tools/tail_stamps.py)
+__device__ unsigned long long pf_tail_stamps[512][8];
+#define TAIL_STAMP(i) \
+  if (threadIdx.x == 0) pf_tail_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime();
+#else
+#define TAIL_STAMP(i)
+#endif
+
+struct TailArgs {
+  pfsgnn_block_tail a;
+  const float* cpart;   // [G][BPG][NC][2F] the edge kernel's column partials
+  int BPG, CT, QB, nunits;   // CT classes per unit, QB units per graph
+  float bscale;
+  float *part, *xss, *yps;   // [nunits][PART_LEN], [nunits][F], [nunits][F]
+};
+
+template <int F>
+__global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
+  constexpr int C2 = 2 * F, K = 4 * F, H = 4 * F, K3 = 3 * F;
+  const pfsgnn_block_tail& A = T.a;
+  const int t = threadIdx.x, G = A.G, NC = A.NC, NF = A.NF;
+  const long long NT = (long long)G * NC, NS = (long long)G * NF;
+  TAIL_STAMP(0)
+  __shared__ float w1[H * K], w2[F * H], wt2[C2 * C2], bb1[H], bb2[F], bt[C2];
+  __shared__ float xin[CT_CLS][K + 1], act[CT_CLS][H + 1], ypl[CT_CLS][F + 1];
+  __shared__ float hs[CT_CLS][C2 + 1];
+  __shared__ float red[4][F];
+  // every weight load of the thread in flight before the first LDS store (a
+  // load -> store loop pays one round trip per element)
+  const bool gws = A.gH * K3 <= CG_GW1;
+  __shared__ float gw1[CG_GW1], gw2[F * CG_MAXH];
+  {
+    constexpr int N1 = (H * K + 255) / 256, N2 = (F * H + 255) / 256, N3 = (C2 * C2 + 255) / 256;
+    constexpr int NG1 = (CG_GW1 + 255) / 256, NG2 = (F * CG_MAXH + 255) / 256;
+    float v1[N1], v2[N2], v3[N3], g1[NG1], g2[NG2];
+    const int ng1 = gws ? A.gH * K3 : 0, ng2 = gws ? F * A.gH : 0;
+#pragma unroll
+    for (int i = 0; i < N1; ++i) v1[i] = t + 256 * i < H * K ? A.W1[t + 256 * i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < N2; ++i) v2[i] = t + 256 * i < F * H ? A.W2[t + 256 * i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < N3; ++i) v3[i] = t + 256 * i < C2 * C2 ? A.Wt2[t + 256 * i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NG1; ++i) g1[i] = t + 256 * i < ng1 ? A.gW1[t + 256 * i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NG2; ++i) g2[i] = t + 256 * i < ng2 ? A.gW2[t + 256 * i] : 0.f;
+    const float b1v = t < H ? A.b1[t] : 0.f, b2v = t < F ? A.b2[t] : 0.f,
+                btv = t < C2 ? A.bt2[t] : 0.f;
+#pragma unroll
+    for (int i = 0; i < N1; ++i) if (t + 256 * i < H * K) w1[t + 256 * i] = v1[i];
+#pragma unroll
+    for (int i = 0; i < N2; ++i) if (t + 256 * i < F * H) w2[t + 256 * i] = v2[i];
+#pragma unroll
+    for (int i = 0; i < N3; ++i) if (t + 256 * i < C2 * C2) wt2[t + 256 * i] = v3[i];
+#pragma unroll
+    for (int i = 0; i < NG1; ++i) if (t + 256 * i < ng1) gw1[t + 256 * i] = g1[i];
+#pragma unroll
+    for (int i = 0; i < NG2; ++i) if (t + 256 * i < ng2) gw2[t + 256 * i] = g2[i];
+    if (t < H) bb1[t] = b1v;
+    if (t < F) bb2[t] = b2v;
+    if (t < C2) bt[t] = btv;
+  }
+  // the next block's weight blocks: We[:, F:2F], We[:, 3F:4F], be, Ws[:, 0:F], bs
+  __shared__ float wet[4 * F * F], weu[4 * F * F], wbe[4 * F], wst[2 * F * F], wbs[2 * F];
+  if (A.We) {
+    constexpr int NE = (4 * F * F + 255) / 256, NS2 = (2 * F * F + 255) / 256;
+    float e1[NE], e2[NE], e3[NS2];
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int x = t + 256 * i, k = x / F, o = x - k * F;
+      e1[i] = x < 4 * F * F ? A.We[(size_t)k * 4 * F + F + o] : 0.f;
+      e2[i] = x < 4 * F * F ? A.We[(size_t)k * 4 * F + 3 * F + o] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NS2; ++i) {
+      const int x = t + 256 * i, k = x / F, o = x - k * F;
+      e3[i] = x < 2 * F * F ? A.Ws[(size_t)k * 2 * F + o] : 0.f;
+    }
+    const float bev = t < 4 * F ? A.be[t] : 0.f, bsv = t < 2 * F ? A.bs[t] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NE; ++i)
+      if (t + 256 * i < 4 * F * F) { wet[t + 256 * i] = e1[i]; weu[t + 256 * i] = e2[i]; }
+#pragma unroll
+    for (int i = 0; i < NS2; ++i)
+      if (t + 256 * i < 2 * F * F) wst[t + 256 * i] = e3[i];
+    if (t < 4 * F) wbe[t] = bev;
+    if (t < 2 * F) wbs[t] = bsv;
+  }
+  __syncthreads();
+  TAIL_STAMP(1)
+  // ---------------------------------------------------------------- phase 1
+  for (int un = blockIdx.x; un < T.nunits; un += gridDim.x) {
+    const int g = un / T.QB, q = un - g * T.QB;
+    const int c0 = q * T.CT, ncl = min(T.CT, NC - c0);
+    const long long nb = (long long)g * NC + c0;
+    // per-class sums of the column partials, in partial order (32 loads of a
+    // thread in flight at once: this is the phase's latency)
+    for (int i = t; i < ncl * C2; i += 256) {
+      const int cl = i / C2, j = i - cl * C2;
+      const float* p = T.cpart + ((size_t)g * T.BPG * NC + c0 + cl) * C2 + j;
+      const size_t bs = (size_t)NC * C2;
+      float s = 0.f;
+      for (int b = 0; b < T.BPG; b += 32) {
+        float v[32];
+#pragma unroll
+        for (int e = 0; e < 32; ++e) v[e] = b + e < T.BPG ? p[(size_t)(b + e) * bs] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 32; ++e) s += v[e];
+      }
+      hs[cl][j] = s;
+      A.hsum[(size_t)j * NT + nb + cl] = s;
+    }
+    TAIL_STAMP(2)
+    for (int i = t; i < ncl * F; i += 256) {
+      const int o = i / ncl, cl = i - o * ncl;
+      xin[cl][o] = A.xt[(size_t)o * NT + nb + cl];
+      xin[cl][3 * F + o] = A.u[(size_t)o * G + g];
+    }
+    // the unit's share of graph g's x_s sums (fibers [f0, f1))
+    {
+      const int f0 = (int)(((long long)NF * q) / T.QB), f1 = (int)(((long long)NF * (q + 1)) / T.QB);
+      float sx[F];
+#pragma unroll
+      for (int o = 0; o < F; ++o) sx[o] = 0.f;
+      for (int f = f0 + t; f < f1; f += 256) {
+#pragma unroll
+        for (int o = 0; o < F; ++o) sx[o] += A.xs[(size_t)o * NS + (size_t)g * NF + f];
+      }
+      const int wv = t >> 6, ln = t & 63;
+#pragma unroll
+      for (int o = 0; o < F; ++o) {
+        const float v = wave_sum(sx[o]);
+        if (ln == 0) red[wv][o] = v;
+      }
+    }
+    __syncthreads();
+    if (t < F) T.xss[(size_t)un * F + t] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    // agg = Wt2 hsum + bscale bt2 (the MLP input's middle block)
+    for (int i = t; i < ncl * C2; i += 256) {
+      const int k = i / ncl, cl = i - k * ncl;
+      float acc = T.bscale * bt[k];
+#pragma unroll
+      for (int j = 0; j < C2; ++j) acc = fmaf(wt2[k * C2 + j], hs[cl][j], acc);
+      xin[cl][F + k] = acc;
+      A.agg[(size_t)k * NT + nb + cl] = acc;
+    }
+    __syncthreads();
+    // node_mlp_2: Z = W1 x + b1, a = lrelu(Z)
+    for (int i = t; i < ncl * H; i += 256) {
+      const int h = i / ncl, cl = i - h * ncl;
+      float z = bb1[h];
+#pragma unroll
+      for (int k = 0; k < K; ++k) z = fmaf(w1[h * K + k], xin[cl][k], z);
+      A.Z[(size_t)h * NT + nb + cl] = z;
+      act[cl][h] = lrelu(z);
+    }
+    __syncthreads();
+    // Yp = W2 a + b2
+    for (int i = t; i < ncl * F; i += 256) {
+      const int o = i / ncl, cl = i - o * ncl;
+      float y = bb2[o];
+#pragma unroll
+      for (int h = 0; h < H; ++h) y = fmaf(w2[o * H + h], act[cl][h], y);
+      A.Yp[(size_t)o * NT + nb + cl] = y;
+      ypl[cl][o] = y;
+    }
+    __syncthreads();
+    // Welford partial of the unit's classes (bn_stats_part's layout) and the
+    // pre-norm sums for the x_t mean
+    if (t < 16) {
+      float* pp = T.part + (size_t)un * PART_LEN;
+      if (t < F) {
+        float mean = 0.f, m2 = 0.f, sum = 0.f;
+        for (int cl = 0; cl < ncl; ++cl) {
+          const float v = ypl[cl][t];
+          const float d = v - mean;
+          mean = fmaf(d, 1.f / (float)(cl + 1), mean);
+          m2 = fmaf(d, v - mean, m2);
+          sum += v;
+        }
+        pp[1 + t] = mean;
+        pp[17 + t] = m2;
+        T.yps[(size_t)un * F + t] = sum;
+      } else {
+        pp[1 + t] = 0.f;
+        pp[17 + t] = 0.f;
+      }
+      if (t == 0) pp[0] = (float)ncl;
+    }
+    __syncthreads();   // (LDS reuse by the next unit)
+  }
+  TAIL_STAMP(3)
+  grid_sync(gridDim.x);
+  TAIL_STAMP(4)
+  // ---------------------------------------------------------------- phase 2
+  __shared__ float cf[4][16];
+  bn_stats_part(T.part, T.nunits, F, (int)NT, A.gamma, A.beta, A.eps, A.rm, A.rv, A.momentum,
+                A.mu, A.var, blockIdx.x == 0, cf);
+  TAIL_STAMP(5)
+  __shared__ float h3[K3], gz[CG_MAXH], vv[F], un3[F], cu[4 * F], zz[F], rs2[2];
+  float* xn = &ypl[0][0];   // [CT_CLS][F + 1]: the normalised x_t of the unit
+  for (int un = blockIdx.x; un < T.nunits; un += gridDim.x) {
+    const int g = un / T.QB, q = un - g * T.QB;
+    const int c0 = q * T.CT, ncl = min(T.CT, NC - c0);
+    const long long nb = (long long)g * NC + c0;
+    for (int i = t; i < ncl * F; i += 256) {
+      const int o = i / ncl, cl = i - o * ncl;
+      const float v = (A.Yp[(size_t)o * NT + nb + cl] - cf[0][o]) * (cf[1][o] * cf[2][o]) + cf[3][o];
+      A.xt_new[(size_t)o * NT + nb + cl] = v;
+      xn[cl * (F + 1) + o] = v;
+    }
+    if (t < F) {
+      float sx = 0.f, sy = 0.f;
+      for (int qq = 0; qq < T.QB; ++qq) {
+        sx += T.xss[(size_t)(g * T.QB + qq) * F + t];
+        sy += T.yps[(size_t)(g * T.QB + qq) * F + t];
+      }
+      const float mx = sx / (float)NF;
+      const float mt = (sy / (float)NC - cf[0][t]) * (cf[1][t] * cf[2][t]) + cf[3][t];
+      h3[t] = A.u[(size_t)t * G + g];
+      h3[F + t] = mx;
+      h3[2 * F + t] = mt;
+      if (q == 0) {
+        A.means[(size_t)t * G + g] = mx;
+        A.means[(size_t)(F + t) * G + g] = mt;
+      }
+    }
+    __syncthreads();
+    // GlobalModel MLP(3F -> gH -> F) of graph g
+    for (int j = t; j < A.gH; j += 256) {
+      float acc = A.gb1[j];
+      for (int k = 0; k < K3; ++k)
+        acc = fmaf(gws ? gw1[j * K3 + k] : A.gW1[(size_t)j * K3 + k], h3[k], acc);
+      gz[j] = acc;
+      if (q == 0) A.gZ[(size_t)j * G + g] = acc;
+    }
+    __syncthreads();
+    if (t < F) {
+      float acc = A.gb2[t];
+      for (int j = 0; j < A.gH; ++j)
+        acc = fmaf(gws ? gw2[t * A.gH + j] : A.gW2[(size_t)t * A.gH + j], lrelu(gz[j]), acc);
+      vv[t] = acc;
+      if (q == 0) A.gV[(size_t)t * G + g] = acc;
+    }
+    __syncthreads();
+    if (t == 0) {   // RMSNorm twice (k_rms2_fwd's arithmetic)
+      if (!A.gw) {
+        for (int c = 0; c < F; ++c) un3[c] = vv[c];
+      } else {
+        float s = 0.f;
+        for (int c = 0; c < F; ++c) s += vv[c] * vv[c];
+        const float a = rsqrtf(s / F + A.reps);
+        float s2 = 0.f;
+        for (int c = 0; c < F; ++c) {
+          const float qv = vv[c] * a * A.gw[c];
+          zz[c] = qv;
+          s2 += qv * qv;
+        }
+        const float b = rsqrtf(s2 / F + A.reps);
+        for (int c = 0; c < F; ++c) un3[c] = zz[c] * b * A.gw[c];
+        rs2[0] = a;
+        rs2[1] = b;
+      }
+    }
+    __syncthreads();
+    if (q == 0) {
+      if (t < F) {
+        A.unew[(size_t)t * G + g] = un3[t];
+        if (A.gw) A.y1[(size_t)t * G + g] = zz[t];
+      }
+      if (A.gw && t == 0) {
+        A.r1[g] = rs2[0];
+        A.r2[g] = rs2[1];
+      }
+    }
+    if (A.We) {
+      if (t < 4 * F) {
+        float acc = wbe[t];
+#pragma unroll
+        for (int o = 0; o < F; ++o) acc = fmaf(weu[t * F + o], un3[o], acc);
+        cu[t] = acc;
+      }
+      __syncthreads();
+      for (int i = t; i < ncl * 4 * F; i += 256) {
+        const int k = i / ncl, cl = i - k * ncl;
+        float acc = cu[k];
+#pragma unroll
+        for (int o = 0; o < F; ++o) acc = fmaf(wet[k * F + o], xn[cl * (F + 1) + o], acc);
+        A.Pt[(size_t)k * NT + nb + cl] = acc;
+      }
+      for (int i = t; i < ncl * 2 * F; i += 256) {
+        const int k = i / ncl, cl = i - k * ncl;
+        float acc = wbs[k];
+#pragma unroll
+        for (int o = 0; o < F; ++o) acc = fmaf(wst[k * F + o], xn[cl * (F + 1) + o], acc);
+        A.Qt[(size_t)k * NT + nb + cl] = acc;
+      }
+    }
+    __syncthreads();   // (LDS reuse by the next unit)
+  }
+  TAIL_STAMP(6)
+}
+
 // ============================================================ backward
 // BatchNorm backward sums per block: Sg[c] = sum dY, Sgx[c] = sum dY * xhat.
 constexpr int SUM_LEN = 32;
@@ -741,17 +1127,36 @@ __global__ __launch_bounds__(256) void k_bn_sums_part(const float* __restrict__ 
         ((scratch[t] + scratch[32 + t]) + scratch[64 + t]) + scratch[96 + t];
 }
 
-// Row k of the input gradient at one lane's node n (k per lane: the block
-// and its add flag are selected per lane)
-__device__ __forceinline__ void out_row_lane(const OutSegs& S, int k, int n, int N, float v) {
-  float* p = S.p[0];
-  int kb = 0, add = S.add[0];
-  if (k >= S.k0[1]) { p = S.p[1]; kb = S.k0[1]; add = S.add[1]; }
-  if (k >= S.k0[2]) { p = S.p[2]; kb = S.k0[2]; add = S.add[2]; }
-  if (k >= S.k0[3]) { p = S.p[3]; kb = S.k0[3]; add = S.add[3]; }
-  if (!p) return;
-  float* q = p + (size_t)(k - kb) * N + n;
-  *q = add ? *q + v : v;
+// Rows [kb, ke) of a chunk's input gradient, staged in LDS (row k at
+// X + (k - kx) * XS_LD, the chunk's 64 nodes), to their output blocks: lane
+// (q, j) takes rows kb + 16 i + 4 wu + q, nodes n0 + 4 j .. + 3 (R >= the
+// rows' 16-row rounds).  Every add block's old values are loaded before the
+// first store, so a wave waits once per call, not once per row.
+template <int R>
+__device__ __forceinline__ void store_rows(const RowOut* tab, const float* X, int kx, int kb,
+                                           int ke, int n0, int N, int wu, int lane) {
+  const int q = lane >> 4, j = lane & 15, nb = n0 + 4 * j;
+  float* p[R];
+  bool ad[R];
+  float o[R][4];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int r = kb + 16 * i + 4 * wu + q;
+    const RowOut d = r < ke ? tab[r] : RowOut{nullptr, 0, 0};
+    p[i] = d.p;
+    ad[i] = d.p && d.add;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[i][e] = (ad[i] && nb + e < N) ? d.p[nb + e] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    if (!p[i]) continue;
+    const int r = kb + 16 * i + 4 * wu + q;
+    const floatx4 v = *reinterpret_cast<const floatx4*>(X + (r - kx) * XS_LD + 4 * j);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (nb + e < N) p[i][nb + e] = ad[i] ? o[i][e] + v[e] : v[e];
+  }
 }
 
 // RS (the wide MLPs, M >= 5): no LDS staging of the input gradient -- each
@@ -794,9 +1199,14 @@ __global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_bwd(
 #pragma unroll
     for (int i = 0; i < M * M; ++i) t1[t + 256 * i] = v[i];
   }
+  __shared__ RowOut rout[16 * M];   // the input-gradient rows' outputs
+  if (want_dx) build_out_rows(outs, K, N, rout);
   const bool bn = spart != nullptr;
   if (bn) {
-    __shared__ float ss[16][SUM_LEN];
+    // (the merge's scratch is the chunk buffer DXs, free until the chunk loop:
+    // a static array would push the RS form's LDS past the 80 KB of two
+    // blocks per CU)
+    float (*ss)[SUM_LEN] = reinterpret_cast<float (*)[SUM_LEN]>(DXs);
     const int c = t & 31, u = t >> 5;  // 8 subsets of the partial list per sum
     float v[32];  // nsp <= 256: every load in flight, then a fixed-order sum
 #pragma unroll
@@ -942,12 +1352,7 @@ __global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_bwd(
             DXs[(16 * i + 4 * kq + r) * XS_LD + wave * 16 + col] = dx[i][r];
         }
         __syncthreads();
-        const int n2 = ch * 64 + lane;
-        const int kend = min(K, 16 * (g0 + GN));
-        if (n2 < N) {
-          for (int k = 16 * g0 + wu; k < kend; k += 4)
-            out_row(outs, k, n2, N, DXs[(k - 16 * g0) * XS_LD + lane]);
-        }
+        store_rows<4>(rout, DXs, 16 * g0, 16 * g0, min(K, 16 * (g0 + GN)), ch * 64, N, wu, lane);
       }
     } else if (want_dx) {
       __syncthreads();                             // previous chunk's stores from DXs done
@@ -982,12 +1387,7 @@ __global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_bwd(
         }
       }
       __syncthreads();
-      // rows wu, wu + 4, ...: one coalesced 256-byte row per wave-instruction,
-      // the output block (and its add flag) wave-uniform
-      const int n2 = ch * 64 + lane;
-      if (n2 < N) {
-        for (int k = wu; k < K; k += 4) out_row(outs, k, n2, N, DXs[k * XS_LD + lane]);
-      }
+      store_rows<M>(rout, DXs, 0, 0, K, ch * 64, N, wu, lane);
     }
   }
 }
@@ -1055,11 +1455,19 @@ int cu_count() {
   }();
   return n;
 }
+// lds: the block's whole LDS, dynamic + the kernel's static arrays
 int grid_for(int N, int m, size_t lds) {
   (void)m;
   const int nch = (N + 63) / 64;
   const int per_cu = (lds <= 80 * 1024) ? 2 : 1;   // (160 KB of LDS per CU)
   return std::max(1, std::min(nch, cu_count() * per_cu));
+}
+// static LDS of a kernel (its __shared__ arrays), read once per instantiation
+template <class K>
+size_t static_lds(K* kernel) {
+  hipFuncAttributes a{};
+  if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(kernel)) != hipSuccess) return 0;
+  return a.sharedSizeBytes;
 }
 
 // pfsgnn_seg list -> InSegs (blocks must be contiguous in the weight columns)
@@ -1107,13 +1515,14 @@ int mlp_fwd_launch(const InSegs& S, int K, int N, const float* W1, int ldw1, int
   if (m > 0 && fwd_rs(m)) m = tiles_for(S.Kp, H);   // (RS: the padded K must fit the tiles)
   if (m <= 0 || (fwd_rs(m) && 16 * m < S.Kp)) return -2;
   const size_t lds = fwd_lds(m);
-  const int grid = grid_for(N, m, lds);
-  *grid_out = grid;
   const bool rs = fwd_rs(m);
   return with_tiles(m, [&](auto mc) {
     constexpr int MM = decltype(mc)::value;
     auto launch = [&](auto rsc) {
       constexpr bool RS = decltype(rsc)::value && MM >= 5;
+      static const size_t stat = static_lds(&k_mlp_fwd<MM, RS>);
+      const int grid = grid_for(N, m, lds + stat);
+      *grid_out = grid;
       static size_t attr = 0;  // dynamic LDS above the 64 KB default must be opted into
       if (lds > 65536 && attr < lds) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mlp_fwd<MM, RS>),
@@ -1129,6 +1538,61 @@ int mlp_fwd_launch(const InSegs& S, int K, int N, const float* W1, int ldw1, int
   });
 }
 }  // namespace
+
+namespace pf {
+// the class launch of pfsgnn_target_block_fwd (k_class_tail_fwd): scratch =
+// tail_ws_floats(...) floats of workspace
+// classes per unit: the smallest of 8, 16, 32 with at most 512 units (one
+// workgroup per CU or fewer, each over its units); 0: too many graphs
+static int tail_ct(int G, int NC) {
+  for (int ct = 8; ct <= CT_CLS; ct *= 2)
+    if ((long long)G * ((NC + ct - 1) / ct) <= 512) return ct;
+  return 0;
+}
+size_t tail_ws_floats(int G, int NC, int F) {
+  const int ct = tail_ct(G, NC);
+  const size_t nu = (size_t)G * ((NC + (ct ? ct : CT_CLS) - 1) / (ct ? ct : CT_CLS));
+  return nu * PART_LEN + 2 * nu * F + 64;
+}
+int class_tail_fwd(const pfsgnn_block_tail& a, const float* cpart, int BPG, float bscale,
+                   float* scratch, hipStream_t st) {
+  const char* where = "pfsgnn_target_block_fwd";
+  TailArgs T{};
+  T.a = a;
+  T.cpart = cpart;
+  T.BPG = BPG;
+  T.CT = tail_ct(a.G, a.NC);
+  PF_REQUIRE(T.CT > 0, where, "more than 512 class units (G * ceil(NC / 32))");
+  T.QB = (a.NC + T.CT - 1) / T.CT;
+  T.nunits = a.G * T.QB;
+  T.bscale = bscale;
+  T.part = scratch;
+  T.xss = T.part + (size_t)T.nunits * PART_LEN;
+  T.yps = T.xss + (size_t)T.nunits * a.F;
+  const int grid = std::min(T.nunits, cu_count());
+  switch (a.F) {
+    case 8: hipLaunchKernelGGL(k_class_tail_fwd<8>, dim3(grid), dim3(256), 0, st, T); break;
+    case 10: hipLaunchKernelGGL(k_class_tail_fwd<10>, dim3(grid), dim3(256), 0, st, T); break;
+    case 16: hipLaunchKernelGGL(k_class_tail_fwd<16>, dim3(grid), dim3(256), 0, st, T); break;
+    default: return pf::fail(where, "Fdim must be 8, 10 or 16");
+  }
+  return 0;
+}
+}  // namespace pf
+
+#ifdef PF_TAIL_STAMPS
+extern "C" int pfsgnn_debug_tail_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_tail_stamps), sizeof(unsigned long long) * 512 * 8) ==
+                 hipSuccess ? 0 : -1;
+}
+#endif
+
+extern "C" int pfsgnn_sync_faults(unsigned* n) {
+  PF_REQUIRE(n, "pfsgnn_sync_faults", "null");
+  if (hipMemcpyFromSymbol(n, HIP_SYMBOL(pf_sync_fault_count), sizeof(unsigned)) != hipSuccess)
+    return pf::fail("pfsgnn_sync_faults", "hipMemcpyFromSymbol");
+  return 0;
+}
 
 extern "C" int pfsgnn_mlp_fwd(const pfsgnn_seg* segs, int nseg, int N, const float* W1, int ldw1,
                               int H, const float* b1, const float* W2, int O, const float* b2,
@@ -1267,13 +1731,14 @@ extern "C" int pfsgnn_mlp_bwd(const float* dY, int N, const float* Yp, const flo
                        spart);
   }
   const size_t lds = bwd_lds(m);
-  const int grid = grid_for(N, m, lds);
   const int want_dx = nout > 0 ? 1 : 0;
   const bool rs = bwd_rs(m);
   const int rc = with_tiles(m, [&](auto mc) {
     constexpr int MM = decltype(mc)::value;
     auto launch = [&](auto rsc) {
       constexpr bool RS = decltype(rsc)::value && MM >= 5;
+      static const size_t stat = static_lds(&k_mlp_bwd<MM, RS>);
+      const int grid = grid_for(N, m, lds + stat);
       static size_t attr = 0;  // dynamic LDS above the 64 KB default must be opted into
       if (lds > 65536 && attr < lds) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mlp_bwd<MM, RS>),

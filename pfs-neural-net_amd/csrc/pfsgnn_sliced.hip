@@ -846,7 +846,9 @@ __global__ __launch_bounds__(256, 2) void ksl_edge_mlp_bwd(
   __shared__ float scratch[4 * SCR];
   CROWS_DECL(H, ptl, PtS, sl_dyn)             // [NC][CP]
   float* acc = sl_dyn + NC * CROWS_FLOATS(H);  // [4][NC][H + 1]
+#ifndef SL_NO_ACC_LDS   // (timing experiment only: no accumulators, SL_NO_ACC too)
   acc_zero(acc, 4 * NC * Acc<H>::S);
+#endif
   float* wacc = acc + wave * NC * Acc<H>::S;
   __shared__ int owners[4][pfm::SL_MAX_NC];
   int* own = owners[wave];
@@ -946,7 +948,9 @@ __global__ __launch_bounds__(256, 2) void ksl_edge_mlp_bwd(
         if (h >= 0) GzEs[(size_t)ks * H * NS + (size_t)h * NS + n] = accF[tt][r];
       }
   }
+#ifndef SL_NO_ACC_LDS
   acc_flush<H>(acc, NC, partCol, colbase);
+#endif
   block_partial(accW2, scratch, F * (H + 1), [&](int a, int s, int jj) {
     const int o = GM<F>::mrow(0, s), h = GM<H>::mrow(a, jj);
     return (o >= 0 && h >= 0) ? o * (H + 1) + h : -1;
@@ -1166,7 +1170,11 @@ int sl_edge_mlp_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* g_t
                     const float* xe, const float* xsc, const float* xsh, const float* Ps,
                     const float* PtS, const float* W1, const float* W2, float* gxe, float* gs,
                     float* pW2, float* pW1, float* pCol, float* tabs, int prec, hipStream_t st) {
+#ifndef SL_NO_ACC_LDS
   const size_t lds = tab_lds(geo, 4 * F) + (size_t)geo.NC * 4 * (4 * F + 1) * sizeof(float);
+#else
+  const size_t lds = tab_lds(geo, 4 * F);
+#endif
   if (kGTab) {
     if (int rc = rows_table(4 * F, PtS, geo.NT, tabs, st)) return rc;
     PtS = tabs;

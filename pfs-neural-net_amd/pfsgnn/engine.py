@@ -394,6 +394,9 @@ class Engine:
         # the LeakyReLU mask of the per-edge layer, kept for the backward (MFMA
         # path; None where the backward recomputes it)
         tmask = be.tmask(d) if self.training and hasattr(be, "tmask") else None
+        if glob is not None and d.sp is None and hasattr(be, "target_block_fwd") and \
+                d.G * -(-d.NC // 32) <= 512 and os.environ.get("PFSGNN_CLASS_TAIL", "1") != "0":
+            return self._target_block_fwd(P, BN, d, pre, xs, xt, xe3, u, Rs, tmask, glob)
         if d.sp is None:
             # the second Linear after the per-class sum, in the op's reduction epilogue
             hsum, agg = be.target_fwd(d, xe3[0], xe3[1], xe3[2], Rs, Wt1,
@@ -425,6 +428,33 @@ class Engine:
                                  self._bn_args(P, BN, pre + "norm."), xs, d.NF, u,
                                  P[pg + "0.weight"], P[pg + "0.bias"], P[pg + "2.weight"],
                                  P[pg + "2.bias"], w, self._rms_eps(u), nxt)
+        st.update(sT=(hT, r["Z"], (r["Yp"], r["mu"], r["var"], pre + "norm.")), xt_new=r["xt"])
+        st["su"] = dict(sU=([(u, 0, False), (r["means"], F, False)], r["gZ"], None), v=r["gV"],
+                        rms=r["rms"], u_new=r["u"], fused=True)
+        st["parts_t"] = (r["Pt"], r["Qt"])
+        return st
+
+    def _target_block_fwd(self, P, BN, d, pre, xs, xt, xe3, u, Rs, tmask, glob):
+        """target_fwd's fused form on a complete batch: TModel's per-edge layer,
+        then its class side, node_mlp_2 + BatchNorm, the GlobalModel and the next
+        block's class parts in one launch (pfsgnn_target_block_fwd)."""
+        be, F = self.be, self.F
+        pg, pnext = glob
+        m2 = pre + "node_mlp_2."
+        nxt = None
+        if pnext is not None:
+            pe, ps = pnext + "edge_model.", pnext + "s_model."
+            nxt = (P[pe + "0.weight"], P[pe + "0.bias"], P[ps + "node_mlp_1.0.weight"],
+                   P[ps + "node_mlp_1.0.bias"])
+        r = be.target_block_fwd(d, xe3[0], xe3[1], xe3[2], Rs, P[pre + "node_mlp_1.0.weight"],
+                                P[pre + "node_mlp_1.2.weight"], P[pre + "node_mlp_1.2.bias"],
+                                tmask, xt, u, P[m2 + "0.weight"], P[m2 + "0.bias"],
+                                P[m2 + "2.weight"], P[m2 + "2.bias"],
+                                self._bn_args(P, BN, pre + "norm."), xs, P[pg + "0.weight"],
+                                P[pg + "0.bias"], P[pg + "2.weight"], P[pg + "2.bias"],
+                                P[pg + "norm.weight"], self._rms_eps(u), nxt)
+        hT = [(xt, 0, False), (r["agg"], F, False), (u, 3 * F, True)]
+        st = dict(xs=xs, xt=xt, xe3=xe3, u=u, Rs=Rs, hsum=r["hsum"], tmask=tmask)
         st.update(sT=(hT, r["Z"], (r["Yp"], r["mu"], r["var"], pre + "norm.")), xt_new=r["xt"])
         st["su"] = dict(sU=([(u, 0, False), (r["means"], F, False)], r["gZ"], None), v=r["gV"],
                         rms=r["rms"], u_new=r["u"], fused=True)

@@ -107,6 +107,23 @@ class LinMap(ctypes.Structure):
 
 LINMP = ctypes.POINTER(LinMap)
 
+
+def _ptrs(*names):
+    return [(n, ctypes.c_void_p) for n in names]
+
+
+class BlockTail(ctypes.Structure):
+    """pfsgnn_block_tail (include/pfsgnn.h): a block tail on a complete batch."""
+    _fields_ = ([("G", I), ("NF", I), ("NC", I), ("F", I)]
+                + _ptrs("y", "sc", "sh", "Rs", "Wt1", "Wt2", "bt2", "tmask", "hsum", "agg",
+                        "xt", "u", "W1", "b1", "W2", "b2", "gamma", "beta",
+                        "Z", "Yp", "rm", "rv", "xt_new", "mu", "var")
+                + [("momentum", FL), ("eps", FL)]
+                + _ptrs("xs", "gW1", "gb1", "gW2", "gb2", "gw")
+                + [("gH", I), ("reps", FL)]
+                + _ptrs("means", "gZ", "gV", "unew", "y1", "r1", "r2",
+                        "We", "be", "Ws", "bs", "Pt", "Qt"))
+
 _SIGS = {
     "pfsgnn_version": ([], ctypes.c_char_p),
     "pfsgnn_last_error": ([], ctypes.c_char_p),
@@ -197,6 +214,9 @@ _SIGS = {
     "pfsgnn_adam": ([P, P, P, P, LL, I, P, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                      ctypes.c_double, ctypes.c_double, P, P], I),
     "pfsgnn_sliced_max_nc": ([I, ctypes.POINTER(ctypes.c_int)], I),
+    "pfsgnn_target_block_fwd": ([ctypes.POINTER(BlockTail), P, SZ, P], I),
+    "pfsgnn_sync_faults": ([ctypes.POINTER(ctypes.c_uint)], I),
+    "pfsgnn_block_tail_bytes": ([], SZ),
     "pfsgnn_sliced_plan_ws_bytes": ([I, I], SZ),
     "pfsgnn_sliced_plan": ([P, I, I, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_sliced_fill": ([P, P, P, P, LL, I, I, P, P, LL, I, P, P, P, P], I),
@@ -641,6 +661,55 @@ class HipBackend:
               bt.data_ptr(), _ptr(rm), _ptr(rv), float(mom), float(eps), Y.data_ptr(),
               mu.data_ptr(), var.data_ptr(), em, len(epi), ws, wsb, _stream())
         return Y, Z, Yp, mu, var, outs
+
+    def target_block_fwd(self, d, y, sc, sh, Rs, Wt1, Wt2, bt2, tmask, xt, u, W1, b1, W2, b2,
+                         bn, xs, gW1, gb1, gW2, gb2, gw, reps, nxt=None):
+        """target_fwd (TModel's per-edge layer) + target_global_fwd on a complete
+        batch, the class side in one launch (pfsgnn_target_block_fwd).  -> dict
+        with target_global_fwd's keys plus hsum and agg."""
+        F, G, NC, NT = d.F, d.G, d.NC, d.NT
+        H = W1.shape[0]
+        assert W1.shape == (4 * F, 4 * F) and W2.shape == (F, 4 * F) and Wt2.shape == (2 * F, 2 * F)
+        self._chk(y, sc, sh, Rs, Wt1, Wt2, bt2, xt, u, W1, b1, W2, b2, xs, gW1, gb1, gW2, gb2, gw)
+        g, bt, rm, rv, mom, eps = bn
+        self._chk(g, bt, rm, rv)
+        gH = gW1.shape[0]
+        r = dict(hsum=self.empty(2 * F, NT), agg=self.empty(2 * F, NT), Z=self.empty(H, NT),
+                 Yp=self.empty(F, NT), xt=self.empty(F, NT), mu=self.empty(F), var=self.empty(F),
+                 means=self.empty(2 * F, G), gZ=self.empty(gH, G), gV=self.empty(F, G),
+                 u=self.empty(F, G))
+        rms = (self.empty(F, G), self.empty(G), self.empty(G)) if gw is not None else None
+        y1, r1, r2 = rms if rms is not None else (None, None, None)
+        We = be_ = Ws = bs = Pt = Qt = None
+        if nxt is not None:
+            We, be_, Ws, bs = nxt
+            self._chk(We, be_, Ws, bs)
+            assert We.shape == (4 * F, 4 * F) and Ws.shape == (2 * F, 2 * F)
+            Pt, Qt = self.empty(4 * F, NT), self.empty(2 * F, NT)
+        a = BlockTail(G=G, NF=d.NF, NC=NC, F=F, y=y.data_ptr(), sc=_ptr(sc), sh=_ptr(sh),
+                      Rs=Rs.data_ptr(), Wt1=Wt1.data_ptr(), Wt2=Wt2.data_ptr(),
+                      bt2=bt2.data_ptr(), tmask=_ptr(tmask), hsum=r["hsum"].data_ptr(),
+                      agg=r["agg"].data_ptr(), xt=xt.data_ptr(), u=u.data_ptr(),
+                      W1=W1.data_ptr(), b1=b1.data_ptr(), W2=W2.data_ptr(), b2=b2.data_ptr(),
+                      gamma=g.data_ptr(), beta=bt.data_ptr(), Z=r["Z"].data_ptr(),
+                      Yp=r["Yp"].data_ptr(), rm=_ptr(rm), rv=_ptr(rv), xt_new=r["xt"].data_ptr(),
+                      mu=r["mu"].data_ptr(), var=r["var"].data_ptr(), momentum=float(mom),
+                      eps=float(eps), xs=xs.data_ptr(), gW1=gW1.data_ptr(), gb1=gb1.data_ptr(),
+                      gW2=gW2.data_ptr(), gb2=gb2.data_ptr(), gw=_ptr(gw), gH=gH,
+                      reps=float(reps), means=r["means"].data_ptr(), gZ=r["gZ"].data_ptr(),
+                      gV=r["gV"].data_ptr(), unew=r["u"].data_ptr(), y1=_ptr(y1), r1=_ptr(r1),
+                      r2=_ptr(r2), We=_ptr(We), be=_ptr(be_), Ws=_ptr(Ws), bs=_ptr(bs),
+                      Pt=_ptr(Pt), Qt=_ptr(Qt))
+        ws, wsb = self._wsargs(d)
+        _call("pfsgnn_target_block_fwd", ctypes.byref(a), ws, wsb, _stream())
+        r["rms"], r["Pt"], r["Qt"] = rms, Pt, Qt
+        return r
+
+    def sync_faults(self):
+        """Device-wide barrier time-outs since load (pfsgnn_sync_faults; 0 when healthy)."""
+        n = ctypes.c_uint(0)
+        _call("pfsgnn_sync_faults", ctypes.byref(n))
+        return n.value
 
     def target_global_fwd(self, segs, G, NC, W1, b1, W2, b2, bn, xs, NF, u, gW1, gb1, gW2, gb2,
                           gw, reps, nxt=None):

@@ -42,6 +42,15 @@ def test_library_is_gfx950_code_object(lib):
     assert b"amdgcn-amd-amdhsa--gfx950" in blob or b"gfx950" in blob
 
 
+def test_block_tail_struct_layout_matches(lib):
+    """native.BlockTail mirrors pfsgnn_block_tail field for field: same size, and
+    the last field where C puts it (every pointer is 8-byte aligned)."""
+    import ctypes
+    from pfsgnn import native
+    assert lib.pfsgnn_block_tail_bytes() == ctypes.sizeof(native.BlockTail)
+    assert native.BlockTail.Qt.offset == ctypes.sizeof(native.BlockTail) - 8
+
+
 def test_workspace_query_is_host_only(lib):
     b = lib.pfsgnn_workspace_bytes(16, 2394, 128, 10)
     assert 1 << 20 < b < 1 << 31
