@@ -806,10 +806,11 @@ __global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
   // load -> store loop pays one round trip per element)
   const bool gws = A.gH * K3 <= CG_GW1;
   __shared__ float gw1[CG_GW1], gw2[F * CG_MAXH];
+  constexpr int N1 = (H * K + 255) / 256, N2 = (F * H + 255) / 256, N3 = (C2 * C2 + 255) / 256;
+  constexpr int NG1 = (CG_GW1 + 255) / 256, NG2 = (F * CG_MAXH + 255) / 256;
+  float v1[N1], v2[N2], v3[N3], g1[NG1], g2[NG2];
+  float b1v, b2v, btv;
   {
-    constexpr int N1 = (H * K + 255) / 256, N2 = (F * H + 255) / 256, N3 = (C2 * C2 + 255) / 256;
-    constexpr int NG1 = (CG_GW1 + 255) / 256, NG2 = (F * CG_MAXH + 255) / 256;
-    float v1[N1], v2[N2], v3[N3], g1[NG1], g2[NG2];
     const int ng1 = gws ? A.gH * K3 : 0, ng2 = gws ? F * A.gH : 0;
 #pragma unroll
     for (int i = 0; i < N1; ++i) v1[i] = t + 256 * i < H * K ? A.W1[t + 256 * i] : 0.f;
@@ -821,8 +822,12 @@ __global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
     for (int i = 0; i < NG1; ++i) g1[i] = t + 256 * i < ng1 ? A.gW1[t + 256 * i] : 0.f;
 #pragma unroll
     for (int i = 0; i < NG2; ++i) g2[i] = t + 256 * i < ng2 ? A.gW2[t + 256 * i] : 0.f;
-    const float b1v = t < H ? A.b1[t] : 0.f, b2v = t < F ? A.b2[t] : 0.f,
-                btv = t < C2 ? A.bt2[t] : 0.f;
+    b1v = t < H ? A.b1[t] : 0.f;
+    b2v = t < F ? A.b2[t] : 0.f;
+    btv = t < C2 ? A.bt2[t] : 0.f;
+  }
+  {
+    const int ng1 = gws ? A.gH * K3 : 0, ng2 = gws ? F * A.gH : 0;
 #pragma unroll
     for (int i = 0; i < N1; ++i) if (t + 256 * i < H * K) w1[t + 256 * i] = v1[i];
 #pragma unroll
@@ -837,6 +842,7 @@ __global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
     if (t < F) bb2[t] = b2v;
     if (t < C2) bt[t] = btv;
   }
+  __syncthreads();
   // the next block's weight blocks: We[:, F:2F], We[:, 3F:4F], be, Ws[:, 0:F], bs
   __shared__ float wet[4 * F * F], weu[4 * F * F], wbe[4 * F], wst[2 * F * F], wbs[2 * F];
   if (A.We) {
@@ -863,7 +869,6 @@ __global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
     if (t < 4 * F) wbe[t] = bev;
     if (t < 2 * F) wbs[t] = bsv;
   }
-  __syncthreads();
   TAIL_STAMP(1)
   // ---------------------------------------------------------------- phase 1
   for (int un = blockIdx.x; un < T.nunits; un += gridDim.x) {
@@ -1545,7 +1550,12 @@ namespace pf {
 // classes per unit: the smallest of 8, 16, 32 with at most 512 units (one
 // workgroup per CU or fewer, each over its units); 0: too many graphs
 static int tail_ct(int G, int NC) {
-  for (int ct = 8; ct <= CT_CLS; ct *= 2)
+  static const int ct0 = [] {   // tuning knob PFSGNN_TAIL_CT: the smallest unit tried
+    const char* e = getenv("PFSGNN_TAIL_CT");
+    const int v = e ? atoi(e) : 16;   // (measured: 16 -- r04u_tail_ct.txt)
+    return v == 8 || v == 16 || v == 32 ? v : 16;
+  }();
+  for (int ct = ct0; ct <= CT_CLS; ct *= 2)
     if ((long long)G * ((NC + ct - 1) / ct) <= 512) return ct;
   return 0;
 }

@@ -46,4 +46,11 @@ for i, n in enumerate(names):
     print(f"  {n:22s} {int(v.min()):8d} {int(np.median(v)):8d} {int(v.max()):8d}")
 v = st[:, 6] - st[:, 0]
 print(f"  {'total':22s} {int(v.min()):8d} {int(np.median(v)):8d} {int(v.max()):8d}")
+# within one XCD (workgroups b with the same b % 8 share a clock): spread of
+# the starts, the barrier arrivals and the barrier exits
+for x in range(2):
+    sub = st[x::8]
+    for i, n in ((0, "start"), (3, "arrive"), (4, "exit")):
+        v = sub[:, i] - sub[:, 0].min()
+        print(f"  xcd {x} {n:7s} min {int(v.min()):7d} median {int(np.median(v)):7d} max {int(v.max()):7d}")
 print("sync faults:", native.HipBackend().sync_faults())
