@@ -607,16 +607,11 @@ int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, const float*
  * g_tot = Ws1e^T g_zs + [Wt1e^T g_zt] + [g_next]; GzS per class;
  * dWs1[:,F:2F], dWs2, dbs2 accumulated; Sg/Sgx = sums of g_tot, g_tot*xhat
  * (xhat = (y-mu1)*inv1) when mu1 != NULL.  Rs/Wt1/g_hsum may be NULL.
- * Optional g_xt += Ws1[:,0:F]^T GzS (x_t[tgt] input gradient, reduction epilogue).
- * Moment coefficients: coef [4][2F][NS] (pfsgnn_moment_coef), or -- gst != NULL,
- * coef NULL -- computed inside the kernel from mean = the whole moment tensor
- * mom [4][2F][NS] and gst [4][2F][NS] = d loss / d [mean, std, skew, kurt]
- * (pfsgnn_moment_coef's arithmetic with NC messages per fiber), which spares
- * its launch. */
+ * Optional g_xt += Ws1[:,0:F]^T GzS (x_t[tgt] input gradient, reduction epilogue). */
 int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                       const float* sh, const float* Qt, const float* Ws1, const float* Ws2,
-                      const float* bs2, const float* mean, const float* coef, const float* gst,
-                      const float* Rs, const float* Wt1, const float* g_hsum, const float* g_next,
+                      const float* bs2, const float* mean, const float* coef, const float* Rs,
+                      const float* Wt1, const float* g_hsum, const float* g_next,
                       const float* mu1, const float* inv1, float* g_tot, float* GzS,
                       float* dWs1, float* dWs2, float* dbs2, float* Sg, float* Sgx,
                       float* g_xt, const unsigned char* tmask, void* ws, size_t ws_bytes,
@@ -627,8 +622,8 @@ int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, const float*
  * variance; n = E) */
 int pfsgnn_source_bwd_bn(int G, int NF, int NC, int F, const float* y, const float* sc,
                          const float* sh, const float* Qt, const float* Ws1, const float* Ws2,
-                         const float* bs2, const float* mean, const float* coef, const float* gst,
-                         const float* Rs, const float* Wt1, const float* g_hsum, const float* g_next,
+                         const float* bs2, const float* mean, const float* coef, const float* Rs,
+                         const float* Wt1, const float* g_hsum, const float* g_next,
                          const float* mu1, const float* inv1, const float* var1,
                          const float* gamma, long long n, float eps, float* g_tot, float* GzS,
                          float* dWs1, float* dWs2, float* dbs2, float* alpha, float* gam0,
@@ -680,11 +675,10 @@ int pfsgnn_sl_target_bwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F
                          const float* sc, const float* sh, const float* Rs, const float* Wt1,
                          const float* g_hsum, float* GzT, float* dWt1, float* gxe, float* g_xs,
                          const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream);
-/* (gst: as pfsgnn_source_bwd's; the sliced ops take coef and refuse gst) */
 int pfsgnn_sl_source_bwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F, const float* y,
                          const float* sc, const float* sh, const float* Qt, const float* Ws1,
                          const float* Ws2, const float* bs2, const float* mean,
-                         const float* coef, const float* gst, const float* Rs, const float* Wt1,
+                         const float* coef, const float* Rs, const float* Wt1,
                          const float* g_hsum, const float* g_next, const float* mu1,
                          const float* inv1, float* g_tot, float* GzS, float* dWs1, float* dWs2,
                          float* dbs2, float* Sg, float* Sgx, float* g_xt,
@@ -692,10 +686,9 @@ int pfsgnn_sl_source_bwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F
 int pfsgnn_sl_source_bwd_bn(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
                             const float* y, const float* sc, const float* sh, const float* Qt,
                             const float* Ws1, const float* Ws2, const float* bs2,
-                            const float* mean, const float* coef, const float* gst,
-                            const float* Rs, const float* Wt1, const float* g_hsum,
-                            const float* g_next, const float* mu1, const float* inv1,
-                            const float* var1,
+                            const float* mean, const float* coef, const float* Rs,
+                            const float* Wt1, const float* g_hsum, const float* g_next,
+                            const float* mu1, const float* inv1, const float* var1,
                             const float* gamma, long long n, float eps, float* g_tot, float* GzS,
                             float* dWs1, float* dWs2, float* dbs2, float* alpha, float* gam0,
                             float* gam1, float* dgamma, float* dbeta, float* g_xt,

@@ -1981,7 +1981,7 @@ __global__ __launch_bounds__(256) void k_bn2_coef_columns_lin(const float* __res
 static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
                            const float* y, const float* sc, const float* sh, const float* Qt,
                            const float* Ws1, const float* Ws2, const float* bs2, const float* mean,
-                           const float* coef, const float* gst, const float* Rs, const float* Wt1,
+                           const float* coef, const float* Rs, const float* Wt1,
                            const float* g_hsum, const float* g_next, const float* mu1,
                            const float* inv1, float* g_tot, float* GzS, float* dWs1, float* dWs2,
                            float* dbs2, float* Sg, float* Sgx, const Bn2Bwd* bb, float* g_xt,
@@ -1990,23 +1990,21 @@ static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
 extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                                  const float* sh, const float* Qt, const float* Ws1,
                                  const float* Ws2, const float* bs2, const float* mean,
-                                 const float* coef, const float* gst, const float* Rs,
-                                 const float* Wt1,
+                                 const float* coef, const float* Rs, const float* Wt1,
                                  const float* g_hsum, const float* g_next, const float* mu1,
                                  const float* inv1, float* g_tot, float* GzS, float* dWs1,
                                  float* dWs2, float* dbs2, float* Sg, float* Sgx, float* g_xt,
                                  const unsigned char* tmask, void* ws, size_t ws_bytes,
                                  void* stream) {
-  return source_bwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, gst, Rs,
-                         Wt1, g_hsum, g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, Sg, Sgx,
-                         nullptr, g_xt, tmask, ws, ws_bytes, stream);
+  return source_bwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+                         g_hsum, g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, Sg, Sgx, nullptr,
+                         g_xt, tmask, ws, ws_bytes, stream);
 }
 
 extern "C" int pfsgnn_source_bwd_bn(int G, int NF, int NC, int F, const float* y, const float* sc,
                                     const float* sh, const float* Qt, const float* Ws1,
                                     const float* Ws2, const float* bs2, const float* mean,
-                                    const float* coef, const float* gst, const float* Rs,
-                                    const float* Wt1,
+                                    const float* coef, const float* Rs, const float* Wt1,
                                     const float* g_hsum, const float* g_next, const float* mu1,
                                     const float* inv1, const float* var1, const float* gamma,
                                     long long n, float eps, float* g_tot, float* GzS, float* dWs1,
@@ -2017,23 +2015,23 @@ extern "C" int pfsgnn_source_bwd_bn(int G, int NF, int NC, int F, const float* y
   PF_REQUIRE(mu1 && inv1 && var1 && gamma && n > 0 && alpha && gam0 && gam1 && dgamma && dbeta,
              "pfsgnn_source_bwd_bn", "null");
   const Bn2Bwd bb{gamma, mu1, var1, n, eps, alpha, gam0, gam1, dgamma, dbeta};
-  return source_bwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, gst, Rs,
-                         Wt1, g_hsum, g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, nullptr,
-                         nullptr, &bb, g_xt, tmask, ws, ws_bytes, stream);
+  return source_bwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+                         g_hsum, g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, nullptr, nullptr,
+                         &bb, g_xt, tmask, ws, ws_bytes, stream);
 }
 
 extern "C" int pfsgnn_sl_source_bwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
                                     const float* y, const float* sc, const float* sh,
                                     const float* Qt, const float* Ws1, const float* Ws2,
                                     const float* bs2, const float* mean, const float* coef,
-                                    const float* gst, const float* Rs, const float* Wt1,
-                                    const float* g_hsum, const float* g_next, const float* mu1,
-                                    const float* inv1, float* g_tot, float* GzS, float* dWs1,
-                                    float* dWs2, float* dbs2, float* Sg, float* Sgx, float* g_xt,
+                                    const float* Rs, const float* Wt1, const float* g_hsum,
+                                    const float* g_next, const float* mu1, const float* inv1,
+                                    float* g_tot, float* GzS, float* dWs1, float* dWs2,
+                                    float* dbs2, float* Sg, float* Sgx, float* g_xt,
                                     const unsigned char* tmask, void* ws, size_t ws_bytes,
                                     void* stream) {
   PF_REQUIRE(sl, "pfsgnn_sl_source_bwd", "null layout");
-  return source_bwd_impl(sl, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, gst, Rs, Wt1,
+  return source_bwd_impl(sl, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
                          g_hsum, g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, Sg, Sgx, nullptr,
                          g_xt, tmask, ws, ws_bytes, stream);
 }
@@ -2041,17 +2039,16 @@ extern "C" int pfsgnn_sl_source_bwd(const pfsgnn_sliced_t* sl, int G, int NF, in
 extern "C" int pfsgnn_sl_source_bwd_bn(
     const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F, const float* y, const float* sc,
     const float* sh, const float* Qt, const float* Ws1, const float* Ws2, const float* bs2,
-    const float* mean, const float* coef, const float* gst, const float* Rs, const float* Wt1,
-    const float* g_hsum, const float* g_next, const float* mu1, const float* inv1,
-    const float* var1, const float* gamma, long long n, float eps, float* g_tot, float* GzS,
-    float* dWs1, float* dWs2, float* dbs2, float* alpha, float* gam0, float* gam1, float* dgamma,
-    float* dbeta, float* g_xt, const unsigned char* tmask, void* ws, size_t ws_bytes,
-    void* stream) {
+    const float* mean, const float* coef, const float* Rs, const float* Wt1, const float* g_hsum,
+    const float* g_next, const float* mu1, const float* inv1, const float* var1,
+    const float* gamma, long long n, float eps, float* g_tot, float* GzS, float* dWs1,
+    float* dWs2, float* dbs2, float* alpha, float* gam0, float* gam1, float* dgamma, float* dbeta,
+    float* g_xt, const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream) {
   PF_REQUIRE(sl && mu1 && inv1 && var1 && gamma && n > 0 && alpha && gam0 && gam1 && dgamma &&
                  dbeta,
              "pfsgnn_sl_source_bwd_bn", "null");
   const Bn2Bwd bb{gamma, mu1, var1, n, eps, alpha, gam0, gam1, dgamma, dbeta};
-  return source_bwd_impl(sl, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, gst, Rs, Wt1,
+  return source_bwd_impl(sl, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
                          g_hsum, g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, nullptr, nullptr,
                          &bb, g_xt, tmask, ws, ws_bytes, stream);
 }
@@ -2059,18 +2056,15 @@ extern "C" int pfsgnn_sl_source_bwd_bn(
 static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
                            const float* y, const float* sc, const float* sh, const float* Qt,
                            const float* Ws1, const float* Ws2, const float* bs2, const float* mean,
-                           const float* coef, const float* gst, const float* Rs, const float* Wt1,
+                           const float* coef, const float* Rs, const float* Wt1,
                            const float* g_hsum, const float* g_next, const float* mu1,
                            const float* inv1, float* g_tot, float* GzS, float* dWs1, float* dWs2,
                            float* dbs2, float* Sg, float* Sgx, const Bn2Bwd* bb, float* g_xt,
                            const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream) {
   if (int rc = check_dims("pfsgnn_source_bwd", G, NF, NC, F)) return rc;
   if (int rc = check_sliced("pfsgnn_source_bwd", sl, NC, F)) return rc;
-  PF_REQUIRE(y && Qt && Ws1 && Ws2 && bs2 && mean && (coef || gst) && g_tot && GzS && dWs1 &&
-                 dWs2 && dbs2,
+  PF_REQUIRE(y && Qt && Ws1 && Ws2 && bs2 && mean && coef && g_tot && GzS && dWs1 && dWs2 && dbs2,
              "pfsgnn_source_bwd", "null");
-  PF_REQUIRE(!gst || !sl, "pfsgnn_source_bwd",
-             "gst (in-kernel moment coefficients) needs a complete batch");
   PF_REQUIRE((Rs == nullptr) == (Wt1 == nullptr) && (Rs == nullptr) == (g_hsum == nullptr),
              "pfsgnn_source_bwd", "Rs, Wt1, g_hsum must be given together");
   PF_REQUIRE(!mu1 || (inv1 && ((Sg && Sgx) || bb)), "pfsgnn_source_bwd",
@@ -2100,17 +2094,11 @@ static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
                                     tmask, tabs, mf_prec(1, F), st))
       return rc;
   } else if (mfma) {
-    if (int rc = pfm::source_bwd(geo, F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, gst, Rs, Wt1,
-                                 ghT, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask,
+    if (int rc = pfm::source_bwd(geo, F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT,
+                                 g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask,
                                  mf_prec(1, F), st))
       return rc;
   } else {
-    if (gst) {   // (the VALU kernel reads coefficients: computed first)
-      float* cf = w.take((size_t)4 * C * geo.NS);
-      PF_REQUIRE(cf, "pfsgnn_source_bwd", "workspace too small");
-      if (int rc = pfsgnn_moment_coef(mean, gst, C, (int)geo.NS, NC, cf, stream)) return rc;
-      coef = cf;
-    }
   DISPATCH_F(F, hipLaunchKernelGGL(k_source_bwd<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo, y,
                                    sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT, g_next,
                                    mu1, inv1, g_tot, pW2, pW1, pCol, pBN));

@@ -39,13 +39,11 @@ int target_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const
 int target_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* Rs, const float* Wt1, const float* ghS, float* gz, float* gxe,
                float* part, const uint8_t* tmask, int prec, hipStream_t st);
-// gst != nullptr: `mean` is the whole moment tensor [4][C][NS] and the moment
-// coefficients are computed in the kernel from it and gst (coef unused)
 int source_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
-               const float* mean, const float* coef, const float* gst, const float* Rs,
-               const float* Wt1, const float* ghS, const float* g_next, const float* mu1,
-               const float* inv1, float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN,
+               const float* mean, const float* coef, const float* Rs, const float* Wt1,
+               const float* ghS, const float* g_next, const float* mu1, const float* inv1,
+               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN,
                const uint8_t* tmask, int prec, hipStream_t st);
 int edge_mlp_bwd(const EdgeGeo& geo, int F, const float* g_tot, const float* alpha,
                  const float* gam0, const float* gam1, const float* y, const float* xe,

@@ -588,8 +588,8 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     EdgeGeo geo, const float* __restrict__ y, const float* __restrict__ sc,
     const float* __restrict__ sh, const float* __restrict__ QtS, const float* __restrict__ Ws1,
     const float* __restrict__ Ws2, const float* __restrict__ bs2, const float* __restrict__ mean,
-    const float* __restrict__ coef, const float* __restrict__ gst, const float* __restrict__ Rs,
-    const float* __restrict__ Wt1, const float* __restrict__ ghS, const float* __restrict__ g_next,
+    const float* __restrict__ coef, const float* __restrict__ Rs, const float* __restrict__ Wt1,
+    const float* __restrict__ ghS, const float* __restrict__ g_next,
     const float* __restrict__ mu1, const float* __restrict__ inv1, float* __restrict__ g_tot,
     float* __restrict__ partW2, float* __restrict__ partW1, float* __restrict__ partCol,
     float* __restrict__ partBN, const uint8_t* __restrict__ tmask) {
@@ -635,38 +635,10 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     if constexpr (!TM) rs[tt] = ld_node<C>(Rs, tt, g4, NS, n, fvalid);
     bias[tt] = ld_vec<C>(bs2, tt, g4);
     mn[tt] = ld_node<C>(mean, tt, g4, NS, n, fvalid);
-    if (gst) {
-      // the moment coefficients of the fiber, from its moments (mean = mom
-      // [4][C][NS]) and their gradients gst (k_moment_coef's arithmetic,
-      // NC messages per fiber): no launch of their own
-      const floatx4 c2 = ld_node<C>(mean + CNS, tt, g4, NS, n, fvalid),
-                    c3 = ld_node<C>(mean + 2 * CNS, tt, g4, NS, n, fvalid),
-                    c4 = ld_node<C>(mean + 3 * CNS, tt, g4, NS, n, fvalid),
-                    gm = ld_node<C>(gst, tt, g4, NS, n, fvalid),
-                    gs = ld_node<C>(gst + CNS, tt, g4, NS, n, fvalid),
-                    gk = ld_node<C>(gst + 2 * CNS, tt, g4, NS, n, fvalid),
-                    gq = ld_node<C>(gst + 3 * CNS, tt, g4, NS, n, fvalid);
-      const float invn = 1.0f / (float)geo.NC;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float var = c2[r] > 0.f ? c2[r] : 0.01f * c2[r];
-        const float sd = sqrtf(var + 1e-6f);
-        const float sd2 = sd * sd, sd3 = sd2 * sd, sd4 = sd2 * sd2;
-        const float A3 = gk[r] / sd3;
-        const float A4 = gq[r] / sd4;
-        const float gstd_tot = gs[r] - 3.f * gk[r] * c3[r] / sd4 - 4.f * gq[r] * c4[r] / (sd4 * sd);
-        const float gvr = gstd_tot / (2.f * sd) * (c2[r] > 0.f ? 1.f : 0.01f);
-        q0[tt][r] = (gm[r] - 3.f * c2[r] * A3 - 4.f * c3[r] * A4) * invn;
-        q1[tt][r] = 2.f * gvr * invn;
-        q2[tt][r] = 3.f * A3 * invn;
-        q3[tt][r] = 4.f * A4 * invn;
-      }
-    } else {
-      q0[tt] = ld_node<C>(coef, tt, g4, NS, n, fvalid);
-      q1[tt] = ld_node<C>(coef + CNS, tt, g4, NS, n, fvalid);
-      q2[tt] = ld_node<C>(coef + 2 * CNS, tt, g4, NS, n, fvalid);
-      q3[tt] = ld_node<C>(coef + 3 * CNS, tt, g4, NS, n, fvalid);
-    }
+    q0[tt] = ld_node<C>(coef, tt, g4, NS, n, fvalid);
+    q1[tt] = ld_node<C>(coef + CNS, tt, g4, NS, n, fvalid);
+    q2[tt] = ld_node<C>(coef + 2 * CNS, tt, g4, NS, n, fvalid);
+    q3[tt] = ld_node<C>(coef + 3 * CNS, tt, g4, NS, n, fvalid);
   }
   const floatx4 scv = ld_fconst<F>(sc, g4, 1.f), shv = ld_fconst<F>(sh, g4, 0.f);
   const floatx4 m1v = ld_fconst<F>(mu1, g4, 0.f), i1v = ld_fconst<F>(inv1, g4, 0.f);
@@ -1107,16 +1079,16 @@ int target_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const
 
 int source_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
-               const float* mean, const float* coef, const float* gst, const float* Rs,
-               const float* Wt1, const float* ghS, const float* g_next, const float* mu1,
-               const float* inv1, float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN,
+               const float* mean, const float* coef, const float* Rs, const float* Wt1,
+               const float* ghS, const float* g_next, const float* mu1, const float* inv1,
+               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN,
                const uint8_t* tmask, int prec, hipStream_t st) {
   if (tmask && Rs) {
-    MF_LAUNCH3(F, prec, true, km_source_bwd, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, gst, Rs,
-               Wt1, ghS, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask)
+    MF_LAUNCH3(F, prec, true, km_source_bwd, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+               ghS, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask)
   } else {
-    MF_LAUNCH3(F, prec, false, km_source_bwd, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, gst, Rs,
-               Wt1, ghS, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask)
+    MF_LAUNCH3(F, prec, false, km_source_bwd, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+               ghS, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask)
   }
   return 0;
 }

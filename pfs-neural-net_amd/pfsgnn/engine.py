@@ -351,8 +351,6 @@ class Engine:
         self.mlp_bwd(P, Gr, pre + "node_mlp_2.", g_xs_new, st["sS"],
                      outs=[(g_xs, F, True), (gst, 8 * F, False), (gu, F, False)])
         self._gu_add(gu, G, g_u)
-        if d.sp is None and getattr(be, "source_bwd_gst", False):
-            return ("gst", gst)     # the coefficients are formed in source_bwd's kernel
         # messages per fiber: NC on complete graphs, the fiber degree otherwise
         return be.moment_coef(st["mom"], gst, d.NC if d.sp is None else d.sp.fib_ptr)
 
@@ -370,14 +368,11 @@ class Engine:
             key = epre + "norm."
             bn2 = (P[key + "weight"], se["var1"], d.E, self.bn_eps, Gr[key + "weight"],
                    Gr[key + "bias"])
-        kw = {"tmask": tmask} if tmask is not None and tpart is not None else {}
-        mean = st["mom"][0]
-        if isinstance(coef, tuple):          # ("gst", gst): coefficients in the kernel
-            mean, coef, kw["gst"] = st["mom"], None, coef[1]
         out = be.source_bwd(
-            d, y, sc, sh, st["Qt"], Ws1, Ws2, P[pre + "node_mlp_1.2.bias"], mean, coef,
+            d, y, sc, sh, st["Qt"], Ws1, Ws2, P[pre + "node_mlp_1.2.bias"], st["mom"][0], coef,
             tpart, g_next, bnstat, Gr[pre + "node_mlp_1.0.weight"], Gr[pre + "node_mlp_1.2.weight"],
-            Gr[pre + "node_mlp_1.2.bias"], bn2=bn2, g_xt=g_xt, **kw)  # + g_xt += Ws1x^T GzS
+            Gr[pre + "node_mlp_1.2.bias"], bn2=bn2, g_xt=g_xt,  # + g_xt += Ws1x^T GzS
+            **({"tmask": tmask} if tmask is not None and tpart is not None else {}))
         g_tot, GzS = out[0], out[1]
         be.wgrad(GzS, st["xt"], Gr[pre + "node_mlp_1.0.weight"], col0=0,
                  db=Gr[pre + "node_mlp_1.0.bias"])

@@ -200,8 +200,8 @@ _SIGS = {
     "pfsgnn_target_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, P, P, P, SZ, P], I),
     "pfsgnn_tmask_bytes": ([I, I, I, I], SZ),
     "pfsgnn_target_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
-    "pfsgnn_source_bwd": ([I, I, I, I] + [P] * 25 + [P, SZ, P], I),
-    "pfsgnn_source_bwd_bn": ([I, I, I, I] + [P] * 18 + [LL, FL] + [P] * 12 + [P, SZ, P], I),
+    "pfsgnn_source_bwd": ([I, I, I, I] + [P] * 24 + [P, SZ, P], I),
+    "pfsgnn_source_bwd_bn": ([I, I, I, I] + [P] * 17 + [LL, FL] + [P] * 12 + [P, SZ, P], I),
     "pfsgnn_edge_bn_grad_sums": ([I, I, I, I, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_edge_mlp_bwd": ([I, I, I, I] + [P] * 21 + [P, SZ, P], I),
     "pfsgnn_loss_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, FL, FL, ULL, P, P, P, P, P, P, P, SZ, P], I),
@@ -1080,21 +1080,13 @@ class HipBackend:
               _ptr(gxe), _ptr(g_xs), _ptr(tmask), ws, wsb, _stream())
         return GzT, gxe
 
-    # complete batches: source_bwd takes the moment gradients (gst) and forms
-    # the moment coefficients in its kernel (engine.source_node_bwd)
-    source_bwd_gst = True
-
     def source_bwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next, bnstat,
-                   dWs1, dWs2, dbs2, bn2=None, g_xt=None, tmask=None, gst=None):
+                   dWs1, dWs2, dbs2, bn2=None, g_xt=None, tmask=None):
         """-> (g_tot, GzS, Sg, Sgx).  With ``bn2`` = (gamma, var1, n, eps, dgamma,
         dbeta) (and ``bnstat``) the edge BatchNorm's backward is finished in the
         same call: -> (g_tot, GzS, None, None, (alpha, gam0, gam1)).  With
-        ``g_xt``: g_xt += Ws1[:, :F]^T GzS as well.  ``gst`` (complete batches,
-        coef None): the moment coefficients from mean = the whole moment tensor
-        [4][2F][NS] and gst in the kernel."""
-        assert (coef is None) != (gst is None)
+        ``g_xt``: g_xt += Ws1[:, :F]^T GzS as well."""
         if self._composed(d):
-            assert gst is None
             out = self._sp.source_bwd(d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next,
                                       bnstat, dWs1, dWs2, dbs2)
             if g_xt is not None:
@@ -1120,9 +1112,8 @@ class HipBackend:
             g_next = g_next.contiguous()
         ws, wsb = self._wsargs(d)
         head = (d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh), Qt.data_ptr(),
-                Ws1.data_ptr(), Ws2.data_ptr(), bs2.data_ptr(), mean.data_ptr(), _ptr(coef),
-                _ptr(gst if gst is None else gst.contiguous()), _ptr(Rs), _ptr(Wt1), _ptr(g_hsum),
-                _ptr(g_next), _ptr(mu1), _ptr(inv1))
+                Ws1.data_ptr(), Ws2.data_ptr(), bs2.data_ptr(), mean.data_ptr(), coef.data_ptr(),
+                _ptr(Rs), _ptr(Wt1), _ptr(g_hsum), _ptr(g_next), _ptr(mu1), _ptr(inv1))
         if bn2 is not None:
             assert bnstat is not None
             gamma, var1, n, eps, dg, db = bn2

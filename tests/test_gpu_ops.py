@@ -541,33 +541,3 @@ def test_edge_ops_node_epilogues(hb, G, NF, NC, F):
     for a, b, nm in zip(oh[1:], oe[1:], ["GzEs", "GzEt", "Vu"]):
         close(a, b, rtol=5e-4, name=nm)
     close(nxs_h, nxs_e, rtol=5e-4, name="g_xs(E)"); close(nxt_h, nxt_e, rtol=5e-4, name="g_xt(E)")
-
-
-@pytest.mark.parametrize("G,NF,NC,F", [(2, 50, 16, 10), (1, 33, 64, 8), (1, 70, 24, 16)])
-def test_source_bwd_in_kernel_moment_coefficients(hb, prec, G, NF, NC, F):
-    """source_bwd with the moment gradients (gst) forms pfsgnn_moment_coef's
-    coefficients in its own kernel: the same outputs as with the coefficients
-    computed by the separate launch (complete batches; every edge path)."""
-    if prec == "bf16x3" and F != 10:
-        pytest.skip("bf16x3 is instantiated for Fdim 10")
-    gen = torch.Generator().manual_seed(7 + G + NF + NC + F)
-    d, _ = dims(G, NF, NC, F)
-    NS, NT, E = d.NS, d.NT, d.E
-    y = cuda(r(F, E, gen=gen))
-    Qt = cuda(r(2 * F, NT, gen=gen) * 0.1)
-    Ws1, Ws2, bs2 = cuda(r(2 * F, 2 * F, scale=0.3, gen=gen)), cuda(r(2 * F, 2 * F, scale=0.3, gen=gen)), \
-        cuda(r(2 * F, gen=gen))
-    mom = r(4, 2 * F, NS, gen=gen)
-    mom[1] = mom[1].abs() + 0.1        # a positive variance for most, as source_fwd gives
-    mom = cuda(mom)
-    gst = cuda(r(4, 2 * F, NS, gen=gen))
-    coef = hb.moment_coef(mom, gst, NC)
-    outs = []
-    for kw in ({"mean": mom[0], "coef": coef}, {"mean": mom, "coef": None, "gst": gst}):
-        grads = [torch.zeros(2 * F, 2 * F, device="cuda"), torch.zeros(2 * F, 2 * F, device="cuda"),
-                 torch.zeros(2 * F, device="cuda")]
-        mean, cf = kw.pop("mean"), kw.pop("coef")
-        o = hb.source_bwd(d, y, None, None, Qt, Ws1, Ws2, bs2, mean, cf, None, None, None, *grads, **kw)
-        outs.append([o[0], o[1]] + grads)
-    for a, b, nm in zip(outs[0], outs[1], ["g_tot", "GzS", "dWs1", "dWs2", "dbs2"]):
-        close(b, a, rtol=1e-5, atol=1e-6, name=nm)
