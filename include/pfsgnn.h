@@ -428,6 +428,16 @@ int pfsgnn_bn2_finalize(const float* mu1, const float* var1, const float* gamma,
 int pfsgnn_bn_eval_coef(const float* gamma, const float* beta, const float* rm,
                         const float* rv, int C, float eps, int times, float* sc, float* sh,
                         void* stream);
+/* Its backward (autograd through a model in eval(), gnn.py:101/154/192): inv =
+ * 1/sqrt(rv + eps) and scale = d out / d y = (gamma inv)^times per channel; with
+ * the input-gradient sums Sg = sum g, Sgx = sum g (y - rm) inv (pfsgnn_rows_bn_sums
+ * or pfsgnn_edge_bn_grad_sums with mu = rm and this inv) dgamma / dbeta accumulate
+ * the parameter gradients of the `times`-fold application.  Sg NULL: inv and
+ * scale only (inv / scale may be NULL when not wanted). */
+int pfsgnn_bn_eval_bwd_coef(const float* gamma, const float* beta, const float* rm,
+                            const float* rv, int C, float eps, int times, const float* Sg,
+                            const float* Sgx, float* inv, float* scale, float* dgamma,
+                            float* dbeta, void* stream);
 /* Y[c][n] = sc[c]*X[c][n] + sh[c] over a channel-major [C][N] table */
 int pfsgnn_affine_rows(const float* X, int C, int N, const float* sc, const float* sh,
                        float* Y, void* stream);

@@ -1881,6 +1881,46 @@ __global__ void k_bn_eval_coef(const float* __restrict__ gamma, const float* __r
   sh[c] = t;
 }
 
+// Backward of eval-mode BatchNorm1d applied `times` times (pfsgnn_bn_eval_coef's
+// affine): y1 = a (y - rm) + beta, a = gamma / sqrt(rv + eps), [y2 = a (y1 - rm)
+// + beta].  d out / d y = a^times; with Sg = sum g, Sgx = sum g (y - rm) inv:
+//   times 1: dgamma += Sgx,                         dbeta += Sg
+//   times 2: dgamma += 2 a Sgx + inv (beta - rm) Sg, dbeta += (a + 1) Sg
+// (d y2 / d gamma = inv (y1 - rm) + a inv (y - rm), d y2 / d beta = a + 1).
+__global__ void k_bn_eval_bwd_coef(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   const float* __restrict__ rm, const float* __restrict__ rv,
+                                   int C, float eps, int times, const float* __restrict__ Sg,
+                                   const float* __restrict__ Sgx, float* __restrict__ inv,
+                                   float* __restrict__ scale, float* __restrict__ dgamma,
+                                   float* __restrict__ dbeta) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  const float sd = sqrtf(rv[c] + eps);
+  const float iv = 1.f / sd, a = gamma[c] / sd;
+  if (inv) inv[c] = iv;
+  if (scale) scale[c] = times == 2 ? a * a : a;
+  if (!Sg) return;
+  if (times == 2) {
+    dgamma[c] += 2.f * a * Sgx[c] + iv * (beta[c] - rm[c]) * Sg[c];
+    dbeta[c] += (a + 1.f) * Sg[c];
+  } else {
+    dgamma[c] += Sgx[c];
+    dbeta[c] += Sg[c];
+  }
+}
+
+extern "C" int pfsgnn_bn_eval_bwd_coef(const float* gamma, const float* beta, const float* rm,
+                                       const float* rv, int C, float eps, int times,
+                                       const float* Sg, const float* Sgx, float* inv,
+                                       float* scale, float* dgamma, float* dbeta, void* stream) {
+  PF_REQUIRE(gamma && beta && rm && rv && C > 0 && C <= 64 && times >= 1 && times <= 2 &&
+                 (!Sg || (Sgx && dgamma && dbeta)),
+             "pfsgnn_bn_eval_bwd_coef", "bad arguments");
+  hipLaunchKernelGGL(k_bn_eval_bwd_coef, dim3(1), dim3(64), 0, as_stream(stream), gamma, beta, rm,
+                     rv, C, eps, times, Sg, Sgx, inv, scale, dgamma, dbeta);
+  return pf::check_launch("pfsgnn_bn_eval_bwd_coef");
+}
+
 extern "C" int pfsgnn_bn_eval_coef(const float* gamma, const float* beta, const float* rm,
                                    const float* rv, int C, float eps, int times, float* sc,
                                    float* sh, void* stream) {

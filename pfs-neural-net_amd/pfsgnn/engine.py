@@ -111,6 +111,9 @@ class Engine:
         self.bn_momentum = bn_momentum
         self.rms_eps = rms_eps
         self.training = True
+        # eval() with autograd: the forward saves what the backward needs
+        # (BatchNorm on running statistics, gnn.py:101/154/192)
+        self.want_grad = False
 
     # ================================================================= MLP
     def _bn_args(self, P, BN, bnkey):
@@ -155,13 +158,14 @@ class Engine:
         if norm and self.training:
             Y, Z, Yp, mu, var = be.mlp_fwd(segs, N, W1, b1, W2, b2, bn=self._bn_args(P, BN, bnkey))
             return Y, (segs, Z, (Yp, mu, var, bnkey))
-        Y, Z, _, _, _ = be.mlp_fwd(segs, N, W1, b1, W2, b2, save_z=self.training)
+        Y, Z, _, _, _ = be.mlp_fwd(segs, N, W1, b1, W2, b2,
+                                   save_z=self.training or self.want_grad)
         if norm:
             # eval: nn.BatchNorm1d on running statistics, applied once (gnn.py:154/192)
-            sc, sh = be.bn_eval_coef(P[bnkey + "weight"], P[bnkey + "bias"],
-                                     BN[bnkey + "running_mean"], BN[bnkey + "running_var"],
+            rm, rv = BN[bnkey + "running_mean"], BN[bnkey + "running_var"]
+            sc, sh = be.bn_eval_coef(P[bnkey + "weight"], P[bnkey + "bias"], rm, rv,
                                      self.bn_eps, 1)
-            Y = be.affine_rows(Y, sc, sh)
+            return be.affine_rows(Y, sc, sh), (segs, Z, ("eval", Y, bnkey, rm, rv))
         return Y, (segs, Z, None)
 
     def mlp_bwd(self, P, Gr, pre, dY, saved, outs=()):
@@ -175,12 +179,27 @@ class Engine:
         W1, W2 = P[pre + "0.weight"], P[pre + "2.weight"]
         K = sum(X.shape[0] for X, _, _ in segs)
         bn = None
+        if bns is not None and bns[0] == "eval":
+            dY = self._bn_eval_bwd(P, Gr, bns[2], 1, dY, bns[1], bns[3], bns[4])
+            bns = None
         if bns is not None:
             Yp, mu, var, key = bns
             bn = (Yp, mu, var, P[key + "weight"], self.bn_eps, Gr[key + "weight"], Gr[key + "bias"])
         dYp, dZ = be.mlp_bwd(dY, Z, W1, W2, K, bn=bn, outs=list(outs))
         be.wgrad(dYp, Z, Gr[pre + "2.weight"], db=Gr[pre + "2.bias"], act_in=True)
         be.wgrad_cat(dZ, segs, Gr[pre + "0.weight"], db=Gr[pre + "0.bias"])
+
+    def _bn_eval_bwd(self, P, Gr, key, times, dY, Yp, rm, rv):
+        """Backward of an eval-mode BatchNorm1d (running statistics rm, rv; applied
+        ``times`` times) at its input Yp: dgamma / dbeta accumulate into Gr and
+        the input gradient scale * dY comes back (pfsgnn_bn_eval_bwd_coef)."""
+        be = self.be
+        g, b = P[key + "weight"], P[key + "bias"]
+        inv, scale = be.bn_eval_bwd_coef(g, b, rm, rv, self.bn_eps, times)
+        Sg, Sgx = be.rows_bn_sums(dY, Yp, rm, inv)
+        be.bn_eval_bwd_coef(g, b, rm, rv, self.bn_eps, times, Sg, Sgx, Gr[key + "weight"],
+                            Gr[key + "bias"])
+        return be.affine_rows(dY, scale, be.zeros(scale.shape[0]))
 
     # MLPs outside the fused op's shapes (output > 16 or a width > 112: Fdim 16's
     # SModel node_mlp_2, a node_prediction decoder over many classes) run as
@@ -199,9 +218,10 @@ class Engine:
                 bns = (Y, mu, var, bnkey)
                 Y = Yn
             else:
-                sc, sh = be.bn_eval_coef(P[bnkey + "weight"], P[bnkey + "bias"],
-                                         BN[bnkey + "running_mean"], BN[bnkey + "running_var"],
+                rm, rv = BN[bnkey + "running_mean"], BN[bnkey + "running_var"]
+                sc, sh = be.bn_eval_coef(P[bnkey + "weight"], P[bnkey + "bias"], rm, rv,
                                          self.bn_eps, 1)
+                bns = ("eval", Y, bnkey, rm, rv)
                 Y = be.affine_rows(Y, sc, sh)
         return Y, ("ops", segs, Z, bns)
 
@@ -209,6 +229,9 @@ class Engine:
         be = self.be
         _, segs, Z, bns = saved
         W1, W2 = P[pre + "0.weight"], P[pre + "2.weight"]
+        if bns is not None and bns[0] == "eval":
+            dY = self._bn_eval_bwd(P, Gr, bns[2], 1, dY, bns[1], bns[3], bns[4])
+            bns = None
         if bns is not None:
             Yp, mu, var, key = bns
             dY = be.bn_bwd(dY, Yp, mu, var, P[key + "weight"], self.bn_eps, Gr[key + "weight"],
@@ -281,17 +304,34 @@ class Engine:
             key = pre + "norm."
             sc, sh = be.bn_eval_coef(P[key + "weight"], P[key + "bias"], BN[key + "running_mean"],
                                      BN[key + "running_var"], self.bn_eps, 2)
-            inv1 = None
-        else:
-            sc = sh = inv1 = None
+            return dict(xs=xs, xt=xt, xe3=xe3, u=u, Ps=Ps, Pt=Pt, y=y, mu1=mu1, var1=var1,
+                        sc=sc, sh=sh, inv1=None, rm=BN[key + "running_mean"],
+                        rv=BN[key + "running_var"])
         return dict(xs=xs, xt=xt, xe3=xe3, u=u, Ps=Ps, Pt=Pt, y=y, mu1=mu1, var1=var1,
-                    sc=sc, sh=sh, inv1=inv1)
+                    sc=None, sh=None, inv1=None)
 
     def edge_bn_coef(self, P, Gr, d, pre, st, Sg, Sgx):
-        """The double BatchNorm's backward coefficients from its gradient sums."""
+        """The double BatchNorm's backward coefficients from its gradient sums
+        (taken about edge_bnstat's centre and scale)."""
         key = pre + "norm."
+        if "rm" in st:      # eval: running statistics, an affine map applied twice
+            _, scale = self.be.bn_eval_bwd_coef(P[key + "weight"], P[key + "bias"], st["rm"],
+                                                st["rv"], self.bn_eps, 2, Sg, Sgx,
+                                                Gr[key + "weight"], Gr[key + "bias"])
+            z = self.be.zeros(scale.shape[0])
+            return scale, z, z
         return self.be.bn2_bwd_coef(Sg, Sgx, st["mu1"], st["var1"], P[key + "weight"], d.E,
                                     self.bn_eps, Gr[key + "weight"], Gr[key + "bias"])
+
+    def edge_bnstat(self, P, pre, st):
+        """(centre, 1/scale) of the edge BatchNorm's gradient sums: the batch
+        statistics in training, the running statistics in eval."""
+        if "rm" in st:
+            key = pre + "norm."
+            inv, _ = self.be.bn_eval_bwd_coef(P[key + "weight"], P[key + "bias"], st["rm"],
+                                              st["rv"], self.bn_eps, 2)
+            return st["rm"], inv
+        return st["mu1"], st["inv1"]
 
     def edge_bwd(self, P, Gr, d, pre, st, g_tot, bnc, want_gxe, g_xs, g_xt, g_u):
         """g_tot: d loss / d xe_new (canonical [F, E]); bnc: the BatchNorm's
@@ -532,16 +572,19 @@ class Engine:
         be.graph_bcast_add2(g_xs, 1.0 / d.NF, g_xt, 1.0 / d.NC, g_m)
 
     # ============================================================ GNN path
-    def forward(self, P, BN, d, xs_in, xt_in, xe_in, u_in, training=True):
+    def forward(self, P, BN, d, xs_in, xt_in, xe_in, u_in, training=True, want_grad=False):
         """GNN.forward (gnn.py:280-305).  xs_in [Fs, NS], xt_in [Ft, NT], xe_in [F, E],
         u_in [F, G] (channel-major).  Returns a context with the outputs
         (xs, xt, xe3, u) and everything backward needs."""
         # eval (training=False): BatchNorm on running statistics, nothing updated;
-        # the context then serves inference only (backward refuses it)
+        # with want_grad the context also serves a backward (gnn.eval() under
+        # autograd: the norms are affine maps then, gnn.py:101/154/192)
         self.training = training
+        self.want_grad = want_grad
         xs, s_enc = self.mlp_fwd(P, "encoder_s.", xs_in)
         xt, t_enc = self.mlp_fwd(P, "encoder_t.", xt_in)
-        ctx = {"d": d, "enc": (s_enc, t_enc), "blocks": [], "training": training}
+        ctx = {"d": d, "enc": (s_enc, t_enc), "blocks": [], "training": training,
+               "want_grad": want_grad}
         xe3 = (xe_in, None, None)
         u = u_in
         parts = None
@@ -585,9 +628,9 @@ class Engine:
         """Accumulates parameter gradients into ``Gr`` (same keys as ``P``).
         g_xe_out is [F, E] canonical, w.r.t. the final edge features."""
         d, be, F = ctx["d"], self.be, self.F
-        if not ctx.get("training", True):
-            raise NotImplementedError("backward through an eval-mode forward (BatchNorm on "
-                                      "running statistics) is not implemented")
+        if not ctx.get("training", True) and not ctx.get("want_grad", False):
+            raise NotImplementedError("this eval-mode forward ran for inference only (forward "
+                                      "with want_grad=True to differentiate through it)")
         # node weight-gradient reductions are batched over the pass (flushed below)
         be.defer_begin()
         try:
@@ -616,7 +659,8 @@ class Engine:
             # train.py objective) contribute nothing and are skipped
             live_t = g_u is not None or g_xt is not None
             live_s = live_t or g_xs is not None
-            bnstat = (se["mu1"], se["inv1"]) if self.normed else None
+            bnstat = self.edge_bnstat(P, p + "edge_model.", se) if self.normed else None
+            ev = "rm" in se     # eval-mode forward: BatchNorm on running statistics
             if live_s:
                 # below the last block g_xs / g_xt are this loop's own accumulators
                 # and are updated in place; the caller's gradients are copied
@@ -634,10 +678,16 @@ class Engine:
                     tpart = (stt["Rs"], P[p + "t_model.node_mlp_1.0.weight"], g_hsum)
                 coef = self.source_node_bwd(P, Gr, d, p + "s_model.", ss, g_xs_new, g_xs_in, g_u_in)
                 g_tot, *bnc = self.source_edge_bwd(P, Gr, d, p + "s_model.", ss, coef, tpart,
-                                                   g_xe, bnstat, g_xt_in, se=se,
+                                                   g_xe, bnstat, g_xt_in,
+                                                   se=None if ev else se,
                                                    epre=p + "edge_model.",
                                                    tmask=stt.get("tmask") if live_t else None)
-                bnc = bnc[0] if self.normed else None
+                if not self.normed:
+                    bnc = None
+                elif ev:
+                    bnc = self.edge_bn_coef(P, Gr, d, p + "edge_model.", se, *bnc)
+                else:
+                    bnc = bnc[0]
             else:
                 g_tot = be.zeros(F, d.EP) if g_xe is None else g_xe
                 bnc = None

@@ -450,15 +450,6 @@ def _engine_for(F, normed, B=0):
     return Engine(backend(), F=F, B=B, normed=normed)
 
 
-def _eval_guard(module):
-    """Eval mode (BatchNorm on running statistics) is inference only here."""
-    if not module.training and torch.is_grad_enabled() and any(
-            p.requires_grad for p in module.parameters()):
-        raise NotImplementedError(f"{type(module).__name__}.forward in eval mode runs inference "
-                                  "only (BatchNorm on running statistics, no backward): call it "
-                                  "under torch.no_grad()")
-
-
 # =================================================================== models
 class _MLPFn(torch.autograd.Function):
     @staticmethod
@@ -507,6 +498,7 @@ class _EdgeFn(torch.autograd.Function):
         d, lay = _graph_of(x_s, x_t, u, edge_index, F)
         eng = _engine_for(F, module.normed)
         eng.training = module.training
+        eng.want_grad = not module.training    # (eval() under autograd: running statistics)
         P, BN = module._flat_params(), module._bn_buffers()
         st = eng.edge_fwd(P, BN, d, "", _cm(x_s), _cm(x_t), (edges_in(edge_attr, lay), None, None), _cm(u))
         if module.normed and module.training:
@@ -524,7 +516,7 @@ class _EdgeFn(torch.autograd.Function):
         gc = be.zeros(F, d.EP) if gc is None else gc.contiguous()
         bnc = None
         if module.normed:
-            Sg, Sgx = be.edge_bn_grad_sums(d, gc, st["y"], st["mu1"], st["inv1"])
+            Sg, Sgx = be.edge_bn_grad_sums(d, gc, st["y"], *eng.edge_bnstat(P, "", st))
             bnc = eng.edge_bn_coef(P, Gr, d, "", st, Sg, Sgx)
         g_xs, g_xt, g_u = be.zeros(F, d.NS), be.zeros(F, d.NT), be.zeros(F, d.G)
         g_xe = eng.edge_bwd(P, Gr, d, "", st, gc, bnc, True, g_xs, g_xt, g_u)
@@ -543,7 +535,6 @@ class EdgeModel(MLP):
 
     def forward(self, x_s, x_t, edge_index, edge_attr, u):
         self._flat_sync()
-        _eval_guard(self)
         return _EdgeFn.apply(x_s, x_t, edge_attr, u, self[0].weight, self, edge_index)
 
 
@@ -554,6 +545,7 @@ class _SourceFn(torch.autograd.Function):
         d, lay = _graph_of(x_s, x_t, u, edge_index, F)
         eng = _engine_for(F, module.normed)
         eng.training = module.training
+        eng.want_grad = not module.training    # (eval() under autograd: running statistics)
         P, BN = module._flat_params(), module._bn_buffers()
         st = eng.source_fwd(P, BN, d, "", _cm(x_s), _cm(x_t), (edges_in(edge_attr, lay), None, None), _cm(u))
         if module.normed and module.training:
@@ -588,7 +580,6 @@ class SModel(_ParamMixin, torch.nn.Module):
 
     def forward(self, x_s, x_t, edge_index, edge_attr, u):
         self._flat_sync()
-        _eval_guard(self)
         return _SourceFn.apply(x_s, x_t, edge_attr, u, self.node_mlp_1[0].weight, self, edge_index)
 
 
@@ -599,6 +590,7 @@ class _TargetFn(torch.autograd.Function):
         d, lay = _graph_of(x_s, x_t, u, edge_index, F)
         eng = _engine_for(F, module.normed)
         eng.training = module.training
+        eng.want_grad = not module.training    # (eval() under autograd: running statistics)
         P, BN = module._flat_params(), module._bn_buffers()
         st = eng.target_fwd(P, BN, d, "", _cm(x_s), _cm(x_t), (edges_in(edge_attr, lay), None, None), _cm(u))
         if module.normed and module.training:
@@ -633,7 +625,6 @@ class TModel(_ParamMixin, torch.nn.Module):
 
     def forward(self, x_s, x_t, edge_index, edge_attr, u):
         self._flat_sync()
-        _eval_guard(self)
         return _TargetFn.apply(x_s, x_t, edge_attr, u, self.node_mlp_1[0].weight, self, edge_index)
 
 
@@ -719,8 +710,11 @@ class _GNNFn(torch.autograd.Function):
     def forward(ctx, anchor, model, d, lay, xs_in, xt_in, xe_in, u_in):
         ctx.set_materialize_grads(False)      # unused outputs -> None -> dead work skipped
         P, BN = model._flat_params(), model._bn_buffers()
-        ectx = model._engine().forward(P, BN, d, xs_in, xt_in, xe_in, u_in)
-        if model.normed:
+        # (eval() under autograd: BatchNorm on running statistics, nothing
+        # updated, the backward differentiates those affine maps)
+        ectx = model._engine().forward(P, BN, d, xs_in, xt_in, xe_in, u_in,
+                                       training=model.training, want_grad=not model.training)
+        if model.normed and model.training:
             model._bump_batches(
                 edge_keys=[f"mpb.{b}.edge_model.norm." for b in range(model.B)],
                 node_keys=[f"mpb.{b}.{m}.norm." for b in range(model.B) for m in ("s_model", "t_model")])
@@ -819,11 +813,11 @@ class GNN(_FlatMixin, torch.nn.Module):
                       normed=self.normed)
 
     def forward(self, graph):
-        if not self.training and torch.is_grad_enabled() and any(
-                p.requires_grad for p in self.parameters()):
-            raise NotImplementedError("GNN.forward in eval mode runs inference only (BatchNorm "
-                                      "on running statistics, no backward): call it under "
-                                      "torch.no_grad()")
+        # eval() with autograd on (gnn.eval() then loss.backward(): BatchNorm on
+        # running statistics, round() the identity, gnn.py:321-325) runs the
+        # differentiable path as in training, nothing updated
+        grad = self.training or (torch.is_grad_enabled() and any(
+            p.requires_grad for p in self.parameters()))
         for t in (graph.x_s, graph.x_t, graph.x_e, graph.x_u):
             if t is not None and t.requires_grad:
                 raise NotImplementedError("gradients w.r.t. the graph inputs are not computed")
@@ -831,7 +825,7 @@ class GNN(_FlatMixin, torch.nn.Module):
         d, lay = geometry(graph.x_s, graph.x_t, graph.x_u, graph.edge_index, self.Fdim)
         xe_in = edges_in(graph.x_e, lay, cache=True)
         out = GNNOutput.__new__(GNNOutput)
-        if self.training:
+        if grad:
             anchor = self.encoder_s[0].weight
             xs, xt, token, u = _GNNFn.apply(anchor, self, d, lay, _cm(graph.x_s), _cm(graph.x_t),
                                             xe_in, _cm(graph.x_u))

@@ -217,6 +217,7 @@ _SIGS = {
     "pfsgnn_target_block_fwd": ([ctypes.POINTER(BlockTail), P, SZ, P], I),
     "pfsgnn_sync_faults": ([ctypes.POINTER(ctypes.c_uint)], I),
     "pfsgnn_block_tail_bytes": ([], SZ),
+    "pfsgnn_bn_eval_bwd_coef": ([P, P, P, P, I, FL, I, P, P, P, P, P, P, P], I),
     "pfsgnn_sliced_plan_ws_bytes": ([I, I], SZ),
     "pfsgnn_sliced_plan": ([P, I, I, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_sliced_fill": ([P, P, P, P, LL, I, I, P, P, LL, I, P, P, P, P], I),
@@ -930,6 +931,19 @@ class HipBackend:
         _call("pfsgnn_bn_eval_coef", gamma.data_ptr(), beta.data_ptr(), rm.data_ptr(),
               rv.data_ptr(), C, float(eps), int(times), sc.data_ptr(), sh.data_ptr(), _stream())
         return sc, sh
+
+    def bn_eval_bwd_coef(self, gamma, beta, rm, rv, eps, times, Sg=None, Sgx=None, dgamma=None,
+                         dbeta=None):
+        """Eval-mode BatchNorm1d backward coefficients (pfsgnn_bn_eval_bwd_coef):
+        -> (inv, scale); with the gradient sums (Sg, Sgx) dgamma / dbeta += the
+        parameter gradients of the ``times``-fold application."""
+        C = gamma.shape[0]
+        self._chk(gamma, beta, rm, rv, Sg, Sgx, dgamma, dbeta)
+        inv, scale = self.empty(C), self.empty(C)
+        _call("pfsgnn_bn_eval_bwd_coef", gamma.data_ptr(), beta.data_ptr(), rm.data_ptr(),
+              rv.data_ptr(), C, float(eps), int(times), _ptr(Sg), _ptr(Sgx), inv.data_ptr(),
+              scale.data_ptr(), _ptr(dgamma), _ptr(dbeta), _stream())
+        return inv, scale
 
     def affine_rows(self, X, sc, sh):
         C, N = X.shape

@@ -307,6 +307,22 @@ class EmuBackend:
     def affine_rows(self, X, sc, sh):
         return X * sc[:, None] + sh[:, None]
 
+    def bn_eval_bwd_coef(self, gamma, beta, rm, rv, eps, times, Sg=None, Sgx=None, dgamma=None,
+                         dbeta=None):
+        """pfsgnn_bn_eval_bwd_coef: eval BatchNorm1d (applied ``times`` times)
+        backward: -> (inv, scale = a^times); dgamma / dbeta += its parameter
+        gradients from Sg = sum g, Sgx = sum g (y - rm) inv."""
+        sd = torch.sqrt(rv.to(gamma.dtype) + eps)
+        inv, a = 1.0 / sd, gamma / sd
+        if Sg is not None:
+            if times == 2:
+                dgamma += 2 * a * Sgx + inv * (beta - rm.to(gamma.dtype)) * Sg
+                dbeta += (a + 1) * Sg
+            else:
+                dgamma += Sgx
+                dbeta += Sg
+        return inv, (a * a if times == 2 else a)
+
     def bn2_finalize(self, mu1, var1, gamma, beta, rm, rv, n, momentum, eps):
         """EdgeModel's BatchNorm applied twice (gnn.py:101 -- ``super().forward``
         already runs ``self.norm`` as the Sequential's last child).  The second

@@ -103,6 +103,47 @@ def test_engine_eval_mode_fp64(G, NF, NC, B):
     assert torch.allclose(u.t(), out.x_u, rtol=1e-9, atol=1e-9)
     for k in BN:
         assert torch.equal(BN[k], BN0[k]), k
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(NotImplementedError):   # an inference-only context
         eng.backward(P, {k: torch.zeros_like(v) for k, v in P.items()}, ctx,
                      g_xe_out=torch.zeros_like(xe))
+
+
+@pytest.mark.parametrize("G,NF,NC,B,normed", [(1, 9, 5, 2, True), (2, 6, 4, 1, True),
+                                              (3, 5, 7, 2, True), (2, 6, 5, 2, False)])
+def test_engine_eval_mode_backward_fp64(G, NF, NC, B, normed):
+    """gnn.eval() under autograd (the reference trains nothing in eval, but its
+    backward works: BatchNorm on running statistics is an affine map, round()
+    the identity, gnn.py:101/154/192/321-325): the engine's eval forward with
+    want_grad + the train.py loss + backward vs the oracle in eval() in fp64."""
+    model, graph = make_problem(G, NF, NC, B=B, seed=11, normed=normed)
+    model.train()
+    with torch.no_grad():
+        model(graph)                     # running stats off their init values
+    ref = copy.deepcopy(model).eval()
+    sharp = 9.0
+    out = ref(graph)
+    uni = torch.as_tensor(uniform_numpy(4321, G * NF * NC), dtype=torch.float64)
+    loss_o, _ = oracle_loss(ref, out.x_e, graph.x_t, G, NF, NC, pclass=0.1, pfiber=0.1,
+                            sharpness=sharp, uniform=uni)
+    loss_o.backward()
+    be = EmuBackend()
+    eng = Engine(be, F=10, B=B, Fs=1, Ft=2, T=12, normed=normed)
+    P = {k: v.detach().clone() for k, v in model.named_parameters()}
+    Gr = {k: torch.zeros_like(v) for k, v in P.items()}
+    BN = {k: v.clone() for k, v in model.state_dict().items() if "running" in k}
+    BN0 = {k: v.clone() for k, v in BN.items()}
+    d = Dims(G, NF, NC, 10)
+    ctx = eng.forward(P, BN, d, graph.x_s.t().contiguous(), graph.x_t.t().contiguous(),
+                      to_canonical(graph.x_e, G, NF, NC), graph.x_u.t().contiguous(),
+                      training=False, want_grad=True)
+    loss_e, _, lctx = eng.loss_forward(P, d, ctx["out"][2], graph.x_t.t().contiguous(), sharp,
+                                       4321, pclass=0.1, pfiber=0.1)
+    eng.backward(P, Gr, ctx, g_xe_out=eng.loss_backward(P, Gr, lctx))
+    assert torch.allclose(loss_e, loss_o, rtol=1e-10, atol=1e-8)
+    for name, prm in ref.named_parameters():
+        gref = prm.grad if prm.grad is not None else torch.zeros_like(prm)
+        scale = gref.abs().max().item() + 1e-12
+        err = (Gr[name] - gref).abs().max().item()
+        assert err <= 1e-8 * max(scale, 1.0), (name, err, scale)
+    for k in BN:
+        assert torch.equal(BN[k], BN0[k]), k

@@ -286,8 +286,6 @@ def test_gnn_eval_forward_matches_oracle(G, NF, NC, B):
     sd0 = {k: v.clone() for k, v in gnn.state_dict().items()}
     data = pfsgnn.BipartiteData(graph.edge_index, graph.x_s.float(), graph.x_t.float(),
                                 graph.x_e.float(), graph.x_u.float())
-    with pytest.raises(NotImplementedError):
-        gnn(data)                         # eval with grad enabled is refused loudly
     with torch.no_grad():
         out = gnn(data)
         loss, _ = loss_function(out, graph.x_t.float().cuda(), pclass=0.1, pfiber=0.1,
@@ -298,6 +296,112 @@ def test_gnn_eval_forward_matches_oracle(G, NF, NC, B):
         check("eval " + nm, getattr(out, nm), getattr(o64, nm), getattr(o32, nm))
     check("eval loss", loss, l64, l32)
     for k, v in gnn.state_dict().items():
+        assert torch.equal(v, sd0[k]), k
+
+
+@pytest.mark.parametrize("G,NF,NC,B,sharp", [(1, 40, 12, 2, 12.0), (2, 24, 16, 2, 5.0),
+                                             (1, 16, 128, 1, 20.0)])
+def test_gnn_eval_backward_matches_oracle(G, NF, NC, B, sharp):
+    """gnn.eval() under autograd: forward on running statistics + the train.py
+    loss + backward, vs the oracle in eval() (gnn.py:101/154/192 as affine
+    maps, round() the identity, gnn.py:321-325); nothing is updated."""
+    model, graph = make_problem(G, NF, NC, B=B, seed=21 + G + NC)
+    model.train()
+    with torch.no_grad():
+        model(graph)                     # running stats off their init values
+    seed = 555 + NC
+
+    def oracle_eval(dtype, reverse=False):
+        m = copy.deepcopy(model).to(dtype).eval()
+        ei, xe = graph.edge_index, graph.x_e
+        if reverse:
+            ei, xe = ei.flip(1), xe.flip(0)
+        g = OGraph(ei, graph.x_s.to(dtype), graph.x_t.to(dtype), xe.to(dtype),
+                   graph.x_u.to(dtype), graph.s_batch, graph.t_batch)
+        out = m(g)
+        if reverse:
+            out.x_e = out.x_e.flip(0)
+        uni = torch.as_tensor(uniform_numpy(seed, G * NF * NC), dtype=dtype)
+        loss, _ = oracle_loss(m, out.x_e, g.x_t, G, NF, NC, pclass=0.1, pfiber=0.1,
+                              sharpness=sharp, uniform=uni)
+        loss.backward()
+        return m, loss
+
+    m64, l64 = oracle_eval(torch.float64)
+    ref32 = [oracle_eval(torch.float32, rv) for rv in (False, True)]
+    import pfsgnn
+    from pfsgnn.train import loss_function
+    gnn = pfsgnn.GNN(B=B, Fdim=10, T=12, F_s=1, F_t=2).cuda()
+    gnn.load_state_dict({k: v.float() for k, v in model.state_dict().items()})
+    gnn.eval()
+    sd0 = {k: v.clone() for k, v in gnn.state_dict().items()}
+    data = pfsgnn.BipartiteData(graph.edge_index, graph.x_s.float(), graph.x_t.float(),
+                                graph.x_e.float(), graph.x_u.float())
+    out = gnn(data)
+    loss, _ = loss_function(out, graph.x_t.float().cuda(), pclass=0.1, pfiber=0.1,
+                            sharpness=sharp, seed=seed)
+    loss.backward()
+    torch.cuda.synchronize()
+    check("eval loss", loss, l64, [r[1] for r in ref32])
+    p64 = dict(m64.named_parameters())
+    p32s = [dict(r[0].named_parameters()) for r in ref32]
+    for name, p in gnn.named_parameters():
+        r64 = p64[name].grad if p64[name].grad is not None else torch.zeros_like(p64[name])
+        r32 = [q[name].grad if q[name].grad is not None else torch.zeros_like(q[name])
+               for q in p32s]
+        ours = p.grad if p.grad is not None else torch.zeros_like(p)
+        check("eval grad " + name, ours, r64, r32)
+    for k, v in gnn.state_dict().items():
+        assert torch.equal(v, sd0[k]), k
+
+
+@pytest.mark.parametrize("kind", ["edge", "source", "target"])
+def test_standalone_models_eval_backward_match_oracle(kind):
+    """The standalone modules in eval() under autograd (running statistics):
+    output and every input / parameter gradient vs the oracle in eval()."""
+    import pfsgnn
+    pairs = {"edge": (ref_gnn.EdgeModel, pfsgnn.EdgeModel), "source": (ref_gnn.SModel, pfsgnn.SModel),
+             "target": (ref_gnn.TModel, pfsgnn.TModel)}
+    G, NF, NC = 2, 20, 16
+    mo, mh, ei, xs, xt, xe, u = _module_case(*pairs[kind], G, NF, NC, seed=6)
+    with torch.no_grad():
+        for n, b in mo.named_buffers():
+            if n.endswith("running_mean"):
+                b.copy_(torch.linspace(-0.5, 0.5, b.numel(), dtype=b.dtype))
+            elif n.endswith("running_var"):
+                b.copy_(torch.linspace(0.5, 2.0, b.numel(), dtype=b.dtype))
+    mh.load_state_dict({k: v.float() if v.is_floating_point() else v
+                        for k, v in mo.state_dict().items()})
+    sb = torch.arange(G).repeat_interleave(NF)
+    tb = torch.arange(G).repeat_interleave(NC)
+    res = {}
+    for dt in (torch.float64, torch.float32):
+        m = copy.deepcopy(mo).to(dt).eval()
+        ins = [t.detach().clone().to(dt).requires_grad_() for t in (xs, xt, xe, u)]
+        out = m(ins[0], ins[1], ei, ins[2], ins[3], tb if kind == "target" else sb)
+        gout = torch.linspace(-1, 1, out.numel(), dtype=dt).reshape(out.shape)
+        (out * gout).sum().backward()
+        res[dt] = (m, out, ins)
+    mh.eval()
+    sd0 = {k: v.clone() for k, v in mh.state_dict().items()}
+    insh = [t.float().cuda().requires_grad_() for t in (xs, xt, xe, u)]
+    outh = mh(insh[0], insh[1], ei.cuda(), insh[2], insh[3])
+    gout = torch.linspace(-1, 1, outh.numel(), dtype=torch.float32, device="cuda").reshape(outh.shape)
+    (outh * gout).sum().backward()
+    (m64, o64, i64), (m32, o32, i32) = res[torch.float64], res[torch.float32]
+    check(kind + " eval out", outh, o64, o32)
+    for nm, a, b, c in zip(["x_s", "x_t", "x_e", "u"], insh, i64, i32):
+        if b.grad is None:
+            continue
+        ga = a.grad if a.grad is not None else torch.zeros_like(a)
+        check(f"{kind} eval d{nm}", ga, b.grad, c.grad)
+    p64, p32 = dict(m64.named_parameters()), dict(m32.named_parameters())
+    for n, p in mh.named_parameters():
+        g64 = p64[n].grad if p64[n].grad is not None else torch.zeros_like(p64[n])
+        g32 = p32[n].grad if p32[n].grad is not None else torch.zeros_like(p32[n])
+        check(f"{kind} eval grad {n}", p.grad if p.grad is not None else torch.zeros_like(p),
+              g64, g32)
+    for k, v in mh.state_dict().items():
         assert torch.equal(v, sd0[k]), k
 
 
