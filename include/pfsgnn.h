@@ -315,6 +315,36 @@ typedef struct {
 int pfsgnn_target_block_fwd(const pfsgnn_block_tail* a, void* ws, size_t ws_bytes, void* stream);
 /* sizeof(pfsgnn_block_tail), for bindings to check their struct layout */
 size_t pfsgnn_block_tail_bytes(void);
+/* The class side of a block's backward on a complete batch (training
+ * BatchNorm, gnn.py:191-192 + 218-223 under autograd) in ONE launch, units of
+ * 16 classes of one graph around two device-wide barriers:
+ *   1. gu_up += per-graph sums of the pending u[batch] gradients of the block
+ *      above (npend tables [F][G*pend_n[i]], pend_n = NF or NC: what
+ *      pfsgnn_graph_reduce_multi would add);
+ *   2. the GlobalModel backward of pfsgnn_global_bwd on dY = gu_up (gV, gdZ, dwp
+ *      written; gu += its u-input gradient; g_xs += d mean_xs / NF and g_xt +=
+ *      d mean_xt / NC broadcast), then TModel's BatchNorm sums on the new g_xt;
+ *   3. pfsgnn_mlp_bwd of node_mlp_2 + BatchNorm on dY = g_xt (dYp, dZ written,
+ *      dgamma / dbeta accumulated) with dX's rows [0, F) added into gxt_in,
+ *      [F, 3F) written to g_agg, [3F, 4F) to gu_t; and g_hsum = Wt2^T g_agg
+ *      (TModel's second Linear, gnn.py:188-190).
+ * node_mlp_2: W1 [4F][4F], W2 [F][4F]; GlobalModel: gW1 [gH][3F], gW2 [F][gH],
+ * RMSNorm weight w (NULL: unnormed, then y1/r1/r2/dwp unused).  Replaces
+ * graph_reduce_multi + global_bwd (2 launches) + mlp_bwd (2) + lin_t. */
+typedef struct {
+  int G, NF, NC, F;
+  const float* pend[4];
+  int pend_n[4];
+  int npend;
+  const float *V, *w, *y1, *r1, *r2, *gZ, *gW1, *gW2;
+  int gH;
+  float *gu_up, *gV, *gdZ, *dwp, *gu, *g_xs, *g_xt;
+  const float *Yp, *mu, *var, *gamma, *Z, *W1, *W2, *Wt2;
+  float eps;
+  float *dgamma, *dbeta, *dYp, *dZ, *gxt_in, *g_agg, *gu_t, *g_hsum;
+} pfsgnn_class_bwd;
+int pfsgnn_target_class_bwd(const pfsgnn_class_bwd* a, void* ws, size_t ws_bytes, void* stream);
+size_t pfsgnn_class_bwd_bytes(void);
 /* device-wide barrier time-outs since load (a diagnostic; *n = count) */
 int pfsgnn_sync_faults(unsigned* n);
 /* One row block of an input-gradient output: rows `rows` of dX go to x

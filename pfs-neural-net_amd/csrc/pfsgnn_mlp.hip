@@ -777,10 +777,14 @@ __device__ void grid_sync(unsigned nb) {
 
 #ifdef PF_TAIL_STAMPS   // (diagnostic build: per-workgroup phase clocks, tools/tail_stamps.py)
 __device__ unsigned long long pf_tail_stamps[512][8];
+__device__ unsigned long long pf_cb_stamps[512][8];
 #define TAIL_STAMP(i) \
   if (threadIdx.x == 0) pf_tail_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime();
+#define CB_STAMP(i) \
+  if (threadIdx.x == 0) pf_cb_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime();
 #else
 #define TAIL_STAMP(i)
+#define CB_STAMP(i)
 #endif
 
 struct TailArgs {
@@ -1081,6 +1085,287 @@ __global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
     __syncthreads();   // (LDS reuse by the next unit)
   }
   TAIL_STAMP(6)
+}
+
+// ---------------------------------------------------------------- fused class backward
+// pfsgnn_target_class_bwd: the class side of a block's backward in one launch
+// (include/pfsgnn.h), units of CB_CLS classes of one graph, three phases
+// around two device-wide barriers (the per-graph u-gradient sums feed the
+// GlobalModel backward; TModel's BatchNorm sums need every class).
+constexpr int CB_CLS = 16;
+constexpr int CB_PLEN = 32;   // BatchNorm-sum partial: sg[16], sx[16]
+
+struct CbArgs {
+  pfsgnn_class_bwd a;
+  int QB, nunits;
+  float *p1, *p2;   // [nunits][F] u-gradient partials, [nunits][CB_PLEN] BatchNorm sums
+};
+
+template <int F>
+__global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
+  constexpr int C2 = 2 * F, K = 4 * F, H = 4 * F, K3 = 3 * F;
+  const pfsgnn_class_bwd& A = T.a;
+  const int t = threadIdx.x, G = A.G, NC = A.NC, NF = A.NF;
+  const long long NT = (long long)G * NC, NS = (long long)G * NF;
+  CB_STAMP(0)
+  __shared__ float w1[H * K], w2[F * H], wt2[C2 * C2];
+  __shared__ float gw1[CG_GW1], gw2[F * CG_MAXH];
+  const bool gws = A.gH * K3 <= CG_GW1;
+  {  // every weight load in flight before the LDS stores
+    constexpr int N1 = (H * K + 255) / 256, N2 = (F * H + 255) / 256, N3 = (C2 * C2 + 255) / 256;
+    constexpr int NG1 = (CG_GW1 + 255) / 256, NG2 = (F * CG_MAXH + 255) / 256;
+    float v1[N1], v2[N2], v3[N3], g1[NG1], g2[NG2];
+    const int ng1 = gws ? A.gH * K3 : 0, ng2 = gws ? F * A.gH : 0;
+#pragma unroll
+    for (int i = 0; i < N1; ++i) v1[i] = t + 256 * i < H * K ? A.W1[t + 256 * i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < N2; ++i) v2[i] = t + 256 * i < F * H ? A.W2[t + 256 * i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < N3; ++i) v3[i] = t + 256 * i < C2 * C2 ? A.Wt2[t + 256 * i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NG1; ++i) g1[i] = t + 256 * i < ng1 ? A.gW1[t + 256 * i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NG2; ++i) g2[i] = t + 256 * i < ng2 ? A.gW2[t + 256 * i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < N1; ++i) if (t + 256 * i < H * K) w1[t + 256 * i] = v1[i];
+#pragma unroll
+    for (int i = 0; i < N2; ++i) if (t + 256 * i < F * H) w2[t + 256 * i] = v2[i];
+#pragma unroll
+    for (int i = 0; i < N3; ++i) if (t + 256 * i < C2 * C2) wt2[t + 256 * i] = v3[i];
+#pragma unroll
+    for (int i = 0; i < NG1; ++i) if (t + 256 * i < ng1) gw1[t + 256 * i] = g1[i];
+#pragma unroll
+    for (int i = 0; i < NG2; ++i) if (t + 256 * i < ng2) gw2[t + 256 * i] = g2[i];
+  }
+  __shared__ float red[4][F];
+  CB_STAMP(1)
+  // ---------------------------------------------------------------- phase 1
+  // the unit's share of its graph's sums of the pending u[batch] gradients
+  for (int un = blockIdx.x; un < T.nunits; un += gridDim.x) {
+    const int g = un / T.QB, q = un - g * T.QB;
+    float s[F];
+#pragma unroll
+    for (int o = 0; o < F; ++o) s[o] = 0.f;
+    for (int i = 0; i < A.npend; ++i) {
+      const int n = A.pend_n[i];
+      const int b0 = (int)(((long long)n * q) / T.QB), b1 = (int)(((long long)n * (q + 1)) / T.QB);
+      const float* X = A.pend[i];
+      const long long ld = (long long)G * n;
+      for (int j = b0 + t; j < b1; j += 256) {
+#pragma unroll
+        for (int o = 0; o < F; ++o) s[o] += X[(size_t)o * ld + (size_t)g * n + j];
+      }
+    }
+    const int wv = t >> 6, ln = t & 63;
+#pragma unroll
+    for (int o = 0; o < F; ++o) {
+      const float v = wave_sum(s[o]);
+      if (ln == 0) red[wv][o] = v;
+    }
+    __syncthreads();
+    if (t < F) T.p1[(size_t)un * F + t] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    __syncthreads();
+  }
+  CB_STAMP(2)
+  grid_sync(gridDim.x);
+  CB_STAMP(3)
+  // ---------------------------------------------------------------- phase 2
+  __shared__ float sdy[F], sy1[F], sv[F], sw[F], sdw[F], gv[F], d1[F];
+  __shared__ float dzg[CG_MAXH], dh[CG_MAXH];
+  for (int un = blockIdx.x; un < T.nunits; un += gridDim.x) {
+    const int g = un / T.QB, q = un - g * T.QB;
+    if (t < F) {
+      float sacc = A.gu_up[(size_t)t * G + g];
+      for (int qq = 0; qq < T.QB; ++qq) sacc += T.p1[(size_t)(g * T.QB + qq) * F + t];
+      sdy[t] = sacc;
+      if (A.w) {
+        sy1[t] = A.y1[(size_t)t * G + g];
+        sv[t] = A.V[(size_t)t * G + g];
+        sw[t] = A.w[t];
+      }
+    }
+    __syncthreads();
+    // GlobalModel backward (k_global_bwd's arithmetic): RMSNorm twice, then the MLP
+    if (!A.w) {
+      if (t < F) gv[t] = sdy[t];
+    } else if (t == 0) {
+      const float a = A.r1[g], b = A.r2[g];
+      float dot = 0.f;
+      for (int c = 0; c < F; ++c) {
+        const float dy = sdy[c], x = sy1[c];
+        sdw[c] = dy * x * b;
+        dot += dy * sw[c] * x;
+      }
+      float dot2 = 0.f;
+      for (int c = 0; c < F; ++c) {
+        const float dy = sdy[c], x1 = sy1[c];
+        const float qv = b * dy * sw[c] - x1 * b * b * b * dot / F;
+        d1[c] = qv;
+        const float x0 = sv[c];
+        sdw[c] += qv * x0 * a;
+        dot2 += qv * sw[c] * x0;
+      }
+      for (int c = 0; c < F; ++c) {
+        const float x0 = sv[c];
+        gv[c] = a * d1[c] * sw[c] - x0 * a * a * a * dot2 / F;
+      }
+    }
+    __syncthreads();
+    if (q == 0 && t < F) {
+      if (A.w) A.dwp[(size_t)t * G + g] = sdw[t];
+      A.gV[(size_t)t * G + g] = gv[t];
+    }
+    for (int j = t; j < A.gH; j += 256) {
+      float acc = 0.f;
+      for (int o = 0; o < F; ++o) acc = fmaf(gws ? gw2[o * A.gH + j] : A.gW2[(size_t)o * A.gH + j], gv[o], acc);
+      const float qv = acc * dlrelu(A.gZ[(size_t)j * G + g]);
+      dzg[j] = qv;
+      if (q == 0) A.gdZ[(size_t)j * G + g] = qv;
+    }
+    __syncthreads();
+    for (int k = t; k < K3; k += 256) {
+      float acc = 0.f;
+      for (int j = 0; j < A.gH; ++j)
+        acc = fmaf(gws ? gw1[j * K3 + k] : A.gW1[(size_t)j * K3 + k], dzg[j], acc);
+      dh[k] = acc;
+    }
+    __syncthreads();
+    if (q == 0 && t < F) A.gu[(size_t)t * G + g] += dh[t];
+    // the means' gradients broadcast: x_s over the unit's fiber share, x_t over its classes
+    {
+      const int f0 = (int)(((long long)NF * q) / T.QB), f1 = (int)(((long long)NF * (q + 1)) / T.QB);
+      const int nf = f1 - f0;
+      for (int i = t; i < nf * F; i += 256) {
+        const int o = i / nf, f = f0 + (i - o * nf);
+        float* p = A.g_xs + (size_t)o * NS + (size_t)g * NF + f;
+        *p = *p + dh[F + o] * (1.0f / (float)NF);
+      }
+    }
+    const int c0 = q * CB_CLS, ncl = min(CB_CLS, NC - c0);
+    const long long nb = (long long)g * NC + c0;
+    // TModel's BatchNorm sums on the updated g_xt (k_bn_sums_part's arithmetic)
+    float sg = 0.f, sx = 0.f;
+    if (t < F * CB_CLS) {
+      const int o = t / CB_CLS, cl = t - o * CB_CLS;
+      if (cl < ncl) {
+        float* p = A.g_xt + (size_t)o * NT + nb + cl;
+        const float v = *p + dh[2 * F + o] * (1.0f / (float)NC);
+        *p = v;
+        const float ic = 1.0f / sqrtf(A.var[o] + A.eps);
+        sg = v;
+        sx = v * ((A.Yp[(size_t)o * NT + nb + cl] - A.mu[o]) * ic);
+      }
+    }
+    // per channel over the unit's classes: 16 consecutive lanes hold one channel
+#pragma unroll
+    for (int off = 1; off < CB_CLS; off <<= 1) {
+      sg += __shfl_xor(sg, off);
+      sx += __shfl_xor(sx, off);
+    }
+    if (t < F * CB_CLS && (t % CB_CLS) == 0) {
+      const int o = t / CB_CLS;
+      T.p2[(size_t)un * CB_PLEN + o] = sg;
+      T.p2[(size_t)un * CB_PLEN + 16 + o] = sx;
+    }
+    __syncthreads();   // (LDS reuse by the next unit)
+  }
+  CB_STAMP(4)
+  grid_sync(gridDim.x);
+  CB_STAMP(5)
+  // ---------------------------------------------------------------- phase 3
+  __shared__ float BC[5][16];
+  __shared__ float mg[16][16], mx[16][16];
+  {  // the units' sums merged in one fixed order: 16 subsets of units (loads
+     // of a subset in flight together), then the subsets in order
+    const int o = t & 15, u0 = t >> 4;
+    float sg = 0.f, sx = 0.f;
+    for (int u = u0; u < T.nunits; u += 64) {
+      float a[4], b[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int uu = u + 16 * e;
+        a[e] = uu < T.nunits ? T.p2[(size_t)uu * CB_PLEN + o] : 0.f;
+        b[e] = uu < T.nunits ? T.p2[(size_t)uu * CB_PLEN + 16 + o] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sg += a[e];
+        sx += b[e];
+      }
+    }
+    mg[u0][o] = sg;
+    mx[u0][o] = sx;
+  }
+  __syncthreads();
+  if (t < F) {
+    float sg = 0.f, sx = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      sg += mg[k][t];
+      sx += mx[k][t];
+    }
+    const float inv = 1.0f / sqrtf(A.var[t] + A.eps);
+    BC[0][t] = A.gamma[t] * inv;
+    BC[1][t] = sg / (float)NT;
+    BC[2][t] = sx / (float)NT;
+    BC[3][t] = A.mu[t];
+    BC[4][t] = inv;
+    if (blockIdx.x == 0) {
+      A.dgamma[t] += sx;
+      A.dbeta[t] += sg;
+    }
+  }
+  __shared__ float gp[CB_CLS][F + 1], dzl[CB_CLS][H + 1], gag[CB_CLS][C2 + 1];
+  __syncthreads();
+  for (int un = blockIdx.x; un < T.nunits; un += gridDim.x) {
+    const int g = un / T.QB, q = un - g * T.QB;
+    const int c0 = q * CB_CLS, ncl = min(CB_CLS, NC - c0);
+    const long long nb = (long long)g * NC + c0;
+    for (int i = t; i < ncl * F; i += 256) {
+      const int o = i / ncl, cl = i - o * ncl;
+      const size_t e = (size_t)o * NT + nb + cl;
+      const float v = BC[0][o] * (A.g_xt[e] - BC[1][o] - (A.Yp[e] - BC[3][o]) * BC[4][o] * BC[2][o]);
+      A.dYp[e] = v;
+      gp[cl][o] = v;
+    }
+    __syncthreads();
+    for (int i = t; i < ncl * H; i += 256) {
+      const int h = i / ncl, cl = i - h * ncl;
+      float acc = 0.f;
+#pragma unroll
+      for (int o = 0; o < F; ++o) acc = fmaf(w2[o * H + h], gp[cl][o], acc);
+      const size_t e = (size_t)h * NT + nb + cl;
+      const float v = acc * dlrelu(A.Z[e]);
+      A.dZ[e] = v;
+      dzl[cl][h] = v;
+    }
+    __syncthreads();
+    for (int i = t; i < ncl * K; i += 256) {
+      const int k = i / ncl, cl = i - k * ncl;
+      float acc = 0.f;
+#pragma unroll
+      for (int h = 0; h < H; ++h) acc = fmaf(w1[h * K + k], dzl[cl][h], acc);
+      if (k < F) {
+        float* p = A.gxt_in + (size_t)k * NT + nb + cl;
+        *p = *p + acc;
+      } else if (k < 3 * F) {
+        A.g_agg[(size_t)(k - F) * NT + nb + cl] = acc;
+        gag[cl][k - F] = acc;
+      } else {
+        A.gu_t[(size_t)(k - 3 * F) * NT + nb + cl] = acc;
+      }
+    }
+    __syncthreads();
+    for (int i = t; i < ncl * C2; i += 256) {
+      const int j = i / ncl, cl = i - j * ncl;
+      float acc = 0.f;
+#pragma unroll
+      for (int m = 0; m < C2; ++m) acc = fmaf(wt2[m * C2 + j], gag[cl][m], acc);
+      A.g_hsum[(size_t)j * NT + nb + cl] = acc;
+    }
+    __syncthreads();   // (LDS reuse by the next unit)
+  }
+  CB_STAMP(6)
 }
 
 // ============================================================ backward
@@ -1591,11 +1876,52 @@ int class_tail_fwd(const pfsgnn_block_tail& a, const float* cpart, int BPG, floa
 }  // namespace pf
 
 #ifdef PF_TAIL_STAMPS
+extern "C" int pfsgnn_debug_cb_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_cb_stamps), sizeof(unsigned long long) * 512 * 8) ==
+                 hipSuccess ? 0 : -1;
+}
 extern "C" int pfsgnn_debug_tail_stamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(pf_tail_stamps), sizeof(unsigned long long) * 512 * 8) ==
                  hipSuccess ? 0 : -1;
 }
 #endif
+
+extern "C" size_t pfsgnn_class_bwd_bytes(void) { return sizeof(pfsgnn_class_bwd); }
+
+extern "C" int pfsgnn_target_class_bwd(const pfsgnn_class_bwd* a, void* ws, size_t ws_bytes,
+                                       void* stream) {
+  const char* where = "pfsgnn_target_class_bwd";
+  PF_REQUIRE(a && a->G > 0 && a->NF > 0 && a->NC > 0, where, "bad arguments");
+  PF_REQUIRE(a->npend >= 0 && a->npend <= 4, where, "at most 4 pending tables");
+  for (int i = 0; i < a->npend; ++i)
+    PF_REQUIRE(a->pend[i] && (a->pend_n[i] == a->NF || a->pend_n[i] == a->NC), where,
+               "pending tables are per fiber or per class");
+  PF_REQUIRE(a->V && a->gZ && a->gW1 && a->gW2 && a->gu_up && a->gV && a->gdZ && a->gu &&
+                 a->g_xs && a->g_xt && a->Yp && a->mu && a->var && a->gamma && a->Z && a->W1 &&
+                 a->W2 && a->Wt2 && a->dgamma && a->dbeta && a->dYp && a->dZ && a->gxt_in &&
+                 a->g_agg && a->gu_t && a->g_hsum,
+             where, "null");
+  PF_REQUIRE(a->gH > 0 && a->gH <= CG_MAXH && 3 * a->F <= CG_MAXH, where, "GlobalModel width <= 192");
+  PF_REQUIRE(!a->w || (a->y1 && a->r1 && a->r2 && a->dwp), where, "RMSNorm needs y1, r1, r2, dwp");
+  CbArgs T{};
+  T.a = *a;
+  T.QB = (a->NC + CB_CLS - 1) / CB_CLS;
+  T.nunits = a->G * T.QB;
+  PF_REQUIRE(T.nunits <= 4096, where, "too many class units");
+  const size_t need = ((size_t)T.nunits * a->F + (size_t)T.nunits * CB_PLEN) * sizeof(float);
+  PF_REQUIRE(ws && ws_bytes >= need, where, "workspace too small");
+  T.p1 = static_cast<float*>(ws);
+  T.p2 = T.p1 + (size_t)T.nunits * a->F;
+  const int grid = std::min(T.nunits, cu_count());
+  hipStream_t st = as_stream(stream);
+  switch (a->F) {
+    case 8: hipLaunchKernelGGL(k_class_bwd<8>, dim3(grid), dim3(256), 0, st, T); break;
+    case 10: hipLaunchKernelGGL(k_class_bwd<10>, dim3(grid), dim3(256), 0, st, T); break;
+    case 16: hipLaunchKernelGGL(k_class_bwd<16>, dim3(grid), dim3(256), 0, st, T); break;
+    default: return pf::fail(where, "Fdim must be 8, 10 or 16");
+  }
+  return pf::check_launch(where);
+}
 
 extern "C" int pfsgnn_sync_faults(unsigned* n) {
   PF_REQUIRE(n, "pfsgnn_sync_faults", "null");

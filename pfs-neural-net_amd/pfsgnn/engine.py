@@ -256,6 +256,9 @@ class Engine:
 
     def _gu_flush(self, G):
         pend, self._gu_pend = getattr(self, "_gu_pend", None) or [], []
+        self._gu_flush_list(pend, G)
+
+    def _gu_flush_list(self, pend, G):
         for i in range(0, len(pend), 4):
             part = pend[i:i + 4]
             assert all(t is part[0][1] for _, t in part)
@@ -501,6 +504,42 @@ class Engine:
         st["parts_t"] = (r["Pt"], r["Qt"])
         return st
 
+    def _class_bwd_ok(self, d, su, stt):
+        """The fused class backward's conditions: a complete batch, training
+        BatchNorm, the fused forward tail's GlobalModel state."""
+        sT = stt.get("sT")
+        return (d.sp is None and self.normed and self.F in (8, 10, 16)
+                and hasattr(self.be, "target_class_bwd") and su.get("fused")
+                and sT is not None and sT[2] is not None and sT[2][0] != "eval"
+                and os.environ.get("PFSGNN_CLASS_BWD", "1") != "0")
+
+    def _class_bwd(self, P, Gr, d, p, su, stt, pend, g_u, g_xs_new, g_xt_new, g_xt_in, g_u_in):
+        """global_bwd + target_node_bwd (and the block above's u-gradient flush)
+        as one launch (pfsgnn_target_class_bwd); their weight gradients stay
+        deferred jobs.  -> g_hsum."""
+        be, F, G = self.be, self.F, d.G
+        pg, pt = p + "global_model.", p + "t_model."
+        m2 = pt + "node_mlp_2."
+        segsU, Zg, _ = su["sU"]
+        hT, ZT, (Yp, mu, var, key) = stt["sT"]
+        w = P[pg + "norm.weight"]
+        gH = P[pg + "0.weight"].shape[0]
+        gV, gdZ, dwp = be.empty(F, G), be.empty(gH, G), be.empty(F, G)
+        r = be.target_class_bwd(d, pend, g_u, su["v"], w, su["rms"], Zg, P[pg + "0.weight"],
+                                P[pg + "2.weight"], gV, gdZ, dwp, g_u_in, g_xs_new, g_xt_new, Yp,
+                                mu, var, P[key + "weight"], self.bn_eps, Gr[key + "weight"],
+                                Gr[key + "bias"], ZT, P[m2 + "0.weight"], P[m2 + "2.weight"],
+                                P[pt + "node_mlp_1.2.weight"], g_xt_in)
+        be.wgrad(gV, Zg, Gr[pg + "2.weight"], db=Gr[pg + "2.bias"], act_in=True)
+        be.wgrad_cat(gdZ, segsU, Gr[pg + "0.weight"], db=Gr[pg + "0.bias"])
+        be.wgrad(dwp, be._ones_row(G), Gr[pg + "norm.weight"].view(F, 1))
+        be.wgrad(r["dYp"], ZT, Gr[m2 + "2.weight"], db=Gr[m2 + "2.bias"], act_in=True)
+        be.wgrad_cat(r["dZ"], hT, Gr[m2 + "0.weight"], db=Gr[m2 + "0.bias"])
+        self._gu_add(r["gu_t"], G, g_u_in)
+        be.wgrad(r["g_agg"], stt["hsum"], Gr[pt + "node_mlp_1.2.weight"],
+                 db=Gr[pt + "node_mlp_1.2.bias"], dbscale=float(d.NF))
+        return r["g_hsum"]
+
     def target_node_bwd(self, P, Gr, d, pre, st, g_xt_new, g_xt, g_u):
         be, F, G = self.be, self.F, d.G
         g_agg = be.empty(2 * F, d.NT)
@@ -643,6 +682,7 @@ class Engine:
         be, F = self.be, self.F
         g_xs, g_xt, g_xe, g_u = g_xs_out, g_xt_out, g_xe_out, g_u_out
         self._gu_pend = []
+        prev_pend = []     # the block above's pending u[batch] gradients
         stride = (F * (d.NS + d.NT + d.G) + 63) // 64 * 64     # 256-byte aligned slices
         acc_all = be.zeros(self.B * stride)
         for b in reversed(range(self.B)):
@@ -667,13 +707,25 @@ class Engine:
                 own = b < self.B - 1
                 g_xs_new = be.zeros(F, d.NS) if g_xs is None else (g_xs if own else g_xs.clone())
                 g_xt_new = be.zeros(F, d.NT) if g_xt is None else (g_xt if own else g_xt.clone())
-                if g_u is not None:
-                    self.global_bwd(P, Gr, d, p + "global_model.", su, g_u, g_xs_new, g_xt_new,
-                                    g_u_in)
                 tpart = None
+                if (g_u is not None and live_t and len(prev_pend) <= 4
+                        and all(tg is g_u for _, tg in prev_pend)
+                        and self._class_bwd_ok(d, su, stt)):
+                    # the block's whole class side in one launch; it also sums the
+                    # block above's pending u[batch] gradients into g_u
+                    g_hsum = self._class_bwd(P, Gr, d, p, su, stt, [X for X, _ in prev_pend],
+                                             g_u, g_xs_new, g_xt_new, g_xt_in, g_u_in)
+                    prev_pend = []
+                else:
+                    self._gu_flush_list(prev_pend, d.G)
+                    prev_pend = []
+                    if g_u is not None:
+                        self.global_bwd(P, Gr, d, p + "global_model.", su, g_u, g_xs_new,
+                                        g_xt_new, g_u_in)
+                    if live_t:
+                        g_hsum = self.target_node_bwd(P, Gr, d, p + "t_model.", stt, g_xt_new,
+                                                      g_xt_in, g_u_in)
                 if live_t:
-                    g_hsum = self.target_node_bwd(P, Gr, d, p + "t_model.", stt, g_xt_new, g_xt_in,
-                                                  g_u_in)
                     self.target_edge_bwd(P, Gr, d, p + "t_model.", stt, g_hsum, False, g_xs_new)
                     tpart = (stt["Rs"], P[p + "t_model.node_mlp_1.0.weight"], g_hsum)
                 coef = self.source_node_bwd(P, Gr, d, p + "s_model.", ss, g_xs_new, g_xs_in, g_u_in)
@@ -696,8 +748,12 @@ class Engine:
                     bnc = self.edge_bn_coef(P, Gr, d, p + "edge_model.", se, Sg, Sgx)
             g_xe = self.edge_bwd(P, Gr, d, p + "edge_model.", se, g_tot, bnc, b > 0,
                                  g_xs_in, g_xt_in, g_u_in)
-            self._gu_flush(d.G)                  # the block's u[batch] gradients, one launch
+            # the block's u[batch] gradients: summed per graph by the next block's
+            # class backward, or in one launch before its GlobalModel reads them
+            self._gu_flush_list(prev_pend, d.G)
+            prev_pend, self._gu_pend = self._gu_pend, []
             g_xs, g_xt, g_u = g_xs_in, g_xt_in, g_u_in
+        self._gu_flush_list(prev_pend, d.G)
         s_enc, t_enc = ctx["enc"]
         self.mlp_bwd(P, Gr, "encoder_s.", g_xs, s_enc)
         self.mlp_bwd(P, Gr, "encoder_t.", g_xt, t_enc)

@@ -112,6 +112,17 @@ def _ptrs(*names):
     return [(n, ctypes.c_void_p) for n in names]
 
 
+class ClassBwd(ctypes.Structure):
+    """pfsgnn_class_bwd (include/pfsgnn.h): a block's class-side backward."""
+    _fields_ = ([("G", I), ("NF", I), ("NC", I), ("F", I), ("pend", ctypes.c_void_p * 4),
+                 ("pend_n", I * 4), ("npend", I)]
+                + _ptrs("V", "w", "y1", "r1", "r2", "gZ", "gW1", "gW2") + [("gH", I)]
+                + _ptrs("gu_up", "gV", "gdZ", "dwp", "gu", "g_xs", "g_xt",
+                        "Yp", "mu", "var", "gamma", "Z", "W1", "W2", "Wt2")
+                + [("eps", FL)]
+                + _ptrs("dgamma", "dbeta", "dYp", "dZ", "gxt_in", "g_agg", "gu_t", "g_hsum"))
+
+
 class BlockTail(ctypes.Structure):
     """pfsgnn_block_tail (include/pfsgnn.h): a block tail on a complete batch."""
     _fields_ = ([("G", I), ("NF", I), ("NC", I), ("F", I)]
@@ -217,6 +228,8 @@ _SIGS = {
     "pfsgnn_target_block_fwd": ([ctypes.POINTER(BlockTail), P, SZ, P], I),
     "pfsgnn_sync_faults": ([ctypes.POINTER(ctypes.c_uint)], I),
     "pfsgnn_block_tail_bytes": ([], SZ),
+    "pfsgnn_target_class_bwd": ([ctypes.POINTER(ClassBwd), P, SZ, P], I),
+    "pfsgnn_class_bwd_bytes": ([], SZ),
     "pfsgnn_bn_eval_bwd_coef": ([P, P, P, P, I, FL, I, P, P, P, P, P, P, P], I),
     "pfsgnn_sliced_plan_ws_bytes": ([I, I], SZ),
     "pfsgnn_sliced_plan": ([P, I, I, P, P, P, P, P, P, SZ, P], I),
@@ -704,6 +717,35 @@ class HipBackend:
         ws, wsb = self._wsargs(d)
         _call("pfsgnn_target_block_fwd", ctypes.byref(a), ws, wsb, _stream())
         r["rms"], r["Pt"], r["Qt"] = rms, Pt, Qt
+        return r
+
+    def target_class_bwd(self, d, pend, gu_up, V, w, rms, gZ, gW1, gW2, gV, gdZ, dwp, gu, g_xs,
+                         g_xt, Yp, mu, var, gamma, eps, dgamma, dbeta, Z, W1, W2, Wt2, gxt_in):
+        """The class side of a block's backward in one launch
+        (pfsgnn_target_class_bwd): pending u-gradient sums into gu_up, the
+        GlobalModel backward, the means broadcast, TModel node_mlp_2 + BatchNorm
+        backward and g_hsum = Wt2^T g_agg.  -> dict(dYp, dZ, g_agg, gu_t, g_hsum)."""
+        F, NT = d.F, d.NT
+        H = W1.shape[0]
+        assert len(pend) <= 4 and W1.shape == (4 * F, 4 * F) and W2.shape == (F, 4 * F)
+        self._chk(gu_up, V, w, gZ, gW1, gW2, gV, gdZ, dwp, gu, g_xs, g_xt, Yp, mu, var, gamma,
+                  dgamma, dbeta, Z, W1, W2, Wt2, gxt_in, *pend)
+        r = dict(dYp=self.empty(F, NT), dZ=self.empty(H, NT), g_agg=self.empty(2 * F, NT),
+                 gu_t=self.empty(F, NT), g_hsum=self.empty(2 * F, NT))
+        y1, r1, r2 = rms if rms is not None else (None, None, None)
+        a = ClassBwd(G=d.G, NF=d.NF, NC=d.NC, F=F, npend=len(pend), gH=gW1.shape[0],
+                     eps=float(eps))
+        for i, X in enumerate(pend):
+            a.pend[i] = X.data_ptr()
+            a.pend_n[i] = X.shape[1] // d.G
+        for k, v in dict(V=V, w=w, y1=y1, r1=r1, r2=r2, gZ=gZ, gW1=gW1, gW2=gW2, gu_up=gu_up,
+                         gV=gV, gdZ=gdZ, dwp=dwp, gu=gu, g_xs=g_xs, g_xt=g_xt, Yp=Yp, mu=mu,
+                         var=var, gamma=gamma, Z=Z, W1=W1, W2=W2, Wt2=Wt2, dgamma=dgamma,
+                         dbeta=dbeta, dYp=r["dYp"], dZ=r["dZ"], gxt_in=gxt_in,
+                         g_agg=r["g_agg"], gu_t=r["gu_t"], g_hsum=r["g_hsum"]).items():
+            setattr(a, k, _ptr(v))
+        ws, wsb = self._wsargs(d)
+        _call("pfsgnn_target_class_bwd", ctypes.byref(a), ws, wsb, _stream())
         return r
 
     def sync_faults(self):

@@ -49,6 +49,8 @@ def test_block_tail_struct_layout_matches(lib):
     from pfsgnn import native
     assert lib.pfsgnn_block_tail_bytes() == ctypes.sizeof(native.BlockTail)
     assert native.BlockTail.Qt.offset == ctypes.sizeof(native.BlockTail) - 8
+    assert lib.pfsgnn_class_bwd_bytes() == ctypes.sizeof(native.ClassBwd)
+    assert native.ClassBwd.g_hsum.offset == ctypes.sizeof(native.ClassBwd) - 8
 
 
 def test_workspace_query_is_host_only(lib):

@@ -53,4 +53,12 @@ for x in range(2):
     for i, n in ((0, "start"), (3, "arrive"), (4, "exit")):
         v = sub[:, i] - sub[:, 0].min()
         print(f"  xcd {x} {n:7s} min {int(v.min()):7d} median {int(np.median(v)):7d} max {int(v.max()):7d}")
+assert native.lib().pfsgnn_debug_cb_stamps(buf) == 0
+st = np.frombuffer(buf, dtype=np.uint64).reshape(512, 8).astype(np.int64)
+st = st[st[:, 0] > 0]
+names = ["weights", "phase 1", "barrier 1", "phase 2", "barrier 2", "phase 3"]
+print(f"class backward: {len(st)} workgroups; ticks per phase (min / median / max):")
+for i, n in enumerate(names):
+    v = st[:, i + 1] - st[:, i]
+    print(f"  {n:22s} {int(v.min()):8d} {int(np.median(v)):8d} {int(v.max()):8d}")
 print("sync faults:", native.HipBackend().sync_faults())
