@@ -471,6 +471,9 @@ struct BnEpi {
 // BatchNorm1d training forward from the MLP's per-block partials: every block
 // merges them (bn_stats_part), block 0 writes mu / var and the running
 // statistics, all apply the norm (+ the epilogues, thread per node).
+// (OT: the output width when known at compile time -- the epilogue's FMA
+// loops then run over the O live channels instead of 16; 0: any O <= 16)
+template <int OT>
 __global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__ part, int nb,
                                                        int O, int N, const float* __restrict__ Yp,
                                                        const float* __restrict__ gamma,
@@ -507,6 +510,7 @@ __global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__
     }
     return;
   }
+  constexpr int OW = OT ? (OT + 3) / 4 * 4 : 16;   // channels the epilogue multiplies
   for (int n = blockIdx.x * 256 + t; n < N; n += gridDim.x * 256) {
     float y[16];
 #pragma unroll
@@ -525,7 +529,7 @@ __global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__
 #pragma unroll
         for (int j = 0; j < 4; ++j) a[j] = eb[e][k0 + j];
 #pragma unroll
-        for (int o4 = 0; o4 < 16; o4 += 4)
+        for (int o4 = 0; o4 < OW; o4 += 4)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const floatx4 w = *reinterpret_cast<const floatx4*>(&ew[e][(k0 + j) * 16 + o4]);
@@ -1979,8 +1983,17 @@ extern "C" int pfsgnn_mlp_fwd_epi(const pfsgnn_seg* segs, int nseg, int N, const
   PF_REQUIRE(rc == 0, where, "no kernel for this width");
   if (bn) {
     const int ag = std::max(1, std::min(256, (int)(((size_t)O * N + 1023) / 1024)));
-    hipLaunchKernelGGL(k_bn_apply_part, dim3(ag), dim3(256), 0, st, part, grid, O, N, Yp, gamma,
-                       beta, eps, rm, rv, momentum, Y, mu, var, E);
+    // (zero weights pad the channels past O within a 4-channel group: ew rows are
+    // 16 wide with o >= O zero, so OW = round-up(O, 4) is exact)
+    if (O == 10)
+      hipLaunchKernelGGL(k_bn_apply_part<10>, dim3(ag), dim3(256), 0, st, part, grid, O, N, Yp,
+                         gamma, beta, eps, rm, rv, momentum, Y, mu, var, E);
+    else if (O == 8)
+      hipLaunchKernelGGL(k_bn_apply_part<8>, dim3(ag), dim3(256), 0, st, part, grid, O, N, Yp,
+                         gamma, beta, eps, rm, rv, momentum, Y, mu, var, E);
+    else
+      hipLaunchKernelGGL(k_bn_apply_part<0>, dim3(ag), dim3(256), 0, st, part, grid, O, N, Yp,
+                         gamma, beta, eps, rm, rv, momentum, Y, mu, var, E);
   }
   return pf::check_launch(where);
 }

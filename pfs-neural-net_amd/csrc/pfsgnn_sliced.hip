@@ -108,12 +108,17 @@ struct SlRows {
   }
 };
 
-// A wave's class accumulator is [NC][D + 1]: the odd row stride spreads the
-// rows of different classes over the LDS banks (a stride of 20 or 40 words maps
-// every class row onto 16 / 8 bank offsets).
+// A wave's class accumulator is [NC][S]: S = D + 1 (odd: the rows of
+// different classes spread over the LDS banks; a stride of 20 or 40 words maps
+// every class row onto 16 / 8 bank offsets) -- or D + 2 when a lane group's
+// rows come in even runs (RPG even: 4F = 32 / 40 / 64), so a lane's channel
+// pairs are 8-byte aligned and its read-add-writes go as float2 (half the LDS
+// instructions; S / 2 odd spreads the rows over the banks the same way).
+constexpr int acc_stride(int D) { return ((D + 3) / 4) % 2 == 0 ? D + 2 : D + 1; }
 template <int D>
 struct Acc {
-  static constexpr int S = D + 1;
+  static constexpr int S = acc_stride(D);
+  static constexpr bool PAIRS = S == D + 2;
 };
 // The class rows of every graph in ClassRows' slot order in global memory,
 // [G*NC][CP] (k_sl_rows_table): ksl_source_bwd reads its two tables from there
@@ -198,13 +203,30 @@ __device__ __forceinline__ void acc_add(float* wacc, int* own, int cl, bool ev, 
     lds_order();
     const bool win = pend && own[cl] == j;
     if (win) {
+      if constexpr (Acc<D>::PAIRS) {
+        // lane group g's rows g*RPG .. g*RPG + RPG - 1 (RPG even) in slot pairs
 #pragma unroll
-      for (int tt = 0; tt < GM<D>::NT; ++tt)
+        for (int tt = 0; tt < GM<D>::NT; ++tt)
 #pragma unroll
-        for (int r = 0; r < GM<D>::nreg(tt); ++r) {
-          const int h = GM<D>::row(g, 4 * tt + r);
-          if (h >= 0) a[h] += v[tt][r];
-        }
+          for (int r = 0; r < GM<D>::nreg(tt); r += 2) {
+            const int h = GM<D>::row(g, 4 * tt + r);
+            if (h >= 0) {
+              float2* q = reinterpret_cast<float2*>(a + h);
+              float2 u = *q;
+              u.x += v[tt][r];
+              u.y += v[tt][r + 1];
+              *q = u;
+            }
+          }
+      } else {
+#pragma unroll
+        for (int tt = 0; tt < GM<D>::NT; ++tt)
+#pragma unroll
+          for (int r = 0; r < GM<D>::nreg(tt); ++r) {
+            const int h = GM<D>::row(g, 4 * tt + r);
+            if (h >= 0) a[h] += v[tt][r];
+          }
+      }
     }
     lds_order();
     pend = pend && !win;
@@ -1108,7 +1130,7 @@ int sl_source_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, co
 int sl_target_fwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, const float* sc,
                   const float* sh, const float* Rs, const float* Wt1, float* part, uint8_t* tmask,
                   int prec, hipStream_t st) {
-  const size_t lds = (size_t)4 * geo.NC * (2 * F + 1) * sizeof(float);
+  const size_t lds = (size_t)4 * geo.NC * acc_stride(2 * F) * sizeof(float);
 #define SL_C(FF, PP)                                                                        \
   case FF * 8 + PP:                                                                         \
     return sl_launch(ksl_target_fwd<FF, PP>, geo, lds, st, geo, sl, y, sc, sh, Rs, Wt1, part, \
@@ -1142,7 +1164,7 @@ int sl_source_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* y, co
                   const float* Wt1, const float* ghS, const float* g_next, const float* mu1,
                   const float* inv1, float* g_tot, float* pW2, float* pW1, float* pCol,
                   float* pBN, const uint8_t* tmask, float* tabs, int prec, hipStream_t st) {
-  const size_t lds = (size_t)geo.NC * 4 * (2 * F + 1) * sizeof(float);
+  const size_t lds = (size_t)geo.NC * 4 * acc_stride(2 * F) * sizeof(float);
   const bool tm = tmask && Rs;
   // the two class tables in global memory (tabs: 2 * NT * CP floats of workspace)
   const long long tlen = geo.NT * cpg_of(2 * F);
@@ -1171,7 +1193,7 @@ int sl_edge_mlp_bwd(const EdgeGeo& geo, const SlGeo& sl, int F, const float* g_t
                     const float* PtS, const float* W1, const float* W2, float* gxe, float* gs,
                     float* pW2, float* pW1, float* pCol, float* tabs, int prec, hipStream_t st) {
 #ifndef SL_NO_ACC_LDS
-  const size_t lds = tab_lds(geo, 4 * F) + (size_t)geo.NC * 4 * (4 * F + 1) * sizeof(float);
+  const size_t lds = tab_lds(geo, 4 * F) + (size_t)geo.NC * 4 * acc_stride(4 * F) * sizeof(float);
 #else
   const size_t lds = tab_lds(geo, 4 * F);
 #endif
@@ -1197,7 +1219,7 @@ int sl_max_nc(int F, int prec) {
     return (int)std::min<size_t>(n, SL_MAX_NC);
   };
   const size_t tc = kGTab ? 0 : (size_t)cp_of(2 * F) * 4, th = kGTab ? 0 : (size_t)cp_of(4 * F) * 4;
-  const size_t ac = (size_t)4 * (2 * F + 1) * 4, ah = (size_t)4 * (4 * F + 1) * 4;
+  const size_t ac = (size_t)4 * acc_stride(2 * F) * 4, ah = (size_t)4 * acc_stride(4 * F) * 4;
   int m = SL_MAX_NC;
   const int fp = FP(prec);
 #define SL_M(FF, PP)                                                                               \
