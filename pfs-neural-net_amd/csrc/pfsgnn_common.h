@@ -23,6 +23,36 @@ __device__ __forceinline__ pf_cptr pf_fresh(const float* p) {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+// ------------------------------------------------------- bf16x3 operands
+// v = hi + lo (+ ~2^-17 |v|): hi = bf16_rne(v), lo = bf16_rne(v - hi); a
+// product of two split operands as Ah Bl + Al Bh + Ah Bh is ~2^-16 relative
+// (the node-level gradient chains and weight gradients: pfsgnn_node.hip
+// wgrad_block, pfsgnn_mlp.hip k_mlp_bwd).  In the 16x16x32 MFMA a lane's 8
+// K slots are two 4-slot halves, so two hidden tiles -- or the hi and lo
+// planes of one -- concatenate into one operand (pfsgnn_mfma_core.h).
+typedef short pf_s16x4 __attribute__((ext_vector_type(4)));
+typedef short pf_s16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 pf_b16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 pf_b16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ float pf_bf(short x) {
+  return __builtin_bit_cast(float, ((uint32_t)(uint16_t)x) << 16);
+}
+__device__ __forceinline__ void pf_split4(float a, float b, float c, float d, pf_s16x4& h,
+                                          pf_s16x4& l) {
+  const pf_b16x4 hb = {(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
+  h = __builtin_bit_cast(pf_s16x4, hb);
+  const pf_b16x4 lb = {(__bf16)(a - pf_bf(h[0])), (__bf16)(b - pf_bf(h[1])),
+                       (__bf16)(c - pf_bf(h[2])), (__bf16)(d - pf_bf(h[3]))};
+  l = __builtin_bit_cast(pf_s16x4, lb);
+}
+__device__ __forceinline__ pf_s16x8 pf_cat8(pf_s16x4 a, pf_s16x4 b) {
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ floatx4 pf_mf8(pf_s16x8 a, pf_s16x8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(pf_b16x8, a),
+                                                 __builtin_bit_cast(pf_b16x8, b), c, 0, 0, 0);
+}
+
 // ------------------------------------------------------------------ errors
 namespace pf {
 void set_error(const std::string& msg);
@@ -31,6 +61,9 @@ int fail(const char* where, const char* what);
 // workspace in floats
 size_t tail_ws_floats(int G, int NC, int F);
 int check_launch(const char* where);
+// the node level's gradient chains / weight gradients in bf16x3 (pfsgnn_node.hip):
+// env `knob` = 0 / 1 when set, else on for every edge path but the exact-fp32 ones
+bool node_x3(const char* knob);
 // brackets one kernel launch with HIP events when pfsgnn_timing_enable(1)
 // extra back-to-back launches of a named main kernel (pfsgnn_timing_repeat;
 // 0 unless bench.py measures that kernel's in-graph duration)

@@ -1432,6 +1432,15 @@ bool sfwd_tiles() {
   }();
   return on;
 }
+// ... and at most this many classes, one wave per 16 fibers over all of them
+// (PFSGNN_SFWD_WAVE_NC, default 32; 0 = always the 4-wave class split)
+int sfwd_wave_nc() {
+  static const int v = [] {
+    const char* e = getenv("PFSGNN_SFWD_WAVE_NC");
+    return e ? atoi(e) : 32;
+  }();
+  return v;
+}
 int mf_bfy() { return g_path == PFSGNN_EDGE_BF16Y || g_path == PFSGNN_EDGE_BF16 ? 1 : 0; }
 // MFMA blocks stage their class-table rows in LDS: at most MAX_CPS classes each
 EdgeGeo geo_mfma(int G, int NF, int NC) {
@@ -1703,7 +1712,7 @@ static int source_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
   if (use_mfma() && NC <= 256 && sfwd_tiles()) {
     pf::Timer tm_("source_fwd", st);
     if (int rc = pfm::source_fwd_tiles(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs, mf_prec(1, F),
-                                       st))
+                                       sfwd_wave_nc(), st))
       return rc;
     tm_.end();
     return pf::check_launch("pfsgnn_source_fwd");

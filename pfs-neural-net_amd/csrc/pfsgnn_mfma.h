@@ -26,10 +26,12 @@ int source_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
                float* partS, int prec, hipStream_t st);
 // the fiber-tile form (pfsgnn_mfma.hip km_source_fwd_ft): moments straight to
-// mom / hs, no partials; NC <= 256
+// mom / hs, no partials; NC <= 256.  NC <= wave_nc (capped at 64): one wave
+// per 16 fibers over all classes (no in-block merge)
 int source_fwd_tiles(const EdgeGeo& geo, int F, const float* y, const float* sc,
                      const float* sh, const float* QtS, const float* Ws1, const float* Ws2,
-                     const float* bs2, float* mom, float* hs, int prec, hipStream_t st);
+                     const float* bs2, float* mom, float* hs, int prec, int wave_nc,
+                     hipStream_t st);
 // TModel's LeakyReLU mask (pfsgnn_mfma.hip mask_bits): target_fwd writes it
 // when `tmask` is non-null (4 bytes per edge), target_bwd / source_bwd read
 // it in place of recomputing that layer when non-null

@@ -284,8 +284,12 @@ __global__ __launch_bounds__(256) void km_source_fwd(EdgeGeo geo, const float* _
 // launch.  Blocks are mapped XCD-aware: the 8 XCDs take blocks round-robin,
 // so block b runs tile (b % 8) * ceil(nb / 8) + b / 8 -- neighbouring tiles,
 // whose 64-byte rows share 128-byte lines, sit in one XCD's L2.
+// WF (few classes, NC <= MF_SFT_WAVE_MAXNC): a block owns 64 fibers, wave w
+// fibers 16w .. 16w + 15 over every class -- no merge, and the block's setup
+// (class table, weight registers) is shared by 4x the edges.
 #define MF_SFT_MAXNC 256
-template <int F, int PREC>
+#define MF_SFT_WAVE_MAXNC 64
+template <int F, int PREC, bool WF>
 __global__ __launch_bounds__(256) void km_source_fwd_ft(
     EdgeGeo geo, int ntiles, const float* __restrict__ y, const float* __restrict__ sc,
     const float* __restrict__ sh, const float* __restrict__ QtS, const float* __restrict__ Ws1,
@@ -298,11 +302,12 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
   const int g4 = lane >> 4, j16 = lane & 15;
   const int per = (ntiles + 7) >> 3, bx = blockIdx.x;
   const int tile = (bx & 7) * per + (bx >> 3);
-  const int TPG = (geo.NF + 15) >> 4;            // tiles per graph
+  constexpr int TF = WF ? 64 : 16;               // fibers per tile
+  const int TPG = (geo.NF + TF - 1) / TF;        // tiles per graph
   if (tile >= ntiles) return;   // (block-uniform: the grid is rounded up to 8 * per)
   const bool tvalid = true;
   const int gg = tile / TPG, ft = tile - gg * TPG;
-  const int f = ft * 16 + j16;
+  const int f = ft * TF + (WF ? wave * 16 : 0) + j16;
   const bool fvalid = tvalid && f < geo.NF;
   const long long NS = geo.NS, n = (long long)gg * geo.NF + (fvalid ? f : 0);
   const int NC = geo.NC;
@@ -326,7 +331,8 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt) S1[tt] = S2[tt] = S3[tt] = S4[tt] = zero4();
   // Pebay coefficients of the k-th message of a wave (count k + 1), as km_source_fwd
-  const int nk = (NC + 3) >> 2;
+  static_assert(MF_SFT_WAVE_MAXNC <= MF_SFT_MAXNC / 4 + 1, "pco rows");
+  const int nk = WF ? NC : (NC + 3) >> 2;
   if (t < nk) {
     const double nn = t + 1, r = 1.0 / nn;
     pco[t][0] = (float)((nn - 1) * r);
@@ -339,15 +345,15 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
     pco[t][7] = 0.f;
   }
   __syncthreads();   // qtl, pco
-  // wave w: classes w + 4k, k = 0 .. (its count) - 1, streamed as k
-  const int kw = (NC - wave + 3) >> 2;
+  // wave w: classes w + 4k, k = 0 .. (its count) - 1, streamed as k (WF: class k)
+  const int kw = WF ? NC : (NC - wave + 3) >> 2;
   auto load = [&](int k) {
     Rows<1> r;
-    r.v[0] = ld_frows<F>(ry, (uint32_t)(wave + 4 * k) * eoc, ro);
+    r.v[0] = ld_frows<F>(ry, (uint32_t)(WF ? k : wave + 4 * k) * eoc, ro);
     return r;
   };
   class_stream<MF_DEPTH_FWD>(0, kw, load, [&](const Rows<1>& rows, int k) {
-    const int c = wave + 4 * k;
+    const int c = WF ? k : wave + 4 * k;
     const floatx4 x[1] = {edge_in<F>(rows.v[0], fm, sc, scv, shv)};
     floatx4 z[NT], a[NT], m[NT];
 #pragma unroll
@@ -371,6 +377,33 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
         S1[tt][r] = fmaf(d, ca[3], S1[tt][r]);
       }
   });
+  const double invn = 1.0 / (double)NC;
+  // the moments' finalize (k_source_finalize's arithmetic) -> mom / hs
+  auto emit = [&](int o, double mean, double M2, double M3, double M4) {
+    const long long idx = (long long)o * NS + n, CNS = (long long)C * NS;
+    const float c2 = (float)(M2 * invn), c3 = (float)(M3 * invn), c4 = (float)(M4 * invn);
+    mom[idx] = (float)mean;
+    mom[CNS + idx] = c2;
+    mom[2 * CNS + idx] = c3;
+    mom[3 * CNS + idx] = c4;
+    const float var = c2 > 0.f ? c2 : 0.01f * c2;  // F.leaky_relu (slope 0.01), gnn.py:141
+    const float sd = sqrtf(var + 1e-6f);
+    hs[idx] = (float)mean;
+    hs[CNS + idx] = sd;
+    hs[2 * CNS + idx] = c3 / (sd * sd * sd);
+    hs[3 * CNS + idx] = c4 / ((sd * sd) * (sd * sd));
+  };
+  if constexpr (WF) {
+    if (!fvalid) return;
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt)
+#pragma unroll
+      for (int r = 0; r < GM<C>::nreg(tt); ++r) {
+        const int o = GM<C>::row(g4, 4 * tt + r);
+        if (o >= 0) emit(o, S1[tt][r], S2[tt][r], S3[tt][r], S4[tt][r]);
+      }
+    return;
+  }
   // merge: waves 1..3 park their states in LDS (qtl is free once every wave is past its loop)
   __syncthreads();
   float* ms = qtl;   // [3][MS][64]
@@ -389,7 +422,6 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
   }
   __syncthreads();
   if (wave != 0 || !fvalid) return;
-  const double invn = 1.0 / (double)NC;
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
@@ -407,18 +439,7 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
                             p[((3 * NT + tt) * 4 + r) * 64]);
         na += nb;
       }
-      const long long idx = (long long)o * NS + n, CNS = (long long)C * NS;
-      const float c2 = (float)(M2 * invn), c3 = (float)(M3 * invn), c4 = (float)(M4 * invn);
-      mom[idx] = (float)mean;
-      mom[CNS + idx] = c2;
-      mom[2 * CNS + idx] = c3;
-      mom[3 * CNS + idx] = c4;
-      const float var = c2 > 0.f ? c2 : 0.01f * c2;  // F.leaky_relu (slope 0.01), gnn.py:141
-      const float sd = sqrtf(var + 1e-6f);
-      hs[idx] = (float)mean;
-      hs[CNS + idx] = sd;
-      hs[2 * CNS + idx] = c3 / (sd * sd * sd);
-      hs[3 * CNS + idx] = c4 / ((sd * sd) * (sd * sd));
+      emit(o, mean, M2, M3, M4);
     }
 }
 
@@ -1041,14 +1062,21 @@ int source_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const
 
 int source_fwd_tiles(const EdgeGeo& geo, int F, const float* y, const float* sc,
                      const float* sh, const float* QtS, const float* Ws1, const float* Ws2,
-                     const float* bs2, float* mom, float* hs, int prec, hipStream_t st) {
+                     const float* bs2, float* mom, float* hs, int prec, int wave_nc,
+                     hipStream_t st) {
   if (geo.NC > MF_SFT_MAXNC) return pf::fail("pfsgnn mfma", "source_fwd_tiles: NC > 256");
-  const int ntiles = geo.G * ((geo.NF + 15) / 16);
+  const bool wf = geo.NC <= std::min(wave_nc, MF_SFT_WAVE_MAXNC);
+  const int TF = wf ? 64 : 16;
+  const int ntiles = geo.G * ((geo.NF + TF - 1) / TF);
   const int nb = 8 * ((ntiles + 7) / 8);
-#define MF_SFT(FF, PP)                                                                    \
-  case FF * 8 + PP:                                                                       \
-    hipLaunchKernelGGL((km_source_fwd_ft<FF, PP>), dim3(nb), dim3(256), 0, st, geo, ntiles, \
-                       y, sc, sh, QtS, Ws1, Ws2, bs2, mom, hs);                           \
+#define MF_SFT(FF, PP)                                                                     \
+  case FF * 8 + PP:                                                                        \
+    if (wf)                                                                                \
+      hipLaunchKernelGGL((km_source_fwd_ft<FF, PP, true>), dim3(nb), dim3(256), 0, st, geo, \
+                         ntiles, y, sc, sh, QtS, Ws1, Ws2, bs2, mom, hs);                  \
+    else                                                                                   \
+      hipLaunchKernelGGL((km_source_fwd_ft<FF, PP, false>), dim3(nb), dim3(256), 0, st, geo, \
+                         ntiles, y, sc, sh, QtS, Ws1, Ws2, bs2, mom, hs);                  \
     break;
   switch (F * 8 + fwd_prec(prec)) {
     MF_SFT(8, 0) MF_SFT(8, 1) MF_SFT(10, 0) MF_SFT(10, 1) MF_SFT(10, 2) MF_SFT(10, 3)

@@ -1457,7 +1457,13 @@ __device__ __forceinline__ void store_rows(const RowOut* tab, const float* X, in
 // lane writes its rows straight from the MFMA output layout (64-byte row
 // segments) -- the output tiles in groups of 4 and no prefetch of Z, so the
 // kernel fits 256 registers and 2 blocks per CU (LDS: the weight images only).
-template <int M, bool RS>
+// X3 (RS only): both gradient chains, dZ = W2^T dYp and dX = W1^T dZ, on
+// split-bf16 16x16x32 MFMAs (pfsgnn_common.h): the weight images hold
+// [hi | lo] of one K-tile (W2^T; W1^T's odd last hidden tile) or the hi and
+// the lo planes of two hidden tiles (W1^T pairs) in the fp32 images' bytes.
+// Per wave and 16 nodes at M = 7: 18 + 77 bf16 MFMAs (16 cycles) instead of
+// 28 + 196 fp32 ones (32 cycles).
+template <int M, bool RS, bool X3 = false>
 __global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_bwd(
     int K, int N, int H, int O, const float* __restrict__ dY, const float* __restrict__ Yp,
     const float* __restrict__ spart, int nsp, const float* __restrict__ mu,
@@ -1487,11 +1493,37 @@ __global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_bwd(
       const int h = 16 * mt + 4 * (l >> 4) + r, k = 16 * mk + (l & 15);
       v[i] = (want_dx && h < H && k < K) ? W1[(size_t)h * ldw1 + k] : 0.f;
     }
+    if constexpr (X3) {
+      static_assert(!X3 || RS, "X3: the RS form only");
+      short* s2 = reinterpret_cast<short*>(T2);
+      short* s1 = reinterpret_cast<short*>(T1);
 #pragma unroll
-    for (int i = 0; i < M; ++i) sm[t + 256 * i] = w[i];
-    float* t1 = reinterpret_cast<float*>(T1);
+      for (int i = 0; i < M; ++i) {   // T2x[mt][l] = [hi(r) | lo(r)]
+        const int idx = t + 256 * i;
+        const int r = idx & 3, l = (idx >> 2) & 63, mt = idx >> 8;
+        const short h = __builtin_bit_cast(short, (__bf16)w[i]);
+        s2[(mt * 64 + l) * 8 + r] = h;
+        s2[(mt * 64 + l) * 8 + 4 + r] = __builtin_bit_cast(short, (__bf16)(w[i] - pf_bf(h)));
+      }
 #pragma unroll
-    for (int i = 0; i < M * M; ++i) t1[t + 256 * i] = v[i];
+      for (int i = 0; i < M * M; ++i) {   // T1x[mk][slot][l]: pairs [hi | hi'], [lo | lo']; odd last [hi | lo]
+        const int idx = t + 256 * i;
+        const int r = idx & 3, l = (idx >> 2) & 63, mt = (idx >> 8) % M, mk = (idx >> 8) / M;
+        const short h = __builtin_bit_cast(short, (__bf16)v[i]);
+        const short lo = __builtin_bit_cast(short, (__bf16)(v[i] - pf_bf(h)));
+        const bool pair = mt < 2 * (M / 2);
+        const int sh = pair ? (mt & ~1) : mt, sl = pair ? sh + 1 : mt;
+        const int ph = pair ? 4 * (mt & 1) + r : r, pl = pair ? ph : 4 + r;
+        s1[((mk * M + sh) * 64 + l) * 8 + ph] = h;
+        s1[((mk * M + sl) * 64 + l) * 8 + pl] = lo;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < M; ++i) sm[t + 256 * i] = w[i];
+      float* t1 = reinterpret_cast<float*>(T1);
+#pragma unroll
+      for (int i = 0; i < M * M; ++i) t1[t + 256 * i] = v[i];
+    }
   }
   __shared__ RowOut rout[16 * M];   // the input-gradient rows' outputs
   if (want_dx) build_out_rows(outs, K, N, rout);
@@ -1594,7 +1626,18 @@ __global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_bwd(
       if (bn && dYp && nv && o < O) dYp[(size_t)o * N + n] = gp[r];
     }
     floatx4 dz[M];
-    {
+    if constexpr (X3) {
+      const pf_s16x8* T2x = reinterpret_cast<const pf_s16x8*>(T2c);
+      pf_s16x4 gh, gl;
+      pf_split4(gp[0], gp[1], gp[2], gp[3], gh, gl);
+      const pf_s16x8 b1 = pf_cat8(gl, gh), b2 = pf_cat8(gh, pf_s16x4{0, 0, 0, 0});
+#pragma unroll
+      for (int mt = 0; mt < M; ++mt) {
+        const pf_s16x8 a = T2x[mt * 64 + lane];
+        dz[mt] = pf_mf8(a, b1, floatx4{0.f, 0.f, 0.f, 0.f});
+        dz[mt] = pf_mf8(a, b2, dz[mt]);
+      }
+    } else {
       floatx4 w[M];
 #pragma unroll
       for (int mt = 0; mt < M; ++mt) {
@@ -1619,14 +1662,45 @@ __global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_bwd(
       // a 64-row LDS buffer, then written as coalesced 256-byte rows (the
       // block and add flag wave-uniform per row), as below
       constexpr int MG = 4;
+      pf_s16x4 zh[M], zl[M];
+      if constexpr (X3) {
+#pragma unroll
+        for (int mt = 0; mt < M; ++mt) pf_split4(dz[mt][0], dz[mt][1], dz[mt][2], dz[mt][3], zh[mt], zl[mt]);
+      }
 #pragma unroll
       for (int g0 = 0; g0 < M; g0 += MG) {
         const int GN = (M - g0) < MG ? (M - g0) : MG;
         floatx4 dx[MG];
 #pragma unroll
         for (int i = 0; i < MG; ++i) dx[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (X3) {
+          const pf_s16x8* T1x = reinterpret_cast<const pf_s16x8*>(T1c);
 #pragma unroll
-        for (int mt = 0; mt < M; ++mt) {
+          for (int p = 0; p < M / 2; ++p) {
+            const pf_s16x8 bl = pf_cat8(zl[2 * p], zl[2 * p + 1]), bh = pf_cat8(zh[2 * p], zh[2 * p + 1]);
+#pragma unroll
+            for (int i = 0; i < MG; ++i)
+              if (i < GN) {
+                const pf_s16x8 ah = T1x[((g0 + i) * M + 2 * p) * 64 + lane];
+                const pf_s16x8 al = T1x[((g0 + i) * M + 2 * p + 1) * 64 + lane];
+                dx[i] = pf_mf8(ah, bl, dx[i]);
+                dx[i] = pf_mf8(al, bh, dx[i]);
+                dx[i] = pf_mf8(ah, bh, dx[i]);
+              }
+          }
+          if constexpr (M & 1) {
+            const pf_s16x8 b1 = pf_cat8(zl[M - 1], zh[M - 1]), b2 = pf_cat8(zh[M - 1], pf_s16x4{0, 0, 0, 0});
+#pragma unroll
+            for (int i = 0; i < MG; ++i)
+              if (i < GN) {
+                const pf_s16x8 a = T1x[((g0 + i) * M + M - 1) * 64 + lane];
+                dx[i] = pf_mf8(a, b1, dx[i]);
+                dx[i] = pf_mf8(a, b2, dx[i]);
+              }
+          }
+        }
+#pragma unroll
+        for (int mt = 0; mt < (X3 ? 0 : M); ++mt) {
           floatx4 w[MG];   // (no read-ahead: the other block's waves cover the LDS latency)
 #pragma unroll
           for (int i = 0; i < MG; ++i)
@@ -2082,25 +2156,30 @@ extern "C" int pfsgnn_mlp_bwd(const float* dY, int N, const float* Yp, const flo
   const size_t lds = bwd_lds(m);
   const int want_dx = nout > 0 ? 1 : 0;
   const bool rs = bwd_rs(m);
+  // the gradient chains in bf16x3 (RS form): PFSGNN_NODE_DX_X3, pf::node_x3's policy
+  const bool x3 = rs && pf::node_x3("PFSGNN_NODE_DX_X3");
   const int rc = with_tiles(m, [&](auto mc) {
     constexpr int MM = decltype(mc)::value;
-    auto launch = [&](auto rsc) {
+    auto launch = [&](auto rsc, auto x3c) {
       constexpr bool RS = decltype(rsc)::value && MM >= 5;
-      static const size_t stat = static_lds(&k_mlp_bwd<MM, RS>);
+      constexpr bool X3 = decltype(x3c)::value && RS;
+      static const size_t stat = static_lds(&k_mlp_bwd<MM, RS, X3>);
       const int grid = grid_for(N, m, lds + stat);
       static size_t attr = 0;  // dynamic LDS above the 64 KB default must be opted into
       if (lds > 65536 && attr < lds) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mlp_bwd<MM, RS>),
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mlp_bwd<MM, RS, X3>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
           return -3;
         attr = lds;
       }
-      hipLaunchKernelGGL((k_mlp_bwd<MM, RS>), dim3(grid), dim3(256), lds, st, K, N, H, O, dY, Yp,
-                         spart, nsp, mu, var, gamma, eps, dgamma, dbeta, Z, W1, ldw1, W2, dYp, dZ,
-                         OS, want_dx);
+      hipLaunchKernelGGL((k_mlp_bwd<MM, RS, X3>), dim3(grid), dim3(256), lds, st, K, N, H, O, dY,
+                         Yp, spart, nsp, mu, var, gamma, eps, dgamma, dbeta, Z, W1, ldw1, W2, dYp,
+                         dZ, OS, want_dx);
       return 0;
     };
-    return rs ? launch(std::true_type{}) : launch(std::false_type{});
+    if (!rs) return launch(std::false_type{}, std::false_type{});
+    return x3 ? launch(std::true_type{}, std::true_type{})
+              : launch(std::true_type{}, std::false_type{});
   });
   PF_REQUIRE(rc != -3, where, "hipFuncSetAttribute (dynamic LDS) failed");
   PF_REQUIRE(rc == 0, where, "no kernel for this width");

@@ -732,7 +732,15 @@ extern "C" int pfsgnn_gemm_multi(const pfsgnn_gemm_job* jobs, int n, void* strea
 #define WG_XBC 2
 #define WG_ONE 3
 #define WG_NONE 4
-template <int TMAX, int PER>
+// X3 (bf16x3): the chunk is staged as split bf16 planes instead -- row =
+// [64 hi | 64 lo] bf16 in the same 272-byte stride, node 32s + 8kq + q at step
+// s (two v_mfma_f32_16x16x32_bf16 K-steps per chunk, three products each:
+// Ah Bl + Al Bh + Ah Bh, ~2^-16 relative per product, fp32 accumulation;
+// 6 x 16 instead of 16 x 32 MFMA cycles per tile and chunk).  A wave owns a
+// contiguous run of tiles (one dY row tile for many X tiles: its A operand is
+// read once), and db -- a bias gradient a following BatchNorm cancels to ~0 --
+// stays an exact fp32 sum of the staged dY values.
+template <int TMAX, int PER, bool X3 = false>
 __device__ __forceinline__ void wgrad_block(const float* __restrict__ dY, int M, const XSegs& S,
                                             int K, int K1, int N, int act_in, int chunk, int vec,
                                             float* __restrict__ part, int bid) {
@@ -815,6 +823,13 @@ __device__ __forceinline__ void wgrad_block(const float* __restrict__ dY, int M,
     return v;
   };
   float4 buf[PER];
+  float dbs[PER];   // X3: this thread's share of db (its dY items), exact fp32
+#pragma unroll
+  for (int i = 0; i < PER; ++i) dbs[i] = 0.f;
+  const bool xdb = X3 && K1 > K;
+  // tile of (wave, j): X3 contiguous runs, else wave + 8 j
+  const int tpw = (NTILE + WG_WAVES - 1) / WG_WAVES;
+  auto tile_of = [&](int j) { return X3 ? (j < tpw ? wave * tpw + j : NTILE) : wave + WG_WAVES * j; };
   if (n0 < n1) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) buf[i] = fetch(n0, i);
@@ -823,11 +838,54 @@ __device__ __forceinline__ void wgrad_block(const float* __restrict__ dY, int M,
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < PER; ++i)
-      if (kind[i] != WG_NONE) *reinterpret_cast<float4*>(lp[i]) = buf[i];
+      if (kind[i] != WG_NONE) {
+        if constexpr (X3) {
+          const int q = t & 15;
+          short* row = reinterpret_cast<short*>(lp[i] - 4 * q);
+          pf_s16x4 h, l;
+          pf_split4(buf[i].x, buf[i].y, buf[i].z, buf[i].w, h, l);
+          *reinterpret_cast<pf_s16x4*>(row + 4 * q) = h;
+          *reinterpret_cast<pf_s16x4*>(row + 64 + 4 * q) = l;
+          if (xdb && kind[i] == WG_DY) dbs[i] += (buf[i].x + buf[i].y) + (buf[i].z + buf[i].w);
+        } else {
+          *reinterpret_cast<float4*>(lp[i]) = buf[i];
+        }
+      }
     __syncthreads();
     if (c + 64 < n1) {  // next chunk's loads in flight during this chunk's MFMAs
 #pragma unroll
       for (int i = 0; i < PER; ++i) buf[i] = fetch(c + 64, i);
+    }
+    if constexpr (X3) {
+      int mprev = -1;
+      pf_s16x8 ah0, al0, ah1, al1;
+#pragma unroll
+      for (int j = 0; j < TMAX; ++j) {
+        const int tile = tile_of(j);
+        if (tile < NTILE) {
+          const int mt = tile / KT, kt = tile - mt * KT;
+          if (mt != mprev) {
+            const short* pa = reinterpret_cast<const short*>(Sd + (16 * mt + col) * WG_LD) + 8 * kq;
+            ah0 = *reinterpret_cast<const pf_s16x8*>(pa);
+            ah1 = *reinterpret_cast<const pf_s16x8*>(pa + 32);
+            al0 = *reinterpret_cast<const pf_s16x8*>(pa + 64);
+            al1 = *reinterpret_cast<const pf_s16x8*>(pa + 96);
+            mprev = mt;
+          }
+          const short* pb = reinterpret_cast<const short*>(Sx + (16 * kt + col) * WG_LD) + 8 * kq;
+          const pf_s16x8 bh0 = *reinterpret_cast<const pf_s16x8*>(pb);
+          const pf_s16x8 bh1 = *reinterpret_cast<const pf_s16x8*>(pb + 32);
+          const pf_s16x8 bl0 = *reinterpret_cast<const pf_s16x8*>(pb + 64);
+          const pf_s16x8 bl1 = *reinterpret_cast<const pf_s16x8*>(pb + 96);
+          acc[j] = pf_mf8(ah0, bl0, acc[j]);
+          acc[j] = pf_mf8(al0, bh0, acc[j]);
+          acc[j] = pf_mf8(ah0, bh0, acc[j]);
+          acc[j] = pf_mf8(ah1, bl1, acc[j]);
+          acc[j] = pf_mf8(al1, bh1, acc[j]);
+          acc[j] = pf_mf8(ah1, bh1, acc[j]);
+        }
+      }
+      continue;
     }
 #pragma unroll
     for (int j = 0; j < TMAX; ++j) {
@@ -850,24 +908,36 @@ __device__ __forceinline__ void wgrad_block(const float* __restrict__ dY, int M,
   }
 #pragma unroll
   for (int j = 0; j < TMAX; ++j) {
-    const int tile = wave + WG_WAVES * j;
+    const int tile = tile_of(j);
     if (tile < NTILE) {
       const int mt = tile / KT, kt = tile - mt * KT;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = 16 * mt + 4 * kq + r, k = 16 * kt + col;
-        if (m < M && k < K1)
+        if (m < M && k < (xdb ? K : K1))
           part[(size_t)bid * M * K1 + (size_t)m * K1 + k] = acc[j][r];
       }
     }
   }
+  if (xdb) {   // db column: the 16 threads of a dY row, fixed xor tree
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      float v = dbs[i];
+      v += __shfl_xor(v, 8, 16);
+      v += __shfl_xor(v, 4, 16);
+      v += __shfl_xor(v, 2, 16);
+      v += __shfl_xor(v, 1, 16);
+      const int r = (t + i * 64 * WG_WAVES) >> 4;
+      if ((t & 15) == 0 && kind[i] == WG_DY) part[(size_t)bid * M * K1 + (size_t)r * K1 + K] = v;
+    }
+  }
 }
 
-template <int TMAX, int PER>
+template <int TMAX, int PER, bool X3>
 __global__ __launch_bounds__(512) void k_wgrad(const float* __restrict__ dY, int M, XSegs S, int K,
                                                int K1, int N, int act_in, int chunk, int vec,
                                                float* __restrict__ part) {
-  wgrad_block<TMAX, PER>(dY, M, S, K, K1, N, act_in, chunk, vec, part, blockIdx.x);
+  wgrad_block<TMAX, PER, X3>(dY, M, S, K, K1, N, act_in, chunk, vec, part, blockIdx.x);
 }
 
 // Several independent weight gradients in one launch (pfsgnn_wgrad_multi):
@@ -886,7 +956,7 @@ struct WgTable {
 };
 static_assert(sizeof(WgTable) <= 4096, "k_wgrad_multi's job table must fit the kernel arguments");
 
-template <int TMAX, int PER>
+template <int TMAX, int PER, bool X3>
 __global__ __launch_bounds__(512) void k_wgrad_multi(WgTable T) {
   const int b = blockIdx.x;
   int jj = 0;
@@ -894,9 +964,14 @@ __global__ __launch_bounds__(512) void k_wgrad_multi(WgTable T) {
   for (int u = 1; u < WG_MULTI; ++u)
     if (u < T.njob && b >= T.j[u].blk0) jj = u;
   const WgJob& J = T.j[jj];   // read in place from the kernel arguments (a copy spills)
-  wgrad_block<TMAX, PER>(J.dY, J.M, J.S, J.K, J.K1, J.N, J.act_in, J.chunk, J.vec, J.part,
-                         b - J.blk0);
+  wgrad_block<TMAX, PER, X3>(J.dY, J.M, J.S, J.K, J.K1, J.N, J.act_in, J.chunk, J.vec, J.part,
+                             b - J.blk0);
 }
+
+// Node-level weight gradients in bf16x3 (wgrad_block's X3 form) on every edge
+// path except the exact-fp32 ones (PFSGNN_EDGE_MFMA_F32, _VALU, _BF16Y);
+// PFSGNN_NODE_WG_X3=0 keeps the fp32 MFMA form everywhere.
+static bool wg_x3() { return pf::node_x3("PFSGNN_NODE_WG_X3"); }
 
 static int wgrad_blocks(int N) {
   static const int cap = [] {   // tuning knob: PFSGNN_WG_BLOCKS (blocks per weight gradient)
@@ -981,13 +1056,14 @@ static int wgrad_launch(const float* dY, int M, const XSegs& S, int nseg, int K,
   float* part = reinterpret_cast<float*>(ws);
   const dim3 grid(P.nblk), blk(64 * WG_WAVES);
   bool launched = false;
+  const bool x3 = wg_x3() && !(P.tm == 16 && P.per == 16);   // (<16, 16> X3 spills)
 #define PF_WG(T, PP)                                                                           \
   if (P.tm == T && P.per == PP) {                                                              \
-    auto fn = &k_wgrad<T, PP>;                                                                 \
-    static bool attr = false;                                                                  \
-    if (!attr) {                                                                               \
+    auto fn = x3 ? &k_wgrad<T, PP, true> : &k_wgrad<T, PP, false>;                             \
+    static bool attr[2] = {false, false};                                                      \
+    if (!attr[x3]) {                                                                           \
       if (!wg_allow_lds(fn)) return pf::fail(where, "hipFuncSetAttribute");                    \
-      attr = true;                                                                             \
+      attr[x3] = true;                                                                         \
     }                                                                                          \
     hipLaunchKernelGGL(fn, grid, blk, P.lds, st, dY, M, S, K, P.K1, N, act_in, P.chunk, P.vec, \
                        part);                                                                  \
@@ -1139,13 +1215,14 @@ extern "C" int pfsgnn_wgrad_multi(const pfsgnn_wgrad_job* jobs, int n, void* par
       T.njob = m;
       bool launched = false;
       const int tm = PL[i].tm, per = PL[i].per;
+      const bool x3 = wg_x3() && !(tm == 16 && per == 16);   // (<16, 16> X3 spills)
 #define PF_WGM(TT, PP)                                                                    \
   if (tm == TT && per == PP) {                                                            \
-    auto fn = &k_wgrad_multi<TT, PP>;                                                     \
-    static bool attr = false;                                                             \
-    if (!attr) {                                                                          \
+    auto fn = x3 ? &k_wgrad_multi<TT, PP, true> : &k_wgrad_multi<TT, PP, false>;          \
+    static bool attr[2] = {false, false};                                                 \
+    if (!attr[x3]) {                                                                      \
       if (!wg_allow_lds(fn)) return pf::fail(where, "hipFuncSetAttribute");               \
-      attr = true;                                                                        \
+      attr[x3] = true;                                                                    \
     }                                                                                     \
     hipLaunchKernelGGL(fn, dim3(blocks), dim3(64 * WG_WAVES), lds, st, T);                \
     launched = true;                                                                      \
@@ -1162,6 +1239,15 @@ extern "C" int pfsgnn_wgrad_multi(const pfsgnn_wgrad_job* jobs, int n, void* par
              reds[i].out, reds[i].ldo, reds[i].add, reds[i].scale};
   return pfsgnn_reduce_batch(rr.data(), (int)rr.size(), stream);
 }
+
+namespace pf {
+bool node_x3(const char* knob) {
+  const char* e = std::getenv(knob);
+  if (e) return std::atoi(e) != 0;
+  const int p = pfsgnn_get_edge_path();
+  return p != PFSGNN_EDGE_MFMA_F32 && p != PFSGNN_EDGE_VALU && p != PFSGNN_EDGE_BF16Y;
+}
+}  // namespace pf
 
 // ------------------------------------------------- deferred reductions
 namespace pf {
