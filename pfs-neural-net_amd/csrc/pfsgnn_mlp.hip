@@ -380,6 +380,7 @@ __global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_fwd(InSeg
 // (double); `write` (one block) stores mu / var and updates the running
 // statistics (unbiased variance).  -> cf[0][o] = mean, cf[1][o] = 1/sqrt(var +
 // eps), cf[2] = gamma, cf[3] = beta (256 threads; nb <= 512).
+template <bool SC1 = false>   // SC1: the partials were handed over in-launch (grid_sync)
 __device__ void bn_stats_part(const float* __restrict__ part, int nb, int O, int N,
                               const float* __restrict__ gamma, const float* __restrict__ beta,
                               float eps, float* __restrict__ rm, float* __restrict__ rv,
@@ -399,9 +400,15 @@ __device__ void bn_stats_part(const float* __restrict__ part, int nb, int O, int
     for (int i = 0; i < PB; ++i) {  // every load of the round in flight before the sums
       const int b = act ? r * 256 + u + 16 * i : nb;
       const float* p = part + (size_t)(b < nb ? b : 0) * PART_LEN;
-      pc[i] = b < nb ? p[0] : 0.f;
-      pm[i] = b < nb ? p[1 + c] : 0.f;
-      pq[i] = b < nb ? p[17 + c] : 0.f;
+      if constexpr (SC1) {
+        pc[i] = b < nb ? ld_sc1(p) : 0.f;
+        pm[i] = b < nb ? ld_sc1(p + 1 + c) : 0.f;
+        pq[i] = b < nb ? ld_sc1(p + 17 + c) : 0.f;
+      } else {
+        pc[i] = b < nb ? p[0] : 0.f;
+        pm[i] = b < nb ? p[1 + c] : 0.f;
+        pq[i] = b < nb ? p[17 + c] : 0.f;
+      }
     }
   };
   // the partials combined in closed form (fixed order, no serial chain of
@@ -744,34 +751,68 @@ __global__ __launch_bounds__(CG_THREADS) void k_class_global_fwd(ClassGlobalArgs
 //      the mean of x_t from the pre-norm sums -- the norm is affine per
 //      channel) and the next block's Pt / Qt (gnn.py:100, 136) of its classes.
 // One launch for what were reduce_columns_lin + mlp_fwd + class_global_fwd.
+constexpr int CT_QBMAX = 64;                // most units per graph (NC <= 64 * CT)
 constexpr int CT_CLS = 32;                  // most classes per unit (8, 16 or 32: the
                                             // smallest that keeps the units <= 512)
 __device__ unsigned pf_tail_bar[2];         // device-wide barrier: arrivals, generation
 __device__ unsigned pf_sync_fault_count;    // barrier time-outs (diagnostic)
 
 // every workgroup of the grid (all resident: the grid is at most one per CU)
-// waits here; the arrivals publish their global writes (agent-scope release)
-// and the waiters acquire them.  A wait that outlives ~2^24 sleeps is counted
-// and abandoned, so no wave can hang on it.
-__device__ void grid_sync(unsigned nb) {
+// waits here.  A wait that outlives ~2^24 sleeps is counted and abandoned, so
+// no wave can hang on it.
+// Default (fenced = 0): no cache maintenance.  Every byte handed across the
+// barrier is stored and loaded with agent-scope relaxed atomics (global_store /
+// load sc1: st_sc1 / ld_sc1), every wave waits for its stores (vmcnt(0)) before
+// the workgroup barrier, one lane counts the workgroup in with a relaxed
+// agent-scope add, and the last arrival -- told by the value its add returned
+// -- resets the counter (its store completed before the generation moves) and
+// bumps the generation the others poll with sc1 loads (MI355X_MICROARCH.md,
+// the sc1 hand-off table's first row: hipMalloc'd bytes, one workgroup per CU).
+// fenced = 1 (PFSGNN_GRID_SYNC_FENCED=1, A/B): the arrival is an agent-scope
+// acq_rel add and the poll an acquire -- an L2 write-back and an L1 invalidate
+// per workgroup and barrier (grid_sync_probe: 4.6 us at 64 workgroups, 15.6 at
+// 256, growing with the workgroups per XCD).
+__device__ void grid_sync(unsigned nb, int fenced) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned gen = __hip_atomic_load(&pf_tail_bar[1], __ATOMIC_ACQUIRE,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned a = __hip_atomic_fetch_add(&pf_tail_bar[0], 1u, __ATOMIC_ACQ_REL,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-    if (a == nb - 1) {
-      __hip_atomic_store(&pf_tail_bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(&pf_tail_bar[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (fenced) {
+      const unsigned gen = __hip_atomic_load(&pf_tail_bar[1], __ATOMIC_ACQUIRE,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned a = __hip_atomic_fetch_add(&pf_tail_bar[0], 1u, __ATOMIC_ACQ_REL,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      if (a == nb - 1) {
+        __hip_atomic_store(&pf_tail_bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&pf_tail_bar[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        unsigned spins = 0;
+        while (__hip_atomic_load(&pf_tail_bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+          __builtin_amdgcn_s_sleep(4);
+          if (++spins > (1u << 24)) {
+            __hip_atomic_fetch_add(&pf_sync_fault_count, 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
     } else {
-      unsigned spins = 0;
-      while (__hip_atomic_load(&pf_tail_bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-        __builtin_amdgcn_s_sleep(4);
-        if (++spins > (1u << 24)) {
-          __hip_atomic_fetch_add(&pf_sync_fault_count, 1u, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-          break;
+      const unsigned gen = __hip_atomic_load(&pf_tail_bar[1], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned a = __hip_atomic_fetch_add(&pf_tail_bar[0], 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      if (a == nb - 1) {
+        __hip_atomic_store(&pf_tail_bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the reset lands before the bump
+        __hip_atomic_fetch_add(&pf_tail_bar[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        unsigned spins = 0;
+        while (__hip_atomic_load(&pf_tail_bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1u << 24)) {
+            __hip_atomic_fetch_add(&pf_sync_fault_count, 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
         }
       }
     }
@@ -796,7 +837,8 @@ struct TailArgs {
   const float* cpart;   // [G][BPG][NC][2F] the edge kernel's column partials
   int BPG, CT, QB, nunits;   // CT classes per unit, QB units per graph
   float bscale;
-  float *part, *xss, *yps;   // [nunits][PART_LEN], [nunits][F], [nunits][F]
+  float *part, *xss, *yps;   // [nunits][PART_LEN], [nunits][F], [nunits][F] (sc1 hand-off)
+  int fenced;                // grid_sync form
 };
 
 template <int F>
@@ -924,7 +966,7 @@ __global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
       }
     }
     __syncthreads();
-    if (t < F) T.xss[(size_t)un * F + t] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    if (t < F) st_sc1(T.xss + (size_t)un * F + t, ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t]);
     // agg = Wt2 hsum + bscale bt2 (the MLP input's middle block)
     for (int i = t; i < ncl * C2; i += 256) {
       const int k = i / ncl, cl = i - k * ncl;
@@ -968,24 +1010,44 @@ __global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
           m2 = fmaf(d, v - mean, m2);
           sum += v;
         }
-        pp[1 + t] = mean;
-        pp[17 + t] = m2;
-        T.yps[(size_t)un * F + t] = sum;
+        st_sc1(pp + 1 + t, mean);
+        st_sc1(pp + 17 + t, m2);
+        st_sc1(T.yps + (size_t)un * F + t, sum);
       } else {
-        pp[1 + t] = 0.f;
-        pp[17 + t] = 0.f;
+        st_sc1(pp + 1 + t, 0.f);
+        st_sc1(pp + 17 + t, 0.f);
       }
-      if (t == 0) pp[0] = (float)ncl;
+      if (t == 0) st_sc1(pp, (float)ncl);
     }
     __syncthreads();   // (LDS reuse by the next unit)
   }
   TAIL_STAMP(3)
-  grid_sync(gridDim.x);
+  grid_sync(gridDim.x, T.fenced);
   TAIL_STAMP(4)
   // ---------------------------------------------------------------- phase 2
   __shared__ float cf[4][16];
-  bn_stats_part(T.part, T.nunits, F, (int)NT, A.gamma, A.beta, A.eps, A.rm, A.rv, A.momentum,
-                A.mu, A.var, blockIdx.x == 0, cf);
+  __shared__ float qs[2][CT_QBMAX * F];   // a graph's xss / yps unit sums
+  // the graph's unit sums: every load in flight at once (one memory round
+  // trip, not QB serial ones), then summed in unit order; for the block's
+  // first unit issued before the statistics merge, with its Yp
+  auto stage_qs = [&](int g) {
+    for (int i = t; i < 2 * F * T.QB; i += 256) {
+      const int w = i / (F * T.QB), r = i - w * F * T.QB;
+      qs[w][r] = ld_sc1((w ? T.yps : T.xss) + (size_t)g * T.QB * F + r);
+    }
+  };
+  float yp0 = 0.f;
+  if ((int)blockIdx.x < T.nunits) {
+    const int un = blockIdx.x, g = un / T.QB, q = un - g * T.QB;
+    const int c0 = q * T.CT, ncl = min(T.CT, NC - c0);
+    if (t < ncl * F) {
+      const int o = t / ncl, cl = t - o * ncl;
+      yp0 = A.Yp[(size_t)o * NT + (long long)g * NC + c0 + cl];
+    }
+    stage_qs(g);
+  }
+  bn_stats_part<true>(T.part, T.nunits, F, (int)NT, A.gamma, A.beta, A.eps, A.rm, A.rv, A.momentum,
+                A.mu, A.var, blockIdx.x == 0, cf);   // (its barriers publish qs)
   TAIL_STAMP(5)
   __shared__ float h3[K3], gz[CG_MAXH], vv[F], un3[F], cu[4 * F], zz[F], rs2[2];
   float* xn = &ypl[0][0];   // [CT_CLS][F + 1]: the normalised x_t of the unit
@@ -993,17 +1055,21 @@ __global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
     const int g = un / T.QB, q = un - g * T.QB;
     const int c0 = q * T.CT, ncl = min(T.CT, NC - c0);
     const long long nb = (long long)g * NC + c0;
+    const bool first = un == (int)blockIdx.x;
     for (int i = t; i < ncl * F; i += 256) {
       const int o = i / ncl, cl = i - o * ncl;
-      const float v = (A.Yp[(size_t)o * NT + nb + cl] - cf[0][o]) * (cf[1][o] * cf[2][o]) + cf[3][o];
+      const float y = (first && i == t) ? yp0 : A.Yp[(size_t)o * NT + nb + cl];
+      const float v = (y - cf[0][o]) * (cf[1][o] * cf[2][o]) + cf[3][o];
       A.xt_new[(size_t)o * NT + nb + cl] = v;
       xn[cl * (F + 1) + o] = v;
     }
+    if (!first) stage_qs(g);
+    __syncthreads();
     if (t < F) {
       float sx = 0.f, sy = 0.f;
       for (int qq = 0; qq < T.QB; ++qq) {
-        sx += T.xss[(size_t)(g * T.QB + qq) * F + t];
-        sy += T.yps[(size_t)(g * T.QB + qq) * F + t];
+        sx += qs[0][qq * F + t];
+        sy += qs[1][qq * F + t];
       }
       const float mx = sx / (float)NF;
       const float mt = (sy / (float)NC - cf[0][t]) * (cf[1][t] * cf[2][t]) + cf[3][t];
@@ -1097,12 +1163,14 @@ __global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
 // around two device-wide barriers (the per-graph u-gradient sums feed the
 // GlobalModel backward; TModel's BatchNorm sums need every class).
 constexpr int CB_CLS = 16;
+constexpr int CB_QBMAX = 64;   // most units per graph (NC <= 1024)
 constexpr int CB_PLEN = 32;   // BatchNorm-sum partial: sg[16], sx[16]
 
 struct CbArgs {
   pfsgnn_class_bwd a;
   int QB, nunits;
-  float *p1, *p2;   // [nunits][F] u-gradient partials, [nunits][CB_PLEN] BatchNorm sums
+  float *p1, *p2;   // [nunits][F] u-gradient partials, [nunits][CB_PLEN] BatchNorm sums (sc1)
+  int fenced;       // grid_sync form
 };
 
 template <int F>
@@ -1167,20 +1235,36 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
       if (ln == 0) red[wv][o] = v;
     }
     __syncthreads();
-    if (t < F) T.p1[(size_t)un * F + t] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    if (t < F) st_sc1(T.p1 + (size_t)un * F + t, ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t]);
     __syncthreads();
   }
   CB_STAMP(2)
-  grid_sync(gridDim.x);
+  grid_sync(gridDim.x, T.fenced);
   CB_STAMP(3)
   // ---------------------------------------------------------------- phase 2
   __shared__ float sdy[F], sy1[F], sv[F], sw[F], sdw[F], gv[F], d1[F];
   __shared__ float dzg[CG_MAXH], dh[CG_MAXH];
+  __shared__ float ps1[CB_QBMAX * F];
   for (int un = blockIdx.x; un < T.nunits; un += gridDim.x) {
     const int g = un / T.QB, q = un - g * T.QB;
+    const int c0 = q * CB_CLS, ncl = min(CB_CLS, NC - c0);
+    const long long nb = (long long)g * NC + c0;
+    // the unit's later operands loaded up front (their latency behind the
+    // GlobalModel backward): gZ, and the x_t gradient / Yp / statistics of
+    // the BatchNorm sums below
+    const float gzv = t < A.gH ? A.gZ[(size_t)t * G + g] : 0.f;
+    const int xo = t / CB_CLS, xcl = t - xo * CB_CLS;
+    const bool xlive = t < F * CB_CLS && xcl < ncl;
+    float* const xp = A.g_xt + (size_t)xo * NT + nb + xcl;
+    const float xtv = xlive ? *xp : 0.f;
+    const float ypv = xlive ? A.Yp[(size_t)xo * NT + nb + xcl] : 0.f;
+    const float vrv = xlive ? A.var[xo] : 0.f, muv = xlive ? A.mu[xo] : 0.f;
+    // the graph's unit partials: every load in flight at once, summed in unit order
+    for (int i = t; i < F * T.QB; i += 256) ps1[i] = ld_sc1(T.p1 + (size_t)g * T.QB * F + i);
+    __syncthreads();
     if (t < F) {
       float sacc = A.gu_up[(size_t)t * G + g];
-      for (int qq = 0; qq < T.QB; ++qq) sacc += T.p1[(size_t)(g * T.QB + qq) * F + t];
+      for (int qq = 0; qq < T.QB; ++qq) sacc += ps1[qq * F + t];
       sdy[t] = sacc;
       if (A.w) {
         sy1[t] = A.y1[(size_t)t * G + g];
@@ -1222,7 +1306,7 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
     for (int j = t; j < A.gH; j += 256) {
       float acc = 0.f;
       for (int o = 0; o < F; ++o) acc = fmaf(gws ? gw2[o * A.gH + j] : A.gW2[(size_t)o * A.gH + j], gv[o], acc);
-      const float qv = acc * dlrelu(A.gZ[(size_t)j * G + g]);
+      const float qv = acc * dlrelu(j == t ? gzv : A.gZ[(size_t)j * G + g]);
       dzg[j] = qv;
       if (q == 0) A.gdZ[(size_t)j * G + g] = qv;
     }
@@ -1236,29 +1320,36 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
     __syncthreads();
     if (q == 0 && t < F) A.gu[(size_t)t * G + g] += dh[t];
     // the means' gradients broadcast: x_s over the unit's fiber share, x_t over its classes
+    // (the read-modify-writes 8 per thread at a time: their loads in flight together)
     {
       const int f0 = (int)(((long long)NF * q) / T.QB), f1 = (int)(((long long)NF * (q + 1)) / T.QB);
-      const int nf = f1 - f0;
-      for (int i = t; i < nf * F; i += 256) {
+      const int nf = f1 - f0, n = nf * F;
+      auto at = [&](int i) {
         const int o = i / nf, f = f0 + (i - o * nf);
-        float* p = A.g_xs + (size_t)o * NS + (size_t)g * NF + f;
-        *p = *p + dh[F + o] * (1.0f / (float)NF);
+        return A.g_xs + (size_t)o * NS + (size_t)g * NF + f;
+      };
+      for (int i0 = t; i0 < n; i0 += 256 * 8) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int i = i0 + 256 * e;
+          v[e] = i < n ? *at(i) : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int i = i0 + 256 * e;
+          if (i < n) *at(i) = v[e] + dh[F + i / nf] * (1.0f / (float)NF);
+        }
       }
     }
-    const int c0 = q * CB_CLS, ncl = min(CB_CLS, NC - c0);
-    const long long nb = (long long)g * NC + c0;
     // TModel's BatchNorm sums on the updated g_xt (k_bn_sums_part's arithmetic)
     float sg = 0.f, sx = 0.f;
-    if (t < F * CB_CLS) {
-      const int o = t / CB_CLS, cl = t - o * CB_CLS;
-      if (cl < ncl) {
-        float* p = A.g_xt + (size_t)o * NT + nb + cl;
-        const float v = *p + dh[2 * F + o] * (1.0f / (float)NC);
-        *p = v;
-        const float ic = 1.0f / sqrtf(A.var[o] + A.eps);
-        sg = v;
-        sx = v * ((A.Yp[(size_t)o * NT + nb + cl] - A.mu[o]) * ic);
-      }
+    if (xlive) {
+      const float v = xtv + dh[2 * F + xo] * (1.0f / (float)NC);
+      *xp = v;
+      const float ic = 1.0f / sqrtf(vrv + A.eps);
+      sg = v;
+      sx = v * ((ypv - muv) * ic);
     }
     // per channel over the unit's classes: 16 consecutive lanes hold one channel
 #pragma unroll
@@ -1268,13 +1359,13 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
     }
     if (t < F * CB_CLS && (t % CB_CLS) == 0) {
       const int o = t / CB_CLS;
-      T.p2[(size_t)un * CB_PLEN + o] = sg;
-      T.p2[(size_t)un * CB_PLEN + 16 + o] = sx;
+      st_sc1(T.p2 + (size_t)un * CB_PLEN + o, sg);
+      st_sc1(T.p2 + (size_t)un * CB_PLEN + 16 + o, sx);
     }
     __syncthreads();   // (LDS reuse by the next unit)
   }
   CB_STAMP(4)
-  grid_sync(gridDim.x);
+  grid_sync(gridDim.x, T.fenced);
   CB_STAMP(5)
   // ---------------------------------------------------------------- phase 3
   __shared__ float BC[5][16];
@@ -1288,8 +1379,8 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int uu = u + 16 * e;
-        a[e] = uu < T.nunits ? T.p2[(size_t)uu * CB_PLEN + o] : 0.f;
-        b[e] = uu < T.nunits ? T.p2[(size_t)uu * CB_PLEN + 16 + o] : 0.f;
+        a[e] = uu < T.nunits ? ld_sc1(T.p2 + (size_t)uu * CB_PLEN + o) : 0.f;
+        b[e] = uu < T.nunits ? ld_sc1(T.p2 + (size_t)uu * CB_PLEN + 16 + o) : 0.f;
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -1333,15 +1424,26 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
       gp[cl][o] = v;
     }
     __syncthreads();
-    for (int i = t; i < ncl * H; i += 256) {
-      const int h = i / ncl, cl = i - h * ncl;
-      float acc = 0.f;
+    {  // (every Z load of the thread issued before the first store)
+      constexpr int NZ = (CB_CLS * H + 255) / 256;
+      float zv[NZ];
 #pragma unroll
-      for (int o = 0; o < F; ++o) acc = fmaf(w2[o * H + h], gp[cl][o], acc);
-      const size_t e = (size_t)h * NT + nb + cl;
-      const float v = acc * dlrelu(A.Z[e]);
-      A.dZ[e] = v;
-      dzl[cl][h] = v;
+      for (int e = 0; e < NZ; ++e) {
+        const int i = t + 256 * e, h = i / max(ncl, 1), cl = i - h * ncl;
+        zv[e] = i < ncl * H ? A.Z[(size_t)h * NT + nb + cl] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < NZ; ++e) {
+        const int i = t + 256 * e;
+        if (i >= ncl * H) continue;
+        const int h = i / ncl, cl = i - h * ncl;
+        float acc = 0.f;
+#pragma unroll
+        for (int o = 0; o < F; ++o) acc = fmaf(w2[o * H + h], gp[cl][o], acc);
+        const float v = acc * dlrelu(zv[e]);
+        A.dZ[(size_t)h * NT + nb + cl] = v;
+        dzl[cl][h] = v;
+      }
     }
     __syncthreads();
     for (int i = t; i < ncl * K; i += 256) {
@@ -1918,14 +2020,24 @@ static int tail_ct(int G, int NC) {
     const int v = e ? atoi(e) : 16;   // (measured: 16 -- r04u_tail_ct.txt)
     return v == 8 || v == 16 || v == 32 ? v : 16;
   }();
-  for (int ct = ct0; ct <= CT_CLS; ct *= 2)
-    if ((long long)G * ((NC + ct - 1) / ct) <= 512) return ct;
+  for (int ct = ct0; ct <= CT_CLS; ct *= 2) {
+    const int qb = (NC + ct - 1) / ct;
+    if ((long long)G * qb <= 512 && qb <= CT_QBMAX) return ct;
+  }
   return 0;
 }
 size_t tail_ws_floats(int G, int NC, int F) {
   const int ct = tail_ct(G, NC);
   const size_t nu = (size_t)G * ((NC + (ct ? ct : CT_CLS) - 1) / (ct ? ct : CT_CLS));
   return nu * PART_LEN + 2 * nu * F + 64;
+}
+// grid_sync's form (A/B knob PFSGNN_GRID_SYNC_FENCED=1: the acq_rel form)
+static int grid_sync_fenced() {
+  static const int v = [] {
+    const char* e = getenv("PFSGNN_GRID_SYNC_FENCED");
+    return e && atoi(e) != 0 ? 1 : 0;
+  }();
+  return v;
 }
 int class_tail_fwd(const pfsgnn_block_tail& a, const float* cpart, int BPG, float bscale,
                    float* scratch, hipStream_t st) {
@@ -1935,13 +2047,15 @@ int class_tail_fwd(const pfsgnn_block_tail& a, const float* cpart, int BPG, floa
   T.cpart = cpart;
   T.BPG = BPG;
   T.CT = tail_ct(a.G, a.NC);
-  PF_REQUIRE(T.CT > 0, where, "more than 512 class units (G * ceil(NC / 32))");
+  PF_REQUIRE(T.CT > 0, where, "more than 512 class units (G * ceil(NC / 32)) or NC > 2048");
   T.QB = (a.NC + T.CT - 1) / T.CT;
+  PF_REQUIRE(T.QB <= CT_QBMAX, where, "more than 64 class units per graph");
   T.nunits = a.G * T.QB;
   T.bscale = bscale;
   T.part = scratch;
   T.xss = T.part + (size_t)T.nunits * PART_LEN;
   T.yps = T.xss + (size_t)T.nunits * a.F;
+  T.fenced = grid_sync_fenced();
   const int grid = std::min(T.nunits, cu_count());
   switch (a.F) {
     case 8: hipLaunchKernelGGL(k_class_tail_fwd<8>, dim3(grid), dim3(256), 0, st, T); break;
@@ -1984,12 +2098,14 @@ extern "C" int pfsgnn_target_class_bwd(const pfsgnn_class_bwd* a, void* ws, size
   CbArgs T{};
   T.a = *a;
   T.QB = (a->NC + CB_CLS - 1) / CB_CLS;
+  PF_REQUIRE(T.QB <= CB_QBMAX, where, "more than 1024 classes per graph");
   T.nunits = a->G * T.QB;
   PF_REQUIRE(T.nunits <= 4096, where, "too many class units");
   const size_t need = ((size_t)T.nunits * a->F + (size_t)T.nunits * CB_PLEN) * sizeof(float);
   PF_REQUIRE(ws && ws_bytes >= need, where, "workspace too small");
   T.p1 = static_cast<float*>(ws);
   T.p2 = T.p1 + (size_t)T.nunits * a->F;
+  T.fenced = pf::grid_sync_fenced();
   const int grid = std::min(T.nunits, cu_count());
   hipStream_t st = as_stream(stream);
   switch (a->F) {

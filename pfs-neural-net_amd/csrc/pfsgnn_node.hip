@@ -971,7 +971,13 @@ __global__ __launch_bounds__(512) void k_wgrad_multi(WgTable T) {
 // Node-level weight gradients in bf16x3 (wgrad_block's X3 form) on every edge
 // path except the exact-fp32 ones (PFSGNN_EDGE_MFMA_F32, _VALU, _BF16Y);
 // PFSGNN_NODE_WG_X3=0 keeps the fp32 MFMA form everywhere.
-static bool wg_x3() { return pf::node_x3("PFSGNN_NODE_WG_X3"); }
+// Only where the MFMAs dominate: >= 4 output tiles per wave (the narrow ones
+// -- a tile or two per wave -- are staging-bound and the operand split costs
+// more than it saves: <1, 4> 36.8 -> 44.4 us, <8, 8> 148 -> 134.5 us,
+// profiles/r04z_step_trace.txt); <16, 16> X3 spills.
+static bool wg_x3_for(int tm, int per) {
+  return tm >= 4 && !(tm == 16 && per == 16) && pf::node_x3("PFSGNN_NODE_WG_X3");
+}
 
 static int wgrad_blocks(int N) {
   static const int cap = [] {   // tuning knob: PFSGNN_WG_BLOCKS (blocks per weight gradient)
@@ -1056,7 +1062,7 @@ static int wgrad_launch(const float* dY, int M, const XSegs& S, int nseg, int K,
   float* part = reinterpret_cast<float*>(ws);
   const dim3 grid(P.nblk), blk(64 * WG_WAVES);
   bool launched = false;
-  const bool x3 = wg_x3() && !(P.tm == 16 && P.per == 16);   // (<16, 16> X3 spills)
+  const bool x3 = wg_x3_for(P.tm, P.per);
 #define PF_WG(T, PP)                                                                           \
   if (P.tm == T && P.per == PP) {                                                              \
     auto fn = x3 ? &k_wgrad<T, PP, true> : &k_wgrad<T, PP, false>;                             \
@@ -1215,7 +1221,7 @@ extern "C" int pfsgnn_wgrad_multi(const pfsgnn_wgrad_job* jobs, int n, void* par
       T.njob = m;
       bool launched = false;
       const int tm = PL[i].tm, per = PL[i].per;
-      const bool x3 = wg_x3() && !(tm == 16 && per == 16);   // (<16, 16> X3 spills)
+      const bool x3 = wg_x3_for(tm, per);
 #define PF_WGM(TT, PP)                                                                    \
   if (tm == TT && per == PP) {                                                            \
     auto fn = x3 ? &k_wgrad_multi<TT, PP, true> : &k_wgrad_multi<TT, PP, false>;          \

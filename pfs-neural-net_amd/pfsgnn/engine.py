@@ -438,7 +438,8 @@ class Engine:
         # path; None where the backward recomputes it)
         tmask = be.tmask(d) if self.training and hasattr(be, "tmask") else None
         if glob is not None and d.sp is None and hasattr(be, "target_block_fwd") and \
-                d.G * -(-d.NC // 32) <= 512 and os.environ.get("PFSGNN_CLASS_TAIL", "1") != "0":
+                d.G * -(-d.NC // 32) <= 512 and d.NC <= 2048 and \
+                os.environ.get("PFSGNN_CLASS_TAIL", "1") != "0":
             return self._target_block_fwd(P, BN, d, pre, xs, xt, xe3, u, Rs, tmask, glob)
         if d.sp is None:
             # the second Linear after the per-class sum, in the op's reduction epilogue
@@ -508,7 +509,7 @@ class Engine:
         """The fused class backward's conditions: a complete batch, training
         BatchNorm, the fused forward tail's GlobalModel state."""
         sT = stt.get("sT")
-        return (d.sp is None and self.normed and self.F in (8, 10, 16)
+        return (d.sp is None and self.normed and self.F in (8, 10, 16) and d.NC <= 1024
                 and hasattr(self.be, "target_class_bwd") and su.get("fused")
                 and sT is not None and sT[2] is not None and sT[2][0] != "eval"
                 and os.environ.get("PFSGNN_CLASS_BWD", "1") != "0")
