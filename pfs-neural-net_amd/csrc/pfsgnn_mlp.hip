@@ -754,7 +754,8 @@ __global__ __launch_bounds__(CG_THREADS) void k_class_global_fwd(ClassGlobalArgs
 constexpr int CT_QBMAX = 64;                // most units per graph (NC <= 64 * CT)
 constexpr int CT_CLS = 32;                  // most classes per unit (8, 16 or 32: the
                                             // smallest that keeps the units <= 512)
-__device__ unsigned pf_tail_bar[2];         // device-wide barrier: arrivals, generation
+__device__ unsigned pf_tail_bar[2];         // device-wide barrier (fenced form): arrivals, generation
+__device__ unsigned pf_tail_bar_w;          // (default form) arrivals | generation << 16
 __device__ unsigned pf_sync_fault_count;    // barrier time-outs (diagnostic)
 
 // every workgroup of the grid (all resident: the grid is at most one per CU)
@@ -765,8 +766,8 @@ __device__ unsigned pf_sync_fault_count;    // barrier time-outs (diagnostic)
 // load sc1: st_sc1 / ld_sc1), every wave waits for its stores (vmcnt(0)) before
 // the workgroup barrier, one lane counts the workgroup in with a relaxed
 // agent-scope add, and the last arrival -- told by the value its add returned
-// -- resets the counter (its store completed before the generation moves) and
-// bumps the generation the others poll with sc1 loads (MI355X_MICROARCH.md,
+// -- resets the count and bumps the generation in one add on the same word
+// (arrivals in the low 16 bits), which the others poll with sc1 loads (MI355X_MICROARCH.md,
 // the sc1 hand-off table's first row: hipMalloc'd bytes, one workgroup per CU).
 // fenced = 1 (PFSGNN_GRID_SYNC_FENCED=1, A/B): the arrival is an agent-scope
 // acq_rel add and the poll an acquire -- an L2 write-back and an L1 invalidate
@@ -796,17 +797,16 @@ __device__ void grid_sync(unsigned nb, int fenced) {
         }
       }
     } else {
-      const unsigned gen = __hip_atomic_load(&pf_tail_bar[1], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned a = __hip_atomic_fetch_add(&pf_tail_bar[0], 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-      if (a == nb - 1) {
-        __hip_atomic_store(&pf_tail_bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the reset lands before the bump
-        __hip_atomic_fetch_add(&pf_tail_bar[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // one word: arrivals in the low 16 bits, the generation above; the last
+      // arrival resets the count and bumps the generation in ONE add
+      unsigned* w = &pf_tail_bar_w;
+      const unsigned a = __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned gen = a >> 16;
+      if ((a & 0xffffu) == nb - 1) {
+        __hip_atomic_fetch_add(w, 0x10000u - nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         unsigned spins = 0;
-        while (__hip_atomic_load(&pf_tail_bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        while ((__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 16) == gen) {
           __builtin_amdgcn_s_sleep(2);
           if (++spins > (1u << 24)) {
             __hip_atomic_fetch_add(&pf_sync_fault_count, 1u, __ATOMIC_RELAXED,

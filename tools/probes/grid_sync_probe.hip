@@ -110,12 +110,32 @@ __device__ void sync3(unsigned nb) {
   __syncthreads();
 }
 
+// Form 4: form 3 with one word (arrivals | generation << 16): the last arrival
+//         resets and bumps in one add (pfsgnn_mlp.hip grid_sync's default)
+__device__ unsigned bar4;
+__device__ void sync4(unsigned nb) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned a = __hip_atomic_fetch_add(&bar4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((a & 0xffffu) == nb - 1) {
+      __hip_atomic_fetch_add(&bar4, 0x10000u - nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      unsigned spins = 0;
+      while ((__hip_atomic_load(&bar4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 16) == (a >> 16) &&
+             ++spins < (1u << 24))
+        __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+
 template <int FORM>
 __global__ __launch_bounds__(256) void k_bar(int n, float* sink) {
   float v = threadIdx.x;
   for (int i = 0; i < n; ++i) {
     if (FORM == 0) sync0(gridDim.x); else if (FORM == 1) sync1(gridDim.x);
-    else if (FORM == 2) sync2(gridDim.x); else sync3(gridDim.x);
+    else if (FORM == 2) sync2(gridDim.x); else if (FORM == 3) sync3(gridDim.x); else sync4(gridDim.x);
     v = v * 1.0001f + 1.f;
   }
   if (v == -1.f) sink[0] = v;
@@ -141,9 +161,10 @@ float run(int nb, int n) {
 
 int main() {
   for (int nb : {64, 128, 256}) {
-    for (int form = 0; form < 4; ++form) {
+    for (int form = 0; form < 5; ++form) {
       auto R = [&](int n) {
-        return form == 0 ? run<0>(nb, n) : form == 1 ? run<1>(nb, n) : form == 2 ? run<2>(nb, n) : run<3>(nb, n);
+        return form == 0 ? run<0>(nb, n) : form == 1 ? run<1>(nb, n) : form == 2 ? run<2>(nb, n)
+             : form == 3 ? run<3>(nb, n) : run<4>(nb, n);
       };
       const float t1 = R(1), t21 = R(21), t0 = R(0);
       printf("blocks %3d form %d: launch %.2f us, 1 barrier %.2f us, per barrier (21 vs 1) %.2f us\n",
