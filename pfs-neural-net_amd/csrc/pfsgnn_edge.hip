@@ -1128,26 +1128,12 @@ __device__ __forceinline__ void reduce_fiber_lin_block(FiberLinLds<C>& S, int bx
   float a[CPW];
 #pragma unroll
   for (int j = 0; j < CPW; ++j) a[j] = 0.f;
-  if (KS <= 2) {   // (the usual case: both partials' loads in flight at once)
-    float x0[CPW], x1[CPW];
+  for (int k = 0; k < KS; ++k) {
+    float x[CPW];
 #pragma unroll
-    for (int j = 0; j < CPW; ++j) {
-      x0[j] = part[(size_t)(w + 4 * j) * NS + nc];
-      x1[j] = KS > 1 ? part[(size_t)len + (size_t)(w + 4 * j) * NS + nc] : 0.f;
-    }
+    for (int j = 0; j < CPW; ++j) x[j] = part[(size_t)k * len + (size_t)(w + 4 * j) * NS + nc];
 #pragma unroll
-    for (int j = 0; j < CPW; ++j) {
-      a[j] += x0[j];
-      if (KS > 1) a[j] += x1[j];
-    }
-  } else {
-    for (int k = 0; k < KS; ++k) {
-      float x[CPW];
-#pragma unroll
-      for (int j = 0; j < CPW; ++j) x[j] = part[(size_t)k * len + (size_t)(w + 4 * j) * NS + nc];
-#pragma unroll
-      for (int j = 0; j < CPW; ++j) a[j] += x[j];
-    }
+    for (int j = 0; j < CPW; ++j) a[j] += x[j];
   }
 #pragma unroll
   for (int j = 0; j < CPW; ++j) {
@@ -1197,56 +1183,20 @@ __device__ __forceinline__ void reduce_columns_lin_block(ColLinLds<C>& S, int bx
   const int t = threadIdx.x, o = t & 15, pl = t >> 4;
   const long long NT = (long long)G * NC, q0 = (long long)bx * CPB;
   stage_lin<C>(L0, L1, ws);
-  if (BPG <= 64) {
-    // every pass's partials (lane pl: groups pl, pl + 16, pl + 32, pl + 48)
-    // loaded at once -- one memory round trip, not one per pass -- then summed
-    // in the loop form's order below (bitwise the same)
-    float x[NP][4];
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int idx = p * 16 + o, cl = idx / C, i = idx - cl * C;
-      const long long q = min(q0 + cl, NT - 1);
-      const long long g = q / NC, c = q - g * NC;
-      const float* pp = part + ((size_t)g * BPG * NC + c) * C + i;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int b = pl + 16 * k;
-        x[p][k] = b < BPG ? pp[(size_t)b * NC * C] : 0.f;
-      }
+  for (int p = 0; p < NP; ++p) {
+    const int idx = p * 16 + o, cl = idx / C, i = idx - cl * C;
+    const long long q = min(q0 + cl, NT - 1);   // clamped: loads unconditional
+    const long long g = q / NC, c = q - g * NC;
+    const float* pp = part + ((size_t)g * BPG * NC + c) * C + i;
+    float s0 = 0.f, s1 = 0.f;
+    int b = pl;
+    for (; b + 16 < BPG; b += 32) {
+      s0 += pp[(size_t)b * NC * C];
+      s1 += pp[(size_t)(b + 16) * NC * C];
     }
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      float s0 = 0.f, s1 = 0.f;
-      if (pl + 16 < BPG) {
-        s0 += x[p][0];
-        s1 += x[p][1];
-        if (pl + 48 < BPG) {
-          s0 += x[p][2];
-          s1 += x[p][3];
-        } else if (pl + 32 < BPG) {
-          s0 += x[p][2];
-        }
-      } else if (pl < BPG) {
-        s0 += x[p][0];
-      }
-      sh[p][pl][o] = s0 + s1;
-    }
-  } else {
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int idx = p * 16 + o, cl = idx / C, i = idx - cl * C;
-      const long long q = min(q0 + cl, NT - 1);   // clamped: loads unconditional
-      const long long g = q / NC, c = q - g * NC;
-      const float* pp = part + ((size_t)g * BPG * NC + c) * C + i;
-      float s0 = 0.f, s1 = 0.f;
-      int b = pl;
-      for (; b + 16 < BPG; b += 32) {
-        s0 += pp[(size_t)b * NC * C];
-        s1 += pp[(size_t)(b + 16) * NC * C];
-      }
-      if (b < BPG) s0 += pp[(size_t)b * NC * C];
-      sh[p][pl][o] = s0 + s1;
-    }
+    if (b < BPG) s0 += pp[(size_t)b * NC * C];
+    sh[p][pl][o] = s0 + s1;
   }
   __syncthreads();
   for (int idx = t; idx < NO; idx += 256) {

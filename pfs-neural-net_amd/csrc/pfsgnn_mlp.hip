@@ -925,77 +925,36 @@ __global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
     const int g = un / T.QB, q = un - g * T.QB;
     const int c0 = q * T.CT, ncl = min(T.CT, NC - c0);
     const long long nb = (long long)g * NC + c0;
-    // the unit's x_t / u inputs and its first two x_s fibers per thread, loaded
-    // with the column partials below (one memory round trip for the phase)
-    float xtp[2], up[2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int i = t + 256 * e, o = i / ncl, cl = i - o * ncl;
-      xtp[e] = i < ncl * F ? A.xt[(size_t)o * NT + nb + cl] : 0.f;
-      up[e] = i < ncl * F ? A.u[(size_t)o * G + g] : 0.f;
-    }
-    const int f0 = (int)(((long long)NF * q) / T.QB), f1 = (int)(((long long)NF * (q + 1)) / T.QB);
-    float xs0[F], xs1[F];
-#pragma unroll
-    for (int o = 0; o < F; ++o) {
-      const float* px = A.xs + (size_t)o * NS + (size_t)g * NF;
-      xs0[o] = f0 + t < f1 ? px[f0 + t] : 0.f;
-      xs1[o] = f0 + t + 256 < f1 ? px[f0 + t + 256] : 0.f;
-    }
-    // per-class sums of the column partials, in partial order: a thread's two
-    // (class, channel) items with up to 40 partials each in flight at once
-    {
-      constexpr int PB = 40;   // (>= the bench's 38 fiber groups per graph)
+    // per-class sums of the column partials, in partial order (32 loads of a
+    // thread in flight at once: this is the phase's latency)
+    for (int i = t; i < ncl * C2; i += 256) {
+      const int cl = i / C2, j = i - cl * C2;
+      const float* p = T.cpart + ((size_t)g * T.BPG * NC + c0 + cl) * C2 + j;
       const size_t bs = (size_t)NC * C2;
-      const int n = ncl * C2;
-      for (int i0 = t; i0 < n; i0 += 512) {
-        const int i1 = i0 + 256;
-        const bool two = i1 < n;
-        const int cl0 = i0 / C2, j0 = i0 - cl0 * C2, cl1 = two ? i1 / C2 : cl0,
-                  j1 = two ? i1 - cl1 * C2 : j0;
-        const float* p0 = T.cpart + ((size_t)g * T.BPG * NC + c0 + cl0) * C2 + j0;
-        const float* p1 = T.cpart + ((size_t)g * T.BPG * NC + c0 + cl1) * C2 + j1;
-        float s0 = 0.f, s1 = 0.f;
-        for (int b = 0; b < T.BPG; b += PB) {
-          float v0[PB], v1[PB];
+      float s = 0.f;
+      for (int b = 0; b < T.BPG; b += 32) {
+        float v[32];
 #pragma unroll
-          for (int e = 0; e < PB; ++e) {
-            v0[e] = b + e < T.BPG ? p0[(size_t)(b + e) * bs] : 0.f;
-            v1[e] = (two && b + e < T.BPG) ? p1[(size_t)(b + e) * bs] : 0.f;
-          }
+        for (int e = 0; e < 32; ++e) v[e] = b + e < T.BPG ? p[(size_t)(b + e) * bs] : 0.f;
 #pragma unroll
-          for (int e = 0; e < PB; ++e) s0 += v0[e];
-#pragma unroll
-          for (int e = 0; e < PB; ++e) s1 += v1[e];
-        }
-        hs[cl0][j0] = s0;
-        A.hsum[(size_t)j0 * NT + nb + cl0] = s0;
-        if (two) {
-          hs[cl1][j1] = s1;
-          A.hsum[(size_t)j1 * NT + nb + cl1] = s1;
-        }
+        for (int e = 0; e < 32; ++e) s += v[e];
       }
+      hs[cl][j] = s;
+      A.hsum[(size_t)j * NT + nb + cl] = s;
     }
     TAIL_STAMP(2)
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int i = t + 256 * e, o = i / ncl, cl = i - o * ncl;
-      if (i < ncl * F) {
-        xin[cl][o] = xtp[e];
-        xin[cl][3 * F + o] = up[e];
-      }
-    }
-    for (int i = t + 512; i < ncl * F; i += 256) {
+    for (int i = t; i < ncl * F; i += 256) {
       const int o = i / ncl, cl = i - o * ncl;
       xin[cl][o] = A.xt[(size_t)o * NT + nb + cl];
       xin[cl][3 * F + o] = A.u[(size_t)o * G + g];
     }
-    // the unit's share of graph g's x_s sums (fibers [f0, f1), in fiber order)
+    // the unit's share of graph g's x_s sums (fibers [f0, f1))
     {
+      const int f0 = (int)(((long long)NF * q) / T.QB), f1 = (int)(((long long)NF * (q + 1)) / T.QB);
       float sx[F];
 #pragma unroll
-      for (int o = 0; o < F; ++o) sx[o] = (0.f + xs0[o]) + xs1[o];
-      for (int f = f0 + t + 512; f < f1; f += 256) {
+      for (int o = 0; o < F; ++o) sx[o] = 0.f;
+      for (int f = f0 + t; f < f1; f += 256) {
 #pragma unroll
         for (int o = 0; o < F; ++o) sx[o] += A.xs[(size_t)o * NS + (size_t)g * NF + f];
       }
@@ -1286,7 +1245,6 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
   __shared__ float sdy[F], sy1[F], sv[F], sw[F], sdw[F], gv[F], d1[F];
   __shared__ float dzg[CG_MAXH], dh[CG_MAXH];
   __shared__ float ps1[CB_QBMAX * F];
-  __shared__ float gxl[F][CB_CLS], ypl2[F][CB_CLS];   // the unit's g_xt / Yp for phase 3
   for (int un = blockIdx.x; un < T.nunits; un += gridDim.x) {
     const int g = un / T.QB, q = un - g * T.QB;
     const int c0 = q * CB_CLS, ncl = min(CB_CLS, NC - c0);
@@ -1301,35 +1259,18 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
     const float xtv = xlive ? *xp : 0.f;
     const float ypv = xlive ? A.Yp[(size_t)xo * NT + nb + xcl] : 0.f;
     const float vrv = xlive ? A.var[xo] : 0.f, muv = xlive ? A.mu[xo] : 0.f;
-    const bool ft = t < F;
-    const float guu = ft ? A.gu_up[(size_t)t * G + g] : 0.f;
-    const float gu0 = (ft && q == 0) ? A.gu[(size_t)t * G + g] : 0.f;
-    if (ft && A.w) {
-      sy1[t] = A.y1[(size_t)t * G + g];
-      sv[t] = A.V[(size_t)t * G + g];
-      sw[t] = A.w[t];
-    }
-    // the unit's share of the x_s broadcast, read up front (XS_PRE per thread)
-    const int f0 = (int)(((long long)NF * q) / T.QB), f1 = (int)(((long long)NF * (q + 1)) / T.QB);
-    const int nf = f1 - f0, nxs = nf * F;
-    auto xs_at = [&](int i) {
-      const int o = i / nf, f = f0 + (i - o * nf);
-      return A.g_xs + (size_t)o * NS + (size_t)g * NF + f;
-    };
-    constexpr int XS_PRE = 16;
-    float xsv[XS_PRE];
-#pragma unroll
-    for (int e = 0; e < XS_PRE; ++e) {
-      const int i = t + 256 * e;
-      xsv[e] = i < nxs ? *xs_at(i) : 0.f;
-    }
     // the graph's unit partials: every load in flight at once, summed in unit order
     for (int i = t; i < F * T.QB; i += 256) ps1[i] = ld_sc1(T.p1 + (size_t)g * T.QB * F + i);
     __syncthreads();
-    if (ft) {
-      float sacc = guu;
+    if (t < F) {
+      float sacc = A.gu_up[(size_t)t * G + g];
       for (int qq = 0; qq < T.QB; ++qq) sacc += ps1[qq * F + t];
       sdy[t] = sacc;
+      if (A.w) {
+        sy1[t] = A.y1[(size_t)t * G + g];
+        sv[t] = A.V[(size_t)t * G + g];
+        sw[t] = A.w[t];
+      }
     }
     __syncthreads();
     // GlobalModel backward (k_global_bwd's arithmetic): RMSNorm twice, then the MLP
@@ -1377,26 +1318,28 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
       dh[k] = acc;
     }
     __syncthreads();
-    if (q == 0 && ft) A.gu[(size_t)t * G + g] = gu0 + dh[t];
-    // the means' gradients broadcast: x_s over the unit's fiber share (the
-    // values read up front; beyond XS_PRE per thread, 8 loads in flight at a
-    // time), x_t over its classes
+    if (q == 0 && t < F) A.gu[(size_t)t * G + g] += dh[t];
+    // the means' gradients broadcast: x_s over the unit's fiber share, x_t over its classes
+    // (the read-modify-writes 8 per thread at a time: their loads in flight together)
+    {
+      const int f0 = (int)(((long long)NF * q) / T.QB), f1 = (int)(((long long)NF * (q + 1)) / T.QB);
+      const int nf = f1 - f0, n = nf * F;
+      auto at = [&](int i) {
+        const int o = i / nf, f = f0 + (i - o * nf);
+        return A.g_xs + (size_t)o * NS + (size_t)g * NF + f;
+      };
+      for (int i0 = t; i0 < n; i0 += 256 * 8) {
+        float v[8];
 #pragma unroll
-    for (int e = 0; e < XS_PRE; ++e) {
-      const int i = t + 256 * e;
-      if (i < nxs) *xs_at(i) = xsv[e] + dh[F + i / nf] * (1.0f / (float)NF);
-    }
-    for (int i0 = t + 256 * XS_PRE; i0 < nxs; i0 += 256 * 8) {
-      float v[8];
+        for (int e = 0; e < 8; ++e) {
+          const int i = i0 + 256 * e;
+          v[e] = i < n ? *at(i) : 0.f;
+        }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int i = i0 + 256 * e;
-        v[e] = i < nxs ? *xs_at(i) : 0.f;
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int i = i0 + 256 * e;
-        if (i < nxs) *xs_at(i) = v[e] + dh[F + i / nf] * (1.0f / (float)NF);
+        for (int e = 0; e < 8; ++e) {
+          const int i = i0 + 256 * e;
+          if (i < n) *at(i) = v[e] + dh[F + i / nf] * (1.0f / (float)NF);
+        }
       }
     }
     // TModel's BatchNorm sums on the updated g_xt (k_bn_sums_part's arithmetic)
@@ -1404,8 +1347,6 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
     if (xlive) {
       const float v = xtv + dh[2 * F + xo] * (1.0f / (float)NC);
       *xp = v;
-      gxl[xo][xcl] = v;
-      ypl2[xo][xcl] = ypv;
       const float ic = 1.0f / sqrtf(vrv + A.eps);
       sg = v;
       sx = v * ((ypv - muv) * ic);
@@ -1429,25 +1370,6 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
   // ---------------------------------------------------------------- phase 3
   __shared__ float BC[5][16];
   __shared__ float mg[16][16], mx[16][16];
-  // one unit per workgroup (the usual grid): its g_xt / Yp are still in LDS
-  // from phase 2, and its Z and gxt_in operands load before the sums merge
-  const bool one = T.nunits <= (int)gridDim.x;
-  constexpr int NZ = (CB_CLS * H + 255) / 256;
-  float zv[NZ], gxi = 0.f;
-  if (one && (int)blockIdx.x < T.nunits) {
-    const int un = blockIdx.x, g = un / T.QB, q = un - g * T.QB;
-    const int c0 = q * CB_CLS, ncl = min(CB_CLS, NC - c0);
-    const long long nb = (long long)g * NC + c0;
-#pragma unroll
-    for (int e = 0; e < NZ; ++e) {
-      const int i = t + 256 * e, h = i / max(ncl, 1), cl = i - h * ncl;
-      zv[e] = i < ncl * H ? A.Z[(size_t)h * NT + nb + cl] : 0.f;
-    }
-    if (t < ncl * F) {
-      const int k = t / ncl, cl = t - k * ncl;
-      gxi = A.gxt_in[(size_t)k * NT + nb + cl];
-    }
-  }
   {  // the units' sums merged in one fixed order: 16 subsets of units (loads
      // of a subset in flight together), then the subsets in order
     const int o = t & 15, u0 = t >> 4;
@@ -1497,19 +1419,18 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
     for (int i = t; i < ncl * F; i += 256) {
       const int o = i / ncl, cl = i - o * ncl;
       const size_t e = (size_t)o * NT + nb + cl;
-      const float xg = one ? gxl[o][cl] : A.g_xt[e], yv = one ? ypl2[o][cl] : A.Yp[e];
-      const float v = BC[0][o] * (xg - BC[1][o] - (yv - BC[3][o]) * BC[4][o] * BC[2][o]);
+      const float v = BC[0][o] * (A.g_xt[e] - BC[1][o] - (A.Yp[e] - BC[3][o]) * BC[4][o] * BC[2][o]);
       A.dYp[e] = v;
       gp[cl][o] = v;
     }
     __syncthreads();
     {  // (every Z load of the thread issued before the first store)
-      if (!one) {
+      constexpr int NZ = (CB_CLS * H + 255) / 256;
+      float zv[NZ];
 #pragma unroll
-        for (int e = 0; e < NZ; ++e) {
-          const int i = t + 256 * e, h = i / max(ncl, 1), cl = i - h * ncl;
-          zv[e] = i < ncl * H ? A.Z[(size_t)h * NT + nb + cl] : 0.f;
-        }
+      for (int e = 0; e < NZ; ++e) {
+        const int i = t + 256 * e, h = i / max(ncl, 1), cl = i - h * ncl;
+        zv[e] = i < ncl * H ? A.Z[(size_t)h * NT + nb + cl] : 0.f;
       }
 #pragma unroll
       for (int e = 0; e < NZ; ++e) {
@@ -1532,7 +1453,7 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
       for (int h = 0; h < H; ++h) acc = fmaf(w1[h * K + k], dzl[cl][h], acc);
       if (k < F) {
         float* p = A.gxt_in + (size_t)k * NT + nb + cl;
-        *p = (one && i == t ? gxi : *p) + acc;
+        *p = *p + acc;
       } else if (k < 3 * F) {
         A.g_agg[(size_t)(k - F) * NT + nb + cl] = acc;
         gag[cl][k - F] = acc;

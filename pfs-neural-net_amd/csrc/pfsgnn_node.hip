@@ -179,38 +179,14 @@ __global__ __launch_bounds__(256) void k_reduce_rows(RedPack pk) {
   const int r = v ? idx / D.cols : 0, c = v ? idx - r * D.cols : 0;
   const float* p = D.part + (size_t)r * D.ldp + c;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  if (D.nb <= 256) {
-    // (every list here: launch_reduce_multi segments longer ones) the lane's
-    // up to 16 partials loaded at once -- one memory round trip -- then summed
-    // in the loop form's order below (bitwise the same)
-    float x[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) x[k] = pl + 16 * k < D.nb ? p[(size_t)(pl + 16 * k) * D.plen] : 0.f;
-    int full = 0;   // rounds of 4 the loop form takes
-#pragma unroll
-    for (int it = 0; it < 4; ++it)
-      if (pl + 64 * it + 48 < D.nb) full = it + 1;
-#pragma unroll
-    for (int it = 0; it < 4; ++it)
-      if (it < full) {
-        s0 += x[4 * it];
-        s1 += x[4 * it + 1];
-        s2 += x[4 * it + 2];
-        s3 += x[4 * it + 3];
-      }
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      if (k >= 4 * full && pl + 16 * k < D.nb) s0 += x[k];
-  } else {
-    int b = pl;
-    for (; b + 48 < D.nb; b += 64) {
-      s0 += p[(size_t)b * D.plen];
-      s1 += p[(size_t)(b + 16) * D.plen];
-      s2 += p[(size_t)(b + 32) * D.plen];
-      s3 += p[(size_t)(b + 48) * D.plen];
-    }
-    for (; b < D.nb; b += 16) s0 += p[(size_t)b * D.plen];
+  int b = pl;
+  for (; b + 48 < D.nb; b += 64) {
+    s0 += p[(size_t)b * D.plen];
+    s1 += p[(size_t)(b + 16) * D.plen];
+    s2 += p[(size_t)(b + 32) * D.plen];
+    s3 += p[(size_t)(b + 48) * D.plen];
   }
+  for (; b < D.nb; b += 16) s0 += p[(size_t)b * D.plen];
   __shared__ float sh[16][17];
   sh[pl][o] = (s0 + s1) + (s2 + s3);
   __syncthreads();
@@ -234,33 +210,14 @@ __global__ __launch_bounds__(256) void k_reduce_seg(RedPack pk) {
   const int b1 = min(D.nb, b0 + RED_SEG);
   float* p = const_cast<float*>(D.part) + (size_t)r * D.ldp + c;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  {
-    // the lane's RED_SEG / RED_P partials loaded at once, then summed in the
-    // order of the 4-accumulator loop (rounds of 4, then the rest into s0)
-    constexpr int NL = RED_SEG / RED_P;
-    static_assert(NL % 4 == 0, "segment lanes");
-    float x[NL];
-#pragma unroll
-    for (int k = 0; k < NL; ++k) {
-      const int b = b0 + pl + RED_P * k;
-      x[k] = b < b1 ? p[(size_t)b * D.plen] : 0.f;
-    }
-    int full = 0;
-#pragma unroll
-    for (int it = 0; it < NL / 4; ++it)
-      if (b0 + pl + 4 * RED_P * it + 3 * RED_P < b1) full = it + 1;
-#pragma unroll
-    for (int it = 0; it < NL / 4; ++it)
-      if (it < full) {
-        s0 += x[4 * it];
-        s1 += x[4 * it + 1];
-        s2 += x[4 * it + 2];
-        s3 += x[4 * it + 3];
-      }
-#pragma unroll
-    for (int k = 0; k < NL; ++k)
-      if (k >= 4 * full && b0 + pl + RED_P * k < b1) s0 += x[k];
+  int b = b0 + pl;
+  for (; b + 3 * RED_P < b1; b += 4 * RED_P) {
+    s0 += p[(size_t)b * D.plen];
+    s1 += p[(size_t)(b + RED_P) * D.plen];
+    s2 += p[(size_t)(b + 2 * RED_P) * D.plen];
+    s3 += p[(size_t)(b + 3 * RED_P) * D.plen];
   }
+  for (; b < b1; b += RED_P) s0 += p[(size_t)b * D.plen];
   __shared__ float sh[RED_P][RED_O];
   sh[pl][o] = (s0 + s1) + (s2 + s3);
   __syncthreads();
