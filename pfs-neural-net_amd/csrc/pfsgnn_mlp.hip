@@ -518,34 +518,49 @@ __global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__
     return;
   }
   constexpr int OW = OT ? (OT + 3) / 4 * 4 : 16;   // channels the epilogue multiplies
-  for (int n = blockIdx.x * 256 + t; n < N; n += gridDim.x * 256) {
-    float y[16];
+  // two nodes per thread and step (8 independent FMA chains: one wave per SIMD
+  // at this grid, so the chains are the latency hiding)
+  const int stride = gridDim.x * 256;
+  for (int n = blockIdx.x * 256 + t; n < N; n += 2 * stride) {
+    const int n2 = n + stride;
+    const bool v2 = n2 < N;
+    float y[2][16];
 #pragma unroll
     for (int o = 0; o < 16; ++o) {
-      y[o] = 0.f;
+      y[0][o] = y[1][o] = 0.f;
       if (o < O) {
-        y[o] = (Yp[(size_t)o * N + n] - cf[0][o]) * (cf[1][o] * cf[2][o]) + cf[3][o];
-        Y[(size_t)o * N + n] = y[o];
+        const float sc = cf[1][o] * cf[2][o];
+        y[0][o] = (Yp[(size_t)o * N + n] - cf[0][o]) * sc + cf[3][o];
+        Y[(size_t)o * N + n] = y[0][o];
+        if (v2) {
+          y[1][o] = (Yp[(size_t)o * N + n2] - cf[0][o]) * sc + cf[3][o];
+          Y[(size_t)o * N + n2] = y[1][o];
+        }
       }
     }
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       if (!E.W[e]) continue;
-      for (int k0 = 0; k0 < E.nk[e]; k0 += 4) {   // 4 independent rows per step
-        float a[4];
+      for (int k0 = 0; k0 < E.nk[e]; k0 += 4) {   // 4 rows x 2 nodes per step
+        float a[2][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] = eb[e][k0 + j];
+        for (int j = 0; j < 4; ++j) a[0][j] = a[1][j] = eb[e][k0 + j];
 #pragma unroll
         for (int o4 = 0; o4 < OW; o4 += 4)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const floatx4 w = *reinterpret_cast<const floatx4*>(&ew[e][(k0 + j) * 16 + o4]);
-            a[j] = fmaf(w[0], y[o4], fmaf(w[1], y[o4 + 1], fmaf(w[2], y[o4 + 2],
-                        fmaf(w[3], y[o4 + 3], a[j]))));
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+              a[u][j] = fmaf(w[0], y[u][o4], fmaf(w[1], y[u][o4 + 1], fmaf(w[2], y[u][o4 + 2],
+                             fmaf(w[3], y[u][o4 + 3], a[u][j]))));
           }
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (k0 + j < E.nk[e]) E.out[e][(size_t)(k0 + j) * N + n] = a[j];
+          if (k0 + j < E.nk[e]) {
+            E.out[e][(size_t)(k0 + j) * N + n] = a[0][j];
+            if (v2) E.out[e][(size_t)(k0 + j) * N + n2] = a[1][j];
+          }
       }
     }
   }

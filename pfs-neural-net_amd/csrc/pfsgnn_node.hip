@@ -830,9 +830,18 @@ __device__ __forceinline__ void wgrad_block(const float* __restrict__ dY, int M,
   // tile of (wave, j): X3 contiguous runs, else wave + 8 j
   const int tpw = (NTILE + WG_WAVES - 1) / WG_WAVES;
   auto tile_of = [&](int j) { return X3 ? (j < tpw ? wave * tpw + j : NTILE) : wave + WG_WAVES * j; };
+  // X3 (the MFMA-light form) keeps two chunks of loads in flight, not one
+  constexpr bool DEEP = X3 && PER <= 8 && TMAX <= 8;
+  float4 buf2[DEEP ? PER : 1];
   if (n0 < n1) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) buf[i] = fetch(n0, i);
+  }
+  if constexpr (DEEP) {
+    if (n0 + 64 < n1) {
+#pragma unroll
+      for (int i = 0; i < PER; ++i) buf2[i] = fetch(n0 + 64, i);
+    }
   }
   for (int c = n0; c < n1; c += 64) {
     __syncthreads();
@@ -852,7 +861,14 @@ __device__ __forceinline__ void wgrad_block(const float* __restrict__ dY, int M,
         }
       }
     __syncthreads();
-    if (c + 64 < n1) {  // next chunk's loads in flight during this chunk's MFMAs
+    if constexpr (DEEP) {   // chunk c + 2's loads join c + 1's in flight
+#pragma unroll
+      for (int i = 0; i < PER; ++i) buf[i] = buf2[i];
+      if (c + 128 < n1) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) buf2[i] = fetch(c + 128, i);
+      }
+    } else if (c + 64 < n1) {  // next chunk's loads in flight during this chunk's MFMAs
 #pragma unroll
       for (int i = 0; i < PER; ++i) buf[i] = fetch(c + 64, i);
     }
