@@ -830,7 +830,9 @@ __device__ __forceinline__ void wgrad_block(const float* __restrict__ dY, int M,
   // tile of (wave, j): X3 contiguous runs, else wave + 8 j
   const int tpw = (NTILE + WG_WAVES - 1) / WG_WAVES;
   auto tile_of = [&](int j) { return X3 ? (j < tpw ? wave * tpw + j : NTILE) : wave + WG_WAVES * j; };
-  // X3 (the MFMA-light form) keeps two chunks of loads in flight, not one
+  // the bf16x3 form keeps two chunks of loads in flight, not one (<8, 8>:
+  // 139 -> 114 us at the bench batch, 1525 -> 915 us at configs[2]); the fp32
+  // form measured slower so (<1, 4>: 37 -> 47 us, profiles/r04ah_*)
   constexpr bool DEEP = X3 && PER <= 8 && TMAX <= 8;
   float4 buf2[DEEP ? PER : 1];
   if (n0 < n1) {
