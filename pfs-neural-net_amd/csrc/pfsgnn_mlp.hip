@@ -541,10 +541,6 @@ __global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       if (!E.W[e]) continue;
-      // the weights are uniform over the block: scalar loads (an LDS broadcast
-      // read per 4 FMAs made this LDS-issue-bound); zero past O, as staged
-      const pf_cptr Wg = pf_fresh(E.W[e] + E.col0[e]);
-      const int ldw = E.ldw[e];
       for (int k0 = 0; k0 < E.nk[e]; k0 += 4) {   // 4 rows x 2 nodes per step
         float a[2][4];
 #pragma unroll
@@ -553,11 +549,7 @@ __global__ __launch_bounds__(256) void k_bn_apply_part(const float* __restrict__
         for (int o4 = 0; o4 < OW; o4 += 4)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int k = k0 + j;
-            floatx4 w;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              w[q] = (o4 + q < O && k < E.nk[e]) ? Wg[(size_t)k * ldw + o4 + q] : 0.f;
+            const floatx4 w = *reinterpret_cast<const floatx4*>(&ew[e][(k0 + j) * 16 + o4]);
 #pragma unroll
             for (int u = 0; u < 2; ++u)
               a[u][j] = fmaf(w[0], y[u][o4], fmaf(w[1], y[u][o4 + 1], fmaf(w[2], y[u][o4 + 2],
