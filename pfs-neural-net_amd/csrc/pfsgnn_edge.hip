@@ -1124,7 +1124,7 @@ __device__ __forceinline__ void reduce_fiber_lin_block(FiberLinLds<C>& S, int bx
   const bool v = n < NS;
   const long long nc = v ? n : NS - 1;   // clamped: every load unconditional
   const long long len = (long long)C * NS;
-  (void)ws;
+  stage_lin<C>(L0, L1, ws);
   float a[CPW];
 #pragma unroll
   for (int j = 0; j < CPW; ++j) a[j] = 0.f;
@@ -1142,33 +1142,19 @@ __device__ __forceinline__ void reduce_fiber_lin_block(FiberLinLds<C>& S, int bx
     if (v && KS > 1) out[(size_t)c * NS + n] = a[j];
   }
   __syncthreads();
-  // epilogues: lane = fiber, its C sums read from LDS once; wave w computes
-  // outputs k = w, w + 4, ... with the (wave-uniform) weights as scalar loads
-  // -- not one LDS weight and one LDS sum read per FMA, which made this
-  // LDS-bound (same FMA order per output as before: bit-identical)
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  const bool ov = n0 + lane < NS;
-  bool any = false;
-#pragma unroll
-  for (int e = 0; e < 2; ++e) any = any || (e ? L1 : L0).W != nullptr;
-  if (!any) return;
-  float rr[C];
-#pragma unroll
-  for (int i = 0; i < C; ++i) rr[i] = res[i][lane];
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
     const NodeLin& L = e ? L1 : L0;
     if (!L.W) continue;
-    const pf_cptr W = pf_fresh(L.W);
-    for (int k = wu; k < L.nk; k += 4) {
+    const float* wk = ws + e * NL_MAXK * C;
+    for (int idx = t; idx < 64 * L.nk; idx += 256) {
+      const int k = idx >> 6, o = idx & 63;
+      if (n0 + o >= NS) continue;
       float acc = L.b ? L.bscale * L.b[k] : 0.f;
 #pragma unroll
-      for (int i = 0; i < C; ++i)
-        acc = fmaf(L.trans ? W[(size_t)i * L.ldw + k] : W[(size_t)k * L.ldw + i], rr[i], acc);
-      if (ov) {
-        float* op = L.out + (size_t)k * L.ldo + n0 + lane;
-        *op = L.add ? *op + acc : acc;
-      }
+      for (int i = 0; i < C; ++i) acc = fmaf(wk[k * C + i], res[i][o], acc);
+      float* op = L.out + (size_t)k * L.ldo + n0 + o;
+      *op = L.add ? *op + acc : acc;
     }
   }
 }
