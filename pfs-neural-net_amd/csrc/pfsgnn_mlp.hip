@@ -2187,7 +2187,14 @@ extern "C" int pfsgnn_mlp_fwd_epi(const pfsgnn_seg* segs, int nseg, int N, const
   PF_REQUIRE(rc != -3, where, "hipFuncSetAttribute (dynamic LDS) failed");
   PF_REQUIRE(rc == 0, where, "no kernel for this width");
   if (bn) {
-    const int ag = std::max(1, std::min(256, (int)(((size_t)O * N + 1023) / 1024)));
+    // most blocks (A/B knob PFSGNN_BN_APPLY_BLOCKS): 1024 -- one wave per SIMD at
+    // 256 left the epilogue's FMA chains exposed (configs[2] 26.11 -> 25.90 ms,
+    // the bench batch unchanged at 374 blocks: profiles/r04aj_*)
+    static const int agmax = [] {
+      const char* e = getenv("PFSGNN_BN_APPLY_BLOCKS");
+      return e && atoi(e) > 0 ? atoi(e) : 1024;
+    }();
+    const int ag = std::max(1, std::min(agmax, (int)(((size_t)O * N + 1023) / 1024)));
     // (zero weights pad the channels past O within a 4-channel group: ew rows are
     // 16 wide with o >= O zero, so OW = round-up(O, 4) is exact)
     if (O == 10)

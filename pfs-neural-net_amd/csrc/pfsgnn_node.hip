@@ -994,7 +994,11 @@ __global__ __launch_bounds__(512) void k_wgrad_multi(WgTable T) {
 // more than it saves: <1, 4> 36.8 -> 44.4 us, <8, 8> 148 -> 134.5 us,
 // profiles/r04z_step_trace.txt); <16, 16> X3 spills.
 static bool wg_x3_for(int tm, int per) {
-  return tm >= 4 && !(tm == 16 && per == 16) && pf::node_x3("PFSGNN_NODE_WG_X3");
+  static const int min_tm = [] {   // A/B knob PFSGNN_WG_X3_MIN_TM
+    const char* e = std::getenv("PFSGNN_WG_X3_MIN_TM");
+    return e ? std::max(1, std::atoi(e)) : 4;
+  }();
+  return tm >= min_tm && !(tm == 16 && per == 16) && pf::node_x3("PFSGNN_NODE_WG_X3");
 }
 
 static int wgrad_blocks(int N) {
