@@ -891,30 +891,7 @@ __global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
     b2v = t < F ? A.b2[t] : 0.f;
     btv = t < C2 ? A.bt2[t] : 0.f;
   }
-  // the next block's weight blocks: We[:, F:2F], We[:, 3F:4F], be, Ws[:, 0:F], bs
-  // (used in phase 2)
-  __shared__ float wet[4 * F * F], weu[4 * F * F], wbe[4 * F], wst[2 * F * F], wbs[2 * F];
-  constexpr int NE = (4 * F * F + 255) / 256, NS2 = (2 * F * F + 255) / 256;
-  float e1[NE], e2[NE], e3[NS2], bev = 0.f, bsv = 0.f;
-  if (A.We) {
-#pragma unroll
-    for (int i = 0; i < NE; ++i) {
-      const int x = t + 256 * i, k = x / F, o = x - k * F;
-      e1[i] = x < 4 * F * F ? A.We[(size_t)k * 4 * F + F + o] : 0.f;
-      e2[i] = x < 4 * F * F ? A.We[(size_t)k * 4 * F + 3 * F + o] : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < NS2; ++i) {
-      const int x = t + 256 * i, k = x / F, o = x - k * F;
-      e3[i] = x < 2 * F * F ? A.Ws[(size_t)k * 2 * F + o] : 0.f;
-    }
-    bev = t < 4 * F ? A.be[t] : 0.f;
-    bsv = t < 2 * F ? A.bs[t] : 0.f;
-  }
-  // the weights' LDS stores wait until the first unit's column sums (which
-  // need none of them) are done: the loads' latency hides behind those sums;
-  // phase 1's next workgroup barrier publishes them
-  auto store_weights = [&]() {
+  {
     const int ng1 = gws ? A.gH * K3 : 0, ng2 = gws ? F * A.gH : 0;
 #pragma unroll
     for (int i = 0; i < N1; ++i) if (t + 256 * i < H * K) w1[t + 256 * i] = v1[i];
@@ -929,7 +906,34 @@ __global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
     if (t < H) bb1[t] = b1v;
     if (t < F) bb2[t] = b2v;
     if (t < C2) bt[t] = btv;
-  };
+  }
+  __syncthreads();
+  // the next block's weight blocks: We[:, F:2F], We[:, 3F:4F], be, Ws[:, 0:F], bs
+  __shared__ float wet[4 * F * F], weu[4 * F * F], wbe[4 * F], wst[2 * F * F], wbs[2 * F];
+  if (A.We) {
+    constexpr int NE = (4 * F * F + 255) / 256, NS2 = (2 * F * F + 255) / 256;
+    float e1[NE], e2[NE], e3[NS2];
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int x = t + 256 * i, k = x / F, o = x - k * F;
+      e1[i] = x < 4 * F * F ? A.We[(size_t)k * 4 * F + F + o] : 0.f;
+      e2[i] = x < 4 * F * F ? A.We[(size_t)k * 4 * F + 3 * F + o] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NS2; ++i) {
+      const int x = t + 256 * i, k = x / F, o = x - k * F;
+      e3[i] = x < 2 * F * F ? A.Ws[(size_t)k * 2 * F + o] : 0.f;
+    }
+    const float bev = t < 4 * F ? A.be[t] : 0.f, bsv = t < 2 * F ? A.bs[t] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NE; ++i)
+      if (t + 256 * i < 4 * F * F) { wet[t + 256 * i] = e1[i]; weu[t + 256 * i] = e2[i]; }
+#pragma unroll
+    for (int i = 0; i < NS2; ++i)
+      if (t + 256 * i < 2 * F * F) wst[t + 256 * i] = e3[i];
+    if (t < 4 * F) wbe[t] = bev;
+    if (t < 2 * F) wbs[t] = bsv;
+  }
   TAIL_STAMP(1)
   // ---------------------------------------------------------------- phase 1
   for (int un = blockIdx.x; un < T.nunits; un += gridDim.x) {
@@ -953,7 +957,6 @@ __global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
       hs[cl][j] = s;
       A.hsum[(size_t)j * NT + nb + cl] = s;
     }
-    if (un == (int)blockIdx.x) store_weights();
     TAIL_STAMP(2)
     for (int i = t; i < ncl * F; i += 256) {
       const int o = i / ncl, cl = i - o * ncl;
@@ -1032,16 +1035,6 @@ __global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
       if (t == 0) st_sc1(pp, (float)ncl);
     }
     __syncthreads();   // (LDS reuse by the next unit)
-  }
-  if (A.We) {   // (phase 2's; published by the grid barrier's workgroup barriers)
-#pragma unroll
-    for (int i = 0; i < NE; ++i)
-      if (t + 256 * i < 4 * F * F) { wet[t + 256 * i] = e1[i]; weu[t + 256 * i] = e2[i]; }
-#pragma unroll
-    for (int i = 0; i < NS2; ++i)
-      if (t + 256 * i < 2 * F * F) wst[t + 256 * i] = e3[i];
-    if (t < 4 * F) wbe[t] = bev;
-    if (t < 2 * F) wbs[t] = bsv;
   }
   TAIL_STAMP(3)
   grid_sync(gridDim.x, T.fenced);
@@ -1205,22 +1198,32 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
   __shared__ float w1[H * K], w2[F * H], wt2[C2 * C2];
   __shared__ float gw1[CG_GW1], gw2[F * CG_MAXH];
   const bool gws = A.gH * K3 <= CG_GW1;
-  // every weight load in flight at once; their LDS stores wait until after
-  // phase 1 (which needs none of them), so their latency hides behind it
-  constexpr int N1 = (H * K + 255) / 256, N2 = (F * H + 255) / 256, N3 = (C2 * C2 + 255) / 256;
-  constexpr int NG1 = (CG_GW1 + 255) / 256, NG2 = (F * CG_MAXH + 255) / 256;
-  float v1[N1], v2[N2], v3[N3], g1[NG1], g2[NG2];
-  const int ng1 = gws ? A.gH * K3 : 0, ng2 = gws ? F * A.gH : 0;
+  {  // every weight load in flight before the LDS stores
+    constexpr int N1 = (H * K + 255) / 256, N2 = (F * H + 255) / 256, N3 = (C2 * C2 + 255) / 256;
+    constexpr int NG1 = (CG_GW1 + 255) / 256, NG2 = (F * CG_MAXH + 255) / 256;
+    float v1[N1], v2[N2], v3[N3], g1[NG1], g2[NG2];
+    const int ng1 = gws ? A.gH * K3 : 0, ng2 = gws ? F * A.gH : 0;
 #pragma unroll
-  for (int i = 0; i < N1; ++i) v1[i] = t + 256 * i < H * K ? A.W1[t + 256 * i] : 0.f;
+    for (int i = 0; i < N1; ++i) v1[i] = t + 256 * i < H * K ? A.W1[t + 256 * i] : 0.f;
 #pragma unroll
-  for (int i = 0; i < N2; ++i) v2[i] = t + 256 * i < F * H ? A.W2[t + 256 * i] : 0.f;
+    for (int i = 0; i < N2; ++i) v2[i] = t + 256 * i < F * H ? A.W2[t + 256 * i] : 0.f;
 #pragma unroll
-  for (int i = 0; i < N3; ++i) v3[i] = t + 256 * i < C2 * C2 ? A.Wt2[t + 256 * i] : 0.f;
+    for (int i = 0; i < N3; ++i) v3[i] = t + 256 * i < C2 * C2 ? A.Wt2[t + 256 * i] : 0.f;
 #pragma unroll
-  for (int i = 0; i < NG1; ++i) g1[i] = t + 256 * i < ng1 ? A.gW1[t + 256 * i] : 0.f;
+    for (int i = 0; i < NG1; ++i) g1[i] = t + 256 * i < ng1 ? A.gW1[t + 256 * i] : 0.f;
 #pragma unroll
-  for (int i = 0; i < NG2; ++i) g2[i] = t + 256 * i < ng2 ? A.gW2[t + 256 * i] : 0.f;
+    for (int i = 0; i < NG2; ++i) g2[i] = t + 256 * i < ng2 ? A.gW2[t + 256 * i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < N1; ++i) if (t + 256 * i < H * K) w1[t + 256 * i] = v1[i];
+#pragma unroll
+    for (int i = 0; i < N2; ++i) if (t + 256 * i < F * H) w2[t + 256 * i] = v2[i];
+#pragma unroll
+    for (int i = 0; i < N3; ++i) if (t + 256 * i < C2 * C2) wt2[t + 256 * i] = v3[i];
+#pragma unroll
+    for (int i = 0; i < NG1; ++i) if (t + 256 * i < ng1) gw1[t + 256 * i] = g1[i];
+#pragma unroll
+    for (int i = 0; i < NG2; ++i) if (t + 256 * i < ng2) gw2[t + 256 * i] = g2[i];
+  }
   __shared__ float red[4][F];
   CB_STAMP(1)
   // ---------------------------------------------------------------- phase 1
@@ -1250,18 +1253,8 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
     if (t < F) st_sc1(T.p1 + (size_t)un * F + t, ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t]);
     __syncthreads();
   }
-#pragma unroll
-  for (int i = 0; i < N1; ++i) if (t + 256 * i < H * K) w1[t + 256 * i] = v1[i];
-#pragma unroll
-  for (int i = 0; i < N2; ++i) if (t + 256 * i < F * H) w2[t + 256 * i] = v2[i];
-#pragma unroll
-  for (int i = 0; i < N3; ++i) if (t + 256 * i < C2 * C2) wt2[t + 256 * i] = v3[i];
-#pragma unroll
-  for (int i = 0; i < NG1; ++i) if (t + 256 * i < ng1) gw1[t + 256 * i] = g1[i];
-#pragma unroll
-  for (int i = 0; i < NG2; ++i) if (t + 256 * i < ng2) gw2[t + 256 * i] = g2[i];
   CB_STAMP(2)
-  grid_sync(gridDim.x, T.fenced);   // (its workgroup barriers publish the weights too)
+  grid_sync(gridDim.x, T.fenced);
   CB_STAMP(3)
   // ---------------------------------------------------------------- phase 2
   __shared__ float sdy[F], sy1[F], sv[F], sw[F], sdw[F], gv[F], d1[F];
