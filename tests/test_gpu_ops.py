@@ -541,3 +541,49 @@ def test_edge_ops_node_epilogues(hb, G, NF, NC, F):
     for a, b, nm in zip(oh[1:], oe[1:], ["GzEs", "GzEt", "Vu"]):
         close(a, b, rtol=5e-4, name=nm)
     close(nxs_h, nxs_e, rtol=5e-4, name="g_xs(E)"); close(nxt_h, nxt_e, rtol=5e-4, name="g_xt(E)")
+
+
+def test_node_x3_policy(hb):
+    """The node level's gradient chains and weight gradients follow the edge
+    path (pf::node_x3): bf16x3 on the default `mfma` path, fp32 on the exact
+    `mfma32` path.  SModel node_mlp_2's shape (100-wide, the RS backward and
+    the <8, 8> weight gradient): mfma32 within 1e-5 of the float64 emulation,
+    mfma within the 5e-5 bar and visibly coarser (the split path is live)."""
+    import pfsgnn
+    blocks, H, O, N, G = [10, 80, 10], 100, 10, 38 * 64 + 26, 16
+    gen = torch.Generator().manual_seed(4242)
+    K = sum(blocks)
+    X, col = [], 0
+    for rows in blocks:
+        X.append((r(rows, N, gen=gen), col, False))
+        col += rows
+    W1, b1 = r(H, K, scale=0.2, gen=gen), r(H, scale=0.3, gen=gen)
+    W2, b2 = r(O, H, scale=0.2, gen=gen), r(O, gen=gen)
+    dY = r(O, N, gen=gen)
+    emu = EmuBackend()
+
+    def run(be, conv):
+        segs = [(conv(t), c, pg) for t, c, pg in X]
+        w = [conv(t) for t in (W1, b1, W2, b2)]
+        Y, Z, Yp, mu, var = be.mlp_fwd(segs, N, *w, bn=None)
+        outs = [(conv(torch.zeros(t.shape[0], N)), t.shape[0], False) for t, _, _ in X]
+        dYp, dZ = be.mlp_bwd(conv(dY), Z, w[0], w[2], K, bn=None, outs=outs)
+        dW1 = conv(torch.zeros(H, K))
+        be.wgrad_cat(dZ, segs, dW1)
+        return {"dZ": dZ, "dX1": outs[1][0], "dW1": dW1}
+
+    ref = run(emu, lambda t: t.clone())
+    prev = pfsgnn.get_edge_path()
+    err = {}
+    try:
+        for path in ("mfma32", "mfma"):
+            pfsgnn.set_edge_path(path)
+            got = run(hb, cuda)
+            err[path] = {k: ((cpu(got[k]) - v).abs().max() / v.abs().max()).item() for k, v in ref.items()}
+    finally:
+        pfsgnn.set_edge_path(prev)
+    for k in ref:
+        assert err["mfma32"][k] <= 1e-5, (k, err)
+        assert err["mfma"][k] <= 5e-5, (k, err)
+    assert err["mfma"]["dW1"] > 4 * err["mfma32"]["dW1"], err   # the bf16x3 weight gradient ran
+    assert err["mfma"]["dX1"] > 4 * err["mfma32"]["dX1"], err   # the bf16x3 input-gradient chain ran
