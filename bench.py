@@ -31,24 +31,32 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 NF, NC, FDIM = 2394, 128, 10      # overridden by --fibers / --classes
-# what each edge path computes in (include/pfsgnn.h); the
-# node level, reductions, BatchNorm statistics and the loss are fp32 in all
+# what each edge path computes in (include/pfsgnn.h).  The
+# node level (per-fiber / per-class MLPs, pf::node_x3) runs its forward in fp32
+# on every path and its gradient chains and weight gradients in bf16x3 on every
+# path but the exact-fp32 ones (mfma32, valu, bf16y); reductions, BatchNorm
+# statistics, Adam and the loss are fp32 everywhere.
+_NODE_X3 = "; node level: fp32 forward, bf16x3 gradient chains and weight gradients"
+_NODE_F32 = "; node level fp32"
 PRECISION = {
     "mfma": "fp32 MFMA forward contractions and recompute; backward gradient chains and weight "
-            "gradients bf16x3 (~2^-16 relative per product); fp32 accumulation and edge state",
+            "gradients bf16x3 (~2^-16 relative per product); fp32 accumulation and edge state"
+            + _NODE_X3,
     "mfma32": "every per-edge contraction exact fp32 MFMA (v_mfma_f32_16x16x4_f32), the weight "
-              "gradients' outer products included; fp32 accumulation and edge state",
+              "gradients' outer products included; fp32 accumulation and edge state" + _NODE_F32,
     "valu": "fp32 fmaf chains on the vector ALU; weight gradients exact fp32 MFMA "
-            "(v_mfma_f32_16x16x4_f32)",
-    "bf16y": "mfma32 arithmetic with the edge state rounded to bf16",
-    "bf16m": "every per-edge contraction a single bf16 MFMA, fp32 accumulation and edge state",
-    "bf16": "single-bf16 MFMA contractions and bf16 edge state",
+            "(v_mfma_f32_16x16x4_f32)" + _NODE_F32,
+    "bf16y": "mfma32 arithmetic with the edge state rounded to bf16" + _NODE_F32,
+    "bf16m": "every per-edge contraction a single bf16 MFMA, fp32 accumulation and edge state"
+             + _NODE_X3,
+    "bf16": "single-bf16 MFMA contractions and bf16 edge state" + _NODE_X3,
     "bf16x6": "forward contractions and their backward recompute on bf16 MFMAs with three-way "
               "split operands (hi+mid+lo, six products: fp32-class, ~2^-24 relative); backward "
-              "gradient chains and weight gradients bf16x3; fp32 accumulation and edge state",
+              "gradient chains and weight gradients bf16x3; fp32 accumulation and edge state"
+              + _NODE_X3,
     "bf16x3": "every per-edge contraction (forward, backward recompute, gradient chains, weight "
               "gradients) on bf16 MFMAs with split hi+lo operands (bf16x3, ~2^-16 relative per "
-              "product); fp32 accumulation, edge state, node level and loss (BASELINE configs[4])",
+              "product); fp32 accumulation, edge state and loss (BASELINE configs[4])" + _NODE_X3,
 }
 # the arithmetic each edge path computes in (`precision` spells it out): the
 # default path's backward products are split-bf16 (bf16x3), its forward fp32
@@ -57,6 +65,7 @@ DTYPE = {"mfma": "f32 (bf16x3 backward products)", "mfma32": "f32", "valu": "f32
          "bf16x6": "f32 (split-bf16 products: bf16x6 forward, bf16x3 backward)", "bf16x3": "bf16x3"}
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: dense fp32-input MFMA (= fp32 vector peak)
+BF16_MFMA_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 
 
 def parse():
@@ -114,28 +123,82 @@ def kernel_bytes_per_edge(F, first_block_excluded=False):
 
 
 # per-edge algorithmic FLOPs (2 per real multiply-add of the unpadded layer
-# shapes); H = 4F hidden units of the EdgeModel MLP,
-# C = 2F of the S/T message MLPs.  source_bwd includes TModel's input-gradient
-# chain (its pre-activation comes from target_fwd's mask, not recomputed);
-# edge_mlp_bwd's input-gradient product is absent in block 0.
-def kernel_flops_per_edge(F, B):
+# shapes), split by the arithmetic they run in: "fwd" the
+# forward contractions (and a backward kernel's recompute of them), "grad" the
+# gradient chains, "wg" the weight gradients (sums over edges of outer
+# products), "valu" the elementwise work (activations, moments, BatchNorm
+# affines).  H = 4F hidden units of the EdgeModel MLP, C = 2F of the S/T
+# message MLPs.  source_bwd includes TModel's input-gradient chain (its
+# pre-activation comes from target_fwd's mask, not recomputed); edge_mlp_bwd's
+# input-gradient product is absent in block 0.
+def kernel_flops_split(F, B):
     H, C = 4 * F, 2 * F
     return {
-        "edge_mlp_fwd": 2 * (H * F + F * H) + 4 * H,
-        "source_fwd": 2 * (C * F + C * C) + 4 * C + 12 * C,
-        "target_fwd": 2 * C * F + 4 * C,
-        "target_bwd": 2 * C * F + 3 * C,
-        "source_bwd": 2 * (C * F + C * C + C * C + F * C + F * C + C * C + C * F) + 12 * C,
-        "edge_mlp_bwd": 2 * (H * F + H * F + H * F + F * H) + 2 * (F * H) * (B - 1) / B + 8 * H,
+        "edge_mlp_fwd": {"fwd": 2 * (H * F + F * H), "valu": 4 * H},
+        "source_fwd": {"fwd": 2 * (C * F + C * C), "valu": 16 * C},
+        "target_fwd": {"fwd": 2 * C * F, "valu": 4 * C},
+        "target_bwd": {"wg": 2 * C * F, "valu": 3 * C},
+        "source_bwd": {"fwd": 2 * (C * F + C * C), "grad": 2 * (C * C + F * C + F * C),
+                       "wg": 2 * (C * C + C * F), "valu": 12 * C},
+        "edge_mlp_bwd": {"fwd": 2 * H * F, "grad": 2 * H * F + 2 * (F * H) * (B - 1) / B,
+                         "wg": 2 * (F * H + H * F), "valu": 8 * H},
     }
 
 
-# the part of kernel_flops_per_edge that recomputes forward activations (the
-# backward kernels keep no per-edge hidden state): EdgeModel's first Linear in
-# edge_mlp_bwd, SModel's message MLP in source_bwd
-def recompute_flops_per_edge(F):
-    H, C = 4 * F, 2 * F
-    return {"edge_mlp_bwd": 2 * H * F, "source_bwd": 2 * (C * F + C * C)}
+EDGE_KERNELS = ["edge_mlp_fwd", "source_fwd", "target_fwd", "target_bwd", "source_bwd",
+                "edge_mlp_bwd"]
+
+
+def kernel_flops_per_edge(F, B):
+    return {k: sum(v.values()) for k, v in kernel_flops_split(F, B).items()}
+
+
+# how each edge path computes each class of flops (include/pfsgnn.h,
+# pfsgnn_mfma_core.h FwdLayer / GradLayer / WgImg): ("f32", 1) exact fp32
+# (MFMA or VALU, 157.3 TF/s), ("bf16", k) k bf16 MFMA products per product
+# (bf16x3 = 3, bf16x6 = 6, single bf16 = 1; 2.5 PF/s dense)
+PATH_ARITH = {
+    "mfma":   {"fwd": ("f32", 1), "grad": ("bf16", 3), "wg": ("bf16", 3)},
+    "mfma32": {"fwd": ("f32", 1), "grad": ("f32", 1), "wg": ("f32", 1)},
+    "valu":   {"fwd": ("f32", 1), "grad": ("f32", 1), "wg": ("f32", 1)},
+    "bf16y":  {"fwd": ("f32", 1), "grad": ("f32", 1), "wg": ("f32", 1)},
+    "bf16m":  {"fwd": ("bf16", 1), "grad": ("bf16", 1), "wg": ("bf16", 3)},
+    "bf16":   {"fwd": ("bf16", 1), "grad": ("bf16", 1), "wg": ("bf16", 3)},
+    "bf16x6": {"fwd": ("bf16", 6), "grad": ("bf16", 3), "wg": ("bf16", 3)},
+    "bf16x3": {"fwd": ("bf16", 3), "grad": ("bf16", 3), "wg": ("bf16", 3)},
+}
+
+
+def compute_floor_s(kernel, F, B, path, E):
+    """The matrix/vector floor of one launch over E edges: fp32 flops at the
+    fp32 peak plus bf16 MFMA products at the dense bf16 peak (MI355X_MICROARCH.md)
+    -> (seconds, {f32 flops, bf16 product-flops})."""
+    ar = PATH_ARITH[path]
+    f32 = bf = 0.0
+    for cls, fl in kernel_flops_split(F, B)[kernel].items():
+        kind, k = ar.get(cls, ("f32", 1))
+        if kind == "f32":
+            f32 += fl * E
+        else:
+            bf += k * fl * E
+    return f32 / (F32_MFMA_PEAK_TFS * 1e12) + bf / (BF16_MFMA_PEAK_TFS * 1e12), \
+        {"f32_flops": int(f32), "bf16_product_flops": int(bf)}
+
+
+def kernel_roofline(kernel, F, B, path, E, bytes_per_launch, seconds):
+    """Both roofs of one launch and the binding one (the larger floor)."""
+    t_mm, fl = compute_floor_s(kernel, F, B, path, E)
+    t_hbm = bytes_per_launch / (HBM_PEAK_GBS * 1e9)
+    hbm = {"achieved": round(bytes_per_launch / seconds / 1e9, 1), "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(t_hbm / seconds, 4), "floor_us": round(t_hbm * 1e6, 1)}
+    # the compute roof in fp32-equivalent TFLOP/s: bf16 products weighted by
+    # the fp32 / bf16 peak ratio, so that achieved / peak = floor / duration
+    eq = fl["f32_flops"] + fl["bf16_product_flops"] * F32_MFMA_PEAK_TFS / BF16_MFMA_PEAK_TFS
+    mm = {"achieved": round(eq / seconds / 1e12, 2), "peak": F32_MFMA_PEAK_TFS,
+          "unit": "TFLOP/s (fp32-equivalent)", "frac": round(t_mm / seconds, 4),
+          "floor_us": round(t_mm * 1e6, 1), **fl}
+    bound = "hbm" if t_hbm >= t_mm else "mfma"
+    return bound, hbm, mm
 
 
 def pmc_traffic(kernel, E, F):
@@ -325,6 +388,9 @@ def main():
     # (PFSGNN_BENCH_ANY_LOSS=1: timing studies of ablation builds, tools/variants.sh)
     assert torch.isfinite(loss).item() or os.environ.get("PFSGNN_BENCH_ANY_LOSS") == "1", \
         "non-finite loss"
+    # no device-wide barrier of the fused class-side launches timed out
+    sync_faults = native.sync_faults()
+    assert sync_faults == 0, f"{sync_faults} device-wide barrier time-outs"
     # ---- N > 1: the eager tail of a step (outside the captured graph): the
     # buffer broadcast before the replay, the gradient all-reduce and Adam
     # after it, each timed alone (synchronised) over a few extra steps
@@ -376,24 +442,13 @@ def main():
             consistency[name + "_bitwise_equal"] = bool(torch.equal(hi, lo))
         assert all(consistency.values()), consistency
 
-    # ---- the dominant kernel's duration INSIDE the replayed step: the step
-    # captured once more with edge_mlp_bwd launched twice back to back
-    # (pfsgnn_timing_repeat; the kernel only overwrites its outputs), both
+    # ---- each edge kernel's duration INSIDE the replayed step: the step
+    # captured once more with that kernel launched twice back to back
+    # (pfsgnn_timing_repeat; the kernel only overwrites its outputs), the two
     # graphs replayed alternately, timed with HIP events on the launch stream;
     # (repeat - plain) / launches per step = the kernel's in-situ time
-    in_graph = None
+    in_graph = {}
     if use_graph and native.get_edge_path() != "valu":
-        native.timing_repeat("edge_mlp_bwd", 1)
-        try:
-            g_rep = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_rep):
-                fwd_bwd()
-                if world == 1:
-                    opt.step()
-        finally:
-            native.timing_repeat("edge_mlp_bwd", 0)
-        torch.cuda.synchronize()
-
         def replay_ms(gx, reps):
             t_a, t_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t_a.record()
@@ -404,20 +459,32 @@ def main():
             return t_a.elapsed_time(t_b) / reps
 
         reps = max(5, min(args.steps, 30))
-        base, rep = [], []
-        g_rep.replay()
-        for _ in range(3):
-            base.append(replay_ms(graph, reps))
-            rep.append(replay_ms(g_rep, reps))
-        base.sort()
-        rep.sort()
-        in_graph = {"kernel": "edge_mlp_bwd", "launches_per_step": B,
-                    "plain_ms_per_step": round(base[1], 4), "repeat_ms_per_step": round(rep[1], 4),
-                    "avg_launch_us": round((rep[1] - base[1]) / B * 1e3, 1),
-                    "method": "marginal time of one extra back-to-back launch per call in the "
-                              "replayed step (median of 3 alternating rounds of %d replays, HIP "
-                              "events on the launch stream)" % reps}
-        del g_rep
+        for kname in EDGE_KERNELS:
+            native.timing_repeat(kname, 1)
+            try:
+                g_rep = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g_rep):
+                    fwd_bwd()
+                    if world == 1:
+                        opt.step()
+            finally:
+                native.timing_repeat(kname, 0)
+            torch.cuda.synchronize()
+            base, rep = [], []
+            g_rep.replay()
+            for _ in range(3):
+                base.append(replay_ms(graph, reps))
+                rep.append(replay_ms(g_rep, reps))
+            base.sort()
+            rep.sort()
+            in_graph[kname] = {"plain_ms_per_step": round(base[1], 4),
+                               "repeat_ms_per_step": round(rep[1], 4),
+                               "extra_ms_per_step": round(rep[1] - base[1], 4)}
+            del g_rep
+        torch.cuda.synchronize()
+        in_graph_method = ("marginal time of one extra back-to-back launch per call in the "
+                           "replayed step (median of 3 alternating rounds of %d replays, HIP "
+                           "events on the launch stream)" % reps)
 
     # ---- the same step on the other edge paths (BASELINE configs[4]: the
     # bf16x3 contractions; the exact-fp32 one), each captured and replayed like
@@ -463,56 +530,64 @@ def main():
     torch.cuda.synchronize()
     native.timing_enable(False)
 
-    # ---- per-kernel times (HIP events on the launch stream, timed region only)
+    # ---- per-kernel times (HIP events on the launch stream) and rooflines:
+    # each edge kernel against both roofs -- algorithmic HBM bytes at 8 TB/s,
+    # and its flops by the arithmetic the edge path runs them in (fp32 at the
+    # fp32 peak, bf16 MFMA products at the bf16 peak); the binding roof is
+    # the one with the larger floor
     per_edge = kernel_bytes_per_edge(FDIM)
     kt = {}
     for k in native.KERNELS:
         ms, n = native.timing_query(k)
         if n:
             kt[k] = (ms, n)
-    dom = max(kt, key=lambda k: kt[k][0])
-    if in_graph is not None:
-        dom = in_graph["kernel"]
-    ms, n = kt[dom]
-    launches_bytes = per_edge.get(dom, 4 * FDIM) * E
-    if dom == "edge_mlp_bwd":      # block 0 writes no input gradient
-        launches_bytes = (per_edge[dom] * (B - 1) + 3 * 4 * FDIM) * E / B
-    eager_avg_s = ms / n / 1e3
-    # the duration the roofline uses: in the replayed step (the timed region's
-    # own conditions) where measured, else the eager one
-    avg_s = in_graph["avg_launch_us"] / 1e6 if in_graph is not None else eager_avg_s
-    achieved = launches_bytes / avg_s / 1e9
-    flops = kernel_flops_per_edge(FDIM, B).get(dom)
+    path = native.get_edge_path()
+    kernels = {}
+    for k in EDGE_KERNELS:
+        if k not in kt:
+            continue
+        ms, n = kt[k]
+        launches = n / prof_steps
+        bpl = per_edge[k] * E
+        if k == "edge_mlp_bwd":      # block 0 writes no input gradient
+            bpl = (per_edge[k] * (B - 1) + 3 * 4 * FDIM) * E / B
+        eager_s = ms / n / 1e3
+        ig = in_graph.get(k)
+        sec = ig["extra_ms_per_step"] / launches / 1e3 if ig and ig["extra_ms_per_step"] > 0 \
+            else eager_s
+        bound, hbm, mm = kernel_roofline(k, FDIM, B, path, E, bpl, sec)
+        kernels[k] = {"bound": bound, "frac": (hbm if bound == "hbm" else mm)["frac"],
+                      "avg_launch_us": round(sec * 1e6, 1),
+                      "timing": "in_graph" if sec != eager_s else "eager",
+                      "eager_avg_launch_us": round(eager_s * 1e6, 1),
+                      "launches_per_step": launches, "bytes_per_launch": int(bpl),
+                      "hbm": hbm, "mfma": mm}
+    dom = max(kernels, key=lambda k: kernels[k]["avg_launch_us"] * kernels[k]["launches_per_step"])
+    kd = kernels[dom]
+    top = kd["hbm"] if kd["bound"] == "hbm" else kd["mfma"]
     tr = pmc_traffic(dom, E, FDIM)
-    hbm = {"achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(achieved / HBM_PEAK_GBS, 4)}
-    # both roofs of the dominant kernel; "bound" names the binding one (the
-    # larger fraction): the fp32-MFMA edge kernels do ~40 flop per HBM byte,
-    # well past the fp32 ridge point (157.3 TF/s / 8 TB/s ~ 20 flop/B)
-    mfma = None
-    if flops is not None:
-        tfs = flops * E / avg_s / 1e12
-        rc = recompute_flops_per_edge(FDIM).get(dom, 0)
-        mfma = {"achieved": round(tfs, 2), "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                "frac": round(tfs / F32_MFMA_PEAK_TFS, 4), "flops_per_launch": int(flops * E),
-                # the same without the forward recompute's flops
-                "frac_excl_recompute": round(tfs * (flops - rc) / flops / F32_MFMA_PEAK_TFS, 4)}
-    top = mfma if mfma is not None and mfma["frac"] > hbm["frac"] else hbm
-    roofline = {"bound": "mfma" if top is mfma else "hbm", "kernel": dom,
+    roofline = {"bound": kd["bound"], "kernel": dom,
                 "achieved": top["achieved"], "peak": top["peak"], "unit": top["unit"],
                 "frac": top["frac"],
                 "traffic": None if tr is None else int(tr[0]),
                 "traffic_source": None if tr is None else f"profiles/{tr[1]} (PMC bytes per launch)",
-                "hbm": hbm, "mfma": mfma,
-                "avg_launch_us": round(avg_s * 1e6, 1), "launches": n,
-                "in_graph": in_graph, "eager_avg_launch_us": round(eager_avg_s * 1e6, 1),
-                "bytes_per_launch": int(launches_bytes),
+                "hbm": kd["hbm"], "mfma": kd["mfma"],
+                "avg_launch_us": kd["avg_launch_us"], "launches": kd["launches_per_step"],
+                "eager_avg_launch_us": kd["eager_avg_launch_us"],
+                "bytes_per_launch": kd["bytes_per_launch"],
+                "edge_kernels": {k: {kk: v[kk] for kk in ("bound", "frac", "avg_launch_us", "timing")}
+                                 | {"hbm_frac": v["hbm"]["frac"], "mfma_frac": v["mfma"]["frac"]}
+                                 for k, v in kernels.items()},
+                "pricing": "algorithmic bytes / 8 TB/s vs fp32 flops / 157.3 TF/s + bf16 MFMA "
+                           "products / 2.5 PF/s (the edge path's arithmetic per flop class: "
+                           f"{PATH_ARITH.get(path)}); the binding roof has the larger floor",
                 "kernel_ms_per_step": {k: round(v[0] / prof_steps, 3) for k, v in kt.items()},
-                "timing": (f"avg_launch_us: in_graph (marginal in the replayed step); "
-                           if in_graph is not None else "") +
+                "timing": (f"avg_launch_us: {in_graph_method}; " if in_graph else "") +
                           f"kernel_ms_per_step and eager_avg_launch_us: HIP events around each "
                           f"launch behind a lead-in spin kernel, {prof_steps} eager steps after "
                           f"the timed region (eager launches run ~5% slower than replayed ones)"}
+    if in_graph:
+        roofline["in_graph"] = in_graph
 
     if rank == 0:
         cpu = None
@@ -539,6 +614,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        line["sync_faults"] = sync_faults
         if consistency is not None:
             line["rank_consistency"] = consistency
         if tail is not None:

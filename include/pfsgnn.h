@@ -289,8 +289,11 @@ int pfsgnn_target_global_fwd(
  * next block's Pt / Qt -- with every output of pfsgnn_target_global_fwd.  The
  * class launch runs G * ceil(NC / 32) units of 32 classes on at most one
  * workgroup per CU with one device-wide barrier between node_mlp_2 (and its
- * BatchNorm partials) and the norm (pfsgnn_sync_faults counts barrier
- * time-outs; 0 in a healthy run).  node_mlp_2's weights: W1 [4F][4F], W2
+ * BatchNorm partials) and the norm.  The grid must be co-resident (checked
+ * against the occupancy API: an error otherwise); a barrier wait that outlives
+ * ~1.5 s -- a workgroup never scheduled because another process holds the
+ * CUs -- raises pfsgnn_sync_faults' count and traps, so the launch fails
+ * instead of computing with partials that were never handed over.  node_mlp_2's weights: W1 [4F][4F], W2
  * [F][4F] (its input [x_t, agg, u[batch]], gnn.py:191).  Replaces
  * pfsgnn_target_fwd + pfsgnn_target_global_fwd (4 launches) on complete graphs. */
 typedef struct {
@@ -318,10 +321,11 @@ size_t pfsgnn_block_tail_bytes(void);
 /* The class side of a block's backward on a complete batch (training
  * BatchNorm, gnn.py:191-192 + 218-223 under autograd) in ONE launch, units of
  * 16 classes of one graph around two device-wide barriers:
- *   1. gu_up += per-graph sums of the pending u[batch] gradients of the block
- *      above (npend tables [F][G*pend_n[i]], pend_n = NF or NC: what
- *      pfsgnn_graph_reduce_multi would add);
- *   2. the GlobalModel backward of pfsgnn_global_bwd on dY = gu_up (gV, gdZ, dwp
+ *   1. dY = gu_up + the per-graph sums of the pending u[batch] gradients of
+ *      the block above (npend tables [F][G*pend_n[i]], pend_n = NF or NC: what
+ *      pfsgnn_graph_reduce_multi would add to gu_up).  gu_up is READ ONLY: the
+ *      sum feeds step 2 and is not written back;
+ *   2. the GlobalModel backward of pfsgnn_global_bwd on that dY (gV, gdZ, dwp
  *      written; gu += its u-input gradient; g_xs += d mean_xs / NF and g_xt +=
  *      d mean_xt / NC broadcast), then TModel's BatchNorm sums on the new g_xt;
  *   3. pfsgnn_mlp_bwd of node_mlp_2 + BatchNorm on dY = g_xt (dYp, dZ written,
@@ -345,8 +349,13 @@ typedef struct {
 } pfsgnn_class_bwd;
 int pfsgnn_target_class_bwd(const pfsgnn_class_bwd* a, void* ws, size_t ws_bytes, void* stream);
 size_t pfsgnn_class_bwd_bytes(void);
-/* device-wide barrier time-outs since load (a diagnostic; *n = count) */
+/* device-wide barrier time-outs since load (*n = count; 0 in a healthy run --
+ * a time-out also traps the launch that hit it) */
 int pfsgnn_sync_faults(unsigned* n);
+/* the device-wide barrier's form for later launches: 0 (default) the sc1
+ * hand-off with relaxed agent-scope counters, 1 acq_rel arrival / acquire poll
+ * (an L2 write-back and L1 invalidate per workgroup); bitwise the same results */
+int pfsgnn_set_grid_sync_fenced(int fenced);
 /* One row block of an input-gradient output: rows `rows` of dX go to x
  * ([rows][N], overwritten, or accumulated when add != 0); x == NULL drops them. */
 typedef struct {

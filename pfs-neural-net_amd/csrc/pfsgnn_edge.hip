@@ -1621,7 +1621,8 @@ static int edge_mlp_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, i
   if (use_mfma()) {
     PF_REQUIRE(part, "pfsgnn_edge_mlp_fwd", "workspace too small");
     { pf::Timer tm_("edge_mlp_fwd", st);
-    if (int rc = pfm::edge_mlp_fwd(geo, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part, mf_prec(0, F), mf_bfy(), st)) return rc;
+    for (int rep = 0, nrep = 1 + pf::repeats("edge_mlp_fwd"); rep < nrep; ++rep)
+      if (int rc = pfm::edge_mlp_fwd(geo, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part, mf_prec(0, F), mf_bfy(), st)) return rc;
     tm_.end(); }
     hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(256), 0, st, part, geo.nblocks, F, geo.E,
                        mu, var, bn);
@@ -1711,9 +1712,10 @@ static int source_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
   }
   if (use_mfma() && NC <= 256 && sfwd_tiles()) {
     pf::Timer tm_("source_fwd", st);
-    if (int rc = pfm::source_fwd_tiles(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs, mf_prec(1, F),
-                                       sfwd_wave_nc(), st))
-      return rc;
+    for (int rep = 0, nrep = 1 + pf::repeats("source_fwd"); rep < nrep; ++rep)
+      if (int rc = pfm::source_fwd_tiles(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs,
+                                         mf_prec(1, F), sfwd_wave_nc(), st))
+        return rc;
     tm_.end();
     return pf::check_launch("pfsgnn_source_fwd");
   }
@@ -1781,7 +1783,9 @@ static int target_fwd_edges(const pfsgnn_sliced_t* sl, const EdgeGeo& geo, int F
                                     mf_prec(1, F), st))
       return rc;
   } else if (use_mfma()) {
-    if (int rc = pfm::target_fwd(geo, F, y, sc, sh, Rs, Wt1, part, tmask, mf_prec(1, F), st)) return rc;
+    for (int rep = 0, nrep = 1 + pf::repeats("target_fwd"); rep < nrep; ++rep)
+      if (int rc = pfm::target_fwd(geo, F, y, sc, sh, Rs, Wt1, part, tmask, mf_prec(1, F), st))
+        return rc;
   } else {
     DISPATCH_F(F, hipLaunchKernelGGL(k_target_fwd<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo,
                                      y, sc, sh, Rs, Wt1, part));
@@ -1889,9 +1893,10 @@ static int target_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
                                     tmask, tabs, mf_prec(1, F), st))
       return rc;
   } else if (use_mfma()) {
-    if (int rc = pfm::target_bwd(geo, F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part, tmask,
-                                 mf_prec(1, F), st))
-      return rc;
+    for (int rep = 0, nrep = 1 + pf::repeats("target_bwd"); rep < nrep; ++rep)
+      if (int rc = pfm::target_bwd(geo, F, y, sc, sh, Rs, Wt1, ghT, gz, gxe, part, tmask,
+                                   mf_prec(1, F), st))
+        return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_target_bwd<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo, y,
                                    sc, sh, Rs, Wt1, ghT, gz, gxe, part));
@@ -2103,10 +2108,11 @@ static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
                                     tmask, tabs, mf_prec(1, F), st))
       return rc;
   } else if (mfma) {
-    if (int rc = pfm::source_bwd(geo, F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT,
-                                 g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask,
-                                 mf_prec(1, F), st))
-      return rc;
+    for (int rep = 0, nrep = 1 + pf::repeats("source_bwd"); rep < nrep; ++rep)
+      if (int rc = pfm::source_bwd(geo, F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+                                   ghT, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask,
+                                   mf_prec(1, F), st))
+        return rc;
   } else {
   DISPATCH_F(F, hipLaunchKernelGGL(k_source_bwd<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo, y,
                                    sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghT, g_next,

@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float*
     r.v[0] = ld_frows<F>(rxe, (uint32_t)c * eoc, ro);
     return r;
   };
-  class_stream<MF_DEPTH_FWD>(c0, c1, load, [&](const Rows<1>& rows, int c) {
+  class_stream<MF_DEPTH_FWD, true>(c0, c1, load, [&](const Rows<1>& rows, int c) {
     const floatx4 x[1] = {edge_in<F>(rows.v[0], fm, xsc, scv, shv)};
     floatx4 z[NT], a[NT];
 #pragma unroll

@@ -120,9 +120,18 @@ __device__ __forceinline__ s16x8 cat8(s16x4 a, s16x4 b) {
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 __device__ __forceinline__ Fr8 cat(const Fr& a, const Fr& b) { return {cat8(a.h, b.h), cat8(a.l, b.l)}; }
+// (A and B are kept live past the MFMA so that its result never lands in their
+// registers: that overlap gives timing-dependent sums on gfx950, pf_mf8.)
+#ifndef MF_SRC_KEEP
+#define MF_SRC_KEEP 1
+#endif
 __device__ __forceinline__ floatx4 mf8(s16x8 a, s16x8 b, floatx4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b16x8, a),
-                                                 __builtin_bit_cast(b16x8, b), c, 0, 0, 0);
+  floatx4 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b16x8, a),
+                                                      __builtin_bit_cast(b16x8, b), c, 0, 0, 0);
+#if MF_SRC_KEEP
+  asm volatile("" : "+v"(d) : "v"(a), "v"(b));
+#endif
+  return d;
 }
 __device__ __forceinline__ floatx4 mma3w(const Fr8& a, const Fr8& b, floatx4 c) {
   c = mf8(a.l, b.h, c);
@@ -755,27 +764,59 @@ __device__ __forceinline__ float group_sum16(float v) {
 }
 
 // ------------------------------------------------------------ class stream
-// The edge rows of a wave's tiles are prefetched D classes ahead through a
-// register ring: D tiles' worth of 64-byte row loads stay in flight per wave.
-// load(c) returns the rows of class c; body(rows, c) consumes them.  The inner
-// loop is unrolled by D so the ring index is static.
-template <int D, class Load, class Body>
+// The edge rows of a wave's tiles are prefetched through a register ring of D
+// slots (slot d holds the rows of class c + d); load(c) returns the rows of
+// class c, body(rows, c) consumes them; the loop is unrolled by D so the slot
+// index is static.  Two refill orders:
+//   LATE = false: a slot is refilled with class c + d + D BEFORE the body of
+//     class c + d runs (conditionally, at the range's end).  The new rows and
+//     the ones being consumed are live together, so hipcc parks each new load
+//     in staging registers and copies it into the ring at the back edge, behind
+//     an s_waitcnt on a load issued one tile earlier;
+//   LATE = true: the slot is refilled AFTER the body (unconditionally, the class
+//     clamped to the range: a few re-reads of the last class at the end), so
+//     the slot keeps its registers across the back edge and D - 1 tiles of row
+//     loads are in flight while a tile computes.
+// Measured per kernel on the bench step (profiles/r05a_ring_ab.txt): LATE is
+// faster for edge_mlp_fwd (4 %), slower for source_bwd (10 %: at D = 2 its
+// refills start a whole body later), within noise elsewhere.
+template <int D, bool LATE = false, class Load, class Body>
 __device__ __forceinline__ void class_stream(int c0, int c1, Load load, Body body) {
   using R = decltype(load(c0));
   R ring[D];
+  if constexpr (!LATE) {
 #pragma unroll
-  for (int d = 0; d < D; ++d)
-    if (c0 + d < c1) ring[d] = load(c0 + d);
-  for (int c = c0; c < c1; c += D) {
+    for (int d = 0; d < D; ++d)
+      if (c0 + d < c1) ring[d] = load(c0 + d);
+    for (int c = c0; c < c1; c += D) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const int cc = c + d;
-      if (cc < c1) {
-        const R cur = ring[d];
-        if (cc + D < c1) ring[d] = load(cc + D);
-        body(cur, cc);
+      for (int d = 0; d < D; ++d) {
+        const int cc = c + d;
+        if (cc < c1) {
+          const R cur = ring[d];
+          if (cc + D < c1) ring[d] = load(cc + D);
+          body(cur, cc);
+        }
       }
     }
+  } else {
+    if (c1 <= c0) return;
+    const int last = c1 - 1;
+#pragma unroll
+    for (int d = 0; d < D; ++d) ring[d] = load(min(c0 + d, last));
+    int c = c0;
+    for (; c + D <= c1; c += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        body(ring[d], c + d);
+        // the refill stays behind the body's last read of the slot
+        __builtin_amdgcn_sched_barrier(0);
+        ring[d] = load(min(c + d + D, last));
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d)
+      if (c + d < c1) body(ring[d], c + d);
   }
 }
 

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <map>
 #include <cstdlib>
 #include <type_traits>
 
@@ -769,13 +770,27 @@ __global__ __launch_bounds__(CG_THREADS) void k_class_global_fwd(ClassGlobalArgs
 constexpr int CT_QBMAX = 64;                // most units per graph (NC <= 64 * CT)
 constexpr int CT_CLS = 32;                  // most classes per unit (8, 16 or 32: the
                                             // smallest that keeps the units <= 512)
-__device__ unsigned pf_tail_bar[2];         // device-wide barrier (fenced form): arrivals, generation
-__device__ unsigned pf_tail_bar_w;          // (default form) arrivals | generation << 16
-__device__ unsigned pf_sync_fault_count;    // barrier time-outs (diagnostic)
+// Device-wide barrier state: a pool of slots, one 128-byte line each; every
+// launch of a barrier kernel takes its own slot (pf::bar_slot(), round robin
+// on the host), so two such launches never share a word even when they run
+// at the same time on different streams.  Word 0: arrivals | generation << 16
+// (default form); words 1, 2: arrivals, generation (fenced form).  A slot is
+// clean between launches: the last arrival of every barrier resets the count.
+constexpr int PF_BAR_SLOTS = 64;
+__device__ unsigned pf_bar_pool[PF_BAR_SLOTS][32];
+__device__ unsigned pf_sync_fault_count;    // barrier time-outs (sticky)
 
-// every workgroup of the grid (all resident: the grid is at most one per CU)
-// waits here.  A wait that outlives ~2^24 sleeps is counted and abandoned, so
-// no wave can hang on it.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "grid_sync's sc1 hand-off is measured for gfx950 only (MI355X_MICROARCH.md)"
+#endif
+
+// Every workgroup of the grid waits here.  The launchers check that the grid
+// is co-resident (pf::check_coresident: at most the occupancy API's blocks per
+// CU times the CUs); a wait that still outlives ~2^24 sleeps (~1.5 s) means a
+// workgroup was never scheduled -- another process holding the CUs -- and
+// the kernel stops: the sticky fault count is raised and the wave traps, so
+// the launch fails (hipErrorLaunchFailure) instead of going on with partials
+// that were never handed over.
 // Default (fenced = 0): no cache maintenance.  Every byte handed across the
 // barrier is stored and loaded with agent-scope relaxed atomics (global_store /
 // load sc1: st_sc1 / ld_sc1), every wave waits for its stores (vmcnt(0)) before
@@ -783,38 +798,38 @@ __device__ unsigned pf_sync_fault_count;    // barrier time-outs (diagnostic)
 // agent-scope add, and the last arrival -- told by the value its add returned
 // -- resets the count and bumps the generation in one add on the same word
 // (arrivals in the low 16 bits), which the others poll with sc1 loads (MI355X_MICROARCH.md,
-// the sc1 hand-off table's first row: hipMalloc'd bytes, one workgroup per CU).
-// fenced = 1 (PFSGNN_GRID_SYNC_FENCED=1, A/B): the arrival is an agent-scope
-// acq_rel add and the poll an acquire -- an L2 write-back and an L1 invalidate
-// per workgroup and barrier (grid_sync_probe: 4.6 us at 64 workgroups, 15.6 at
-// 256, growing with the workgroups per XCD).
-__device__ void grid_sync(unsigned nb, int fenced) {
+// the sc1 hand-off table's first row).
+// fenced = 1 (pfsgnn_set_grid_sync_fenced / PFSGNN_GRID_SYNC_FENCED=1): the
+// arrival is an agent-scope acq_rel add and the poll an acquire -- an L2
+// write-back and an L1 invalidate per workgroup and barrier (grid_sync_probe:
+// 4.6 us at 64 workgroups, 15.6 at 256).  Both forms give bitwise the same
+// results (tests/test_gpu_grid_sync.py).
+__device__ __forceinline__ void grid_sync_fault() {
+  __hip_atomic_fetch_add(&pf_sync_fault_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_trap();
+}
+__device__ void grid_sync(unsigned* bar, unsigned nb, int fenced) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     if (fenced) {
-      const unsigned gen = __hip_atomic_load(&pf_tail_bar[1], __ATOMIC_ACQUIRE,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned a = __hip_atomic_fetch_add(&pf_tail_bar[0], 1u, __ATOMIC_ACQ_REL,
+      const unsigned gen = __hip_atomic_load(&bar[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned a = __hip_atomic_fetch_add(&bar[1], 1u, __ATOMIC_ACQ_REL,
                                                 __HIP_MEMORY_SCOPE_AGENT);
       if (a == nb - 1) {
-        __hip_atomic_store(&pf_tail_bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(&pf_tail_bar[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&bar[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&bar[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         unsigned spins = 0;
-        while (__hip_atomic_load(&pf_tail_bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        while (__hip_atomic_load(&bar[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) {
           __builtin_amdgcn_s_sleep(4);
-          if (++spins > (1u << 24)) {
-            __hip_atomic_fetch_add(&pf_sync_fault_count, 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
+          if (++spins > (1u << 24)) grid_sync_fault();
         }
       }
     } else {
       // one word: arrivals in the low 16 bits, the generation above; the last
       // arrival resets the count and bumps the generation in ONE add
-      unsigned* w = &pf_tail_bar_w;
+      unsigned* w = &bar[0];
       const unsigned a = __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned gen = a >> 16;
       if ((a & 0xffffu) == nb - 1) {
@@ -823,11 +838,7 @@ __device__ void grid_sync(unsigned nb, int fenced) {
         unsigned spins = 0;
         while ((__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 16) == gen) {
           __builtin_amdgcn_s_sleep(2);
-          if (++spins > (1u << 24)) {
-            __hip_atomic_fetch_add(&pf_sync_fault_count, 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
+          if (++spins > (1u << 24)) grid_sync_fault();
         }
       }
     }
@@ -854,6 +865,7 @@ struct TailArgs {
   float bscale;
   float *part, *xss, *yps;   // [nunits][PART_LEN], [nunits][F], [nunits][F] (sc1 hand-off)
   int fenced;                // grid_sync form
+  unsigned* bar;             // grid_sync slot (pf_bar_pool)
 };
 
 template <int F>
@@ -1037,7 +1049,7 @@ __global__ __launch_bounds__(256) void k_class_tail_fwd(TailArgs T) {
     __syncthreads();   // (LDS reuse by the next unit)
   }
   TAIL_STAMP(3)
-  grid_sync(gridDim.x, T.fenced);
+  grid_sync(T.bar, gridDim.x, T.fenced);
   TAIL_STAMP(4)
   // ---------------------------------------------------------------- phase 2
   __shared__ float cf[4][16];
@@ -1186,6 +1198,7 @@ struct CbArgs {
   int QB, nunits;
   float *p1, *p2;   // [nunits][F] u-gradient partials, [nunits][CB_PLEN] BatchNorm sums (sc1)
   int fenced;       // grid_sync form
+  unsigned* bar;    // grid_sync slot (pf_bar_pool)
 };
 
 template <int F>
@@ -1254,7 +1267,7 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
     __syncthreads();
   }
   CB_STAMP(2)
-  grid_sync(gridDim.x, T.fenced);
+  grid_sync(T.bar, gridDim.x, T.fenced);
   CB_STAMP(3)
   // ---------------------------------------------------------------- phase 2
   __shared__ float sdy[F], sy1[F], sv[F], sw[F], sdw[F], gv[F], d1[F];
@@ -1380,7 +1393,7 @@ __global__ __launch_bounds__(256) void k_class_bwd(CbArgs T) {
     __syncthreads();   // (LDS reuse by the next unit)
   }
   CB_STAMP(4)
-  grid_sync(gridDim.x, T.fenced);
+  grid_sync(T.bar, gridDim.x, T.fenced);
   CB_STAMP(5)
   // ---------------------------------------------------------------- phase 3
   __shared__ float BC[5][16];
@@ -2046,13 +2059,40 @@ size_t tail_ws_floats(int G, int NC, int F) {
   const size_t nu = (size_t)G * ((NC + (ct ? ct : CT_CLS) - 1) / (ct ? ct : CT_CLS));
   return nu * PART_LEN + 2 * nu * F + 64;
 }
-// grid_sync's form (A/B knob PFSGNN_GRID_SYNC_FENCED=1: the acq_rel form)
-static int grid_sync_fenced() {
-  static const int v = [] {
-    const char* e = getenv("PFSGNN_GRID_SYNC_FENCED");
-    return e && atoi(e) != 0 ? 1 : 0;
-  }();
-  return v;
+// grid_sync's form: 0 the sc1 hand-off (default), 1 the acq_rel form
+// (PFSGNN_GRID_SYNC_FENCED=1 at load, or pfsgnn_set_grid_sync_fenced)
+static int g_grid_sync_fenced = [] {
+  const char* e = getenv("PFSGNN_GRID_SYNC_FENCED");
+  return e && atoi(e) != 0 ? 1 : 0;
+}();
+static int grid_sync_fenced() { return g_grid_sync_fenced; }
+// the barrier slot of the next launch (round robin over pf_bar_pool)
+static unsigned* bar_slot() {
+  static unsigned* pool[64] = {};
+  static int next = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!pool[dev]) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(pf_bar_pool)) != hipSuccess) return nullptr;
+    pool[dev] = static_cast<unsigned*>(p);
+  }
+  const int slot = next;
+  next = (next + 1) % PF_BAR_SLOTS;
+  return pool[dev] + (size_t)slot * 32;
+}
+// every workgroup of a grid_sync launch must be resident at once: the grid is
+// at most one per CU, so the occupancy API must admit >= 1 block per CU (LDS,
+// registers) -- checked once per kernel
+static bool check_coresident(const void* kernel, int grid) {
+  static std::map<const void*, int> per_cu;
+  auto it = per_cu.find(kernel);
+  if (it == per_cu.end()) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, 256, 0) != hipSuccess) n = 0;
+    it = per_cu.emplace(kernel, n).first;
+  }
+  return it->second >= 1 && grid <= it->second * cu_count();
 }
 int class_tail_fwd(const pfsgnn_block_tail& a, const float* cpart, int BPG, float bscale,
                    float* scratch, hipStream_t st) {
@@ -2071,12 +2111,18 @@ int class_tail_fwd(const pfsgnn_block_tail& a, const float* cpart, int BPG, floa
   T.xss = T.part + (size_t)T.nunits * PART_LEN;
   T.yps = T.xss + (size_t)T.nunits * a.F;
   T.fenced = grid_sync_fenced();
+  T.bar = bar_slot();
+  PF_REQUIRE(T.bar, where, "barrier slot");
   const int grid = std::min(T.nunits, cu_count());
+  const void* kern = a.F == 8 ? (const void*)k_class_tail_fwd<8>
+                   : a.F == 10 ? (const void*)k_class_tail_fwd<10>
+                   : a.F == 16 ? (const void*)k_class_tail_fwd<16> : nullptr;
+  PF_REQUIRE(kern, where, "Fdim must be 8, 10 or 16");
+  PF_REQUIRE(check_coresident(kern, grid), where, "the barrier grid is not co-resident");
   switch (a.F) {
     case 8: hipLaunchKernelGGL(k_class_tail_fwd<8>, dim3(grid), dim3(256), 0, st, T); break;
     case 10: hipLaunchKernelGGL(k_class_tail_fwd<10>, dim3(grid), dim3(256), 0, st, T); break;
-    case 16: hipLaunchKernelGGL(k_class_tail_fwd<16>, dim3(grid), dim3(256), 0, st, T); break;
-    default: return pf::fail(where, "Fdim must be 8, 10 or 16");
+    default: hipLaunchKernelGGL(k_class_tail_fwd<16>, dim3(grid), dim3(256), 0, st, T); break;
   }
   return 0;
 }
@@ -2121,15 +2167,27 @@ extern "C" int pfsgnn_target_class_bwd(const pfsgnn_class_bwd* a, void* ws, size
   T.p1 = static_cast<float*>(ws);
   T.p2 = T.p1 + (size_t)T.nunits * a->F;
   T.fenced = pf::grid_sync_fenced();
+  T.bar = pf::bar_slot();
+  PF_REQUIRE(T.bar, where, "barrier slot");
   const int grid = std::min(T.nunits, cu_count());
+  const void* kern = a->F == 8 ? (const void*)k_class_bwd<8>
+                   : a->F == 10 ? (const void*)k_class_bwd<10>
+                   : a->F == 16 ? (const void*)k_class_bwd<16> : nullptr;
+  PF_REQUIRE(kern, where, "Fdim must be 8, 10 or 16");
+  PF_REQUIRE(pf::check_coresident(kern, grid), where, "the barrier grid is not co-resident");
   hipStream_t st = as_stream(stream);
   switch (a->F) {
     case 8: hipLaunchKernelGGL(k_class_bwd<8>, dim3(grid), dim3(256), 0, st, T); break;
     case 10: hipLaunchKernelGGL(k_class_bwd<10>, dim3(grid), dim3(256), 0, st, T); break;
-    case 16: hipLaunchKernelGGL(k_class_bwd<16>, dim3(grid), dim3(256), 0, st, T); break;
-    default: return pf::fail(where, "Fdim must be 8, 10 or 16");
+    default: hipLaunchKernelGGL(k_class_bwd<16>, dim3(grid), dim3(256), 0, st, T); break;
   }
   return pf::check_launch(where);
+}
+
+extern "C" int pfsgnn_set_grid_sync_fenced(int fenced) {
+  PF_REQUIRE(fenced == 0 || fenced == 1, "pfsgnn_set_grid_sync_fenced", "0 or 1");
+  pf::g_grid_sync_fenced = fenced;
+  return 0;
 }
 
 extern "C" int pfsgnn_sync_faults(unsigned* n) {

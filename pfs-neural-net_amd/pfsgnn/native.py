@@ -227,6 +227,7 @@ _SIGS = {
     "pfsgnn_sliced_max_nc": ([I, ctypes.POINTER(ctypes.c_int)], I),
     "pfsgnn_target_block_fwd": ([ctypes.POINTER(BlockTail), P, SZ, P], I),
     "pfsgnn_sync_faults": ([ctypes.POINTER(ctypes.c_uint)], I),
+    "pfsgnn_set_grid_sync_fenced": ([I], I),
     "pfsgnn_block_tail_bytes": ([], SZ),
     "pfsgnn_target_class_bwd": ([ctypes.POINTER(ClassBwd), P, SZ, P], I),
     "pfsgnn_class_bwd_bytes": ([], SZ),
@@ -310,6 +311,20 @@ def timing_enable(on=True):
     """on: False / True (events around each launch) / "spin" (the same behind
     a lead-in spin kernel: the kernel's own time in an eager step)."""
     lib().pfsgnn_timing_enable(2 if on == "spin" else (1 if on else 0))
+
+
+def sync_faults():
+    """Device-wide barrier time-outs since the library was loaded (0 when healthy;
+    a time-out also traps its launch)."""
+    n = ctypes.c_uint(0)
+    _check(lib().pfsgnn_sync_faults(ctypes.byref(n)), "pfsgnn_sync_faults")
+    return n.value
+
+
+def set_grid_sync_fenced(fenced):
+    """The device-wide barrier's form for later launches: False the sc1 hand-off
+    (default), True acq_rel arrival / acquire poll (pfsgnn_set_grid_sync_fenced)."""
+    _check(lib().pfsgnn_set_grid_sync_fenced(1 if fenced else 0), "pfsgnn_set_grid_sync_fenced")
 
 
 def timing_repeat(name, extra):
