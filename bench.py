@@ -291,9 +291,17 @@ def main():
     # every rank on cuda:0 and the gloo backend instead of RCCL
     if os.environ.get("PFSGNN_BENCH_SAME_DEVICE") == "1":
         local = 0
+        # ranks sharing one GPU cannot promise a co-resident grid to the fused
+        # class-side launches (device-wide barrier): use their unfused form
+        for knob in ("PFSGNN_FUSED_TAIL", "PFSGNN_CLASS_TAIL", "PFSGNN_CLASS_BWD"):
+            os.environ.setdefault(knob, "0")
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
+    # the data-parallel code path (collectives in the step): N > 1, or forced at
+    # N = 1 (PFSGNN_DIST_FORCE=1 under torchrun --nproc-per-node 1) to rehearse
+    # the RCCL capture on one GPU
+    dist_path = world > 1 or os.environ.get("PFSGNN_DIST_FORCE") == "1"
+    if dist_path:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = os.environ.get("PFSGNN_BENCH_BACKEND", "nccl")
         if backend == "nccl":
@@ -351,37 +359,58 @@ def main():
             step()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        # N > 1: the whole step -- buffer broadcast, forward, loss, backward,
+        # the gradient all-reduce and Adam -- is ONE captured graph, as at N = 1
+        # (RCCL collectives capture into HIP graphs); if the capture fails the
+        # tail (broadcast, all-reduce, Adam) runs eagerly around the replay
+        # (PFSGNN_BENCH_EAGER_TAIL=1 forces that form)
+        tail_in_graph = not dist_path or (os.environ.get("PFSGNN_BENCH_EAGER_TAIL") != "1" and
+                                          dist.get_backend() == "nccl")
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            static_loss = fwd_bwd()
-            if world == 1:
-                opt.step()
+        if tail_in_graph:
+            try:
+                with torch.cuda.graph(graph):
+                    sync_buffers(gnn)
+                    static_loss = fwd_bwd()
+                    allreduce_gradients(gnn)
+                    opt.step()
+            except Exception as exc:  # noqa: BLE001
+                if not dist_path:
+                    raise
+                print(f"[bench] capturing the collectives failed ({exc!r}): eager tail",
+                      file=sys.stderr, flush=True)
+                tail_in_graph = False
+                torch.cuda.synchronize()
+                graph = torch.cuda.CUDAGraph()
+        if not tail_in_graph:
+            with torch.cuda.graph(graph):
+                static_loss = fwd_bwd()
         torch.cuda.synchronize()
 
         def step():  # noqa: F811
-            if world > 1:
+            if not tail_in_graph:
                 sync_buffers(gnn)
             graph.replay()
-            if world > 1:
+            if not tail_in_graph:
                 allreduce_gradients(gnn)
                 opt.step()
             return static_loss
 
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_path:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_path:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if rank == 0:
         print(f"[bench] {args.steps} timed steps: {elapsed:.2f}s", file=sys.stderr, flush=True)
-    if world > 1:
+    if dist_path:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -391,11 +420,11 @@ def main():
     # no device-wide barrier of the fused class-side launches timed out
     sync_faults = native.sync_faults()
     assert sync_faults == 0, f"{sync_faults} device-wide barrier time-outs"
-    # ---- N > 1: the eager tail of a step (outside the captured graph): the
-    # buffer broadcast before the replay, the gradient all-reduce and Adam
-    # after it, each timed alone (synchronised) over a few extra steps
+    # ---- N > 1: the tail of a step -- the buffer broadcast before the
+    # forward, the gradient all-reduce and Adam after the backward -- each run
+    # eagerly and timed alone (synchronised) over a few extra steps
     tail = None
-    if world > 1 and use_graph:
+    if dist_path and use_graph:
         t_sync, t_red, t_adam = [], [], []
         for i in range(min(args.steps, 10)):
             torch.cuda.synchronize()
@@ -417,17 +446,18 @@ def main():
             t_adam.append(te - td)
         med = lambda v: sorted(v)[len(v) // 2] * 1e3  # noqa: E731
         tail = {"sync_buffers_ms": round(med(t_sync), 4), "allreduce_ms": round(med(t_red), 4),
-                "adam_ms": round(med(t_adam), 4),
-                "note": "per step, each part synchronised alone (median of %d steps after the "
-                        "timed region); in the timed steps they run unsynchronised around the "
-                        "graph replay" % len(t_sync)}
+                "adam_ms": round(med(t_adam), 4), "in_graph": tail_in_graph,
+                "note": "per step, each part run eagerly and synchronised alone (median of %d "
+                        "steps after the timed region); in the timed steps they are %s" %
+                        (len(t_sync), "part of the one captured step graph" if tail_in_graph
+                         else "launched eagerly around the graph replay")}
         t = torch.tensor([tail["sync_buffers_ms"], tail["allreduce_ms"], tail["adam_ms"]],
                          device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         tail.update(sync_buffers_ms=round(float(t[0]), 4), allreduce_ms=round(float(t[1]), 4),
                     adam_ms=round(float(t[2]), 4), over_ranks="max")
     consistency = None
-    if world > 1:
+    if dist_path:
         # every rank must end the K steps with bitwise the same parameters
         # (one all-reduce, the same Adam) and, after the buffer broadcast that
         # opens the next step, the same BatchNorm buffers
@@ -464,8 +494,11 @@ def main():
             try:
                 g_rep = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g_rep):
+                    if tail_in_graph:
+                        sync_buffers(gnn)
                     fwd_bwd()
-                    if world == 1:
+                    if tail_in_graph:
+                        allreduce_gradients(gnn)
                         opt.step()
             finally:
                 native.timing_repeat(kname, 0)
@@ -594,6 +627,17 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(B, args.cpu_seconds)
         value = world * E * args.steps / elapsed
+        if NC == 16 and G * world == 2048:
+            bcfg = (f"BASELINE configs[3]: 2048 synthetic {NF}x{NC} graphs sharded over "
+                    f"{world} GPU(s), {G} per GPU, RCCL gradient all-reduce")
+        elif NC == 16 and G == 256 and world == 1:
+            bcfg = f"BASELINE configs[2]: 256 synthetic {NF}x{NC} graphs on one GPU"
+        elif (NF, NC, B) == (2394, 128, 8):
+            bcfg = ("BASELINE metric / configs[4] shape (2394x128, 8 message-passing rounds)" +
+                    (f", weak-scaled over {world} GPUs (configs[3]'s data-parallel sharding)"
+                     if world > 1 else ""))
+        else:
+            bcfg = None
         metric = "training-step edges/sec on 2394\u00d7128 bipartite batches; % HBM roofline"
         if (NF, NC) != (2394, 128):
             metric = f"training-step edges/sec on {NF}\u00d7{NC} bipartite batches; % HBM roofline"
@@ -610,7 +654,7 @@ def main():
                                    f"(GNN fwd + train.py loss + bwd + Adam)",
                        "fibers": NF, "classes": NC, "graphs_per_gpu": G, "global_graphs": G * world,
                        "blocks": B, "fdim": FDIM, "edges_per_gpu_step": E,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}", "baseline_config": bcfg},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
@@ -622,7 +666,7 @@ def main():
         if alt:
             line["alt_paths"] = alt
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_path:
         dist.destroy_process_group()
 
 

@@ -48,15 +48,12 @@ __device__ __forceinline__ void pf_split4(float a, float b, float c, float d, pf
 __device__ __forceinline__ pf_s16x8 pf_cat8(pf_s16x4 a, pf_s16x4 b) {
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
-// v_mfma_f32_16x16x32_bf16 whose result never lands in its A / B registers: a
-// result register overlapping an A or B operand gives timing-dependent sums on
-// gfx950 (ROCm 7.2 hipcc allocates that overlap; DESIGN.md §MFMA operand
-// overlap), so A and B are kept live past the MFMA by an empty asm tied to it.
+// (No MF_SRC_KEEP here, pfsgnn_mfma_core.h mf8: the node kernels are
+// reproducible without it, tests/test_gpu_determinism.py, and the asm forced
+// their results out of AGPRs: k_mlp_bwd<7> 43 -> 53 us.)
 __device__ __forceinline__ floatx4 pf_mf8(pf_s16x8 a, pf_s16x8 b, floatx4 c) {
-  floatx4 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(pf_b16x8, a),
-                                                      __builtin_bit_cast(pf_b16x8, b), c, 0, 0, 0);
-  asm volatile("" : "+v"(d) : "v"(a), "v"(b));
-  return d;
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(pf_b16x8, a),
+                                                 __builtin_bit_cast(pf_b16x8, b), c, 0, 0, 0);
 }
 
 // ------------------------------------------------------------------ errors

@@ -456,7 +456,7 @@ __global__ __launch_bounds__(256) void km_target_fwd(EdgeGeo geo, const float* _
                                                      uint8_t* __restrict__ tmask) {
   constexpr int C = 2 * F, NT = GM<C>::NT;
   MF_GEO
-  __shared__ float colbuf[COL_CH * 4 * C];
+  __shared__ __attribute__((aligned(16))) float colbuf[COL_CH * 4 * C];
   FwdLayer<PREC, C, F> L1;
   L1.load([&](int h, int k) { return Wt1[h * 2 * F + F + k]; }, lane);
   floatx4 rs[NT];
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   using WI = WgImg<PREC>;
   MF_GEO
   __shared__ __attribute__((aligned(16))) short imgs[4 * NIMG * WI::U];
-  __shared__ float colbuf[COL_CH * 4 * C];
+  __shared__ __attribute__((aligned(16))) float colbuf[COL_CH * 4 * C];
   __shared__ float scratch[4 * SCR];
   __shared__ __attribute__((aligned(16))) float qtl[MF_MAX_CPS * ClassRows<C>::CP];
   __shared__ __attribute__((aligned(16))) float ghl[MF_MAX_CPS * ClassRows<C>::CP];
@@ -862,7 +862,7 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
   using WI = WgImg<PREC>;
   MF_GEO
   __shared__ __attribute__((aligned(16))) short imgs[4 * NIMG * WI::U];
-  __shared__ float colbuf[COL_CH * 4 * H];
+  __shared__ __attribute__((aligned(16))) float colbuf[COL_CH * 4 * H];
   __shared__ float scratch[4 * SCR];
   __shared__ __attribute__((aligned(16))) float ptl[MF_MAX_CPS * ClassRows<H>::CP];
   ClassRows<H>::stage(ptl, PtS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
@@ -872,7 +872,11 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
   short* im_gz = im_a + NT * WI::U;
   short* im_x = im_gz + NT * WI::U;
 
+#ifdef MF_EMB_REC_B6   // (A/B: the default path's recompute on bf16x6 instead of fp32 MFMA)
+  std::conditional_t<PREC == 1, LayerB6<H, F>, FwdLayer<FP(PREC), H, F>> L1;
+#else
   FwdLayer<FP(PREC), H, F> L1;
+#endif
   L1.load([&](int h, int k) { return W1[h * 4 * F + 2 * F + k]; }, lane);
   // gradient chains: exact fp32, bf16x3 or bf16 by PREC
   GradLayer<PREC, H, F> L2T;

@@ -120,12 +120,32 @@ __device__ __forceinline__ s16x8 cat8(s16x4 a, s16x4 b) {
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 __device__ __forceinline__ Fr8 cat(const Fr& a, const Fr& b) { return {cat8(a.h, b.h), cat8(a.l, b.l)}; }
-// (A and B are kept live past the MFMA so that its result never lands in their
-// registers: that overlap gives timing-dependent sums on gfx950, pf_mf8.)
+// MF_SRC_KEEP: an empty asm after every split-bf16 MFMA reads its result and its
+// A / B operands.  Without it the bf16x3 / bf16x6 SModel forward
+// (km_source_fwd_ft) gave run-to-run different moments on identical inputs
+// (~2.5k of 6.1M elements, tools/op_det_probe.py; every other kernel and path
+// reproducible); with it every probe is bitwise reproducible
+// (profiles/r05a_op_determinism.txt, tests/test_gpu_determinism.py).  What in
+// the compiler's output for that kernel raced is not isolated: the hand-written
+// probes of the suspect patterns -- an MFMA result written over its own A or B,
+// an LDS load into a chained MFMA's SrcC right behind it -- are exact on
+// gfx950 (tools/probes/mfma_overlap.hip, profiles/r05a_mfma_overlap.txt).
+// MF_SRC_PIN (A/B): also pass B (1) / A (2) through an opaque asm before the
+// MFMA so that no result is allocated over an operand at all: 1.7 % slower
+// step, not needed for reproducibility (profiles/r05d_pin_ab.txt).
 #ifndef MF_SRC_KEEP
 #define MF_SRC_KEEP 1
 #endif
+#ifndef MF_SRC_PIN
+#define MF_SRC_PIN 0
+#endif
 __device__ __forceinline__ floatx4 mf8(s16x8 a, s16x8 b, floatx4 c) {
+#if MF_SRC_KEEP && (MF_SRC_PIN & 1)
+  asm volatile("" : "+v"(b));   // B as an opaque value: not rebuilt from its halves for the keep
+#endif
+#if MF_SRC_KEEP && (MF_SRC_PIN & 2)
+  asm volatile("" : "+v"(a));
+#endif
   floatx4 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b16x8, a),
                                                       __builtin_bit_cast(b16x8, b), c, 0, 0, 0);
 #if MF_SRC_KEEP
@@ -718,17 +738,21 @@ __device__ __forceinline__ floatx4 WgImg<0>::colsum(const TA&, const floatx4& v)
 
 // Per-class column partials of the block, chunked: each wave parks its 16-fiber
 // sums of COL_CH classes in buf[COL_CH][4][CW]; the block then writes the 4-wave
-// sums (fixed order) to part[(rowbase + c) * CW + h] ([G][NFG][NC][CW] layout).
+// sums (fixed order) to part[(rowbase + c) * CW + h] ([G][NFG][NC][CW] layout),
+// four channels per thread (CW % 4 == 0: 16-byte LDS reads and global stores).
 #ifndef COL_CH
-#define COL_CH 8
+#define COL_CH 16
 #endif
 template <int CW>
 __device__ __forceinline__ void col_flush(const float* buf, int nch, int cbase, float* part,
                                           long long rowbase) {
-  for (int idx = threadIdx.x; idx < nch * CW; idx += PF_BLOCK) {
-    const int cc = idx / CW, h = idx - cc * CW;
-    const float* b = buf + cc * 4 * CW + h;
-    part[(rowbase + cbase + cc) * CW + h] = ((b[0] + b[CW]) + b[2 * CW]) + b[3 * CW];
+  static_assert(CW % 4 == 0, "column width");
+  constexpr int Q = CW / 4;
+  for (int i = threadIdx.x; i < nch * Q; i += PF_BLOCK) {
+    const int cc = i / Q, q = i - cc * Q;
+    const floatx4* b = reinterpret_cast<const floatx4*>(buf + cc * 4 * CW) + q;
+    const floatx4 v = ((b[0] + b[Q]) + b[2 * Q]) + b[3 * Q];
+    *reinterpret_cast<floatx4*>(part + (rowbase + cbase + cc) * CW + 4 * q) = v;
   }
 }
 

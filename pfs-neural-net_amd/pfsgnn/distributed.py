@@ -20,6 +20,15 @@ import os
 import torch
 import torch.distributed as dist
 
+# PFSGNN_DIST_FORCE=1: run the collectives even in a world of one rank (a
+# process group of one member: RCCL still launches its kernels, which is how
+# bench.py rehearses capturing them into the step's HIP graph on one GPU)
+_FORCE = os.environ.get("PFSGNN_DIST_FORCE") == "1"
+
+
+def _active():
+    return dist.is_initialized() and (dist.get_world_size() > 1 or _FORCE)
+
 
 def init_from_env(backend=None):
     """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* (torchrun)."""
@@ -37,7 +46,7 @@ def init_from_env(backend=None):
 
 def broadcast_parameters(model, src=0):
     """Rank `src`'s parameters and BatchNorm buffers to every rank (start of training)."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    if not _active():
         return
     flat = model.flat_parameters()[0] if hasattr(model, "flat_parameters") else None
     if flat is not None:
@@ -85,7 +94,7 @@ def sync_buffers(model, src=0):
     running statistics and batch counters.  Call it at the start of a step,
     before the forward, as DDP does (the forward then reads and updates the
     same buffers on every rank)."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    if not _active():
         return
     groups = {}
     for n, b in model.named_buffers():
@@ -96,7 +105,7 @@ def sync_buffers(model, src=0):
 
 def allreduce_gradients(model):
     """Mean of the gradients over ranks: one collective on the flat grad buffer."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    if not _active():
         return
     world = dist.get_world_size()
     if hasattr(model, "flat_parameters"):

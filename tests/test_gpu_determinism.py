@@ -1,0 +1,94 @@
+"""Bitwise reproducibility at the bench geometry (16 complete 2394x128 graphs).
+
+Round 5 found the bf16x3 / bf16x6 SModel forward (km_source_fwd_ft) giving
+run-to-run different moments on identical inputs -- a few thousand of 6.1 M
+elements, enough to move a parity check past its bar now and then -- while
+the smaller parity graphs and the default path were reproducible.  The fix
+lives in the MFMA helper (pfsgnn_mfma_core.h, MF_SRC_KEEP); these tests hold
+it: each forward edge op three times on the same inputs, on every path that is
+held to the parity bar plus bf16x3, and one forward + backward of the whole
+model twice, must agree bit for bit."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+PATHS = ["mfma", "bf16x6", "bf16x3", "mfma32"]
+
+
+@pytest.fixture(scope="module")
+def bench_inputs():
+    from pfsgnn.engine import Dims
+    G, NF, NC, F = 16, 2394, 128, 10
+    d = Dims(G, NF, NC, F)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    c = lambda *s, sc=1.0, off=0.0: (torch.randn(*s, device="cuda", generator=g) * sc + off)  # noqa: E731
+    t = dict(xe=c(F, d.E, sc=2, off=3), xsc=c(F, sc=0.5, off=1), xsh=c(F), Ps=c(4 * F, d.NS),
+             Pt=c(4 * F, d.NT), W1=c(4 * F, 4 * F, sc=0.3), W2=c(F, 4 * F, sc=0.3), b2=c(F),
+             y=c(F, d.E), sc=c(F, sc=0.3, off=1), sh=c(F), Qt=c(2 * F, d.NT),
+             Ws1=c(2 * F, 2 * F, sc=0.3), Ws2=c(2 * F, 2 * F, sc=0.3), bs2=c(2 * F),
+             Rs=c(2 * F, d.NS), Wt1=c(2 * F, 2 * F, sc=0.3))
+    return d, t
+
+
+@pytest.mark.parametrize("path", PATHS)
+def test_forward_edge_ops_bitwise_reproducible(bench_inputs, path):
+    import pfsgnn
+    from pfsgnn.native import HipBackend
+    d, t = bench_inputs
+    hb = HipBackend()
+    prev = pfsgnn.get_edge_path()
+    pfsgnn.set_edge_path(path)
+    try:
+        runs = []
+        for _ in range(3):
+            y, mu, var = hb.edge_mlp_fwd(d, t["xe"], t["xsc"], t["xsh"], t["Ps"], t["Pt"], t["W1"],
+                                         t["W2"], t["b2"])
+            hs = torch.zeros(8 * d.F, d.NS, device="cuda")
+            mom = hb.source_fwd(d, t["y"], t["sc"], t["sh"], t["Qt"], t["Ws1"], t["Ws2"], t["bs2"], hs)
+            hsum = hb.target_fwd(d, t["y"], t["sc"], t["sh"], t["Rs"], t["Wt1"])
+            runs.append([y.clone(), mu.clone(), var.clone(), mom.clone(), hs, hsum.clone()])
+        torch.cuda.synchronize()
+        for r in runs[1:]:
+            for a, b, nm in zip(runs[0], r, ("y", "mu", "var", "mom", "hs", "hsum")):
+                assert torch.equal(a, b), f"{path}: {nm} differs between identical launches " \
+                    f"({int((a != b).sum())} of {a.numel()} elements)"
+    finally:
+        pfsgnn.set_edge_path(prev)
+
+
+@pytest.mark.parametrize("path", ["mfma", "bf16x6"])
+def test_training_step_bitwise_reproducible(path):
+    import pfsgnn
+    from pfsgnn.train import loss_function
+    G, NF, NC, F = 16, 2394, 128, 10
+    prev = pfsgnn.get_edge_path()
+    pfsgnn.set_edge_path(path)
+    try:
+        gen = torch.Generator().manual_seed(5)
+        ci = torch.cat([torch.randint(2, 13, (G * NC, 1), generator=gen).float(),
+                        torch.randint(1000, 100000, (G * NC, 1), generator=gen).float()], 1)
+        e = torch.arange(G * NF * NC)
+        data = pfsgnn.BipartiteData(torch.stack([e // NC, (e // (NF * NC)) * NC + e % NC]),
+                                    torch.arange(NF, dtype=torch.float).repeat(G).reshape(-1, 1),
+                                    ci, 2.0 + 8.0 * torch.rand(G * NF * NC, F, generator=gen),
+                                    torch.zeros(G, F))
+        ci = ci.cuda()
+        torch.manual_seed(0)
+        gnn = pfsgnn.GNN(B=8, Fdim=F, T=NC, F_s=1, F_t=2).cuda()
+        gnn.train()
+        state = {k: v.clone() for k, v in gnn.state_dict().items()}
+        res = []
+        for _ in range(2):
+            gnn.load_state_dict(state)
+            gnn.zero_grad()
+            out = gnn(data)
+            loss, _ = loss_function(out, ci, pclass=0.1, pfiber=0.1, sharpness=10.0, seed=7)
+            loss.backward()
+            res.append((loss.detach().clone(), out.x_e.detach().clone(),
+                        torch.cat([p.grad.reshape(-1) for p in gnn.parameters() if p.grad is not None])))
+        torch.cuda.synchronize()
+        for a, b, nm in zip(res[0], res[1], ("loss", "x_e", "grads")):
+            assert torch.equal(a, b), f"{path}: {nm} differs between identical steps"
+    finally:
+        pfsgnn.set_edge_path(prev)
