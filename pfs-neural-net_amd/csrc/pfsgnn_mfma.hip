@@ -45,6 +45,13 @@
 // stays bitwise reproducible.
 #include "pfsgnn_mfma_core.h"
 
+// MF_WG_EARLY_READS (default 1): the backward kernels issue their transposed
+// weight-gradient image reads right after writing the images, ahead of the
+// input-gradient chains (0: at their first use, round 4's order)
+#ifndef MF_WG_EARLY_READS
+#define MF_WG_EARLY_READS 1
+#endif
+
 namespace {
 
 // ============================================================ EdgeModel fwd
@@ -735,6 +742,19 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     }
     WI::put(im_x, lane, x[0], split(x[0]));
     lds_order();
+#if MF_WG_EARLY_READS
+    // the transposed image reads go out now, ahead of the input-gradient
+    // chains (as in km_edge_mlp_bwd)
+    const typename WI::R rx = WI::rd(im_x, lane);
+    typename WI::R ra[NT], rgm[NT], rgz[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+      ra[tt] = WI::rd(im_a + tt * WI::U, lane);
+      rgm[tt] = WI::rd(im_gm + tt * WI::U, lane);
+      rgz[tt] = WI::rd(im_gz + tt * WI::U, lane);
+    }
+    lds_order();
+#endif
     floatx4 g[1] = {zero4()};
     if constexpr (PREC >= 1) L1sT.apply(sgz, g); else L1sT.apply(gz, g);
     if (tpart) {  // TModel's per-edge input gradient (gnn.py:188-190)
@@ -774,17 +794,31 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     }
     // ---- weight gradients (edge = K) through the transposed images
     lds_order();
+#if MF_WG_EARLY_READS
+    const typename WI::TB tx = WI::B(rx);
+    typename WI::TB ta[NT];
+#pragma unroll
+    for (int nb = 0; nb < NT; ++nb) ta[nb] = WI::B(ra[nb]);
+#else
     const typename WI::TB tx = WI::B(im_x, lane);
     typename WI::TB ta[NT];
 #pragma unroll
     for (int nb = 0; nb < NT; ++nb) ta[nb] = WI::B(im_a + nb * WI::U, lane);
+#endif
     const int cl = c - cbase;
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
+#if MF_WG_EARLY_READS
+      const typename WI::TA tgm = WI::A(rgm[tt]);
+#pragma unroll
+      for (int nb = 0; nb < NT; ++nb) accW2[tt * NT + nb] = WI::mma(tgm, ta[nb], accW2[tt * NT + nb]);
+      const typename WI::TA tgz = WI::A(rgz[tt]);
+#else
       const typename WI::TA tgm = WI::A(im_gm + tt * WI::U, lane);
 #pragma unroll
       for (int nb = 0; nb < NT; ++nb) accW2[tt * NT + nb] = WI::mma(tgm, ta[nb], accW2[tt * NT + nb]);
       const typename WI::TA tgz = WI::A(im_gz + tt * WI::U, lane);
+#endif
       accW1[tt] = WI::mma(tgz, tx, accW1[tt]);
       const floatx4 cs = WI::colsum(tgz, gz[tt]);
       if (j16 == WI::CS_LANE) {
@@ -944,20 +978,45 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
     }
     WI::put(im_x, lane, x[0], split(x[0]));
     lds_order();
+#if MF_WG_EARLY_READS
+    // every transposed image read is issued before the edge-input gradient
+    // chain (a wave's LDS operations run in order, so they see the writes
+    // above): their latency hides behind that chain instead of stalling the
+    // weight-gradient MFMAs one read group at a time
+    const typename WI::R rgy = WI::rd(im_gy, lane), rx = WI::rd(im_x, lane);
+    typename WI::R ra[NT], rgz[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+      ra[tt] = WI::rd(im_a + tt * WI::U, lane);
+      rgz[tt] = WI::rd(im_gz + tt * WI::U, lane);
+    }
+    lds_order();
+#endif
     if (gxe) {
       floatx4 gx[1] = {zero4()};
       if constexpr (PREC >= 1) L1T.apply(sgz, gx); else L1T.apply(gz, gx);
       st_frows<F>(gxe, EB * F, (uint32_t)c * eoc, ro, g4, fvalid, gx[0]);
     }
+#if MF_WG_EARLY_READS
+    const typename WI::TA tgy = WI::A(rgy);
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) accW2[tt] = WI::mma(tgy, WI::B(ra[tt]), accW2[tt]);
+    const typename WI::TB tx = WI::B(rx);
+#else
     const typename WI::TA tgy = WI::A(im_gy, lane);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt)
       accW2[tt] = WI::mma(tgy, WI::B(im_a + tt * WI::U, lane), accW2[tt]);
     const typename WI::TB tx = WI::B(im_x, lane);
+#endif
     const int cl = c - cbase;
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
+#if MF_WG_EARLY_READS
+      const typename WI::TA tgz = WI::A(rgz[tt]);
+#else
       const typename WI::TA tgz = WI::A(im_gz + tt * WI::U, lane);
+#endif
       accW1[tt] = WI::mma(tgz, tx, accW1[tt]);
       const floatx4 cs = WI::colsum(tgz, gz[tt]);
       if (j16 == WI::CS_LANE) {

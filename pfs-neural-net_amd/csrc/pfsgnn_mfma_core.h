@@ -517,6 +517,12 @@ struct WgImg {
   static constexpr int CS_LANE = 0;
   using TA = s16x8;
   using TB = WgB;
+  // rd(): the raw transposed read of an image (issued early, its LDS latency
+  // hidden behind other work); A() / B() assemble the MFMA operands from it
+  using R = Fr;
+  static __device__ __forceinline__ R rd(const short* im, int lane) { return img_tr2(im, lane); }
+  static __device__ __forceinline__ TA A(const R& r) { return cat8(r.h, r.l); }
+  static __device__ __forceinline__ TB B(const R& r) { return {cat8(r.l, r.h), cat8(r.h, s16x4{})}; }
   static __device__ __forceinline__ void put(short* im, int lane, const floatx4&, const Fr& s) {
     img_put2(im, lane, s);
   }
@@ -535,6 +541,12 @@ struct WgImg<0> {
   static constexpr int CS_LANE = 15;
   using TA = floatx4;
   using TB = floatx4;
+  using R = floatx4;
+  static __device__ __forceinline__ R rd(const short* im, int lane) {
+    return imgf_tr(reinterpret_cast<const float*>(im), lane);
+  }
+  static __device__ __forceinline__ TA A(const R& r) { return r; }
+  static __device__ __forceinline__ TB B(const R& r) { return r; }
   static __device__ __forceinline__ void put(short* im, int lane, const floatx4& v, const Fr&) {
     imgf_put(reinterpret_cast<float*>(im), lane, v);
   }

@@ -72,12 +72,16 @@ def check(name, ours, r64, r32):
     assert err <= bound, f"{name} [{mode}]: err {err:.3e} > bound {bound:.3e} (oracle32 err {ref_err:.3e}, scale {scale:.3e})"
 
 
-def oracle_step(model, graph, G, NF, NC, seed, sharp, dtype, reverse=False):
+def oracle_step(model, graph, G, NF, NC, seed, sharp, dtype, reverse=False, hook=None):
     """The reference training step on the oracle.  reverse=True feeds the edges
     in reversed order (the scatters then sum in another order: a second fp32
-    rounding of the same step) and restores train.py's order for the loss."""
+    rounding of the same step) and restores train.py's order for the loss.
+    hook(m), if given, is called on the oracle's model copy before the forward
+    (module hooks that capture intermediates)."""
     m = copy.deepcopy(model).to(dtype)
     m.train()
+    if hook is not None:
+        hook(m)
     ei, xe = graph.edge_index, graph.x_e
     if reverse:
         ei, xe = ei.flip(1), xe.flip(0)

@@ -9,7 +9,9 @@
 #   bench16    configs[2]: 256 graphs of 2394x16
 #   trace      rocprofv3 --kernel-trace --stats of a short bench run
 #   pmc        SQ / FETCH_SIZE / WRITE_SIZE passes (tools/prof_pmc.sh)
+#   pmcbwd     SQ passes over the two backward edge kernels (tools/pmc_edge_bwd.sh)
 #   precision  the edge paths' precision table at configs[4]'s shape
+#   bias       the BatchNorm-cancelled bias gradients vs random fp32 orders
 #   sparse     general-graph throughput (tools/sparse_bench.py)
 #   dist1      the data-parallel step with RCCL captured, one rank (torchrun)
 #   rank2      two ranks on the box's one GPU over gloo (rehearsal)
@@ -24,7 +26,9 @@ for r in "$@"; do
     bench16) specs+=("${tag}_bench16:300:python bench.py --classes 16 --graphs 256 --steps 50 --alt-paths , --no-cpu-baseline > gpurun_out/${tag}_bench16.json") ;;
     trace) specs+=("${tag}_trace:360:bash tools/trace_only.sh gpurun_out ${tag}") ;;
     pmc) specs+=("${tag}_pmc:600:bash tools/prof_pmc.sh gpurun_out/${tag}_pmc") ;;
+    pmcbwd) specs+=("${tag}_pmcbwd:400:bash tools/pmc_edge_bwd.sh gpurun_out/${tag}_pmcbwd") ;;
     precision) specs+=("${tag}_precision:700:PFSGNN_TOL_OUT=gpurun_out/${tag}_precision.json python -u -m pytest -x -v -s --timeout 600 --timeout-method thread tests/test_gpu_precision_table.py -m gpu") ;;
+    bias) specs+=("${tag}_bias:400:PFSGNN_BIAS_OUT=gpurun_out/${tag}_bias.json python -u -m pytest -x -v -s --timeout 300 --timeout-method thread tests/test_gpu_bias_noise.py -m gpu") ;;
     sparse) specs+=("${tag}_sparse:400:SPARSE_DENSITIES=1.0,0.3 python tools/sparse_bench.py > gpurun_out/${tag}_sparse.txt") ;;
     dist1) specs+=("${tag}_dist1:240:PFSGNN_DIST_FORCE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --steps 30 --warmup 3 --alt-paths , --no-cpu-baseline > gpurun_out/${tag}_dist1.json") ;;
     rank2) specs+=("${tag}_rank2:300:PFSGNN_BENCH_SAME_DEVICE=1 PFSGNN_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29518 bench.py --steps 10 --warmup 2 --alt-paths , --no-cpu-baseline > gpurun_out/${tag}_rank2.json") ;;
