@@ -216,6 +216,11 @@ int pfsgnn_defer_end(void* stream);
 size_t pfsgnn_defer_need(void);
 int pfsgnn_wgrad_multi(const pfsgnn_wgrad_job* jobs, int n, void* part, size_t part_bytes,
                        void* stream);
+/* pfsgnn_defer_end + pfsgnn_wgrad_multi(jobs) as one flush: the jobs' kernels,
+ * then the pass's queued edge reductions and the jobs' own in one batch (no
+ * job reads a weight gradient, so the order does not change a result). */
+int pfsgnn_defer_end_multi(const pfsgnn_wgrad_job* jobs, int n, void* part, size_t part_bytes,
+                           void* stream);
 
 /* BatchNorm1d training forward over N rows (biased var for the output,
  * unbiased for the running update; rm/rv may be NULL). */
@@ -375,6 +380,25 @@ int pfsgnn_mlp_bwd(const float* dY, int N, const float* Yp, const float* mu, con
                    const float* W1, int ldw1, int H, int K, const float* W2, int O, float* dYp,
                    float* dZ, const pfsgnn_oseg* outs, int nout, void* ws, size_t ws_bytes,
                    void* stream);
+/* the same with SModel's node_mlp_2 backward (gnn.py:140-154) folded in:
+ *   bn_part != NULL: the BatchNorm sums already made by the producer of dY
+ *     (pfsgnn_target_bwd_bn's bn_part, bn_nparts = ceil(N / 64) per-block
+ *     partials [n][32]: sum dY in 0..16, sum dY*xhat in 16..32) instead of a
+ *     sums launch of its own (gamma required);
+ *   coef != NULL: dX rows [mom_k0, mom_k0 + 4 mom_c) -- d loss / d [mean; std;
+ *     skew; kurt] of mom_c (16..20) message channels -- are not written; they
+ *     become pfsgnn_moment_coef(mom, ., mom_c, N, mom_n)'s coefficients coef
+ *     [4][mom_c][N] in the same launch (mom: pfsgnn_source_fwd's [4][mom_c][N];
+ *     mom_n: messages per fiber).  The outs entry covering those rows may be
+ *     NULL.  Needs the wide form (K or H > 64).
+ * Replaces k_bn_sums_part + pfsgnn_mlp_bwd + pfsgnn_moment_coef. */
+int pfsgnn_mlp_bwd_pre(const float* dY, int N, const float* Yp, const float* mu,
+                       const float* var, const float* gamma, float eps, float* dgamma,
+                       float* dbeta, const float* Z, const float* W1, int ldw1, int H, int K,
+                       const float* W2, int O, float* dYp, float* dZ, const pfsgnn_oseg* outs,
+                       int nout, const float* bn_part, int bn_nparts, const float* mom,
+                       float* coef, int mom_k0, int mom_c, int mom_n, void* ws,
+                       size_t ws_bytes, void* stream);
 /* Several independent small products in one launch: each job is a
  * pfsgnn_lin_cat (trans 0: Y[M][N] (+)= W . act(x_segs) + bscale*b) or a
  * pfsgnn_lin_t (trans 1: Y[M][N] (+)= W^T[M][K] . segs[0] (* lrelu'(Z)), W
@@ -651,6 +675,18 @@ int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, const float*
                       const float* sh, const float* Rs, const float* Wt1, const float* g_hsum,
                       float* GzT, float* dWt1, float* gxe, float* g_xs,
                       const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream);
+/* the same (complete graphs) where g_xs is final after this call and feeds
+ * SModel's node_mlp_2 + BatchNorm backward (gnn.py:153-154): the epilogue
+ * that finishes g_xs also writes that BatchNorm's backward sums over its
+ * fibers, bn_part [ceil(G*NF / 64)][32] (sum g_xs, sum g_xs*(Yp - mu) /
+ * sqrt(var + eps) per channel; bn_Yp [F][G*NF] the pre-norm output, bn_mu /
+ * bn_var its batch statistics) for pfsgnn_mlp_bwd_pre. */
+int pfsgnn_target_bwd_bn(int G, int NF, int NC, int F, const float* y, const float* sc,
+                         const float* sh, const float* Rs, const float* Wt1, const float* g_hsum,
+                         float* GzT, float* dWt1, float* gxe, float* g_xs,
+                         const unsigned char* tmask, const float* bn_Yp, const float* bn_mu,
+                         const float* bn_var, float bn_eps, float* bn_part, void* ws,
+                         size_t ws_bytes, void* stream);
 /* SModel edge backward fused with TModel's per-edge input gradient, the
  * downstream edge gradient and the edge BatchNorm's two gradient sums:
  * g_tot = Ws1e^T g_zs + [Wt1e^T g_zt] + [g_next]; GzS per class;

@@ -400,7 +400,7 @@ struct RedDesc {
   int ldo, add;
   float scale;
 };
-#define PF_MAX_RED 48   // (48 x 64 B: the descriptor pack stays under the 4 KB kernel-argument limit)
+#define PF_MAX_RED 96   // (packed 40-byte descriptors, pfsgnn_node.hip RedDev: 3840 B of kernel arguments)
 void launch_reduce_multi(const RedDesc* d, int n, hipStream_t st);
 // Deferred weight-gradient reductions (pfsgnn_defer_begin / _end): while a
 // pass is open, the edge backward kernels put their weight partials in the
@@ -435,6 +435,10 @@ static inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // (pfsgnn_set_sync_buffer); without one the callers keep their reduce launch.
 namespace pf {
 unsigned* sync_counters(size_t n);   // n counters, or nullptr
+// a launch's own run of n <= 128 counters (round robin over the buffer, so
+// launches in flight at the same time on different streams never share one),
+// or nullptr without a sync buffer
+unsigned* sync_slot(size_t n);
 }  // namespace pf
 // true in every thread of the block that arrives last of `expect` at *cnt
 // (the caller's stores of its partial must all be st_sc1); flag: an LDS word
@@ -449,4 +453,134 @@ __device__ __forceinline__ bool last_arrival(unsigned* cnt, unsigned expect, int
   }
   __syncthreads();
   return *flag != 0;
+}
+
+__device__ __forceinline__ void st_sc1d(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1d(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------ in-launch Welford finalize
+// With `bn` (EdgeModel training forward): also the double BatchNorm's affine
+// and running statistics of each channel, as pfsgnn_bn2_finalize computes them.
+struct Bn2Args {
+  const float* gamma;
+  const float* beta;
+  float* rm;
+  float* rv;
+  float momentum, eps;
+  float *sc, *sh, *inv1, *inv2;
+};
+
+// The BatchNorm statistics of an edge kernel's per-block Welford partials
+// ([nb][1 + 2F]: count, mean[F], M2[F], every value stored st_sc1) finished by
+// the kernel's own last blocks instead of a k_moments_finalize launch (the
+// hand-off protocol above): the last block of each group of MOM_GROUP partials
+// merges them in double into a group partial (count, sum count*mean, M2 about
+// the group mean), and the last group merges the groups and writes mu, the
+// biased var (+ the double BatchNorm's coefficients and running statistics).
+// Partials are assigned to threads in a fixed pattern and summed by fixed
+// trees: bitwise reproducible, and within double rounding of the one-launch
+// closed form.
+constexpr int MOM_GROUP = 64, MOM_MAXG = 64;   // nb <= 4096
+struct MomFin {
+  unsigned* cnt;   // 1 + MOM_MAXG hand-off counters (pf::sync_slot); nullptr: off
+  double* gp;      // [MOM_MAXG][3][16] group partials
+  float* mu;
+  float* var;
+  long long n;     // the statistics' element count (var = M2 / n)
+  Bn2Args bn;
+};
+
+template <int F>
+__device__ void mom_finalize(const float* part, int nb, int b, const MomFin& f) {
+  static_assert(F <= 16, "mom_finalize: 16 channels per thread slot");
+  __shared__ int flag;
+  __shared__ double red[4][3][16];
+  const int t = threadIdx.x, k = t & 15, j = t >> 4, wv = t >> 6;
+  // the 16 slots j of channel k summed in one order: lanes j, j^1.. of a wave
+  // (xor 16, 32), then the 4 waves
+  auto slot_sum = [&](double v, int w) -> double {
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if ((t & 63) < 16) red[wv][w][k] = v;
+    __syncthreads();
+    return (red[0][w][k] + red[1][w][k]) + (red[2][w][k] + red[3][w][k]);
+  };
+  const int grp = b / MOM_GROUP, ng = (nb + MOM_GROUP - 1) / MOM_GROUP;
+  const int b0 = grp * MOM_GROUP, nin = min(MOM_GROUP, nb - b0);
+  if (!last_arrival(f.cnt + 1 + grp, (unsigned)nin, &flag)) return;
+  // every load unconditional (clamped index) so that all 12 are in flight at
+  // once; the out-of-range ones are zeroed after
+  float lc[4], lm[4], lq[4];
+  const int kc = min(k, F - 1);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float* p = part + (size_t)(b0 + min(j + 16 * i, nin - 1)) * (1 + 2 * F);
+    lc[i] = ld_sc1(p);
+    lm[i] = ld_sc1(p + 1 + kc);
+    lq[i] = ld_sc1(p + 1 + F + kc);
+  }
+  double c[4], m[4], q[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bool ok = j + 16 * i < nin && k < F;
+    c[i] = ok ? (double)lc[i] : 0.0;
+    m[i] = ok ? (double)lm[i] : 0.0;
+    q[i] = ok ? (double)lq[i] : 0.0;
+  }
+  const double N = slot_sum((c[0] + c[1]) + (c[2] + c[3]), 0);
+  const double S = slot_sum((c[0] * m[0] + c[1] * m[1]) + (c[2] * m[2] + c[3] * m[3]), 1);
+  const double mg = N > 0.0 ? S / N : 0.0;
+  double Q = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const double d = m[i] - mg;
+    Q += q[i] + c[i] * d * d;
+  }
+  Q = slot_sum(Q, 2);
+  if (t < F) {
+    double* g = f.gp + (size_t)grp * 48;
+    st_sc1d(g + t, N);
+    st_sc1d(g + 16 + t, S);
+    st_sc1d(g + 32 + t, Q);
+  }
+  if (!last_arrival(f.cnt, (unsigned)ng, &flag)) return;
+  // the groups, the same way (red's rows are rewritten only after the
+  // barriers of last_arrival)
+  double gn[4], gs[4], gq[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const double* g = f.gp + (size_t)min(j + 16 * i, ng - 1) * 48;
+    gn[i] = ld_sc1d(g + kc);
+    gs[i] = ld_sc1d(g + 16 + kc);
+    gq[i] = ld_sc1d(g + 32 + kc);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bool ok = j + 16 * i < ng && k < F;
+    gn[i] = ok ? gn[i] : 0.0;
+    gs[i] = ok ? gs[i] : 0.0;
+    gq[i] = ok ? gq[i] : 0.0;
+  }
+  const double NT = slot_sum((gn[0] + gn[1]) + (gn[2] + gn[3]), 0);
+  const double ST = slot_sum((gs[0] + gs[1]) + (gs[2] + gs[3]), 1);
+  const double M0 = NT > 0.0 ? ST / NT : 0.0;
+  double QT = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const double d = gn[i] > 0.0 ? gs[i] / gn[i] - M0 : 0.0;
+    QT += gq[i] + gn[i] * d * d;
+  }
+  QT = slot_sum(QT, 2);
+  if (t < F) {
+    const float mu = (float)M0, v = (float)(QT / (double)f.n);
+    f.mu[t] = mu;
+    f.var[t] = v;
+    if (f.bn.gamma)
+      bn2_coef(f.bn.gamma, f.bn.beta, f.bn.rm, f.bn.rv, t, f.n, f.bn.momentum, f.bn.eps, mu, v,
+               f.bn.sc, f.bn.sh, f.bn.inv1, f.bn.inv2);
+  }
 }

@@ -314,16 +314,8 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
   return r;
 }
 
-// With `bn` (EdgeModel training forward): also the double BatchNorm's affine
-// and running statistics of channel k, as pfsgnn_bn2_finalize computes them.
-struct Bn2Args {
-  const float* gamma;
-  const float* beta;
-  float* rm;
-  float* rv;
-  float momentum, eps;
-  float *sc, *sh, *inv1, *inv2;
-};
+// With `bn` (EdgeModel training forward, Bn2Args: pfsgnn_common.h): also the
+// double BatchNorm's affine and running statistics of channel k.
 
 #define MF_PB 16  // partials per thread (nb <= 4096 in one round: the edge grids)
 static_assert(256 * MF_PB == 4096, "MF_PB: one round of the partial loop covers 4096 blocks");
@@ -1105,16 +1097,30 @@ __device__ __forceinline__ void stage_lin(const NodeLin& L0, const NodeLin& L1, 
 // to two epilogues.  A block owns 64 fibers (lane = fiber, coalesced rows);
 // wave w sums channels w, w+4, ...; the epilogues read the block's sums and
 // the staged weights from LDS.
+// FiberBnSums (part != nullptr): the BatchNorm-backward sums of the node
+// gradient L0 finishes, per block over its 64 fibers -- part[bx][0..16) =
+// sum g, part[bx][16..32) = sum g * (Yp - mu) / sqrt(var + eps) for the L0.nk
+// channels -- as k_bn_sums_part's per-block partials (pfsgnn_mlp.hip), so that
+// the MLP backward that reads g next needs no sums launch of its own.
+struct FiberBnSums {
+  const float* Yp;
+  const float* mu;
+  const float* var;
+  float eps;
+  float* part;   // [ceil(NS / 64)][32]
+};
 template <int C>
 struct FiberLinLds {
   float res[C][65];
   float ws[2 * NL_MAXK * C];
+  float fin[16][65];   // (FiberBnSums) L0's final rows
 };
 template <int C>
 __device__ __forceinline__ void reduce_fiber_lin_block(FiberLinLds<C>& S, int bx,
                                                        const float* __restrict__ part, int KS,
                                                        long long NS, float* __restrict__ out,
-                                                       const NodeLin& L0, const NodeLin& L1) {
+                                                       const NodeLin& L0, const NodeLin& L1,
+                                                       const FiberBnSums& bs = FiberBnSums{}) {
   static_assert(C % 4 == 0, "C must be a multiple of 4");
   constexpr int CPW = C / 4;
   auto& res = S.res;
@@ -1154,7 +1160,41 @@ __device__ __forceinline__ void reduce_fiber_lin_block(FiberLinLds<C>& S, int bx
 #pragma unroll
       for (int i = 0; i < C; ++i) acc = fmaf(wk[k * C + i], res[i][o], acc);
       float* op = L.out + (size_t)k * L.ldo + n0 + o;
-      *op = L.add ? *op + acc : acc;
+      const float r = L.add ? *op + acc : acc;
+      *op = r;
+      if (e == 0 && bs.part) S.fin[k][o] = r;
+    }
+  }
+  if (bs.part) {
+    // lane group (k, j): channel k, fibers 4j..4j+3; the 16 groups of a
+    // channel combined by a fixed xor tree
+    __syncthreads();
+    const int k = t >> 4, j = t & 15;
+    float sg = 0.f, sx = 0.f;
+    if (k < L0.nk) {
+      const float m = bs.mu[k], ic = 1.0f / sqrtf(bs.var[k] + bs.eps);
+      float yp[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long long f = n0 + 4 * j + i;
+        yp[i] = bs.Yp[(size_t)k * NS + (f < NS ? f : NS - 1)];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (n0 + 4 * j + i >= NS) continue;
+        const float g = S.fin[k][4 * j + i];
+        sg += g;
+        sx += g * ((yp[i] - m) * ic);
+      }
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {
+      sg += __shfl_xor(sg, off, 16);
+      sx += __shfl_xor(sx, off, 16);
+    }
+    if (j == 0) {
+      bs.part[(size_t)bx * 32 + k] = sg;
+      bs.part[(size_t)bx * 32 + 16 + k] = sx;
     }
   }
 }
@@ -1230,9 +1270,9 @@ __device__ __forceinline__ void reduce_columns_lin_block(ColLinLds<C>& S, int bx
 template <int C>
 __global__ __launch_bounds__(256) void k_reduce_fiber_lin(const float* __restrict__ part, int KS,
                                                           long long NS, float* __restrict__ out,
-                                                          NodeLin L0, NodeLin L1) {
+                                                          NodeLin L0, NodeLin L1, FiberBnSums bs) {
   __shared__ FiberLinLds<C> S;
-  reduce_fiber_lin_block<C>(S, blockIdx.x, part, KS, NS, out, L0, L1);
+  reduce_fiber_lin_block<C>(S, blockIdx.x, part, KS, NS, out, L0, L1, bs);
 }
 template <int C>
 __global__ __launch_bounds__(256) void k_reduce_columns_lin(const float* __restrict__ part, int G,
@@ -1358,15 +1398,17 @@ NodeLin lin_t_add(const float* W, int ldw, int col0, int nk, float* out, long lo
   return NodeLin{W ? W + col0 : nullptr, ldw, 1, nk, 1, nullptr, 0.f, out, ldo};
 }
 int fiber_finish_lin(const EdgeGeo& geo, int C, const float* dst, float* out, const NodeLin& L0,
-                     const NodeLin& L1, hipStream_t st) {
+                     const NodeLin& L1, hipStream_t st, const FiberBnSums& bs = FiberBnSums{}) {
   if (L0.nk > NL_MAXK || L1.nk > NL_MAXK) return pf::fail("fiber_finish_lin", "nk > 32");
+  if (bs.part && (!L0.W || L0.nk > 16))
+    return pf::fail("fiber_finish_lin", "BatchNorm sums need the first epilogue (<= 16 rows)");
   if (!L0.W && !L1.W) {
     fiber_finish(geo, C, dst, out, st);
     return 0;
   }
   const float* src = geo.KS == 1 ? out : dst;
   DISPATCH_C(C, hipLaunchKernelGGL(k_reduce_fiber_lin<CC>, dim3((unsigned)((geo.NS + 63) / 64)),
-                                   dim3(256), 0, st, src, geo.KS, geo.NS, out, L0, L1));
+                                   dim3(256), 0, st, src, geo.KS, geo.NS, out, L0, L1, bs));
   return 0;
 }
 int columns_lin(const float* part, int G, int BPG, int NC, int C, float* out, const NodeLin& L0,
@@ -1563,7 +1605,7 @@ size_t edge_ws_floats(const EdgeGeo& geo, int G, int NC, int F) {
   const size_t H = 4 * F, C = 2 * F;
   const size_t colp = (size_t)G * geo.NFG * NC;
   size_t edge = 0;
-  edge = std::max(edge, nb * (1 + 2 * F));                                          // mlp fwd
+  edge = std::max(edge, nb * (1 + 2 * F) + 2 * 48 * MOM_MAXG + 256);               // mlp fwd
   edge = std::max(edge, ks * 4 * C * NS + C * NS + 1024);                           // source fwd
   edge = std::max(edge, colp * C + 1024);                                           // target fwd
   edge = std::max(edge, nb * C * F + ks * C * NS + 1024);                           // target bwd
@@ -1620,12 +1662,26 @@ static int edge_mlp_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, i
   }
   if (use_mfma()) {
     PF_REQUIRE(part, "pfsgnn_edge_mlp_fwd", "workspace too small");
+    // the statistics finished by the kernel's last blocks (mom_finalize) when
+    // the library has hand-off counters, else by a k_moments_finalize launch
+    MomFin fin{};
+    if (geo.nblocks <= MOM_GROUP * MOM_MAXG && F <= 16) {
+      unsigned* cnt = pf::sync_slot(1 + MOM_MAXG);
+      double* gp = cnt ? reinterpret_cast<double*>(w.take(2 * 48 * MOM_MAXG)) : nullptr;
+      if (gp) fin = MomFin{cnt, gp, mu, var, geo.E, bn};
+    }
     { pf::Timer tm_("edge_mlp_fwd", st);
-    for (int rep = 0, nrep = 1 + pf::repeats("edge_mlp_fwd"); rep < nrep; ++rep)
-      if (int rc = pfm::edge_mlp_fwd(geo, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part, mf_prec(0, F), mf_bfy(), st)) return rc;
+    for (int rep = 0, nrep = 1 + pf::repeats("edge_mlp_fwd"); rep < nrep; ++rep) {
+      MomFin fr = fin;   // (a timing repeat leaves the running statistics alone)
+      if (rep + 1 < nrep) fr.bn.rm = fr.bn.rv = nullptr;
+      if (int rc = pfm::edge_mlp_fwd(geo, F, xe, xsc, xsh, Ps, Pt, W1, W2, b2, y, part, fr,
+                                     mf_prec(0, F), mf_bfy(), st))
+        return rc;
+    }
     tm_.end(); }
-    hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(256), 0, st, part, geo.nblocks, F, geo.E,
-                       mu, var, bn);
+    if (!fin.cnt)
+      hipLaunchKernelGGL(k_moments_finalize, dim3(F), dim3(256), 0, st, part, geo.nblocks, F, geo.E,
+                         mu, var, bn);
     return pf::check_launch("pfsgnn_edge_mlp_fwd");
   }
   const float* PtT = class_rows(Pt, 4 * F, geo, w, st);
@@ -1870,7 +1926,8 @@ static int target_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
                            const float* y, const float* sc, const float* sh, const float* Rs,
                            const float* Wt1, const float* g_hsum, float* GzT, float* dWt1,
                            float* gxe, float* g_xs, const unsigned char* tmask, void* ws,
-                           size_t ws_bytes, void* stream) {
+                           size_t ws_bytes, void* stream,
+                           const FiberBnSums& bs = FiberBnSums{}) {
   if (int rc = check_dims("pfsgnn_target_bwd", G, NF, NC, F)) return rc;
   if (int rc = check_sliced("pfsgnn_target_bwd", sl, NC, F)) return rc;
   PF_REQUIRE(y && Rs && Wt1 && g_hsum && GzT && dWt1, "pfsgnn_target_bwd", "null");
@@ -1905,7 +1962,7 @@ static int target_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
   // g_xs += Wt1[:, 0:F]^T GzT (gnn.py:188, the x_s[src] input gradient)
   if (int rc = fiber_finish_lin(geo, C, gz, GzT, lin_t_add(g_xs ? Wt1 : nullptr, 2 * F, 0, F, g_xs,
                                                            geo.NS),
-                                no_lin(), st))
+                                no_lin(), st, bs))
     return rc;
   const RedDesc rd{part, geo.nblocks, (size_t)C * F, F, C, F, dWt1 + F, C, 1, 1.f};
   if (defer) pf::defer_push(&rd, 1);
@@ -1920,6 +1977,19 @@ extern "C" int pfsgnn_target_bwd(int G, int NF, int NC, int F, const float* y, c
                                  size_t ws_bytes, void* stream) {
   return target_bwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Rs, Wt1, g_hsum, GzT, dWt1, gxe, g_xs,
                          tmask, ws, ws_bytes, stream);
+}
+
+extern "C" int pfsgnn_target_bwd_bn(int G, int NF, int NC, int F, const float* y,
+                                    const float* sc, const float* sh, const float* Rs,
+                                    const float* Wt1, const float* g_hsum, float* GzT, float* dWt1,
+                                    float* gxe, float* g_xs, const unsigned char* tmask,
+                                    const float* bn_Yp, const float* bn_mu, const float* bn_var,
+                                    float bn_eps, float* bn_part, void* ws, size_t ws_bytes,
+                                    void* stream) {
+  PF_REQUIRE(g_xs && bn_Yp && bn_mu && bn_var && bn_part, "pfsgnn_target_bwd_bn", "null");
+  return target_bwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Rs, Wt1, g_hsum, GzT, dWt1, gxe, g_xs,
+                         tmask, ws, ws_bytes, stream,
+                         FiberBnSums{bn_Yp, bn_mu, bn_var, bn_eps, bn_part});
 }
 
 extern "C" int pfsgnn_sl_target_bwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,

@@ -21,7 +21,8 @@ static constexpr int MAX_CPS = 64;
 
 int edge_mlp_fwd(const EdgeGeo& geo, int F, const float* xe, const float* xsc, const float* xsh,
                  const float* Ps, const float* PtS, const float* W1, const float* W2,
-                 const float* b2, float* y, float* part, int prec, int bfy, hipStream_t st);
+                 const float* b2, float* y, float* part, const MomFin& fin, int prec, int bfy,
+                 hipStream_t st);
 int source_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
                float* partS, int prec, hipStream_t st);

@@ -57,7 +57,8 @@ namespace {
 // ============================================================ EdgeModel fwd
 // y = W2 lrelu(Ps[f] + Pt[c] + W1[:, 2F:3F] x) + b2 per edge (gnn.py:86-101 with
 // the node parts of the first Linear precomputed per node); Welford partials of
-// y per block for the (double) BatchNorm.
+// y per block for the (double) BatchNorm, finished in the launch by its last
+// blocks when `fin` has counters (mom_finalize, pfsgnn_common.h).
 template <int F, int PREC>
 __global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float* __restrict__ xe,
                                                        const float* __restrict__ xsc,
@@ -68,7 +69,8 @@ __global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float*
                                                        const float* __restrict__ W2,
                                                        const float* __restrict__ b2,
                                                        float* __restrict__ y,
-                                                       float* __restrict__ part, int bfy) {
+                                                       float* __restrict__ part, int bfy,
+                                                       MomFin fin) {
   constexpr int H = 4 * F, NT = GM<H>::NT;
   MF_GEO
   __shared__ __attribute__((aligned(16))) float ptl[MF_MAX_CPS * ClassRows<H>::CP];
@@ -179,11 +181,12 @@ __global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float*
       }
       C0 = tot;
     }
-    float* p = part + (size_t)bx * (1 + 2 * F);
-    if (t == 0) p[0] = C0;
-    p[1 + t] = M0;
-    p[1 + F + t] = Q0;
+    float* p = part + (size_t)bx * (1 + 2 * F);   // (sc1: mom_finalize's hand-off)
+    if (t == 0) st_sc1(p, C0);
+    st_sc1(p + 1 + t, M0);
+    st_sc1(p + 1 + F + t, Q0);
   }
+  if (fin.cnt) mom_finalize<F>(part, geo.nblocks, bx, fin);
 }
 
 // ============================================================ SModel fwd
@@ -1111,8 +1114,12 @@ static inline int fwd_prec(int prec) { return FP(prec); }
 
 int edge_mlp_fwd(const EdgeGeo& geo, int F, const float* xe, const float* xsc, const float* xsh,
                  const float* Ps, const float* PtS, const float* W1, const float* W2,
-                 const float* b2, float* y, float* part, int prec, int bfy, hipStream_t st) {
-  MF_LAUNCH(F, fwd_prec(prec), km_edge_mlp_fwd, xe, xsc, xsh, Ps, PtS, W1, W2, b2, y, part, bfy)
+                 const float* b2, float* y, float* part, const MomFin& fin, int prec, int bfy,
+                 hipStream_t st) {
+  if (fin.cnt && (geo.nblocks > MOM_GROUP * MOM_MAXG || F > 16))
+    return pf::fail("pfsgnn mfma", "edge_mlp_fwd: in-launch finalize needs <= 4096 blocks");
+  MF_LAUNCH(F, fwd_prec(prec), km_edge_mlp_fwd, xe, xsc, xsh, Ps, PtS, W1, W2, b2, y, part, bfy,
+            fin)
   return 0;
 }
 

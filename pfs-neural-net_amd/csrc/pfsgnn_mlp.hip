@@ -80,15 +80,91 @@ __device__ __forceinline__ void build_in_rows(const InSegs& S, int K, int N, Row
   if (k >= S.k0[3]) { p = S.p[3]; kb = S.k0[3]; pg = S.pg[3]; }
   tab[k] = RowIn{p + (size_t)(k - kb) * (pg ? S.Gc : N), pg, 0};
 }
-__device__ __forceinline__ void build_out_rows(const OutSegs& S, int K, int N, RowOut* tab) {
-  const int k = threadIdx.x;
-  if (k >= K) return;
+// SModel's moment-gradient coefficients (k_moment_coef's arithmetic,
+// pfsgnn_node.hip) made in k_mlp_bwd's input-gradient epilogue (coef !=
+// nullptr): the dX rows [k0, k0 + 4 C2) -- d loss / d [mean; std; skew; kurt]
+// of C2 = 2F message channels (gnn.py:140-153) -- are then never written;
+// the epilogue turns them into coef [4][C2][N] straight from LDS.  To put a
+// channel's four rows into one 64-row store group, dX row r' of the kernel
+// holds input row mom_row(r'): r' = 4c + m (c < C2, m = moment) first, the
+// other input rows after them in order.  (16 <= C2 <= 20: channels 0..15 fill
+// the first 64-row group, 16.. open the second.)
+struct MomCoef {
+  const float* mom;   // [4][C2][N]: mean, c2, c3, c4 (pfsgnn_source_fwd's mom)
+  float* coef;        // [4][C2][N]
+  int C2, k0;
+  float invn;         // 1 / messages per fiber
+};
+__device__ __host__ __forceinline__ int mom_row(int r, const MomCoef& mc) {
+  if (!mc.coef) return r;
+  const int nm = 4 * mc.C2;
+  if (r < nm) return mc.k0 + (r & 3) * mc.C2 + (r >> 2);
+  const int q = r - nm;
+  return q < mc.k0 ? q : q + nm;
+}
+__device__ __forceinline__ void build_out_rows(const OutSegs& S, int K, int N, RowOut* tab,
+                                               const MomCoef& mc) {
+  const int r = threadIdx.x;
+  if (r >= K) return;
+  const int k = mom_row(r, mc);
+  if (mc.coef && k >= mc.k0 && k < mc.k0 + 4 * mc.C2) {   // (made into coef, not stored)
+    tab[r] = RowOut{nullptr, 0, 0};
+    return;
+  }
   float* p = S.p[0];
   int kb = 0, add = S.add[0];
   if (k >= S.k0[1]) { p = S.p[1]; kb = S.k0[1]; add = S.add[1]; }
   if (k >= S.k0[2]) { p = S.p[2]; kb = S.k0[2]; add = S.add[2]; }
   if (k >= S.k0[3]) { p = S.p[3]; kb = S.k0[3]; add = S.add[3]; }
-  tab[k] = RowOut{p ? p + (size_t)(k - kb) * N : nullptr, add, 0};
+  tab[r] = RowOut{p ? p + (size_t)(k - kb) * N : nullptr, add, 0};
+}
+// the coefficients of channels c0 .. c0 + 256 / (64 / NPT) - 1 for the chunk's
+// 64 nodes from their gradient rows 4 (c - c0) + m staged in X ([row][ld]);
+// thread (channel, j) takes nodes NPT j .. NPT j + NPT - 1 (NPT = 4: 16
+// channels; NPT = 1: 4 channels, fewer registers for the mid-loop group)
+template <int NPT>
+__device__ __forceinline__ void mom_coef_epi(const MomCoef& mc, const float* X, int ld, int c0,
+                                             int n0, int N) {
+  constexpr int TPC = 64 / NPT;   // threads per channel
+  const int t = threadIdx.x, cl = t / TPC, j = t % TPC, c = c0 + cl;
+  if (c >= mc.C2) return;
+  // (the bases as VGPR values: the kernel's scalar registers are spent, and
+  // uniform address math here spilled them)
+  const float* mom = mc.mom;
+  float* coef = mc.coef;
+  int C2 = mc.C2;
+  float invn = mc.invn;
+  asm volatile("" : "+v"(mom), "+v"(coef), "+v"(C2), "+v"(invn), "+v"(N));
+  const size_t CN = (size_t)C2 * N;
+  float m2[NPT], m3[NPT], m4[NPT];
+#pragma unroll
+  for (int e = 0; e < NPT; ++e) {   // every load in flight (clamped node)
+    const int n = min(n0 + NPT * j + e, N - 1);
+    const size_t i = (size_t)c * N + n;
+    m2[e] = mom[CN + i];
+    m3[e] = mom[2 * CN + i];
+    m4[e] = mom[3 * CN + i];
+  }
+#pragma unroll
+  for (int e = 0; e < NPT; ++e) {
+    const int n = n0 + NPT * j + e;
+    if (n >= N) continue;
+    const float c2 = m2[e], c3 = m3[e], c4 = m4[e];
+    const float* xr = X + 4 * cl * ld + NPT * j + e;
+    const float gmean = xr[0], gstd = xr[ld], gskew = xr[2 * ld], gkurt = xr[3 * ld];
+    const float var = c2 > 0.f ? c2 : 0.01f * c2;
+    const float sd = sqrtf(var + 1e-6f);
+    const float sd2 = sd * sd, sd3 = sd2 * sd, sd4 = sd2 * sd2;
+    const float A3 = gskew / sd3;
+    const float A4 = gkurt / sd4;
+    const float gstd_tot = gstd - 3.f * gskew * c3 / sd4 - 4.f * gkurt * c4 / (sd4 * sd);
+    const float gvr = gstd_tot / (2.f * sd) * (c2 > 0.f ? 1.f : 0.01f);
+    const size_t i = (size_t)c * N + n;
+    coef[i] = (gmean - 3.f * c2 * A3 - 4.f * c3 * A4) * invn;
+    coef[CN + i] = 2.f * gvr * invn;
+    coef[2 * CN + i] = 3.f * A3 * invn;
+    coef[3 * CN + i] = 4.f * A4 * invn;
+  }
 }
 
 // node tables of a chunk staged in LDS as [row][XS_LD]: a wave's 16-node
@@ -1600,7 +1676,7 @@ __global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_bwd(
     const float* __restrict__ var, const float* __restrict__ gamma, float eps,
     float* __restrict__ dgamma, float* __restrict__ dbeta, const float* __restrict__ Z,
     const float* __restrict__ W1, int ldw1, const float* __restrict__ W2,
-    float* __restrict__ dYp, float* __restrict__ dZ, OutSegs outs, int want_dx) {
+    float* __restrict__ dYp, float* __restrict__ dZ, OutSegs outs, int want_dx, MomCoef mc) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   floatx4* T2 = reinterpret_cast<floatx4*>(sm);  // [M][64]: W2^T per hidden tile
   floatx4* T1 = T2 + M * 64;                     // [M][M][64]: W1^T per (input tile, hidden tile)
@@ -1621,7 +1697,7 @@ __global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_bwd(
       const int idx = t + 256 * i;
       const int r = idx & 3, l = (idx >> 2) & 63, mt = (idx >> 8) % M, mk = (idx >> 8) / M;
       const int h = 16 * mt + 4 * (l >> 4) + r, k = 16 * mk + (l & 15);
-      v[i] = (want_dx && h < H && k < K) ? W1[(size_t)h * ldw1 + k] : 0.f;
+      v[i] = (want_dx && h < H && k < K) ? W1[(size_t)h * ldw1 + mom_row(k, mc)] : 0.f;
     }
     if constexpr (X3) {
       static_assert(!X3 || RS, "X3: the RS form only");
@@ -1656,7 +1732,7 @@ __global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_bwd(
     }
   }
   __shared__ RowOut rout[16 * M];   // the input-gradient rows' outputs
-  if (want_dx) build_out_rows(outs, K, N, rout);
+  if (want_dx) build_out_rows(outs, K, N, rout, mc);
   const bool bn = spart != nullptr;
   if (bn) {
     // (the merge's scratch is the chunk buffer DXs, free until the chunk loop:
@@ -1664,15 +1740,17 @@ __global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_bwd(
     // blocks per CU)
     float (*ss)[SUM_LEN] = reinterpret_cast<float (*)[SUM_LEN]>(DXs);
     const int c = t & 31, u = t >> 5;  // 8 subsets of the partial list per sum
-    float v[32];  // nsp <= 256: every load in flight, then a fixed-order sum
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      const int b = u + 8 * i;
-      v[i] = b < nsp ? spart[(size_t)b * SUM_LEN + c] : 0.f;
-    }
     float s = 0.f;
+    for (int r0 = 0; r0 < nsp; r0 += 256) {   // (one round for nsp <= 256)
+      float v[32];  // every load of the round in flight, then a fixed-order sum
 #pragma unroll
-    for (int i = 0; i < 32; ++i) s += v[i];
+      for (int i = 0; i < 32; ++i) {
+        const int b = r0 + u + 8 * i;
+        v[i] = b < nsp ? spart[(size_t)b * SUM_LEN + c] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 32; ++i) s += v[i];
+    }
     ss[u][c] = s;
     __syncthreads();
     if (t < 16) {
@@ -1797,8 +1875,13 @@ __global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_bwd(
 #pragma unroll
         for (int mt = 0; mt < M; ++mt) pf_split4(dz[mt][0], dz[mt][1], dz[mt][2], dz[mt][3], zh[mt], zl[mt]);
       }
+      // (groups last to first: with the moment epilogue, group 0's 16 channels
+      // are turned into coefficients after the loop, when the split dZ
+      // registers are dead)
+      constexpr int NG = (M + MG - 1) / MG;
 #pragma unroll
-      for (int g0 = 0; g0 < M; g0 += MG) {
+      for (int gi = NG - 1; gi >= 0; --gi) {
+        const int g0 = gi * MG;
         const int GN = (M - g0) < MG ? (M - g0) : MG;
         floatx4 dx[MG];
 #pragma unroll
@@ -1851,7 +1934,20 @@ __global__ __launch_bounds__(256, ((M <= 3 || RS) ? 2 : 1)) void k_mlp_bwd(
         }
         __syncthreads();
         store_rows<4>(rout, DXs, 16 * g0, 16 * g0, min(K, 16 * (g0 + GN)), ch * 64, N, wu, lane);
+#if !defined(MLP_NO_MOMEPI) && !defined(MLP_NO_MOMEPI1)
+        if (gi == 1 && mc.coef && 16 < mc.C2) {
+          __builtin_amdgcn_sched_barrier(0);
+          mom_coef_epi<1>(mc, DXs, XS_LD, 16, ch * 64, N);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#endif
       }
+#ifndef MLP_NO_MOMEPI
+      if (mc.coef) {   // (group 0 is in DXs)
+        __builtin_amdgcn_sched_barrier(0);
+        mom_coef_epi<4>(mc, DXs, XS_LD, 0, ch * 64, N);
+      }
+#endif
     } else if (want_dx) {
       __syncthreads();                             // previous chunk's stores from DXs done
       // dX = W1^T dZ: K-step group mt (hidden tile) over the M output tiles, its
@@ -2312,13 +2408,15 @@ extern "C" int pfsgnn_target_global_fwd(
   return pf::check_launch(where);
 }
 
-extern "C" int pfsgnn_mlp_bwd(const float* dY, int N, const float* Yp, const float* mu,
-                              const float* var, const float* gamma, float eps, float* dgamma,
-                              float* dbeta, const float* Z, const float* W1, int ldw1, int H,
-                              int K, const float* W2, int O, float* dYp, float* dZ,
-                              const pfsgnn_oseg* outs, int nout, void* ws, size_t ws_bytes,
-                              void* stream) {
-  const char* where = "pfsgnn_mlp_bwd";
+// pre_part / pre_n: the BatchNorm sums' per-block partials ([pre_n][32]) made
+// by the producer of dY (pfsgnn_target_bwd_bn); nullptr: k_bn_sums_part here
+static int mlp_bwd_impl(const char* where, const float* dY, int N, const float* Yp,
+                        const float* mu, const float* var, const float* gamma, float eps,
+                        float* dgamma, float* dbeta, const float* Z, const float* W1, int ldw1,
+                        int H, int K, const float* W2, int O, float* dYp, float* dZ,
+                        const pfsgnn_oseg* outs, int nout, void* ws, size_t ws_bytes,
+                        void* stream, const float* pre_part, int pre_n,
+                        const MomCoef& mco = MomCoef{}) {
   PF_REQUIRE(dY && Z && W1 && W2 && dZ && N > 0 && H > 0 && K > 0 && O > 0 && O <= 16, where,
              "bad arguments");
   const bool bn = gamma != nullptr;
@@ -2340,18 +2438,25 @@ extern "C" int pfsgnn_mlp_bwd(const float* dY, int N, const float* Yp, const flo
   PF_REQUIRE(m > 0, where, "K, H > 112 not supported");
   PF_REQUIRE(ws && ws_bytes >= pfsgnn_mlp_ws_bytes(N), where, "workspace too small");
   hipStream_t st = as_stream(stream);
-  float* spart = nullptr;
+  const float* spart = nullptr;
   int nsp = 0;
-  if (bn) {
-    spart = reinterpret_cast<float*>(static_cast<char*>(ws) +
-                                      align256((size_t)512 * PART_LEN * sizeof(float)));
+  if (bn && pre_part) {
+    spart = pre_part;
+    nsp = pre_n;
+  } else if (bn) {
+    float* sp = reinterpret_cast<float*>(static_cast<char*>(ws) +
+                                         align256((size_t)512 * PART_LEN * sizeof(float)));
     nsp = std::max(1, std::min(256, (N + 255) / 256));
     hipLaunchKernelGGL(k_bn_sums_part, dim3(nsp), dim3(256), 0, st, dY, Yp, O, N, mu, var, eps,
-                       spart);
+                       sp);
+    spart = sp;
   }
   const size_t lds = bwd_lds(m);
   const int want_dx = nout > 0 ? 1 : 0;
   const bool rs = bwd_rs(m);
+  PF_REQUIRE(!mco.coef || (rs && want_dx && mco.mom && mco.C2 >= 16 && mco.C2 <= 20 &&
+                           mco.k0 >= 0 && mco.k0 + 4 * mco.C2 <= K),
+             where, "the moment epilogue needs the RS form, dX and 16..20 channels inside K");
   // the gradient chains in bf16x3 (RS form): PFSGNN_NODE_DX_X3, pf::node_x3's policy
   const bool x3 = rs && pf::node_x3("PFSGNN_NODE_DX_X3");
   const int rc = with_tiles(m, [&](auto mc) {
@@ -2370,7 +2475,7 @@ extern "C" int pfsgnn_mlp_bwd(const float* dY, int N, const float* Yp, const flo
       }
       hipLaunchKernelGGL((k_mlp_bwd<MM, RS, X3>), dim3(grid), dim3(256), lds, st, K, N, H, O, dY,
                          Yp, spart, nsp, mu, var, gamma, eps, dgamma, dbeta, Z, W1, ldw1, W2, dYp,
-                         dZ, OS, want_dx);
+                         dZ, OS, want_dx, mco);
       return 0;
     };
     if (!rs) return launch(std::false_type{}, std::false_type{});
@@ -2380,4 +2485,30 @@ extern "C" int pfsgnn_mlp_bwd(const float* dY, int N, const float* Yp, const flo
   PF_REQUIRE(rc != -3, where, "hipFuncSetAttribute (dynamic LDS) failed");
   PF_REQUIRE(rc == 0, where, "no kernel for this width");
   return pf::check_launch(where);
+}
+
+extern "C" int pfsgnn_mlp_bwd(const float* dY, int N, const float* Yp, const float* mu,
+                              const float* var, const float* gamma, float eps, float* dgamma,
+                              float* dbeta, const float* Z, const float* W1, int ldw1, int H,
+                              int K, const float* W2, int O, float* dYp, float* dZ,
+                              const pfsgnn_oseg* outs, int nout, void* ws, size_t ws_bytes,
+                              void* stream) {
+  return mlp_bwd_impl("pfsgnn_mlp_bwd", dY, N, Yp, mu, var, gamma, eps, dgamma, dbeta, Z, W1,
+                      ldw1, H, K, W2, O, dYp, dZ, outs, nout, ws, ws_bytes, stream, nullptr, 0);
+}
+
+extern "C" int pfsgnn_mlp_bwd_pre(const float* dY, int N, const float* Yp, const float* mu,
+                                  const float* var, const float* gamma, float eps, float* dgamma,
+                                  float* dbeta, const float* Z, const float* W1, int ldw1, int H,
+                                  int K, const float* W2, int O, float* dYp, float* dZ,
+                                  const pfsgnn_oseg* outs, int nout, const float* bn_part,
+                                  int bn_nparts, const float* mom, float* coef, int mom_k0,
+                                  int mom_c, int mom_n, void* ws, size_t ws_bytes, void* stream) {
+  PF_REQUIRE(!bn_part || (gamma && bn_nparts > 0 && bn_nparts <= 65536), "pfsgnn_mlp_bwd_pre",
+             "BatchNorm sum partials need gamma and 1..65536 partials");
+  PF_REQUIRE(!coef || (mom && mom_n > 0), "pfsgnn_mlp_bwd_pre", "coef needs mom and mom_n > 0");
+  const MomCoef mc{coef ? mom : nullptr, coef, mom_c, mom_k0, coef ? 1.0f / (float)mom_n : 0.f};
+  return mlp_bwd_impl("pfsgnn_mlp_bwd_pre", dY, N, Yp, mu, var, gamma, eps, dgamma, dbeta, Z, W1,
+                      ldw1, H, K, W2, O, dYp, dZ, outs, nout, ws, ws_bytes, stream, bn_part,
+                      bn_part ? bn_nparts : 0, mc);
 }

@@ -150,13 +150,28 @@ extern "C" const char* pfsgnn_version(void) { return "pfsgnn 0.1 gfx950"; }
 
 // ---------------------------------------------------------------- reduce
 // Partial reductions out[r][c] (+)= scale * sum_b part[b*plen + r*ldp + c],
-// up to PF_MAX_RED independent ones per launch (blockIdx.z picks one; block
+// up to PF_MAX_RED (96) independent ones per launch (blockIdx.z picks one; block
 // layout below).  Long lists (nb > 256) first take an in-place stage: segment s of RED_SEG
 // partials is summed into the segment's first row (each block touches only its
 // own cells; the descriptors of one launch never share cells).
 #define RED_SEG 128
+// a RedDesc as the kernels read it: 40 bytes, so that 96 share one launch's
+// 4 KB of kernel arguments (a backward pass's ~200 weight-gradient
+// reductions in 3 launches, not 5); the add flag rides in cols' top bit
+#define PF_PACK_RED PF_MAX_RED
+struct RedDev {
+  const float* part;
+  float* out;
+  uint32_t plen;
+  int nb, ldp, ldo;
+  uint16_t rows, colsa;
+  float scale;
+  __device__ __host__ int cols() const { return colsa & 0x7fff; }
+  __device__ __host__ bool add() const { return (colsa >> 15) != 0; }
+};
+static_assert(sizeof(RedDev) == 40, "RedDev layout");
 struct RedPack {
-  RedDesc d[PF_MAX_RED];
+  RedDev d[PF_PACK_RED];
 };
 static_assert(sizeof(RedPack) <= 4096, "k_reduce_rows' descriptor pack must fit the kernel arguments");
 
@@ -171,12 +186,13 @@ static_assert(sizeof(RedPack) <= 4096, "k_reduce_rows' descriptor pack must fit 
 #define RED_O 64
 #define RED_P 4
 __global__ __launch_bounds__(256) void k_reduce_rows(RedPack pk) {
-  const RedDesc& D = pk.d[blockIdx.z];
+  const RedDev& D = pk.d[blockIdx.z];
   const int t = threadIdx.x, o = t & 15, pl = t >> 4;
   const int idx = blockIdx.x * 16 + o;
-  if (blockIdx.x * 16 >= D.rows * D.cols) return;
-  const bool v = idx < D.rows * D.cols;
-  const int r = v ? idx / D.cols : 0, c = v ? idx - r * D.cols : 0;
+  const int cols = D.cols();
+  if (blockIdx.x * 16 >= D.rows * cols) return;
+  const bool v = idx < D.rows * cols;
+  const int r = v ? idx / cols : 0, c = v ? idx - r * cols : 0;
   const float* p = D.part + (size_t)r * D.ldp + c;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   int b = pl;
@@ -195,18 +211,19 @@ __global__ __launch_bounds__(256) void k_reduce_rows(RedPack pk) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) s += sh[i][t];
     float* op = D.out + (size_t)r * D.ldo + c;
-    *op = D.add ? (*op + D.scale * s) : D.scale * s;
+    *op = D.add() ? (*op + D.scale * s) : D.scale * s;
   }
 }
 
 __global__ __launch_bounds__(256) void k_reduce_seg(RedPack pk) {
-  const RedDesc& D = pk.d[blockIdx.z];
+  const RedDev& D = pk.d[blockIdx.z];
   const int t = threadIdx.x, o = t & (RED_O - 1), pl = t / RED_O;
   const int idx = blockIdx.x * RED_O + o;
   const int b0 = blockIdx.y * RED_SEG;
-  if (blockIdx.x * RED_O >= D.rows * D.cols || b0 >= D.nb || D.nb <= 2 * RED_SEG) return;
-  const bool v = idx < D.rows * D.cols;
-  const int r = v ? idx / D.cols : 0, c = v ? idx - r * D.cols : 0;
+  const int cols = D.cols();
+  if (blockIdx.x * RED_O >= D.rows * cols || b0 >= D.nb || D.nb <= 2 * RED_SEG) return;
+  const bool v = idx < D.rows * cols;
+  const int r = v ? idx / cols : 0, c = v ? idx - r * cols : 0;
   const int b1 = min(D.nb, b0 + RED_SEG);
   float* p = const_cast<float*>(D.part) + (size_t)r * D.ldp + c;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
@@ -229,16 +246,26 @@ __global__ __launch_bounds__(256) void k_reduce_seg(RedPack pk) {
   }
 }
 
+static RedDev red_dev(const RedDesc& a) {
+  if (a.rows < 0 || a.rows > 65535 || a.cols < 0 || a.cols > 32767 ||
+      a.plen * (a.nb > 2 * RED_SEG ? RED_SEG : 1) > 0xffffffffull) {
+    pf::fail("launch_reduce_multi", "reduction wider than the packed descriptor");
+    return RedDev{a.part, a.out, 0, 0, 0, 0, 0, 0, 0.f};   // (nothing reduced; error recorded)
+  }
+  return RedDev{a.part, a.out, (uint32_t)a.plen, a.nb, a.ldp, a.ldo, (uint16_t)a.rows,
+                (uint16_t)(a.cols | (a.add ? 0x8000 : 0)), a.scale};
+}
+
 void launch_reduce_multi(const RedDesc* d, int n, hipStream_t st) {
-  for (int i0 = 0; i0 < n; i0 += PF_MAX_RED) {
-    const int m = std::min(PF_MAX_RED, n - i0);
+  for (int i0 = 0; i0 < n; i0 += PF_PACK_RED) {
+    const int m = std::min(PF_PACK_RED, n - i0);
     RedPack pk{};
     int gx = 1, gxs = 1, gy = 1;
     bool seg = false;
     for (int i = 0; i < m; ++i) {
-      pk.d[i] = d[i0 + i];
-      gx = std::max(gx, (pk.d[i].rows * pk.d[i].cols + 15) / 16);
-      gxs = std::max(gxs, (pk.d[i].rows * pk.d[i].cols + RED_O - 1) / RED_O);
+      pk.d[i] = red_dev(d[i0 + i]);
+      gx = std::max(gx, (pk.d[i].rows * pk.d[i].cols() + 15) / 16);
+      gxs = std::max(gxs, (pk.d[i].rows * pk.d[i].cols() + RED_O - 1) / RED_O);
       if (pk.d[i].nb > 2 * RED_SEG) {
         seg = true;
         gy = std::max(gy, (pk.d[i].nb + RED_SEG - 1) / RED_SEG);
@@ -1187,15 +1214,13 @@ extern "C" size_t pfsgnn_wgrad_multi_bytes(const pfsgnn_wgrad_job* jobs, int n) 
   return tot + 256;
 }
 
-extern "C" int pfsgnn_wgrad_multi(const pfsgnn_wgrad_job* jobs, int n, void* part,
-                                  size_t part_bytes, void* stream) {
-  const char* where = "pfsgnn_wgrad_multi";
-  PF_REQUIRE(n >= 0 && (jobs || n == 0), where, "bad arguments");
-  if (n == 0) return 0;
-  hipStream_t st = as_stream(stream);
+static int reduce_batch_desc(const std::vector<RedDesc>& reds, hipStream_t st);
+
+// the jobs' kernels; their reductions are appended to `reds`
+static int wgrad_multi_launch(const pfsgnn_wgrad_job* jobs, int n, void* part, size_t part_bytes,
+                              hipStream_t st, std::vector<RedDesc>& reds, const char* where) {
   std::vector<WgJob> J(n);
   std::vector<WgPlan> PL(n);
-  std::vector<RedDesc> reds;
   size_t off = 0;
   char* base = static_cast<char*>(part);
   for (int i = 0; i < n; ++i) {
@@ -1260,12 +1285,20 @@ extern "C" int pfsgnn_wgrad_multi(const pfsgnn_wgrad_job* jobs, int n, void* par
       if (!launched) return pf::fail(where, "no kernel for this shape");
     }
   }
+  return 0;
+}
+
+extern "C" int pfsgnn_wgrad_multi(const pfsgnn_wgrad_job* jobs, int n, void* part,
+                                  size_t part_bytes, void* stream) {
+  const char* where = "pfsgnn_wgrad_multi";
+  PF_REQUIRE(n >= 0 && (jobs || n == 0), where, "bad arguments");
+  if (n == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  std::vector<RedDesc> reds;
+  if (int rc = wgrad_multi_launch(jobs, n, part, part_bytes, st, reds, where)) return rc;
   // the reductions, batched (a launch never holds two into the same cells)
-  std::vector<pfsgnn_red> rr(reds.size());
-  for (size_t i = 0; i < reds.size(); ++i)
-    rr[i] = {reds[i].part, reds[i].nb, reds[i].plen, reds[i].ldp, reds[i].rows, reds[i].cols,
-             reds[i].out, reds[i].ldo, reds[i].add, reds[i].scale};
-  return pfsgnn_reduce_batch(rr.data(), (int)rr.size(), stream);
+  if (int rc = reduce_batch_desc(reds, st)) return rc;
+  return pf::check_launch(where);
 }
 
 namespace pf {
@@ -1309,6 +1342,14 @@ unsigned* g_sync = nullptr;
 size_t g_sync_n = 0;
 }  // namespace
 unsigned* sync_counters(size_t n) { return (g_sync && n <= g_sync_n) ? g_sync : nullptr; }
+unsigned* sync_slot(size_t n) {
+  constexpr size_t SLOT = 128;   // counters per slot (512 bytes)
+  static size_t next = 0;
+  const size_t nslots = g_sync ? g_sync_n / SLOT : 0;
+  if (n > SLOT || nslots < 2) return nullptr;
+  next = next + 1 < nslots ? next + 1 : 1;   // (slot 0: sync_counters' own)
+  return g_sync + next * SLOT;
+}
 }  // namespace pf
 
 extern "C" size_t pfsgnn_sync_bytes(void) { return (size_t)1 << 20; }
@@ -1337,13 +1378,29 @@ extern "C" int pfsgnn_defer_end(void* stream) {
   pf::DeferCtx& D = pf::g_defer;
   PF_REQUIRE(D.on, "pfsgnn_defer_end", "no deferred pass is open");
   D.on = false;
-  std::vector<pfsgnn_red> rr(D.q.size());
-  for (size_t i = 0; i < D.q.size(); ++i) {
-    const RedDesc& r = D.q[i];
-    rr[i] = {r.part, r.nb, r.plen, r.ldp, r.rows, r.cols, r.out, r.ldo, r.add, r.scale};
-  }
-  D.q.clear();
-  return pfsgnn_reduce_batch(rr.data(), (int)rr.size(), stream);
+  std::vector<RedDesc> reds;
+  reds.swap(D.q);
+  if (int rc = reduce_batch_desc(reds, as_stream(stream))) return rc;
+  return pf::check_launch("pfsgnn_defer_end");
+}
+
+extern "C" int pfsgnn_defer_end_multi(const pfsgnn_wgrad_job* jobs, int n, void* part,
+                                      size_t part_bytes, void* stream) {
+  const char* where = "pfsgnn_defer_end_multi";
+  pf::DeferCtx& D = pf::g_defer;
+  PF_REQUIRE(D.on, where, "no deferred pass is open");
+  PF_REQUIRE(n >= 0 && (jobs || n == 0), where, "bad arguments");
+  D.on = false;
+  std::vector<RedDesc> reds;
+  reds.swap(D.q);
+  hipStream_t st = as_stream(stream);
+  // the jobs' kernels first (they read activations and gradients, never a
+  // weight gradient), then the pass's deferred edge reductions and the jobs'
+  // own in one batch
+  if (n > 0)
+    if (int rc = wgrad_multi_launch(jobs, n, part, part_bytes, st, reds, where)) return rc;
+  if (int rc = reduce_batch_desc(reds, st)) return rc;
+  return pf::check_launch(where);
 }
 
 // Output rectangles of two reductions intersect?  Exact when both write rows
@@ -1367,15 +1424,11 @@ static bool red_overlap(const RedDesc& a, const RedDesc& b) {
   return rows_meet && cols_meet;
 }
 
-extern "C" int pfsgnn_reduce_batch(const pfsgnn_red* reds, int n, void* stream) {
-  PF_REQUIRE(n >= 0 && (reds || n == 0), "pfsgnn_reduce_batch", "bad arguments");
-  hipStream_t st = as_stream(stream);
+static int reduce_batch_desc(const std::vector<RedDesc>& reds, hipStream_t st) {
   std::vector<RedDesc> group;
-  for (int i = 0; i < n; ++i) {
-    const pfsgnn_red& r = reds[i];
-    PF_REQUIRE(r.part && r.out && r.nb > 0 && r.rows > 0 && r.cols > 0, "pfsgnn_reduce_batch",
+  for (const RedDesc& d : reds) {
+    PF_REQUIRE(d.part && d.out && d.nb > 0 && d.rows > 0 && d.cols > 0, "pfsgnn_reduce_batch",
                "bad reduction");
-    const RedDesc d{r.part, r.nb, r.plen, r.ldp, r.rows, r.cols, r.out, r.ldo, r.add, r.scale};
     bool clash = (int)group.size() == PF_MAX_RED;
     for (const RedDesc& g : group) clash = clash || red_overlap(g, d);
     if (clash) {  // a launch never holds two reductions into the same cells
@@ -1385,6 +1438,17 @@ extern "C" int pfsgnn_reduce_batch(const pfsgnn_red* reds, int n, void* stream) 
     group.push_back(d);
   }
   if (!group.empty()) launch_reduce_multi(group.data(), (int)group.size(), st);
+  return 0;
+}
+
+extern "C" int pfsgnn_reduce_batch(const pfsgnn_red* reds, int n, void* stream) {
+  PF_REQUIRE(n >= 0 && (reds || n == 0), "pfsgnn_reduce_batch", "bad arguments");
+  std::vector<RedDesc> v(n);
+  for (int i = 0; i < n; ++i) {
+    const pfsgnn_red& r = reds[i];
+    v[i] = RedDesc{r.part, r.nb, r.plen, r.ldp, r.rows, r.cols, r.out, r.ldo, r.add, r.scale};
+  }
+  if (int rc = reduce_batch_desc(v, as_stream(stream))) return rc;
   return pf::check_launch("pfsgnn_reduce_batch");
 }
 

@@ -168,10 +168,11 @@ class Engine:
             return be.affine_rows(Y, sc, sh), (segs, Z, ("eval", Y, bnkey, rm, rv))
         return Y, (segs, Z, None)
 
-    def mlp_bwd(self, P, Gr, pre, dY, saved, outs=()):
+    def mlp_bwd(self, P, Gr, pre, dY, saved, outs=(), bn_part=None, mom_coef=None):
         """Backward of mlp_fwd: the input gradient goes to ``outs`` = [(tensor or
         None, rows, add)] over the K input rows (empty: none wanted); the weight
-        gradients accumulate into Gr."""
+        gradients accumulate into Gr.  ``bn_part``: the BatchNorm's backward sums
+        already made by dY's producer (_fiber_bn_sums)."""
         be = self.be
         if saved[0] == "ops":
             return self._mlp_bwd_ops(P, Gr, pre, dY, saved, outs)
@@ -185,9 +186,24 @@ class Engine:
         if bns is not None:
             Yp, mu, var, key = bns
             bn = (Yp, mu, var, P[key + "weight"], self.bn_eps, Gr[key + "weight"], Gr[key + "bias"])
-        dYp, dZ = be.mlp_bwd(dY, Z, W1, W2, K, bn=bn, outs=list(outs))
+        kw = {"bn_part": bn_part} if bn_part is not None else {}
+        if mom_coef is not None:
+            kw["mom_coef"] = mom_coef
+        dYp, dZ = be.mlp_bwd(dY, Z, W1, W2, K, bn=bn, outs=list(outs), **kw)
         be.wgrad(dYp, Z, Gr[pre + "2.weight"], db=Gr[pre + "2.bias"], act_in=True)
         be.wgrad_cat(dZ, segs, Gr[pre + "0.weight"], db=Gr[pre + "0.bias"])
+
+    def _fiber_bn_sums(self, d, ss):
+        """SModel's node_mlp_2 BatchNorm backward sums made by TModel's edge
+        backward, whose epilogue finishes g_xs (pfsgnn_target_bwd_bn): the
+        (Yp, mu, var, eps) to hand it, or None (then mlp_bwd sums them)."""
+        sS = ss.get("sS")
+        if (d.sp is not None or not self.normed or not getattr(self.be, "fiber_bn_sums", False)
+                or os.environ.get("PFSGNN_FIBER_BN_SUMS", "1") == "0" or sS is None
+                or sS[0] == "ops" or sS[2] is None or sS[2][0] == "eval"):
+            return None
+        Yp, mu, var, _ = sS[2]
+        return (Yp, mu, var, self.bn_eps)
 
     def _bn_eval_bwd(self, P, Gr, key, times, dY, Yp, rm, rv):
         """Backward of an eval-mode BatchNorm1d (running statistics rm, rv; applied
@@ -386,13 +402,33 @@ class Engine:
         st.update(sS=sS, xs_new=xs_new)
         return st
 
-    def source_node_bwd(self, P, Gr, d, pre, st, g_xs_new, g_xs, g_u):
+    def _mom_epi_ok(self, d, st):
+        """node_mlp_2's backward can turn the moment gradients into the
+        coefficients itself (pfsgnn_mlp_bwd_pre's coef): complete graphs, the
+        fused MLP in its wide register form, 16..20 message channels."""
+        sS = st.get("sS")
+        return (d.sp is None and getattr(self.be, "fiber_bn_sums", False)
+                and self.F in (8, 10) and sS is not None and sS[0] != "ops"
+                and os.environ.get("PFSGNN_MOM_EPI", "1") != "0"
+                and os.environ.get("PFSGNN_MLP_BWD_RS", "1") != "0")
+
+    def source_node_bwd(self, P, Gr, d, pre, st, g_xs_new, g_xs, g_u, bn_part=None):
         """Node half of the SModel backward; returns the per-fiber moment coefficients."""
         be, F, G = self.be, self.F, d.G
-        gst = be.empty(8 * F, d.NS)          # d loss / d [mean, std, skew, kurt]
         gu = be.empty(F, d.NS)               # d loss / d u[batch], per fiber
+        if self._mom_epi_ok(d, st):
+            # d loss / d [mean, std, skew, kurt] never leaves the kernel: its
+            # epilogue makes the coefficients (k_moment_coef's arithmetic)
+            coef = be.empty(4, 2 * F, d.NS)
+            self.mlp_bwd(P, Gr, pre + "node_mlp_2.", g_xs_new, st["sS"],
+                         outs=[(g_xs, F, True), (None, 8 * F, False), (gu, F, False)],
+                         bn_part=bn_part, mom_coef=(st["mom"], coef, F, d.NC))
+            self._gu_add(gu, G, g_u)
+            return coef
+        gst = be.empty(8 * F, d.NS)          # d loss / d [mean, std, skew, kurt]
         self.mlp_bwd(P, Gr, pre + "node_mlp_2.", g_xs_new, st["sS"],
-                     outs=[(g_xs, F, True), (gst, 8 * F, False), (gu, F, False)])
+                     outs=[(g_xs, F, True), (gst, 8 * F, False), (gu, F, False)],
+                     bn_part=bn_part)
         self._gu_add(gu, G, g_u)
         # messages per fiber: NC on complete graphs, the fiber degree otherwise
         return be.moment_coef(st["mom"], gst, d.NC if d.sp is None else d.sp.fib_ptr)
@@ -557,17 +593,21 @@ class Engine:
             be.wgrad(g_agg, d.sp.deg_t, Gr[pre + "node_mlp_1.2.bias"].view(-1, 1))
         return be.lin_t(Wt2, 0, 2 * F, g_agg)
 
-    def target_edge_bwd(self, P, Gr, d, pre, st, g_hsum, want_gxe, g_xs):
+    def target_edge_bwd(self, P, Gr, d, pre, st, g_hsum, want_gxe, g_xs, bn_sums=None):
+        """-> gxe; with ``bn_sums`` (_fiber_bn_sums) -> (gxe, BatchNorm sum partials)."""
         be, F = self.be, self.F
         Wt1 = P[pre + "node_mlp_1.0.weight"]
         y, sc, sh = st["xe3"]
         kw = {"tmask": st["tmask"]} if st.get("tmask") is not None else {}
-        GzT, gxe = be.target_bwd(d, y, sc, sh, st["Rs"], Wt1, g_hsum,
-                                 Gr[pre + "node_mlp_1.0.weight"], want_gxe=want_gxe,
-                                 g_xs=g_xs, **kw)          # + g_xs += Wt1s^T GzT
+        if bn_sums is not None:
+            kw["bn_sums"] = bn_sums
+        out = be.target_bwd(d, y, sc, sh, st["Rs"], Wt1, g_hsum,
+                            Gr[pre + "node_mlp_1.0.weight"], want_gxe=want_gxe,
+                            g_xs=g_xs, **kw)          # + g_xs += Wt1s^T GzT
+        GzT, gxe = out[0], out[1]
         be.wgrad(GzT, st["xs"], Gr[pre + "node_mlp_1.0.weight"], col0=0,
                  db=Gr[pre + "node_mlp_1.0.bias"])
-        return gxe
+        return (gxe, out[2]) if bn_sums is not None else gxe
 
     # --- GlobalModel (gnn.py:208-223; its RMSNorm also runs twice)
     def global_fwd(self, P, d, pre, xs, xt, u):
@@ -726,10 +766,18 @@ class Engine:
                     if live_t:
                         g_hsum = self.target_node_bwd(P, Gr, d, p + "t_model.", stt, g_xt_new,
                                                       g_xt_in, g_u_in)
+                bn_part = None
                 if live_t:
-                    self.target_edge_bwd(P, Gr, d, p + "t_model.", stt, g_hsum, False, g_xs_new)
+                    # (g_xs_new is final after TModel's edge backward: its epilogue
+                    # also makes SModel's BatchNorm backward sums)
+                    bn_sums = self._fiber_bn_sums(d, ss)
+                    r = self.target_edge_bwd(P, Gr, d, p + "t_model.", stt, g_hsum, False,
+                                             g_xs_new, bn_sums=bn_sums)
+                    if bn_sums is not None:
+                        bn_part = r[1]
                     tpart = (stt["Rs"], P[p + "t_model.node_mlp_1.0.weight"], g_hsum)
-                coef = self.source_node_bwd(P, Gr, d, p + "s_model.", ss, g_xs_new, g_xs_in, g_u_in)
+                coef = self.source_node_bwd(P, Gr, d, p + "s_model.", ss, g_xs_new, g_xs_in, g_u_in,
+                                            bn_part=bn_part)
                 g_tot, *bnc = self.source_edge_bwd(P, Gr, d, p + "s_model.", ss, coef, tpart,
                                                    g_xe, bnstat, g_xt_in,
                                                    se=None if ev else se,

@@ -164,6 +164,7 @@ _SIGS = {
     "pfsgnn_wgrad_multi": ([WGJP, I, P, SZ, P], I),
     "pfsgnn_defer_begin": ([P, SZ], I),
     "pfsgnn_defer_end": ([P], I),
+    "pfsgnn_defer_end_multi": ([WGJP, I, P, SZ, P], I),
     "pfsgnn_defer_need": ([], SZ),
     "pfsgnn_bn_fwd": ([P, I, I, P, P, P, P, FL, FL, P, P, P, P, SZ, P], I),
     "pfsgnn_bn_bwd": ([P, P, P, P, P, FL, I, I, P, P, P, P, SZ, P], I),
@@ -177,6 +178,8 @@ _SIGS = {
                                  + [P] * 6 + [P, SZ, P], I),
     "pfsgnn_mlp_bwd": ([P, I, P, P, P, P, FL, P, P, P, P, I, I, I, P, I, P, P, OSEGP, I, P, SZ,
                         P], I),
+    "pfsgnn_mlp_bwd_pre": ([P, I, P, P, P, P, FL, P, P, P, P, I, I, I, P, I, P, P, OSEGP, I, P, I,
+                            P, P, I, I, I, P, SZ, P], I),
     "pfsgnn_build_complete": ([I, I, I, I, P, P], I),
     "pfsgnn_graph_reduce": ([P, I, I, I, I, P, P], I),
     "pfsgnn_graph_reduce_add": ([P, I, I, I, I, P, P], I),
@@ -211,6 +214,7 @@ _SIGS = {
     "pfsgnn_target_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, P, P, P, SZ, P], I),
     "pfsgnn_tmask_bytes": ([I, I, I, I], SZ),
     "pfsgnn_target_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_target_bwd_bn": ([I, I, I, I] + [P] * 14 + [FL, P, P, SZ, P], I),
     "pfsgnn_source_bwd": ([I, I, I, I] + [P] * 24 + [P, SZ, P], I),
     "pfsgnn_source_bwd_bn": ([I, I, I, I] + [P] * 17 + [LL, FL] + [P] * 12 + [P, SZ, P], I),
     "pfsgnn_edge_bn_grad_sums": ([I, I, I, I, P, P, P, P, P, P, P, SZ, P], I),
@@ -414,6 +418,7 @@ class HipBackend:
     """The op set of pfsgnn.engine on libpfsgnn.so (fp32, channel-major)."""
 
     name = "hip"
+    fiber_bn_sums = True     # target_bwd(bn_sums=...) / mlp_bwd(bn_part=...)
 
     def __init__(self, device=None):
         if not torch.cuda.is_available():
@@ -559,30 +564,31 @@ class HipBackend:
         jobs, self._jobs = getattr(self, "_jobs", None), None
         if jobs is None:
             return
-        _call("pfsgnn_defer_end", _stream())
+        arr, arena = None, None
+        if jobs:
+            arr = (WgJob * len(jobs))()
+            for i, (job, _keep) in enumerate(jobs):
+                arr[i] = job
+            need = lib().pfsgnn_wgrad_multi_bytes(arr, len(jobs))
+            if need == 0:
+                raise RuntimeError("pfsgnn_wgrad_multi_bytes: " + lib().pfsgnn_last_error().decode())
+            arena = getattr(self, "_arena", None)
+            if arena is None or arena.numel() < need:
+                # grown during warm-up, before any graph capture; a replaced arena
+                # stays alive (see __init__)
+                if arena is not None:
+                    self._retired.append(arena)
+                self._arena = arena = torch.empty(max(need, 64 << 20), dtype=torch.uint8,
+                                                  device=self.device)
+        # the jobs and every queued reduction of the pass in one flush
+        _call("pfsgnn_defer_end_multi", arr, len(jobs), None if arena is None else arena.data_ptr(),
+              0 if arena is None else arena.numel(), _stream())
         need = lib().pfsgnn_defer_need()
         ea = getattr(self, "_earena", None)
         if need and (ea is None or ea.numel() < need):
             if ea is not None:
                 self._retired.append(ea)
             self._earena = torch.empty(need + (1 << 20), dtype=torch.uint8, device=self.device)
-        if not jobs:
-            return
-        arr = (WgJob * len(jobs))()
-        for i, (job, _keep) in enumerate(jobs):
-            arr[i] = job
-        need = lib().pfsgnn_wgrad_multi_bytes(arr, len(jobs))
-        if need == 0:
-            raise RuntimeError("pfsgnn_wgrad_multi_bytes: " + lib().pfsgnn_last_error().decode())
-        arena = getattr(self, "_arena", None)
-        if arena is None or arena.numel() < need:
-            # grown during warm-up, before any graph capture; a replaced arena
-            # stays alive (see __init__)
-            if arena is not None:
-                self._retired.append(arena)
-            self._arena = arena = torch.empty(max(need, 64 << 20), dtype=torch.uint8,
-                                              device=self.device)
-        _call("pfsgnn_wgrad_multi", arr, len(jobs), arena.data_ptr(), arena.numel(), _stream())
 
     def _wgrad_job(self, dY, arr, nseg, N, act_in, dW, db, dbscale, keep):
         job = WgJob(dY.data_ptr(), dY.shape[0], arr, nseg, N, int(act_in), dW.data_ptr(),
@@ -805,10 +811,15 @@ class HipBackend:
         r["rms"], r["Pt"], r["Qt"] = rms, Pt, Qt
         return r
 
-    def mlp_bwd(self, dY, Z, W1, W2, K, bn=None, outs=()):
+    def mlp_bwd(self, dY, Z, W1, W2, K, bn=None, outs=(), bn_part=None, mom_coef=None):
         """Input side of the MLP(+BN) backward.  ``bn`` = (Yp, mu, var, gamma, eps,
         dgamma, dbeta) or None; ``outs`` = [(tensor or None, rows, add)] covering
-        the K input rows (empty: no input gradient).  Returns (dYp, dZ)."""
+        the K input rows (empty: no input gradient); ``bn_part``: the BatchNorm
+        sums' partials the producer of dY already made (target_bwd's
+        ``bn_sums``), else they are summed here; ``mom_coef`` = (mom, coef, k0,
+        n): input rows [k0, k0 + 4C) are SModel's moment gradients, turned into
+        moment_coef(mom, ., n)'s coefficients in coef instead of written.
+        Returns (dYp, dZ)."""
         H, ldw1 = W1.shape
         O, N = dY.shape
         dY = dY.contiguous()
@@ -830,6 +841,25 @@ class HipBackend:
             arr[i].rows = int(rows)
             arr[i].add = int(bool(add))
         ws, wsb = self._wsargs(getattr(self, "_dims", None))
+        if bn_part is not None or mom_coef is not None:
+            nparts = 0
+            if bn_part is not None:
+                assert bn is not None and bn_part.shape == ((N + 63) // 64, 32), bn_part.shape
+                self._chk(bn_part)
+                nparts = bn_part.shape[0]
+            mom = coef = None
+            k0 = C = n = 0
+            if mom_coef is not None:
+                mom, coef, k0, n = mom_coef
+                self._chk(mom, coef)
+                C = mom.shape[1]
+                assert mom.shape == (4, C, N) and coef.shape == (4, C, N), (mom.shape, coef.shape)
+            _call("pfsgnn_mlp_bwd_pre", dY.data_ptr(), N, _ptr(Yp), _ptr(mu), _ptr(var), _ptr(g),
+                  float(eps), _ptr(dg), _ptr(db), Z.data_ptr(), W1.data_ptr(), ldw1, H, int(K),
+                  W2.data_ptr(), O, None if bn is None else dYp.data_ptr(), dZ.data_ptr(), arr,
+                  len(outs), _ptr(bn_part), nparts, _ptr(mom), _ptr(coef), int(k0), int(C),
+                  int(n), ws, wsb, _stream())
+            return dYp, dZ
         _call("pfsgnn_mlp_bwd", dY.data_ptr(), N, _ptr(Yp), _ptr(mu), _ptr(var), _ptr(g),
               float(eps), _ptr(dg), _ptr(db), Z.data_ptr(), W1.data_ptr(), ldw1, H, int(K),
               W2.data_ptr(), O, None if bn is None else dYp.data_ptr(), dZ.data_ptr(), arr,
@@ -1133,9 +1163,26 @@ class HipBackend:
         return hsum if agg is None else (hsum, A)
 
     def target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False, g_xs=None,
-                   tmask=None):
+                   tmask=None, bn_sums=None):
         """-> (GzT, gxe); with ``g_xs``: g_xs += Wt1[:, :F]^T GzT as well;
-        ``tmask``: the forward's mask (target_fwd), read instead of recomputed."""
+        ``tmask``: the forward's mask (target_fwd), read instead of recomputed.
+        ``bn_sums`` = (Yp, mu, var, eps) of the BatchNorm whose backward reads the
+        finished g_xs next (SModel's, gnn.py:154; complete graphs): its sums come
+        out of the same call -> (GzT, gxe, partials for mlp_bwd's bn_part)."""
+        if bn_sums is not None:
+            assert g_xs is not None and not self._composed(d) and d.sp is None
+            Yp, mu, var, eps = bn_sums
+            self._chk(g_xs, Yp, mu, var)
+            GzT = self.empty(2 * d.F, d.NS)
+            gxe = self.empty(d.F, d.EP) if want_gxe else None
+            part = self.empty((d.NS + 63) // 64, 32)
+            g_hsum = g_hsum.contiguous()
+            ws, wsb = self._wsargs(d)
+            _call("pfsgnn_target_bwd_bn", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
+                  Rs.data_ptr(), Wt1.data_ptr(), g_hsum.data_ptr(), GzT.data_ptr(),
+                  dWt1.data_ptr(), _ptr(gxe), g_xs.data_ptr(), _ptr(tmask), Yp.data_ptr(),
+                  mu.data_ptr(), var.data_ptr(), float(eps), part.data_ptr(), ws, wsb, _stream())
+            return GzT, gxe, part
         if self._composed(d):
             out = self._sp.target_bwd(d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=want_gxe)
             if g_xs is not None:

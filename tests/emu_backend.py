@@ -64,6 +64,7 @@ def _aff(x, sc, sh):
 
 class EmuBackend:
     name = "emu"
+    fiber_bn_sums = True   # target_bwd(bn_sums=...) / mlp_bwd(bn_part=...), as HipBackend
 
     def __init__(self, dtype=torch.float64):
         self.dtype = dtype
@@ -192,11 +193,15 @@ class EmuBackend:
             r["Qt"] = self.lin(Ws, 0, F, xt, b=bs)
         return r
 
-    def mlp_bwd(self, dY, Z, W1, W2, K, bn=None, outs=()):
+    def mlp_bwd(self, dY, Z, W1, W2, K, bn=None, outs=(), bn_part=None, mom_coef=None):
         dYp = dY
         if bn is not None:
             Yp, mu, var, g, eps, dg, db = bn
-            dYp = self.bn_bwd(dY, Yp, mu, var, g, eps, dg, db)
+            sums = None
+            if bn_part is not None:   # pfsgnn_mlp_bwd_pre: the producer's per-block partials
+                O = dY.shape[0]
+                sums = (bn_part[:, :O].sum(0), bn_part[:, 16:16 + O].sum(0))
+            dYp = self.bn_bwd(dY, Yp, mu, var, g, eps, dg, db, sums=sums)
         dZ = (W2.t() @ dYp) * dlrelu(Z)
         if outs:
             dX = W1[:, :K].t() @ dZ
@@ -208,6 +213,10 @@ class EmuBackend:
                     else:
                         t.copy_(dX[r:r + rows])
                 r += rows
+            if mom_coef is not None:   # pfsgnn_mlp_bwd_pre's moment epilogue
+                mom, coef, k0, n = mom_coef
+                C = mom.shape[1]
+                coef.copy_(self.moment_coef(mom, dX[k0:k0 + 4 * C], n))
         return dYp, dZ
 
     def bn_fwd(self, X, gamma, beta, rm, rv, momentum, eps):
@@ -220,11 +229,10 @@ class EmuBackend:
             rv.mul_(1 - momentum).add_(momentum * (var * n / max(n - 1, 1)).to(rv.dtype))
         return Y, mu, var
 
-    def bn_bwd(self, dY, X, mu, var, gamma, eps, dgamma, dbeta):
+    def bn_bwd(self, dY, X, mu, var, gamma, eps, dgamma, dbeta, sums=None):
         inv = 1.0 / torch.sqrt(var + eps)
         xh = (X - mu[:, None]) * inv[:, None]
-        Sg = dY.sum(1)
-        Sgx = (dY * xh).sum(1)
+        Sg, Sgx = sums if sums is not None else (dY.sum(1), (dY * xh).sum(1))
         n = X.shape[1]
         dgamma += Sgx
         dbeta += Sg
@@ -435,10 +443,23 @@ class EmuBackend:
         at = lrelu(zt)
         return _seg(at, cls, d.NT)
 
-    def target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False, g_xs=None):
+    def target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False, g_xs=None,
+                   bn_sums=None):
         out = self._target_bwd(d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=want_gxe)
         if g_xs is not None:
             self.lin_t(Wt1, 0, d.F, out[0], out=g_xs, add=True)
+        if bn_sums is not None:   # pfsgnn_target_bwd_bn: per-64-fiber partials [nb][32]
+            Yp, mu, var, eps = bn_sums
+            O, NS = g_xs.shape
+            xh = (Yp - mu[:, None]) / torch.sqrt(var[:, None] + eps)
+            nb = (NS + 63) // 64
+            part = torch.zeros(nb, 32, dtype=g_xs.dtype, device=g_xs.device)
+            pad = nb * 64 - NS
+            gp = torch.nn.functional.pad(g_xs, (0, pad)).reshape(O, nb, 64)
+            xp = torch.nn.functional.pad(g_xs * xh, (0, pad)).reshape(O, nb, 64)
+            part[:, :O] = gp.sum(2).t()
+            part[:, 16:16 + O] = xp.sum(2).t()
+            return out[0], out[1], part
         return out
 
     def _target_bwd(self, d, y, sc, sh, Rs, Wt1, g_hsum, dWt1, want_gxe=False):
