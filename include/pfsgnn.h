@@ -845,9 +845,13 @@ int pfsgnn_edges_from_canonical(const float* y, const float* sc, const float* sh
  * those, so they are left untouched (matters when weight_decay != 0).
  * The hyper-parameters are the Python floats (doubles) torch's Adam holds:
  * its scalars 1 - beta1, 1 - beta2 and lr / (1 - beta1^t) are formed in
- * double and rounded to fp32 once, as torch does (torch/optim/adam.py
- * _single_tensor_adam), so the update is torch's bit for bit up to the
- * order of the last division (CUDA's addcdiv: value * (m / denom)). */
+ * double and rounded to fp32 once, as torch's capturable=False Adam does
+ * (torch/optim/adam.py _multi_tensor_adam / _single_tensor_adam), so the
+ * update is that one's bit for bit up to the order of the last division
+ * (CUDA's addcdiv: value * (m / denom)).  With step_dev the same double
+ * scalars are formed from the device count (once per block): still the
+ * capturable=False update at that step, not torch's capturable=True one,
+ * whose corrections come from fp32 step tensors. */
 int pfsgnn_adam(float* p, const float* g, float* m, float* v, long long n, int step,
                 const float* step_dev, double lr, double beta1, double beta2, double eps,
                 double weight_decay, const unsigned char* live, void* stream);

@@ -51,6 +51,11 @@
 #ifndef MF_WG_EARLY_READS
 #define MF_WG_EARLY_READS 1
 #endif
+// MF_FWD_PAIRS (default 1): edge_mlp_fwd runs its classes two per body
+// (class_stream_pairs), their MFMA chains interleaved (0: one per body)
+#ifndef MF_FWD_PAIRS
+#define MF_FWD_PAIRS 0
+#endif
 
 namespace {
 
@@ -95,6 +100,60 @@ __global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float*
     r.v[0] = ld_frows<F>(rxe, (uint32_t)c * eoc, ro);
     return r;
   };
+#if MF_FWD_PAIRS && !defined(MF_ABL_NOL1) && !defined(MF_ABL_NOLRELU) && !defined(MF_ABL_NOL2) && \
+    !defined(MF_ABL_NOSTORE) && !defined(MF_ABL_NOSTATS)
+  // two classes per body: both chains interleave; the stores and the Welford
+  // updates stay in class order (bitwise the single-class results)
+  auto finish = [&](floatx4 yo, int c) {
+    if (bfy) {
+      const s16x4 h = hi4(yo);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) yo[r] = bf_f(h[r]);
+    }
+    st_frows<F>(y, EB * F, (uint32_t)c * eoc, ro, g4, fvalid, yo);
+    if (fvalid) {
+      cnt += 1.f;
+      const float rc = __builtin_amdgcn_rcpf(cnt);
+#pragma unroll
+      for (int r = 0; r < GM<F>::RPG; ++r) {
+        const float d = yo[r] - mean[r];
+        mean[r] = fmaf(d, rc, mean[r]);
+        m2[r] = fmaf(d, yo[r] - mean[r], m2[r]);
+      }
+    }
+  };
+  auto one = [&](const Rows<1>& rows, int c) {
+    const floatx4 x[1] = {edge_in<F>(rows.v[0], fm, xsc, scv, shv)};
+    floatx4 z[NT], a[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) z[tt] = ps[tt] + ClassRows<H>::get(ptl, c - c0, tt, g4);
+    L1.apply(x, z);
+    lrelu_act<H>(z, a);
+    floatx4 yo[1] = {bb};
+    L2.apply(a, yo);
+    finish(yo[0], c);
+  };
+  auto two = [&](const Rows<1>& ra, int ca, const Rows<1>& rb, int cb) {
+    const floatx4 xa[1] = {edge_in<F>(ra.v[0], fm, xsc, scv, shv)};
+    const floatx4 xb[1] = {edge_in<F>(rb.v[0], fm, xsc, scv, shv)};
+    floatx4 za[NT], zb[NT], aa[NT], ab[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+      za[tt] = ps[tt] + ClassRows<H>::get(ptl, ca - c0, tt, g4);
+      zb[tt] = ps[tt] + ClassRows<H>::get(ptl, cb - c0, tt, g4);
+    }
+    L1.apply(xa, za);
+    L1.apply(xb, zb);
+    lrelu_act<H>(za, aa);
+    lrelu_act<H>(zb, ab);
+    floatx4 ya[1] = {bb}, yb[1] = {bb};
+    L2.apply(aa, ya);
+    L2.apply(ab, yb);
+    finish(ya[0], ca);
+    finish(yb[0], cb);
+  };
+  class_stream_pairs<MF_DEPTH_FWD>(c0, c1, load, one, two);
+#else
   class_stream<MF_DEPTH_FWD, true>(c0, c1, load, [&](const Rows<1>& rows, int c) {
     const floatx4 x[1] = {edge_in<F>(rows.v[0], fm, xsc, scv, shv)};
     floatx4 z[NT], a[NT];
@@ -143,6 +202,7 @@ __global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float*
       }
     }
   });
+#endif
   // Chan merge over the 16 fibers of the group, then over the 4 waves
 #pragma unroll
   for (int off = 1; off < 16; off <<= 1) {
@@ -362,17 +422,8 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
     r.v[0] = ld_frows<F>(ry, (uint32_t)(WF ? k : wave + 4 * k) * eoc, ro);
     return r;
   };
-  class_stream<MF_DEPTH_FWD>(0, kw, load, [&](const Rows<1>& rows, int k) {
-    const int c = WF ? k : wave + 4 * k;
-    const floatx4 x[1] = {edge_in<F>(rows.v[0], fm, sc, scv, shv)};
-    floatx4 z[NT], a[NT], m[NT];
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt) z[tt] = ClassRows<C>::get(qtl, c, tt, g4);
-    L1.apply(x, z);
-    lrelu_act<C>(z, a);
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt) m[tt] = bias[tt];
-    L2.apply(a, m);
+  // the k-th message folded into the lane's moments (Pebay, count k + 1)
+  auto fold = [&](const floatx4 (&m)[NT], int k) {
     const floatx4 ca = *reinterpret_cast<const floatx4*>(&pco[k][0]);
     const floatx4 cb = *reinterpret_cast<const floatx4*>(&pco[k][4]);
 #pragma unroll
@@ -386,7 +437,42 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
         S2[tt][r] = fmaf(d2, ca[0], m2);
         S1[tt][r] = fmaf(d, ca[3], S1[tt][r]);
       }
+  };
+  auto message = [&](const Rows<1>& rows, int k, floatx4 (&m)[NT]) {
+    const int c = WF ? k : wave + 4 * k;
+    const floatx4 x[1] = {edge_in<F>(rows.v[0], fm, sc, scv, shv)};
+    floatx4 z[NT], a[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) z[tt] = ClassRows<C>::get(qtl, c, tt, g4);
+    L1.apply(x, z);
+    lrelu_act<C>(z, a);
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) m[tt] = bias[tt];
+    L2.apply(a, m);
+  };
+#if MF_FWD_PAIRS
+  // two messages per body (independent chains interleaved), folded in order
+  class_stream_pairs<MF_DEPTH_FWD>(
+      0, kw, load,
+      [&](const Rows<1>& rows, int k) {
+        floatx4 m[NT];
+        message(rows, k, m);
+        fold(m, k);
+      },
+      [&](const Rows<1>& ra, int ka, const Rows<1>& rb, int kb) {
+        floatx4 ma[NT], mb[NT];
+        message(ra, ka, ma);
+        message(rb, kb, mb);
+        fold(ma, ka);
+        fold(mb, kb);
+      });
+#else
+  class_stream<MF_DEPTH_FWD>(0, kw, load, [&](const Rows<1>& rows, int k) {
+    floatx4 m[NT];
+    message(rows, k, m);
+    fold(m, k);
   });
+#endif
   const double invn = 1.0 / (double)NC;
   // the moments' finalize (k_source_finalize's arithmetic) -> mom / hs
   auto emit = [&](int o, double mean, double M2, double M3, double M4) {
@@ -482,12 +568,13 @@ __global__ __launch_bounds__(256) void km_target_fwd(EdgeGeo geo, const float* _
     r.v[0] = ld_frows<F>(ry, (uint32_t)c * eoc, ro);
     return r;
   };
-  class_stream<MF_DEPTH_FWD>(c0, c1, load, [&](const Rows<1>& rows, int c) {
+  auto pre = [&](const Rows<1>& rows, floatx4 (&z)[NT]) {
     const floatx4 x[1] = {edge_in<F>(rows.v[0], fm, sc, scv, shv)};
-    floatx4 z[NT];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) z[tt] = rs[tt];
     L1.apply(x, z);
+  };
+  auto post = [&](const floatx4 (&z)[NT], int c) {
     if (tmask && fvalid)
       (tmask + (uint32_t)c * eoc)[opaque(eo0 + g4)] = (uint8_t)mask_bits<C>(z);
     const int cl = c - cbase;
@@ -505,7 +592,29 @@ __global__ __launch_bounds__(256) void km_target_fwd(EdgeGeo geo, const float* _
       __syncthreads();
       cbase = c + 1;
     }
+  };
+#if MF_FWD_PAIRS
+  class_stream_pairs<MF_DEPTH_FWD>(
+      c0, c1, load,
+      [&](const Rows<1>& rows, int c) {
+        floatx4 z[NT];
+        pre(rows, z);
+        post(z, c);
+      },
+      [&](const Rows<1>& ra, int ca, const Rows<1>& rb, int cb) {
+        floatx4 za[NT], zb[NT];
+        pre(ra, za);
+        pre(rb, zb);
+        post(za, ca);
+        post(zb, cb);
+      });
+#else
+  class_stream<MF_DEPTH_FWD>(c0, c1, load, [&](const Rows<1>& rows, int c) {
+    floatx4 z[NT];
+    pre(rows, z);
+    post(z, c);
   });
+#endif
 }
 
 // ============================================================ TModel bwd

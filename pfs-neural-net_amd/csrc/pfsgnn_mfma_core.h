@@ -856,6 +856,37 @@ __device__ __forceinline__ void class_stream(int c0, int c1, Load load, Body bod
   }
 }
 
+// The LATE ring with the body applied to class PAIRS: body2(rows_a, ca,
+// rows_b, cb) gets two consecutive classes, so that their independent MFMA
+// chains interleave in one instruction stream (a forward kernel's single-class
+// body is one dependent chain per layer); body1 takes an odd last class.
+template <int D, class Load, class Body1, class Body2>
+__device__ __forceinline__ void class_stream_pairs(int c0, int c1, Load load, Body1 body1,
+                                                   Body2 body2) {
+  static_assert(D % 2 == 0, "class pairs need an even ring");
+  using R = decltype(load(c0));
+  R ring[D];
+  if (c1 <= c0) return;
+  const int last = c1 - 1;
+#pragma unroll
+  for (int d = 0; d < D; ++d) ring[d] = load(min(c0 + d, last));
+  int c = c0;
+  for (; c + D <= c1; c += D) {
+#pragma unroll
+    for (int d = 0; d < D; d += 2) {
+      body2(ring[d], c + d, ring[d + 1], c + d + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      ring[d] = load(min(c + d + D, last));
+      ring[d + 1] = load(min(c + d + 1 + D, last));
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < D; d += 2) {
+    if (c + d + 1 < c1) body2(ring[d], c + d, ring[d + 1], c + d + 1);
+    else if (c + d < c1) body1(ring[d], c + d);
+  }
+}
+
 template <int NA>
 struct Rows {
   floatx4 v[NA];

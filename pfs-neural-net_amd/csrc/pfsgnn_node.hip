@@ -2204,12 +2204,18 @@ extern "C" int pfsgnn_moment_coef_seg(const float* mom, const float* gst, int C,
 }
 
 // ---------------------------------------------------------------- adam
-// torch.optim.Adam as the reference runs it on a GPU (torch/optim/adam.py
-// _multi_tensor_adam, the default for device tensors; amsgrad=False): the
-// scalars torch forms in double (1 - beta1, 1 - beta2, lr / bias_correction1,
-// sqrt(bias_correction2)) are formed in double here too and rounded to fp32
-// once, and the element arithmetic is fp32 in the order of torch's device
-// kernels, fused multiply-adds where they contract:
+// torch.optim.Adam as the reference runs it on a GPU with capturable=False
+// (torch/optim/adam.py _multi_tensor_adam, the default for device tensors;
+// _single_tensor_adam forms the same scalars; amsgrad=False): the scalars torch
+// forms from the Python-float step in double (1 - beta1, 1 - beta2,
+// lr / bias_correction1, sqrt(bias_correction2)) are formed in double here too
+// and rounded to fp32 once, and the element arithmetic is fp32 in the order of
+// torch's device kernels, fused multiply-adds where they contract.  The
+// step_dev form (our capturable graphs: the count lives on the device) keeps
+// these double-scalar semantics -- one double pow per block from the device
+// count -- and so matches torch's NON-capturable update at that step; torch's
+// own capturable=True variant forms the corrections from fp32 step tensors
+// and can differ from both in the last ulp.
 //   exp_avg.lerp_(g, 1 - beta1)          m = fma(1 - beta1, g - m, m)
 //   exp_avg_sq.mul_(beta2)               v = v * beta2
 //   .addcmul_(g, g, 1 - beta2)           v = fma(1 - beta2, g * g, v)
@@ -2223,19 +2229,25 @@ struct AdamK {
 __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                        float* __restrict__ v, long long n, AdamK k,
                        const float* __restrict__ step_dev, const unsigned char* __restrict__ live) {
+  float neg_step = k.neg_step, bc2_sqrt = k.bc2_sqrt;
+  if (step_dev) {  // device step count: the corrections once per block
+    __shared__ float sc[2];
+    if (threadIdx.x == 0) {
+      const double st = (double)*step_dev;
+      const double bc1 = 1.0 - pow(k.beta1, st);
+      const double bc2 = 1.0 - pow(k.beta2, st);
+      sc[0] = (float)(-(k.lr / bc1));
+      sc[1] = (float)sqrt(bc2);
+    }
+    __syncthreads();
+    neg_step = sc[0];
+    bc2_sqrt = sc[1];
+  }
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   // a parameter whose .grad the reference leaves None is skipped by
   // torch.optim.Adam: no decay, moments and value untouched
   if (live && !live[i]) return;
-  float neg_step = k.neg_step, bc2_sqrt = k.bc2_sqrt;
-  if (step_dev) {  // capturable form: the step count lives on the device
-    const double st = (double)*step_dev;
-    const double bc1 = 1.0 - pow(k.beta1, st);
-    const double bc2 = 1.0 - pow(k.beta2, st);
-    neg_step = (float)(-(k.lr / bc1));
-    bc2_sqrt = (float)sqrt(bc2);
-  }
   float gi = g[i];
   if (k.wd != 0.f) gi = fmaf(k.wd, p[i], gi);              // grad.add(param, alpha=wd)
   const float mo = m[i];

@@ -27,7 +27,7 @@ from test_gpu_parity import check, ours_step  # noqa: E402
 FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "g16_oracle.npz")
 
 
-@pytest.fixture(params=["mfma", "mfma32", "bf16x6"])
+@pytest.fixture(params=os.environ.get("PFSGNN_G16_PATHS", "mfma,mfma32,bf16x6").split(","))
 def path(request):
     import pfsgnn
     prev = pfsgnn.get_edge_path()
