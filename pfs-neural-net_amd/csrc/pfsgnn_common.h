@@ -435,7 +435,7 @@ static inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // (pfsgnn_set_sync_buffer); without one the callers keep their reduce launch.
 namespace pf {
 unsigned* sync_counters(size_t n);   // n counters, or nullptr
-// a launch's own run of n <= 128 counters (round robin over the buffer, so
+// a launch's own run of n counters (round robin over the buffer, so
 // launches in flight at the same time on different streams never share one),
 // or nullptr without a sync buffer
 unsigned* sync_slot(size_t n);

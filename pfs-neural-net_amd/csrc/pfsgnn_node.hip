@@ -1343,12 +1343,18 @@ size_t g_sync_n = 0;
 }  // namespace
 unsigned* sync_counters(size_t n) { return (g_sync && n <= g_sync_n) ? g_sync : nullptr; }
 unsigned* sync_slot(size_t n) {
-  constexpr size_t SLOT = 128;   // counters per slot (512 bytes)
-  static size_t next = 0;
+  // contiguous runs of 128-counter slots, handed out round robin over the
+  // buffer (slot 0 is sync_counters' own), so that launches in flight at once
+  // never share a counter
+  constexpr size_t SLOT = 128;
+  static size_t next = 1;
   const size_t nslots = g_sync ? g_sync_n / SLOT : 0;
-  if (n > SLOT || nslots < 2) return nullptr;
-  next = next + 1 < nslots ? next + 1 : 1;   // (slot 0: sync_counters' own)
-  return g_sync + next * SLOT;
+  const size_t need = (n + SLOT - 1) / SLOT;
+  if (n == 0 || nslots < 2 || need > (nslots - 1) / 4) return nullptr;
+  if (next + need > nslots) next = 1;
+  unsigned* p = g_sync + next * SLOT;
+  next += need;
+  return p;
 }
 }  // namespace pf
 

@@ -26,8 +26,8 @@ for r in "$@"; do
     bench16) specs+=("${tag}_bench16:300:python bench.py --classes 16 --graphs 256 --steps 50 --alt-paths , --no-cpu-baseline > gpurun_out/${tag}_bench16.json") ;;
     trace) specs+=("${tag}_trace:360:bash tools/trace_only.sh gpurun_out ${tag}") ;;
     pmc) specs+=("${tag}_pmc:600:bash tools/prof_pmc.sh gpurun_out/${tag}_pmc")
-         specs+=("${tag}_pmcsum:120:python tools/pmc_traffic.py gpurun_out/${tag}_pmc ${tag} > gpurun_out/${tag}_traffic.log && cp profiles/${tag}_traffic.json gpurun_out/ && python tools/pmc_summary.py gpurun_out/${tag}_pmc/sq/run_counter_collection.csv > gpurun_out/${tag}_pmc_sq.txt") ;;
-    pmcbwd) specs+=("${tag}_pmcbwd:400:bash tools/pmc_edge_bwd.sh gpurun_out/${tag}_pmcbwd") ;;
+         specs+=("${tag}_pmcsum:120:python tools/pmc_traffic.py gpurun_out/${tag}_pmc ${tag} > gpurun_out/${tag}_traffic.log && cp profiles/${tag}_traffic.json gpurun_out/ && python tools/pmc_summary.py gpurun_out/${tag}_pmc/sq/run_counter_collection.csv > gpurun_out/${tag}_pmc_sq.txt && rm -rf gpurun_out/${tag}_pmc") ;;
+    pmcbwd) specs+=("${tag}_pmcbwd:400:bash tools/pmc_edge_bwd.sh gpurun_out/${tag}_pmcbwd && rm -rf gpurun_out/${tag}_pmcbwd/p1 gpurun_out/${tag}_pmcbwd/p2 gpurun_out/${tag}_pmcbwd/p3") ;;
     precision) specs+=("${tag}_precision:700:PFSGNN_TOL_OUT=gpurun_out/${tag}_precision.json python -u -m pytest -x -v -s --timeout 600 --timeout-method thread tests/test_gpu_precision_table.py -m gpu") ;;
     bias) specs+=("${tag}_bias:400:PFSGNN_BIAS_OUT=gpurun_out/${tag}_bias.json python -u -m pytest -x -v -s --timeout 300 --timeout-method thread tests/test_gpu_bias_noise.py -m gpu") ;;
     sparse) specs+=("${tag}_sparse:400:SPARSE_DENSITIES=1.0,0.3 python tools/sparse_bench.py > gpurun_out/${tag}_sparse.txt") ;;
