@@ -508,6 +508,12 @@ int pfsgnn_affine_rows(const float* X, int C, int N, const float* sc, const floa
 int pfsgnn_bn2_bwd_coef(const float* Sg, const float* Sgx, const float* mu1, const float* var1,
                         const float* gamma, int C, long long n, float eps, float* alpha,
                         float* gam0, float* gam1, float* dgamma, float* dbeta, void* stream);
+/* the same from per-block partials part [nparts][2C] (sum g in 0..C, sum
+ * g*xhat in C..2C; pfsgnn_loss_bwd_bn's bn_part), summed in a fixed order */
+int pfsgnn_bn2_bwd_coef_part(const float* part, int nparts, int C, const float* gamma,
+                             const float* mu1, const float* var1, long long n, float eps,
+                             float* alpha, float* gam0, float* gam1, float* dgamma, float* dbeta,
+                             void* stream);
 /* SModel moment backward (gnn.py:140-153) -> per-fiber coefficients of
  * g_m = C0 + d(C1 + d(C2 + d C3)), d = m - mean.  mom [4][C][NS] =
  * (mean, c2, c3, c4); gst [4C][NS] = dL/d(mean, std, skew, kurt). */
@@ -814,6 +820,21 @@ int pfsgnn_loss_bwd(int G, int NF, int NC, int F, const float* y, const float* s
                     const float* Gf, const float* Gv, const float* tmean, const float* gscale,
                     float* dWd1, float* dbd1, float* dWd2, float* dbd2, float* gxe,
                     void* ws, size_t ws_bytes, void* stream);
+/* the same, also writing the final EdgeModel BatchNorm's backward sums of gxe
+ * (gnn.py:101, the last block's; train.py's objective reads nothing else of
+ * it): bn_part [pfsgnn_loss_bn_parts(G, NF, NC)][2F] per-block partials of
+ * sum gxe and sum gxe * (y - bn_mu1) * bn_inv1, for pfsgnn_bn2_bwd_coef_part --
+ * in place of a pass that reads gxe and y back (pfsgnn_edge_bn_grad_sums) */
+int pfsgnn_loss_bn_parts(int G, int NF, int NC);
+int pfsgnn_loss_bwd_bn(int G, int NF, int NC, int F, const float* y, const float* sc,
+                       const float* sh, const float* Wd1, const float* bd1, const float* Wd2,
+                       const float* bd2, const float* ci, float scale, float sharpness,
+                       float noiselevel, unsigned long long seed,
+                       const unsigned long long* seed_dev, const float* Gn, const float* Gf,
+                       const float* Gv, const float* tmean, const float* gscale, float* dWd1,
+                       float* dbd1, float* dWd2, float* dbd2, float* gxe, const float* bn_mu1,
+                       const float* bn_inv1, float* bn_part, void* ws, size_t ws_bytes,
+                       void* stream);
 
 /* ---------------------------------------------------------------- layout
  * The reference takes an arbitrary edge_index [2][E] (int64, gnn.py:7).  A

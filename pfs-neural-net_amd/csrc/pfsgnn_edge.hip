@@ -2047,6 +2047,18 @@ __global__ __launch_bounds__(256) void k_bn2_coef_part(const float* __restrict__
                                                        float* __restrict__ Sgx) {
   bn2_coef_block(blockIdx.x, part, nb, F, bb, Sg, Sgx);
 }
+extern "C" int pfsgnn_bn2_bwd_coef_part(const float* part, int nparts, int F, const float* gamma,
+                                        const float* mu1, const float* var1, long long n,
+                                        float eps, float* alpha, float* gam0, float* gam1,
+                                        float* dgamma, float* dbeta, void* stream) {
+  PF_REQUIRE(part && nparts > 0 && F > 0 && F <= 16 && gamma && mu1 && var1 && alpha && gam0 &&
+                 gam1 && dgamma && dbeta,
+             "pfsgnn_bn2_bwd_coef_part", "bad arguments");
+  const Bn2Bwd bb{gamma, mu1, var1, n, eps, alpha, gam0, gam1, dgamma, dbeta};
+  hipLaunchKernelGGL(k_bn2_coef_part, dim3(F), dim3(256), 0, as_stream(stream), part, nparts, F,
+                     bb, nullptr, nullptr);
+  return pf::check_launch("pfsgnn_bn2_bwd_coef_part");
+}
 // k_bn2_coef_part (blocks [0, F)) and source_bwd's class-column reduction (the
 // rest) in one launch: independent, both read only source_bwd's partials
 template <int C>

@@ -278,7 +278,7 @@ __global__ __launch_bounds__(256) void k_loss_finalize(
   }
 }
 
-template <int F>
+template <int F, bool BN>
 __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __restrict__ y,
                                                   const float* __restrict__ sc,
                                                   const float* __restrict__ sh,
@@ -296,7 +296,10 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
                                                   const float* __restrict__ gscale,
                                                   float* __restrict__ gxe,
                                                   float* __restrict__ partW,
-                                                  float* __restrict__ partV) {
+                                                  float* __restrict__ partV,
+                                                  const float* __restrict__ bn_mu1,
+                                                  const float* __restrict__ bn_inv1,
+                                                  float* __restrict__ partBN) {
   using WG = WGrad<F, F + 1>;  // g_zd (x) [x, 1] -> dWd1 | dbd1
   EDGE_PROLOGUE
   const uint64_t key = seed_dev ? pf_noise_key(*seed_dev) : key0;
@@ -314,10 +317,18 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
   for (int j = 0; j <= F; ++j) acc[j] = 0.f;
   const float gs = gscale ? gscale[0] : 1.f;
   const float Gf_f = fvalid ? Gf[n] : 0.f;
+  // (partBN) the final edge BatchNorm's backward sums of the gradient this
+  // kernel writes: sum g and sum g * (y - mu1) * inv1 per channel
+  // (1/scale applied once, after the loop)
+  float bsg[F], bsx[F];
+#pragma unroll
+  for (int k = 0; k < F; ++k) bsg[k] = bsx[k] = 0.f;
   Y_PREFETCH_DECL(F)
   CLASS_LOOP_BEGIN
     const float Ti = ci[cn], Gn_c = Gn[cn], Gv_c = Gv[cn], tm_c = tmean[cn];
-    float x[F + 1];
+    float x[F + 1], yr[F];   // (BN: y - mu1, kept for the sums)
+#pragma unroll
+    for (int k = 0; k < F; ++k) yr[k] = BN ? yq[k] - bn_mu1[k] : 0.f;
     Y_TAKE(F, x)
     x[F] = 1.f;
     const float noise = noiselevel * (pf_uniform(key, (uint64_t)eu) - 0.5f);
@@ -349,6 +360,10 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
 #pragma unroll
         for (int j = 0; j < F; ++j) s = fmaf(dwp[j * F + k], gz[j], s);
         gxe[(long long)k * E + e] = s;
+        if (BN) {
+          bsg[k] += s;
+          bsx[k] = fmaf(s, yr[k], bsx[k]);
+        }
       }
     }
     wg.stage(region, gz, x, lane);
@@ -363,6 +378,22 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
 #pragma unroll
     for (int i = 0; i <= F; ++i) val = (i == t) ? acc[i] : val;
     partV[(size_t)bx * (F + 1) + t] = val;
+  }
+  if (BN) {   // [nb][2F]: sum g | sum g xhat, the layout k_bn2_coef_part reads
+    __shared__ float bred[4 * 2 * F];
+    float v[2 * F];
+#pragma unroll
+    for (int k = 0; k < F; ++k) {
+      v[k] = bsg[k];
+      v[F + k] = bsx[k] * bn_inv1[k];
+    }
+    block_sum<2 * F>(v, bred);
+    if (t < 2 * F) {
+      float val = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2 * F; ++i) val = (i == t) ? v[i] : val;
+      partBN[(size_t)bx * 2 * F + t] = val;
+    }
   }
 }
 
@@ -559,15 +590,15 @@ extern "C" int pfsgnn_loss_finalize(int G, int NF, int NC, const float* n_prime,
   return pf::check_launch("pfsgnn_loss_finalize");
 }
 
-extern "C" int pfsgnn_loss_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
-                               const float* sh, const float* Wd1, const float* bd1,
-                               const float* Wd2, const float* bd2, const float* ci, float scale,
-                               float sharpness, float noiselevel, unsigned long long seed,
-                               const unsigned long long* seed_dev, const float* Gn,
-                               const float* Gf, const float* Gv,
-                               const float* tmean, const float* gscale, float* dWd1, float* dbd1,
-                               float* dWd2, float* dbd2, float* gxe, void* ws, size_t ws_bytes,
-                               void* stream) {
+static int loss_bwd_impl(int G, int NF, int NC, int F, const float* y, const float* sc,
+                         const float* sh, const float* Wd1, const float* bd1, const float* Wd2,
+                         const float* bd2, const float* ci, float scale, float sharpness,
+                         float noiselevel, unsigned long long seed,
+                         const unsigned long long* seed_dev, const float* Gn, const float* Gf,
+                         const float* Gv, const float* tmean, const float* gscale, float* dWd1,
+                         float* dbd1, float* dWd2, float* dbd2, float* gxe, const float* bn_mu1,
+                         const float* bn_inv1, float* bn_part, void* ws, size_t ws_bytes,
+                         void* stream) {
   if (int rc = check_dims("pfsgnn_loss_bwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(y && Wd1 && bd1 && Wd2 && bd2 && ci && Gn && Gf && Gv && tmean && dWd1 && dbd1 &&
                  dWd2 && dbd2 && gxe,
@@ -582,9 +613,17 @@ extern "C" int pfsgnn_loss_bwd(int G, int NF, int NC, int F, const float* y, con
   const SoftFloor sf = make_softfloor(sharpness);
   const uint64_t key = pf_noise_key((uint64_t)seed);
   { pf::Timer tm_("loss_bwd", st);
-  DISPATCH_F(F, hipLaunchKernelGGL(k_loss_bwd<FF>, dim3(edge_grid(geo)), dim3(256), 0, st, geo, y, sc,
-                                   sh, Wd1, bd1, Wd2, bd2, ci, scale, sf, noiselevel, key, seed_dev, Gn, Gf,
-                                   Gv, tmean, gscale, gxe, pW, pV));
+  if (bn_part) {
+    DISPATCH_F(F, hipLaunchKernelGGL((k_loss_bwd<FF, true>), dim3(edge_grid(geo)), dim3(256), 0, st,
+                                     geo, y, sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sf, noiselevel,
+                                     key, seed_dev, Gn, Gf, Gv, tmean, gscale, gxe, pW, pV, bn_mu1,
+                                     bn_inv1, bn_part));
+  } else {
+    DISPATCH_F(F, hipLaunchKernelGGL((k_loss_bwd<FF, false>), dim3(edge_grid(geo)), dim3(256), 0, st,
+                                     geo, y, sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sf, noiselevel,
+                                     key, seed_dev, Gn, Gf, Gv, tmean, gscale, gxe, pW, pV, nullptr,
+                                     nullptr, nullptr));
+  }
   tm_.end(); }
   {
     RedDesc rd[4] = {{pW, (int)nb, (size_t)F * (F + 1), F + 1, F, F, dWd1, F, 1, 1.f},
@@ -594,6 +633,40 @@ extern "C" int pfsgnn_loss_bwd(int G, int NF, int NC, int F, const float* y, con
     launch_reduce_multi(rd, 4, st);
   }
   return pf::check_launch("pfsgnn_loss_bwd");
+}
+
+extern "C" int pfsgnn_loss_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
+                               const float* sh, const float* Wd1, const float* bd1,
+                               const float* Wd2, const float* bd2, const float* ci, float scale,
+                               float sharpness, float noiselevel, unsigned long long seed,
+                               const unsigned long long* seed_dev, const float* Gn,
+                               const float* Gf, const float* Gv,
+                               const float* tmean, const float* gscale, float* dWd1, float* dbd1,
+                               float* dWd2, float* dbd2, float* gxe, void* ws, size_t ws_bytes,
+                               void* stream) {
+  return loss_bwd_impl(G, NF, NC, F, y, sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sharpness,
+                       noiselevel, seed, seed_dev, Gn, Gf, Gv, tmean, gscale, dWd1, dbd1, dWd2,
+                       dbd2, gxe, nullptr, nullptr, nullptr, ws, ws_bytes, stream);
+}
+
+extern "C" int pfsgnn_loss_bn_parts(int G, int NF, int NC) {
+  return make_geo(G, NF, NC).nblocks;
+}
+
+extern "C" int pfsgnn_loss_bwd_bn(int G, int NF, int NC, int F, const float* y, const float* sc,
+                                  const float* sh, const float* Wd1, const float* bd1,
+                                  const float* Wd2, const float* bd2, const float* ci,
+                                  float scale, float sharpness, float noiselevel,
+                                  unsigned long long seed, const unsigned long long* seed_dev,
+                                  const float* Gn, const float* Gf, const float* Gv,
+                                  const float* tmean, const float* gscale, float* dWd1,
+                                  float* dbd1, float* dWd2, float* dbd2, float* gxe,
+                                  const float* bn_mu1, const float* bn_inv1, float* bn_part,
+                                  void* ws, size_t ws_bytes, void* stream) {
+  PF_REQUIRE(bn_mu1 && bn_inv1 && bn_part, "pfsgnn_loss_bwd_bn", "null");
+  return loss_bwd_impl(G, NF, NC, F, y, sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sharpness,
+                       noiselevel, seed, seed_dev, Gn, Gf, Gv, tmean, gscale, dWd1, dbd1, dWd2,
+                       dbd2, gxe, bn_mu1, bn_inv1, bn_part, ws, ws_bytes, stream);
 }
 
 extern "C" int pfsgnn_layout_analyze(const int64_t* edge_index, long long E, int G, int NF, int NC,

@@ -713,13 +713,16 @@ class Engine:
                                       "with want_grad=True to differentiate through it)")
         # node weight-gradient reductions are batched over the pass (flushed below)
         be.defer_begin()
+        # the final edge BatchNorm's backward sums, made by the loss backward
+        # when it alone produced g_xe (train._LossFn; any other consumer drops them)
+        g_bn_part = ctx.pop("g_xe_bn_part", None)
         try:
-            self._backward(P, Gr, ctx, d, g_xs_out, g_xt_out, g_xe_out, g_u_out)
+            self._backward(P, Gr, ctx, d, g_xs_out, g_xt_out, g_xe_out, g_u_out, g_bn_part)
         finally:
             self._gu_pend = None
             be.defer_flush()
 
-    def _backward(self, P, Gr, ctx, d, g_xs_out, g_xt_out, g_xe_out, g_u_out):
+    def _backward(self, P, Gr, ctx, d, g_xs_out, g_xt_out, g_xe_out, g_u_out, g_bn_part=None):
         be, F = self.be, self.F
         g_xs, g_xt, g_xe, g_u = g_xs_out, g_xt_out, g_xe_out, g_u_out
         self._gu_pend = []
@@ -792,7 +795,14 @@ class Engine:
             else:
                 g_tot = be.zeros(F, d.EP) if g_xe is None else g_xe
                 bnc = None
-                if self.normed:
+                if self.normed and b == self.B - 1 and g_xe is not None and g_bn_part is not None:
+                    # the loss backward, the only consumer of the final edge
+                    # state, made this BatchNorm's backward sums as it wrote g_xe
+                    key = p + "edge_model.norm."
+                    bnc = be.bn2_bwd_coef_part(g_bn_part, se["mu1"], se["var1"], P[key + "weight"],
+                                               d.E, self.bn_eps, Gr[key + "weight"],
+                                               Gr[key + "bias"])
+                elif self.normed:
                     Sg, Sgx = be.edge_bn_grad_sums(d, g_tot, se["y"], *bnstat)
                     bnc = self.edge_bn_coef(P, Gr, d, p + "edge_model.", se, Sg, Sgx)
             g_xe = self.edge_bwd(P, Gr, d, p + "edge_model.", se, g_tot, bnc, b > 0,
@@ -826,12 +836,29 @@ class Engine:
                     fiber_time=fiber_time, time=tt)
         return loss.sum(), diag, lctx
 
-    def loss_backward(self, P, Gr, lctx, gscale=1.0):
+    def loss_bnstat(self, ectx):
+        """(mu1, inv1) of the final block's edge BatchNorm when the loss
+        backward can make its backward sums (training statistics, complete
+        batch, a backend with loss_bwd(bn=...)); else None."""
+        blocks = ectx.get("blocks") if ectx is not None else None
+        if (not blocks or not self.normed or not ectx.get("training", True)
+                or not getattr(self.be, "loss_bn_part", False)
+                or os.environ.get("PFSGNN_LOSS_BN_SUMS", "1") == "0"):
+            return None
+        se = blocks[-1][0]
+        if "rm" in se or se.get("inv1") is None:
+            return None
+        return se["mu1"], se["inv1"]
+
+    def loss_backward(self, P, Gr, lctx, gscale=1.0, bnstat=None):
+        """-> gxe (canonical [F, E]); with ``bnstat`` (loss_bnstat) -> (gxe,
+        the final edge BatchNorm's backward-sum partials)."""
         be, d = self.be, lctx["d"]
         y, sc, sh = lctx["xe3"]
         dec = [P["decoder_e.0.weight"], P["decoder_e.0.bias"], P["decoder_e.2.weight"], P["decoder_e.2.bias"]]
+        kw = {"bn": bnstat} if bnstat is not None else {}
         return be.loss_bwd(d, y, sc, sh, *dec, lctx["ci"], lctx["scale"], lctx["sharpness"],
                            lctx["noiselevel"], lctx["seed"], lctx["Gn"], lctx["Gf"], lctx["Gv"],
                            lctx["tmean"], gscale,
                            Gr["decoder_e.0.weight"], Gr["decoder_e.0.bias"],
-                           Gr["decoder_e.2.weight"], Gr["decoder_e.2.bias"])
+                           Gr["decoder_e.2.weight"], Gr["decoder_e.2.bias"], **kw)

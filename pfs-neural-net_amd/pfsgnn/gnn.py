@@ -754,6 +754,8 @@ class _EdgesOutFn(torch.autograd.Function):
             gc = gc.contiguous()
             prev = ectx.get("g_xe_canonical")
             ectx["g_xe_canonical"] = gc if prev is None else prev + gc
+            # (a second consumer: the loss's BatchNorm sums no longer cover g_xe)
+            ectx.pop("g_xe_bn_part", None)
         return None, None, None, None, None
 
 

@@ -196,6 +196,7 @@ _SIGS = {
     "pfsgnn_bn_eval_coef": ([P, P, P, P, I, FL, I, P, P, P], I),
     "pfsgnn_affine_rows": ([P, I, I, P, P, P, P], I),
     "pfsgnn_bn2_bwd_coef": ([P, P, P, P, P, I, LL, FL, P, P, P, P, P, P], I),
+    "pfsgnn_bn2_bwd_coef_part": ([P, I, I, P, P, P, LL, FL, P, P, P, P, P, P], I),
     "pfsgnn_moment_coef": ([P, P, I, I, I, P, P], I),
     "pfsgnn_moment_coef_seg": ([P, P, I, I, P, P, P], I),
     "pfsgnn_sparse_layout_ws_bytes": ([LL], SZ),
@@ -223,6 +224,9 @@ _SIGS = {
     "pfsgnn_loss_finalize": ([I, I, I, P, P, P, P, FL, FL, FL, FL, FL, FL, P, P, P, P, P, P, P], I),
     "pfsgnn_loss_bwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, FL, FL, ULL, P, P, P, P, P, P,
                          P, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_loss_bn_parts": ([I, I, I], I),
+    "pfsgnn_loss_bwd_bn": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, FL, FL, ULL, P, P, P, P, P,
+                            P, P, P, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_layout_analyze": ([P, LL, I, I, I, P, P, P, SZ, P], I),
     "pfsgnn_edges_to_canonical": ([P, I, I, I, I, I, P, P, P], I),
     "pfsgnn_edges_from_canonical": ([P, P, P, I, I, I, I, I, P, I, P, P], I),
@@ -419,6 +423,7 @@ class HipBackend:
 
     name = "hip"
     fiber_bn_sums = True     # target_bwd(bn_sums=...) / mlp_bwd(bn_part=...)
+    loss_bn_part = True      # loss_bwd(bn=...) / bn2_bwd_coef_part
 
     def __init__(self, device=None):
         if not torch.cuda.is_available():
@@ -1040,6 +1045,17 @@ class HipBackend:
               Y.data_ptr(), _stream())
         return Y
 
+    def bn2_bwd_coef_part(self, part, mu1, var1, gamma, n, eps, dgamma, dbeta):
+        """bn2_bwd_coef from per-block partials [nparts, 2C] (loss_bwd's ``bn``)."""
+        C = mu1.shape[0]
+        assert part.dim() == 2 and part.shape[1] == 2 * C, part.shape
+        self._chk(part)
+        a, g0, g1 = self.empty(C), self.empty(C), self.empty(C)
+        _call("pfsgnn_bn2_bwd_coef_part", part.data_ptr(), part.shape[0], C, gamma.data_ptr(),
+              mu1.data_ptr(), var1.data_ptr(), int(n), float(eps), a.data_ptr(), g0.data_ptr(),
+              g1.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), _stream())
+        return a, g0, g1
+
     def bn2_bwd_coef(self, Sg, Sgx, mu1, var1, gamma, n, eps, dgamma, dbeta):
         C = mu1.shape[0]
         a, g0, g1 = self.empty(C), self.empty(C), self.empty(C)
@@ -1328,7 +1344,9 @@ class HipBackend:
         return loss, utils, variance, Gn, Gf, Gv
 
     def loss_bwd(self, d, y, sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sharpness, noiselevel, seed,
-                 Gn, Gf, Gv, tmean, gscale, dWd1, dbd1, dWd2, dbd2):
+                 Gn, Gf, Gv, tmean, gscale, dWd1, dbd1, dWd2, dbd2, bn=None):
+        """-> gxe; with ``bn`` = (mu1, inv1) of the final edge BatchNorm ->
+        (gxe, its backward sums' per-block partials) (pfsgnn_loss_bwd_bn)."""
         gxe = self.empty(d.F, d.E)
         gs = None
         if isinstance(gscale, torch.Tensor):
@@ -1337,6 +1355,18 @@ class HipBackend:
             gs = torch.full((1,), float(gscale), dtype=torch.float32, device=self.device)
         ci = ci.contiguous()
         ws, wsb = self._wsargs(d)
+        if bn is not None:
+            mu1, inv1 = bn
+            self._chk(mu1, inv1)
+            part = self.empty(lib().pfsgnn_loss_bn_parts(d.G, d.NF, d.NC), 2 * d.F)
+            _call("pfsgnn_loss_bwd_bn", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
+                  Wd1.data_ptr(), bd1.data_ptr(), Wd2.data_ptr(), bd2.data_ptr(), ci.data_ptr(),
+                  float(scale), float(sharpness), float(noiselevel), *self._seed_args(seed),
+                  Gn.data_ptr(), Gf.data_ptr(), Gv.data_ptr(), tmean.data_ptr(), _ptr(gs),
+                  dWd1.data_ptr(), dbd1.data_ptr(), dWd2.data_ptr(), dbd2.data_ptr(),
+                  gxe.data_ptr(), mu1.data_ptr(), inv1.data_ptr(), part.data_ptr(), ws, wsb,
+                  _stream())
+            return gxe, part
         _call("pfsgnn_loss_bwd", d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
               Wd1.data_ptr(), bd1.data_ptr(), Wd2.data_ptr(), bd2.data_ptr(), ci.data_ptr(),
               float(scale), float(sharpness), float(noiselevel), *self._seed_args(seed),

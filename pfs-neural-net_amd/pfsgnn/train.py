@@ -70,12 +70,22 @@ class _LossFn(torch.autograd.Function):
             return (None,) * 13
         eng = model._engine()
         P, Gr = model._flat_params(), model._recording_grads()
-        gc = eng.loss_backward(P, Gr, lctx, gscale=g_loss)
+        prev = ectx.get("g_xe_canonical")
+        # the final edge BatchNorm's backward sums come out of the same pass when
+        # this loss is the edge state's only consumer so far
+        bns = eng.loss_bnstat(ectx) if prev is None else None
+        out = eng.loss_backward(P, Gr, lctx, gscale=g_loss, bnstat=bns)
+        gc, part = out if bns is not None else (out, None)
         model._mark_live(Gr.used)
         # hand the canonical [F, E] gradient straight to the GNN's backward
         # (gnn._GNNFn.backward); the edge-state token gets none
-        prev = ectx.get("g_xe_canonical")
-        ectx["g_xe_canonical"] = gc if prev is None else prev + gc
+        if prev is None:
+            ectx["g_xe_canonical"] = gc
+            if part is not None:
+                ectx["g_xe_bn_part"] = part
+        else:
+            ectx["g_xe_canonical"] = prev + gc
+            ectx.pop("g_xe_bn_part", None)
         return (None,) * 13
 
 

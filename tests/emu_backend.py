@@ -65,6 +65,7 @@ def _aff(x, sc, sh):
 class EmuBackend:
     name = "emu"
     fiber_bn_sums = True   # target_bwd(bn_sums=...) / mlp_bwd(bn_part=...), as HipBackend
+    loss_bn_part = True    # loss_bwd(bn=...) / bn2_bwd_coef_part, as HipBackend
 
     def __init__(self, dtype=torch.float64):
         self.dtype = dtype
@@ -351,6 +352,11 @@ class EmuBackend:
             rv.mul_(1 - momentum).add_(momentum * (var2 * f).to(rv.dtype))
         return sc, sh, inv1, inv2
 
+    def bn2_bwd_coef_part(self, part, mu1, var1, gamma, n, eps, dgamma, dbeta):
+        C = mu1.shape[0]
+        S = part.sum(0)
+        return self.bn2_bwd_coef(S[:C], S[C:], mu1, var1, gamma, n, eps, dgamma, dbeta)
+
     def bn2_bwd_coef(self, Sg, Sgx, mu1, var1, gamma, n, eps, dgamma, dbeta):
         """Backward of the double BatchNorm as g_y = alpha*g + gam0 + gam1*y."""
         inv1 = 1.0 / torch.sqrt(var1 + eps)
@@ -594,7 +600,19 @@ class EmuBackend:
         return n_prime, fiber_time, tmean, tvar, tt_user
 
     def loss_bwd(self, d, y, sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sharpness, noiselevel, seed,
-                 Gn, Gf, Gv, tmean, gscale, dWd1, dbd1, dWd2, dbd2):
+                 Gn, Gf, Gv, tmean, gscale, dWd1, dbd1, dWd2, dbd2, bn=None):
+        gxe = self._loss_bwd(d, y, sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sharpness, noiselevel,
+                             seed, Gn, Gf, Gv, tmean, gscale, dWd1, dbd1, dWd2, dbd2)
+        if bn is None:
+            return gxe
+        # the HIP kernel's per-block partials, here as two halves of the edges
+        h = d.E // 2
+        parts = [self.edge_bn_grad_sums(d, gxe[:, a:b], y[:, a:b], *bn)
+                 for a, b in ((0, h), (h, d.E))]
+        return gxe, torch.stack([torch.cat(p) for p in parts])
+
+    def _loss_bwd(self, d, y, sc, sh, Wd1, bd1, Wd2, bd2, ci, scale, sharpness, noiselevel, seed,
+                  Gn, Gf, Gv, tmean, gscale, dWd1, dbd1, dWd2, dbd2):
         fib, cls = _edge_index(d, y.device)
         uni = self.noise_uniform(seed, d.E)[_user_index(d, y.device)]
         Gn, Gf, Gv = Gn * gscale, Gf * gscale, Gv * gscale

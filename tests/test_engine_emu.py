@@ -18,7 +18,7 @@ from oracle.ref_train import loss_function as oracle_loss
 from pfsgnn.engine import Engine, param_names
 
 
-def run_pair(G, NF, NC, F=10, B=2, normed=True, sharp=12.0, seed=0):
+def run_pair(G, NF, NC, F=10, B=2, normed=True, sharp=12.0, seed=0, loss_bn=False):
     model, graph = make_problem(G, NF, NC, F=F, B=B, seed=seed, normed=normed)
     ref = copy.deepcopy(model)
     ref.train()
@@ -39,14 +39,22 @@ def run_pair(G, NF, NC, F=10, B=2, normed=True, sharp=12.0, seed=0):
                       to_canonical(graph.x_e, G, NF, NC), graph.x_u.t().contiguous())
     loss_e, diag_e, lctx = eng.loss_forward(P, d, ctx["out"][2], graph.x_t.t().contiguous(), sharp,
                                            1234, pclass=0.1, pfiber=0.1)
-    g_next = eng.loss_backward(P, Gr, lctx)
+    if loss_bn:   # the loss backward also makes the last edge BatchNorm's sums
+        bns = eng.loss_bnstat(ctx)
+        assert bns is not None
+        g_next, ctx["g_xe_bn_part"] = eng.loss_backward(P, Gr, lctx, bnstat=bns)
+    else:
+        g_next = eng.loss_backward(P, Gr, lctx)
     eng.backward(P, Gr, ctx, g_xe_out=g_next)
+    assert "g_xe_bn_part" not in ctx
     return ref, out, loss_o, ctx, loss_e, P, Gr, BN, be
 
 
-@pytest.mark.parametrize("G,NF,NC,B", [(1, 9, 5, 2), (2, 6, 4, 1), (3, 5, 7, 2)])
-def test_engine_matches_oracle_fp64(G, NF, NC, B):
-    ref, out, loss_o, ctx, loss_e, P, Gr, BN, be = run_pair(G, NF, NC, B=B)
+@pytest.mark.parametrize("G,NF,NC,B,loss_bn", [(1, 9, 5, 2, False), (2, 6, 4, 1, False),
+                                               (3, 5, 7, 2, False), (2, 6, 4, 1, True),
+                                               (3, 5, 7, 2, True)])
+def test_engine_matches_oracle_fp64(G, NF, NC, B, loss_bn):
+    ref, out, loss_o, ctx, loss_e, P, Gr, BN, be = run_pair(G, NF, NC, B=B, loss_bn=loss_bn)
     xs, xt, xe3, u = ctx["out"]
     xe = be.edge_apply(ctx["d"], *xe3)
     assert torch.allclose(xs.t(), out.x_s, rtol=1e-9, atol=1e-9)

@@ -270,6 +270,31 @@ def test_loss_ops(hb, G, NF, NC):
         close(gxh, gxe, rtol=2e-3, atol=1e-4, name="loss gxe")
         for a, b, nm in zip(gh, ge, ["dWd1", "dbd1", "dWd2", "dbd2"]):
             close(a, b, rtol=2e-3, atol=1e-4, name=nm)
+        # the BatchNorm-sums arm (pfsgnn_loss_bwd_bn): the same gradient, bitwise,
+        # plus per-block partials of sum g and sum g (y - mu1) inv1
+        mu1, var1 = r(F, gen=gen), r(F, gen=gen).abs() + 0.5
+        inv1 = 1.0 / torch.sqrt(var1 + 1e-5)
+        gh2 = [torch.zeros_like(t) for t in gh]
+        gxh2, part = hb.loss_bwd(d, cuda(y), cuda(sc), cuda(sh),
+                                 *[cuda(a) if isinstance(a, torch.Tensor) else a for a in args],
+                                 fh[3], fh[4], fh[5], oh[2], 1.0, *gh2, bn=(cuda(mu1), cuda(inv1)))
+        assert torch.equal(gxh2, gxh)
+        for a, b in zip(gh2, gh):
+            assert torch.equal(a, b)
+        # (about the HIP gradient itself, so only the sums' rounding is compared)
+        Sg, Sgx = emu.edge_bn_grad_sums(de, cpu(gxh), cpu(cuda(y)), mu1, inv1)
+        S = part.double().sum(0).cpu()
+        mag = cpu(gxh).abs().sum(1).max().item()   # fp32 summation error scale
+        close(S[:F], Sg, rtol=0, atol=1e-5 * mag, name="loss bn Sg")
+        close(S[F:], Sgx, rtol=0, atol=1e-5 * mag * (inv1.max().item() * 6), name="loss bn Sgx")
+        gamma = r(F, gen=gen)
+        dgh, dbh = torch.zeros(F, device="cuda"), torch.zeros(F, device="cuda")
+        dgh2, dbh2 = torch.zeros(F, device="cuda"), torch.zeros(F, device="cuda")
+        a1 = hb.bn2_bwd_coef_part(part, cuda(mu1), cuda(var1), cuda(gamma), d.E, 1e-5, dgh, dbh)
+        a2 = hb.bn2_bwd_coef(part[:, :F].sum(0), part[:, F:].sum(0), cuda(mu1), cuda(var1),
+                             cuda(gamma), d.E, 1e-5, dgh2, dbh2)
+        for x, yv in zip(list(a1) + [dgh, dbh], list(a2) + [dgh2, dbh2]):
+            close(x, yv, rtol=1e-4, atol=1e-6, name="bn2 coef part")
 
 
 def test_noise_bit_exact(hb):
