@@ -64,10 +64,16 @@ static SoftFloor make_softfloor(float sharpness) {
   return s;
 }
 
-// decoder_e + softplus*scale + softfloor + clamp (train.py:42-49, gnn.py:307-312)
+// decoder_e + softplus*scale + softfloor + clamp (train.py:42-49, gnn.py:307-312).
+// LOSS_FAST: sin / cos of 2 pi x as one sincospi of 2x (the reduction is exact
+// in revolutions, no large-argument path) and one reciprocal of T_i per edge
+// for the two divisions by it
+#ifndef LOSS_FAST
+#define LOSS_FAST 1
+#endif
 template <int F>
 struct EdgeLoss {
-  float zd[F], ad[F], pred, time, Ti, xx, th, graw, gal, tt;
+  float zd[F], ad[F], pred, time, Ti, xx, th, graw, gal, tt, cth, invTi;
   __device__ __forceinline__ void run(const float (&x)[F], const float* __restrict__ Wd1,
                                       const float* __restrict__ bd1, const float* __restrict__ Wd2,
                                       const float* __restrict__ bd2, float scale, float Ti_,
@@ -85,9 +91,18 @@ struct EdgeLoss {
     const float sp = pred > 20.f ? pred : log1pf(expf(pred));  // F.softplus (threshold 20)
     time = sp * scale;
     Ti = Ti_;
+#if LOSS_FAST
+    invTi = 1.0f / Ti;
+    xx = fmaf(time, invTi, noise);
+    float sth;
+    sincospif(2.0f * xx, &sth, &cth);
+    graw = xx + sf.inv_pi * (atanf(sf.r * sth / (1.0f - sf.r * cth)) - sf.corr);
+#else
     xx = time / Ti + noise;
     th = sf.two_pi * xx;
-    graw = xx + sf.inv_pi * (atanf(sf.r * sinf(th) / (1.0f - sf.r * cosf(th))) - sf.corr);
+    cth = cosf(th);
+    graw = xx + sf.inv_pi * (atanf(sf.r * sinf(th) / (1.0f - sf.r * cth)) - sf.corr);
+#endif
     gal = graw < 0.f ? 0.f : graw;  // torch.maximum(0, g) (NaN propagates)
     tt = gal * Ti;
   }
@@ -341,9 +356,13 @@ __global__ __launch_bounds__(256) void k_loss_bwd(EdgeGeo geo, const float* __re
     const float g_tt = Gf_f + Gv_c * (L.tt - tm_c);
     const float g_gal = Gn_c + Ti * g_tt;
     const float mask = L.graw > 0.f ? 1.f : (L.graw == 0.f ? 0.5f : 0.f);
-    const float cth = cosf(L.th);
+    const float cth = L.cth;
     const float dsf = 1.f + 2.f * (sf.r * cth - sf.r * sf.r) / (1.f - 2.f * sf.r * cth + sf.r * sf.r);
+#if LOSS_FAST
+    const float g_time = g_gal * mask * dsf * L.invTi;
+#else
     const float g_time = g_gal * mask * dsf / Ti;
+#endif
     const float sig = L.pred > 20.f ? 1.f : 1.f / (1.f + expf(-L.pred));
     const float g_pred = fvalid ? gs * g_time * scale * sig : 0.f;
     float gz[F];
@@ -542,6 +561,15 @@ int check_dims(const char* where, int G, int NF, int NC, int F) {
     case 16: { constexpr int FF = 16; __VA_ARGS__; } break;  \
     default: return pf::fail("dispatch", "unsupported F");   \
   }
+// the loss kernels' grid: class splits to about PFSGNN_LOSS_BLOCKS blocks
+// (A/B knob; default PF_TARGET_BLOCKS)
+EdgeGeo loss_geo(int G, int NF, int NC) {
+  static const int tb = [] {
+    const char* e = getenv("PFSGNN_LOSS_BLOCKS");
+    return e && atoi(e) > 0 ? atoi(e) : PF_TARGET_BLOCKS;
+  }();
+  return make_geo(G, NF, NC, tb);
+}
 }  // namespace
 
 
@@ -554,7 +582,7 @@ extern "C" int pfsgnn_loss_fwd(int G, int NF, int NC, int F, const float* y, con
   if (int rc = check_dims("pfsgnn_loss_fwd", G, NF, NC, F)) return rc;
   PF_REQUIRE(y && Wd1 && bd1 && Wd2 && bd2 && ci && n_prime && fiber_time && tmean && tvar,
              "pfsgnn_loss_fwd", "null");
-  const EdgeGeo geo = make_geo(G, NF, NC);
+  const EdgeGeo geo = loss_geo(G, NF, NC);
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
   float* part = w.take((size_t)G * geo.NFG * NC * 4);
   float* ftp = geo.KS == 1 ? fiber_time : w.take((size_t)geo.KS * geo.NS);
@@ -603,7 +631,7 @@ static int loss_bwd_impl(int G, int NF, int NC, int F, const float* y, const flo
   PF_REQUIRE(y && Wd1 && bd1 && Wd2 && bd2 && ci && Gn && Gf && Gv && tmean && dWd1 && dbd1 &&
                  dWd2 && dbd2 && gxe,
              "pfsgnn_loss_bwd", "null");
-  const EdgeGeo geo = make_geo(G, NF, NC);
+  const EdgeGeo geo = loss_geo(G, NF, NC);
   const size_t nb = geo.nblocks;
   Ws w{reinterpret_cast<char*>(ws), ws_bytes};
   float* pW = w.take(nb * F * (F + 1));
@@ -650,7 +678,7 @@ extern "C" int pfsgnn_loss_bwd(int G, int NF, int NC, int F, const float* y, con
 }
 
 extern "C" int pfsgnn_loss_bn_parts(int G, int NF, int NC) {
-  return make_geo(G, NF, NC).nblocks;
+  return loss_geo(G, NF, NC).nblocks;
 }
 
 extern "C" int pfsgnn_loss_bwd_bn(int G, int NF, int NC, int F, const float* y, const float* sc,
