@@ -1054,20 +1054,34 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
     r.v[2] = ld_frows<F>(rxe, co, ro);
     return r;
   };
-  class_stream<MF_DEPTH_BWD>(c0, c1, load, [&](const Rows<3>& rows, int c) {
-    floatx4 gy[1] = {zero4()};
+  // head: g_y, the edge input and the first Linear's recompute of a class
+  struct Head {
+    floatx4 gy, x, z[NT];
+  };
+  auto head = [&](const Rows<3>& rows, int c) {
+    Head hd;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) hd.gy[r] = 0.f;
 #pragma unroll
     for (int r = 0; r < GM<F>::RPG; ++r)
-      gy[0][r] = fm[r] ? fmaf(g1v[r], rows.v[1][r], fmaf(alv[r], rows.v[0][r], g0v[r])) : 0.f;
+      hd.gy[r] = fm[r] ? fmaf(g1v[r], rows.v[1][r], fmaf(alv[r], rows.v[0][r], g0v[r])) : 0.f;
+    hd.x = edge_in<F>(rows.v[2], fm, xsc, scv, shv);
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) hd.z[tt] = ps[tt] + ClassRows<H>::get(ptl, c - c0, tt, g4);
+    const floatx4 xx[1] = {hd.x};
+    L1.apply(xx, hd.z);
+    return hd;
+  };
+  auto tail = [&](const Head& hd, int c) {
+    floatx4 gy[1] = {hd.gy};
     accB += gy[0];
-    const floatx4 x[1] = {edge_in<F>(rows.v[2], fm, xsc, scv, shv)};
+    const floatx4 x[1] = {hd.x};
     floatx4 z[NT], a[NT], gz[NT];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
-      z[tt] = ps[tt] + ClassRows<H>::get(ptl, c - c0, tt, g4);
+      z[tt] = hd.z[tt];
       gz[tt] = zero4();
     }
-    L1.apply(x, z);
     lrelu_act<H>(z, a);
     const Fr sgy[1] = {split(gy[0])};
     if constexpr (PREC >= 1) L2T.apply(sgy, gz); else L2T.apply(gy, gz);
@@ -1145,7 +1159,14 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
       __syncthreads();
       cbase = c + 1;
     }
-  });
+  };
+  // (the pipeline's second head fits the register file at Fdim <= 10 on the
+  // split-bf16 gradient paths; the fp32 and single-bf16 forms would spill or
+  // lose a wave)
+  if constexpr (MF_BWD_PIPE && F <= 10 && PREC != 0 && PREC != 2)
+    class_stream_pipe<MF_DEPTH_BWD>(c0, c1, load, head, tail);
+  else
+    class_stream<MF_DEPTH_BWD>(c0, c1, load, [&](const Rows<3>& rows, int c) { tail(head(rows, c), c); });
   if (fvalid) {
     float* dst = GzEs + (size_t)ks * H * NS + n;
 #pragma unroll

@@ -15,6 +15,9 @@
 #ifndef MF_DEPTH_BWD
 #define MF_DEPTH_BWD 2   // (backward kernels: more arrays per class, more registers)
 #endif
+#ifndef MF_BWD_PIPE
+#define MF_BWD_PIPE 1    // edge_mlp_bwd: the next class's head before this class's tail (class_stream_pipe)
+#endif
 
 namespace {
 
@@ -853,6 +856,38 @@ __device__ __forceinline__ void class_stream(int c0, int c1, Load load, Body bod
 #pragma unroll
     for (int d = 0; d < D - 1; ++d)
       if (c + d < c1) body(ring[d], c + d);
+  }
+}
+
+// A two-stage software pipeline over the class stream: head(rows, c) (the
+// class's independent first stage: loads consumed, its recompute MFMAs
+// issued) runs for class c + 1 before tail(h, c) finishes class c, so the
+// head's MFMA chains execute under the tail's vector work instead of at the
+// start of the next class's dependency chain.  Loads stay D classes ahead;
+// past the last class the head and the refills repeat the last class
+// (clamped, side-effect free; their results are unused).
+template <int D, class Load, class Head, class Tail>
+__device__ __forceinline__ void class_stream_pipe(int c0, int c1, Load load, Head head, Tail tail) {
+  using R = decltype(load(c0));
+  if (c1 <= c0) return;
+  const int last = c1 - 1;
+  R ring[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) ring[d] = load(min(c0 + d, last));
+  auto h = head(ring[0], c0);
+  ring[0] = load(min(c0 + D, last));
+  for (int c = c0; c < c1; c += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int cc = c + d;
+      if (cc < c1) {
+        const int s = (d + 1) % D;   // ring slot of class cc + 1 (constant once unrolled)
+        const auto hn = head(ring[s], min(cc + 1, last));
+        ring[s] = load(min(cc + 1 + D, last));
+        tail(h, cc);
+        h = hn;
+      }
+    }
   }
 }
 
