@@ -1034,7 +1034,10 @@ static int wgrad_blocks(int N) {
     const int v = e ? std::atoi(e) : 0;
     return v > 0 ? std::min(v, 256) : 256;
   }();
-  int s = (N + 127) / 128;
+  // >= ~400 nodes per block: at the bench shape (38k nodes) 96 blocks, not 256,
+  // -0.035 ms per step (profiles/r05af_wg_blocks_ab.txt); configs[2]'s 613k
+  // nodes keep 256 (96 there: +0.12 ms, r05ag_wg_blocks_configs2_ab.txt)
+  int s = (N + 399) / 400;
   return std::max(1, std::min(s, cap));   // <= 2*RED_SEG: one reduce launch
 }
 
