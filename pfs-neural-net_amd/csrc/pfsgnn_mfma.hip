@@ -64,8 +64,11 @@ namespace {
 // the node parts of the first Linear precomputed per node); Welford partials of
 // y per block for the (double) BatchNorm, finished in the launch by its last
 // blocks when `fin` has counters (mom_finalize, pfsgnn_common.h).
+#ifndef MF_EFWD_MINB
+#define MF_EFWD_MINB 6   // six waves per SIMD (80 VGPRs, no spills at ring depth 3; profiles/r05aj_fwd_occupancy_ab.txt)
+#endif
 template <int F, int PREC>
-__global__ __launch_bounds__(256) void km_edge_mlp_fwd(EdgeGeo geo, const float* __restrict__ xe,
+__global__ __launch_bounds__(256, (F <= 10 && PREC <= 1) ? MF_EFWD_MINB : 1) void km_edge_mlp_fwd(EdgeGeo geo, const float* __restrict__ xe,
                                                        const float* __restrict__ xsc,
                                                        const float* __restrict__ xsh,
                                                        const float* __restrict__ Ps,

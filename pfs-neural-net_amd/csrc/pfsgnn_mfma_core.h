@@ -10,7 +10,7 @@
 #include <type_traits>
 
 #ifndef MF_DEPTH_FWD
-#define MF_DEPTH_FWD 4   // classes of edge rows in flight per wave (forward kernels)
+#define MF_DEPTH_FWD 3   // classes of edge rows in flight per wave (forward kernels; 4 measured the same or slower with six waves of edge_mlp_fwd, r05aj)
 #endif
 #ifndef MF_DEPTH_BWD
 #define MF_DEPTH_BWD 2   // (backward kernels: more arrays per class, more registers)
