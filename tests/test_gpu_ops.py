@@ -53,8 +53,11 @@ def prec(request):
     pfsgnn.set_edge_path(prev)
 
 
+# (+ blocks of one and of two classes: the edge_mlp_bwd class pipeline's
+# shortest streams, class_stream_pipe)
 EDGE_CASES = [(G, NF, NC, 10) for G, NF, NC in GEOMS] + [(2, 50, 16, 8), (1, 33, 64, 8),
-                                                         (2, 50, 16, 16), (1, 70, 24, 16)]
+                                                         (2, 50, 16, 16), (1, 70, 24, 16),
+                                                         (1, 9, 1, 10), (2, 30, 2, 10)]
 
 
 @pytest.mark.parametrize("G,NF,NC,F", EDGE_CASES)
