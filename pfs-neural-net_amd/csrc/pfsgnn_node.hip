@@ -151,10 +151,12 @@ extern "C" const char* pfsgnn_version(void) { return "pfsgnn 0.1 gfx950"; }
 // ---------------------------------------------------------------- reduce
 // Partial reductions out[r][c] (+)= scale * sum_b part[b*plen + r*ldp + c],
 // up to PF_MAX_RED (96) independent ones per launch (blockIdx.z picks one; block
-// layout below).  Long lists (nb > 256) first take an in-place stage: segment s of RED_SEG
+// layout below).  Long lists (nb > 2 RED_SEG) first take an in-place stage: segment s of RED_SEG
 // partials is summed into the segment's first row (each block touches only its
 // own cells; the descriptors of one launch never share cells).
-#define RED_SEG 128
+#ifndef RED_SEG
+#define RED_SEG 256   // (128: +0.01 ms per step, 64: +0.06; profiles/r05as_red_seg_ab.txt)
+#endif
 // a RedDesc as the kernels read it: 40 bytes, so that 96 share one launch's
 // 4 KB of kernel arguments (a backward pass's ~200 weight-gradient
 // reductions in 3 launches, not 5); the add flag rides in cols' top bit
