@@ -56,8 +56,16 @@ PRECISION = {
               + _NODE_X3,
     "bf16x3": "every per-edge contraction (forward, backward recompute, gradient chains, weight "
               "gradients) on bf16 MFMAs with split hi+lo operands (bf16x3, ~2^-16 relative per "
-              "product); fp32 accumulation, edge state and loss (BASELINE configs[4])" + _NODE_X3,
+              "product); fp32 accumulation, edge state and loss" + _NODE_X3,
 }
+# Whether a path meets the fp32 parity bar (tests/test_gpu_parity.py: every
+# tensor within max(16 x the fp32 oracle's error, TOL_REL x its scale) of the
+# fp64 oracle) on EVERY parity case -- the BASELINE configs[4] requirement.
+# bf16x3 passes at the bench geometry (0.28 of the bar, profiles/r05i_precision.json)
+# but misses it on the small parity graphs (up to 8.3x on encoder gradients,
+# profiles/r05a_bf16x3_parity_report.log), so it is not a configs[4] answer.
+MEETS_FP32_TOL = {"mfma": True, "mfma32": True, "valu": True, "bf16x6": True, "bf16x3": False,
+                  "bf16y": False, "bf16m": False, "bf16": False}
 # the arithmetic each edge path computes in (`precision` spells it out): the
 # default path's backward products are split-bf16 (bf16x3), its forward fp32
 DTYPE = {"mfma": "f32 (bf16x3 backward products)", "mfma32": "f32", "valu": "f32",
@@ -83,7 +91,8 @@ def parse():
                     help="launch every kernel from Python instead of replaying a captured HIP graph")
     ap.add_argument("--edge-path", default=os.environ.get("PFSGNN_EDGE_PATH", "mfma"),
                     help="per-edge kernel precision: mfma (default: fp32 forward, bf16x3 "
-                         "gradient chains), mfma32, valu, bf16y, bf16m, bf16, bf16x3 (configs[4])")
+                         "gradient chains), mfma32, valu, bf16x6 (configs[4] at fp32 tolerance), bf16x3, "
+                         "bf16y, bf16m, bf16")
     ap.add_argument("--alt-paths", default="bf16x3,bf16x6,mfma32",
                     help="other edge paths whose step rate is measured after the headline "
                          "one (N=1, graph replay; reported in alt_paths; '' for none)")
@@ -519,8 +528,9 @@ def main():
                            "replayed step (median of 3 alternating rounds of %d replays, HIP "
                            "events on the launch stream)" % reps)
 
-    # ---- the same step on the other edge paths (BASELINE configs[4]: the
-    # bf16x3 contractions; the exact-fp32 one), each captured and replayed like
+    # ---- the same step on the other edge paths (BASELINE configs[4]: the split-
+    # bf16 contractions, each flagged meets_fp32_tolerance or not; the exact-fp32
+    # one), each captured and replayed like
     # the headline path, N=1 only; the parameters keep training (synthetic data)
     alt = {}
     if world == 1 and use_graph and args.alt_paths:
@@ -542,7 +552,7 @@ def main():
             torch.cuda.synchronize()
             el = time.perf_counter() - t0
             alt[pth] = {"value": E * args.steps / el, "ms_per_step": el / args.steps * 1e3,
-                        "precision": PRECISION[pth]}
+                        "precision": PRECISION[pth], "meets_fp32_tolerance": MEETS_FP32_TOL[pth]}
             del g2
         native.set_edge_path(args.edge_path)
 
@@ -649,6 +659,7 @@ def main():
             "dtype": DTYPE[args.edge_path],
             "data": "synthetic",
             "precision": PRECISION[args.edge_path],
+            "meets_fp32_tolerance": MEETS_FP32_TOL[args.edge_path],
             "config": {"workload": f"{G} complete bipartite {NF}x{NC} graphs per GPU, {B} "
                                    f"message-passing blocks, Fdim {FDIM}; full training step "
                                    f"(GNN fwd + train.py loss + bwd + Adam)",

@@ -22,7 +22,10 @@
  *     pfsgnn_workspace_bytes(G, NF, NC, F) bytes;
  *   - `stream` is a hipStream_t; every call is asynchronous on it and
  *     graph-capturable (no allocation, no synchronisation inside);
- *   - return 0 on success, <0 on error (pfsgnn_last_error() has the text).
+ *   - return 0 on success, <0 on error (pfsgnn_last_error() has the text);
+ *   - calls come from ONE host thread at a time (the error text, the
+ *     deferred-reduction queue and the device-wide barrier slots' round robin
+ *     are plain process state), as from the reference's training loop.
  *
  * Supported feature widths F (Fdim): 8, 10, 16.
  */
@@ -52,19 +55,21 @@ size_t pfsgnn_workspace_bytes(int G, int NF, int NC, int F);
  *   PFSGNN_EDGE_BF16Y -- MFMA_F32 arithmetic with the edge state y rounded to
  *       bf16 where it is stored (the numerics of bf16 edge-state storage);
  *   PFSGNN_EDGE_BF16 -- every per-edge contraction a single bf16 MFMA (fp32
- *       accumulation) + bf16 edge state (BASELINE configs[4]; Fdim 10);
+ *       accumulation) + bf16 edge state (Fdim 10; 13-132x over the fp32 bar);
  *   PFSGNN_EDGE_BF16_MFMA -- the bf16 contractions with the fp32 edge state;
  *   PFSGNN_EDGE_BF16X3 -- every per-edge contraction, the forward ones and
  *       their backward recompute included, on v_mfma_f32_16x16x32_bf16 with
  *       split operands (bf16 hi + lo, ~2^-16 relative per product, fp32
- *       accumulation and edge state; BASELINE configs[4] at fp32 tolerance);
+ *       accumulation and edge state; inside the fp32 bar at the bench
+ *       geometry, up to 8.3x over it on small graphs: not a configs[4] answer);
  *   PFSGNN_EDGE_BF16X6 -- the forward contractions and their
  *       backward recompute on v_mfma_f32_16x16x32_bf16 with three-way split
  *       operands (hi + mid + lo, the six products down to ~2^-18: fp32-class
  *       products), the gradient chains and weight gradients as
- *       PFSGNN_EDGE_MFMA.  Built for Fdim 10; at other Fdims this path runs
+ *       PFSGNN_EDGE_MFMA: BASELINE configs[4] at fp32 tolerance (every parity
+ *       case).  Built for Fdim 10; at other Fdims this path runs
  *       the PFSGNN_EDGE_MFMA arithmetic.
- * The fp32-class paths (MFMA, MFMA_F32, VALU) produce the same outputs to the
+ * The fp32-class paths (MFMA, MFMA_F32, VALU, BF16X6) produce the same outputs to the
  * parity tolerance; the bf16 paths' deviation is measured, not bounded
  * (DESIGN.md §Numerics).  Node-level ops, reductions and the loss are shared. */
 #define PFSGNN_EDGE_VALU 0

@@ -64,6 +64,8 @@ int fail(const char* where, const char* what);
 // workspace in floats
 size_t tail_ws_floats(int G, int NC, int F);
 int check_launch(const char* where);
+int fail_pending(const char* where, const char* what);
+int take_pending(int rc);
 // the node level's gradient chains / weight gradients in bf16x3 (pfsgnn_node.hip):
 // env `knob` = 0 / 1 when set, else on for every edge path but the exact-fp32 ones
 bool node_x3(const char* knob);
@@ -401,7 +403,7 @@ struct RedDesc {
   float scale;
 };
 #define PF_MAX_RED 96   // (packed 40-byte descriptors, pfsgnn_node.hip RedDev: 3840 B of kernel arguments)
-void launch_reduce_multi(const RedDesc* d, int n, hipStream_t st);
+int launch_reduce_multi(const RedDesc* d, int n, hipStream_t st);
 // Deferred weight-gradient reductions (pfsgnn_defer_begin / _end): while a
 // pass is open, the edge backward kernels put their weight partials in the
 // caller's arena and queue the reductions; nullptr when closed or full (the
@@ -410,7 +412,7 @@ namespace pf {
 float* defer_take(size_t nfloats);
 void defer_push(const RedDesc* d, int n);
 }  // namespace pf
-void launch_reduce_rows(const float* part, int nb, size_t plen, int ldp, int rows, int cols,
+int launch_reduce_rows(const float* part, int nb, size_t plen, int ldp, int rows, int cols,
                         float* out, int ldo, int add, float scale, hipStream_t st);
 // Column partials [G][NFG][NC][C] -> channel-major node tensor out[C][G*NC].
 void launch_reduce_columns(const float* part, int G, int BPG, int NC, int C, float* out,
@@ -431,6 +433,13 @@ static inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // partial with sc1 loads (agent-scope relaxed atomic loads) after another
 // barrier, and resets the counter for the next launch.  No release fence
 // (no L2 write-back) is needed: no partial is ever held in a non-coherent L2.
+// The winning block's counting lane then runs ONE agent-scope acquire
+// (buffer_inv sc1 + s_waitcnt vmcnt(0)) before the barrier that releases its
+// other waves (round 6): the guide's table row is measured for one workgroup
+// per CU, and edge_mlp_fwd runs several per CU with 84-byte partials that
+// straddle lines written by other blocks, so the hand-off keeps the consumer
+// acquire the guide prescribes outside a row (MI355X_MICROARCH.md, "Consumer,
+// always").  It is paid once per winning block (<= 1 + 64 per launch).
 // The counters live in the library's zero-initialised sync buffer
 // (pfsgnn_set_sync_buffer); without one the callers keep their reduce launch.
 namespace pf {
@@ -448,7 +457,11 @@ __device__ __forceinline__ bool last_arrival(unsigned* cnt, unsigned expect, int
   if (threadIdx.x == 0) {
     const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old + 1u == expect ? 1 : 0;
-    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (last) {
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     *flag = last;
   }
   __syncthreads();

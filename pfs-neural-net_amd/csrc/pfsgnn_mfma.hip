@@ -51,8 +51,9 @@
 #ifndef MF_WG_EARLY_READS
 #define MF_WG_EARLY_READS 1
 #endif
-// MF_FWD_PAIRS (default 1): edge_mlp_fwd runs its classes two per body
-// (class_stream_pairs), their MFMA chains interleaved (0: one per body)
+// MF_FWD_PAIRS (default 0): 1 runs edge_mlp_fwd's classes two per body
+// (class_stream_pairs), their MFMA chains interleaved -- measured slower
+// (profiles/r05p_*pairs_ab.txt, r05q_*pairs_ab.txt), kept for the A/B
 #ifndef MF_FWD_PAIRS
 #define MF_FWD_PAIRS 0
 #endif
@@ -1208,7 +1209,7 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
 // ============================================================ host launchers
 
 // Instantiations: Fdim 8, 10, 16 for the fp32 / bf16x3 precisions (PREC 0, 1);
-// the single-bf16 path (PREC 2, BASELINE configs[4]) at Fdim 10.
+// the single-bf16 path (PREC 2) at Fdim 10.
 #define MF_CASE(FF, PP, K, ...)                                                   \
   case FF * 8 + PP: {                                                             \
     hipLaunchKernelGGL((K<FF, PP>), dim3(edge_grid(geo)), dim3(256), 0, st, geo,    \

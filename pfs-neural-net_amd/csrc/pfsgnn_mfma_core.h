@@ -360,8 +360,8 @@ __device__ __forceinline__ floatx4 mma3g(s16x8 a_hl, const WgB& b, floatx4 c) {
 
 // ------------------------------------------------------------ bf16 layer
 // y (+)= W x with every product a single v_mfma_f32_16x16x16_bf16 on bf16
-// operands (RNE), fp32 accumulation: the "bf16" edge path (BASELINE configs[4],
-// PFSGNN_EDGE_BF16) -- one MFMA per K-tile where LayerF issues GM<K>::RPG.
+// operands (RNE), fp32 accumulation: the "bf16" edge path
+// (PFSGNN_EDGE_BF16) -- one MFMA per K-tile where LayerF issues GM<K>::RPG.
 template <int M, int K>
 struct LayerB1 {
   static constexpr int MT = GM<M>::NT, KT = GM<K>::NT, KP = (KT + 1) / 2;

@@ -847,9 +847,11 @@ constexpr int CT_QBMAX = 64;                // most units per graph (NC <= 64 * 
 constexpr int CT_CLS = 32;                  // most classes per unit (8, 16 or 32: the
                                             // smallest that keeps the units <= 512)
 // Device-wide barrier state: a pool of slots, one 128-byte line each; every
-// launch of a barrier kernel takes its own slot (pf::bar_slot(), round robin
-// on the host), so two such launches never share a word even when they run
-// at the same time on different streams.  Word 0: arrivals | generation << 16
+// launch of a barrier kernel takes the next slot (pf::bar_slot(), round robin
+// on the host), so two such launches share no word as long as fewer than
+// PF_BAR_SLOTS of them are in flight at once (a captured step holds 7).  The
+// round-robin counter is plain host state: launches come from ONE host thread
+// (the library's contract, include/pfsgnn.h).  Word 0: arrivals | generation << 16
 // (default form); words 1, 2: arrivals, generation (fenced form).  A slot is
 // clean between launches: the last arrival of every barrier resets the count.
 constexpr int PF_BAR_SLOTS = 64;

@@ -23,7 +23,24 @@ int fail(const char* where, const char* what) {
   g_err = std::string(where) + ": " + what;
   return -1;
 }
+// A failure found by a void launcher deep in a call (launch_reduce_multi's
+// descriptor limits): recorded here, returned by the C entry point's closing
+// check_launch, so no caller reports success with work silently skipped.
+static bool g_fail_pending = false;
+int fail_pending(const char* where, const char* what) {
+  g_fail_pending = true;
+  return fail(where, what);
+}
+// a caller that returns the launcher's error itself takes it off the pending slot
+int take_pending(int rc) {
+  g_fail_pending = false;
+  return rc;
+}
 int check_launch(const char* where) {
+  if (g_fail_pending) {
+    g_fail_pending = false;
+    return -1;   // (g_err already names the failing launcher)
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     g_err = std::string(where) + ": " + hipGetErrorString(e);
@@ -248,17 +265,22 @@ __global__ __launch_bounds__(256) void k_reduce_seg(RedPack pk) {
   }
 }
 
+static bool red_fits(const RedDesc& a) {
+  return a.rows >= 0 && a.rows <= 65535 && a.cols >= 0 && a.cols <= 32767 &&
+         a.plen * (a.nb > 2 * RED_SEG ? RED_SEG : 1) <= 0xffffffffull;
+}
 static RedDev red_dev(const RedDesc& a) {
-  if (a.rows < 0 || a.rows > 65535 || a.cols < 0 || a.cols > 32767 ||
-      a.plen * (a.nb > 2 * RED_SEG ? RED_SEG : 1) > 0xffffffffull) {
-    pf::fail("launch_reduce_multi", "reduction wider than the packed descriptor");
-    return RedDev{a.part, a.out, 0, 0, 0, 0, 0, 0, 0.f};   // (nothing reduced; error recorded)
-  }
   return RedDev{a.part, a.out, (uint32_t)a.plen, a.nb, a.ldp, a.ldo, (uint16_t)a.rows,
                 (uint16_t)(a.cols | (a.add ? 0x8000 : 0)), a.scale};
 }
 
-void launch_reduce_multi(const RedDesc* d, int n, hipStream_t st) {
+// -> 0, or -1 with nothing launched when a descriptor does not fit the packed
+// 40-byte RedDev (rows > 65535, cols > 32767 or a segment stride past 32 bits);
+// the failure is also left pending for the entry point's check_launch
+int launch_reduce_multi(const RedDesc* d, int n, hipStream_t st) {
+  for (int i = 0; i < n; ++i)
+    if (!red_fits(d[i]))
+      return pf::fail_pending("launch_reduce_multi", "reduction wider than the packed descriptor");
   for (int i0 = 0; i0 < n; i0 += PF_PACK_RED) {
     const int m = std::min(PF_PACK_RED, n - i0);
     RedPack pk{};
@@ -283,12 +305,13 @@ void launch_reduce_multi(const RedDesc* d, int n, hipStream_t st) {
     }
     hipLaunchKernelGGL(k_reduce_rows, dim3(gx, 1, m), dim3(256), 0, st, pk);
   }
+  return 0;
 }
 
-void launch_reduce_rows(const float* part, int nb, size_t plen, int ldp, int rows, int cols,
+int launch_reduce_rows(const float* part, int nb, size_t plen, int ldp, int rows, int cols,
                         float* out, int ldo, int add, float scale, hipStream_t st) {
   RedDesc d{part, nb, plen, ldp, rows, cols, out, ldo, add, scale};
-  launch_reduce_multi(&d, 1, st);
+  return launch_reduce_multi(&d, 1, st);
 }
 
 // per-class sums over the BPG fiber groups of a graph: out[i][g*NC + c] =
@@ -1443,12 +1466,14 @@ static int reduce_batch_desc(const std::vector<RedDesc>& reds, hipStream_t st) {
     bool clash = (int)group.size() == PF_MAX_RED;
     for (const RedDesc& g : group) clash = clash || red_overlap(g, d);
     if (clash) {  // a launch never holds two reductions into the same cells
-      launch_reduce_multi(group.data(), (int)group.size(), st);
+      if (int rc = launch_reduce_multi(group.data(), (int)group.size(), st))
+        return pf::take_pending(rc);
       group.clear();
     }
     group.push_back(d);
   }
-  if (!group.empty()) launch_reduce_multi(group.data(), (int)group.size(), st);
+  if (!group.empty())
+    if (int rc = launch_reduce_multi(group.data(), (int)group.size(), st)) return pf::take_pending(rc);
   return 0;
 }
 

@@ -22,6 +22,9 @@ _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpfsgnn.
 if os.environ.get("PFSGNN_LIB_VARIANT"):
     _LIB_PATH = os.path.join(os.path.dirname(_LIB_PATH),
                              "libpfsgnn_" + os.environ["PFSGNN_LIB_VARIANT"] + ".so")
+# (a test-only build elsewhere in the tree, by path: tests/native/libpfsgnn_lossexact.so)
+if os.environ.get("PFSGNN_LIB_PATH"):
+    _LIB_PATH = os.environ["PFSGNN_LIB_PATH"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -284,7 +287,7 @@ def set_edge_path(path):
     (mfma32 with the edge state rounded to bf16), "bf16m" (single-bf16 MFMA
     contractions), "bf16" (bf16m + bf16 edge state) or "bf16x3" (every
     per-edge contraction on bf16 MFMAs with split hi + lo operands, forward and
-    recompute included; BASELINE configs[4] at fp32 tolerance) or "bf16x6"
+    recompute included; inside the fp32 bar at the bench geometry only) or "bf16x6"
     (the forward contractions and recompute on bf16 MFMAs with three-way split
     operands, fp32-class products; gradient chains as "mfma").  The bf16
     paths are built for Fdim 10; at other Fdims "bf16x6" runs the "mfma"

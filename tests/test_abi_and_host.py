@@ -133,3 +133,18 @@ def test_tensor_cache_keys_on_object_not_address():
         t = torch.zeros(3)
         c.put(t, (), i)
     assert len(c.d) <= 4
+
+
+def test_oversize_reduction_fails_loudly(lib):
+    """a reduction wider than the packed 40-byte descriptor (rows >
+    65535, cols > 32767) is refused with a non-zero return and an error text,
+    before anything is launched (host-only: the pointers are never touched),
+    instead of being skipped with success reported."""
+    import ctypes
+    from pfsgnn import native
+    for rows, cols in ((70000, 4), (4, 40000)):
+        r = native.Red(part=0x1000, nb=3, plen=rows * cols, ldp=cols, rows=rows, cols=cols,
+                       out=0x2000, ldo=cols, add=0, scale=1.0)
+        rc = lib.pfsgnn_reduce_batch(ctypes.byref(r), 1, None)
+        assert rc != 0
+        assert "packed descriptor" in lib.pfsgnn_last_error().decode()

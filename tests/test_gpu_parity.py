@@ -96,10 +96,10 @@ def oracle_step(model, graph, G, NF, NC, seed, sharp, dtype, reverse=False, hook
     return m, out, loss
 
 
-def ours_step(model, graph, G, NF, NC, B, seed, sharp, normed=True):
+def ours_step(model, graph, G, NF, NC, B, seed, sharp, normed=True, F=10):
     import pfsgnn
     from pfsgnn.train import loss_function
-    gnn = pfsgnn.GNN(B=B, Fdim=10, T=12, F_s=1, F_t=2, normed=normed).cuda()
+    gnn = pfsgnn.GNN(B=B, Fdim=F, T=12, F_s=1, F_t=2, normed=normed).cuda()
     gnn.load_state_dict({k: v.float() for k, v in model.state_dict().items()})
     gnn.train()
     data = pfsgnn.BipartiteData(graph.edge_index, graph.x_s.float(), graph.x_t.float(), graph.x_e.float(),
