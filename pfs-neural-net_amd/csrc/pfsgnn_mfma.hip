@@ -57,6 +57,11 @@
 #ifndef MF_FWD_PAIRS
 #define MF_FWD_PAIRS 0
 #endif
+// MF_SB_PACK (default 1): source_bwd's packed weight-gradient tiles at Fdim 10
+// (5 images / 5 outer-product tiles instead of 7 / 6; 0: the unpacked form)
+#ifndef MF_SB_PACK
+#define MF_SB_PACK 1
+#endif
 
 namespace {
 
@@ -738,7 +743,16 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     float* __restrict__ partW2, float* __restrict__ partW1, float* __restrict__ partCol,
     float* __restrict__ partBN, const uint8_t* __restrict__ tmask) {
   constexpr int C = 2 * F, NT = GM<C>::NT;
-  constexpr int NIMG = 3 * NT + 1;          // g_m | a | g_zs | x
+  // PACK (Fdim 10: C = 20 messages, 2 tiles of which the second holds ONE row
+  // per lane group; x has 3 rows per group): the weight-gradient operands are
+  // packed into 5 images instead of 7 -- R1 = g_m tile 0, R2 = g_zs tile 0,
+  // R3 = [g_m tile 1 | g_zs tile 1] (register slots 0, 1), C1 = a tile 0,
+  // C2 = [a tile 1 | x] (slot 0, slots 1-3) -- and dWs2 / dWs1 come out of 5
+  // outer-product tiles (R1 C1, R1 C2, R2 C2, R3 C1, R3 C2) instead of 6, the
+  // padding rows of one operand carrying the other's live rows.  Every output
+  // element is the same products in the same order: bitwise the unpacked sums.
+  constexpr bool PACK = MF_SB_PACK && NT == 2 && GM<C>::nreg(1) == 1 && GM<F>::NT == 1 && GM<F>::RPG == 3;
+  constexpr int NIMG = PACK ? 5 : 3 * NT + 1;   // g_m | a | g_zs | x (packed: R1 R2 R3 C1 C2)
   constexpr int SCR = C * (C + 1) > C * F ? C * (C + 1) : C * F;
   using WI = WgImg<PREC>;
   MF_GEO
@@ -754,6 +768,13 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   short* im_a = img + NT * WI::U;
   short* im_gz = im_a + NT * WI::U;
   short* im_x = im_gz + NT * WI::U;
+  // (PACK) R1 R2 R3 C1 C2
+  short* im_r1 = img;
+  short* im_r2 = img + WI::U;
+  short* im_r3 = img + 2 * WI::U;
+  short* im_c1 = img + 3 * WI::U;
+  short* im_c2 = img + 4 * WI::U;
+  (void)im_r1; (void)im_r2; (void)im_r3; (void)im_c1; (void)im_c2;
   const long long CNS = (long long)C * NS;
   const bool tpart = Rs != nullptr;
 
@@ -790,6 +811,7 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   const Rsrc ry = rsrc(y, EB * F), rgn = rsrc(g_next, EB * F), rtm = rsrc(tmask, EB);
 
   floatx4 accW2[NT * NT], accW1[NT], accB[NT];
+  floatx4 accP[5];   // (PACK) R1 C1, R1 C2, R2 C2, R3 C1, R3 C2
 #pragma unroll
   for (int tt = 0; tt < NT; ++tt) {
     accW1[tt] = zero4();
@@ -797,7 +819,10 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
 #pragma unroll
     for (int nb = 0; nb < NT; ++nb) accW2[tt * NT + nb] = zero4();
   }
+#pragma unroll
+  for (int i = 0; i < 5; ++i) accP[i] = zero4();
   floatx4 sg = zero4(), sgx = zero4();
+  const s16x8 ones = ones_reg();
   __syncthreads();   // qtl, ghl
 
   int cbase = c0;
@@ -850,24 +875,41 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     // the weight-gradient images are written first: their LDS latency hides
     // behind the input-gradient chains below
     lds_order();
+    [[maybe_unused]] floatx4 r3v, c2v;
+    if constexpr (PACK) {
+      r3v = floatx4{gm[1][0], gz[1][0], 0.f, 0.f};
+      c2v = floatx4{as[1][0], x[0][0], x[0][1], x[0][2]};
+      const Fr sr3 = {s16x4{sgm[1].h[0], sgz[1].h[0], 0, 0}, s16x4{sgm[1].l[0], sgz[1].l[0], 0, 0}};
+      WI::put(im_r1, lane, gm[0], sgm[0]);
+      WI::put(im_r2, lane, gz[0], sgz[0]);
+      WI::put(im_r3, lane, r3v, sr3);
+      WI::put(im_c1, lane, as[0], split(as[0]));
+      WI::put(im_c2, lane, c2v, split(c2v));
+    } else {
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) {
-      WI::put(im_gm + tt * WI::U, lane, gm[tt], sgm[tt]);
-      WI::put(im_a + tt * WI::U, lane, as[tt], split(as[tt]));
-      WI::put(im_gz + tt * WI::U, lane, gz[tt], sgz[tt]);
+      for (int tt = 0; tt < NT; ++tt) {
+        WI::put(im_gm + tt * WI::U, lane, gm[tt], sgm[tt]);
+        WI::put(im_a + tt * WI::U, lane, as[tt], split(as[tt]));
+        WI::put(im_gz + tt * WI::U, lane, gz[tt], sgz[tt]);
+      }
+      WI::put(im_x, lane, x[0], split(x[0]));
     }
-    WI::put(im_x, lane, x[0], split(x[0]));
     lds_order();
 #if MF_WG_EARLY_READS
     // the transposed image reads go out now, ahead of the input-gradient
     // chains (as in km_edge_mlp_bwd)
-    const typename WI::R rx = WI::rd(im_x, lane);
-    typename WI::R ra[NT], rgm[NT], rgz[NT];
+    typename WI::R rx, ra[NT], rgm[NT], rgz[NT], rp[5];
+    if constexpr (PACK) {
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) {
-      ra[tt] = WI::rd(im_a + tt * WI::U, lane);
-      rgm[tt] = WI::rd(im_gm + tt * WI::U, lane);
-      rgz[tt] = WI::rd(im_gz + tt * WI::U, lane);
+      for (int i = 0; i < 5; ++i) rp[i] = WI::rd(img + i * WI::U, lane);
+    } else {
+      rx = WI::rd(im_x, lane);
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) {
+        ra[tt] = WI::rd(im_a + tt * WI::U, lane);
+        rgm[tt] = WI::rd(im_gm + tt * WI::U, lane);
+        rgz[tt] = WI::rd(im_gz + tt * WI::U, lane);
+      }
     }
     lds_order();
 #endif
@@ -910,6 +952,32 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     }
     // ---- weight gradients (edge = K) through the transposed images
     lds_order();
+    const int cl = c - cbase;
+    if constexpr (PACK) {
+#if MF_WG_EARLY_READS
+      const typename WI::TB tc1 = WI::B(rp[3]), tc2 = WI::B(rp[4]);
+      const typename WI::TA t1 = WI::A(rp[0]), t2 = WI::A(rp[1]), t3 = WI::A(rp[2]);
+#else
+      const typename WI::TB tc1 = WI::B(im_c1, lane), tc2 = WI::B(im_c2, lane);
+      const typename WI::TA t1 = WI::A(im_r1, lane), t2 = WI::A(im_r2, lane), t3 = WI::A(im_r3, lane);
+#endif
+      accP[0] = WI::mma(t1, tc1, accP[0]);
+      accP[1] = WI::mma(t1, tc2, accP[1]);
+      accP[2] = WI::mma(t2, tc2, accP[2]);
+      accP[3] = WI::mma(t3, tc1, accP[3]);
+      accP[4] = WI::mma(t3, tc2, accP[4]);
+      // per-class sums of g_zs: R2's rows, and R3's register slot 1
+      const floatx4 cs2 = WI::colsum(t2, gz[0], ones), cs3 = WI::colsum(t3, r3v, ones);
+      if (j16 == WI::CS_LANE) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int h = GM<C>::mrow(0, 4 * g4 + r);
+          if (h >= 0) colbuf[(cl * 4 + wave) * C + h] = cs2[r];
+        }
+        const int h1 = GM<C>::row(g4, 4);
+        if (h1 >= 0) colbuf[(cl * 4 + wave) * C + h1] = cs3[1];
+      }
+    } else {
 #if MF_WG_EARLY_READS
     const typename WI::TB tx = WI::B(rx);
     typename WI::TB ta[NT];
@@ -921,7 +989,6 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
 #pragma unroll
     for (int nb = 0; nb < NT; ++nb) ta[nb] = WI::B(im_a + nb * WI::U, lane);
 #endif
-    const int cl = c - cbase;
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
 #if MF_WG_EARLY_READS
@@ -945,6 +1012,7 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
         }
       }
     }
+    }
     if (cl == COL_CH - 1 || c == c1 - 1) {
       __syncthreads();
       col_flush<C>(colbuf, cl + 1, cbase, partCol, colbase);
@@ -952,10 +1020,23 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
       cbase = c + 1;
     }
   });
-  block_partial(accW2, scratch, C * (C + 1), [&](int a, int s, int jj) {
-    const int o = GM<C>::mrow(a / NT, s), h = GM<C>::mrow(a % NT, jj);
-    return (o >= 0 && h >= 0) ? o * (C + 1) + h : -1;
-  }, partW2 + (size_t)bx * C * (C + 1));
+  if constexpr (PACK) {
+    // dWs2 [o][h]: R1 C1 (tile-0 rows x tile-0 columns), R1 C2 and R3 C1 (slot 0
+    // of C2 / R3: the tile-1 row of each lane group), R3 C2 (both slot 0)
+    block_partial(accP, scratch, C * (C + 1), [&](int a, int s, int jj) {
+      int o = -1, h = -1;
+      if (a == 0) { o = GM<C>::mrow(0, s); h = GM<C>::mrow(0, jj); }
+      if (a == 1 && (jj & 3) == 0) { o = GM<C>::mrow(0, s); h = GM<C>::row(jj >> 2, 4); }
+      if (a == 3 && (s & 3) == 0) { o = GM<C>::row(s >> 2, 4); h = GM<C>::mrow(0, jj); }
+      if (a == 4 && (s & 3) == 0 && (jj & 3) == 0) { o = GM<C>::row(s >> 2, 4); h = GM<C>::row(jj >> 2, 4); }
+      return (o >= 0 && h >= 0) ? o * (C + 1) + h : -1;
+    }, partW2 + (size_t)bx * C * (C + 1));
+  } else {
+    block_partial(accW2, scratch, C * (C + 1), [&](int a, int s, int jj) {
+      const int o = GM<C>::mrow(a / NT, s), h = GM<C>::mrow(a % NT, jj);
+      return (o >= 0 && h >= 0) ? o * (C + 1) + h : -1;
+    }, partW2 + (size_t)bx * C * (C + 1));
+  }
   // dbs2 (exact fp32 sums of g_m: a bias gradient cancels to ~0 through the
   // BatchNorm that follows) -> column C of the same partial
   {
@@ -973,10 +1054,22 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
       partW2[(size_t)bx * C * (C + 1) + t * (C + 1) + C] =
           ((scratch[t] + scratch[C + t]) + scratch[2 * C + t]) + scratch[3 * C + t];
   }
-  block_partial(accW1, scratch, C * F, [&](int a, int s, int jj) {
-    const int h = GM<C>::mrow(a, s), k = GM<F>::mrow(0, jj);
-    return (h >= 0 && k >= 0) ? h * F + k : -1;
-  }, partW1 + (size_t)bx * C * F);
+  if constexpr (PACK) {
+    // dWs1 [h][k]: R2 C2 (tile-0 rows x C2's slots 1-3 = x) and R3 C2 (R3's
+    // slot 1 = the tile-1 row of g_zs)
+    block_partial(accP, scratch, C * F, [&](int a, int s, int jj) {
+      int h = -1, k = -1;
+      if ((jj & 3) != 0) k = GM<F>::row(jj >> 2, (jj & 3) - 1);
+      if (a == 2) h = GM<C>::mrow(0, s);
+      if (a == 4 && (s & 3) == 1) h = GM<C>::row(s >> 2, 4);
+      return (h >= 0 && k >= 0) ? h * F + k : -1;
+    }, partW1 + (size_t)bx * C * F);
+  } else {
+    block_partial(accW1, scratch, C * F, [&](int a, int s, int jj) {
+      const int h = GM<C>::mrow(a, s), k = GM<F>::mrow(0, jj);
+      return (h >= 0 && k >= 0) ? h * F + k : -1;
+    }, partW1 + (size_t)bx * C * F);
+  }
   if (mu1) {
     __syncthreads();
 #pragma unroll
@@ -1047,6 +1140,7 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
   const floatx4 scv = ld_fconst<F>(xsc, g4, 1.f), shv = ld_fconst<F>(xsh, g4, 0.f);
   MF_FMASK(F)
   const Rsrc rgt = rsrc(g_tot, EB * F), ry = rsrc(y, EB * F), rxe = rsrc(xe, EB * F);
+  const s16x8 ones = ones_reg();
   __syncthreads();   // ptl
 
   int cbase = c0;
@@ -1148,7 +1242,7 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
       const typename WI::TA tgz = WI::A(im_gz + tt * WI::U, lane);
 #endif
       accW1[tt] = WI::mma(tgz, tx, accW1[tt]);
-      const floatx4 cs = WI::colsum(tgz, gz[tt]);
+      const floatx4 cs = WI::colsum(tgz, gz[tt], ones);
       if (j16 == WI::CS_LANE) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {

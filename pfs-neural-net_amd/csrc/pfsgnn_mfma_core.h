@@ -351,6 +351,12 @@ __device__ __forceinline__ s16x8 ones8() {
   const short o = (short)0x3F80;
   return s16x8{o, o, o, o, o, o, o, o};
 }
+// ones8() as an opaque register value: made once, kept in its 4 VGPRs
+__device__ __forceinline__ s16x8 ones_reg() {
+  s16x8 o = ones8();
+  asm volatile("" : "+v"(o));
+  return o;
+}
 struct WgB {
   s16x8 lh, h0;   // [Bl | Bh], [Bh | 0]
 };
@@ -537,6 +543,11 @@ struct WgImg {
   static __device__ __forceinline__ floatx4 colsum(const TA& a, const floatx4&) {
     return mf8(a, ones8(), zero4());
   }
+  // the same with the ones operand held by the caller (ones_reg(), made once
+  // before the class loop: hipcc otherwise rebuilds it with 3 v_mov per use)
+  static __device__ __forceinline__ floatx4 colsum(const TA& a, const floatx4&, const s16x8& ones) {
+    return mf8(a, ones, zero4());
+  }
 };
 template <>
 struct WgImg<0> {
@@ -561,6 +572,9 @@ struct WgImg<0> {
     return mmaf(a, b, c);
   }
   static __device__ __forceinline__ floatx4 colsum(const TA&, const floatx4& v);
+  static __device__ __forceinline__ floatx4 colsum(const TA& a, const floatx4& v, const s16x8&) {
+    return colsum(a, v);
+  }
 };
 
 // ------------------------------------------------------------ memory

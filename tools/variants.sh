@@ -6,7 +6,7 @@
 set -e
 cd "$(dirname "$0")/../pfs-neural-net_amd"
 make -j8 >/dev/null
-objs=$(ls build/*.o | grep -v -e pfsgnn_mfma.o -e pfsgnn_sliced.o -e var_)
+objs=$(ls build/*.o | grep -v -e pfsgnn_mfma.o -e pfsgnn_sliced.o -e var_ -e pfsgnn_loss_exact.o)
 flags=$(make -s -f - print <<'MK'
 include Makefile
 print:
