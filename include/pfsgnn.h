@@ -664,6 +664,20 @@ int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, const float*
                       const float* sh, const float* Qt, const float* Ws1, const float* Ws2,
                       const float* bs2, float* mom, float* hs, void* ws, size_t ws_bytes,
                       void* stream);
+/* The SModel message cache (round 6): bytes of the per-edge messages m
+ * [2F][E] (gnn.py:136, the output of node_mlp_1) that the current edge path
+ * keeps between the forward and the backward -- complete graphs on the
+ * PFSGNN_EDGE_MFMA / _MFMA_F32 paths when PFSGNN_MSG=1 is set, 0 otherwise
+ * (the backward then recomputes them; the default: the forward's extra
+ * 80 B per edge of writes cost more than the recompute).  pfsgnn_source_fwd_msg = pfsgnn_source_fwd + writes the
+ * messages to `msg` (this many bytes); pfsgnn_source_bwd(_bn)_msg read them in
+ * place of recomputing node_mlp_1's second Linear -- bit for bit the values the
+ * forward computed, so results equal the recomputing calls'. */
+size_t pfsgnn_msg_bytes(int G, int NF, int NC, int F);
+int pfsgnn_source_fwd_msg(int G, int NF, int NC, int F, const float* y, const float* sc,
+                          const float* sh, const float* Qt, const float* Ws1, const float* Ws2,
+                          const float* bs2, float* mom, float* hs, float* msg, void* ws,
+                          size_t ws_bytes, void* stream);
 /* TModel per-edge message, summed per class before its second Linear
  * (gnn.py:188-190): hsum[:,c] = sum_f lrelu(Rs[:,f] + Wt1[:,F:2F] x); with Wt2
  * (optional, [2F][2F]) also that Linear in the same call's reduction epilogue:
@@ -725,6 +739,26 @@ int pfsgnn_source_bwd_bn(int G, int NF, int NC, int F, const float* y, const flo
                          float* dWs1, float* dWs2, float* dbs2, float* alpha, float* gam0,
                          float* gam1, float* dgamma, float* dbeta, float* g_xt,
                          const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream);
+/* pfsgnn_source_bwd / _bn with the forward's message cache (pfsgnn_msg_bytes) */
+int pfsgnn_source_bwd_msg(int G, int NF, int NC, int F, const float* y, const float* sc,
+                          const float* sh, const float* Qt, const float* Ws1, const float* Ws2,
+                          const float* bs2, const float* mean, const float* coef,
+                          const float* Rs, const float* Wt1, const float* g_hsum,
+                          const float* g_next, const float* mu1, const float* inv1,
+                          float* g_tot, float* GzS, float* dWs1, float* dWs2, float* dbs2,
+                          float* Sg, float* Sgx, float* g_xt, const unsigned char* tmask,
+                          const float* msg, void* ws, size_t ws_bytes, void* stream);
+int pfsgnn_source_bwd_bn_msg(int G, int NF, int NC, int F, const float* y, const float* sc,
+                             const float* sh, const float* Qt, const float* Ws1,
+                             const float* Ws2, const float* bs2, const float* mean,
+                             const float* coef, const float* Rs, const float* Wt1,
+                             const float* g_hsum, const float* g_next, const float* mu1,
+                             const float* inv1, const float* var1, const float* gamma,
+                             long long n, float eps, float* g_tot, float* GzS, float* dWs1,
+                             float* dWs2, float* dbs2, float* alpha, float* gam0, float* gam1,
+                             float* dgamma, float* dbeta, float* g_xt,
+                             const unsigned char* tmask, const float* msg, void* ws,
+                             size_t ws_bytes, void* stream);
 /* Sg = sum g, Sgx = sum g*(y-mu1)*inv1 (standalone EdgeModel backward). */
 int pfsgnn_edge_bn_grad_sums(int G, int NF, int NC, int F, const float* g, const float* y,
                              const float* mu1, const float* inv1, float* Sg, float* Sgx,

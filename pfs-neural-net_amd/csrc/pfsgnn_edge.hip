@@ -1745,11 +1745,37 @@ extern "C" int pfsgnn_sl_edge_mlp_fwd_bn(const pfsgnn_sliced_t* sl, int G, int N
                            ws_bytes, stream);
 }
 
+// The SModel message cache (pfsgnn_msg_bytes): available on the complete-graph
+// fiber-tile path of the mfma / mfma32 edge arithmetic, while its [2F][E]
+// fp32 rows fit 32-bit byte offsets; OFF by default, PFSGNN_MSG=1 turns it on.
+// Measured at the bench geometry (profiles/r06e_msg_cache_ab.txt): source_bwd
+// 2.36 -> 2.21 ms per step, but source_fwd 1.19 -> 1.75 ms (the 80 B per edge
+// of message writes, 392 MB per launch), the step +0.8 ms.
+static bool msg_on() {
+  static const bool on = [] {
+    const char* e = getenv("PFSGNN_MSG");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+static size_t msg_bytes(int G, int NF, int NC, int F) {
+  if (G <= 0 || NF <= 0 || NC <= 0 || (F != 8 && F != 10 && F != 16)) return 0;
+  if (!msg_on() || !use_mfma() || NC > 256 || !sfwd_tiles()) return 0;
+  const int p = mf_prec(1, F);
+  if (p != 0 && p != 1) return 0;
+  const unsigned long long b = (unsigned long long)G * NF * NC * 2 * F * 4;
+  return b < (1ull << 32) ? (size_t)b : 0;
+}
+extern "C" size_t pfsgnn_msg_bytes(int G, int NF, int NC, int F) { return msg_bytes(G, NF, NC, F); }
+
 static int source_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
                            const float* y, const float* sc, const float* sh, const float* Qt,
                            const float* Ws1, const float* Ws2, const float* bs2, float* mom,
-                           float* hs, void* ws, size_t ws_bytes, void* stream) {
+                           float* hs, void* ws, size_t ws_bytes, void* stream,
+                           float* msg = nullptr) {
   if (int rc = check_dims("pfsgnn_source_fwd", G, NF, NC, F)) return rc;
+  PF_REQUIRE(!msg || (!sl && msg_bytes(G, NF, NC, F) > 0), "pfsgnn_source_fwd_msg",
+             "the message cache is not kept on this path (pfsgnn_msg_bytes is 0)");
   if (int rc = check_sliced("pfsgnn_source_fwd", sl, NC, F)) return rc;
   PF_REQUIRE(y && Qt && Ws1 && Ws2 && bs2 && mom && hs, "pfsgnn_source_fwd", "null");
   const EdgeGeo geo = geo_of(G, NF, NC, sl);
@@ -1769,7 +1795,7 @@ static int source_fwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
   if (use_mfma() && NC <= 256 && sfwd_tiles()) {
     pf::Timer tm_("source_fwd", st);
     for (int rep = 0, nrep = 1 + pf::repeats("source_fwd"); rep < nrep; ++rep)
-      if (int rc = pfm::source_fwd_tiles(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs,
+      if (int rc = pfm::source_fwd_tiles(geo, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs, msg,
                                          mf_prec(1, F), sfwd_wave_nc(), st))
         return rc;
     tm_.end();
@@ -1803,6 +1829,16 @@ extern "C" int pfsgnn_source_fwd(int G, int NF, int NC, int F, const float* y, c
                                  void* ws, size_t ws_bytes, void* stream) {
   return source_fwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs, ws,
                          ws_bytes, stream);
+}
+
+extern "C" int pfsgnn_source_fwd_msg(int G, int NF, int NC, int F, const float* y,
+                                     const float* sc, const float* sh, const float* Qt,
+                                     const float* Ws1, const float* Ws2, const float* bs2,
+                                     float* mom, float* hs, float* msg, void* ws, size_t ws_bytes,
+                                     void* stream) {
+  PF_REQUIRE(msg, "pfsgnn_source_fwd_msg", "null message cache");
+  return source_fwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mom, hs, ws,
+                         ws_bytes, stream, msg);
 }
 
 extern "C" int pfsgnn_sl_source_fwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
@@ -2081,7 +2117,8 @@ static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
                            const float* g_hsum, const float* g_next, const float* mu1,
                            const float* inv1, float* g_tot, float* GzS, float* dWs1, float* dWs2,
                            float* dbs2, float* Sg, float* Sgx, const Bn2Bwd* bb, float* g_xt,
-                           const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream);
+                           const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream,
+                           const float* msg = nullptr);
 
 extern "C" int pfsgnn_source_bwd(int G, int NF, int NC, int F, const float* y, const float* sc,
                                  const float* sh, const float* Qt, const float* Ws1,
@@ -2114,6 +2151,39 @@ extern "C" int pfsgnn_source_bwd_bn(int G, int NF, int NC, int F, const float* y
   return source_bwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
                          g_hsum, g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, nullptr, nullptr,
                          &bb, g_xt, tmask, ws, ws_bytes, stream);
+}
+
+extern "C" int pfsgnn_source_bwd_msg(int G, int NF, int NC, int F, const float* y,
+                                     const float* sc, const float* sh, const float* Qt,
+                                     const float* Ws1, const float* Ws2, const float* bs2,
+                                     const float* mean, const float* coef, const float* Rs,
+                                     const float* Wt1, const float* g_hsum, const float* g_next,
+                                     const float* mu1, const float* inv1, float* g_tot, float* GzS,
+                                     float* dWs1, float* dWs2, float* dbs2, float* Sg, float* Sgx,
+                                     float* g_xt, const unsigned char* tmask, const float* msg,
+                                     void* ws, size_t ws_bytes, void* stream) {
+  PF_REQUIRE(msg, "pfsgnn_source_bwd_msg", "null message cache");
+  return source_bwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+                         g_hsum, g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, Sg, Sgx, nullptr,
+                         g_xt, tmask, ws, ws_bytes, stream, msg);
+}
+
+extern "C" int pfsgnn_source_bwd_bn_msg(
+    int G, int NF, int NC, int F, const float* y, const float* sc, const float* sh,
+    const float* Qt, const float* Ws1, const float* Ws2, const float* bs2, const float* mean,
+    const float* coef, const float* Rs, const float* Wt1, const float* g_hsum,
+    const float* g_next, const float* mu1, const float* inv1, const float* var1,
+    const float* gamma, long long n, float eps, float* g_tot, float* GzS, float* dWs1,
+    float* dWs2, float* dbs2, float* alpha, float* gam0, float* gam1, float* dgamma,
+    float* dbeta, float* g_xt, const unsigned char* tmask, const float* msg, void* ws,
+    size_t ws_bytes, void* stream) {
+  PF_REQUIRE(msg && mu1 && inv1 && var1 && gamma && n > 0 && alpha && gam0 && gam1 && dgamma &&
+                 dbeta,
+             "pfsgnn_source_bwd_bn_msg", "null");
+  const Bn2Bwd bb{gamma, mu1, var1, n, eps, alpha, gam0, gam1, dgamma, dbeta};
+  return source_bwd_impl(nullptr, G, NF, NC, F, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+                         g_hsum, g_next, mu1, inv1, g_tot, GzS, dWs1, dWs2, dbs2, nullptr, nullptr,
+                         &bb, g_xt, tmask, ws, ws_bytes, stream, msg);
 }
 
 extern "C" int pfsgnn_sl_source_bwd(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int F,
@@ -2156,8 +2226,11 @@ static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
                            const float* g_hsum, const float* g_next, const float* mu1,
                            const float* inv1, float* g_tot, float* GzS, float* dWs1, float* dWs2,
                            float* dbs2, float* Sg, float* Sgx, const Bn2Bwd* bb, float* g_xt,
-                           const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream) {
+                           const unsigned char* tmask, void* ws, size_t ws_bytes, void* stream,
+                           const float* msg) {
   if (int rc = check_dims("pfsgnn_source_bwd", G, NF, NC, F)) return rc;
+  PF_REQUIRE(!msg || (!sl && msg_bytes(G, NF, NC, F) > 0), "pfsgnn_source_bwd_msg",
+             "the message cache is not kept on this path (pfsgnn_msg_bytes is 0)");
   if (int rc = check_sliced("pfsgnn_source_bwd", sl, NC, F)) return rc;
   PF_REQUIRE(y && Qt && Ws1 && Ws2 && bs2 && mean && coef && g_tot && GzS && dWs1 && dWs2 && dbs2,
              "pfsgnn_source_bwd", "null");
@@ -2191,7 +2264,7 @@ static int source_bwd_impl(const pfsgnn_sliced_t* sl, int G, int NF, int NC, int
       return rc;
   } else if (mfma) {
     for (int rep = 0, nrep = 1 + pf::repeats("source_bwd"); rep < nrep; ++rep)
-      if (int rc = pfm::source_bwd(geo, F, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+      if (int rc = pfm::source_bwd(geo, F, msg, y, sc, sh, QtT, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
                                    ghT, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask,
                                    mf_prec(1, F), st))
         return rc;

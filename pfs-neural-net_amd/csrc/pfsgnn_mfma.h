@@ -31,7 +31,7 @@ int source_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const
 // per 16 fibers over all classes (no in-block merge)
 int source_fwd_tiles(const EdgeGeo& geo, int F, const float* y, const float* sc,
                      const float* sh, const float* QtS, const float* Ws1, const float* Ws2,
-                     const float* bs2, float* mom, float* hs, int prec, int wave_nc,
+                     const float* bs2, float* mom, float* hs, float* msg, int prec, int wave_nc,
                      hipStream_t st);
 // TModel's LeakyReLU mask (pfsgnn_mfma.hip mask_bits): target_fwd writes it
 // when `tmask` is non-null (4 bytes per edge), target_bwd / source_bwd read
@@ -42,11 +42,13 @@ int target_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const
 int target_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
                const float* Rs, const float* Wt1, const float* ghS, float* gz, float* gxe,
                float* part, const uint8_t* tmask, int prec, hipStream_t st);
-int source_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
-               const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
-               const float* mean, const float* coef, const float* Rs, const float* Wt1,
-               const float* ghS, const float* g_next, const float* mu1, const float* inv1,
-               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN,
+// msg (optional): the SModel message cache [2F][E] written by source_fwd_tiles
+// (mfma / mfma32 paths): read in place of recomputing the message's second layer
+int source_bwd(const EdgeGeo& geo, int F, const float* msg, const float* y, const float* sc,
+               const float* sh, const float* QtS, const float* Ws1, const float* Ws2,
+               const float* bs2, const float* mean, const float* coef, const float* Rs,
+               const float* Wt1, const float* ghS, const float* g_next, const float* mu1,
+               const float* inv1, float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN,
                const uint8_t* tmask, int prec, hipStream_t st);
 int edge_mlp_bwd(const EdgeGeo& geo, int F, const float* g_tot, const float* alpha,
                  const float* gam0, const float* gam1, const float* y, const float* xe,

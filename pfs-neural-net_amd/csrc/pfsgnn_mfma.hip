@@ -62,6 +62,12 @@
 #ifndef MF_SB_PACK
 #define MF_SB_PACK 1
 #endif
+// MF_WG4 (default 1): the backward kernels' split-bf16 weight gradients as the
+// four products of the split operands (WgImg::mma4: B read twice, no [Bh | 0]
+// operand assembled); 0: the three-product form (mma3g)
+#ifndef MF_WG4
+#define MF_WG4 1
+#endif
 
 namespace {
 
@@ -373,7 +379,7 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
     EdgeGeo geo, int ntiles, const float* __restrict__ y, const float* __restrict__ sc,
     const float* __restrict__ sh, const float* __restrict__ QtS, const float* __restrict__ Ws1,
     const float* __restrict__ Ws2, const float* __restrict__ bs2, float* __restrict__ mom,
-    float* __restrict__ hs) {
+    float* __restrict__ hs, float* __restrict__ msg) {
   constexpr int C = 2 * F, NT = GM<C>::NT, CP = ClassRows<C>::CP;
   constexpr int MS = 4 * 4 * NT;   // a lane's merge state: 4 sums x NT tiles x 4 slots
   const int t = threadIdx.x, lane = t & 63;
@@ -405,6 +411,7 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
   for (int tt = 0; tt < NT; ++tt) bias[tt] = ld_vec<C>(bs2, tt, g4);
   const floatx4 scv = ld_fconst<F>(sc, g4, 1.f), shv = ld_fconst<F>(sh, g4, 0.f);
   MF_FMASK(F)
+  const RowOff<C> roC(eo0, RB, g4);   // (the message cache's rows)
   const Rsrc ry = rsrc(y, EB * F);
   floatx4 S1[NT], S2[NT], S3[NT], S4[NT];
 #pragma unroll
@@ -458,6 +465,7 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) m[tt] = bias[tt];
     L2.apply(a, m);
+    if (msg) st_rows_nt<C>(msg, (uint32_t)c * eoc, roC, g4, fvalid, m);
   };
 #if MF_FWD_PAIRS
   // two messages per body (independent chains interleaved), folded in order
@@ -732,9 +740,14 @@ __global__ __launch_bounds__(256) void km_target_bwd(EdgeGeo geo, const float* _
 // message MLP; plus TModel's recomputed input gradient, the downstream edge
 // gradient and the edge BatchNorm's two gradient sums.  dWs2 += g_m a^T,
 // dbs2 += g_m, dWs1[:, F:2F] += g_zs x^T, per-class sums of g_zs (-> g_Qt).
-template <int F, int PREC, bool TM>
+// MSG: the forward's messages m are read from the message cache (msg, written
+// by km_source_fwd_ft) instead of recomputed through node_mlp_1's second Linear:
+// the same values bit for bit (the cache holds what the forward computed), 10
+// fewer fp32 MFMAs per class and that layer's dependent chain off the class's
+// critical path, for 80 B per edge written in the forward and read here.
+template <int F, int PREC, bool TM, bool MSG = false>
 __global__ __launch_bounds__(256, 2) void km_source_bwd(
-    EdgeGeo geo, const float* __restrict__ y, const float* __restrict__ sc,
+    EdgeGeo geo, const float* __restrict__ msg, const float* __restrict__ y, const float* __restrict__ sc,
     const float* __restrict__ sh, const float* __restrict__ QtS, const float* __restrict__ Ws1,
     const float* __restrict__ Ws2, const float* __restrict__ bs2, const float* __restrict__ mean,
     const float* __restrict__ coef, const float* __restrict__ Rs, const float* __restrict__ Wt1,
@@ -787,7 +800,7 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   rec_bind(L1t, recw + R1 + R2);
   L1s.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
   if constexpr (!TM) L1t.load([&](int h, int k) { return tpart ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
-  L2.load([&](int o, int h) { return Ws2[o * C + h]; }, lane);
+  if constexpr (!MSG) L2.load([&](int o, int h) { return Ws2[o * C + h]; }, lane);
   // gradient chains: exact fp32, bf16x3 or bf16 by PREC
   GradLayer<PREC, C, C> L2T;
   L2T.load([&](int h, int o) { return Ws2[o * C + h]; }, lane);
@@ -809,6 +822,8 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   const floatx4 m1v = ld_fconst<F>(mu1, g4, 0.f), i1v = ld_fconst<F>(inv1, g4, 0.f);
   MF_FMASK(F)
   const Rsrc ry = rsrc(y, EB * F), rgn = rsrc(g_next, EB * F), rtm = rsrc(tmask, EB);
+  [[maybe_unused]] const Rsrc rms = rsrc(msg, EB * C);
+  [[maybe_unused]] const RowOff<C> roC(eo0, RB, g4);
 
   floatx4 accW2[NT * NT], accW1[NT], accB[NT];
   floatx4 accP[5];   // (PACK) R1 C1, R1 C2, R2 C2, R3 C1, R3 C2
@@ -826,26 +841,38 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   __syncthreads();   // qtl, ghl
 
   int cbase = c0;
+  using RowsT = Rows<MSG ? 2 + NT : 2>;
   auto load = [&](int c) {
-    Rows<2> r;
+    RowsT r;
     const uint32_t co = (uint32_t)c * eoc;
     r.v[0] = ld_frows<F>(ry, co, ro);
     r.v[1] = g_next ? ld_frows<F>(rgn, co, ro) : zero4();
     if constexpr (TM) r.m = tpart ? __builtin_amdgcn_raw_buffer_load_b8(rtm, eo0 + g4, co, 0) : 0u;
+    if constexpr (MSG) {
+      floatx4 mv[NT];
+      ld_rows_nt<C>(rms, co, roC, mv);
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) r.v[2 + tt] = mv[tt];
+    }
     return r;
   };
-  class_stream<MF_DEPTH_BWD>(c0, c1, load, [&](const Rows<2>& rows, int c) {
+  class_stream<MF_DEPTH_BWD>(c0, c1, load, [&](const RowsT& rows, int c) {
     const floatx4 yr = rows.v[0], gnr = rows.v[1];
     const floatx4 x[1] = {edge_in<F>(yr, fm, sc, scv, shv)};
-    // ---- forward recompute: z_s, a_s, m
+    // ---- forward recompute: z_s, a_s, m (MSG: m from the message cache)
     floatx4 zs[NT], as[NT], m[NT];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) zs[tt] = ClassRows<C>::get(qtl, c - c0, tt, g4);
     L1s.apply(x, zs);
     lrelu_act<C>(zs, as);
+    if constexpr (MSG) {
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) m[tt] = bias[tt];
-    L2.apply(as, m);
+      for (int tt = 0; tt < NT; ++tt) m[tt] = rows.v[2 + tt];
+    } else {
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) m[tt] = bias[tt];
+      L2.apply(as, m);
+    }
     floatx4 gm[NT];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
@@ -898,10 +925,15 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
 #if MF_WG_EARLY_READS
     // the transposed image reads go out now, ahead of the input-gradient
     // chains (as in km_edge_mlp_bwd)
-    typename WI::R rx, ra[NT], rgm[NT], rgz[NT], rp[5];
+    typename WI::R rx, ra[NT], rgm[NT], rgz[NT], rp[5], rq[2];
     if constexpr (PACK) {
 #pragma unroll
       for (int i = 0; i < 5; ++i) rp[i] = WI::rd(img + i * WI::U, lane);
+#if MF_WG4
+      lds_order();   // (the B images' second reads: mma4)
+      rq[0] = WI::rd(im_c1, lane);
+      rq[1] = WI::rd(im_c2, lane);
+#endif
     } else {
       rx = WI::rd(im_x, lane);
 #pragma unroll
@@ -954,18 +986,25 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
     lds_order();
     const int cl = c - cbase;
     if constexpr (PACK) {
-#if MF_WG_EARLY_READS
-      const typename WI::TB tc1 = WI::B(rp[3]), tc2 = WI::B(rp[4]);
-      const typename WI::TA t1 = WI::A(rp[0]), t2 = WI::A(rp[1]), t3 = WI::A(rp[2]);
-#else
-      const typename WI::TB tc1 = WI::B(im_c1, lane), tc2 = WI::B(im_c2, lane);
-      const typename WI::TA t1 = WI::A(im_r1, lane), t2 = WI::A(im_r2, lane), t3 = WI::A(im_r3, lane);
+#if !MF_WG_EARLY_READS
+#error "source_bwd's packed tiles read their images early (MF_WG_EARLY_READS)"
 #endif
+      const typename WI::TA t1 = WI::A(rp[0]), t2 = WI::A(rp[1]), t3 = WI::A(rp[2]);
+#if MF_WG4
+      const typename WI::TB4 tc1 = WI::B4(rp[3], rq[0]), tc2 = WI::B4(rp[4], rq[1]);
+      accP[0] = WI::mma4(t1, tc1, accP[0]);
+      accP[1] = WI::mma4(t1, tc2, accP[1]);
+      accP[2] = WI::mma4(t2, tc2, accP[2]);
+      accP[3] = WI::mma4(t3, tc1, accP[3]);
+      accP[4] = WI::mma4(t3, tc2, accP[4]);
+#else
+      const typename WI::TB tc1 = WI::B(rp[3]), tc2 = WI::B(rp[4]);
       accP[0] = WI::mma(t1, tc1, accP[0]);
       accP[1] = WI::mma(t1, tc2, accP[1]);
       accP[2] = WI::mma(t2, tc2, accP[2]);
       accP[3] = WI::mma(t3, tc1, accP[3]);
       accP[4] = WI::mma(t3, tc2, accP[4]);
+#endif
       // per-class sums of g_zs: R2's rows, and R3's register slot 1
       const floatx4 cs2 = WI::colsum(t2, gz[0], ones), cs3 = WI::colsum(t3, r3v, ones);
       if (j16 == WI::CS_LANE) {
@@ -1208,12 +1247,18 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
     // above): their latency hides behind that chain instead of stalling the
     // weight-gradient MFMAs one read group at a time
     const typename WI::R rgy = WI::rd(im_gy, lane), rx = WI::rd(im_x, lane);
-    typename WI::R ra[NT], rgz[NT];
+    typename WI::R ra[NT], rgz[NT], ra2[NT], rx2;
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) {
       ra[tt] = WI::rd(im_a + tt * WI::U, lane);
       rgz[tt] = WI::rd(im_gz + tt * WI::U, lane);
     }
+#if MF_WG4
+    lds_order();   // (the B images' second reads: mma4)
+    rx2 = WI::rd(im_x, lane);
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) ra2[tt] = WI::rd(im_a + tt * WI::U, lane);
+#endif
     lds_order();
 #endif
     if (gxe) {
@@ -1221,7 +1266,12 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
       if constexpr (PREC >= 1) L1T.apply(sgz, gx); else L1T.apply(gz, gx);
       st_frows<F>(gxe, EB * F, (uint32_t)c * eoc, ro, g4, fvalid, gx[0]);
     }
-#if MF_WG_EARLY_READS
+#if MF_WG_EARLY_READS && MF_WG4
+    const typename WI::TA tgy = WI::A(rgy);
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) accW2[tt] = WI::mma4(tgy, WI::B4(ra[tt], ra2[tt]), accW2[tt]);
+    const typename WI::TB4 tx = WI::B4(rx, rx2);
+#elif MF_WG_EARLY_READS
     const typename WI::TA tgy = WI::A(rgy);
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) accW2[tt] = WI::mma(tgy, WI::B(ra[tt]), accW2[tt]);
@@ -1241,7 +1291,11 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
 #else
       const typename WI::TA tgz = WI::A(im_gz + tt * WI::U, lane);
 #endif
+#if MF_WG_EARLY_READS && MF_WG4
+      accW1[tt] = WI::mma4(tgz, tx, accW1[tt]);
+#else
       accW1[tt] = WI::mma(tgz, tx, accW1[tt]);
+#endif
       const floatx4 cs = WI::colsum(tgz, gz[tt], ones);
       if (j16 == WI::CS_LANE) {
 #pragma unroll
@@ -1360,7 +1414,7 @@ int source_fwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const
 
 int source_fwd_tiles(const EdgeGeo& geo, int F, const float* y, const float* sc,
                      const float* sh, const float* QtS, const float* Ws1, const float* Ws2,
-                     const float* bs2, float* mom, float* hs, int prec, int wave_nc,
+                     const float* bs2, float* mom, float* hs, float* msg, int prec, int wave_nc,
                      hipStream_t st) {
   if (geo.NC > MF_SFT_MAXNC) return pf::fail("pfsgnn mfma", "source_fwd_tiles: NC > 256");
   const bool wf = geo.NC <= std::min(wave_nc, MF_SFT_WAVE_MAXNC);
@@ -1371,10 +1425,10 @@ int source_fwd_tiles(const EdgeGeo& geo, int F, const float* y, const float* sc,
   case FF * 8 + PP:                                                                        \
     if (wf)                                                                                \
       hipLaunchKernelGGL((km_source_fwd_ft<FF, PP, true>), dim3(nb), dim3(256), 0, st, geo, \
-                         ntiles, y, sc, sh, QtS, Ws1, Ws2, bs2, mom, hs);                  \
+                         ntiles, y, sc, sh, QtS, Ws1, Ws2, bs2, mom, hs, msg);             \
     else                                                                                   \
       hipLaunchKernelGGL((km_source_fwd_ft<FF, PP, false>), dim3(nb), dim3(256), 0, st, geo, \
-                         ntiles, y, sc, sh, QtS, Ws1, Ws2, bs2, mom, hs);                  \
+                         ntiles, y, sc, sh, QtS, Ws1, Ws2, bs2, mom, hs, msg);             \
     break;
   switch (F * 8 + fwd_prec(prec)) {
     MF_SFT(8, 0) MF_SFT(8, 1) MF_SFT(10, 0) MF_SFT(10, 1) MF_SFT(10, 2) MF_SFT(10, 3)
@@ -1403,17 +1457,41 @@ int target_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const
   return 0;
 }
 
-int source_bwd(const EdgeGeo& geo, int F, const float* y, const float* sc, const float* sh,
-               const float* QtS, const float* Ws1, const float* Ws2, const float* bs2,
-               const float* mean, const float* coef, const float* Rs, const float* Wt1,
-               const float* ghS, const float* g_next, const float* mu1, const float* inv1,
-               float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN,
+int source_bwd(const EdgeGeo& geo, int F, const float* msg, const float* y, const float* sc,
+               const float* sh, const float* QtS, const float* Ws1, const float* Ws2,
+               const float* bs2, const float* mean, const float* coef, const float* Rs,
+               const float* Wt1, const float* ghS, const float* g_next, const float* mu1,
+               const float* inv1, float* g_tot, float* pW2, float* pW1, float* pCol, float* pBN,
                const uint8_t* tmask, int prec, hipStream_t st) {
+  if (msg) {   // the message cache: Fdim 8 / 10 / 16 on the mfma / mfma32 paths
+    if (prec != 0 && prec != 1) return pf::fail("pfsgnn mfma", "message cache: mfma paths only");
+#define MF_CASE_MSG(FF, PP, TT)                                                                  \
+  case FF * 8 + PP:                                                                             \
+    hipLaunchKernelGGL((km_source_bwd<FF, PP, TT, true>), dim3(edge_grid(geo)), dim3(256), 0, st, \
+                       geo, msg, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1, ghS, g_next, \
+                       mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask);                           \
+    break;
+    if (tmask && Rs) {
+      switch (F * 8 + prec) {
+        MF_CASE_MSG(8, 0, true) MF_CASE_MSG(8, 1, true) MF_CASE_MSG(10, 0, true)
+        MF_CASE_MSG(10, 1, true) MF_CASE_MSG(16, 0, true) MF_CASE_MSG(16, 1, true)
+        default: return pf::fail("pfsgnn mfma", "unsupported Fdim for this edge path");
+      }
+    } else {
+      switch (F * 8 + prec) {
+        MF_CASE_MSG(8, 0, false) MF_CASE_MSG(8, 1, false) MF_CASE_MSG(10, 0, false)
+        MF_CASE_MSG(10, 1, false) MF_CASE_MSG(16, 0, false) MF_CASE_MSG(16, 1, false)
+        default: return pf::fail("pfsgnn mfma", "unsupported Fdim for this edge path");
+      }
+    }
+#undef MF_CASE_MSG
+    return 0;
+  }
   if (tmask && Rs) {
-    MF_LAUNCH3(F, prec, true, km_source_bwd, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+    MF_LAUNCH3(F, prec, true, km_source_bwd, nullptr, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
                ghS, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask)
   } else {
-    MF_LAUNCH3(F, prec, false, km_source_bwd, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
+    MF_LAUNCH3(F, prec, false, km_source_bwd, nullptr, y, sc, sh, QtS, Ws1, Ws2, bs2, mean, coef, Rs, Wt1,
                ghS, g_next, mu1, inv1, g_tot, pW2, pW1, pCol, pBN, tmask)
   }
   return 0;

@@ -540,6 +540,19 @@ struct WgImg {
   static __device__ __forceinline__ floatx4 mma(const TA& a, const TB& b, floatx4 c) {
     return mma3g(a, b, c);
   }
+  // The four-product form (MF_WG4): B as [Bh | Bl] and [Bl | Bh], read from the
+  // image twice (r, r2: the second pass behind an lds_order(), so that hipcc
+  // keeps two loads instead of one load and register copies), against
+  // A = [Ah | Al]: Ah Bh + Al Bl, then Ah Bl + Al Bh -- the exact product of the
+  // split operands, with no [Bh | 0] operand to assemble (3 v_mov per B
+  // operand and use in the three-product form).
+  using TB4 = WgB;   // {lh = [Bl | Bh], h0 = [Bh | Bl]}
+  static __device__ __forceinline__ TB4 B4(const R& r, const R& r2) {
+    return {cat8(r2.l, r2.h), cat8(r.h, r.l)};
+  }
+  static __device__ __forceinline__ floatx4 mma4(const TA& a, const TB4& b, floatx4 c) {
+    return mf8(a, b.h0, mf8(a, b.lh, c));
+  }
   static __device__ __forceinline__ floatx4 colsum(const TA& a, const floatx4&) {
     return mf8(a, ones8(), zero4());
   }
@@ -569,6 +582,11 @@ struct WgImg<0> {
   }
   static __device__ __forceinline__ TB B(const short* im, int lane) { return A(im, lane); }
   static __device__ __forceinline__ floatx4 mma(const TA& a, const TB& b, floatx4 c) {
+    return mmaf(a, b, c);
+  }
+  using TB4 = floatx4;
+  static __device__ __forceinline__ TB4 B4(const R& r, const R&) { return r; }
+  static __device__ __forceinline__ floatx4 mma4(const TA& a, const TB4& b, floatx4 c) {
     return mmaf(a, b, c);
   }
   static __device__ __forceinline__ floatx4 colsum(const TA&, const floatx4& v);
@@ -668,6 +686,34 @@ __device__ __forceinline__ void st_frows(float* p, uint32_t bytes, uint32_t co, 
     if (valid && k >= 0) *reinterpret_cast<float*>(base + opaque(ro.o[r])) = v[r];
   }
 #endif
+}
+
+// The lane's rows of a D-wide edge tensor (D > 16 allowed: GM<D>::NT tiles),
+// loaded / stored at class byte offset co (the SModel message cache, msg:
+// source_fwd stores the message, source_bwd loads it in place of recomputing
+// the message MLP's second layer)
+template <int D>
+__device__ __forceinline__ void ld_rows_nt(Rsrc p, uint32_t co, const RowOff<D>& ro,
+                                           floatx4 (&v)[GM<D>::NT]) {
+#pragma unroll
+  for (int t = 0; t < GM<D>::NT; ++t) {
+    v[t] = zero4();
+#pragma unroll
+    for (int r = 0; r < GM<D>::nreg(t); ++r)
+      v[t][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(p, ro.o[4 * t + r], co, 0));
+  }
+}
+template <int D>
+__device__ __forceinline__ void st_rows_nt(float* p, uint32_t co, const RowOff<D>& ro, int g,
+                                           bool valid, const floatx4 (&v)[GM<D>::NT]) {
+  char* base = reinterpret_cast<char*>(p) + co;
+#pragma unroll
+  for (int t = 0; t < GM<D>::NT; ++t)
+#pragma unroll
+    for (int r = 0; r < GM<D>::nreg(t); ++r) {
+      const int k = GM<D>::row(g, 4 * t + r);
+      if (valid && k >= 0) *reinterpret_cast<float*>(base + opaque(ro.o[4 * t + r])) = v[t][r];
+    }
 }
 
 // per-feature constants of an F-wide block in the lane's slot order

@@ -387,11 +387,18 @@ class Engine:
         if Qt is None:
             Qt = be.lin(Ws1, 0, F, xt, b=bs1)
         hmom = be.empty(8 * F, d.NS)
-        mom = be.source_fwd(d, xe3[0], xe3[1], xe3[2], Qt, Ws1, Ws2, bs2, hmom)
+        # the per-edge messages, kept for the backward (complete graphs on the
+        # mfma paths; None where source_bwd recomputes them)
+        msg = be.msg_cache(d) if (self.training or self.want_grad) and \
+            hasattr(be, "msg_cache") else None
+        if msg is not None:
+            mom = be.source_fwd(d, xe3[0], xe3[1], xe3[2], Qt, Ws1, Ws2, bs2, hmom, msg=msg)
+        else:
+            mom = be.source_fwd(d, xe3[0], xe3[1], xe3[2], Qt, Ws1, Ws2, bs2, hmom)
         # node_mlp_2 input [x, mean, std, skew, kurt, u[batch]] (gnn.py:153), in place,
         # + its BatchNorm1d (gnn.py:154) in the same fused op
         hS = [(xs, 0, False), (hmom, F, False), (u, 9 * F, True)]
-        st = dict(xs=xs, xt=xt, xe3=xe3, u=u, Qt=Qt, mom=mom)
+        st = dict(xs=xs, xt=xt, xe3=xe3, u=u, Qt=Qt, mom=mom, msg=msg)
         if epi:
             names = list(epi)
             xs_new, sS, outs = self.mlp_fwd(P, pre + "node_mlp_2.", hS, pre + "norm.", BN,
@@ -451,7 +458,8 @@ class Engine:
             d, y, sc, sh, st["Qt"], Ws1, Ws2, P[pre + "node_mlp_1.2.bias"], st["mom"][0], coef,
             tpart, g_next, bnstat, Gr[pre + "node_mlp_1.0.weight"], Gr[pre + "node_mlp_1.2.weight"],
             Gr[pre + "node_mlp_1.2.bias"], bn2=bn2, g_xt=g_xt,  # + g_xt += Ws1x^T GzS
-            **({"tmask": tmask} if tmask is not None and tpart is not None else {}))
+            **({"tmask": tmask} if tmask is not None and tpart is not None else {}),
+            **({"msg": st["msg"]} if st.get("msg") is not None else {}))
         g_tot, GzS = out[0], out[1]
         be.wgrad(GzS, st["xt"], Gr[pre + "node_mlp_1.0.weight"], col0=0,
                  db=Gr[pre + "node_mlp_1.0.bias"])

@@ -221,6 +221,10 @@ _SIGS = {
     "pfsgnn_target_bwd_bn": ([I, I, I, I] + [P] * 14 + [FL, P, P, SZ, P], I),
     "pfsgnn_source_bwd": ([I, I, I, I] + [P] * 24 + [P, SZ, P], I),
     "pfsgnn_source_bwd_bn": ([I, I, I, I] + [P] * 17 + [LL, FL] + [P] * 12 + [P, SZ, P], I),
+    "pfsgnn_msg_bytes": ([I, I, I, I], SZ),
+    "pfsgnn_source_fwd_msg": ([I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, SZ, P], I),
+    "pfsgnn_source_bwd_msg": ([I, I, I, I] + [P] * 25 + [P, SZ, P], I),
+    "pfsgnn_source_bwd_bn_msg": ([I, I, I, I] + [P] * 17 + [LL, FL] + [P] * 13 + [P, SZ, P], I),
     "pfsgnn_edge_bn_grad_sums": ([I, I, I, I, P, P, P, P, P, P, P, SZ, P], I),
     "pfsgnn_edge_mlp_bwd": ([I, I, I, I] + [P] * 21 + [P, SZ, P], I),
     "pfsgnn_loss_fwd": ([I, I, I, I, P, P, P, P, P, P, P, P, FL, FL, FL, ULL, P, P, P, P, P, P, P, SZ, P], I),
@@ -1135,16 +1139,29 @@ class HipBackend:
               inv1.data_ptr(), inv2.data_ptr(), ws, wsb, _stream())
         return y, mu, var, sc, sh, inv1
 
-    def source_fwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, hs_out):
+    def source_fwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, hs_out, msg=None):
+        """-> mom; ``msg`` (from ``msg_cache(d)``) receives the per-edge messages
+        for source_bwd (pfsgnn_source_fwd_msg)."""
         if self._composed(d):
             return self._sp.source_fwd(d, y, sc, sh, Qt, Ws1, Ws2, bs2, hs_out)
         mom = self.empty(4, 2 * d.F, d.NS)
         self._chk(y, Qt, Ws1, Ws2, bs2, hs_out)
         ws, wsb = self._wsargs(d)
-        self._ecall("source_fwd", d, d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh),
-              Qt.data_ptr(), Ws1.data_ptr(), Ws2.data_ptr(), bs2.data_ptr(), mom.data_ptr(),
-              hs_out.data_ptr(), ws, wsb, _stream())
+        args = (d.G, d.NF, d.NC, d.F, y.data_ptr(), _ptr(sc), _ptr(sh), Qt.data_ptr(),
+                Ws1.data_ptr(), Ws2.data_ptr(), bs2.data_ptr(), mom.data_ptr(), hs_out.data_ptr())
+        if msg is not None:
+            _call("pfsgnn_source_fwd_msg", *args, msg.data_ptr(), ws, wsb, _stream())
+        else:
+            self._ecall("source_fwd", d, *args, ws, wsb, _stream())
         return mom
+
+    def msg_cache(self, d):
+        """A buffer for SModel's per-edge messages [2F][E] (pfsgnn_msg_bytes),
+        or None when the current path recomputes them in the backward."""
+        if self._composed(d) or d.sp is not None:
+            return None
+        n = lib().pfsgnn_msg_bytes(d.G, d.NF, d.NC, d.F)
+        return torch.empty(n // 4, dtype=torch.float32, device=self.device) if n else None
 
     def tmask(self, d):
         """A buffer for TModel's LeakyReLU mask (pfsgnn_tmask_bytes), or None
@@ -1218,7 +1235,7 @@ class HipBackend:
         return GzT, gxe
 
     def source_bwd(self, d, y, sc, sh, Qt, Ws1, Ws2, bs2, mean, coef, tpart, g_next, bnstat,
-                   dWs1, dWs2, dbs2, bn2=None, g_xt=None, tmask=None):
+                   dWs1, dWs2, dbs2, bn2=None, g_xt=None, tmask=None, msg=None):
         """-> (g_tot, GzS, Sg, Sgx).  With ``bn2`` = (gamma, var1, n, eps, dgamma,
         dbeta) (and ``bnstat``) the edge BatchNorm's backward is finished in the
         same call: -> (g_tot, GzS, None, None, (alpha, gam0, gam1)).  With
@@ -1255,14 +1272,21 @@ class HipBackend:
             assert bnstat is not None
             gamma, var1, n, eps, dg, db = bn2
             a, g0, g1 = self.empty(d.F), self.empty(d.F), self.empty(d.F)
-            self._ecall("source_bwd_bn", d, *head, var1.data_ptr(), gamma.data_ptr(), int(n),
-                  float(eps), g_tot.data_ptr(), GzS.data_ptr(), dWs1.data_ptr(), dWs2.data_ptr(),
-                  dbs2.data_ptr(), a.data_ptr(), g0.data_ptr(), g1.data_ptr(), dg.data_ptr(),
-                  db.data_ptr(), _ptr(g_xt), _ptr(tmask), ws, wsb, _stream())
+            tail = (var1.data_ptr(), gamma.data_ptr(), int(n), float(eps), g_tot.data_ptr(),
+                    GzS.data_ptr(), dWs1.data_ptr(), dWs2.data_ptr(), dbs2.data_ptr(),
+                    a.data_ptr(), g0.data_ptr(), g1.data_ptr(), dg.data_ptr(), db.data_ptr(),
+                    _ptr(g_xt), _ptr(tmask))
+            if msg is not None:
+                _call("pfsgnn_source_bwd_bn_msg", *head, *tail, msg.data_ptr(), ws, wsb, _stream())
+            else:
+                self._ecall("source_bwd_bn", d, *head, *tail, ws, wsb, _stream())
             return g_tot, GzS, None, None, (a, g0, g1)
-        self._ecall("source_bwd", d, *head, g_tot.data_ptr(), GzS.data_ptr(), dWs1.data_ptr(),
-              dWs2.data_ptr(), dbs2.data_ptr(), _ptr(Sg), _ptr(Sgx), _ptr(g_xt), _ptr(tmask), ws,
-              wsb, _stream())
+        tail = (g_tot.data_ptr(), GzS.data_ptr(), dWs1.data_ptr(), dWs2.data_ptr(),
+                dbs2.data_ptr(), _ptr(Sg), _ptr(Sgx), _ptr(g_xt), _ptr(tmask))
+        if msg is not None:
+            _call("pfsgnn_source_bwd_msg", *head, *tail, msg.data_ptr(), ws, wsb, _stream())
+        else:
+            self._ecall("source_bwd", d, *head, *tail, ws, wsb, _stream())
         return g_tot, GzS, Sg, Sgx
 
     def edge_bn_grad_sums(self, d, g, y, mu1, inv1):

@@ -92,3 +92,54 @@ def test_training_step_bitwise_reproducible(path):
             assert torch.equal(a, b), f"{path}: {nm} differs between identical steps"
     finally:
         pfsgnn.set_edge_path(prev)
+
+
+@pytest.mark.parametrize("path", ["mfma", "bf16x3"])
+def test_node_mlp_ops_bitwise_reproducible(path):
+    """The node-level MLP kernels on the split-bf16 node path (pf::node_x3: the
+    bf16x3 gradient chains of k_mlp_bwd's register form and wgrad_block's weight
+    gradients, on every edge path but the exact-fp32 ones) at the bench
+    geometry's SModel node_mlp_2 shape (K = 100 in three input blocks, H = 100,
+    O = 10, N = 16 x 2394 fibers, BatchNorm): forward, backward and both weight
+    gradients three times on the same inputs, bitwise equal.  VERDICT r05 item
+    2: these kernels issue the same v_mfma_f32_16x16x32_bf16 as the edge
+    kernels without the MF_SRC_KEEP guard (pfsgnn_common.h pf_mf8)."""
+    import pfsgnn
+    from pfsgnn.native import HipBackend
+    hb = HipBackend()
+    prev = pfsgnn.get_edge_path()
+    pfsgnn.set_edge_path(path)
+    try:
+        N, H, O, blocks = 16 * 2394, 100, 10, [10, 80, 10]
+        K = sum(blocks)
+        g = torch.Generator(device="cuda").manual_seed(11)
+        rnd = lambda *s, sc=1.0: torch.randn(*s, device="cuda", generator=g) * sc  # noqa: E731
+        X, col = [], 0
+        for rows in blocks:
+            X.append((rnd(rows, N), col, False))
+            col += rows
+        W1, b1, W2, b2 = rnd(H, K, sc=0.2), rnd(H, sc=0.3), rnd(O, H, sc=0.2), rnd(O)
+        gam, bet = rnd(O, sc=0.2) + 1, rnd(O, sc=0.1)
+        dY = rnd(O, N)
+        runs = []
+        for _ in range(3):
+            rm, rv = torch.zeros(O, device="cuda"), torch.ones(O, device="cuda")
+            Y, Z, Yp, mu, var = hb.mlp_fwd(X, N, W1, b1, W2, b2, bn=(gam, bet, rm, rv, 0.1, 1e-5))
+            dg, db = torch.zeros(O, device="cuda"), torch.zeros(O, device="cuda")
+            bufs = [torch.zeros(t.shape[0], N, device="cuda") for t, _, _ in X]
+            outs = [(b, t.shape[0], False) for b, (t, _, _) in zip(bufs, X)]
+            dYp, dZ = hb.mlp_bwd(dY, Z, W1, W2, K, bn=(Yp, mu, var, gam, 1e-5, dg, db), outs=outs)
+            dW1, db1 = torch.zeros(H, K, device="cuda"), torch.zeros(H, device="cuda")
+            dW2, db2 = torch.zeros(O, H, device="cuda"), torch.zeros(O, device="cuda")
+            hb.wgrad(dYp, Z, dW2, db=db2, act_in=True)
+            hb.wgrad_cat(dZ, X, dW1, db=db1)
+            runs.append([t.clone() for t in (Y, Z, Yp, dYp, dZ, dW1, db1, dW2, db2, dg, db, *bufs)])
+        torch.cuda.synchronize()
+        names = ("Y", "Z", "Yp", "dYp", "dZ", "dW1", "db1", "dW2", "db2", "dgamma", "dbeta",
+                 "dX0", "dX1", "dX2")
+        for r in runs[1:]:
+            for a, b, nm in zip(runs[0], r, names):
+                assert torch.equal(a, b), f"{path}: node {nm} differs between identical launches " \
+                    f"({int((a != b).sum())} of {a.numel()} elements)"
+    finally:
+        pfsgnn.set_edge_path(prev)
