@@ -62,6 +62,11 @@
 #ifndef MF_SB_PACK
 #define MF_SB_PACK 1
 #endif
+// MF_SB_LDSW (default 0): source_bwd's split-bf16 gradient-chain weights in
+// LDS (LayerB3S) instead of registers (-32 VGPRs)
+#ifndef MF_SB_LDSW
+#define MF_SB_LDSW 0
+#endif
 // MF_WG4 (default 1): the backward kernels' split-bf16 weight gradients as the
 // four products of the split operands (WgImg::mma4: B read twice, no [Bh | 0]
 // operand assembled); 0: the three-product form (mma3g)
@@ -801,10 +806,20 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
   L1s.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
   if constexpr (!TM) L1t.load([&](int h, int k) { return tpart ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
   if constexpr (!MSG) L2.load([&](int o, int h) { return Ws2[o * C + h]; }, lane);
-  // gradient chains: exact fp32, bf16x3 or bf16 by PREC
-  GradLayer<PREC, C, C> L2T;
+  // gradient chains: exact fp32, bf16x3 or bf16 by PREC (MF_SB_LDSW: the
+  // split-bf16 weight operands read from LDS per use instead of registers)
+  constexpr bool LW = MF_SB_LDSW && std::is_same_v<GradLayer<PREC, C, C>, LayerB3<C, C>>;
+  using GL2 = std::conditional_t<LW, LayerB3S<C, C>, GradLayer<PREC, C, C>>;
+  using GL1 = std::conditional_t<LW, LayerB3S<F, C>, GradLayer<PREC, F, C>>;
+  GL2 L2T;
+  GL1 L1sT, L1tT;
+  if constexpr (LW) {
+    __shared__ s16x8 gw[(LayerB3S<C, C>::NOP + 2 * LayerB3S<F, C>::NOP) * 64];
+    L2T.bind(gw);
+    L1sT.bind(gw + LayerB3S<C, C>::NOP * 64);
+    L1tT.bind(gw + (LayerB3S<C, C>::NOP + LayerB3S<F, C>::NOP) * 64);
+  }
   L2T.load([&](int h, int o) { return Ws2[o * C + h]; }, lane);
-  GradLayer<PREC, F, C> L1sT, L1tT;
   L1sT.load([&](int k, int h) { return Ws1[h * 2 * F + F + k]; }, lane);
   L1tT.load([&](int k, int h) { return tpart ? Wt1[h * 2 * F + F + k] : 0.f; }, lane);
   floatx4 rs[NT], bias[NT], mn[NT], q0[NT], q1[NT], q2[NT], q3[NT];

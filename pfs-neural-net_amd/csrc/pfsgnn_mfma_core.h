@@ -226,6 +226,59 @@ struct LayerB3 {
   }
 };
 
+// The same bf16x3 layer with its split weight operands staged in LDS instead
+// of held in registers (per lane, in the register form's order: the pairs'
+// [Wh | Wh'] and [Wl | Wl'], then an odd last K-tile's [Wh | Wl]; one
+// ds_read_b128 per MFMA operand): frees 4 VGPRs per operand for a kernel
+// whose registers are the limit.  bind() gives the LDS block; load() is
+// executed by every wave, wave 0 writes (the kernel's __syncthreads after its
+// staging publishes them).
+template <int M, int K>
+struct LayerB3S {
+  static constexpr int MT = GM<M>::NT, KT = GM<K>::NT, KP = KT / 2;
+  static constexpr bool ODD = (KT & 1) != 0;
+  static constexpr int NOP = MT * (2 * KP + (ODD ? 1 : 0));   // s16x8 operands per lane
+  const s16x8* w = nullptr;
+  s16x8* base = nullptr;
+  __device__ __forceinline__ void bind(s16x8* lds) { base = lds; }
+  static __device__ __forceinline__ int op(int t, int k) { return t * (2 * KP + (ODD ? 1 : 0)) + k; }
+  template <class Fn>
+  __device__ __forceinline__ void load(Fn fn, int lane) {
+    w = base + lane;
+    if ((threadIdx.x >> 6) != 0) return;
+    LayerB3<M, K> r;
+    r.load(fn, lane);
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+#pragma unroll
+      for (int p = 0; p < KP; ++p) {
+        base[op(t, 2 * p) * 64 + lane] = r.ap[t][p].h;
+        base[op(t, 2 * p + 1) * 64 + lane] = r.ap[t][p].l;
+      }
+      if constexpr (ODD) base[op(t, 2 * KP) * 64 + lane] = r.ao[t];
+    }
+  }
+  __device__ __forceinline__ void apply(const Fr (&x)[KT], floatx4 (&y)[MT]) const {
+#pragma unroll
+    for (int p = 0; p < KP; ++p) {
+      const Fr8 xp = cat(x[2 * p], x[2 * p + 1]);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const Fr8 a = {w[op(t, 2 * p) * 64], w[op(t, 2 * p + 1) * 64]};
+        y[t] = mma3w(a, xp, y[t]);
+      }
+    }
+    if constexpr (ODD) {
+      const s16x8 xlh = cat8(x[KT - 1].l, x[KT - 1].h), xh0 = cat8(x[KT - 1].h, s16x4{});
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const s16x8 a = w[op(t, 2 * KP) * 64];
+        y[t] = mf8(a, xh0, mf8(a, xlh, y[t]));
+      }
+    }
+  }
+};
+
 // ------------------------------------------------------------ bf16x6 layer
 // y (+)= W x with three-way split operands v = vh + vm + vl (each bf16 RNE,
 // |v - vh - vm - vl| <= ~2^-27 |v|) and the six products whose order is at most
