@@ -84,8 +84,22 @@ namespace {
 #ifndef MF_EFWD_MINB
 #define MF_EFWD_MINB 6   // six waves per SIMD (80 VGPRs, no spills at ring depth 3; profiles/r05aj_fwd_occupancy_ab.txt)
 #endif
+// MF_EFWD_B6S (default 1): at PREC 4 (bf16x6) the split weight tuples of both
+// layers staged in LDS (LayerB6S) instead of registers, so that the kernel
+// holds MF_EFWD_MINB6 waves per SIMD (84 VGPRs, five; the register form: 128
+// VGPRs, four; six waves spill 17 VGPRs).  edge_mlp_fwd -0.02 to -0.03 ms, the
+// step -0.01 / -0.02 ms with MF_SFT_B6S (profiles/r06n_ab.txt); bitwise the
+// register form's results
+#ifndef MF_EFWD_B6S
+#define MF_EFWD_B6S 1
+#endif
+#ifndef MF_EFWD_MINB6
+#define MF_EFWD_MINB6 5
+#endif
 template <int F, int PREC>
-__global__ __launch_bounds__(256, (F <= 10 && PREC <= 1) ? MF_EFWD_MINB : 1) void km_edge_mlp_fwd(EdgeGeo geo, const float* __restrict__ xe,
+__global__ __launch_bounds__(256, (F <= 10 && PREC <= 1) ? MF_EFWD_MINB
+                                  : (F <= 10 && PREC == 4 && MF_EFWD_B6S) ? MF_EFWD_MINB6 : 1)
+void km_edge_mlp_fwd(EdgeGeo geo, const float* __restrict__ xe,
                                                        const float* __restrict__ xsc,
                                                        const float* __restrict__ xsh,
                                                        const float* __restrict__ Ps,
@@ -100,9 +114,15 @@ __global__ __launch_bounds__(256, (F <= 10 && PREC <= 1) ? MF_EFWD_MINB : 1) voi
   MF_GEO
   __shared__ __attribute__((aligned(16))) float ptl[MF_MAX_CPS * ClassRows<H>::CP];
   ClassRows<H>::stage(ptl, PtS, geo.NT, (long long)gg * geo.NC + c0, c1 - c0);
-  FwdLayer<PREC, H, F> L1;
+  constexpr bool B6S = MF_EFWD_B6S && PREC == 4;
+  std::conditional_t<B6S, LayerB6S<H, F>, FwdLayer<PREC, H, F>> L1;
+  std::conditional_t<B6S, LayerB6S<F, H>, FwdLayer<PREC, F, H>> L2;
+  if constexpr (B6S) {
+    __shared__ s16x8 w6[(LayerB6S<H, F>::NOP + LayerB6S<F, H>::NOP) * 64];
+    L1.bind(w6);
+    L2.bind(w6 + LayerB6S<H, F>::NOP * 64);
+  }
   L1.load([&](int h, int k) { return W1[h * 4 * F + 2 * F + k]; }, lane);
-  FwdLayer<PREC, F, H> L2;
   L2.load([&](int o, int h) { return W2[o * H + h]; }, lane);
   floatx4 ps[NT];
 #pragma unroll
@@ -306,6 +326,10 @@ __global__ __launch_bounds__(256) void km_source_fwd(EdgeGeo geo, const float* _
   //   M3 += d^3 A3 - 3 d M2 / n;  M2 += d^2 A2;  mean += d / n
   // A2 = (n-1)/n, A3 = (n-1)(n-2)/n^2, A4 = (n-1)(n^2-3n+3)/n^3 (12 VALU per
   // element, the M2 / M3 of the previous count on the right-hand sides)
+  static_assert(MF_MAX_CPS <= MF_PEB_ROWS, "Pebay table rows");
+#if MF_PEB_CONST
+  const auto& pco = c_peb.v;
+#else
   __shared__ __attribute__((aligned(16))) float pco[MF_MAX_CPS][8];
   if (t < c1 - c0) {
     const double nn = t + 1, r = 1.0 / nn;
@@ -318,7 +342,8 @@ __global__ __launch_bounds__(256) void km_source_fwd(EdgeGeo geo, const float* _
     pco[t][6] = (float)(-3 * r);                                  // -3/n
     pco[t][7] = 0.f;
   }
-  __syncthreads();   // qtl, pco
+#endif
+  __syncthreads();   // qtl
   auto load = [&](int c) {
     Rows<1> r;
     r.v[0] = ld_frows<F>(ry, (uint32_t)c * eoc, ro);
@@ -379,6 +404,15 @@ __global__ __launch_bounds__(256) void km_source_fwd(EdgeGeo geo, const float* _
 // (class table, weight registers) is shared by 4x the edges.
 #define MF_SFT_MAXNC 256
 #define MF_SFT_WAVE_MAXNC 64
+#ifndef MF_SFT_B6S
+#define MF_SFT_B6S 3   // bit 0: L1's tuples in LDS, bit 1: L2's
+#endif
+// dynamic LDS floats of km_source_fwd_ft: the class table [NC][CP], which the
+// waves' merge reuses as [3][MS][64] after the class loop
+static inline size_t sft_lds_floats(int NC, int F) {
+  const int C = 2 * F, NT = (((C + 3) / 4) + 3) / 4, CP = 16 * NT, MS = 16 * NT;
+  return std::max((size_t)NC * CP, (size_t)3 * MS * 64);
+}
 template <int F, int PREC, bool WF>
 __global__ __launch_bounds__(256) void km_source_fwd_ft(
     EdgeGeo geo, int ntiles, const float* __restrict__ y, const float* __restrict__ sc,
@@ -404,12 +438,27 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
   const uint32_t RB = (uint32_t)geo.E * 4u;
   const uint32_t eo0 = (uint32_t)((((long long)gg * NC) * geo.NF + (fvalid ? f : 0)) * 4);
   const uint32_t eoc = (uint32_t)geo.NF * 4u, EB = (uint32_t)geo.E * 4u;
-  __shared__ __attribute__((aligned(16))) float qtl[MF_SFT_MAXNC * CP];
+  // the class table (and, after the loop, the waves' merge scratch), sized by
+  // the launch: sft_lds_floats(NC, F) floats of dynamic LDS
+  extern __shared__ __attribute__((aligned(16))) float qtl[];
+#if MF_PEB_CONST
+  const auto& pco = c_peb.v;
+  static_assert(MF_SFT_MAXNC / 4 + 1 <= MF_PEB_ROWS, "Pebay table rows");
+#else
   __shared__ __attribute__((aligned(16))) float pco[MF_SFT_MAXNC / 4 + 1][8];
+#endif
   ClassRows<C>::stage(qtl, QtS, geo.NT, (long long)gg * NC, NC);
-  FwdLayer<PREC, C, F> L1;
+  // (MF_SFT_B6S: bf16x6's split weight tuples in LDS, LayerB6S -- four waves
+  // per SIMD instead of three with them in registers; source_fwd -0.01 ms)
+  constexpr bool B6S1 = (MF_SFT_B6S & 1) && PREC == 4, B6S2 = (MF_SFT_B6S & 2) && PREC == 4;
+  std::conditional_t<B6S1, LayerB6S<C, F>, FwdLayer<PREC, C, F>> L1;
+  std::conditional_t<B6S2, LayerB6S<C, C>, FwdLayer<PREC, C, C>> L2;
+  if constexpr (B6S1 || B6S2) {
+    __shared__ s16x8 w6[(LayerB6S<C, F>::NOP + LayerB6S<C, C>::NOP) * 64];
+    if constexpr (B6S1) L1.bind(w6);
+    if constexpr (B6S2) L2.bind(w6 + LayerB6S<C, F>::NOP * 64);
+  }
   L1.load([&](int h, int k) { return Ws1[h * 2 * F + F + k]; }, lane);
-  FwdLayer<PREC, C, C> L2;
   L2.load([&](int o, int h) { return Ws2[o * C + h]; }, lane);
   floatx4 bias[NT];
 #pragma unroll
@@ -423,6 +472,7 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
   for (int tt = 0; tt < NT; ++tt) S1[tt] = S2[tt] = S3[tt] = S4[tt] = zero4();
   // Pebay coefficients of the k-th message of a wave (count k + 1), as km_source_fwd
   static_assert(MF_SFT_WAVE_MAXNC <= MF_SFT_MAXNC / 4 + 1, "pco rows");
+#if !MF_PEB_CONST
   const int nk = WF ? NC : (NC + 3) >> 2;
   if (t < nk) {
     const double nn = t + 1, r = 1.0 / nn;
@@ -435,7 +485,8 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
     pco[t][6] = (float)(-3 * r);
     pco[t][7] = 0.f;
   }
-  __syncthreads();   // qtl, pco
+#endif
+  __syncthreads();   // qtl (and the LDS Pebay table)
   // wave w: classes w + 4k, k = 0 .. (its count) - 1, streamed as k (WF: class k)
   const int kw = WF ? NC : (NC - wave + 3) >> 2;
   auto load = [&](int k) {
@@ -526,6 +577,7 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
   __syncthreads();
   float* ms = qtl;   // [3][MS][64]
   static_assert(3 * MS * 64 <= MF_SFT_MAXNC * CP, "merge scratch exceeds the class table");
+  // (sft_lds_floats sizes the dynamic table for max(NC * CP, 3 * MS * 64))
   if (wave > 0) {
     float* p = ms + (size_t)(wave - 1) * MS * 64 + lane;
 #pragma unroll
@@ -1436,13 +1488,14 @@ int source_fwd_tiles(const EdgeGeo& geo, int F, const float* y, const float* sc,
   const int TF = wf ? 64 : 16;
   const int ntiles = geo.G * ((geo.NF + TF - 1) / TF);
   const int nb = 8 * ((ntiles + 7) / 8);
+  const size_t lds = sft_lds_floats(geo.NC, F) * sizeof(float);
 #define MF_SFT(FF, PP)                                                                     \
   case FF * 8 + PP:                                                                        \
     if (wf)                                                                                \
-      hipLaunchKernelGGL((km_source_fwd_ft<FF, PP, true>), dim3(nb), dim3(256), 0, st, geo, \
+      hipLaunchKernelGGL((km_source_fwd_ft<FF, PP, true>), dim3(nb), dim3(256), lds, st, geo, \
                          ntiles, y, sc, sh, QtS, Ws1, Ws2, bs2, mom, hs, msg);             \
     else                                                                                   \
-      hipLaunchKernelGGL((km_source_fwd_ft<FF, PP, false>), dim3(nb), dim3(256), 0, st, geo, \
+      hipLaunchKernelGGL((km_source_fwd_ft<FF, PP, false>), dim3(nb), dim3(256), lds, st, geo, \
                          ntiles, y, sc, sh, QtS, Ws1, Ws2, bs2, mom, hs, msg);             \
     break;
   switch (F * 8 + fwd_prec(prec)) {

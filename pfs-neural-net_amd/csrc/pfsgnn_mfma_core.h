@@ -124,18 +124,19 @@ __device__ __forceinline__ s16x8 cat8(s16x4 a, s16x4 b) {
 }
 __device__ __forceinline__ Fr8 cat(const Fr& a, const Fr& b) { return {cat8(a.h, b.h), cat8(a.l, b.l)}; }
 // MF_SRC_KEEP: an empty asm after every split-bf16 MFMA reads its result and its
-// A / B operands.  Without it the bf16x3 / bf16x6 SModel forward
-// (km_source_fwd_ft) gave run-to-run different moments on identical inputs
-// (~2.5k of 6.1M elements, tools/op_det_probe.py; every other kernel and path
-// reproducible); with it every probe is bitwise reproducible
-// (profiles/r05a_op_determinism.txt, tests/test_gpu_determinism.py).  What in
-// the compiler's output for that kernel raced is not isolated: the hand-written
-// probes of the suspect patterns -- an MFMA result written over its own A or B,
-// an LDS load into a chained MFMA's SrcC right behind it -- are exact on
-// gfx950 (tools/probes/mfma_overlap.hip, profiles/r05a_mfma_overlap.txt).
+// A / B operands -- a scheduling choice: without it edge_mlp_bwd runs 2.38 ->
+// 2.61 ms per step (profiles/r06n_ab.txt).  Rounds 5-6 kept it for
+// reproducibility: the SModel forward (km_source_fwd_ft) gave run-to-run
+// different M3 / M4 without it.  That race followed the per-block LDS table of
+// Pebay coefficients, not the MFMAs: only M3 / M4 of two channels (lane group 3,
+// the low halves of packed-fp32 pairs) moved, S1 / S2 stayed bitwise; wait
+// states behind every MFMA made it worse, while the table's coefficients from
+// VALU, from scalar loads (c_peb below), or no packed-fp32 FMAs at all
+// (-fno-slp-vectorize) each made every probe exact, MF_SRC_KEEP on or off
+// (profiles/r06m_race_bisect.txt, r06n_opdet.txt).  The table is now c_peb.
 // MF_SRC_PIN (A/B): also pass B (1) / A (2) through an opaque asm before the
 // MFMA so that no result is allocated over an operand at all: 1.7 % slower
-// step, not needed for reproducibility (profiles/r05d_pin_ab.txt).
+// step (profiles/r05d_pin_ab.txt).
 #ifndef MF_SRC_KEEP
 #define MF_SRC_KEEP 1
 #endif
@@ -793,6 +794,36 @@ __device__ __forceinline__ floatx4 ld_node(const float* p, int t, int g, long lo
   }
   return v;
 }
+
+// Pebay's count-only coefficients of the n-th folded message (n = k + 1), one
+// 32-byte row per count -- A2 A3 A4 1/n | 6/n^2 -4/n -3/n 0 -- evaluated in
+// double at compile time and rounded once (the values the SModel forward
+// kernels used to build in LDS per block, bitwise).  The row index is
+// wave-uniform, so a fold reads its row with one scalar load into SGPRs.
+// MF_PEB_CONST=0 restores the per-block LDS table: read back with ds_read_b128
+// into VGPRs that packed-fp32 FMAs then broadcast (op_sel_hi), that form gave
+// run-to-run different M3 / M4 on gfx950 ("the source_fwd race").
+#ifndef MF_PEB_CONST
+#define MF_PEB_CONST 1
+#endif
+#define MF_PEB_ROWS 65
+struct PebayTable {
+  float v[MF_PEB_ROWS][8];
+  constexpr PebayTable() : v{} {
+    for (int t = 0; t < MF_PEB_ROWS; ++t) {
+      const double nn = t + 1, r = 1.0 / nn;
+      v[t][0] = (float)((nn - 1) * r);
+      v[t][1] = (float)((nn - 1) * (nn - 2) * r * r);
+      v[t][2] = (float)((nn - 1) * (nn * nn - 3 * nn + 3) * r * r * r);
+      v[t][3] = (float)r;
+      v[t][4] = (float)(6 * r * r);
+      v[t][5] = (float)(-4 * r);
+      v[t][6] = (float)(-3 * r);
+      v[t][7] = 0.f;
+    }
+  }
+};
+__constant__ __attribute__((aligned(32))) static const PebayTable c_peb = PebayTable();
 
 // The block's class rows [c0, c1) of a channel-major per-class node table
 // [D][NT], staged once in LDS in the kernels' slot order (they are re-read for

@@ -3,8 +3,11 @@
 Round 5 found the bf16x3 / bf16x6 SModel forward (km_source_fwd_ft) giving
 run-to-run different moments on identical inputs -- a few thousand of 6.1 M
 elements, enough to move a parity check past its bar now and then -- while
-the smaller parity graphs and the default path were reproducible.  The fix
-lives in the MFMA helper (pfsgnn_mfma_core.h, MF_SRC_KEEP); these tests hold
+the smaller parity graphs and the default path were reproducible.  Round 5
+hid it behind a scheduling change (MF_SRC_KEEP); round 6 traced it to the
+kernel's per-block LDS table of Pebay coefficients and replaced that table
+with a compile-time constant one read by scalar loads (pfsgnn_mfma_core.h,
+c_peb; profiles/r06m_race_bisect.txt).  These tests hold
 it: each forward edge op three times on the same inputs, on every path that is
 held to the parity bar plus bf16x3, and one forward + backward of the whole
 model twice, must agree bit for bit."""
