@@ -1197,6 +1197,9 @@ __global__ __launch_bounds__(256, 2) void km_source_bwd(
 // dW1[:, 2F:3F] += g_z x^T, per-fiber (-> g_Ps) and per-class (-> g_Pt) sums of
 // g_z, and the edge-input gradient W1[:, 2F:3F]^T g_z when the block has an
 // upstream edge input.
+#ifndef MF_BWD_PIPE6
+#define MF_BWD_PIPE6 0   // 1: the class pipeline on bf16x6 too: its LDS-tuple recompute then spills 16 VGPRs, edge_mlp_bwd 2.36 -> 2.42 ms (profiles/r06p_ab.txt)
+#endif
 template <int F, int PREC>
 __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
     EdgeGeo geo, const float* __restrict__ g_tot, const float* __restrict__ alpha,
@@ -1382,7 +1385,7 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
   // (the pipeline's second head fits the register file at Fdim <= 10 on the
   // split-bf16 gradient paths; the fp32 and single-bf16 forms would spill or
   // lose a wave)
-  if constexpr (MF_BWD_PIPE && F <= 10 && PREC != 0 && PREC != 2)
+  if constexpr (MF_BWD_PIPE && F <= 10 && PREC != 0 && PREC != 2 && (PREC != 4 || MF_BWD_PIPE6))
     class_stream_pipe<MF_DEPTH_BWD>(c0, c1, load, head, tail);
   else
     class_stream<MF_DEPTH_BWD>(c0, c1, load, [&](const Rows<3>& rows, int c) { tail(head(rows, c), c); });
