@@ -1459,7 +1459,18 @@ __global__ __launch_bounds__(256, 2) void km_edge_mlp_bwd(
     default: return pf::fail("pfsgnn mfma", "unsupported Fdim for this edge path"); \
   }
 
+// MF_PART: the library builds this file twice (Makefile) so that the MFMA
+// helper's MF_SRC_KEEP scheduling tie can differ per kernel: part 1 = every
+// launcher but edge_mlp_bwd's (MF_SRC_KEEP=0), part 2 = edge_mlp_bwd's alone
+// (MF_SRC_KEEP=1: without the tie it runs 2.38 -> 2.61 ms per step, while the
+// other kernels run faster without it; profiles/r06n_ab.txt, r06r_keep_ab.txt).
+// A kernel is instantiated only by its launcher, so each object holds its own.
+// MF_PART 0 (a plain compile) = both.
+#ifndef MF_PART
+#define MF_PART 0
+#endif
 namespace pfm {
+#if MF_PART != 2
 
 // forward kernels only distinguish fp32 (0, 1), single bf16 (2) and bf16x3 (3)
 static inline int fwd_prec(int prec) { return FP(prec); }
@@ -1568,6 +1579,8 @@ int source_bwd(const EdgeGeo& geo, int F, const float* msg, const float* y, cons
   return 0;
 }
 
+#endif  // MF_PART != 2
+#if MF_PART != 1
 int edge_mlp_bwd(const EdgeGeo& geo, int F, const float* g_tot, const float* alpha,
                  const float* gam0, const float* gam1, const float* y, const float* xe,
                  const float* xsc, const float* xsh, const float* Ps, const float* PtS,
@@ -1577,5 +1590,6 @@ int edge_mlp_bwd(const EdgeGeo& geo, int F, const float* g_tot, const float* alp
             gxe, gs, pW2, pW1, pCol)
   return 0;
 }
+#endif  // MF_PART != 1
 
 }  // namespace pfm
