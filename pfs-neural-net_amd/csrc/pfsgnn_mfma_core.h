@@ -125,7 +125,9 @@ __device__ __forceinline__ s16x8 cat8(s16x4 a, s16x4 b) {
 __device__ __forceinline__ Fr8 cat(const Fr& a, const Fr& b) { return {cat8(a.h, b.h), cat8(a.l, b.l)}; }
 // MF_SRC_KEEP: an empty asm after every split-bf16 MFMA reads its result and its
 // A / B operands -- a scheduling choice: without it edge_mlp_bwd runs 2.38 ->
-// 2.61 ms per step (profiles/r06n_ab.txt).  Rounds 5-6 kept it for
+// 2.61 ms per step, the other kernels slightly faster (profiles/r06n_ab.txt),
+// so the library builds edge_mlp_bwd with it and the rest of pfsgnn_mfma.hip
+// without (MF_PART there, the Makefile).  Rounds 5-6 kept it for
 // reproducibility: the SModel forward (km_source_fwd_ft) gave run-to-run
 // different M3 / M4 without it.  That race followed the per-block LDS table of
 // Pebay coefficients, not the MFMAs: only M3 / M4 of two channels (lane group 3,
