@@ -146,3 +146,45 @@ def test_node_mlp_ops_bitwise_reproducible(path):
                     f"({int((a != b).sum())} of {a.numel()} elements)"
     finally:
         pfsgnn.set_edge_path(prev)
+
+
+@pytest.mark.parametrize("density", [0.3, 0.999])
+def test_sliced_step_bitwise_reproducible(density):
+    """The general-graph (sliced) kernels at the bench geometry (16 x 2394x128
+    at 30 % / 99.9 % density, B = 8): a forward + backward twice from the same
+    state, every output and parameter gradient bitwise equal.  Their Pebay
+    coefficients are per-lane global loads, not the LDS table that raced in
+    km_source_fwd_ft, and since round 6 they run without the MF_SRC_KEEP tie
+    (profiles/r06t_sparse_keep_ab.txt); this holds both."""
+    import pfsgnn
+    G, NF, NC, B, F = 16, 2394, 128, 8, 10
+    gen = torch.Generator().manual_seed(0)
+    keep = torch.rand(G, NF, NC, generator=gen) < density
+    g, f, c = torch.nonzero(keep, as_tuple=True)
+    perm = torch.randperm(g.numel(), generator=gen)
+    ei = torch.stack([(g * NF + f)[perm], (g * NC + c)[perm]])
+    E = ei.shape[1]
+    xt = torch.cat([torch.randint(2, 13, (G * NC, 1), generator=gen).float(),
+                    torch.randint(1000, 100000, (G * NC, 1), generator=gen).float()], 1)
+    data = pfsgnn.BipartiteData(ei, torch.arange(NF, dtype=torch.float).repeat(G).reshape(-1, 1), xt,
+                                2.0 + 8.0 * torch.rand(E, F, generator=gen), torch.zeros(G, F))
+    torch.manual_seed(0)
+    gnn = pfsgnn.GNN(B=B, Fdim=F, T=NC, F_s=1, F_t=2).cuda()
+    gnn.train()
+    w = [torch.randn(n, F, device="cuda") * 1e-3 for n in (G * NF, G * NC, E, G)]
+    state = {k: v.clone() for k, v in gnn.state_dict().items()}
+    res = []
+    for _ in range(2):
+        gnn.load_state_dict(state)
+        gnn.zero_grad()
+        out = gnn(data)
+        loss = ((out.x_s * w[0]).sum() + (out.x_t * w[1]).sum() + (out.x_e * w[2]).sum()
+                + (out.x_u * w[3]).sum())
+        loss.backward()
+        res.append([t.detach().clone() for t in (out.x_s, out.x_t, out.x_e, out.x_u)]
+                   + [p.grad.clone() for p in gnn.parameters()])
+    torch.cuda.synchronize()
+    names = ["x_s", "x_t", "x_e", "x_u"] + [n for n, _ in gnn.named_parameters()]
+    for a, b, nm in zip(res[0], res[1], names):
+        assert torch.equal(a, b), f"density {density}: {nm} differs between identical steps " \
+            f"({int((a != b).sum())} of {a.numel()} elements)"
