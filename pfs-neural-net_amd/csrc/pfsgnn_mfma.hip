@@ -413,6 +413,9 @@ static inline size_t sft_lds_floats(int NC, int F) {
   const int C = 2 * F, NT = (((C + 3) / 4) + 3) / 4, CP = 16 * NT, MS = 16 * NT;
   return std::max((size_t)NC * CP, (size_t)3 * MS * 64);
 }
+#if !MF_PEB_CONST && defined(MF_PEB_DIAG)
+__device__ unsigned g_peb_diag_n = 0;
+#endif
 template <int F, int PREC, bool WF>
 __global__ __launch_bounds__(256) void km_source_fwd_ft(
     EdgeGeo geo, int ntiles, const float* __restrict__ y, const float* __restrict__ sc,
@@ -498,6 +501,18 @@ __global__ __launch_bounds__(256) void km_source_fwd_ft(
   auto fold = [&](const floatx4 (&m)[NT], int k) {
     const floatx4 ca = *reinterpret_cast<const floatx4*>(&pco[k][0]);
     const floatx4 cb = *reinterpret_cast<const floatx4*>(&pco[k][4]);
+#if !MF_PEB_CONST && defined(MF_PEB_DIAG)
+    {  // (diagnostic build, tools/race_bisect.sh: the LDS rows against c_peb)
+      unsigned badm = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        badm |= ((ca[j] != c_peb.v[k][j]) ? 1u : 0u) << j | ((cb[j] != c_peb.v[k][4 + j]) ? 1u : 0u) << (4 + j);
+      if (badm) {
+        const unsigned nd = atomicAdd(&g_peb_diag_n, 1u);
+        if (nd < 48) printf("PEBDIAG block %d wave %d lane %d k %d mask %x\n", (int)blockIdx.x, wave, lane, k, badm);
+      }
+    }
+#endif
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt)
 #pragma unroll

@@ -13,6 +13,8 @@
 #   nokeep   the old table, MF_SRC_KEEP=0 (about 20x more)
 #   pin      the old table, MF_SRC_PIN=3 (no race seen)
 #   noslp    the old table, -fno-slp-vectorize: no packed-fp32 FMAs (no race)
+#   diag     the old table, every fold's rows compared in-kernel with c_peb
+#            (MF_PEB_DIAG: a printf per mismatch; none, while the race stays)
 # and the fixed tree's default (c_peb, scalar loads), with and without the tie.
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -24,12 +26,13 @@ build)
     sft1 "$P -DMF_SFT_B6S=1" nokeep "-DMF_PEB_CONST=0 -DMF_SRC_KEEP=0" || exit 1
   bash tools/variants.sh pin "$P -DMF_SRC_PIN=3" noslp "$P -fno-slp-vectorize" \
     fixed "-DMF_SRC_KEEP=1" fixednokeep "-DMF_SRC_KEEP=0" || exit 1
+  bash tools/variants.sh diag "$P -DMF_PEB_DIAG" || exit 1
   ;;
 run)
   mkdir -p gpurun_out
-  for v in lds nob6s sft1 nokeep pin noslp fixed fixednokeep; do
+  for v in lds nob6s sft1 nokeep pin noslp fixed fixednokeep diag; do
     PFSGNN_LIB_VARIANT=$v timeout -k 10 150 python tools/op_det_probe.py 16 2394 128 bf16x6 5 2>&1 |
-      grep source_fwd | sed "s/^/$v /" >> gpurun_out/race_bisect.txt || exit 2
+      grep -e source_fwd -e PEBDIAG | sed "s/^/$v /" >> gpurun_out/race_bisect.txt || exit 2
   done
   PFSGNN_LIB_VARIANT=lds timeout -k 10 150 python tools/op_det_where.py 16 2394 128 bf16x6 4 \
     > gpurun_out/race_where.txt 2>&1 || exit 3
